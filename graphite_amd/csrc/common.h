@@ -1,0 +1,95 @@
+// common.h -- shared device/host definitions of the emesh timing engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace gnoc {
+
+// Output ports per tile (network_model_emesh_hop_by_hop.h:43-50) + injection router port.
+enum : uint32_t { P_SELF = 0, P_LEFT = 1, P_RIGHT = 2, P_DOWN = 3, P_UP = 4, P_INJ = 5, PORTS = 6 };
+
+// Input sides of a mesh router output port: where the packet came from.
+// IN_LOCAL = from this tile's injection router (emesh_hop_by_hop.cc:151-159),
+// IN_W/IN_E/IN_S/IN_N = from the neighbour's RIGHT/LEFT/UP/DOWN output.
+enum : uint32_t { IN_LOCAL = 0, IN_W = 1, IN_E = 2, IN_S = 3, IN_N = 4, INS = 5 };
+
+// One hop record in HBM: the arrival of packet `id` at an output-port queue at
+// time `t` (picoseconds).  aux packs the destination tile (20 bits) and the
+// packet's flit count F (12 bits) so no gather is needed downstream.
+struct __attribute__((aligned(16))) Rec
+{
+   uint64_t t;
+   uint32_t id;
+   uint32_t aux;
+};
+static_assert(sizeof(Rec) == 16, "Rec must be 16 bytes");
+
+constexpr uint32_t AUX_DST_BITS = 20;
+constexpr uint32_t AUX_DST_MASK = (1u << AUX_DST_BITS) - 1;
+constexpr uint32_t AUX_F_MAX = (1u << (32 - AUX_DST_BITS)) - 1;
+
+__host__ __device__ inline uint32_t aux_pack(uint32_t dst, uint32_t F) { return dst | (F << AUX_DST_BITS); }
+__host__ __device__ inline uint32_t aux_dst(uint32_t a) { return a & AUX_DST_MASK; }
+__host__ __device__ inline uint32_t aux_F(uint32_t a) { return a >> AUX_DST_BITS; }
+
+__host__ __device__ inline uint32_t slot_of(uint32_t tile, uint32_t dir, uint32_t in)
+{
+   return (tile * PORTS + dir) * INS + in;
+}
+
+// Which input side a packet arrives on after leaving through `dir`.
+__host__ __device__ inline uint32_t in_side_after(uint32_t dir)
+{
+   return dir == P_RIGHT ? IN_W : dir == P_LEFT ? IN_E : dir == P_UP ? IN_S : dir == P_DOWN ? IN_N : IN_LOCAL;
+}
+
+struct DevCfg
+{
+   uint32_t W, H, N;
+   uint32_t flit_width;
+   uint64_t R, Lk;
+   double f;
+   uint64_t rl_ps;       // Latency(R + Lk, f).toPicosec()
+   int contention;
+   int analytical;
+   int max_list;
+   uint32_t magicW;      // ceil(2^32 / W) style reciprocal for tile -> (x, y)
+};
+
+// Latency::toPicosec, common/misc/time_types.h:81-86.  F1: f == 1.0 exactly,
+// where the double expression equals 1000*c for every c < 2^43.
+template <bool F1>
+__host__ __device__ __forceinline__ uint64_t ps_of(uint64_t c, double f)
+{
+   if (F1) return c * 1000ull;
+   return (uint64_t) ceil(((double) 1000 * (double) c) / f);
+}
+
+// Time::toCycles, common/misc/time_types.h:104-109.  F1 fast path is exact for
+// ps < 2^42 * 1000 (validated at submit).
+template <bool F1>
+__host__ __device__ __forceinline__ uint64_t cyc_of(uint64_t ps, double f)
+{
+   if (F1) return (ps + 999ull) / 1000ull;
+   return (uint64_t) ceil(((double) ps * f) / (double) 1.0e3);
+}
+
+// tile -> (x, y) with W <= 65535, tile < 2^20: exact via 32x32->64 multiply.
+__host__ __device__ __forceinline__ void tile_xy(uint32_t tile, uint32_t W, uint32_t magicW, uint32_t& x, uint32_t& y)
+{
+   uint32_t q = (uint32_t) (((uint64_t) tile * magicW) >> 32);
+   if ((q + 1) * W <= tile) q++;
+   if (q * W > tile) q--;
+   y = q;
+   x = tile - q * W;
+}
+
+// Dimension-ordered XY route step, network_model_emesh_hop_by_hop.cc:229-240.
+__host__ __device__ __forceinline__ uint32_t xy_dir(uint32_t cx, uint32_t cy, uint32_t dx, uint32_t dy)
+{
+   return cx > dx ? P_LEFT : cx < dx ? P_RIGHT : cy > dy ? P_DOWN : cy < dy ? P_UP : P_SELF;
+}
+
+}  // namespace gnoc

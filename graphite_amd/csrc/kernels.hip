@@ -1,0 +1,775 @@
+// kernels.hip -- CDNA4 (gfx950) kernels of the emesh_hop_by_hop timing engine.
+//
+// The reference walks each packet hop by hop through per-port history-tree
+// queues (network_model_emesh_hop_by_hop.cc:146-264, router_model.cc:70-108,
+// queue_model_history_tree.cc:43-126).  With XY routing the output-port graph
+// is acyclic (injection -> X chain of the source row -> Y chain of the
+// destination column -> SELF), and with arrivals served in (time, id) order
+// every history-tree queue is the FIFO max-plus recurrence
+//     c_i = max(X - t_i, 0),  X <- max(t_i, X) + F_i
+// plus an M/G/1 prologue while the queue has never been idle.
+// So the engine processes ports level by level along that DAG; each port's
+// whole-trace arrival stream is the (t, id)-merge of its input streams, which
+// are sorted because each producer emits in FIFO order.
+#include "common.h"
+
+namespace gnoc {
+
+// ----------------------------------------------------------------------------
+// Preprocessing: classify packets, count records per (port, input side).
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, const uint64_t* __restrict__ inj,
+                                                  const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                                                  const uint32_t* __restrict__ bits, const uint32_t* __restrict__ flags,
+                                                  uint32_t* __restrict__ aux, uint8_t* __restrict__ routed,
+                                                  uint64_t* __restrict__ final_ps, uint32_t* __restrict__ slot_cnt,
+                                                  int32_t* __restrict__ diff, unsigned long long* __restrict__ counters)
+{
+   uint64_t hops = 0, nrouted = 0;
+   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const uint32_t s = src[i], d = dst[i];
+      const uint32_t fl = flags ? flags[i] : 0u;
+      const uint32_t b = bits[i];
+      // NetworkModel::computeNumFlits, network_model.cc:202-212
+      const uint32_t F = (b % c.flit_width) ? b / c.flit_width + 1 : b / c.flit_width;
+      const bool bypass = (s == d) || (fl & 1u);   // processCornerCases self-send; isModelEnabled()==false
+      aux[i] = aux_pack(d, F);
+      routed[i] = bypass ? 0 : 1;
+      if (bypass)
+      {
+         final_ps[i] = inj[i];
+         continue;
+      }
+      uint32_t sx, sy, dx, dy;
+      tile_xy(s, c.W, c.magicW, sx, sy);
+      tile_xy(d, c.W, c.magicW, dx, dy);
+      nrouted++;
+      hops += (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
+      atomicAdd(&slot_cnt[slot_of(s, P_INJ, IN_LOCAL)], 1u);
+      atomicAdd(&slot_cnt[slot_of(s, xy_dir(sx, sy, dx, dy), IN_LOCAL)], 1u);
+      const uint32_t ydir = dy > sy ? P_UP : dy < sy ? P_DOWN : P_SELF;
+      // diff layout: [0] RIGHT rows H x (W+1), [1] LEFT rows, [2] UP cols W x (H+1), [3] DOWN cols
+      int32_t* dR = diff;
+      int32_t* dL = dR + (size_t) c.H * (c.W + 1);
+      int32_t* dU = dL + (size_t) c.H * (c.W + 1);
+      int32_t* dD = dU + (size_t) c.W * (c.H + 1);
+      if (dx > sx)
+      {
+         if (dx > sx + 1) { atomicAdd(&dR[sy * (c.W + 1) + sx + 1], 1); atomicAdd(&dR[sy * (c.W + 1) + dx], -1); }
+         atomicAdd(&slot_cnt[slot_of(sy * c.W + dx, ydir, IN_W)], 1u);
+      }
+      else if (dx < sx)
+      {
+         if (dx + 1 < sx) { atomicAdd(&dL[sy * (c.W + 1) + dx + 1], 1); atomicAdd(&dL[sy * (c.W + 1) + sx], -1); }
+         atomicAdd(&slot_cnt[slot_of(sy * c.W + dx, ydir, IN_E)], 1u);
+      }
+      if (dy > sy)
+      {
+         if (dy > sy + 1) { atomicAdd(&dU[dx * (c.H + 1) + sy + 1], 1); atomicAdd(&dU[dx * (c.H + 1) + dy], -1); }
+         atomicAdd(&slot_cnt[slot_of(d, P_SELF, IN_S)], 1u);
+      }
+      else if (dy < sy)
+      {
+         if (dy + 1 < sy) { atomicAdd(&dD[dx * (c.H + 1) + dy + 1], 1); atomicAdd(&dD[dx * (c.H + 1) + sy], -1); }
+         atomicAdd(&slot_cnt[slot_of(d, P_SELF, IN_N)], 1u);
+      }
+   }
+   // block-reduce the two counters
+   __shared__ unsigned long long red[2][4];
+   for (int off = 32; off > 0; off >>= 1)
+   {
+      hops += __shfl_down(hops, off);
+      nrouted += __shfl_down(nrouted, off);
+   }
+   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+   if (l == 0) { red[0][w] = hops; red[1][w] = nrouted; }
+   __syncthreads();
+   if (threadIdx.x == 0)
+   {
+      unsigned long long h = 0, r = 0;
+      for (int k = 0; k < (int) (blockDim.x >> 6); k++) { h += red[0][k]; r += red[1][k]; }
+      atomicAdd(&counters[0], h);
+      atomicAdd(&counters[1], r);
+   }
+}
+
+// Turn the chain difference arrays into slot counts (one thread per row/column chain).
+__global__ void k_chain_prefix(DevCfg c, const int32_t* __restrict__ diff, uint32_t* __restrict__ slot_cnt)
+{
+   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+   const int32_t* dR = diff;
+   const int32_t* dL = dR + (size_t) c.H * (c.W + 1);
+   const int32_t* dU = dL + (size_t) c.H * (c.W + 1);
+   const int32_t* dD = dU + (size_t) c.W * (c.H + 1);
+   if (i < c.H)
+   {
+      int32_t r = 0, l = 0;
+      for (uint32_t x = 0; x < c.W; x++)
+      {
+         r += dR[i * (c.W + 1) + x];
+         l += dL[i * (c.W + 1) + x];
+         slot_cnt[slot_of(i * c.W + x, P_RIGHT, IN_W)] += (uint32_t) r;
+         slot_cnt[slot_of(i * c.W + x, P_LEFT, IN_E)] += (uint32_t) l;
+      }
+   }
+   else if (i < c.H + c.W)
+   {
+      const uint32_t x = i - c.H;
+      int32_t u = 0, d = 0;
+      for (uint32_t y = 0; y < c.H; y++)
+      {
+         u += dU[x * (c.H + 1) + y];
+         d += dD[x * (c.H + 1) + y];
+         slot_cnt[slot_of(y * c.W + x, P_UP, IN_S)] += (uint32_t) u;
+         slot_cnt[slot_of(y * c.W + x, P_DOWN, IN_N)] += (uint32_t) d;
+      }
+   }
+}
+
+// Exclusive scan of slot counts -> 64-bit slot bases; base[nslots] = total.
+// Single 1024-thread block; nslots = 30 N is small.
+__global__ __launch_bounds__(1024) void k_scan_slots(uint32_t nslots, const uint32_t* __restrict__ cnt,
+                                                     uint64_t* __restrict__ base)
+{
+   __shared__ uint64_t part[1024];
+   const uint32_t per = (nslots + 1023) / 1024;
+   const uint32_t lo = threadIdx.x * per, hi = min(lo + per, nslots);
+   uint64_t s = 0;
+   for (uint32_t i = lo; i < hi; i++) s += cnt[i];
+   part[threadIdx.x] = s;
+   __syncthreads();
+   for (uint32_t off = 1; off < 1024; off <<= 1)
+   {
+      uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+   }
+   uint64_t run = part[threadIdx.x] - s;
+   for (uint32_t i = lo; i < hi; i++) { base[i] = run; run += cnt[i]; }
+   if (threadIdx.x == 1023) base[nslots] = part[1023];
+}
+
+// ----------------------------------------------------------------------------
+// Injection grouping: stable partition of the (t, id)-ordered trace by source
+// tile into the injection-port input slots.  One wave per chunk; ranks among
+// equal sources inside a wave come from a ballot-built match mask.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t match_mask(uint32_t key, bool valid, int nbits)
+{
+   uint64_t m = __ballot(valid);
+   for (int b = 0; b < nbits; b++)
+   {
+      const bool bit = (key >> b) & 1u;
+      const uint64_t bb = __ballot(bit && valid);
+      m &= bit ? bb : ~bb;
+   }
+   return m;
+}
+
+template <bool SCATTER>
+__global__ __launch_bounds__(64) void k_inj_group(uint64_t n, uint32_t chunk, uint32_t N, int nbits,
+                                                  const uint32_t* __restrict__ src, const uint8_t* __restrict__ routed,
+                                                  const uint64_t* __restrict__ inj, const uint32_t* __restrict__ aux,
+                                                  uint32_t* __restrict__ hist, const uint64_t* __restrict__ offs,
+                                                  Rec* __restrict__ recs, uint32_t nchunks)
+{
+   extern __shared__ uint32_t h[];   // N counters
+   const uint32_t lane = threadIdx.x;
+   for (uint32_t s = lane; s < N; s += 64) h[s] = 0;
+   __syncthreads();
+   const uint64_t lo = (uint64_t) blockIdx.x * chunk;
+   const uint64_t hi = min(lo + chunk, n);
+   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+   for (uint64_t k = lo; k < hi; k += 64)
+   {
+      const uint64_t i = k + lane;
+      const bool valid = i < hi && routed[i];
+      const uint32_t s = valid ? src[i] : 0u;
+      const uint64_t m = match_mask(s, valid, nbits);
+      uint32_t old = valid ? h[s] : 0u;
+      __syncthreads();
+      const uint32_t rank = old + (uint32_t) __popcll(m & lt);
+      if (valid && (63 - __clzll(m)) == (int) lane) h[s] = old + (uint32_t) __popcll(m);
+      if (SCATTER && valid)
+      {
+         const uint64_t pos = offs[(uint64_t) s * nchunks + blockIdx.x] + rank;
+         Rec r;
+         r.t = inj[i];
+         r.id = (uint32_t) i;
+         r.aux = aux[i];
+         recs[pos] = r;
+      }
+      __syncthreads();
+   }
+   if (!SCATTER)
+      for (uint32_t s = lane; s < N; s += 64) hist[(uint64_t) s * nchunks + blockIdx.x] = h[s];
+}
+
+// Per source tile: exclusive scan over chunks, offset by the slot base.
+__global__ __launch_bounds__(256) void k_inj_offsets(uint32_t nchunks, const uint32_t* __restrict__ hist,
+                                                     const uint64_t* __restrict__ slot_base, uint64_t* __restrict__ offs)
+{
+   __shared__ uint64_t part[256];
+   const uint32_t s = blockIdx.x;
+   const uint32_t per = (nchunks + 255) / 256;
+   const uint32_t lo = threadIdx.x * per, hi = min(lo + per, nchunks);
+   const uint32_t* hrow = hist + (uint64_t) s * nchunks;
+   uint64_t sum = 0;
+   for (uint32_t i = lo; i < hi; i++) sum += hrow[i];
+   part[threadIdx.x] = sum;
+   __syncthreads();
+   for (uint32_t off = 1; off < 256; off <<= 1)
+   {
+      uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+   }
+   uint64_t run = part[threadIdx.x] - sum + slot_base[slot_of(s, P_INJ, IN_LOCAL)];
+   for (uint32_t i = lo; i < hi; i++) { offs[(uint64_t) s * nchunks + i] = run; run += hrow[i]; }
+}
+
+// ----------------------------------------------------------------------------
+// Port stream kernel: one workgroup owns one output-port queue and streams its
+// whole arrival history.  Per round: load up to T records of each input
+// stream into LDS, merge the prefix that is provably complete ((t,id) <= the
+// smallest last-loaded key of any stream with more data), run the queue
+// recurrence (serial M/G/1 prologue while the queue has never idled, then a
+// block-wide max-plus scan), and route every record to its next port's input
+// slot (or write the packet's final time at SELF).
+// ----------------------------------------------------------------------------
+constexpr int ST = 256;          // records per input per round
+constexpr int SMAXIN = 4;        // max input streams per port
+constexpr int SMAXE = ST * SMAXIN;
+constexpr int STHREADS = 256;
+
+struct SerialState
+{
+   uint64_t X;        // start of the tail free interval [X, inf)
+   int g;             // number of gap intervals in the history tree
+   int mode;          // 1 while the serial (tree + M/G/1) path is required
+   double s1, s2;     // QueueModelMG1 sums
+   uint64_t narr, newest;
+   uint64_t mg1;
+};
+
+struct PortSmem
+{
+   uint64_t in_t[SMAXIN][ST];
+   uint32_t in_id[SMAXIN][ST];
+   uint32_t in_aux[SMAXIN][ST];
+   uint64_t m_t[SMAXE];
+   uint32_t m_id[SMAXE];
+   uint32_t m_aux[SMAXE];
+   uint64_t m_c[SMAXE];
+   uint64_t wA[STHREADS / 64], wB[STHREADS / 64], wC[STHREADS / 64];
+   uint32_t e_cnt[SMAXIN];
+   uint32_t s0;
+   SerialState ss;
+};
+
+__device__ __forceinline__ bool key_le(uint64_t t1, uint32_t i1, uint64_t t2, uint32_t i2)
+{
+   return t1 < t2 || (t1 == t2 && i1 <= i2);
+}
+__device__ __forceinline__ bool key_lt(uint64_t t1, uint32_t i1, uint64_t t2, uint32_t i2)
+{
+   return t1 < t2 || (t1 == t2 && i1 < i2);
+}
+
+// QueueModelMG1::computeQueueDelay (queue_model_m_g_1.cc:17-46); same operation
+// order; this translation unit is compiled with -ffp-contract=off.
+__device__ uint64_t mg1_delay(const SerialState& s)
+{
+   if (s.narr == 0) return 0;
+   double variance = ((s.s2 / (double) s.narr) - ((s.s1 / (double) s.narr) * (s.s1 / (double) s.narr)));
+   double service_rate = 1.0 / (s.s1 / (double) s.narr);
+   double arrival_rate = ((double) s.narr) / (double) s.newest;
+   if (arrival_rate >= service_rate) arrival_rate = 0.999 * service_rate;
+   return (uint64_t) ceil(0.5 * service_rate * arrival_rate * ((1 / (service_rate * service_rate)) + variance) /
+                          (service_rate - arrival_rate));
+}
+
+// One history-tree request with arrivals in non-decreasing time
+// (queue_model_history_tree.cc:43-126 specialised; DESIGN.md "queue").
+__device__ uint64_t serial_step(SerialState& s, uint64_t t, uint64_t p, int L, int analytical)
+{
+   if (s.g + 1 >= L) s.g--;   // :50-56 prune the oldest free interval
+   uint64_t d;
+   if (analytical && s.g == 0 && s.X > t + p)
+   {
+      d = mg1_delay(s);        // :58-64 M/G/1 fallback, tree untouched
+      s.mg1++;
+   }
+   else if (t >= s.X)
+   {
+      d = 0;
+      if (t - s.X >= 1) s.g++;   // :79-86 idle period becomes a gap
+      s.X = t + p;
+   }
+   else
+   {
+      d = s.X - t;               // :101-112 wait for the tail interval
+      s.X = s.X + p;
+   }
+   // QueueModelMG1::updateQueue, queue_model_m_g_1.cc:48-56
+   s.s2 += ((double) p * (double) p);
+   s.s1 += (double) p;
+   s.narr++;
+   const uint64_t nw = t + d + p;
+   s.newest = s.newest > nw ? s.newest : nw;
+   return d;
+}
+
+// ----------------------------------------------------------------------------
+// Fixup: restore (t, id) order of an input slot whose producer emitted out of
+// FIFO order (rare: M/G/1 requests, or f != 1 GHz ties).  Run by the consuming
+// port's workgroup before it streams the slot.
+// ----------------------------------------------------------------------------
+constexpr int FIX_LDS = 2048;
+
+struct FixSmem
+{
+   uint64_t kt[FIX_LDS];
+   uint32_t ki[FIX_LDS];
+   uint32_t ka[FIX_LDS];
+};
+
+__device__ void fixup_slot(FixSmem& fx, Rec* __restrict__ r, uint32_t n)
+{
+   const uint32_t tid = threadIdx.x;
+   if (n <= 1) return;
+   if (n <= (uint32_t) FIX_LDS)
+   {
+      uint32_t P = 1;
+      while (P < n) P <<= 1;
+      for (uint32_t i = tid; i < P; i += blockDim.x)
+      {
+         if (i < n) { fx.kt[i] = r[i].t; fx.ki[i] = r[i].id; fx.ka[i] = r[i].aux; }
+         else { fx.kt[i] = ~0ull; fx.ki[i] = ~0u; fx.ka[i] = 0; }
+      }
+      __syncthreads();
+      for (uint32_t k = 2; k <= P; k <<= 1)
+      {
+         for (uint32_t j = k >> 1; j > 0; j >>= 1)
+         {
+            for (uint32_t i = tid; i < P; i += blockDim.x)
+            {
+               const uint32_t l = i ^ j;
+               if (l > i)
+               {
+                  const bool up = (i & k) == 0;
+                  const bool gt = key_lt(fx.kt[l], fx.ki[l], fx.kt[i], fx.ki[i]);
+                  if (gt == up)
+                  {
+                     uint64_t tt = fx.kt[i]; fx.kt[i] = fx.kt[l]; fx.kt[l] = tt;
+                     uint32_t ti = fx.ki[i]; fx.ki[i] = fx.ki[l]; fx.ki[l] = ti;
+                     uint32_t ta = fx.ka[i]; fx.ka[i] = fx.ka[l]; fx.ka[l] = ta;
+                  }
+               }
+            }
+            __syncthreads();
+         }
+      }
+      for (uint32_t i = tid; i < n; i += blockDim.x)
+      {
+         Rec o;
+         o.t = fx.kt[i];
+         o.id = fx.ki[i];
+         o.aux = fx.ka[i];
+         r[i] = o;
+      }
+   }
+   else if (tid == 0)
+   {
+      // nearly sorted: insertion sort, O(n + inversions)
+      for (uint32_t i = 1; i < n; i++)
+      {
+         const Rec v = r[i];
+         uint32_t j = i;
+         while (j > 0 && key_lt(v.t, v.id, r[j - 1].t, r[j - 1].id)) { r[j] = r[j - 1]; j--; }
+         r[j] = v;
+      }
+   }
+   __syncthreads();
+}
+
+template <bool F1>
+__global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32_t* __restrict__ ports,
+                                                          const uint32_t* __restrict__ slot_cnt,
+                                                          const uint64_t* __restrict__ slot_base,
+                                                          Rec* __restrict__ recs, uint64_t* __restrict__ final_ps,
+                                                          uint64_t* __restrict__ port_sum, uint64_t* __restrict__ port_cnt,
+                                                          uint64_t* __restrict__ port_mg1, uint32_t* __restrict__ dirty,
+                                                          unsigned int* __restrict__ errflag)
+{
+   __shared__ __attribute__((aligned(16))) char smraw[sizeof(PortSmem) > sizeof(FixSmem) ? sizeof(PortSmem) : sizeof(FixSmem)];
+   PortSmem& sm = *reinterpret_cast<PortSmem*>(smraw);
+   FixSmem& fx = *reinterpret_cast<FixSmem*>(smraw);
+   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+   const uint32_t port = ports[blockIdx.x];
+   const uint32_t tile = port / PORTS, dir = port % PORTS;
+
+   // restore order of input slots a producer flagged (M/G/1 or f != 1 ties)
+   for (uint32_t in = 0; in < INS; in++)
+   {
+      const uint32_t sl = slot_of(tile, dir, in);
+      if (dirty[sl])
+      {
+         fixup_slot(fx, recs + slot_base[sl], slot_cnt[sl]);
+         if (tid == 0) dirty[sl] = 0;
+      }
+   }
+   __syncthreads();
+
+   // input streams (non-empty slots of this port), block-uniform
+   uint64_t ib[SMAXIN];
+   uint32_t icnt[SMAXIN];
+   uint32_t nin = 0;
+   for (uint32_t in = 0; in < INS; in++)
+   {
+      const uint32_t sl = slot_of(tile, dir, in);
+      const uint32_t k = slot_cnt[sl];
+      if (k && nin < SMAXIN) { ib[nin] = slot_base[sl]; icnt[nin] = k; nin++; }
+   }
+   for (uint32_t k = nin; k < SMAXIN; k++) { ib[k] = 0; icnt[k] = 0; }
+
+   // output: next tile and input side (same for every record of this port)
+   uint32_t tx, ty;
+   tile_xy(tile, c.W, c.magicW, tx, ty);
+   uint32_t ntile = tile, nin_side = IN_LOCAL;
+   if (dir == P_RIGHT) { ntile = tile + 1; nin_side = IN_W; }
+   else if (dir == P_LEFT) { ntile = tile - 1; nin_side = IN_E; }
+   else if (dir == P_UP) { ntile = tile + c.W; nin_side = IN_S; }
+   else if (dir == P_DOWN) { ntile = tile - c.W; nin_side = IN_N; }
+   uint32_t nx, ny;
+   tile_xy(ntile, c.W, c.magicW, nx, ny);
+   uint64_t obase[5];
+   uint32_t ocap[5];
+   for (uint32_t d = 0; d < 5; d++)
+   {
+      obase[d] = slot_base[slot_of(ntile, d, nin_side)];
+      ocap[d] = slot_cnt[slot_of(ntile, d, nin_side)];
+   }
+   uint32_t ocur[5] = { 0, 0, 0, 0, 0 };   // records written per next-direction
+
+   uint32_t cur[SMAXIN] = { 0, 0, 0, 0 };
+   uint64_t X0 = 0;                         // carried queue state (cycles)
+   uint64_t st_sum = 0, st_cnt = 0;
+   bool first_round = true;
+
+   if (tid == 0)
+   {
+      sm.ss.X = 0; sm.ss.g = 0; sm.ss.mode = 0; sm.ss.s1 = 0; sm.ss.s2 = 0;
+      sm.ss.narr = 0; sm.ss.newest = 0; sm.ss.mg1 = 0;
+   }
+
+   for (;;)
+   {
+      uint32_t nl[SMAXIN];
+      uint32_t remtot = 0;
+      for (uint32_t k = 0; k < SMAXIN; k++)
+      {
+         const uint32_t rem = icnt[k] - cur[k];
+         nl[k] = rem < (uint32_t) ST ? rem : (uint32_t) ST;
+         remtot += rem;
+      }
+      if (remtot == 0) break;
+
+      // ---- load
+      for (uint32_t j = tid; j < (uint32_t) SMAXE; j += STHREADS)
+      {
+         const uint32_t k = j / ST, i = j % ST;
+         if (i < nl[k])
+         {
+            const Rec r = recs[ib[k] + cur[k] + i];
+            sm.in_t[k][i] = r.t;
+            sm.in_id[k][i] = r.id;
+            sm.in_aux[k][i] = r.aux;
+         }
+      }
+      __syncthreads();
+
+      // ---- bound = min last-loaded key over streams that continue past this round
+      uint64_t bt = ~0ull;
+      uint32_t bi = ~0u;
+      for (uint32_t k = 0; k < SMAXIN; k++)
+      {
+         if (icnt[k] - cur[k] > nl[k])
+         {
+            const uint64_t t = sm.in_t[k][nl[k] - 1];
+            const uint32_t id = sm.in_id[k][nl[k] - 1];
+            if (key_lt(t, id, bt, bi)) { bt = t; bi = id; }
+         }
+      }
+
+      // ---- merge: rank = own index + #smaller keys in the other streams
+      for (uint32_t j = tid; j < (uint32_t) SMAXE; j += STHREADS)
+      {
+         const uint32_t k = j / ST, i = j % ST;
+         if (i >= nl[k]) continue;
+         const uint64_t t = sm.in_t[k][i];
+         const uint32_t id = sm.in_id[k][i];
+         if (!key_le(t, id, bt, bi)) continue;
+         uint32_t rank = i;
+         for (uint32_t o = 0; o < SMAXIN; o++)
+         {
+            if (o == k || nl[o] == 0) continue;
+            uint32_t lo = 0, hi = nl[o];
+            while (lo < hi)
+            {
+               const uint32_t mid = (lo + hi) >> 1;
+               if (key_lt(sm.in_t[o][mid], sm.in_id[o][mid], t, id)) lo = mid + 1; else hi = mid;
+            }
+            rank += lo;
+         }
+         sm.m_t[rank] = t;
+         sm.m_id[rank] = id;
+         sm.m_aux[rank] = sm.in_aux[k][i];
+      }
+      if (tid < SMAXIN)
+      {
+         // emitted count of stream tid: upper_bound of the bound key
+         uint32_t lo = 0, hi = nl[tid];
+         while (lo < hi)
+         {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (key_le(sm.in_t[tid][mid], sm.in_id[tid][mid], bt, bi)) lo = mid + 1; else hi = mid;
+         }
+         sm.e_cnt[tid] = lo;
+      }
+      __syncthreads();
+      uint32_t E = 0;
+      for (uint32_t k = 0; k < SMAXIN; k++) E += sm.e_cnt[k];
+
+      // ---- queue recurrence
+      if (first_round)
+      {
+         first_round = false;
+         if (tid == 0 && c.analytical && E > 0 &&
+             (c.max_list <= 2 || cyc_of<F1>(sm.m_t[0], c.f) == 0))
+         {
+            sm.ss.mode = 1;
+         }
+         __syncthreads();
+      }
+      if (sm.ss.mode)
+      {
+         if (tid == 0)
+         {
+            SerialState s = sm.ss;
+            s.X = X0;
+            uint32_t e = 0;
+            for (; e < E && s.mode; e++)
+            {
+               const uint64_t tc = cyc_of<F1>(sm.m_t[e], c.f);
+               const uint64_t p = aux_F(sm.m_aux[e]);
+               sm.m_c[e] = serial_step(s, tc, p, c.max_list, c.analytical);
+               if (c.max_list > 2 && s.g >= 1) s.mode = 0;
+            }
+            sm.s0 = e;
+            sm.ss = s;
+         }
+         __syncthreads();
+         X0 = sm.ss.X;
+      }
+      else if (tid == 0)
+      {
+         sm.s0 = 0;
+      }
+      __syncthreads();
+      const uint32_t s0 = sm.s0;
+
+      // block max-plus scan over [s0, E): element map X -> max(X + p, tc + p)
+      {
+         const uint32_t cnt = E - s0;
+         const uint32_t per = (cnt + STHREADS - 1) / STHREADS;
+         const uint32_t lo = s0 + min(tid * per, cnt), hi = s0 + min((tid + 1) * per, cnt);
+         uint64_t A = 0, B = 0;
+         for (uint32_t e = lo; e < hi; e++)
+         {
+            const uint64_t tc = cyc_of<F1>(sm.m_t[e], c.f);
+            const uint64_t p = aux_F(sm.m_aux[e]);
+            A += p;
+            const uint64_t b1 = B + p, b2 = tc + p;
+            B = b1 > b2 ? b1 : b2;
+         }
+         // inclusive wave scan of (A,B) with op (a1,b1).(a2,b2) = (a1+a2, max(b1+a2, b2))
+         uint64_t iA = A, iB = B;
+         for (int off = 1; off < 64; off <<= 1)
+         {
+            const uint64_t pA = __shfl_up(iA, off), pB = __shfl_up(iB, off);
+            if ((int) lane >= off)
+            {
+               const uint64_t nb = pB + iA;
+               iB = nb > iB ? nb : iB;
+               iA = pA + iA;
+            }
+         }
+         if (lane == 63) { sm.wA[wv] = iA; sm.wB[wv] = iB; }
+         __syncthreads();
+         // prefix of whole waves before this one
+         uint64_t PA = 0, PB = 0;
+         for (uint32_t w = 0; w < wv; w++)
+         {
+            const uint64_t nb = PB + sm.wA[w];
+            PB = nb > sm.wB[w] ? nb : sm.wB[w];
+            PA += sm.wA[w];
+         }
+         // exclusive within wave
+         uint64_t eA = __shfl_up(iA, 1), eB = __shfl_up(iB, 1);
+         if (lane == 0) { eA = 0; eB = 0; }
+         // combine: prefix(waves) then exclusive(lanes)
+         const uint64_t nb = PB + eA;
+         const uint64_t CB = nb > eB ? nb : eB;
+         const uint64_t CA = PA + eA;
+         uint64_t X = X0 + CA;
+         X = X > CB ? X : CB;
+         for (uint32_t e = lo; e < hi; e++)
+         {
+            const uint64_t tc = cyc_of<F1>(sm.m_t[e], c.f);
+            const uint64_t p = aux_F(sm.m_aux[e]);
+            sm.m_c[e] = X > tc ? X - tc : 0;
+            X = (X > tc ? X : tc) + p;
+         }
+         // new carry = X0 composed with the whole block
+         uint64_t TA = 0, TB = 0;
+         for (uint32_t w = 0; w < STHREADS / 64; w++)
+         {
+            const uint64_t b = TB + sm.wA[w];
+            TB = b > sm.wB[w] ? b : sm.wB[w];
+            TA += sm.wA[w];
+         }
+         const uint64_t nx0 = X0 + TA;
+         X0 = nx0 > TB ? nx0 : TB;
+      }
+      __syncthreads();
+
+      // ---- outputs: route each record; positions by block prefix count per next direction
+      {
+         const uint32_t per = (E + STHREADS - 1) / STHREADS;
+         const uint32_t lo = min(tid * per, E), hi = min((tid + 1) * per, E);
+         uint64_t packed = 0;   // 5 x 12-bit counters
+         for (uint32_t e = lo; e < hi; e++)
+         {
+            uint32_t ndir = 0;
+            if (dir != P_SELF)
+            {
+               uint32_t dx, dy;
+               tile_xy(aux_dst(sm.m_aux[e]), c.W, c.magicW, dx, dy);
+               ndir = xy_dir(nx, ny, dx, dy);
+            }
+            packed += 1ull << (12 * ndir);
+         }
+         uint64_t inc = packed;
+         for (int off = 1; off < 64; off <<= 1)
+         {
+            const uint64_t v = __shfl_up(inc, off);
+            if ((int) lane >= off) inc += v;
+         }
+         if (lane == 63) sm.wC[wv] = inc;
+         __syncthreads();
+         uint64_t pre = inc - packed;
+         for (uint32_t w = 0; w < wv; w++) pre += sm.wC[w];
+         uint64_t tot = 0;
+         for (uint32_t w = 0; w < STHREADS / 64; w++) tot += sm.wC[w];
+         for (uint32_t e = lo; e < hi; e++)
+         {
+            const uint64_t t = sm.m_t[e];
+            const uint32_t id = sm.m_id[e], ax = sm.m_aux[e];
+            const uint64_t cc = sm.m_c[e];
+            st_sum += cc;
+            st_cnt++;
+            const uint64_t tn = t + ps_of<F1>(cc, c.f) + (dir == P_INJ ? 0ull : c.rl_ps);
+            if (dir == P_SELF)
+            {
+               final_ps[id] = tn + ps_of<F1>(aux_F(ax), c.f);
+               continue;
+            }
+            uint32_t dx, dy;
+            tile_xy(aux_dst(ax), c.W, c.magicW, dx, dy);
+            const uint32_t ndir = xy_dir(nx, ny, dx, dy);
+            const uint32_t r = (uint32_t) ((pre >> (12 * ndir)) & 0xFFF);
+            pre += 1ull << (12 * ndir);
+            if (ocur[ndir] + r >= ocap[ndir])
+            {
+               atomicOr(errflag, 1u);   // route-count invariant broken: never write out of the slot
+               continue;
+            }
+            Rec o;
+            o.t = tn;
+            o.id = id;
+            o.aux = ax;
+            recs[obase[ndir] + ocur[ndir] + r] = o;
+         }
+         for (uint32_t d = 0; d < 5; d++) ocur[d] += (uint32_t) ((tot >> (12 * d)) & 0xFFF);
+      }
+
+      for (uint32_t k = 0; k < SMAXIN; k++) cur[k] += sm.e_cnt[k];
+      __syncthreads();
+   }
+
+   // ---- per-port counters (RouterModel::updateContentionCounters, router_model.cc:136-144)
+   for (int off = 32; off > 0; off >>= 1)
+   {
+      st_sum += __shfl_down(st_sum, off);
+      st_cnt += __shfl_down(st_cnt, off);
+   }
+   if (lane == 0) { sm.wA[wv] = st_sum; sm.wB[wv] = st_cnt; }
+   __syncthreads();
+   if (tid == 0)
+   {
+      uint64_t a = 0, b = 0;
+      for (uint32_t w = 0; w < STHREADS / 64; w++) { a += sm.wA[w]; b += sm.wB[w]; }
+      port_sum[port] = a;
+      port_cnt[port] = b;
+      port_mg1[port] = sm.ss.mg1;
+      // Outputs can leave FIFO order only through M/G/1 requests or, for f != 1,
+      // equal-time pairs; mark this port's output slots for the fixup sort.
+      if (dir != P_SELF && (sm.ss.mg1 > 0 || !F1))
+         for (uint32_t d = 0; d < 5; d++) dirty[slot_of(ntile, d, nin_side)] = 1;
+   }
+}
+
+// ----------------------------------------------------------------------------
+// Finalize: zero-load and contention per packet (NetPacket fields).
+// ----------------------------------------------------------------------------
+template <bool F1>
+__global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const uint64_t* __restrict__ inj,
+                                                  const uint32_t* __restrict__ src, const uint32_t* __restrict__ aux,
+                                                  const uint8_t* __restrict__ routed, uint64_t* __restrict__ final_ps,
+                                                  uint64_t* __restrict__ zl, uint64_t* __restrict__ cont, int closed_form)
+{
+   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+   {
+      if (!routed[i]) { zl[i] = 0; cont[i] = 0; continue; }
+      uint32_t sx, sy, dx, dy;
+      tile_xy(src[i], c.W, c.magicW, sx, sy);
+      tile_xy(aux_dst(aux[i]), c.W, c.magicW, dx, dy);
+      const uint64_t hops = (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
+      // Hop::Hop accumulates Latency(0) at injection, Latency(R+Lk) per mesh router,
+      // Latency(F) at receive (network_model.cc:142-150, 556-563).
+      const uint64_t z = ps_of<F1>(0, c.f) + hops * c.rl_ps + ps_of<F1>(aux_F(aux[i]), c.f);
+      zl[i] = z;
+      if (closed_form) final_ps[i] = inj[i] + z;
+      cont[i] = final_ps[i] - inj[i] - z;
+   }
+}
+
+// explicit instantiations
+template __global__ void k_inj_group<false>(uint64_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
+                                            const uint64_t*, const uint32_t*, uint32_t*, const uint64_t*, Rec*, uint32_t);
+template __global__ void k_inj_group<true>(uint64_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
+                                           const uint64_t*, const uint32_t*, uint32_t*, const uint64_t*, Rec*, uint32_t);
+template __global__ void k_port_stream<true>(DevCfg, const uint32_t*, const uint32_t*, const uint64_t*, Rec*, uint64_t*,
+                                             uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
+template __global__ void k_port_stream<false>(DevCfg, const uint32_t*, const uint32_t*, const uint64_t*, Rec*, uint64_t*,
+                                              uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
+template __global__ void k_finalize<true>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,
+                                          const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int);
+template __global__ void k_finalize<false>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,
+                                           const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int);
+
+}  // namespace gnoc

@@ -1,0 +1,137 @@
+// trace.cpp -- synthetic packet traces (host side, not on the timed path).
+//
+// Restates the traffic of tests/benchmarks/synthetic_network/synthetic_network.cc
+// so the engine and the oracle see the same deterministic, timestamp-ordered
+// input the reference app would inject (with fixed seeds instead of time(NULL)).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "gnoc.h"
+
+namespace {
+
+// glibc drand48_r: x <- (0x5DEECE66D x + 0xB) mod 2^48, result x / 2^48;
+// srand48_r(seed): x = (seed << 16) | 0x330E  (common/misc/random.h:15-28).
+struct Drand48
+{
+   uint64_t x;
+   explicit Drand48(long seed) { x = ((uint64_t) (uint32_t) seed << 16) | 0x330Eull; }
+   double next()
+   {
+      x = (0x5DEECE66Dull * x + 0xBull) & ((1ull << 48) - 1);
+      return (double) x / 281474976710656.0;   // exact: 48-bit mantissa
+   }
+};
+
+// NetworkModelEMeshHopByHop::computeMemoryControllerPositions, emesh_hop_by_hop.cc:323-364
+std::vector<uint32_t> mc_positions(int W, int H, int num)
+{
+   std::vector<uint32_t> out;
+   const int mw = (int) std::floor(std::sqrt((double) num));
+   const int mh = (int) std::ceil(1.0 * num / mw);
+   int k = 0;
+   for (int j = 0; j < mh && k < num; j++)
+      for (int i = 0; i < mw && k < num; i++)
+      {
+         int sx = W / mw, sy = H / mh;
+         const int bx = i * sx, by = j * sy;
+         if (i == mw - 1) sx = W - (mw - 1) * sx;
+         if (j == mh - 1) sy = H - (mh - 1) * sy;
+         out.push_back((uint32_t) ((bx + sx / 2) + (by + sy / 2) * W));
+         k++;
+      }
+   return out;
+}
+
+}  // namespace
+
+extern "C" int gnoc_trace_synthetic(int32_t W, int32_t H, double f, double load, uint64_t ppt, uint32_t payload,
+                                    uint64_t seed, double hot_frac, int32_t num_hot, uint64_t* inject_ps,
+                                    uint32_t* src, uint32_t* dst, uint32_t* bits, size_t capacity, size_t* n_out)
+{
+   if (W <= 0 || H <= 0 || !(f > 0) || !(load > 0) || load > 1.0 || !n_out) return GNOC_EINVAL;
+   const int N = W * H;
+   const uint64_t total = (uint64_t) N * ppt;
+   *n_out = (size_t) total;
+   if (!inject_ps) return GNOC_OK;
+   if (capacity < total || !src || !dst || !bits) return GNOC_EINVAL;
+   if (hot_frac > 0 && num_hot <= 0) return GNOC_EINVAL;
+
+   // uniformRandomTrafficGenerator, synthetic_network.cc:247-301: send_matrix[slot][sender]
+   std::vector<uint32_t> sendm((size_t) N * N);
+   sendm[0] = (uint32_t) (N / 2);
+   for (int i = 0; i < N; i++)
+   {
+      if (i) sendm[(size_t) i * N] = sendm[(size_t) (i - 1) * N + 1 % N];
+      for (int j = 1; j < N; j++)
+         sendm[(size_t) i * N + j] = (uint32_t) ((13ull * sendm[(size_t) i * N + j - 1] + 5) % (uint64_t) N);
+   }
+   // the reference asserts every slot row and sender column is a permutation (:269-293)
+   {
+      std::vector<uint8_t> seen(N);
+      for (int i = 0; i < N; i++)
+      {
+         std::fill(seen.begin(), seen.end(), 0);
+         for (int j = 0; j < N; j++) seen[sendm[(size_t) i * N + j]] = 1;
+         for (int j = 0; j < N; j++) if (!seen[j]) return GNOC_EINVAL;
+      }
+   }
+   const std::vector<uint32_t> hot = hot_frac > 0 ? mc_positions(W, H, num_hot) : std::vector<uint32_t>();
+
+   // Per tile: the cycle of each send (Bernoulli per cycle while packets remain,
+   // synthetic_network.cc:182-221, canSendPacket :230-233).
+   std::vector<std::vector<uint64_t>> cyc(N);
+   std::vector<std::vector<uint32_t>> dsts(N);
+   auto work = [&](int t0, int t1) {
+      for (int t = t0; t < t1; t++)
+      {
+         Drand48 r((long) (seed + (uint64_t) t));
+         Drand48 rh((long) (seed + 0x5bd1e995ull + (uint64_t) t));
+         auto& c = cyc[t];
+         auto& d = dsts[t];
+         c.resize(ppt);
+         d.resize(ppt);
+         uint64_t sent = 0;
+         for (uint64_t cycle = 0; sent < ppt; cycle++)
+         {
+            if (r.next() * 1.0 < load)
+            {
+               uint32_t dd = sendm[(size_t) (sent % (uint64_t) N) * N + t];
+               if (hot_frac > 0 && rh.next() < hot_frac)
+                  dd = hot[(size_t) (rh.next() * (double) hot.size()) % hot.size()];
+               c[sent] = cycle;
+               d[sent] = dd;
+               sent++;
+            }
+         }
+      }
+   };
+   const int nth = (int) std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+   std::vector<std::thread> th;
+   for (int k = 0; k < nth; k++) th.emplace_back(work, (int) ((int64_t) N * k / nth), (int) ((int64_t) N * (k + 1) / nth));
+   for (auto& x : th) x.join();
+
+   // global (cycle, src) order via counting sort on cycle; stable in src
+   uint64_t maxc = 0;
+   for (int t = 0; t < N; t++) if (ppt) maxc = std::max(maxc, cyc[t][ppt - 1]);
+   std::vector<uint64_t> start(maxc + 2, 0);
+   for (int t = 0; t < N; t++) for (uint64_t k = 0; k < ppt; k++) start[cyc[t][k] + 1]++;
+   for (uint64_t k = 1; k < start.size(); k++) start[k] += start[k - 1];
+   // ONE_CYCLE = Latency(1, f) in picoseconds (synthetic_network.cc:224)
+   const uint64_t one = (uint64_t) std::ceil(((double) 1000 * 1.0) / f);
+   const uint32_t nbits = (64u + payload) * 8u;   // NetPacket::bufferSize()*8, network.cc:705-708
+   for (int t = 0; t < N; t++)
+      for (uint64_t k = 0; k < ppt; k++)
+      {
+         const uint64_t pos = start[cyc[t][k]]++;
+         inject_ps[pos] = cyc[t][k] * one;
+         src[pos] = (uint32_t) t;
+         dst[pos] = dsts[t][k];
+         bits[pos] = nbits;
+      }
+   return GNOC_OK;
+}

@@ -1,0 +1,269 @@
+"""ctypes binding of the C ABI in include/gnoc.h (libgnoc.so).
+
+This is plumbing for tests and bench.py: the product is the HIP engine behind
+the C ABI.  Loading fails loudly if the built library is missing -- there is
+no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libgnoc.so")
+
+GNOC_OK = 0
+GNOC_EINVAL = -1
+GNOC_ETRACE = -2
+GNOC_EHIP = -3
+GNOC_ESTATE = -4
+GNOC_EUNSUPPORTED = -5
+GNOC_ENOMEM = -6
+
+PORT_SELF, PORT_LEFT, PORT_RIGHT, PORT_DOWN, PORT_UP, PORT_INJ = range(6)
+PORTS_PER_TILE = 6
+PKT_UNMODELED = 0x1
+
+# Every symbol include/gnoc.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "gnoc_config_default", "gnoc_create", "gnoc_submit", "gnoc_submit_device", "gnoc_run",
+    "gnoc_get_packet_results", "gnoc_get_port_stats", "gnoc_get_summary", "gnoc_device_final_ps",
+    "gnoc_last_error", "gnoc_destroy", "gnoc_trace_synthetic", "gnoc_abi_version",
+)
+
+
+class GnocConfig(ctypes.Structure):
+    _fields_ = [
+        ("mesh_width", ctypes.c_int32),
+        ("mesh_height", ctypes.c_int32),
+        ("num_tiles", ctypes.c_int32),
+        ("flit_width", ctypes.c_int32),
+        ("router_delay", ctypes.c_uint64),
+        ("link_delay", ctypes.c_uint64),
+        ("frequency_ghz", ctypes.c_double),
+        ("tile_width_mm", ctypes.c_double),
+        ("contention_enabled", ctypes.c_int32),
+        ("queue_type", ctypes.c_int32),
+        ("analytical_enabled", ctypes.c_int32),
+        ("max_list_size", ctypes.c_int32),
+        ("broadcast_tree_enabled", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+    ]
+
+
+class GnocPackets(ctypes.Structure):
+    _fields_ = [
+        ("inject_ps", ctypes.c_void_p),
+        ("src", ctypes.c_void_p),
+        ("dst", ctypes.c_void_p),
+        ("bits", ctypes.c_void_p),
+        ("flags", ctypes.c_void_p),
+    ]
+
+
+class GnocSummary(ctypes.Structure):
+    _fields_ = [
+        ("packets", ctypes.c_uint64),
+        ("routed_packets", ctypes.c_uint64),
+        ("mesh_hops", ctypes.c_uint64),
+        ("records", ctypes.c_uint64),
+        ("mg1_uses", ctypes.c_uint64),
+        ("levels", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("last_run_ms", ctypes.c_double),
+    ]
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libgnoc.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    lib.gnoc_config_default.argtypes = [ctypes.POINTER(GnocConfig), ctypes.c_int32]
+    lib.gnoc_config_default.restype = None
+    lib.gnoc_create.argtypes = [ctypes.POINTER(GnocConfig), ctypes.POINTER(vp)]
+    lib.gnoc_submit.argtypes = [vp, ctypes.POINTER(GnocPackets), sz]
+    lib.gnoc_submit_device.argtypes = [vp, ctypes.POINTER(GnocPackets), sz]
+    lib.gnoc_run.argtypes = [vp]
+    lib.gnoc_get_packet_results.argtypes = [vp, vp, vp, vp, sz]
+    lib.gnoc_get_port_stats.argtypes = [vp, vp, vp, vp, sz]
+    lib.gnoc_get_summary.argtypes = [vp, ctypes.POINTER(GnocSummary)]
+    lib.gnoc_device_final_ps.argtypes = [vp, ctypes.POINTER(vp)]
+    lib.gnoc_last_error.argtypes = [vp]
+    lib.gnoc_last_error.restype = ctypes.c_char_p
+    lib.gnoc_destroy.argtypes = [vp]
+    lib.gnoc_destroy.restype = None
+    lib.gnoc_trace_synthetic.argtypes = [
+        ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint32,
+        ctypes.c_uint64, ctypes.c_double, ctypes.c_int32, vp, vp, vp, vp, sz, ctypes.POINTER(sz)]
+    lib.gnoc_abi_version.argtypes = []
+    _lib = lib
+    return lib
+
+
+class GnocError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"gnoc error {code}: {msg}")
+        self.code = code
+
+
+@dataclass
+class EngineConfig:
+    """The carbon_sim.cfg keys the emesh_hop_by_hop path reads."""
+    num_tiles: int = 64                     # general/total_cores
+    mesh_width: int = 0                     # derived: floor(sqrt(N))
+    mesh_height: int = 0                    # derived: ceil(N / W)
+    flit_width: int = 64                    # network/emesh_hop_by_hop/flit_width
+    router_delay: int = 1                   # network/emesh_hop_by_hop/router/delay
+    link_delay: int = 1                     # network/emesh_hop_by_hop/link/delay
+    frequency_ghz: float = 1.0              # network DVFS domain
+    tile_width_mm: float = 1.0              # general/tile_width
+    contention_enabled: bool = True         # network/emesh_hop_by_hop/queue_model/enabled
+    queue_type: int = 0                     # history_tree
+    analytical_enabled: bool = True         # queue_model/history_tree/analytical_model_enabled
+    max_list_size: int = 100                # queue_model/history_tree/max_list_size
+    broadcast_tree_enabled: bool = True
+    device: int = 0
+
+    @property
+    def width(self) -> int:
+        import math
+        return self.mesh_width or int(math.floor(math.sqrt(self.num_tiles)))
+
+    @property
+    def height(self) -> int:
+        import math
+        return self.mesh_height or int(math.ceil(self.num_tiles / self.width))
+
+    def to_c(self) -> GnocConfig:
+        c = GnocConfig()
+        for f in GnocConfig._fields_:
+            v = getattr(self, f[0])
+            setattr(c, f[0], int(v) if not isinstance(v, float) else v)
+        return c
+
+
+@dataclass
+class Trace:
+    inject_ps: np.ndarray
+    src: np.ndarray
+    dst: np.ndarray
+    bits: np.ndarray
+    flags: Optional[np.ndarray] = None
+
+    def __len__(self) -> int:
+        return int(self.inject_ps.shape[0])
+
+    def normalized(self) -> "Trace":
+        f = self.flags if self.flags is not None else np.zeros(len(self), np.uint32)
+        return Trace(np.ascontiguousarray(self.inject_ps, np.uint64), np.ascontiguousarray(self.src, np.uint32),
+                     np.ascontiguousarray(self.dst, np.uint32), np.ascontiguousarray(self.bits, np.uint32),
+                     np.ascontiguousarray(f, np.uint32))
+
+
+def synthetic_trace(width: int, height: int, offered_load: float, packets_per_tile: int, seed: int = 1,
+                    payload_bytes: int = 8, frequency_ghz: float = 1.0, hotspot_fraction: float = 0.0,
+                    num_hotspots: int = 16) -> Trace:
+    lib = load()
+    n = ctypes.c_size_t(0)
+    rc = lib.gnoc_trace_synthetic(width, height, frequency_ghz, offered_load, packets_per_tile, payload_bytes,
+                                  seed, hotspot_fraction, num_hotspots, None, None, None, None, 0, ctypes.byref(n))
+    if rc:
+        raise GnocError(rc, "trace size query failed")
+    N = n.value
+    t = Trace(np.empty(N, np.uint64), np.empty(N, np.uint32), np.empty(N, np.uint32), np.empty(N, np.uint32),
+              np.zeros(N, np.uint32))
+    rc = lib.gnoc_trace_synthetic(width, height, frequency_ghz, offered_load, packets_per_tile, payload_bytes,
+                                  seed, hotspot_fraction, num_hotspots, t.inject_ps.ctypes.data, t.src.ctypes.data,
+                                  t.dst.ctypes.data, t.bits.ctypes.data, N, ctypes.byref(n))
+    if rc:
+        raise GnocError(rc, "synthetic trace generation failed (invalid LCG schedule for this tile count?)")
+    return t
+
+
+@dataclass
+class Results:
+    final_ps: np.ndarray
+    zero_load_ps: np.ndarray
+    contention_ps: np.ndarray
+    port_sum_delay: np.ndarray
+    port_count: np.ndarray
+    port_mg1: np.ndarray
+    summary: dict = field(default_factory=dict)
+
+
+class Engine:
+    """One engine handle per GPU (gnoc_create)."""
+
+    def __init__(self, cfg: EngineConfig):
+        self.lib = load()
+        self.cfg = cfg
+        self._h = ctypes.c_void_p()
+        c = cfg.to_c()
+        rc = self.lib.gnoc_create(ctypes.byref(c), ctypes.byref(self._h))
+        if rc:
+            raise GnocError(rc, "gnoc_create rejected the configuration")
+        self._n = 0
+        self._keep = None
+
+    def _check(self, rc: int) -> None:
+        if rc:
+            raise GnocError(rc, self.lib.gnoc_last_error(self._h).decode())
+
+    def close(self) -> None:
+        if self._h:
+            self.lib.gnoc_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def submit(self, tr: Trace) -> None:
+        tr = tr.normalized()
+        pk = GnocPackets(tr.inject_ps.ctypes.data, tr.src.ctypes.data, tr.dst.ctypes.data, tr.bits.ctypes.data,
+                         tr.flags.ctypes.data)
+        self._check(self.lib.gnoc_submit(self._h, ctypes.byref(pk), len(tr)))
+        self._n = len(tr)
+
+    def submit_device(self, inject_ps: int, src: int, dst: int, bits: int, flags: int, n: int, keep=None) -> None:
+        """Arrays already resident in HBM (device pointers, e.g. torch tensor data_ptr())."""
+        pk = GnocPackets(inject_ps, src, dst, bits, flags)
+        self._check(self.lib.gnoc_submit_device(self._h, ctypes.byref(pk), n))
+        self._n = n
+        self._keep = keep
+
+    def run(self) -> None:
+        self._check(self.lib.gnoc_run(self._h))
+
+    def summary(self) -> dict:
+        s = GnocSummary()
+        self._check(self.lib.gnoc_get_summary(self._h, ctypes.byref(s)))
+        return {f[0]: getattr(s, f[0]) for f in GnocSummary._fields_ if f[0] != "reserved"}
+
+    def results(self) -> Results:
+        n = self._n
+        fin, zl, ct = (np.empty(n, np.uint64) for _ in range(3))
+        self._check(self.lib.gnoc_get_packet_results(self._h, fin.ctypes.data, zl.ctypes.data, ct.ctypes.data, n))
+        npt = self.cfg.width * self.cfg.height * PORTS_PER_TILE
+        ps, pc, pm = (np.empty(npt, np.uint64) for _ in range(3))
+        self._check(self.lib.gnoc_get_port_stats(self._h, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data, npt))
+        return Results(fin, zl, ct, ps, pc, pm, self.summary())
+
+    def device_final_ps(self) -> int:
+        p = ctypes.c_void_p()
+        self._check(self.lib.gnoc_device_final_ps(self._h, ctypes.byref(p)))
+        return int(p.value)

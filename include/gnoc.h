@@ -1,0 +1,181 @@
+/*
+ * gnoc.h -- C ABI of the MI355X emesh_hop_by_hop timing engine (libgnoc.so).
+ *
+ * Drop-in boundary for Graphite's on-chip network timing path.  In Graphite a
+ * packet walks
+ *   Network::forwardPacket            common/network/network.cc:215-262
+ *   NetworkModel::__routePacket       common/network/network_model.cc:87-116
+ *   NetworkModelEMeshHopByHop::routePacket
+ *                                     common/network/models/network_model_emesh_hop_by_hop.cc:146-264
+ *   RouterModel::processPacket        common/network/components/router/router_model.cc:70-108
+ *   QueueModelHistoryTree::computeQueueDelay
+ *                                     common/shared_models/queue_models/queue_model_history_tree.cc:43-126
+ *   NetworkModel::processReceivedPacket
+ *                                     common/network/network_model.cc:142-150
+ * once per hop, one packet at a time.  This library replaces that whole walk
+ * for a batch of packets: the caller submits a (inject_ps, packet_id)-ordered
+ * trace, calls gnoc_run, and reads back per-packet final time / zero-load /
+ * contention (the three NetPacket fields the reference updates,
+ * network.h:27-55) and per-output-port contention counters
+ * (RouterModel::_total_contention_delay / _total_packets, router_model.h:84-85,
+ * QueueModelHistoryTree::_total_requests_using_analytical_model,
+ * queue_model_history_tree.h:38).
+ *
+ * Plain C types only; no HIP/torch types cross this boundary.  All functions
+ * return 0 on success or a negative GNOC_E* code, and never abort (the
+ * reference aborts through LOG_PRINT_ERROR, common/misc/log.cc:360-362).
+ * Calls on one engine are not thread-safe; distinct engines are independent.
+ * The caller owns every array it passes; nothing is retained after a call.
+ */
+#ifndef GNOC_H
+#define GNOC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNOC_ABI_VERSION 1
+
+/* error codes */
+#define GNOC_OK             0
+#define GNOC_EINVAL        -1   /* bad argument / configuration                    */
+#define GNOC_ETRACE        -2   /* trace violates the submit contract              */
+#define GNOC_EHIP          -3   /* HIP runtime error (message in gnoc_last_error)  */
+#define GNOC_ESTATE        -4   /* call out of order (e.g. run before submit)      */
+#define GNOC_EUNSUPPORTED  -5   /* valid for the reference, not implemented here   */
+#define GNOC_ENOMEM        -6
+
+/* queue model types, QueueModel::create (common/shared_models/queue_model.cc:18-38) */
+#define GNOC_QUEUE_HISTORY_TREE 0
+
+/* per-packet flags */
+#define GNOC_PKT_UNMODELED  0x1u   /* NetworkModel::isModelEnabled() == false
+                                      (network_model.cc:171-183): zero delay, no queue update */
+
+/* output ports per tile: mesh router ports SELF,LEFT,RIGHT,DOWN,UP
+ * (network_model_emesh_hop_by_hop.h:43-50) then the injection router's port */
+#define GNOC_PORT_SELF   0
+#define GNOC_PORT_LEFT   1
+#define GNOC_PORT_RIGHT  2
+#define GNOC_PORT_DOWN   3
+#define GNOC_PORT_UP     4
+#define GNOC_PORT_INJ    5
+#define GNOC_PORTS_PER_TILE 6
+
+/* Configuration: exactly the carbon_sim.cfg keys the path reads. */
+typedef struct gnoc_config
+{
+   int32_t  mesh_width;            /* floor(sqrt(N)), emesh_hop_by_hop.cc:54 (0 = derive from num_tiles) */
+   int32_t  mesh_height;           /* ceil(N / width), emesh_hop_by_hop.cc:55                            */
+   int32_t  num_tiles;             /* general/total_cores (application tiles)                            */
+   int32_t  flit_width;            /* network/emesh_hop_by_hop/flit_width (bits)                        */
+   uint64_t router_delay;          /* network/emesh_hop_by_hop/router/delay (cycles)                    */
+   uint64_t link_delay;            /* network/emesh_hop_by_hop/link/delay (cycles); must equal
+                                      ceil(f * 0.01 * tile_width), emesh_hop_by_hop.cc:126              */
+   double   frequency_ghz;         /* network DVFS-domain frequency (dvfs/domains), default 1.0        */
+   double   tile_width_mm;         /* general/tile_width                                                */
+   int32_t  contention_enabled;    /* network/emesh_hop_by_hop/queue_model/enabled                      */
+   int32_t  queue_type;            /* network/emesh_hop_by_hop/queue_model/type (GNOC_QUEUE_*)          */
+   int32_t  analytical_enabled;    /* queue_model/history_tree/analytical_model_enabled                 */
+   int32_t  max_list_size;         /* queue_model/history_tree/max_list_size (>= 2)                     */
+   int32_t  broadcast_tree_enabled;/* network/emesh_hop_by_hop/broadcast_tree_enabled (parsed only)     */
+   int32_t  device;                /* HIP device ordinal                                                */
+} gnoc_config;
+
+/* Fill with carbon_sim.cfg defaults for an N-tile mesh (carbon_sim.cfg:300-313, 388-392). */
+void gnoc_config_default(gnoc_config *cfg, int32_t num_tiles);
+
+/* Packet trace, struct-of-arrays.  Packet id = array index.  The trace must
+ * be ordered by (inject_ps, id), i.e. inject_ps non-decreasing. */
+typedef struct gnoc_packets
+{
+   const uint64_t *inject_ps;   /* NetPacket::time at Network::netSend                 */
+   const uint32_t *src;         /* TILE_ID(pkt.sender)                                  */
+   const uint32_t *dst;         /* TILE_ID(pkt.receiver) (BROADCAST not supported yet)  */
+   const uint32_t *bits;        /* NetworkModel::getModeledLength(pkt), bits            */
+   const uint32_t *flags;       /* GNOC_PKT_* (may be NULL = all zero)                  */
+} gnoc_packets;
+
+typedef struct gnoc_engine gnoc_engine;
+
+typedef struct gnoc_summary
+{
+   uint64_t packets;            /* packets submitted                                    */
+   uint64_t routed_packets;     /* packets that entered the mesh (not self/unmodeled)   */
+   uint64_t mesh_hops;          /* mesh-router traversals = sum over routed of (H+1);
+                                   the reference's "Switch Allocator Requests"         */
+   uint64_t records;            /* hop records materialised (injection + mesh)          */
+   uint64_t mg1_uses;           /* requests served by the M/G/1 fallback                */
+   uint32_t levels;             /* dependency levels executed                           */
+   uint32_t reserved;
+   double   last_run_ms;        /* device time of the last gnoc_run (HIP events)        */
+} gnoc_summary;
+
+/* Replaces NetworkModel::createModel(..., NETWORK_EMESH_HOP_BY_HOP)
+ * (network_model.cc:50-71) + the RouterModel/QueueModel::create calls of
+ * NetworkModelEMeshHopByHop::createRouterAndLinkModels (emesh_hop_by_hop.cc:73-128).
+ * Validates what the reference asserts: N == W*H (:56-58, :309-320), the link
+ * delay identity (:126), queue type (queue_model.cc:33-36). */
+int gnoc_create(const gnoc_config *cfg, gnoc_engine **out);
+
+/* Replaces the stream of Network::netSend/forwardPacket calls
+ * (network.cc:174-262): hands the engine one batch.  Host pointers; copied. */
+int gnoc_submit(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
+
+/* Same, but the arrays already live in device memory (HBM) on cfg->device;
+ * they must stay valid until gnoc_run returns. */
+int gnoc_submit_device(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
+
+/* Runs the whole batch (all hops of all packets) on the GPU.  Blocking. */
+int gnoc_run(gnoc_engine *eng);
+
+/* Per-packet results (each pointer may be NULL).  NetPacket::time after
+ * NetworkModel::processReceivedPacket, and NetPacket::zero_load_delay /
+ * contention_delay, all in picoseconds. */
+int gnoc_get_packet_results(gnoc_engine *eng, uint64_t *final_ps, uint64_t *zero_load_ps,
+                            uint64_t *contention_ps, size_t n);
+
+/* Per-output-port counters, arrays of num_tiles*6, index tile*6 + GNOC_PORT_*.
+ * sum_delay/count = RouterModel::_total_contention_delay/_total_packets
+ * (router_model.cc:136-144; injection router for GNOC_PORT_INJ); mg1_uses =
+ * QueueModelHistoryTree::getTotalRequestsUsingAnalyticalModel. */
+int gnoc_get_port_stats(gnoc_engine *eng, uint64_t *sum_delay, uint64_t *count,
+                        uint64_t *mg1_uses, size_t nports);
+
+int gnoc_get_summary(gnoc_engine *eng, gnoc_summary *out);
+
+/* Device pointer to the final_ps array (uint64_t[n]) of the last run, for
+ * callers that keep results in HBM (e.g. multi-GPU gathers). */
+int gnoc_device_final_ps(gnoc_engine *eng, void **dptr);
+
+const char *gnoc_last_error(const gnoc_engine *eng);
+void gnoc_destroy(gnoc_engine *eng);
+
+/* ---- trace helpers (not on the timed path) ---------------------------- */
+
+/* Synthetic traffic of tests/benchmarks/synthetic_network/synthetic_network.cc:
+ * per tile, per cycle, Bernoulli(offered_load) with drand48_r seeded
+ * (seed + tile) (the reference seeds with time(NULL), common/misc/random.h:15-18);
+ * destinations from the reference's uniform_random LCG schedule (:247-301).
+ * hotspot_fraction > 0 redirects that fraction of packets (own drand48 stream,
+ * seed + 0x5bd1e995 + tile) uniformly to the memory-controller tiles of
+ * computeMemoryControllerPositions(num_hotspots, N) (emesh_hop_by_hop.cc:323-364).
+ * Packets are 8-byte USER messages -> (sizeof(NetPacket)=64 + payload)*8 bits
+ * (network.cc:705-708).  Output is (inject_ps, src)-ordered; ids are ranks.
+ * Call with NULL arrays to get the count in *n_out. */
+int gnoc_trace_synthetic(int32_t mesh_width, int32_t mesh_height, double frequency_ghz,
+                         double offered_load, uint64_t packets_per_tile, uint32_t payload_bytes,
+                         uint64_t seed, double hotspot_fraction, int32_t num_hotspots,
+                         uint64_t *inject_ps, uint32_t *src, uint32_t *dst, uint32_t *bits,
+                         size_t capacity, size_t *n_out);
+
+int gnoc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GNOC_H */

@@ -1,0 +1,428 @@
+/*
+ * gnoc_oracle.c -- CPU ORACLE for the emesh_hop_by_hop timing path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the checker the HIP engine is
+ * compared against; it is never linked into, loaded by, or called from the
+ * product library (graphite_amd/_build/libgnoc.so).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may use it.
+ *
+ * It is a plain-C restatement of the reference algorithm, function by
+ * function, with file:line citations into /root/reference (Graphite):
+ *
+ *   - QueueModelHistoryTree::computeQueueDelay
+ *       common/shared_models/queue_models/queue_model_history_tree.cc:43-126
+ *     The AVL interval tree (common/misc/interval_tree.cc:265-394) is
+ *     restated as a sorted array of disjoint free intervals with first-fit
+ *     search; DESIGN.md and tests/test_oracle.py pin this equivalence
+ *     against the real IntervalTree compiled from the reference
+ *     (oracle/_ref, see oracle/Makefile).
+ *   - QueueModelMG1::computeQueueDelay / updateQueue
+ *       common/shared_models/queue_models/queue_model_m_g_1.cc:17-56
+ *   - Latency::toPicosec / Time::toCycles   common/misc/time_types.h:81-109
+ *   - RouterModel::processPacket            common/network/components/router/router_model.cc:70-108
+ *   - ElectricalLinkModel                   common/network/components/link/electrical_link_model.cc:13-45
+ *   - NetworkModelEMeshHopByHop::routePacket
+ *       common/network/models/network_model_emesh_hop_by_hop.cc:146-264
+ *   - NetworkModel::__routePacket / processCornerCases / __processReceivedPacket /
+ *     processReceivedPacket / Hop::Hop      common/network/network_model.cc:87-150, 413-468, 556-563
+ *   - Network::forwardPacket hop loop       common/network/network.cc:215-262
+ *
+ * Parity contract: a single-threaded event loop whose
+ * priority queue is keyed (time_ps, packet_id); one event per packet at a
+ * time; the Hop -> packet field copy of network.cc:234-237.
+ *
+ * Pinned by: the reference's own known-answer test
+ * tests/unit/history_tree/history_tree.cc:9-20 (10 packets, incl. out-of-order
+ * arrivals) and by differential tests against oracle/_ref (real
+ * IntervalTree + QueueModelMG1 + time_types.h compiled from the reference).
+ *
+ * Compiled with -ffp-contract=off so the FP64 M/G/1 expression keeps the
+ * reference's operation order (no fused multiply-add).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_EXPORT __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------ */
+/* time_types.h:81-86 and :104-109                                          */
+/* ------------------------------------------------------------------------ */
+static uint64_t lat_to_ps(uint64_t cycles, double f)
+{
+   /* (UInt64) ceil( ((double) 1000*_cycles) / ((double) _frequency) ) */
+   return (uint64_t) ceil(((double) 1000 * (double) cycles) / ((double) f));
+}
+
+static uint64_t time_to_cycles(uint64_t ps, double f)
+{
+   /* (UInt64) ceil(((double) (_picosec) * ((double) frequency)) / double(1.0e3)) */
+   return (uint64_t) ceil(((double) ps * (double) f) / (double) 1.0e3);
+}
+
+ORC_EXPORT uint64_t orc_lat_to_ps(uint64_t c, double f) { return lat_to_ps(c, f); }
+ORC_EXPORT uint64_t orc_time_to_cycles(uint64_t p, double f) { return time_to_cycles(p, f); }
+
+/* ------------------------------------------------------------------------ */
+/* QueueModelHistoryTree (+ QueueModelMG1)                                  */
+/* ------------------------------------------------------------------------ */
+typedef struct { uint64_t first, second; } orc_interval;
+
+typedef struct
+{
+   orc_interval *iv;      /* free intervals, sorted by .first, disjoint    */
+   int n;                 /* IntervalTree::_size                           */
+   int max_list_size;     /* queue_model/history_tree/max_list_size        */
+   int analytical;        /* queue_model/history_tree/analytical_model_enabled */
+   uint64_t min_proc;     /* _min_processing_time (RouterModel passes 1)   */
+   /* QueueModelMG1 state, queue_model_m_g_1.cc:8-12 */
+   double s2, s1;
+   uint64_t narr, newest;
+   /* counters */
+   uint64_t mg1_uses;     /* _total_requests_using_analytical_model        */
+   uint64_t total_requests, util_cycles, last_request_time; /* queue_model.cc:40-53 */
+} orc_queue;
+
+ORC_EXPORT orc_queue *orc_queue_create(int max_list_size, int analytical, uint64_t min_proc)
+{
+   if (max_list_size < 2 || min_proc < 1)
+      return NULL; /* reference aborts / corrupts its tree for these */
+   orc_queue *q = (orc_queue *) calloc(1, sizeof(orc_queue));
+   q->iv = (orc_interval *) calloc((size_t) max_list_size + 1, sizeof(orc_interval));
+   q->max_list_size = max_list_size;
+   q->analytical = analytical;
+   q->min_proc = min_proc;
+   /* queue_model_history_tree.cc:29-30: start node [0, UINT64_MAX) */
+   q->iv[0].first = 0;
+   q->iv[0].second = UINT64_MAX;
+   q->n = 1;
+   return q;
+}
+
+ORC_EXPORT void orc_queue_destroy(orc_queue *q)
+{
+   if (!q) return;
+   free(q->iv);
+   free(q);
+}
+
+ORC_EXPORT uint64_t orc_queue_mg1_uses(const orc_queue *q) { return q->mg1_uses; }
+ORC_EXPORT int orc_queue_size(const orc_queue *q) { return q->n; }
+
+static void iv_remove(orc_queue *q, int i)
+{
+   memmove(&q->iv[i], &q->iv[i + 1], (size_t) (q->n - i - 1) * sizeof(orc_interval));
+   q->n--;
+}
+
+static void iv_insert(orc_queue *q, orc_interval v)
+{
+   int i = q->n;
+   while (i > 0 && q->iv[i - 1].first > v.first) { q->iv[i] = q->iv[i - 1]; i--; }
+   q->iv[i] = v;
+   q->n++;
+}
+
+/* IntervalTree::searchTree (interval_tree.cc:365-394) restated.  For the
+ * disjoint, non-adjacent, non-empty intervals the history tree maintains, the
+ * BST descent returns the FIRST interval in key order that either contains
+ * [a, b) or starts after a and is at least (b - a) long. */
+static int iv_search(const orc_queue *q, uint64_t a, uint64_t b)
+{
+   for (int i = 0; i < q->n; i++)
+   {
+      const orc_interval *v = &q->iv[i];
+      if (a >= v->first && b <= v->second) return i;
+      if (a < v->first && (v->second - v->first) >= (b - a)) return i;
+   }
+   return -1;
+}
+
+/* QueueModelMG1::computeQueueDelay, queue_model_m_g_1.cc:17-46 */
+static uint64_t mg1_delay(const orc_queue *q)
+{
+   if (q->narr == 0) return 0;
+   double variance = ((q->s2 / (double) q->narr) -
+                      ((q->s1 / (double) q->narr) * (q->s1 / (double) q->narr)));
+   double service_rate = 1.0 / (q->s1 / (double) q->narr);
+   double arrival_rate = ((double) q->narr) / (double) q->newest;
+   if (arrival_rate >= service_rate)
+      arrival_rate = 0.999 * service_rate;
+   return (uint64_t) ceil(0.5 * service_rate * arrival_rate *
+                          ((1 / (service_rate * service_rate)) + variance) /
+                          (service_rate - arrival_rate));
+}
+
+/* QueueModelMG1::updateQueue, queue_model_m_g_1.cc:48-56 */
+static void mg1_update(orc_queue *q, uint64_t t, uint64_t p, uint64_t d)
+{
+   q->s2 += ((double) p * (double) p);
+   q->s1 += (double) p;
+   q->narr++;
+   uint64_t nw = t + d + p;
+   q->newest = (q->newest > nw) ? q->newest : nw;
+}
+
+/* QueueModelHistoryTree::computeQueueDelay, queue_model_history_tree.cc:43-126 */
+ORC_EXPORT uint64_t orc_queue_compute(orc_queue *q, uint64_t t, uint64_t p)
+{
+   uint64_t d = UINT64_MAX;
+   const uint64_t m = q->min_proc;
+
+   /* :49-56  prune the minimum node when the tree is full */
+   if (q->n >= q->max_list_size)
+      iv_remove(q, 0);
+
+   /* :58-64  analytical fallback when the earliest free interval starts after the packet */
+   if (q->analytical && q->iv[0].first > (t + p))
+   {
+      q->mg1_uses++;
+      d = mg1_delay(q);
+   }
+   else
+   {
+      int i = iv_search(q, t, t + p);
+      if (i < 0) abort(); /* :69-73 LOG_PRINT_ERROR("node = (NULL)") */
+      orc_interval *nd = &q->iv[i];
+      if (t >= nd->first)
+      {
+         d = 0;
+         if ((t - nd->first) >= m)
+         {
+            uint64_t second = nd->second;
+            nd->second = t;
+            if ((second - (t + p)) >= m)
+            {
+               orc_interval nx = { t + p, second };
+               iv_insert(q, nx);
+            }
+         }
+         else
+         {
+            if ((nd->second - (t + p)) >= m)
+               nd->first = t + p;
+            else
+               iv_remove(q, i);
+         }
+      }
+      else
+      {
+         d = nd->first - t;
+         if ((nd->second - (nd->first + p)) >= m)
+            nd->first = nd->first + p;
+         else
+            iv_remove(q, i);
+      }
+   }
+
+   /* :118  M/G/1 statistics are updated on every request */
+   mg1_update(q, t, p, d);
+
+   /* queue_model.cc:48-53 updateQueueUtilizationCounters */
+   q->util_cycles += p;
+   uint64_t lr = t + d + p;
+   q->last_request_time = (q->last_request_time > lr) ? q->last_request_time : lr;
+   q->total_requests++;
+   return d;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Event-driven network harness                                            */
+/* ------------------------------------------------------------------------ */
+enum { NODE_SEND = 0, NODE_RECEIVE = 1, NODE_EMESH = 2 };   /* network_model.h:116-117, emesh .h:38-41 */
+enum { PORT_SELF = 0, PORT_LEFT, PORT_RIGHT, PORT_DOWN, PORT_UP, PORT_INJ };  /* emesh .h:43-50 + injection */
+#define PORTS_PER_TILE 6
+#define ORC_FLAG_UNMODELED 1u
+
+typedef struct { uint64_t t; uint32_t id; } heap_ent;
+
+typedef struct { heap_ent *a; size_t n, cap; } heap_t;
+
+static int he_less(heap_ent x, heap_ent y) { return x.t < y.t || (x.t == y.t && x.id < y.id); }
+
+static void heap_push(heap_t *h, heap_ent e)
+{
+   if (h->n == h->cap)
+   {
+      h->cap = h->cap ? h->cap * 2 : 1024;
+      h->a = (heap_ent *) realloc(h->a, h->cap * sizeof(heap_ent));
+   }
+   size_t i = h->n++;
+   while (i > 0)
+   {
+      size_t p = (i - 1) / 2;
+      if (!he_less(e, h->a[p])) break;
+      h->a[i] = h->a[p];
+      i = p;
+   }
+   h->a[i] = e;
+}
+
+static heap_ent heap_pop(heap_t *h)
+{
+   heap_ent top = h->a[0];
+   heap_ent last = h->a[--h->n];
+   size_t i = 0;
+   for (;;)
+   {
+      size_t l = 2 * i + 1, r = l + 1, s = i;
+      heap_ent best = last;
+      if (l < h->n && he_less(h->a[l], best)) { s = l; best = h->a[l]; }
+      if (r < h->n && he_less(h->a[r], best)) { s = r; }
+      if (s == i) break;
+      h->a[i] = h->a[s];
+      i = s;
+   }
+   if (h->n) h->a[i] = last;
+   return top;
+}
+
+/* Returns 0 on success, <0 on invalid configuration / trace.
+ * Outputs are arrays of n (per packet) or 6*W*H (per port, index tile*6+port,
+ * port 0..4 = SELF,LEFT,RIGHT,DOWN,UP of the mesh router, 5 = injection router). */
+ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
+                       uint64_t router_delay, uint64_t link_delay, double frequency,
+                       int contention_enabled, int analytical_enabled, int max_list_size,
+                       size_t n, const uint64_t *inject_ps, const uint32_t *src,
+                       const uint32_t *dst, const uint32_t *bits, const uint32_t *flags,
+                       uint64_t *final_ps, uint64_t *zero_load_ps, uint64_t *contention_ps,
+                       uint64_t *port_sum_delay, uint64_t *port_count, uint64_t *port_mg1)
+{
+   const int W = mesh_width, H = mesh_height;
+   if (W <= 0 || H <= 0 || flit_width <= 0 || frequency <= 0.0) return -1;
+   if (contention_enabled && max_list_size < 2) return -1;
+   const uint32_t N = (uint32_t) (W * H);
+   const size_t nports = (size_t) N * PORTS_PER_TILE;
+
+   for (size_t i = 0; i < n; i++)
+   {
+      if (src[i] >= N || dst[i] >= N) return -2;
+      if (i > 0 && inject_ps[i] < inject_ps[i - 1]) return -3; /* must be time ordered */
+   }
+
+   orc_queue **q = NULL;
+   if (contention_enabled)
+   {
+      q = (orc_queue **) calloc(nports, sizeof(orc_queue *));
+      for (size_t p = 0; p < nports; p++)
+         q[p] = orc_queue_create(max_list_size, analytical_enabled, 1);
+   }
+   memset(port_sum_delay, 0, nports * sizeof(uint64_t));
+   memset(port_count, 0, nports * sizeof(uint64_t));
+   memset(port_mg1, 0, nports * sizeof(uint64_t));
+
+   /* per-packet running state (NetPacket fields, network.h:27-55) */
+   uint64_t *ptime = (uint64_t *) malloc(n * sizeof(uint64_t));
+   uint32_t *ptile = (uint32_t *) malloc(n * sizeof(uint32_t));
+   uint8_t *pnode = (uint8_t *) malloc(n ? n : 1);
+   heap_t h = { 0, 0, 0 };
+
+   for (size_t i = 0; i < n; i++)
+   {
+      ptime[i] = inject_ps[i];
+      ptile[i] = src[i];
+      pnode[i] = NODE_SEND;
+      zero_load_ps[i] = 0;
+      contention_ps[i] = 0;
+      heap_ent e = { inject_ps[i], (uint32_t) i };
+      heap_push(&h, e);
+   }
+
+   const uint64_t rl_ps = lat_to_ps(router_delay + link_delay, frequency);
+
+   while (h.n)
+   {
+      heap_ent e = heap_pop(&h);
+      const uint32_t id = e.id;
+      const uint64_t t = ptime[id];
+      const uint32_t F = (bits[id] % (uint32_t) flit_width) ? bits[id] / (uint32_t) flit_width + 1
+                                                           : bits[id] / (uint32_t) flit_width; /* network_model.cc:202-212 */
+      const int modeled = !(flags[id] & ORC_FLAG_UNMODELED); /* network_model.cc:171-183 */
+
+      if (pnode[id] == NODE_SEND)
+      {
+         /* network_model.cc:413-468 processCornerCases: self-send -> RECEIVE, no delay;
+          * network_model.cc:129-133 __processReceivedPacket returns early for it. */
+         if (src[id] == dst[id] || !modeled)
+         {
+            /* unmodeled packets traverse with zero router/link delay and no
+             * queue interaction (router_model.cc:74-75, electrical_link_model.cc:32-33),
+             * and __processReceivedPacket skips serialization. */
+            final_ps[id] = t;
+            continue;
+         }
+         /* emesh routePacket SEND_TILE branch, :151-159: injection router (delay 0) */
+         uint64_t c0 = 0;
+         if (contention_enabled)
+         {
+            const size_t port = (size_t) src[id] * PORTS_PER_TILE + PORT_INJ;
+            c0 = orc_queue_compute(q[port], time_to_cycles(t, frequency), F);
+            port_sum_delay[port] += c0;
+            port_count[port]++;
+         }
+         /* Hop(pkt, tile, EMESH, Latency(0,f), Latency(c0,f)); network_model.cc:556-563 */
+         const uint64_t c0ps = lat_to_ps(c0, frequency), zl = lat_to_ps(0, frequency);
+         ptime[id] = t + c0ps + zl;
+         zero_load_ps[id] += zl;
+         contention_ps[id] += c0ps;
+         pnode[id] = NODE_EMESH;
+         heap_ent ne = { ptime[id], id };
+         heap_push(&h, ne);
+         continue;
+      }
+
+      /* EMESH unicast branch, :223-256 */
+      const int cur = (int) ptile[id];
+      const int cx = cur % W, cy = cur / W;
+      const int dx = (int) (dst[id] % (uint32_t) W), dy = (int) (dst[id] / (uint32_t) W);
+      int port, next;
+      if (cx > dx)      { port = PORT_LEFT;  next = cur - 1; }
+      else if (cx < dx) { port = PORT_RIGHT; next = cur + 1; }
+      else if (cy > dy) { port = PORT_DOWN;  next = cur - W; }
+      else if (cy < dy) { port = PORT_UP;    next = cur + W; }
+      else              { port = PORT_SELF;  next = cur;     }
+
+      /* RouterModel::processPacket (router_model.cc:70-108) + link (electrical_link_model.cc:29-45) */
+      uint64_t c = 0;
+      if (contention_enabled)
+      {
+         const size_t qp = (size_t) cur * PORTS_PER_TILE + (size_t) port;
+         c = orc_queue_compute(q[qp], time_to_cycles(t, frequency), F);
+         port_sum_delay[qp] += c;
+         port_count[qp]++;
+      }
+      const uint64_t cps = lat_to_ps(c, frequency);
+      ptime[id] = t + cps + rl_ps;
+      zero_load_ps[id] += rl_ps;
+      contention_ps[id] += cps;
+
+      if (port == PORT_SELF)
+      {
+         /* RECEIVE_TILE: network_model.cc:142-150 serialization, once */
+         const uint64_t fps = lat_to_ps(F, frequency);
+         ptime[id] += fps;
+         zero_load_ps[id] += fps;
+         final_ps[id] = ptime[id];
+         continue;
+      }
+      ptile[id] = (uint32_t) next;
+      heap_ent ne = { ptime[id], id };
+      heap_push(&h, ne);
+   }
+
+   if (contention_enabled)
+   {
+      for (size_t p = 0; p < nports; p++)
+      {
+         port_mg1[p] = q[p]->mg1_uses;
+         orc_queue_destroy(q[p]);
+      }
+      free(q);
+   }
+   free(h.a);
+   free(ptime);
+   free(ptile);
+   free(pnode);
+   return 0;
+}

@@ -1,0 +1,140 @@
+"""ctypes front-end of the CPU oracle (oracle/gnoc_oracle.c) and of the optional
+reference build (oracle/_ref/libgnoc_ref.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker.  The product (graphite_amd) never
+imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "_build", "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libgnoc_ref.so")
+REF_DIR = os.environ.get("GNOC_REF_DIR", "/root/reference")
+
+_orc = None
+_ref = None
+
+
+def build(ref: bool | None = None) -> None:
+    """make the oracle (and, when the reference tree exists here, oracle/_ref)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    if ref is None:
+        ref = os.path.isdir(REF_DIR)
+    if ref:
+        subprocess.run(["make", "-s", "-C", HERE, "ref", f"REF_DIR={REF_DIR}"], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _orc
+    if _orc is None:
+        if not os.path.exists(ORACLE_SO):
+            build(ref=False)
+        L = ctypes.CDLL(ORACLE_SO)
+        u64, vp = ctypes.c_uint64, ctypes.c_void_p
+        L.orc_queue_create.restype = vp
+        L.orc_queue_create.argtypes = [ctypes.c_int, ctypes.c_int, u64]
+        L.orc_queue_compute.restype = u64
+        L.orc_queue_compute.argtypes = [vp, u64, u64]
+        L.orc_queue_mg1_uses.restype = u64
+        L.orc_queue_mg1_uses.argtypes = [vp]
+        L.orc_queue_size.argtypes = [vp]
+        L.orc_queue_destroy.argtypes = [vp]
+        L.orc_queue_destroy.restype = None
+        L.orc_lat_to_ps.restype = u64
+        L.orc_lat_to_ps.argtypes = [u64, ctypes.c_double]
+        L.orc_time_to_cycles.restype = u64
+        L.orc_time_to_cycles.argtypes = [u64, ctypes.c_double]
+        L.orc_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u64, u64, ctypes.c_double, ctypes.c_int,
+                              ctypes.c_int, ctypes.c_int, ctypes.c_size_t] + [vp] * 11
+        _orc = L
+    return _orc
+
+
+def ref_lib() -> ctypes.CDLL | None:
+    """The reference-compiled components, or None when not built (e.g. on the GPU box)."""
+    global _ref
+    if _ref is None:
+        if not os.path.exists(REF_SO):
+            return None
+        L = ctypes.CDLL(REF_SO)
+        u64, vp = ctypes.c_uint64, ctypes.c_void_p
+        L.ref_queue_create.restype = vp
+        L.ref_queue_create.argtypes = [ctypes.c_int, ctypes.c_int, u64]
+        L.ref_queue_compute.restype = u64
+        L.ref_queue_compute.argtypes = [vp, u64, u64]
+        L.ref_queue_mg1_uses.restype = u64
+        L.ref_queue_mg1_uses.argtypes = [vp]
+        L.ref_queue_size.restype = ctypes.c_uint32
+        L.ref_queue_size.argtypes = [vp]
+        L.ref_queue_destroy.argtypes = [vp]
+        L.ref_queue_destroy.restype = None
+        L.ref_lat_to_ps.restype = u64
+        L.ref_lat_to_ps.argtypes = [u64, ctypes.c_double]
+        L.ref_time_to_cycles.restype = u64
+        L.ref_time_to_cycles.argtypes = [u64, ctypes.c_double]
+        _ref = L
+    return _ref
+
+
+class Queue:
+    """QueueModelHistoryTree(min_processing_time=1) restated (oracle)."""
+
+    def __init__(self, max_list_size: int = 100, analytical: bool = True, min_proc: int = 1):
+        self.L = lib()
+        self.h = self.L.orc_queue_create(max_list_size, int(analytical), min_proc)
+        if not self.h:
+            raise ValueError("invalid history_tree parameters")
+
+    def compute(self, t: int, p: int) -> int:
+        return int(self.L.orc_queue_compute(self.h, t, p))
+
+    @property
+    def mg1_uses(self) -> int:
+        return int(self.L.orc_queue_mg1_uses(self.h))
+
+    def __del__(self):
+        try:
+            self.L.orc_queue_destroy(self.h)
+        except Exception:
+            pass
+
+
+@dataclass
+class OracleResult:
+    final_ps: np.ndarray
+    zero_load_ps: np.ndarray
+    contention_ps: np.ndarray
+    port_sum_delay: np.ndarray
+    port_count: np.ndarray
+    port_mg1: np.ndarray
+
+
+def run(cfg, tr) -> OracleResult:
+    """Event-driven reference walk of every packet (see gnoc_oracle.c).  cfg is a
+    graphite_amd.gnoc.EngineConfig-like object, tr a Trace-like object."""
+    L = lib()
+    n = int(tr.inject_ps.shape[0])
+    W, H = cfg.width, cfg.height
+    inj = np.ascontiguousarray(tr.inject_ps, np.uint64)
+    src = np.ascontiguousarray(tr.src, np.uint32)
+    dst = np.ascontiguousarray(tr.dst, np.uint32)
+    bits = np.ascontiguousarray(tr.bits, np.uint32)
+    flags = np.ascontiguousarray(tr.flags if tr.flags is not None else np.zeros(n, np.uint32), np.uint32)
+    fin, zl, ct = (np.zeros(n, np.uint64) for _ in range(3))
+    npt = W * H * 6
+    ps, pc, pm = (np.zeros(npt, np.uint64) for _ in range(3))
+    rc = L.orc_run(W, H, cfg.flit_width, cfg.router_delay, cfg.link_delay, cfg.frequency_ghz,
+                   int(cfg.contention_enabled), int(cfg.analytical_enabled), cfg.max_list_size, n,
+                   inj.ctypes.data, src.ctypes.data, dst.ctypes.data, bits.ctypes.data, flags.ctypes.data,
+                   fin.ctypes.data, zl.ctypes.data, ct.ctypes.data, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data)
+    if rc:
+        raise ValueError(f"oracle rejected input (rc={rc})")
+    return OracleResult(fin, zl, ct, ps, pc, pm)

@@ -1,0 +1,58 @@
+"""Regenerate the network-level golden vectors in tests/golden/*.npz.
+
+Inputs: small seeded traces (tests/traces.py, and the synthetic_network
+restatement in libgnoc).  Expected outputs: the CPU oracle (oracle/gnoc_oracle.c),
+which is itself pinned by the reference's history_tree KAT and by differential
+tests against the reference's compiled IntervalTree / QueueModelMG1 / time_types.h
+(tests/test_oracle.py).  Run from the repo root:  python tests/golden/make_golden.py
+"""
+import dataclasses
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+from graphite_amd import gnoc  # noqa: E402
+from oracle import oracle  # noqa: E402
+from tests.traces import random_trace  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def case(name, cfg, tr):
+    r = oracle.run(cfg, tr)
+    d = {k: v for k, v in dataclasses.asdict(cfg).items()}
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), cfg=json.dumps(d), inject_ps=tr.inject_ps,
+                        src=tr.src, dst=tr.dst, bits=tr.bits,
+                        flags=tr.flags if tr.flags is not None else np.zeros(len(tr), np.uint32),
+                        final_ps=r.final_ps, zero_load_ps=r.zero_load_ps, contention_ps=r.contention_ps,
+                        port_sum_delay=r.port_sum_delay, port_count=r.port_count, port_mg1=r.port_mg1)
+    print(name, len(tr), "mg1", int(r.port_mg1.sum()))
+
+
+def main():
+    E = gnoc.EngineConfig
+    case("g_4x4_burst_mg1", E(num_tiles=16), random_trace(1500, 4, 4, seed=1, max_cycle=200, burst0=60))
+    case("g_8x8_synthetic_0p05", E(num_tiles=64), gnoc.synthetic_trace(8, 8, 0.05, 60, seed=3))
+    case("g_8x8_saturated", E(num_tiles=64), random_trace(4000, 8, 8, seed=2, max_cycle=150, burst0=100))
+    case("g_4x4_self_unmodeled", E(num_tiles=16),
+         random_trace(1500, 4, 4, seed=4, max_cycle=300, self_frac=0.2, unmodeled_frac=0.2))
+    case("g_6x6_flit16_r2", E(num_tiles=36, flit_width=16, router_delay=2),
+         random_trace(1500, 6, 6, seed=5, max_cycle=800, burst0=10, bits_choices=[72, 576, 584]))
+    case("g_6x6_flit128_r0", E(num_tiles=36, flit_width=128, router_delay=0),
+         random_trace(1500, 6, 6, seed=6, max_cycle=400, burst0=10, bits_choices=[72, 576, 1088]))
+    case("g_4x4_link2", E(num_tiles=16, tile_width_mm=150.0, link_delay=2),
+         random_trace(1500, 4, 4, seed=7, max_cycle=400, burst0=10))
+    case("g_4x4_f0p9", E(num_tiles=16, frequency_ghz=0.9),
+         random_trace(1500, 4, 4, seed=8, max_cycle=400, burst0=10, ps_jitter=True, frequency_ghz=0.9))
+    case("g_4x4_list2", E(num_tiles=16, max_list_size=2), random_trace(1500, 4, 4, seed=9, max_cycle=200, burst0=30))
+    case("g_2x4_noanalytical", E(num_tiles=8, analytical_enabled=False),
+         random_trace(1000, 2, 4, seed=10, max_cycle=200, burst0=30))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+"""GPU engine vs CPU oracle: bit-exact per-packet times and per-port counters.
+
+Integer/ps arithmetic, so the bar is exact equality (np.array_equal) on every
+output array.  Runs on the MI355X box through the C ABI (libgnoc.so).
+"""
+import numpy as np
+import pytest
+
+from graphite_amd import gnoc
+from oracle import oracle
+from tests.traces import random_trace
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(cfg, tr):
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    got = eng.results()
+    eng.close()
+    ref = oracle.run(cfg, tr)
+    return got, ref
+
+
+def assert_same(got, ref, tr=None):
+    for name in ("final_ps", "zero_load_ps", "contention_ps"):
+        a, b = getattr(got, name), getattr(ref, name)
+        if not np.array_equal(a, b):
+            bad = np.nonzero(a != b)[0]
+            raise AssertionError(f"{name}: {bad.size} mismatches, first id {bad[0]}: gpu {a[bad[0]]} oracle {b[bad[0]]}")
+    for name in ("port_sum_delay", "port_count", "port_mg1"):
+        a, b = getattr(got, name), getattr(ref, name)
+        if not np.array_equal(a, b):
+            bad = np.nonzero(a != b)[0]
+            raise AssertionError(f"{name}: {bad.size} ports differ, first port {bad[0]}: gpu {a[bad[0]]} oracle {b[bad[0]]}")
+
+
+@pytest.mark.parametrize("load,ppt", [(0.02, 300), (0.05, 300), (0.3, 100)])
+def test_synthetic_8x8(load, ppt):
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = gnoc.synthetic_trace(8, 8, load, ppt, seed=11)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+    assert got.summary["mesh_hops"] == int(ref.port_count.reshape(-1, 6)[:, :5].sum())
+
+
+def test_saturated_mg1_is_exercised():
+    """Saturated 8x8 from t=0: the M/G/1 fallback fires and must match."""
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = random_trace(20000, 8, 8, seed=3, max_cycle=300, burst0=400)
+    got, ref = run_both(cfg, tr)
+    assert ref.port_mg1.sum() > 0
+    assert_same(got, ref)
+
+
+@pytest.mark.parametrize("W,H", [(4, 4), (2, 4), (3, 3), (1, 5), (6, 6)])
+def test_mesh_shapes_and_bursts(W, H):
+    cfg = gnoc.EngineConfig(num_tiles=W * H, mesh_width=W, mesh_height=H)
+    tr = random_trace(3000, W, H, seed=W * 10 + H, max_cycle=400, burst0=50, self_frac=0.05)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+
+
+def test_self_and_unmodeled_bypass():
+    cfg = gnoc.EngineConfig(num_tiles=16)
+    tr = random_trace(4000, 4, 4, seed=5, max_cycle=500, self_frac=0.2, unmodeled_frac=0.2)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+    selfm = tr.src == tr.dst
+    assert np.array_equal(got.final_ps[selfm], tr.inject_ps[selfm])
+
+
+@pytest.mark.parametrize("flit_width", [16, 32, 128])
+@pytest.mark.parametrize("router_delay", [0, 2])
+def test_flit_width_router_delay(flit_width, router_delay):
+    cfg = gnoc.EngineConfig(num_tiles=36, flit_width=flit_width, router_delay=router_delay)
+    tr = random_trace(5000, 6, 6, seed=flit_width + router_delay, max_cycle=2000, burst0=20,
+                      bits_choices=[72, 576, 584, 1088])
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+
+
+def test_link_delay_two():
+    # tile_width 150 mm at 1 GHz -> ceil(1.5) = 2-cycle links (electrical_link_model.cc:13-16)
+    cfg = gnoc.EngineConfig(num_tiles=16, tile_width_mm=150.0, link_delay=2)
+    tr = random_trace(4000, 4, 4, seed=9, max_cycle=600, burst0=10)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+
+
+@pytest.mark.parametrize("freq", [0.9, 1.5, 0.7])
+def test_non_unit_frequency(freq):
+    import math
+    lk = math.ceil(freq * 0.01 * 1.0)
+    cfg = gnoc.EngineConfig(num_tiles=16, frequency_ghz=freq, link_delay=lk)
+    tr = random_trace(3000, 4, 4, seed=int(freq * 10), max_cycle=500, burst0=8, ps_jitter=True,
+                      frequency_ghz=freq)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+
+
+@pytest.mark.parametrize("max_list,analytical", [(2, 1), (3, 1), (100, 0), (5, 1)])
+def test_queue_parameters(max_list, analytical):
+    cfg = gnoc.EngineConfig(num_tiles=16, max_list_size=max_list, analytical_enabled=bool(analytical))
+    tr = random_trace(3000, 4, 4, seed=max_list * 7 + analytical, max_cycle=300, burst0=30)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+
+
+def test_contention_disabled():
+    cfg = gnoc.EngineConfig(num_tiles=64, contention_enabled=False)
+    tr = gnoc.synthetic_trace(8, 8, 0.1, 100, seed=2)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+    assert got.contention_ps.max() == 0
+
+
+def test_empty_and_single():
+    cfg = gnoc.EngineConfig(num_tiles=16)
+    tr = random_trace(0, 4, 4)
+    got, ref = run_both(cfg, tr)
+    assert got.final_ps.size == 0
+    tr = random_trace(1, 4, 4, seed=1)
+    tr.src[:] = 0
+    tr.dst[:] = 15
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+    # zero-load closed form: (H+1)(R+Lk) + F = 7*2 + 9
+    assert int(got.final_ps[0] - tr.inject_ps[0]) == (7 * 2 + 9) * 1000
+
+
+def test_hotspot_32x32():
+    cfg = gnoc.EngineConfig(num_tiles=1024)
+    tr = gnoc.synthetic_trace(32, 32, 0.005, 40, seed=4, hotspot_fraction=0.2, num_hotspots=16)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+
+
+def test_uniform_32x32():
+    cfg = gnoc.EngineConfig(num_tiles=1024)
+    tr = gnoc.synthetic_trace(32, 32, 0.01, 60, seed=5)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+
+
+def test_repeatable_bytes():
+    """Deterministic by construction: the same batch twice gives identical bytes."""
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = gnoc.synthetic_trace(8, 8, 0.08, 200, seed=13)
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    a = eng.results()
+    eng.run()
+    b = eng.results()
+    assert np.array_equal(a.final_ps, b.final_ps) and np.array_equal(a.port_sum_delay, b.port_sum_delay)

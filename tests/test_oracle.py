@@ -1,0 +1,92 @@
+"""The CPU oracle, pinned before it is trusted.
+
+* the reference's own known-answer test, tests/unit/history_tree/history_tree.cc:9-20
+  (committed as tests/golden/history_tree_kat.json);
+* differential checks against oracle/_ref, i.e. the reference's real
+  IntervalTree (interval_tree.cc), QueueModelMG1 (queue_model_m_g_1.cc) and
+  Latency/Time (time_types.h) compiled from /root/reference (skipped where the
+  reference tree is absent, e.g. on the GPU box);
+* committed network-level golden vectors (tests/golden/*.npz, produced by
+  tests/golden/make_golden.py from this oracle once it passed the above).
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_history_tree_kat():
+    kat = json.load(open(os.path.join(GOLD, "history_tree_kat.json")))
+    q = oracle.Queue(100, True, 1)
+    for t, p, expect in kat["packets"]:
+        assert q.compute(t, p) == expect
+
+
+def _ref_or_skip():
+    r = oracle.ref_lib()
+    if r is None:
+        pytest.skip("oracle/_ref not built (reference tree absent)")
+    return r
+
+
+def test_ref_kat():
+    r = _ref_or_skip()
+    kat = json.load(open(os.path.join(GOLD, "history_tree_kat.json")))
+    q = r.ref_queue_create(100, 1, 1)
+    got = [r.ref_queue_compute(q, t, p) for t, p, _ in kat["packets"]]
+    r.ref_queue_destroy(q)
+    assert got == [e for *_, e in kat["packets"]]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_queue_vs_reference_tree(seed):
+    """Sorted-array free list + M/G/1 == real AVL IntervalTree + QueueModelMG1,
+    including out-of-order arrivals, the analytical branch and pruning."""
+    r = _ref_or_skip()
+    L = oracle.lib()
+    rng = random.Random(seed)
+    for _ in range(400):
+        ml = rng.choice([2, 3, 4, 7, 100])
+        an = rng.choice([0, 1])
+        qo = L.orc_queue_create(ml, an, 1)
+        qr = r.ref_queue_create(ml, an, 1)
+        t = 0
+        for _ in range(rng.randint(1, 250)):
+            mode = rng.random()
+            if mode < 0.6:
+                t += rng.choice([0, 0, 1, 2, 3, 9, 40])
+            tt = t if mode < 0.85 else max(0, t - rng.randint(0, 60))
+            p = rng.randint(1, 12)
+            assert L.orc_queue_compute(qo, tt, p) == r.ref_queue_compute(qr, tt, p)
+        assert L.orc_queue_mg1_uses(qo) == r.ref_queue_mg1_uses(qr)
+        L.orc_queue_destroy(qo)
+        r.ref_queue_destroy(qr)
+
+
+def test_time_conversions_vs_reference():
+    r = _ref_or_skip()
+    L = oracle.lib()
+    rng = random.Random(1)
+    for f in (1.0, 0.9, 1.5, 0.7, 2.0, 0.333, 1.1):
+        for _ in range(2000):
+            c = rng.choice([rng.randint(0, 100), rng.randint(0, 10**9), rng.randint(0, 2**40)])
+            assert L.orc_lat_to_ps(c, f) == r.ref_lat_to_ps(c, f)
+            p = rng.choice([rng.randint(0, 10**5), rng.randint(0, 10**12), rng.randint(0, 2**50)])
+            assert L.orc_time_to_cycles(p, f) == r.ref_time_to_cycles(p, f)
+
+
+@pytest.mark.parametrize("name", sorted(f[:-4] for f in os.listdir(GOLD) if f.endswith(".npz")) if os.path.isdir(GOLD) else [])
+def test_network_golden(name):
+    from graphite_amd.gnoc import EngineConfig, Trace
+    z = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+    cfg = EngineConfig(**json.loads(str(z["cfg"])))
+    tr = Trace(z["inject_ps"], z["src"], z["dst"], z["bits"], z["flags"])
+    res = oracle.run(cfg, tr)
+    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1"):
+        assert np.array_equal(getattr(res, k), z[k]), k
