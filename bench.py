@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Benchmark: packet-hops simulated per second for Graphite's emesh_hop_by_hop
+network model on MI355X (BASELINE.json metric), plus HBM-roofline fraction.
+
+One step = one complete gnoc_run over a resident synthetic trace: every hop of
+every packet through the per-port history-tree/M-G-1 queues, bit-exact with the
+reference model (tests/test_gpu_parity.py).  Default workload = BASELINE.json
+configs[1]: 32x32 (1024 tiles), uniform_random traffic, offered load 0.005
+pkt/tile/cycle, 10,000 packets per tile (10.24 M packets, ~229 M mesh hops).
+
+Multi-GPU (torchrun, one rank per GPU): each rank simulates its own independent
+32x32 trace (seed + rank) -- the sweep-style sharding of SURVEY.md 8(e); there is
+no collective on the data path, so scaling is "weak".  Ranks synchronise only
+for the barrier and the max-over-ranks time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# torch first: libgnoc.so then binds to the same HIP runtime (SONAME libamdhip64.so.7)
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+BYTES_PER_HOP = 32.0    # 16-B hop record written once + read once
+BYTES_PER_PKT = 24.0    # trace read + final_ps write
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mesh", type=int, default=32)
+    ap.add_argument("--load", type=float, default=0.005)
+    ap.add_argument("--ppt", type=int, default=10000, help="packets per tile")
+    ap.add_argument("--mix", choices=("uniform", "hotspot"), default="uniform")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-sample-ppt", type=int, default=1000)
+    ap.add_argument("--verify", type=int, default=0, help="also check the GPU result vs the oracle (slow)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    from graphite_amd import gnoc
+
+    W = H = a.mesh
+    hot = 0.2 if a.mix == "hotspot" else 0.0
+    t0 = time.time()
+    tr = gnoc.synthetic_trace(W, H, a.load, a.ppt, seed=a.seed + rank, hotspot_fraction=hot, num_hotspots=16)
+    gen_s = time.time() - t0
+    cfg = gnoc.EngineConfig(num_tiles=W * H, device=local)
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)          # trace now resident in HBM; steps start from there
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        eng.run()
+    summ = eng.summary()
+
+    barrier_sync()
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        eng.run()
+    barrier_sync()
+    elapsed = time.perf_counter() - t_start
+
+    # kernel-level timing on the engine's own stream (HIP events), separate pass
+    eng.set_profiling(True)
+    eng.run()
+    kst = eng.kernel_stats()
+    eng.set_profiling(False)
+
+    hops = int(summ["mesh_hops"])
+    pkts = int(summ["routed_packets"])
+    t = torch.tensor([elapsed, float(hops), float(pkts)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:3], op=dist.ReduceOp.SUM)
+        t[0] = tmax[0]
+    elapsed_max, hops_all, pkts_all = float(t[0]), float(t[1]), float(t[2])
+
+    if a.verify:
+        from oracle import oracle
+        import numpy as np
+        got = eng.results()
+        ref = oracle.run(cfg, tr)
+        assert np.array_equal(got.final_ps, ref.final_ps), "GPU result differs from oracle"
+
+    if rank == 0:
+        value = hops_all * a.steps / elapsed_max
+        ms_step = elapsed_max / a.steps * 1e3
+        port_ms, port_launches = kst.get("k_port_stream", (0.0, 0))
+        # dominant kernel: k_port_stream, the per-port merge/queue/route stream.
+        # Algorithmic bytes over all its launches: 32 B per mesh hop + 24 B per packet.
+        alg_bytes = hops * BYTES_PER_HOP + pkts * BYTES_PER_PKT
+        achieved = alg_bytes / (port_ms * 1e-3) / 1e9 if port_ms > 0 else 0.0
+        whole_job_gbs = value * (BYTES_PER_HOP + BYTES_PER_PKT * pkts / max(hops, 1)) / 1e9
+        line = {
+            "metric": "packet-hops simulated/sec (node) + % HBM roofline, 1024-tile emesh",
+            "value": value,
+            "unit": "packet-hops/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (synthetic_network.cc uniform_random restated, fixed seeds)",
+            "config": {
+                "workload": f"emesh_hop_by_hop {W}x{H} {a.mix} load={a.load} pkts/tile={a.ppt}",
+                "tiles": W * H, "packets_per_rank": len(tr), "mesh_hops_per_rank": hops,
+                "flit_width": 64, "router_delay": 1, "link_delay": 1, "queue": "history_tree+mg1",
+                "parallelism": f"replicas{world}" if world > 1 else "single",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None,
+                "kernel": "k_port_stream",
+                "kernel_launches": port_launches,
+                "kernel_avg_us": port_ms * 1e3 / max(port_launches, 1),
+                "whole_job_frac": whole_job_gbs / HBM_PEAK_GBS,
+            },
+            "kernel_ms": {k: round(v[0], 4) for k, v in kst.items()},
+            "trace_gen_s": round(gen_s, 2),
+        }
+        if a.cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(a, W, H, hot)
+        print(json.dumps(line), flush=True)
+
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(a, W, H, hot):
+    """The CPU oracle (event-driven restatement of the reference path) timed on
+    one host core over a bounded sample of the same workload."""
+    from graphite_amd import gnoc
+    from oracle import oracle
+    tr = gnoc.synthetic_trace(W, H, a.load, a.cpu_sample_ppt, seed=a.seed, hotspot_fraction=hot, num_hotspots=16)
+    cfg = gnoc.EngineConfig(num_tiles=W * H)
+    t0 = time.perf_counter()
+    r = oracle.run(cfg, tr)
+    dt = time.perf_counter() - t0
+    hops = int(r.port_count.reshape(-1, 6)[:, :5].sum())
+    return {"value": hops / dt, "unit": "packet-hops/s", "cores": 1, "kind": "port",
+            "sample": f"{W}x{H} {a.mix} load={a.load} pkts/tile={a.cpu_sample_ppt}: {len(tr)} packets, "
+                      f"{hops} mesh hops in {dt:.2f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -73,7 +73,48 @@ struct gnoc_engine
    uint32_t h_levels = 0;
    double last_ms = 0.0;
    uint64_t* h_pinned = nullptr;
+
+   // kernel profiling (gnoc_set_profiling)
+   bool prof = false;
+   std::vector<hipEvent_t> evpool;
+   std::vector<int> evkid;     // kernel class per recorded launch
+   size_t evused = 0;
+   double kms[16] = {};
+   uint32_t klaunch[16] = {};
 };
+
+enum KernelClass { KC_CLASSIFY, KC_CHAIN, KC_SCAN, KC_INJ_COUNT, KC_INJ_OFFS, KC_INJ_SCATTER, KC_PORT, KC_FINALIZE, KC_N };
+static const char* const kKernelNames[KC_N] = { "k_classify", "k_chain_prefix", "k_scan_slots", "k_inj_group<count>",
+                                                "k_inj_offsets", "k_inj_group<scatter>", "k_port_stream", "k_finalize" };
+
+static hipError_t prof_mark(gnoc_engine* e, int kid)
+{
+   if (!e->prof) return hipSuccess;
+   while (e->evpool.size() < e->evused + 2)
+   {
+      hipEvent_t ev;
+      hipError_t r = hipEventCreate(&ev);
+      if (r != hipSuccess) return r;
+      e->evpool.push_back(ev);
+   }
+   e->evkid.push_back(kid);
+   return hipEventRecord(e->evpool[e->evused++], e->stream);
+}
+static hipError_t prof_end(gnoc_engine* e)
+{
+   if (!e->prof) return hipSuccess;
+   return hipEventRecord(e->evpool[e->evused++], e->stream);
+}
+
+// Launch with optional start/end events (kernel class kid).
+#define GNOC_LAUNCH(eng, kid, ...)                                     \
+   do                                                                  \
+   {                                                                   \
+      GNOC_HIP(eng, prof_mark(eng, kid));                              \
+      hipLaunchKernelGGL(__VA_ARGS__);                                 \
+      GNOC_HIP(eng, hipGetLastError());                                \
+      GNOC_HIP(eng, prof_end(eng));                                    \
+   } while (0)
 
 #define GNOC_HIP(eng, call)                                                                           \
    do                                                                                                 \
@@ -85,6 +126,21 @@ struct gnoc_engine
          return GNOC_EHIP;                                                                            \
       }                                                                                               \
    } while (0)
+
+static hipError_t prof_collect(gnoc_engine* e)
+{
+   for (int k = 0; k < KC_N; k++) { e->kms[k] = 0; e->klaunch[k] = 0; }
+   if (!e->prof) return hipSuccess;
+   for (size_t i = 0; i < e->evkid.size(); i++)
+   {
+      float ms = 0;
+      hipError_t r = hipEventElapsedTime(&ms, e->evpool[2 * i], e->evpool[2 * i + 1]);
+      if (r != hipSuccess) return r;
+      e->kms[e->evkid[i]] += ms;
+      e->klaunch[e->evkid[i]]++;
+   }
+   return hipSuccess;
+}
 
 static int fail(gnoc_engine* e, int code, const std::string& msg)
 {
@@ -181,6 +237,7 @@ void gnoc_destroy(gnoc_engine* e)
    if (e->ev0) (void) hipEventDestroy(e->ev0);
    if (e->ev1) (void) hipEventDestroy(e->ev1);
    if (e->h_pinned) (void) hipHostFree(e->h_pinned);
+   for (hipEvent_t ev : e->evpool) (void) hipEventDestroy(ev);
    if (e->stream) (void) hipStreamDestroy(e->stream);
    delete e;
 }
@@ -331,6 +388,8 @@ int gnoc_run(gnoc_engine* e)
    GNOC_HIP(e, e->port_cnt.ensure(nports * 8));
    GNOC_HIP(e, e->port_mg1.ensure(nports * 8));
 
+   e->evused = 0;
+   e->evkid.clear();
    GNOC_HIP(e, hipEventRecord(e->ev0, s));
    GNOC_HIP(e, hipMemsetAsync(e->slot_cnt.p, 0, (size_t) nslots * 4, s));
    GNOC_HIP(e, hipMemsetAsync(e->diff.p, 0, ndiff * 4, s));
@@ -342,7 +401,7 @@ int gnoc_run(gnoc_engine* e)
 
    const uint32_t cls_grid = (uint32_t) std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 8192));
    if (n)
-      hipLaunchKernelGGL(k_classify, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src, e->d_dst,
+      GNOC_LAUNCH(e, KC_CLASSIFY, k_classify, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src, e->d_dst,
                          e->d_bits, e->d_flags, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
                          e->slot_cnt.as<uint32_t>(), e->diff.as<int32_t>(), e->counters.as<unsigned long long>());
    GNOC_HIP(e, hipGetLastError());
@@ -353,11 +412,11 @@ int gnoc_run(gnoc_engine* e)
       if (n)
       {
          if (e->f1)
-            hipLaunchKernelGGL(k_finalize<true>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
+            GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<true>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
                                e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
                                e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), 1);
          else
-            hipLaunchKernelGGL(k_finalize<false>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
+            GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<false>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
                                e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
                                e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), 1);
       }
@@ -376,9 +435,9 @@ int gnoc_run(gnoc_engine* e)
       return GNOC_OK;
    }
 
-   hipLaunchKernelGGL(k_chain_prefix, dim3((c.W + c.H + 255) / 256), dim3(256), 0, s, c, e->diff.as<int32_t>(),
+   GNOC_LAUNCH(e, KC_CHAIN, k_chain_prefix, dim3((c.W + c.H + 255) / 256), dim3(256), 0, s, c, e->diff.as<int32_t>(),
                       e->slot_cnt.as<uint32_t>());
-   hipLaunchKernelGGL(k_scan_slots, dim3(1), dim3(1024), 0, s, nslots, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>());
+   GNOC_LAUNCH(e, KC_SCAN, k_scan_slots, dim3(1), dim3(1024), 0, s, nslots, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>());
    GNOC_HIP(e, hipGetLastError());
 
    // read back slot counts (route-static layout) and the record total
@@ -403,12 +462,12 @@ int gnoc_run(gnoc_engine* e)
       while ((1u << nbits) < N) nbits++;
       GNOC_HIP(e, e->hist.ensure((size_t) nchunks * N * 4));
       GNOC_HIP(e, e->offs.ensure((size_t) nchunks * N * 8));
-      hipLaunchKernelGGL(k_inj_group<false>, dim3(nchunks), dim3(64), N * 4, s, (uint64_t) n, chunk, N, nbits, e->d_src,
+      GNOC_LAUNCH(e, KC_INJ_COUNT, k_inj_group<false>, dim3(nchunks), dim3(64), N * 4, s, (uint64_t) n, chunk, N, nbits, e->d_src,
                          e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(),
                          (const uint64_t*) nullptr, (Rec*) nullptr, nchunks);
-      hipLaunchKernelGGL(k_inj_offsets, dim3(N), dim3(256), 0, s, nchunks, e->hist.as<uint32_t>(),
+      GNOC_LAUNCH(e, KC_INJ_OFFS, k_inj_offsets, dim3(N), dim3(256), 0, s, nchunks, e->hist.as<uint32_t>(),
                          e->slot_base.as<uint64_t>(), e->offs.as<uint64_t>());
-      hipLaunchKernelGGL(k_inj_group<true>, dim3(nchunks), dim3(64), N * 4, s, (uint64_t) n, chunk, N, nbits, e->d_src,
+      GNOC_LAUNCH(e, KC_INJ_SCATTER, k_inj_group<true>, dim3(nchunks), dim3(64), N * 4, s, (uint64_t) n, chunk, N, nbits, e->d_src,
                          e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(),
                          e->offs.as<uint64_t>(), e->recs.as<Rec>(), nchunks);
       GNOC_HIP(e, hipGetLastError());
@@ -427,12 +486,12 @@ int gnoc_run(gnoc_engine* e)
       if (!cnt) continue;
       const uint32_t* ports = e->plan_ports.as<uint32_t>() + lp.off[l];
       if (e->f1)
-         hipLaunchKernelGGL(k_port_stream<true>, dim3(cnt), dim3(STHREADS), 0, s, c, ports, e->slot_cnt.as<uint32_t>(),
+         GNOC_LAUNCH(e, KC_PORT, k_port_stream<true>, dim3(cnt), dim3(STHREADS), 0, s, c, ports, e->slot_cnt.as<uint32_t>(),
                             e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
                             e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
                             e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
       else
-         hipLaunchKernelGGL(k_port_stream<false>, dim3(cnt), dim3(STHREADS), 0, s, c, ports, e->slot_cnt.as<uint32_t>(),
+         GNOC_LAUNCH(e, KC_PORT, k_port_stream<false>, dim3(cnt), dim3(STHREADS), 0, s, c, ports, e->slot_cnt.as<uint32_t>(),
                             e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
                             e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
                             e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
@@ -442,11 +501,11 @@ int gnoc_run(gnoc_engine* e)
    if (n)
    {
       if (e->f1)
-         hipLaunchKernelGGL(k_finalize<true>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
+         GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<true>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
                             e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
                             e->cont.as<uint64_t>(), 0);
       else
-         hipLaunchKernelGGL(k_finalize<false>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
+         GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<false>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
                             e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
                             e->cont.as<uint64_t>(), 0);
    }
@@ -457,6 +516,7 @@ int gnoc_run(gnoc_engine* e)
    float ms = 0;
    GNOC_HIP(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
    e->last_ms = ms;
+   GNOC_HIP(e, prof_collect(e));
    if (*(unsigned int*) (e->h_pinned + 4)) return fail(e, GNOC_EHIP, "internal: route-count invariant violated");
    e->ran = true;
    return GNOC_OK;
@@ -513,6 +573,27 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
       GNOC_HIP(e, hipSetDevice(e->cfg.device));
       GNOC_HIP(e, hipMemcpy(m.data(), e->port_mg1.p, m.size() * 8, hipMemcpyDeviceToHost));
       for (uint64_t v : m) out->mg1_uses += v;
+   }
+   return GNOC_OK;
+}
+
+int gnoc_set_profiling(gnoc_engine* e, int enable)
+{
+   if (!e) return GNOC_EINVAL;
+   e->prof = enable != 0;
+   return GNOC_OK;
+}
+
+int gnoc_get_kernel_stats(gnoc_engine* e, const char** names, double* total_ms, uint32_t* launches, size_t cap,
+                          size_t* count)
+{
+   if (!e || !count) return GNOC_EINVAL;
+   *count = KC_N;
+   for (size_t k = 0; k < (size_t) KC_N && k < cap; k++)
+   {
+      if (names) names[k] = kKernelNames[k];
+      if (total_ms) total_ms[k] = e->kms[k];
+      if (launches) launches[k] = e->klaunch[k];
    }
    return GNOC_OK;
 }

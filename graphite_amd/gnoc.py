@@ -33,6 +33,7 @@ EXPORTED = (
     "gnoc_config_default", "gnoc_create", "gnoc_submit", "gnoc_submit_device", "gnoc_run",
     "gnoc_get_packet_results", "gnoc_get_port_stats", "gnoc_get_summary", "gnoc_device_final_ps",
     "gnoc_last_error", "gnoc_destroy", "gnoc_trace_synthetic", "gnoc_abi_version",
+    "gnoc_set_profiling", "gnoc_get_kernel_stats",
 )
 
 
@@ -108,6 +109,9 @@ def load() -> ctypes.CDLL:
         ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_uint64, ctypes.c_double, ctypes.c_int32, vp, vp, vp, vp, sz, ctypes.POINTER(sz)]
     lib.gnoc_abi_version.argtypes = []
+    lib.gnoc_set_profiling.argtypes = [vp, ctypes.c_int]
+    lib.gnoc_get_kernel_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(sz)]
     _lib = lib
     return lib
 
@@ -262,6 +266,19 @@ class Engine:
         ps, pc, pm = (np.empty(npt, np.uint64) for _ in range(3))
         self._check(self.lib.gnoc_get_port_stats(self._h, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data, npt))
         return Results(fin, zl, ct, ps, pc, pm, self.summary())
+
+    def set_profiling(self, on: bool) -> None:
+        self._check(self.lib.gnoc_set_profiling(self._h, int(on)))
+
+    def kernel_stats(self) -> dict:
+        """{kernel class: (total device ms over the last run, launches)}"""
+        cap = 32
+        names = (ctypes.c_char_p * cap)()
+        ms = (ctypes.c_double * cap)()
+        ln = (ctypes.c_uint32 * cap)()
+        cnt = ctypes.c_size_t()
+        self._check(self.lib.gnoc_get_kernel_stats(self._h, names, ms, ln, cap, ctypes.byref(cnt)))
+        return {names[i].decode(): (ms[i], ln[i]) for i in range(min(cnt.value, cap))}
 
     def device_final_ps(self) -> int:
         p = ctypes.c_void_p()

@@ -151,6 +151,15 @@ int gnoc_get_summary(gnoc_engine *eng, gnoc_summary *out);
  * callers that keep results in HBM (e.g. multi-GPU gathers). */
 int gnoc_device_final_ps(gnoc_engine *eng, void **dptr);
 
+/* Kernel timing (HIP events on the engine's stream around every launch of
+ * gnoc_run).  Off by default; costs one event record per launch when on. */
+int gnoc_set_profiling(gnoc_engine *eng, int enable);
+
+/* Per kernel class: name, summed device ms over the last gnoc_run, launches.
+ * Fills up to cap entries; *count = number of classes. */
+int gnoc_get_kernel_stats(gnoc_engine *eng, const char **names, double *total_ms,
+                          uint32_t *launches, size_t cap, size_t *count);
+
 const char *gnoc_last_error(const gnoc_engine *eng);
 void gnoc_destroy(gnoc_engine *eng);
 
