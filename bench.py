@@ -116,8 +116,9 @@ def main():
     if rank == 0:
         value = hops_all * a.steps / elapsed_max
         ms_step = elapsed_max / a.steps * 1e3
-        port_ms, port_launches = kst.get("k_port_stream", (0.0, 0))
-        # dominant kernel: k_port_stream, the per-port merge/queue/route stream.
+        dom = max(("k_chunk", "k_port_stream"), key=lambda k: kst.get(k, (0.0, 0))[0])
+        port_ms, port_launches = kst.get(dom, (0.0, 0))
+        # dominant kernel: the per-port merge/queue/route stream (k_chunk, or k_port_stream on the v1 path).
         # Algorithmic bytes over all its launches: 32 B per mesh hop + 24 B per packet.
         alg_bytes = hops * BYTES_PER_HOP + pkts * BYTES_PER_PKT
         achieved = alg_bytes / (port_ms * 1e-3) / 1e9 if port_ms > 0 else 0.0
@@ -140,6 +141,7 @@ def main():
                 "tiles": W * H, "packets_per_rank": len(tr), "mesh_hops_per_rank": hops,
                 "flit_width": 64, "router_delay": 1, "link_delay": 1, "queue": "history_tree+mg1",
                 "parallelism": f"replicas{world}" if world > 1 else "single",
+                "engine_path": int(summ.get("engine_path", -1)),
             },
             "roofline": {
                 "bound": "hbm",
@@ -148,7 +150,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None,
-                "kernel": "k_port_stream",
+                "kernel": dom,
                 "kernel_launches": port_launches,
                 "kernel_avg_us": port_ms * 1e3 / max(port_launches, 1),
                 "whole_job_frac": whole_job_gbs / HBM_PEAK_GBS,

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -10,6 +11,7 @@
 
 #include "gnoc.h"
 #include "kernels.hip"
+#include "kernels_v2.hip"
 
 using namespace gnoc;
 
@@ -67,6 +69,10 @@ struct gnoc_engine
    DevBuf slot_cnt, slot_base, diff, counters;
    DevBuf dirty, recs, port_sum, port_cnt, port_mg1;
    DevBuf hist, offs, plan_ports;
+   DevBuf samp_t, samp_id, nexc, cflags, cstate, lctr, chunks;
+   int force_v1 = 0;          // GNOC_ENGINE=v1, or set after a v2 overflow
+   int used_v2 = 0;
+   uint64_t h_chunks = 0;
    std::vector<uint32_t> h_slot_cnt;
    uint64_t h_counters[2] = { 0, 0 };
    uint64_t h_records = 0;
@@ -83,9 +89,10 @@ struct gnoc_engine
    uint32_t klaunch[16] = {};
 };
 
-enum KernelClass { KC_CLASSIFY, KC_CHAIN, KC_SCAN, KC_INJ_COUNT, KC_INJ_OFFS, KC_INJ_SCATTER, KC_PORT, KC_FINALIZE, KC_N };
+enum KernelClass { KC_CLASSIFY, KC_CHAIN, KC_SCAN, KC_INJ_COUNT, KC_INJ_OFFS, KC_INJ_SCATTER, KC_PORT, KC_FINALIZE, KC_INJ_SAMPLES, KC_CHUNK, KC_N };
 static const char* const kKernelNames[KC_N] = { "k_classify", "k_chain_prefix", "k_scan_slots", "k_inj_group<count>",
-                                                "k_inj_offsets", "k_inj_group<scatter>", "k_port_stream", "k_finalize" };
+                                                "k_inj_offsets", "k_inj_group<scatter>", "k_port_stream", "k_finalize",
+                                                "k_inj_samples", "k_chunk" };
 
 static hipError_t prof_mark(gnoc_engine* e, int kid)
 {
@@ -361,7 +368,98 @@ static void build_plan(const gnoc_engine* e, LevelPlan& lp)
    lp.off.push_back((uint32_t) lp.ports.size());
 }
 
-int gnoc_run(gnoc_engine* e)
+
+constexpr int GNOC_V2_RETRY = 1000;
+
+static int run_levels_v1(gnoc_engine* e)
+{
+   const DevCfg& c = e->dc;
+   hipStream_t s = e->stream;
+   LevelPlan lp;
+   build_plan(e, lp);
+   GNOC_HIP(e, e->plan_ports.ensure(std::max<size_t>(1, lp.ports.size()) * 4));
+   if (!lp.ports.empty())
+      GNOC_HIP(e, hipMemcpyAsync(e->plan_ports.p, lp.ports.data(), lp.ports.size() * 4, hipMemcpyHostToDevice, s));
+   e->h_levels = (uint32_t) (lp.off.size() - 1);
+   for (size_t l = 0; l + 1 < lp.off.size(); l++)
+   {
+      const uint32_t cnt = lp.off[l + 1] - lp.off[l];
+      if (!cnt) continue;
+      const uint32_t* ports = e->plan_ports.as<uint32_t>() + lp.off[l];
+      if (e->f1)
+         GNOC_LAUNCH(e, KC_PORT, k_port_stream<true>, dim3(cnt), dim3(STHREADS), 0, s, c, ports, e->slot_cnt.as<uint32_t>(),
+                            e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
+                            e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
+                            e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
+      else
+         GNOC_LAUNCH(e, KC_PORT, k_port_stream<false>, dim3(cnt), dim3(STHREADS), 0, s, c, ports, e->slot_cnt.as<uint32_t>(),
+                            e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
+                            e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
+                            e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
+   }
+   return GNOC_OK;
+}
+
+static int run_levels_v2(gnoc_engine* e)
+{
+   const DevCfg& c = e->dc;
+   hipStream_t s = e->stream;
+   const uint32_t N = c.N;
+   const uint32_t nslots = N * PORTS * INS;
+   LevelPlan lp;
+   build_plan(e, lp);
+   const size_t nlev = lp.off.size() - 1;
+   e->h_levels = (uint32_t) nlev;
+   // chunk plan: ~C2_TARGET records per chunk, key ranges cut on the port's largest input
+   std::vector<ChunkDesc> ch;
+   std::vector<uint32_t> choff(nlev + 1, 0);
+   uint32_t g = 0;
+   for (size_t l = 0; l < nlev; l++)
+   {
+      choff[l] = (uint32_t) ch.size();
+      for (uint32_t k = lp.off[l]; k < lp.off[l + 1]; k++)
+      {
+         const uint32_t port = lp.ports[k];
+         uint64_t tot = 0;
+         for (uint32_t in = 0; in < INS; in++) tot += e->h_slot_cnt[port * INS + in];
+         const uint32_t nc = (uint32_t) std::max<uint64_t>(1, (tot + C2_TARGET - 1) / C2_TARGET);
+         for (uint32_t j = 0; j < nc; j++) ch.push_back(ChunkDesc{ port, j, nc, g });
+         g += nc;
+      }
+   }
+   choff[nlev] = (uint32_t) ch.size();
+   e->h_chunks = ch.size();
+   const uint64_t total = e->h_records;
+   GNOC_HIP(e, e->samp_t.ensure((total / 64 + 1) * 8));
+   GNOC_HIP(e, e->samp_id.ensure((total / 64 + 1) * 4));
+   GNOC_HIP(e, e->nexc.ensure((size_t) nslots * 4));
+   GNOC_HIP(e, e->cflags.ensure(std::max<size_t>(1, ch.size()) * 4));
+   GNOC_HIP(e, e->cstate.ensure(std::max<size_t>(1, ch.size()) * 16 * 8));
+   GNOC_HIP(e, e->lctr.ensure(std::max<size_t>(1, nlev) * 4));
+   GNOC_HIP(e, e->chunks.ensure(std::max<size_t>(1, ch.size()) * sizeof(ChunkDesc)));
+   GNOC_HIP(e, hipMemsetAsync(e->nexc.p, 0, (size_t) nslots * 4, s));
+   GNOC_HIP(e, hipMemsetAsync(e->cflags.p, 0, std::max<size_t>(1, ch.size()) * 4, s));
+   GNOC_HIP(e, hipMemsetAsync(e->lctr.p, 0, std::max<size_t>(1, nlev) * 4, s));
+   if (!ch.empty())
+      GNOC_HIP(e, hipMemcpyAsync(e->chunks.p, ch.data(), ch.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
+   if (e->n)
+      GNOC_LAUNCH(e, KC_INJ_SAMPLES, k_inj_samples, dim3(N), dim3(256), 0, s, N, e->slot_cnt.as<uint32_t>(),
+                  e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>());
+   for (size_t l = 0; l < nlev; l++)
+   {
+      const uint32_t cnt = choff[l + 1] - choff[l];
+      if (!cnt) continue;
+      GNOC_LAUNCH(e, KC_CHUNK, k_chunk, dim3(cnt), dim3(C2_T), 0, s, c, e->chunks.as<ChunkDesc>() + choff[l],
+                  e->lctr.as<unsigned>() + l, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->recs.as<Rec>(),
+                  e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(), e->cflags.as<uint32_t>(),
+                  e->cstate.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
+                  e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
+                  e->counters.as<unsigned>() + 8);
+   }
+   return GNOC_OK;
+}
+
+static int run_once(gnoc_engine* e)
 {
    if (!e) return GNOC_EINVAL;
    if (!e->submitted) return fail(e, GNOC_ESTATE, "gnoc_run before gnoc_submit");
@@ -473,30 +571,18 @@ int gnoc_run(gnoc_engine* e)
       GNOC_HIP(e, hipGetLastError());
    }
 
-   // level plan (host, from the route-static slot counts)
-   LevelPlan lp;
-   build_plan(e, lp);
-   GNOC_HIP(e, e->plan_ports.ensure(std::max<size_t>(1, lp.ports.size()) * 4));
-   if (!lp.ports.empty())
-      GNOC_HIP(e, hipMemcpyAsync(e->plan_ports.p, lp.ports.data(), lp.ports.size() * 4, hipMemcpyHostToDevice, s));
-   e->h_levels = (uint32_t) (lp.off.size() - 1);
-   for (size_t l = 0; l + 1 < lp.off.size(); l++)
+   const bool v2 = e->f1 && c.max_list >= 3 && !e->force_v1;
+   e->used_v2 = v2;
+   if (v2)
    {
-      const uint32_t cnt = lp.off[l + 1] - lp.off[l];
-      if (!cnt) continue;
-      const uint32_t* ports = e->plan_ports.as<uint32_t>() + lp.off[l];
-      if (e->f1)
-         GNOC_LAUNCH(e, KC_PORT, k_port_stream<true>, dim3(cnt), dim3(STHREADS), 0, s, c, ports, e->slot_cnt.as<uint32_t>(),
-                            e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
-                            e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
-                            e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
-      else
-         GNOC_LAUNCH(e, KC_PORT, k_port_stream<false>, dim3(cnt), dim3(STHREADS), 0, s, c, ports, e->slot_cnt.as<uint32_t>(),
-                            e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
-                            e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
-                            e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
+      int rc = run_levels_v2(e);
+      if (rc) return rc;
    }
-   GNOC_HIP(e, hipGetLastError());
+   else
+   {
+      int rc = run_levels_v1(e);
+      if (rc) return rc;
+   }
 
    if (n)
    {
@@ -517,9 +603,28 @@ int gnoc_run(gnoc_engine* e)
    GNOC_HIP(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
    e->last_ms = ms;
    GNOC_HIP(e, prof_collect(e));
-   if (*(unsigned int*) (e->h_pinned + 4)) return fail(e, GNOC_EHIP, "internal: route-count invariant violated");
+   const unsigned errf = *(unsigned int*) (e->h_pinned + 4);
+   if (errf & 1u) return fail(e, GNOC_EHIP, "internal: route-count invariant violated");
+   if (errf & 6u) return GNOC_V2_RETRY;   // burst beyond the chunk splitter / look-back timeout
    e->ran = true;
    return GNOC_OK;
+}
+
+int gnoc_run(gnoc_engine* e)
+{
+   if (!e) return GNOC_EINVAL;
+   const char* env = std::getenv("GNOC_ENGINE");
+   const int forced = env && std::strcmp(env, "v1") == 0;
+   e->force_v1 = forced;
+   int rc = run_once(e);
+   if (rc == GNOC_V2_RETRY)
+   {
+      e->force_v1 = 1;   // exact but slower whole-port streams
+      rc = run_once(e);
+      e->force_v1 = forced;
+      if (rc == GNOC_V2_RETRY) rc = fail(e, GNOC_EHIP, "internal: v1 path reported overflow");
+   }
+   return rc;
 }
 
 int gnoc_get_packet_results(gnoc_engine* e, uint64_t* final_ps, uint64_t* zero_load_ps, uint64_t* contention_ps, size_t n)
@@ -567,6 +672,7 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
    out->records = e->h_records;
    out->levels = e->h_levels;
    out->last_run_ms = e->last_ms;
+   out->engine_path = e->dc.contention ? (uint32_t) e->used_v2 : 2u;
    if (e->ran && e->dc.contention)
    {
       std::vector<uint64_t> m((size_t) e->dc.N * PORTS);

@@ -127,7 +127,8 @@ __global__ void k_chain_prefix(DevCfg c, const int32_t* __restrict__ diff, uint3
    }
 }
 
-// Exclusive scan of slot counts -> 64-bit slot bases; base[nslots] = total.
+// Exclusive scan of slot counts (rounded up to 64 records, so every slot starts
+// on a 1 KiB boundary and its 1-in-64 key samples index as base/64) -> bases.
 // Single 1024-thread block; nslots = 30 N is small.
 __global__ __launch_bounds__(1024) void k_scan_slots(uint32_t nslots, const uint32_t* __restrict__ cnt,
                                                      uint64_t* __restrict__ base)
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(1024) void k_scan_slots(uint32_t nslots, const uint
    const uint32_t per = (nslots + 1023) / 1024;
    const uint32_t lo = threadIdx.x * per, hi = min(lo + per, nslots);
    uint64_t s = 0;
-   for (uint32_t i = lo; i < hi; i++) s += cnt[i];
+   for (uint32_t i = lo; i < hi; i++) s += (cnt[i] + 63) & ~63u;   // slots start 64-record aligned (1 KiB)
    part[threadIdx.x] = s;
    __syncthreads();
    for (uint32_t off = 1; off < 1024; off <<= 1)
@@ -147,7 +148,7 @@ __global__ __launch_bounds__(1024) void k_scan_slots(uint32_t nslots, const uint
       __syncthreads();
    }
    uint64_t run = part[threadIdx.x] - s;
-   for (uint32_t i = lo; i < hi; i++) { base[i] = run; run += cnt[i]; }
+   for (uint32_t i = lo; i < hi; i++) { base[i] = run; run += (cnt[i] + 63) & ~63u; }
    if (threadIdx.x == 1023) base[nslots] = part[1023];
 }
 

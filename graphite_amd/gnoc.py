@@ -74,7 +74,7 @@ class GnocSummary(ctypes.Structure):
         ("records", ctypes.c_uint64),
         ("mg1_uses", ctypes.c_uint64),
         ("levels", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("engine_path", ctypes.c_uint32),
         ("last_run_ms", ctypes.c_double),
     ]
 
@@ -256,7 +256,7 @@ class Engine:
     def summary(self) -> dict:
         s = GnocSummary()
         self._check(self.lib.gnoc_get_summary(self._h, ctypes.byref(s)))
-        return {f[0]: getattr(s, f[0]) for f in GnocSummary._fields_ if f[0] != "reserved"}
+        return {f[0]: getattr(s, f[0]) for f in GnocSummary._fields_ }
 
     def results(self) -> Results:
         n = self._n

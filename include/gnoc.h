@@ -110,7 +110,7 @@ typedef struct gnoc_summary
    uint64_t records;            /* hop records materialised (injection + mesh)          */
    uint64_t mg1_uses;           /* requests served by the M/G/1 fallback                */
    uint32_t levels;             /* dependency levels executed                           */
-   uint32_t reserved;
+   uint32_t engine_path;        /* 0 whole-port streams, 1 chunked look-back, 2 closed form */
    double   last_run_ms;        /* device time of the last gnoc_run (HIP events)        */
 } gnoc_summary;
 

@@ -155,3 +155,56 @@ def test_repeatable_bytes():
     eng.run()
     b = eng.results()
     assert np.array_equal(a.final_ps, b.final_ps) and np.array_equal(a.port_sum_delay, b.port_sum_delay)
+
+
+def test_serial_prefix_spans_chunks():
+    """A 3000-packet burst at t=0 from one tile keeps its injection queue in the
+    history-tree/M-G-1 serial prefix across several chunks (look-back must hand
+    over the serial state), and floods one row (burst splitting)."""
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = random_trace(12000, 8, 8, seed=21, max_cycle=4000)
+    tr.inject_ps[:3000] = 0
+    tr.src[:3000] = 9
+    order = np.lexsort((np.arange(len(tr)), tr.inject_ps))
+    tr = type(tr)(tr.inject_ps[order], tr.src[order], tr.dst[order], tr.bits[order], tr.flags[order])
+    got, ref = run_both(cfg, tr)
+    assert ref.port_mg1.sum() > 1000
+    assert_same(got, ref)
+
+
+def test_bursty_input_splits_leaves():
+    """Bursts on one input of a port (many packets at the same cycle from one
+    tile towards one column) force the chunk splitter to cut leaves."""
+    cfg = gnoc.EngineConfig(num_tiles=256, analytical_enabled=False)
+    rng = np.random.default_rng(3)
+    n = 60000
+    t = np.sort(rng.integers(0, 20000, n)).astype(np.uint64) * np.uint64(1000)
+    src = rng.integers(0, 256, n).astype(np.uint32)
+    dst = rng.integers(0, 256, n).astype(np.uint32)
+    burst = (t // 1000) % 2000 < 30
+    src[burst] = 16 * 5 + 1
+    dst[burst] = 16 * 12 + 14
+    tr = gnoc.Trace(t, src, dst, np.full(n, 576, np.uint32), np.zeros(n, np.uint32))
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+
+
+def test_engine_paths_agree():
+    """Whole-port streams (v1) and chunked look-back (v2) give identical bytes."""
+    import os
+    cfg = gnoc.EngineConfig(num_tiles=256)
+    tr = gnoc.synthetic_trace(16, 16, 0.02, 200, seed=8)
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    a = eng.results()
+    assert a.summary["engine_path"] == 1
+    os.environ["GNOC_ENGINE"] = "v1"
+    try:
+        eng.run()
+        b = eng.results()
+    finally:
+        del os.environ["GNOC_ENGINE"]
+    assert b.summary["engine_path"] == 0
+    for k in ("final_ps", "port_sum_delay", "port_count", "port_mg1"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
