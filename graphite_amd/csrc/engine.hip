@@ -69,7 +69,7 @@ struct gnoc_engine
    DevBuf slot_cnt, slot_base, diff, counters;
    DevBuf dirty, recs, port_sum, port_cnt, port_mg1;
    DevBuf hist, offs, plan_ports;
-   DevBuf samp_t, samp_id, nexc, cflags, cstate, lctr, chunks;
+   DevBuf samp_t, samp_id, nexc, cflags, cstate, lctr, chunks, stamps, portio;
    int force_v1 = 0;          // GNOC_ENGINE=v1, or set after a v2 overflow
    int used_v2 = 0;
    uint64_t h_chunks = 0;
@@ -410,7 +410,15 @@ static int run_levels_v2(gnoc_engine* e)
    build_plan(e, lp);
    const size_t nlev = lp.off.size() - 1;
    e->h_levels = (uint32_t) nlev;
-   // chunk plan: ~C2_TARGET records per chunk, key ranges cut on the port's largest input
+   // slot bases exactly as k_scan_slots lays them out (64-record aligned)
+   std::vector<uint64_t> hbase((size_t) nslots + 1);
+   {
+      uint64_t run = 0;
+      for (uint32_t i = 0; i < nslots; i++) { hbase[i] = run; run += (e->h_slot_cnt[i] + 63) & ~63u; }
+      hbase[nslots] = run;
+   }
+   // port descriptions + chunk plan: ~C2_TARGET records per chunk, cut on the port's largest input
+   std::vector<PortIO> pio;
    std::vector<ChunkDesc> ch;
    std::vector<uint32_t> choff(nlev + 1, 0);
    uint32_t g = 0;
@@ -420,15 +428,54 @@ static int run_levels_v2(gnoc_engine* e)
       for (uint32_t k = lp.off[l]; k < lp.off[l + 1]; k++)
       {
          const uint32_t port = lp.ports[k];
+         PortIO io;
+         std::memset(&io, 0, sizeof(io));
+         io.port = port;
+         io.tile = port / PORTS;
+         io.dir = port % PORTS;
          uint64_t tot = 0;
-         for (uint32_t in = 0; in < INS; in++) tot += e->h_slot_cnt[port * INS + in];
+         for (uint32_t in = 0; in < INS; in++)
+         {
+            const uint32_t sl = port * INS + in;
+            const uint32_t n = e->h_slot_cnt[sl];
+            tot += n;
+            if (n && io.nin < C2_IN)
+            {
+               io.slot[io.nin] = sl;
+               io.base[io.nin] = hbase[sl];
+               io.cnt[io.nin] = n;
+               io.nmain[io.nin] = n;
+               if (n > io.cnt[io.sb]) io.sb = io.nin;
+               io.nin++;
+            }
+         }
+         io.ntile = io.tile;
+         io.nside = IN_LOCAL;
+         if (io.dir == P_RIGHT) { io.ntile = io.tile + 1; io.nside = IN_W; }
+         else if (io.dir == P_LEFT) { io.ntile = io.tile - 1; io.nside = IN_E; }
+         else if (io.dir == P_UP) { io.ntile = io.tile + c.W; io.nside = IN_S; }
+         else if (io.dir == P_DOWN) { io.ntile = io.tile - c.W; io.nside = IN_N; }
+         io.nx = io.ntile % c.W;
+         io.ny = io.ntile / c.W;
+         for (uint32_t d = 0; d < 5; d++)
+         {
+            const uint32_t os = slot_of(io.ntile, d, io.nside);
+            io.oslot[d] = os;
+            io.obase[d] = io.dir == P_SELF ? 0 : hbase[os];
+            io.ocnt[d] = io.dir == P_SELF ? 0 : e->h_slot_cnt[os];
+         }
+         const uint32_t pidx = (uint32_t) pio.size();
+         pio.push_back(io);
          const uint32_t nc = (uint32_t) std::max<uint64_t>(1, (tot + C2_TARGET - 1) / C2_TARGET);
-         for (uint32_t j = 0; j < nc; j++) ch.push_back(ChunkDesc{ port, j, nc, g });
+         for (uint32_t j = 0; j < nc; j++) ch.push_back(ChunkDesc{ pidx, j, nc, g });
          g += nc;
       }
    }
    choff[nlev] = (uint32_t) ch.size();
    e->h_chunks = ch.size();
+   GNOC_HIP(e, e->portio.ensure(std::max<size_t>(1, pio.size()) * sizeof(PortIO)));
+   if (!pio.empty())
+      GNOC_HIP(e, hipMemcpyAsync(e->portio.p, pio.data(), pio.size() * sizeof(PortIO), hipMemcpyHostToDevice, s));
    const uint64_t total = e->h_records;
    GNOC_HIP(e, e->samp_t.ensure((total / 64 + 1) * 8));
    GNOC_HIP(e, e->samp_id.ensure((total / 64 + 1) * 4));
@@ -445,16 +492,32 @@ static int run_levels_v2(gnoc_engine* e)
    if (e->n)
       GNOC_LAUNCH(e, KC_INJ_SAMPLES, k_inj_samples, dim3(N), dim3(256), 0, s, N, e->slot_cnt.as<uint32_t>(),
                   e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>());
+   const char* stv = std::getenv("GNOC_STAMPS");
+   const bool stamps = stv && *stv == '1';
+   if (stamps)
+   {
+      GNOC_HIP(e, e->stamps.ensure(std::max<size_t>(1, ch.size()) * 16 * 8));
+      GNOC_HIP(e, hipMemsetAsync(e->stamps.p, 0, std::max<size_t>(1, ch.size()) * 16 * 8, s));
+   }
    for (size_t l = 0; l < nlev; l++)
    {
       const uint32_t cnt = choff[l + 1] - choff[l];
       if (!cnt) continue;
-      GNOC_LAUNCH(e, KC_CHUNK, k_chunk, dim3(cnt), dim3(C2_T), 0, s, c, e->chunks.as<ChunkDesc>() + choff[l],
+      uint64_t* sp = stamps ? e->stamps.as<uint64_t>() + (uint64_t) choff[l] * 16 : nullptr;
+      if (stamps)
+      GNOC_LAUNCH(e, KC_CHUNK, k_chunk<true>, dim3(cnt), dim3(C2_T), 0, s, c, e->chunks.as<ChunkDesc>() + choff[l], e->portio.as<PortIO>(),
                   e->lctr.as<unsigned>() + l, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->recs.as<Rec>(),
                   e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(), e->cflags.as<uint32_t>(),
                   e->cstate.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
                   e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
-                  e->counters.as<unsigned>() + 8);
+                  e->counters.as<unsigned>() + 8, sp);
+      else
+      GNOC_LAUNCH(e, KC_CHUNK, k_chunk<false>, dim3(cnt), dim3(C2_T), 0, s, c, e->chunks.as<ChunkDesc>() + choff[l], e->portio.as<PortIO>(),
+                  e->lctr.as<unsigned>() + l, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->recs.as<Rec>(),
+                  e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(), e->cflags.as<uint32_t>(),
+                  e->cstate.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
+                  e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
+                  e->counters.as<unsigned>() + 8, (uint64_t*) nullptr);
    }
    return GNOC_OK;
 }
@@ -701,6 +764,17 @@ int gnoc_get_kernel_stats(gnoc_engine* e, const char** names, double* total_ms, 
       if (total_ms) total_ms[k] = e->kms[k];
       if (launches) launches[k] = e->klaunch[k];
    }
+   return GNOC_OK;
+}
+
+extern "C" __attribute__((visibility("default"))) int gnoc_debug_stamps(gnoc_engine* e, uint64_t* out, size_t cap,
+                                                                     size_t* nchunks)
+{
+   if (!e || !nchunks) return GNOC_EINVAL;
+   *nchunks = e->h_chunks;
+   if (!out || !e->stamps.p) return GNOC_OK;
+   const size_t n = std::min(cap, (size_t) e->h_chunks * 16);
+   GNOC_HIP(e, hipMemcpy(out, e->stamps.p, n * 8, hipMemcpyDeviceToHost));
    return GNOC_OK;
 }
 

@@ -28,7 +28,7 @@ constexpr uint32_t SPIN_LIMIT = 1u << 24;
 
 struct ChunkDesc
 {
-   uint32_t port, j, nc, gbase;   // port, chunk index in port, chunks of port, state index of chunk 0
+   uint32_t port, j, nc, gbase;   // PortIO index, chunk index in port, chunks of port, state index of chunk 0
 };
 
 // carried queue state (exclusive prefix of a chunk / leaf)
@@ -40,6 +40,24 @@ struct Carry
    uint64_t narr, newest;
    uint32_t cnt[5];
 };
+
+// Per-port static description (host-built from the route-static slot layout),
+// copied into LDS by every chunk; nmain/nx_exc are refreshed from nexc[].
+struct __attribute__((aligned(16))) PortIO
+{
+   uint32_t tile, dir, port, nin;
+   uint64_t base[C2_IN];
+   uint32_t slot[C2_IN];
+   uint32_t cnt[C2_IN];
+   uint32_t nmain[C2_IN];
+   uint32_t nx_exc[C2_IN];
+   uint64_t obase[5];
+   uint32_t oslot[5];
+   uint32_t ocnt[5];
+   uint32_t ntile, nside, nx, ny;
+   uint32_t sb, pad0;
+};
+static_assert(sizeof(PortIO) % 4 == 0, "PortIO copy granularity");
 
 struct C2Smem
 {
@@ -64,6 +82,8 @@ struct C2Smem
    uint32_t search[8];
    Carry cy;
    uint64_t st_sum, st_cnt, st_mg1;
+   uint32_t published;
+   PortIO io;
 };
 
 __device__ __forceinline__ uint32_t ld_flag(const uint32_t* p)
@@ -204,17 +224,6 @@ __device__ ScanOut block_scan_seg(C2Smem& sm, uint32_t lo, uint32_t hi, uint32_t
    o.tc1 = T1;
    return o;
 }
-
-struct PortIO
-{
-   uint32_t tile, dir, port;
-   uint32_t nin;
-   uint32_t slot[C2_IN];
-   uint64_t base[C2_IN];
-   uint32_t nmain[C2_IN], nx_exc[C2_IN], cnt[C2_IN];
-   uint32_t ntile, nside, nx, ny;
-   uint32_t oslot[5];
-};
 
 // Load one leaf (main ranges sm.lo/hi + exceptions with key in [klo,khi)) into LDS and merge.
 __device__ void load_merge(C2Smem& sm, const PortIO& io, const Rec* __restrict__ recs, uint64_t klo_t, uint32_t klo_i,
@@ -359,16 +368,16 @@ __device__ void process_leaf(C2Smem& sm, const PortIO& io, const DevCfg& c, Rec*
             {
                // M/G/1-served: may leave FIFO order -> exception tail of the slot
                const uint32_t x = atomicAdd(&nexc[os], 1u);
-               recs[slot_base[os] + slot_cnt[os] - 1 - x] = o;
+               recs[io.obase[nd] + io.ocnt[nd] - 1 - x] = o;
             }
             else
             {
                const uint32_t pos = sm.cy.cnt[nd]++;
-               recs[slot_base[os] + pos] = o;
+               recs[io.obase[nd] + pos] = o;
                if ((pos & 63) == 0)
                {
-                  samp_t[slot_base[os] / 64 + pos / 64] = tn;
-                  samp_id[slot_base[os] / 64 + pos / 64] = id;
+                  samp_t[io.obase[nd] / 64 + pos / 64] = tn;
+                  samp_id[io.obase[nd] / 64 + pos / 64] = id;
                }
             }
          }
@@ -413,8 +422,7 @@ __device__ void process_leaf(C2Smem& sm, const PortIO& io, const DevCfg& c, Rec*
       const uint32_t nd = route_dir(ax, dir, io.nx, io.ny, c);
       const uint32_t pos = sm.cy.cnt[nd] + get_dir(c0, c1, nd);
       add_dir(c0, c1, nd);
-      const uint32_t os = io.oslot[nd];
-      const uint64_t gb = slot_base[os];
+      const uint64_t gb = io.obase[nd];
       Rec o;
       o.t = tn;
       o.id = id;
@@ -568,14 +576,23 @@ __device__ void publish_inc(uint64_t* __restrict__ st, uint32_t* __restrict__ fl
    __hip_atomic_store(&flags[cidx], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(C2_T) void k_chunk(DevCfg c, const ChunkDesc* __restrict__ chunks, unsigned* __restrict__ ctr,
+#define STAMP(k)                                                                                         \
+   do                                                                                                   \
+   {                                                                                                    \
+      if (STAMPS && stamps && tid == 0) stamps[(uint64_t) sm.cid * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+   } while (0)
+
+template <bool STAMPS>
+__global__ __launch_bounds__(C2_T) void k_chunk(DevCfg c, const ChunkDesc* __restrict__ chunks, const PortIO* __restrict__ ports,
+                                                unsigned* __restrict__ ctr,
                                                 const uint32_t* __restrict__ slot_cnt, const uint64_t* __restrict__ slot_base,
                                                 Rec* __restrict__ recs, uint64_t* __restrict__ samp_t,
                                                 uint32_t* __restrict__ samp_id, uint32_t* __restrict__ nexc,
                                                 uint32_t* __restrict__ flags, uint64_t* __restrict__ st,
                                                 uint64_t* __restrict__ final_ps, unsigned long long* __restrict__ port_sum,
                                                 unsigned long long* __restrict__ port_cnt,
-                                                unsigned long long* __restrict__ port_mg1, unsigned* __restrict__ errflag)
+                                                unsigned long long* __restrict__ port_mg1, unsigned* __restrict__ errflag,
+                                                uint64_t* __restrict__ stamps)
 {
    __shared__ C2Smem sm;
    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -585,43 +602,31 @@ __global__ __launch_bounds__(C2_T) void k_chunk(DevCfg c, const ChunkDesc* __res
       sm.st_sum = 0;
       sm.st_cnt = 0;
       sm.st_mg1 = 0;
+      sm.published = 0;
    }
    __syncthreads();
+   STAMP(0);
    const ChunkDesc d = chunks[sm.cid];
    const uint32_t cidx = d.gbase + d.j;
 
-   PortIO io;
-   io.port = d.port;
-   io.tile = d.port / PORTS;
-   io.dir = d.port % PORTS;
-   io.nin = 0;
-   for (uint32_t in = 0; in < INS; in++)
+   // ---- port description -> LDS (one coalesced copy), refresh exception counts
    {
-      const uint32_t sl = slot_of(io.tile, io.dir, in);
-      const uint32_t k = slot_cnt[sl];
-      if (k && io.nin < C2_IN)
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(ports + d.port);
+      uint32_t* dstw = reinterpret_cast<uint32_t*>(&sm.io);
+      for (uint32_t k = tid; k < (uint32_t) (sizeof(PortIO) / 4); k += C2_T) dstw[k] = src[k];
+      __syncthreads();
+      if (tid < sm.io.nin)
       {
-         io.slot[io.nin] = sl;
-         io.base[io.nin] = slot_base[sl];
-         io.cnt[io.nin] = k;
-         io.nx_exc[io.nin] = nexc[sl];
-         io.nmain[io.nin] = k - io.nx_exc[io.nin];
-         io.nin++;
+         const uint32_t x = nexc[sm.io.slot[tid]];
+         sm.io.nx_exc[tid] = x;
+         sm.io.nmain[tid] = sm.io.cnt[tid] - x;
       }
+      __syncthreads();
    }
-   io.ntile = io.tile;
-   io.nside = IN_LOCAL;
-   if (io.dir == P_RIGHT) { io.ntile = io.tile + 1; io.nside = IN_W; }
-   else if (io.dir == P_LEFT) { io.ntile = io.tile - 1; io.nside = IN_E; }
-   else if (io.dir == P_UP) { io.ntile = io.tile + c.W; io.nside = IN_S; }
-   else if (io.dir == P_DOWN) { io.ntile = io.tile - c.W; io.nside = IN_N; }
-   tile_xy(io.ntile, c.W, c.magicW, io.nx, io.ny);
-   for (uint32_t k = 0; k < 5; k++) io.oslot[k] = slot_of(io.ntile, k, io.nside);
+   const PortIO& io = sm.io;
 
    // ---- chunk key range from the largest input (exact index split, no search)
-   uint32_t sb = 0;
-   for (uint32_t s = 1; s < io.nin; s++)
-      if (io.nmain[s] > io.nmain[sb]) sb = s;
+   const uint32_t sb = io.sb;
    const uint32_t nb = io.nmain[sb];
    const uint32_t ilo = (uint32_t) (((uint64_t) d.j * nb) / d.nc);
    const uint32_t ihi = (uint32_t) (((uint64_t) (d.j + 1) * nb) / d.nc);
@@ -631,6 +636,7 @@ __global__ __launch_bounds__(C2_T) void k_chunk(DevCfg c, const ChunkDesc* __res
    if (has_lo) { const Rec r = recs[io.base[sb] + ilo]; klo_t = r.t; klo_i = r.id; }
    if (has_hi) { const Rec r = recs[io.base[sb] + ihi]; khi_t = r.t; khi_i = r.id; }
 
+   STAMP(1);
    // ---- main ranges of the other inputs (waves search in parallel)
    for (uint32_t q = wv; q < 2 * C2_IN; q += C2_T / 64)
    {
@@ -649,6 +655,7 @@ __global__ __launch_bounds__(C2_T) void k_chunk(DevCfg c, const ChunkDesc* __res
       if (lane == 0) sm.search[q] = v;
    }
    __syncthreads();
+   STAMP(2);
    uint32_t total = 0;
    uint32_t rlo[C2_IN], rhi[C2_IN];
    for (uint32_t s = 0; s < C2_IN; s++)
@@ -672,23 +679,43 @@ __global__ __launch_bounds__(C2_T) void k_chunk(DevCfg c, const ChunkDesc* __res
       if (tid < C2_IN) { sm.lo[tid] = rlo[tid]; sm.hi[tid] = rhi[tid]; }
       __syncthreads();
       load_merge(sm, io, recs, klo_t, klo_i, khi_t, khi_i, has_lo, has_hi);
+      STAMP(3);
       if (d.j == 0)
       {
          if (tid == 0 && c.analytical && sm.E > 0 && cyc_of<true>(sm.kt[sm.perm[0]], c.f) == 0) sm.cy.mode = 1;
          __syncthreads();
       }
-      else
+      const bool early = d.j > 0 || !sm.cy.mode;
+      if (early)
       {
          // FIFO aggregate of this chunk, published before looking back
          const uint32_t E = sm.E;
          const uint32_t per = (E + C2_T - 1) / C2_T;
          const uint32_t lo = min(tid * per, E), hi = min((tid + 1) * per, E);
          const ScanOut so = block_scan_seg(sm, lo, hi, io.dir, io.nx, io.ny, c);
-         if (tid == 0) publish_agg(st, flags, cidx, so.tA, so.tB, so.tc0, so.tc1);
-         if (wv == 0) lookback(sm, d.gbase, d.j, flags, st, errflag);
-         __syncthreads();
+         STAMP(4);
+         if (d.j > 0)
+         {
+            if (tid == 0) publish_agg(st, flags, cidx, so.tA, so.tB, so.tc0, so.tc1);
+            STAMP(5);
+            if (wv == 0) lookback(sm, d.gbase, d.j, flags, st, errflag);
+            __syncthreads();
+         }
+         STAMP(6);
+         // In FIFO mode the inclusive state is exclusive (x) aggregate: publish it now,
+         // before writing outputs, so successors stop waiting as early as possible.
+         if (tid == 0 && !sm.cy.mode)
+         {
+            Carry inc = sm.cy;
+            const uint64_t nx0 = inc.X + so.tA;
+            inc.X = nx0 > so.tB ? nx0 : so.tB;
+            for (uint32_t k = 0; k < 5; k++) inc.cnt[k] += get_dir(so.tc0, so.tc1, k);
+            publish_inc(st, flags, cidx, inc);
+            sm.published = 1;
+         }
       }
       process_leaf(sm, io, c, recs, samp_t, samp_id, nexc, slot_cnt, slot_base, final_ps);
+      STAMP(7);
    }
    else
    {
@@ -788,7 +815,9 @@ __global__ __launch_bounds__(C2_T) void k_chunk(DevCfg c, const ChunkDesc* __res
    // ---- publish inclusive state, per-port counters
    if (tid == 0)
    {
-      publish_inc(st, flags, cidx, sm.cy);
+      if (!sm.published) publish_inc(st, flags, cidx, sm.cy);
+      if (STAMPS && stamps) stamps[(uint64_t) sm.cid * 16 + 8] = __builtin_amdgcn_s_memtime();
+      if (STAMPS && stamps) stamps[(uint64_t) sm.cid * 16 + 9] = (uint64_t) d.j | ((uint64_t) io.dir << 32);
       atomicAdd(&port_sum[io.port], (unsigned long long) sm.st_sum);
       atomicAdd(&port_cnt[io.port], (unsigned long long) sm.st_cnt);
       if (sm.st_mg1) atomicAdd(&port_mg1[io.port], (unsigned long long) sm.st_mg1);

@@ -1,0 +1,43 @@
+"""Diagnostic: per-phase s_memtime stamps of the chunk kernel (GNOC_STAMPS=1).
+Prints median cycles per phase by port direction. Dev tool, not a test."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["GNOC_STAMPS"] = "1"
+from graphite_amd import gnoc  # noqa: E402
+
+mesh = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+ppt = int(sys.argv[2]) if len(sys.argv) > 2 else 10000
+tr = gnoc.synthetic_trace(mesh, mesh, 0.005, ppt, seed=1)
+eng = gnoc.Engine(gnoc.EngineConfig(num_tiles=mesh * mesh))
+eng.submit(tr)
+eng.run()
+lib = eng.lib
+lib.gnoc_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+n = ctypes.c_size_t()
+lib.gnoc_debug_stamps(eng._h, None, 0, ctypes.byref(n))
+buf = np.zeros(n.value * 16, np.uint64)
+lib.gnoc_debug_stamps(eng._h, buf.ctypes.data, buf.size, ctypes.byref(n))
+st = buf.reshape(-1, 16).astype(np.int64)
+j = st[:, 9] & 0xFFFFFFFF
+d = st[:, 9] >> 32
+names = ["dq->desc", "keys", "search", "load+merge", "aggscan", "publish_agg", "lookback", "process", "publish_inc"]
+print("chunks", st.shape[0], "summary", eng.summary())
+for dirn, label in ((5, "INJ"), (2, "RIGHT"), (1, "LEFT"), (4, "UP"), (3, "DOWN"), (0, "SELF")):
+    m = (d == dirn) & (j > 0) & (st[:, 7] > 0)
+    if not m.any():
+        continue
+    s = st[m]
+    out = []
+    for k in range(1, 9):
+        prev = k - 1
+        if k == 7 and True:
+            prev = 6
+        dd = s[:, k] - s[:, prev]
+        out.append(f"{names[k]}={int(np.median(dd))}")
+    tot = np.median(s[:, 8] - s[:, 0])
+    print(f"{label:6s} n={m.sum():6d} total={int(tot)} " + " ".join(out))
