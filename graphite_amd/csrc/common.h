@@ -16,8 +16,9 @@ enum : uint32_t { P_SELF = 0, P_LEFT = 1, P_RIGHT = 2, P_DOWN = 3, P_UP = 4, P_I
 enum : uint32_t { IN_LOCAL = 0, IN_W = 1, IN_E = 2, IN_S = 3, IN_N = 4, INS = 5 };
 
 // One hop record in HBM: the arrival of packet `id` at an output-port queue at
-// time `t` (picoseconds).  aux packs the destination tile (20 bits) and the
-// packet's flit count F (12 bits) so no gather is needed downstream.
+// time `t` (picoseconds).  aux packs the destination's mesh coordinates and the
+// packet's flit count F, so routing needs no division and no gather downstream:
+//   aux = dx | dy << 10 | F << 20      (W, H <= 1024, F <= 4095; checked at submit)
 struct __attribute__((aligned(16))) Rec
 {
    uint64_t t;
@@ -26,13 +27,19 @@ struct __attribute__((aligned(16))) Rec
 };
 static_assert(sizeof(Rec) == 16, "Rec must be 16 bytes");
 
-constexpr uint32_t AUX_DST_BITS = 20;
-constexpr uint32_t AUX_DST_MASK = (1u << AUX_DST_BITS) - 1;
-constexpr uint32_t AUX_F_MAX = (1u << (32 - AUX_DST_BITS)) - 1;
+constexpr uint32_t AUX_C_BITS = 10;
+constexpr uint32_t AUX_C_MASK = (1u << AUX_C_BITS) - 1;
+constexpr uint32_t AUX_F_SHIFT = 2 * AUX_C_BITS;
+constexpr uint32_t AUX_F_MAX = (1u << (32 - AUX_F_SHIFT)) - 1;
+constexpr uint32_t MESH_DIM_MAX = 1u << AUX_C_BITS;
 
-__host__ __device__ inline uint32_t aux_pack(uint32_t dst, uint32_t F) { return dst | (F << AUX_DST_BITS); }
-__host__ __device__ inline uint32_t aux_dst(uint32_t a) { return a & AUX_DST_MASK; }
-__host__ __device__ inline uint32_t aux_F(uint32_t a) { return a >> AUX_DST_BITS; }
+__host__ __device__ inline uint32_t aux_pack(uint32_t dx, uint32_t dy, uint32_t F)
+{
+   return dx | (dy << AUX_C_BITS) | (F << AUX_F_SHIFT);
+}
+__host__ __device__ inline uint32_t aux_dx(uint32_t a) { return a & AUX_C_MASK; }
+__host__ __device__ inline uint32_t aux_dy(uint32_t a) { return (a >> AUX_C_BITS) & AUX_C_MASK; }
+__host__ __device__ inline uint32_t aux_F(uint32_t a) { return a >> AUX_F_SHIFT; }
 
 __host__ __device__ inline uint32_t slot_of(uint32_t tile, uint32_t dir, uint32_t in)
 {

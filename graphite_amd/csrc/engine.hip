@@ -1,5 +1,16 @@
 // engine.hip -- host orchestration + C ABI (include/gnoc.h) of the MI355X
 // emesh_hop_by_hop timing engine.  Single translation unit with the kernels.
+//
+// A run is one fixed sequence of launches on the engine's stream:
+//   prep (prep.hip)   classify -> injection-slot layout -> stable scatter ->
+//                     row histograms -> slot counts -> slot bases
+//   plan (level.hip)  per-port descriptors and chunk -> port maps, on device
+//   levels            one persistent k_level launch per level of the port DAG
+//   finalize          zero-load / contention per packet
+// The v3 path never waits for the host between launches.  Configurations the
+// chunked path does not cover (f != 1 GHz, max_list_size <= 2) and the rare
+// overflow retry use the whole-port stream kernel of kernels.hip (v1), whose
+// plan is built on the host from the read-back slot counts.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -11,7 +22,8 @@
 
 #include "gnoc.h"
 #include "kernels.hip"
-#include "kernels_v2.hip"
+#include "level.hip"
+#include "prep.hip"
 
 using namespace gnoc;
 
@@ -40,13 +52,16 @@ struct DevBuf
    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-struct LevelPlan
-{
-   std::vector<uint32_t> ports;        // all levels concatenated
-   std::vector<uint32_t> off;          // level -> [off[l], off[l+1])
-};
-
 }  // namespace
+
+enum KernelClass
+{
+   KC_CLASSIFY, KC_SRC_TOT, KC_INJ_BASE, KC_SRC_OFFS, KC_SCATTER, KC_ROW_HIST, KC_PROW, KC_SLOT_COUNTS, KC_SCAN,
+   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_N
+};
+static const char* const kKernelNames[KC_N] = { "k_classify", "k_src_tot", "k_inj_base", "k_src_offs", "k_scatter",
+                                                "k_row_hist", "k_prow", "k_slot_counts", "k_scan_slots", "k_plan",
+                                                "k_level", "k_port_stream", "k_finalize" };
 
 struct gnoc_engine
 {
@@ -56,9 +71,15 @@ struct gnoc_engine
    hipStream_t stream = nullptr;
    hipEvent_t ev0 = nullptr, ev1 = nullptr;
    std::string err;
+   int level_grid = 0;
+
+   // static level plan of the port DAG (host + device copies)
+   std::vector<uint32_t> lvl_ports, lvl_off;
+   DevBuf d_lvl_ports, d_lvl_off;
 
    // trace
    size_t n = 0;
+   uint64_t rec_bound = 0;    // records incl. slot padding (from the trace at submit)
    bool submitted = false, ran = false;
    const uint64_t* d_inj = nullptr;
    const uint32_t *d_src = nullptr, *d_dst = nullptr, *d_bits = nullptr, *d_flags = nullptr;
@@ -66,13 +87,12 @@ struct gnoc_engine
 
    // work
    DevBuf aux, routed, final_ps, zl, cont;
-   DevBuf slot_cnt, slot_base, diff, counters;
-   DevBuf dirty, recs, port_sum, port_cnt, port_mg1;
-   DevBuf hist, offs, plan_ports;
-   DevBuf samp_t, samp_id, nexc, cflags, cstate, lctr, chunks, stamps, portio;
-   int force_v1 = 0;          // GNOC_ENGINE=v1, or set after a v2 overflow
-   int used_v2 = 0;
-   uint64_t h_chunks = 0;
+   DevBuf hist, tot, slot_cnt, slot_base, counters, gtot;
+   DevBuf recs, samp_t, samp_id, Hs, Pp, Prow, nexc, dirty;
+   DevBuf pio, pnc, pgb, lvl_cbase, chunk_port, flags, st, lvl_ctr;
+   DevBuf port_sum, port_cnt, port_mg1, plan_ports;
+   int force_v1 = 0;
+   int used_v3 = 0;
    std::vector<uint32_t> h_slot_cnt;
    uint64_t h_counters[2] = { 0, 0 };
    uint64_t h_records = 0;
@@ -83,16 +103,11 @@ struct gnoc_engine
    // kernel profiling (gnoc_set_profiling)
    bool prof = false;
    std::vector<hipEvent_t> evpool;
-   std::vector<int> evkid;     // kernel class per recorded launch
+   std::vector<int> evkid;
    size_t evused = 0;
-   double kms[16] = {};
-   uint32_t klaunch[16] = {};
+   double kms[KC_N] = {};
+   uint32_t klaunch[KC_N] = {};
 };
-
-enum KernelClass { KC_CLASSIFY, KC_CHAIN, KC_SCAN, KC_INJ_COUNT, KC_INJ_OFFS, KC_INJ_SCATTER, KC_PORT, KC_FINALIZE, KC_INJ_SAMPLES, KC_CHUNK, KC_N };
-static const char* const kKernelNames[KC_N] = { "k_classify", "k_chain_prefix", "k_scan_slots", "k_inj_group<count>",
-                                                "k_inj_offsets", "k_inj_group<scatter>", "k_port_stream", "k_finalize",
-                                                "k_inj_samples", "k_chunk" };
 
 static hipError_t prof_mark(gnoc_engine* e, int kid)
 {
@@ -113,16 +128,6 @@ static hipError_t prof_end(gnoc_engine* e)
    return hipEventRecord(e->evpool[e->evused++], e->stream);
 }
 
-// Launch with optional start/end events (kernel class kid).
-#define GNOC_LAUNCH(eng, kid, ...)                                     \
-   do                                                                  \
-   {                                                                   \
-      GNOC_HIP(eng, prof_mark(eng, kid));                              \
-      hipLaunchKernelGGL(__VA_ARGS__);                                 \
-      GNOC_HIP(eng, hipGetLastError());                                \
-      GNOC_HIP(eng, prof_end(eng));                                    \
-   } while (0)
-
 #define GNOC_HIP(eng, call)                                                                           \
    do                                                                                                 \
    {                                                                                                  \
@@ -132,6 +137,16 @@ static hipError_t prof_end(gnoc_engine* e)
          (eng)->err = std::string(#call) + ": " + hipGetErrorString(e_);                              \
          return GNOC_EHIP;                                                                            \
       }                                                                                               \
+   } while (0)
+
+// Launch with optional start/end events (kernel class kid).
+#define GNOC_LAUNCH(eng, kid, ...)                                     \
+   do                                                                  \
+   {                                                                   \
+      GNOC_HIP(eng, prof_mark(eng, kid));                              \
+      hipLaunchKernelGGL(__VA_ARGS__);                                 \
+      GNOC_HIP(eng, hipGetLastError());                                \
+      GNOC_HIP(eng, prof_end(eng));                                    \
    } while (0)
 
 static hipError_t prof_collect(gnoc_engine* e)
@@ -153,6 +168,41 @@ static int fail(gnoc_engine* e, int code, const std::string& msg)
 {
    if (e) e->err = msg;
    return code;
+}
+
+// Levels of the output-port DAG under XY routing: injection ports; X levels
+// (RIGHT at x = l-1, LEFT at x = W-l, every row); Y levels (UP at y = k, DOWN at
+// y = H-1-k, every column); SELF ports.  Every port's producers sit in earlier levels.
+static void build_static_levels(gnoc_engine* e)
+{
+   const uint32_t W = e->dc.W, H = e->dc.H, N = e->dc.N;
+   auto& P = e->lvl_ports;
+   auto& O = e->lvl_off;
+   P.clear();
+   O.clear();
+   O.push_back(0);
+   for (uint32_t t = 0; t < N; t++) P.push_back(t * PORTS + P_INJ);
+   O.push_back((uint32_t) P.size());
+   for (uint32_t l = 1; l < W; l++)
+   {
+      for (uint32_t y = 0; y < H; y++)
+      {
+         P.push_back((y * W + (l - 1)) * PORTS + P_RIGHT);
+         P.push_back((y * W + (W - l)) * PORTS + P_LEFT);
+      }
+      O.push_back((uint32_t) P.size());
+   }
+   for (uint32_t k = 0; k + 1 < H; k++)
+   {
+      for (uint32_t x = 0; x < W; x++)
+      {
+         P.push_back((k * W + x) * PORTS + P_UP);
+         P.push_back(((H - 1 - k) * W + x) * PORTS + P_DOWN);
+      }
+      O.push_back((uint32_t) P.size());
+   }
+   for (uint32_t t = 0; t < N; t++) P.push_back(t * PORTS + P_SELF);
+   O.push_back((uint32_t) P.size());
 }
 
 extern "C" {
@@ -192,7 +242,8 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    }
    if (c.num_tiles <= 0) c.num_tiles = c.mesh_width * c.mesh_height;
    if (c.num_tiles != c.mesh_width * c.mesh_height) return GNOC_EINVAL;   // :56-58
-   if (c.num_tiles > (1 << 15)) return GNOC_EUNSUPPORTED;
+   if (c.num_tiles > (1 << 14)) return GNOC_EUNSUPPORTED;
+   if (c.mesh_width > (int32_t) MESH_DIM_MAX || c.mesh_height > (int32_t) MESH_DIM_MAX) return GNOC_EUNSUPPORTED;
    if (c.flit_width <= 0) return GNOC_EINVAL;                             // computeNumFlits(-1) = 0 flits
    if (!(c.frequency_ghz > 0.0)) return GNOC_EINVAL;
    // ElectricalLinkModel delay, electrical_link_model.cc:13-16, asserted at emesh_hop_by_hop.cc:126
@@ -219,17 +270,28 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    d.analytical = c.analytical_enabled;
    d.max_list = c.max_list_size;
    d.magicW = d.W == 1 ? 0xFFFFFFFFu : (uint32_t) ((1ull << 32) / d.W);
+   build_static_levels(e);
 
    hipError_t he = hipSetDevice(c.device);
    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
    if (he == hipSuccess) he = hipEventCreate(&e->ev0);
    if (he == hipSuccess) he = hipEventCreate(&e->ev1);
    if (he == hipSuccess) he = hipHostMalloc((void**) &e->h_pinned, 64, hipHostMallocDefault);
+   if (he == hipSuccess) he = e->d_lvl_ports.ensure(e->lvl_ports.size() * 4);
+   if (he == hipSuccess) he = e->d_lvl_off.ensure(e->lvl_off.size() * 4);
+   if (he == hipSuccess)
+      he = hipMemcpy(e->d_lvl_ports.p, e->lvl_ports.data(), e->lvl_ports.size() * 4, hipMemcpyHostToDevice);
+   if (he == hipSuccess) he = hipMemcpy(e->d_lvl_off.p, e->lvl_off.data(), e->lvl_off.size() * 4, hipMemcpyHostToDevice);
+   if (he == hipSuccess)
+   {
+      int per_cu = 0, cus = 0;
+      he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_level, LV_T, 0);
+      if (he == hipSuccess) he = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
+      e->level_grid = std::max(1, per_cu) * std::max(1, cus);
+   }
    if (he != hipSuccess)
    {
-      std::string msg = std::string("HIP init failed: ") + hipGetErrorString(he);
       gnoc_destroy(e);
-      (void) msg;
       return GNOC_EHIP;
    }
    *out = e;
@@ -251,18 +313,34 @@ void gnoc_destroy(gnoc_engine* e)
 
 const char* gnoc_last_error(const gnoc_engine* e) { return e ? e->err.c_str() : "null engine"; }
 
-static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n)
+// Records the batch materialises: one per injection + one per mesh router
+// traversal, plus per-slot 64-record alignment.  Route-static, so known at submit.
+static uint64_t record_bound(const gnoc_engine* e, uint64_t records)
 {
-   const uint32_t N = e->dc.N;
+   return records + 64ull * ((uint64_t) e->dc.N * PORTS * INS) + 64;
+}
+
+static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n, uint64_t* records)
+{
+   const uint32_t N = e->dc.N, W = e->dc.W;
+   uint64_t rec = 0;
    for (size_t i = 0; i < n; i++)
    {
-      if (pk->src[i] >= N || pk->dst[i] >= N) return fail(e, GNOC_ETRACE, "tile id out of range at packet " + std::to_string(i));
+      const uint32_t s = pk->src[i], d = pk->dst[i];
+      if (s >= N || d >= N) return fail(e, GNOC_ETRACE, "tile id out of range at packet " + std::to_string(i));
       if (i && pk->inject_ps[i] < pk->inject_ps[i - 1]) return fail(e, GNOC_ETRACE, "trace not ordered by inject_ps at packet " + std::to_string(i));
       const uint32_t F = (pk->bits[i] + (uint32_t) e->cfg.flit_width - 1) / (uint32_t) e->cfg.flit_width;
-      if (F == 0 && pk->src[i] != pk->dst[i]) return fail(e, GNOC_ETRACE, "zero-flit packet " + std::to_string(i));
+      const bool bypass = s == d || (pk->flags && (pk->flags[i] & GNOC_PKT_UNMODELED));
+      if (F == 0 && !bypass) return fail(e, GNOC_ETRACE, "zero-flit packet " + std::to_string(i));
       if (F > AUX_F_MAX) return fail(e, GNOC_EUNSUPPORTED, "packet longer than 4095 flits");
+      if (!bypass)
+      {
+         const int64_t sx = s % W, sy = s / W, dx = d % W, dy = d / W;
+         rec += 2 + (uint64_t) (std::llabs(sx - dx) + std::llabs(sy - dy));
+      }
    }
    if (n && pk->inject_ps[n - 1] >= (1ull << 50)) return fail(e, GNOC_EUNSUPPORTED, "inject time beyond 2^50 ps");
+   *records = rec;
    return GNOC_OK;
 }
 
@@ -271,8 +349,10 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    if (!e || !pk) return GNOC_EINVAL;
    if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return fail(e, GNOC_EINVAL, "null trace array");
    if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
-   int rc = validate_host_trace(e, pk, n);
+   uint64_t records = 0;
+   int rc = validate_host_trace(e, pk, n, &records);
    if (rc) return rc;
+   if (record_bound(e, records) >= (1ull << 32)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32 hop records");
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    GNOC_HIP(e, e->t_inj.ensure(n * 8));
    GNOC_HIP(e, e->t_src.ensure(n * 4));
@@ -297,6 +377,7 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    e->d_bits = e->t_bits.as<uint32_t>();
    e->d_flags = e->t_flags.as<uint32_t>();
    e->n = n;
+   e->rec_bound = record_bound(e, records);
    e->submitted = true;
    e->ran = false;
    return GNOC_OK;
@@ -313,214 +394,120 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    e->d_bits = pk->bits;
    e->d_flags = pk->flags;
    e->n = n;
+   // size the record buffers from the trace (route-static): classify once now
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   GNOC_HIP(e, e->counters.ensure(64));
+   GNOC_HIP(e, e->aux.ensure(n * 4 + 4));
+   GNOC_HIP(e, e->routed.ensure(n + 4));
+   GNOC_HIP(e, e->final_ps.ensure(n * 8 + 8));
+   const uint32_t N = e->dc.N;
+   const uint32_t pch = std::max<uint32_t>(16384u, (4u * N + 63u) & ~63u);
+   const uint32_t nch = (uint32_t) std::max<uint64_t>(1, (n + pch - 1) / pch);
+   GNOC_HIP(e, e->hist.ensure((size_t) nch * N * 4));
+   GNOC_HIP(e, hipMemsetAsync(e->counters.p, 0, 64, e->stream));
+   hipLaunchKernelGGL(k_classify, dim3(nch), dim3(256), N * 4, e->stream, e->dc, (uint64_t) n, pch, e->d_inj, e->d_src,
+                         e->d_dst, e->d_bits, e->d_flags, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(),
+                         e->final_ps.as<uint64_t>(), e->hist.as<uint32_t>(), e->counters.as<unsigned long long>());
+   GNOC_HIP(e, hipGetLastError());
+   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 16, hipMemcpyDeviceToHost, e->stream));
+   GNOC_HIP(e, hipStreamSynchronize(e->stream));
+   const uint64_t records = e->h_pinned[0] + e->h_pinned[1];
+   if (record_bound(e, records) >= (1ull << 32)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32 hop records");
+   e->rec_bound = record_bound(e, records);
    e->submitted = true;
    e->ran = false;
    return GNOC_OK;
 }
 
-static void build_plan(const gnoc_engine* e, LevelPlan& lp)
-{
-   const uint32_t W = e->dc.W, H = e->dc.H, N = e->dc.N;
-   const std::vector<uint32_t>& cnt = e->h_slot_cnt;
-   auto nonempty = [&](uint32_t port) {
-      for (uint32_t in = 0; in < INS; in++)
-         if (cnt[port * INS + in]) return true;
-      return false;
-   };
-   lp.ports.clear();
-   lp.off.clear();
-   auto push_level = [&](const std::vector<uint32_t>& v) {
-      lp.off.push_back((uint32_t) lp.ports.size());
-      for (uint32_t p : v)
-         if (nonempty(p)) lp.ports.push_back(p);
-   };
-   std::vector<uint32_t> v;
-   // level 0: injection ports
-   v.clear();
-   for (uint32_t t = 0; t < N; t++) v.push_back(t * PORTS + P_INJ);
-   push_level(v);
-   // X levels 1..W-1: RIGHT at x = l-1, LEFT at x = W-l (all rows)
-   for (uint32_t l = 1; l < W; l++)
-   {
-      v.clear();
-      for (uint32_t y = 0; y < H; y++)
-      {
-         v.push_back((y * W + (l - 1)) * PORTS + P_RIGHT);
-         v.push_back((y * W + (W - l)) * PORTS + P_LEFT);
-      }
-      push_level(v);
-   }
-   // Y levels: UP at y = k, DOWN at y = H-1-k
-   for (uint32_t k = 0; k + 1 < H; k++)
-   {
-      v.clear();
-      for (uint32_t x = 0; x < W; x++)
-      {
-         v.push_back((k * W + x) * PORTS + P_UP);
-         v.push_back(((H - 1 - k) * W + x) * PORTS + P_DOWN);
-      }
-      push_level(v);
-   }
-   // SELF level
-   v.clear();
-   for (uint32_t t = 0; t < N; t++) v.push_back(t * PORTS + P_SELF);
-   push_level(v);
-   lp.off.push_back((uint32_t) lp.ports.size());
-}
-
-
-constexpr int GNOC_V2_RETRY = 1000;
-
+// ---------------------------------------------------------------------------
+// v1: whole-port streams, host-built plan (f != 1 GHz, max_list_size <= 2, retries)
+// ---------------------------------------------------------------------------
 static int run_levels_v1(gnoc_engine* e)
 {
    const DevCfg& c = e->dc;
    hipStream_t s = e->stream;
-   LevelPlan lp;
-   build_plan(e, lp);
-   GNOC_HIP(e, e->plan_ports.ensure(std::max<size_t>(1, lp.ports.size()) * 4));
-   if (!lp.ports.empty())
-      GNOC_HIP(e, hipMemcpyAsync(e->plan_ports.p, lp.ports.data(), lp.ports.size() * 4, hipMemcpyHostToDevice, s));
-   e->h_levels = (uint32_t) (lp.off.size() - 1);
-   for (size_t l = 0; l + 1 < lp.off.size(); l++)
+   const uint32_t nslots = c.N * PORTS * INS;
+   e->h_slot_cnt.resize(nslots);
+   GNOC_HIP(e, hipMemcpyAsync(e->h_slot_cnt.data(), e->slot_cnt.p, (size_t) nslots * 4, hipMemcpyDeviceToHost, s));
+   GNOC_HIP(e, hipStreamSynchronize(s));
+   std::vector<uint32_t> ports, off;
+   for (size_t l = 0; l + 1 < e->lvl_off.size(); l++)
    {
-      const uint32_t cnt = lp.off[l + 1] - lp.off[l];
+      off.push_back((uint32_t) ports.size());
+      for (uint32_t k = e->lvl_off[l]; k < e->lvl_off[l + 1]; k++)
+      {
+         const uint32_t p = e->lvl_ports[k];
+         bool any = false;
+         for (uint32_t in = 0; in < INS; in++) any |= e->h_slot_cnt[p * INS + in] != 0;
+         if (any) ports.push_back(p);
+      }
+   }
+   off.push_back((uint32_t) ports.size());
+   GNOC_HIP(e, e->plan_ports.ensure(std::max<size_t>(1, ports.size()) * 4));
+   if (!ports.empty())
+      GNOC_HIP(e, hipMemcpyAsync(e->plan_ports.p, ports.data(), ports.size() * 4, hipMemcpyHostToDevice, s));
+   GNOC_HIP(e, e->dirty.ensure((size_t) nslots * 4));
+   GNOC_HIP(e, hipMemsetAsync(e->dirty.p, 0, (size_t) nslots * 4, s));
+   e->h_levels = (uint32_t) (off.size() - 1);
+   for (size_t l = 0; l + 1 < off.size(); l++)
+   {
+      const uint32_t cnt = off[l + 1] - off[l];
       if (!cnt) continue;
-      const uint32_t* ports = e->plan_ports.as<uint32_t>() + lp.off[l];
+      const uint32_t* pp = e->plan_ports.as<uint32_t>() + off[l];
       if (e->f1)
-         GNOC_LAUNCH(e, KC_PORT, k_port_stream<true>, dim3(cnt), dim3(STHREADS), 0, s, c, ports, e->slot_cnt.as<uint32_t>(),
-                            e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
-                            e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
-                            e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
+         GNOC_LAUNCH(e, KC_PORT, k_port_stream<true>, dim3(cnt), dim3(STHREADS), 0, s, c, pp, e->slot_cnt.as<uint32_t>(),
+                     e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
+                     e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
+                     e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
       else
-         GNOC_LAUNCH(e, KC_PORT, k_port_stream<false>, dim3(cnt), dim3(STHREADS), 0, s, c, ports, e->slot_cnt.as<uint32_t>(),
-                            e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
-                            e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
-                            e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
+         GNOC_LAUNCH(e, KC_PORT, k_port_stream<false>, dim3(cnt), dim3(STHREADS), 0, s, c, pp, e->slot_cnt.as<uint32_t>(),
+                     e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
+                     e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
+                     e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
    }
    return GNOC_OK;
 }
 
-static int run_levels_v2(gnoc_engine* e)
+// ---------------------------------------------------------------------------
+// v3: device-planned chunked levels
+// ---------------------------------------------------------------------------
+static int run_levels_v3(gnoc_engine* e)
 {
    const DevCfg& c = e->dc;
    hipStream_t s = e->stream;
-   const uint32_t N = c.N;
-   const uint32_t nslots = N * PORTS * INS;
-   LevelPlan lp;
-   build_plan(e, lp);
-   const size_t nlev = lp.off.size() - 1;
-   e->h_levels = (uint32_t) nlev;
-   // slot bases exactly as k_scan_slots lays them out (64-record aligned)
-   std::vector<uint64_t> hbase((size_t) nslots + 1);
-   {
-      uint64_t run = 0;
-      for (uint32_t i = 0; i < nslots; i++) { hbase[i] = run; run += (e->h_slot_cnt[i] + 63) & ~63u; }
-      hbase[nslots] = run;
-   }
-   // port descriptions + chunk plan: ~C2_TARGET records per chunk, cut on the port's largest input
-   std::vector<PortIO> pio;
-   std::vector<ChunkDesc> ch;
-   std::vector<uint32_t> choff(nlev + 1, 0);
-   uint32_t g = 0;
-   for (size_t l = 0; l < nlev; l++)
-   {
-      choff[l] = (uint32_t) ch.size();
-      for (uint32_t k = lp.off[l]; k < lp.off[l + 1]; k++)
-      {
-         const uint32_t port = lp.ports[k];
-         PortIO io;
-         std::memset(&io, 0, sizeof(io));
-         io.port = port;
-         io.tile = port / PORTS;
-         io.dir = port % PORTS;
-         uint64_t tot = 0;
-         for (uint32_t in = 0; in < INS; in++)
-         {
-            const uint32_t sl = port * INS + in;
-            const uint32_t n = e->h_slot_cnt[sl];
-            tot += n;
-            if (n && io.nin < C2_IN)
-            {
-               io.slot[io.nin] = sl;
-               io.base[io.nin] = hbase[sl];
-               io.cnt[io.nin] = n;
-               io.nmain[io.nin] = n;
-               if (n > io.cnt[io.sb]) io.sb = io.nin;
-               io.nin++;
-            }
-         }
-         io.ntile = io.tile;
-         io.nside = IN_LOCAL;
-         if (io.dir == P_RIGHT) { io.ntile = io.tile + 1; io.nside = IN_W; }
-         else if (io.dir == P_LEFT) { io.ntile = io.tile - 1; io.nside = IN_E; }
-         else if (io.dir == P_UP) { io.ntile = io.tile + c.W; io.nside = IN_S; }
-         else if (io.dir == P_DOWN) { io.ntile = io.tile - c.W; io.nside = IN_N; }
-         io.nx = io.ntile % c.W;
-         io.ny = io.ntile / c.W;
-         for (uint32_t d = 0; d < 5; d++)
-         {
-            const uint32_t os = slot_of(io.ntile, d, io.nside);
-            io.oslot[d] = os;
-            io.obase[d] = io.dir == P_SELF ? 0 : hbase[os];
-            io.ocnt[d] = io.dir == P_SELF ? 0 : e->h_slot_cnt[os];
-         }
-         const uint32_t pidx = (uint32_t) pio.size();
-         pio.push_back(io);
-         const uint32_t nc = (uint32_t) std::max<uint64_t>(1, (tot + C2_TARGET - 1) / C2_TARGET);
-         for (uint32_t j = 0; j < nc; j++) ch.push_back(ChunkDesc{ pidx, j, nc, g });
-         g += nc;
-      }
-   }
-   choff[nlev] = (uint32_t) ch.size();
-   e->h_chunks = ch.size();
-   GNOC_HIP(e, e->portio.ensure(std::max<size_t>(1, pio.size()) * sizeof(PortIO)));
-   if (!pio.empty())
-      GNOC_HIP(e, hipMemcpyAsync(e->portio.p, pio.data(), pio.size() * sizeof(PortIO), hipMemcpyHostToDevice, s));
-   const uint64_t total = e->h_records;
-   GNOC_HIP(e, e->samp_t.ensure((total / 64 + 1) * 8));
-   GNOC_HIP(e, e->samp_id.ensure((total / 64 + 1) * 4));
-   GNOC_HIP(e, e->nexc.ensure((size_t) nslots * 4));
-   GNOC_HIP(e, e->cflags.ensure(std::max<size_t>(1, ch.size()) * 4));
-   GNOC_HIP(e, e->cstate.ensure(std::max<size_t>(1, ch.size()) * 16 * 8));
-   GNOC_HIP(e, e->lctr.ensure(std::max<size_t>(1, nlev) * 4));
-   GNOC_HIP(e, e->chunks.ensure(std::max<size_t>(1, ch.size()) * sizeof(ChunkDesc)));
-   GNOC_HIP(e, hipMemsetAsync(e->nexc.p, 0, (size_t) nslots * 4, s));
-   GNOC_HIP(e, hipMemsetAsync(e->cflags.p, 0, std::max<size_t>(1, ch.size()) * 4, s));
-   GNOC_HIP(e, hipMemsetAsync(e->lctr.p, 0, std::max<size_t>(1, nlev) * 4, s));
-   if (!ch.empty())
-      GNOC_HIP(e, hipMemcpyAsync(e->chunks.p, ch.data(), ch.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice, s));
-   if (e->n)
-      GNOC_LAUNCH(e, KC_INJ_SAMPLES, k_inj_samples, dim3(N), dim3(256), 0, s, N, e->slot_cnt.as<uint32_t>(),
-                  e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>());
-   const char* stv = std::getenv("GNOC_STAMPS");
-   const bool stamps = stv && *stv == '1';
-   if (stamps)
-   {
-      GNOC_HIP(e, e->stamps.ensure(std::max<size_t>(1, ch.size()) * 16 * 8));
-      GNOC_HIP(e, hipMemsetAsync(e->stamps.p, 0, std::max<size_t>(1, ch.size()) * 16 * 8, s));
-   }
-   for (size_t l = 0; l < nlev; l++)
-   {
-      const uint32_t cnt = choff[l + 1] - choff[l];
-      if (!cnt) continue;
-      uint64_t* sp = stamps ? e->stamps.as<uint64_t>() + (uint64_t) choff[l] * 16 : nullptr;
-      if (stamps)
-      GNOC_LAUNCH(e, KC_CHUNK, k_chunk<true>, dim3(cnt), dim3(C2_T), 0, s, c, e->chunks.as<ChunkDesc>() + choff[l], e->portio.as<PortIO>(),
-                  e->lctr.as<unsigned>() + l, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->recs.as<Rec>(),
-                  e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(), e->cflags.as<uint32_t>(),
-                  e->cstate.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
+   const uint32_t P = (uint32_t) e->lvl_ports.size();
+   const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
+   const uint64_t chunk_bound = e->rec_bound / LV_CTGT + P + 1;
+   GNOC_HIP(e, e->pio.ensure((size_t) P * sizeof(PortIO3)));
+   GNOC_HIP(e, e->pnc.ensure((size_t) P * 4));
+   GNOC_HIP(e, e->pgb.ensure((size_t) P * 4));
+   GNOC_HIP(e, e->lvl_cbase.ensure((size_t) (L + 1) * 4));
+   GNOC_HIP(e, e->chunk_port.ensure(chunk_bound * 4));
+   GNOC_HIP(e, e->flags.ensure(chunk_bound * 4));
+   GNOC_HIP(e, e->st.ensure(chunk_bound * 16 * 8));
+   GNOC_HIP(e, e->lvl_ctr.ensure((size_t) L * 4));
+   GNOC_HIP(e, hipMemsetAsync(e->flags.p, 0, chunk_bound * 4, s));
+   GNOC_HIP(e, hipMemsetAsync(e->lvl_ctr.p, 0, (size_t) L * 4, s));
+   const uint32_t pg = (P + 255) / 256;
+   GNOC_LAUNCH(e, KC_PLAN, k_plan_ports, dim3(pg), dim3(256), 0, s, c, P, e->d_lvl_ports.as<uint32_t>(),
+               e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
+               LV_CTGT);
+   GNOC_LAUNCH(e, KC_PLAN, k_plan_scan, dim3(1), dim3(1024), 0, s, P, L, e->d_lvl_off.as<uint32_t>(),
+               e->pnc.as<uint32_t>(), e->pgb.as<uint32_t>(), e->lvl_cbase.as<uint32_t>());
+   GNOC_LAUNCH(e, KC_PLAN, k_plan_expand, dim3(pg), dim3(256), 0, s, P, e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
+               e->pgb.as<uint32_t>(), e->chunk_port.as<uint32_t>());
+   e->h_levels = L;
+   for (uint32_t l = 0; l < L; l++)
+      GNOC_LAUNCH(e, KC_LEVEL, k_level, dim3(e->level_grid), dim3(LV_T), 0, s, c, l, e->lvl_cbase.as<uint32_t>(),
+                  e->lvl_ctr.as<unsigned>(), e->chunk_port.as<uint32_t>(), e->pio.as<PortIO3>(), e->recs.as<Rec>(),
+                  e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(), e->flags.as<uint32_t>(),
+                  e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
                   e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
-                  e->counters.as<unsigned>() + 8, sp);
-      else
-      GNOC_LAUNCH(e, KC_CHUNK, k_chunk<false>, dim3(cnt), dim3(C2_T), 0, s, c, e->chunks.as<ChunkDesc>() + choff[l], e->portio.as<PortIO>(),
-                  e->lctr.as<unsigned>() + l, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->recs.as<Rec>(),
-                  e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(), e->cflags.as<uint32_t>(),
-                  e->cstate.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
-                  e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
-                  e->counters.as<unsigned>() + 8, (uint64_t*) nullptr);
-   }
+                  e->counters.as<unsigned>() + 8);
    return GNOC_OK;
 }
+
+constexpr int GNOC_V3_RETRY = 1000;
 
 static int run_once(gnoc_engine* e)
 {
@@ -529,22 +516,38 @@ static int run_once(gnoc_engine* e)
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    const DevCfg& c = e->dc;
    const size_t n = e->n;
-   const uint32_t N = c.N;
+   const uint32_t N = c.N, W = c.W, H = c.H;
    const uint32_t nslots = N * PORTS * INS;
    const size_t nports = (size_t) N * PORTS;
    hipStream_t s = e->stream;
+   const uint32_t pch = std::max<uint32_t>(16384u, (4u * N + 63u) & ~63u);
+   const uint32_t nch = (uint32_t) std::max<uint64_t>(1, (n + pch - 1) / pch);
+   int nbits = 0;
+   while ((1u << nbits) < N) nbits++;
+   // row-histogram grouping: ~512 workgroups, LDS per group <= 32 KiB of source bins
+   uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(W, 512 / H));
+   while (G < W && (W / G + 1) * W * 3 > 8192) G++;
+   const int pp_lds = N <= 8192;
+   size_t rh_lds = (size_t) ((W + G - 1) / G) * W * 3 * 4 + (pp_lds ? (size_t) N * 4 : 0);
 
-   GNOC_HIP(e, e->aux.ensure(n * 4));
-   GNOC_HIP(e, e->routed.ensure(n));
-   GNOC_HIP(e, e->final_ps.ensure(n * 8));
-   GNOC_HIP(e, e->zl.ensure(n * 8));
-   GNOC_HIP(e, e->cont.ensure(n * 8));
+   GNOC_HIP(e, e->aux.ensure(n * 4 + 4));
+   GNOC_HIP(e, e->routed.ensure(n + 4));
+   GNOC_HIP(e, e->final_ps.ensure(n * 8 + 8));
+   GNOC_HIP(e, e->zl.ensure(n * 8 + 8));
+   GNOC_HIP(e, e->cont.ensure(n * 8 + 8));
+   GNOC_HIP(e, e->hist.ensure((size_t) nch * N * 4));
+   GNOC_HIP(e, e->tot.ensure((size_t) N * 4));
    GNOC_HIP(e, e->slot_cnt.ensure((size_t) nslots * 4));
    GNOC_HIP(e, e->slot_base.ensure(((size_t) nslots + 1) * 8));
-   const size_t ndiff = 2 * (size_t) c.H * (c.W + 1) + 2 * (size_t) c.W * (c.H + 1);
-   GNOC_HIP(e, e->diff.ensure(ndiff * 4));
    GNOC_HIP(e, e->counters.ensure(64));
-   GNOC_HIP(e, e->dirty.ensure((size_t) nslots * 4));
+   GNOC_HIP(e, e->gtot.ensure(16));
+   GNOC_HIP(e, e->recs.ensure(e->rec_bound * sizeof(Rec)));
+   GNOC_HIP(e, e->samp_t.ensure((e->rec_bound / 64 + 1) * 8));
+   GNOC_HIP(e, e->samp_id.ensure((e->rec_bound / 64 + 1) * 4));
+   GNOC_HIP(e, e->Hs.ensure((size_t) N * W * 3 * 4));
+   GNOC_HIP(e, e->Pp.ensure((size_t) H * G * N * 4));
+   GNOC_HIP(e, e->Prow.ensure((size_t) H * N * 4));
+   GNOC_HIP(e, e->nexc.ensure((size_t) nslots * 4));
    GNOC_HIP(e, e->port_sum.ensure(nports * 8));
    GNOC_HIP(e, e->port_cnt.ensure(nports * 8));
    GNOC_HIP(e, e->port_mg1.ensure(nports * 8));
@@ -552,20 +555,19 @@ static int run_once(gnoc_engine* e)
    e->evused = 0;
    e->evkid.clear();
    GNOC_HIP(e, hipEventRecord(e->ev0, s));
-   GNOC_HIP(e, hipMemsetAsync(e->slot_cnt.p, 0, (size_t) nslots * 4, s));
-   GNOC_HIP(e, hipMemsetAsync(e->diff.p, 0, ndiff * 4, s));
    GNOC_HIP(e, hipMemsetAsync(e->counters.p, 0, 64, s));
-   GNOC_HIP(e, hipMemsetAsync(e->dirty.p, 0, (size_t) nslots * 4, s));
+   GNOC_HIP(e, hipMemsetAsync(e->slot_cnt.p, 0, (size_t) nslots * 4, s));
+   GNOC_HIP(e, hipMemsetAsync(e->nexc.p, 0, (size_t) nslots * 4, s));
    GNOC_HIP(e, hipMemsetAsync(e->port_sum.p, 0, nports * 8, s));
    GNOC_HIP(e, hipMemsetAsync(e->port_cnt.p, 0, nports * 8, s));
    GNOC_HIP(e, hipMemsetAsync(e->port_mg1.p, 0, nports * 8, s));
+   if (!pp_lds) GNOC_HIP(e, hipMemsetAsync(e->Pp.p, 0, (size_t) H * G * N * 4, s));
 
-   const uint32_t cls_grid = (uint32_t) std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 8192));
-   if (n)
-      GNOC_LAUNCH(e, KC_CLASSIFY, k_classify, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src, e->d_dst,
-                         e->d_bits, e->d_flags, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
-                         e->slot_cnt.as<uint32_t>(), e->diff.as<int32_t>(), e->counters.as<unsigned long long>());
-   GNOC_HIP(e, hipGetLastError());
+   // always launched: for an empty batch it writes the all-zero source histogram
+   GNOC_LAUNCH(e, KC_CLASSIFY, k_classify, dim3(nch), dim3(256), N * 4, s, c, (uint64_t) n, pch, e->d_inj, e->d_src,
+                  e->d_dst, e->d_bits, e->d_flags, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(),
+                  e->final_ps.as<uint64_t>(), e->hist.as<uint32_t>(), e->counters.as<unsigned long long>());
+   const uint32_t fin_grid = (uint32_t) std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 8192));
 
    if (!c.contention)
    {
@@ -573,15 +575,14 @@ static int run_once(gnoc_engine* e)
       if (n)
       {
          if (e->f1)
-            GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<true>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
-                               e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
-                               e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), 1);
+            GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<true>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
+                        e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
+                        e->cont.as<uint64_t>(), 1);
          else
-            GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<false>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
-                               e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
-                               e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), 1);
+            GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<false>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj,
+                        e->d_src, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
+                        e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), 1);
       }
-      GNOC_HIP(e, hipGetLastError());
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 16, hipMemcpyDeviceToHost, s));
       GNOC_HIP(e, hipEventRecord(e->ev1, s));
       GNOC_HIP(e, hipStreamSynchronize(s));
@@ -592,83 +593,67 @@ static int run_once(gnoc_engine* e)
       float ms = 0;
       GNOC_HIP(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
       e->last_ms = ms;
+      GNOC_HIP(e, prof_collect(e));
+      e->used_v3 = 0;
       e->ran = true;
       return GNOC_OK;
    }
 
-   GNOC_LAUNCH(e, KC_CHAIN, k_chain_prefix, dim3((c.W + c.H + 255) / 256), dim3(256), 0, s, c, e->diff.as<int32_t>(),
-                      e->slot_cnt.as<uint32_t>());
-   GNOC_LAUNCH(e, KC_SCAN, k_scan_slots, dim3(1), dim3(1024), 0, s, nslots, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>());
-   GNOC_HIP(e, hipGetLastError());
-
-   // read back slot counts (route-static layout) and the record total
-   e->h_slot_cnt.resize(nslots);
-   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->slot_base.as<uint64_t>() + nslots, 8, hipMemcpyDeviceToHost, s));
-   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 1, e->counters.p, 16, hipMemcpyDeviceToHost, s));
-   GNOC_HIP(e, hipMemcpyAsync(e->h_slot_cnt.data(), e->slot_cnt.p, (size_t) nslots * 4, hipMemcpyDeviceToHost, s));
-   GNOC_HIP(e, hipStreamSynchronize(s));
-   const uint64_t total = e->h_pinned[0];
-   e->h_counters[0] = e->h_pinned[1];
-   e->h_counters[1] = e->h_pinned[2];
-   e->h_records = total;
-   GNOC_HIP(e, e->recs.ensure(total * sizeof(Rec)));
-
-   // injection grouping
+   const uint32_t ng = (N + 255) / 256;
+   GNOC_LAUNCH(e, KC_SRC_TOT, k_src_tot, dim3(ng), dim3(256), 0, s, N, nch, e->hist.as<uint32_t>(), e->tot.as<uint32_t>());
+   GNOC_LAUNCH(e, KC_INJ_BASE, k_inj_base, dim3(1), dim3(1024), 0, s, N, e->tot.as<uint32_t>(), e->slot_cnt.as<uint32_t>(),
+               e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>());
+   GNOC_LAUNCH(e, KC_SRC_OFFS, k_src_offs, dim3(ng), dim3(256), 0, s, N, nch, e->hist.as<uint32_t>(),
+               e->slot_base.as<uint64_t>());
    if (n)
-   {
-      uint32_t chunk = 4096;
-      while ((n + chunk - 1) / chunk * (uint64_t) N > (64ull << 20)) chunk *= 2;
-      const uint32_t nchunks = (uint32_t) ((n + chunk - 1) / chunk);
-      int nbits = 0;
-      while ((1u << nbits) < N) nbits++;
-      GNOC_HIP(e, e->hist.ensure((size_t) nchunks * N * 4));
-      GNOC_HIP(e, e->offs.ensure((size_t) nchunks * N * 8));
-      GNOC_LAUNCH(e, KC_INJ_COUNT, k_inj_group<false>, dim3(nchunks), dim3(64), N * 4, s, (uint64_t) n, chunk, N, nbits, e->d_src,
-                         e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(),
-                         (const uint64_t*) nullptr, (Rec*) nullptr, nchunks);
-      GNOC_LAUNCH(e, KC_INJ_OFFS, k_inj_offsets, dim3(N), dim3(256), 0, s, nchunks, e->hist.as<uint32_t>(),
-                         e->slot_base.as<uint64_t>(), e->offs.as<uint64_t>());
-      GNOC_LAUNCH(e, KC_INJ_SCATTER, k_inj_group<true>, dim3(nchunks), dim3(64), N * 4, s, (uint64_t) n, chunk, N, nbits, e->d_src,
-                         e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(),
-                         e->offs.as<uint64_t>(), e->recs.as<Rec>(), nchunks);
-      GNOC_HIP(e, hipGetLastError());
-   }
+      GNOC_LAUNCH(e, KC_SCATTER, k_scatter, dim3(nch), dim3(64), N * 4, s, (uint64_t) n, pch, N, nbits, e->d_src,
+                  e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(), e->recs.as<Rec>(),
+                  e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>());
+   GNOC_LAUNCH(e, KC_ROW_HIST, k_row_hist, dim3(G, H), dim3(256), rh_lds, s, c, G, e->recs.as<Rec>(),
+               e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->Hs.as<uint32_t>(), e->Pp.as<uint32_t>(), pp_lds);
+   GNOC_LAUNCH(e, KC_PROW, k_prow, dim3((uint32_t) (((uint64_t) H * N + 255) / 256)), dim3(256), 0, s, N, H, G,
+               e->Pp.as<uint32_t>(), e->Prow.as<uint32_t>());
+   GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts, dim3((N * 5 + 255) / 256), dim3(256), 0, s, c, e->Hs.as<uint32_t>(),
+               e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>());
+   GNOC_LAUNCH(e, KC_SCAN, k_scan_slots, dim3(1), dim3(1024), 0, s, N, e->slot_cnt.as<uint32_t>(),
+               e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>(), e->gtot.as<uint64_t>() + 1);
 
-   const bool v2 = e->f1 && c.max_list >= 3 && !e->force_v1;
-   e->used_v2 = v2;
-   if (v2)
+   const bool v3 = e->f1 && c.max_list >= 3 && !e->force_v1;
+   e->used_v3 = v3;
    {
-      int rc = run_levels_v2(e);
-      if (rc) return rc;
-   }
-   else
-   {
-      int rc = run_levels_v1(e);
+      int rc = v3 ? run_levels_v3(e) : run_levels_v1(e);
       if (rc) return rc;
    }
 
    if (n)
    {
       if (e->f1)
-         GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<true>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
-                            e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
-                            e->cont.as<uint64_t>(), 0);
+         GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<true>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
+                     e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
+                     e->cont.as<uint64_t>(), 0);
       else
-         GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<false>, dim3(cls_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
-                            e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
-                            e->cont.as<uint64_t>(), 0);
+         GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<false>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
+                     e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
+                     e->cont.as<uint64_t>(), 0);
    }
-   GNOC_HIP(e, hipGetLastError());
    GNOC_HIP(e, hipEventRecord(e->ev1, s));
+   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 16, hipMemcpyDeviceToHost, s));
+   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 2, e->gtot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
    GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 4, e->counters.as<unsigned int>() + 8, 4, hipMemcpyDeviceToHost, s));
    GNOC_HIP(e, hipStreamSynchronize(s));
+   e->h_counters[0] = e->h_pinned[0];
+   e->h_counters[1] = e->h_pinned[1];
+   e->h_records = e->h_counters[0] + e->h_counters[1];
+   if (e->h_pinned[2] > e->rec_bound) return fail(e, GNOC_EHIP, "internal: slot layout exceeds the record bound");
    float ms = 0;
    GNOC_HIP(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
    e->last_ms = ms;
    GNOC_HIP(e, prof_collect(e));
    const unsigned errf = *(unsigned int*) (e->h_pinned + 4);
+   // a leaf the splitter could not cut (or a look-back timeout) leaves garbage
+   // downstream, so it takes precedence: rerun exactly on the v1 path
+   if (errf & 6u) return GNOC_V3_RETRY;
    if (errf & 1u) return fail(e, GNOC_EHIP, "internal: route-count invariant violated");
-   if (errf & 6u) return GNOC_V2_RETRY;   // burst beyond the chunk splitter / look-back timeout
    e->ran = true;
    return GNOC_OK;
 }
@@ -680,12 +665,12 @@ int gnoc_run(gnoc_engine* e)
    const int forced = env && std::strcmp(env, "v1") == 0;
    e->force_v1 = forced;
    int rc = run_once(e);
-   if (rc == GNOC_V2_RETRY)
+   if (rc == GNOC_V3_RETRY)
    {
       e->force_v1 = 1;   // exact but slower whole-port streams
       rc = run_once(e);
       e->force_v1 = forced;
-      if (rc == GNOC_V2_RETRY) rc = fail(e, GNOC_EHIP, "internal: v1 path reported overflow");
+      if (rc == GNOC_V3_RETRY) rc = fail(e, GNOC_EHIP, "internal: v1 path reported overflow");
    }
    return rc;
 }
@@ -735,7 +720,7 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
    out->records = e->h_records;
    out->levels = e->h_levels;
    out->last_run_ms = e->last_ms;
-   out->engine_path = e->dc.contention ? (uint32_t) e->used_v2 : 2u;
+   out->engine_path = e->dc.contention ? (uint32_t) e->used_v3 : 2u;
    if (e->ran && e->dc.contention)
    {
       std::vector<uint64_t> m((size_t) e->dc.N * PORTS);
@@ -764,17 +749,6 @@ int gnoc_get_kernel_stats(gnoc_engine* e, const char** names, double* total_ms, 
       if (total_ms) total_ms[k] = e->kms[k];
       if (launches) launches[k] = e->klaunch[k];
    }
-   return GNOC_OK;
-}
-
-extern "C" __attribute__((visibility("default"))) int gnoc_debug_stamps(gnoc_engine* e, uint64_t* out, size_t cap,
-                                                                     size_t* nchunks)
-{
-   if (!e || !nchunks) return GNOC_EINVAL;
-   *nchunks = e->h_chunks;
-   if (!out || !e->stamps.p) return GNOC_OK;
-   const size_t n = std::min(cap, (size_t) e->h_chunks * 16);
-   GNOC_HIP(e, hipMemcpy(out, e->stamps.p, n * 8, hipMemcpyDeviceToHost));
    return GNOC_OK;
 }
 

@@ -16,223 +16,6 @@
 namespace gnoc {
 
 // ----------------------------------------------------------------------------
-// Preprocessing: classify packets, count records per (port, input side).
-// ----------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, const uint64_t* __restrict__ inj,
-                                                  const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                                                  const uint32_t* __restrict__ bits, const uint32_t* __restrict__ flags,
-                                                  uint32_t* __restrict__ aux, uint8_t* __restrict__ routed,
-                                                  uint64_t* __restrict__ final_ps, uint32_t* __restrict__ slot_cnt,
-                                                  int32_t* __restrict__ diff, unsigned long long* __restrict__ counters)
-{
-   uint64_t hops = 0, nrouted = 0;
-   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
-   {
-      const uint32_t s = src[i], d = dst[i];
-      const uint32_t fl = flags ? flags[i] : 0u;
-      const uint32_t b = bits[i];
-      // NetworkModel::computeNumFlits, network_model.cc:202-212
-      const uint32_t F = (b % c.flit_width) ? b / c.flit_width + 1 : b / c.flit_width;
-      const bool bypass = (s == d) || (fl & 1u);   // processCornerCases self-send; isModelEnabled()==false
-      aux[i] = aux_pack(d, F);
-      routed[i] = bypass ? 0 : 1;
-      if (bypass)
-      {
-         final_ps[i] = inj[i];
-         continue;
-      }
-      uint32_t sx, sy, dx, dy;
-      tile_xy(s, c.W, c.magicW, sx, sy);
-      tile_xy(d, c.W, c.magicW, dx, dy);
-      nrouted++;
-      hops += (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
-      atomicAdd(&slot_cnt[slot_of(s, P_INJ, IN_LOCAL)], 1u);
-      atomicAdd(&slot_cnt[slot_of(s, xy_dir(sx, sy, dx, dy), IN_LOCAL)], 1u);
-      const uint32_t ydir = dy > sy ? P_UP : dy < sy ? P_DOWN : P_SELF;
-      // diff layout: [0] RIGHT rows H x (W+1), [1] LEFT rows, [2] UP cols W x (H+1), [3] DOWN cols
-      int32_t* dR = diff;
-      int32_t* dL = dR + (size_t) c.H * (c.W + 1);
-      int32_t* dU = dL + (size_t) c.H * (c.W + 1);
-      int32_t* dD = dU + (size_t) c.W * (c.H + 1);
-      if (dx > sx)
-      {
-         if (dx > sx + 1) { atomicAdd(&dR[sy * (c.W + 1) + sx + 1], 1); atomicAdd(&dR[sy * (c.W + 1) + dx], -1); }
-         atomicAdd(&slot_cnt[slot_of(sy * c.W + dx, ydir, IN_W)], 1u);
-      }
-      else if (dx < sx)
-      {
-         if (dx + 1 < sx) { atomicAdd(&dL[sy * (c.W + 1) + dx + 1], 1); atomicAdd(&dL[sy * (c.W + 1) + sx], -1); }
-         atomicAdd(&slot_cnt[slot_of(sy * c.W + dx, ydir, IN_E)], 1u);
-      }
-      if (dy > sy)
-      {
-         if (dy > sy + 1) { atomicAdd(&dU[dx * (c.H + 1) + sy + 1], 1); atomicAdd(&dU[dx * (c.H + 1) + dy], -1); }
-         atomicAdd(&slot_cnt[slot_of(d, P_SELF, IN_S)], 1u);
-      }
-      else if (dy < sy)
-      {
-         if (dy + 1 < sy) { atomicAdd(&dD[dx * (c.H + 1) + dy + 1], 1); atomicAdd(&dD[dx * (c.H + 1) + sy], -1); }
-         atomicAdd(&slot_cnt[slot_of(d, P_SELF, IN_N)], 1u);
-      }
-   }
-   // block-reduce the two counters
-   __shared__ unsigned long long red[2][4];
-   for (int off = 32; off > 0; off >>= 1)
-   {
-      hops += __shfl_down(hops, off);
-      nrouted += __shfl_down(nrouted, off);
-   }
-   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-   if (l == 0) { red[0][w] = hops; red[1][w] = nrouted; }
-   __syncthreads();
-   if (threadIdx.x == 0)
-   {
-      unsigned long long h = 0, r = 0;
-      for (int k = 0; k < (int) (blockDim.x >> 6); k++) { h += red[0][k]; r += red[1][k]; }
-      atomicAdd(&counters[0], h);
-      atomicAdd(&counters[1], r);
-   }
-}
-
-// Turn the chain difference arrays into slot counts (one thread per row/column chain).
-__global__ void k_chain_prefix(DevCfg c, const int32_t* __restrict__ diff, uint32_t* __restrict__ slot_cnt)
-{
-   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-   const int32_t* dR = diff;
-   const int32_t* dL = dR + (size_t) c.H * (c.W + 1);
-   const int32_t* dU = dL + (size_t) c.H * (c.W + 1);
-   const int32_t* dD = dU + (size_t) c.W * (c.H + 1);
-   if (i < c.H)
-   {
-      int32_t r = 0, l = 0;
-      for (uint32_t x = 0; x < c.W; x++)
-      {
-         r += dR[i * (c.W + 1) + x];
-         l += dL[i * (c.W + 1) + x];
-         slot_cnt[slot_of(i * c.W + x, P_RIGHT, IN_W)] += (uint32_t) r;
-         slot_cnt[slot_of(i * c.W + x, P_LEFT, IN_E)] += (uint32_t) l;
-      }
-   }
-   else if (i < c.H + c.W)
-   {
-      const uint32_t x = i - c.H;
-      int32_t u = 0, d = 0;
-      for (uint32_t y = 0; y < c.H; y++)
-      {
-         u += dU[x * (c.H + 1) + y];
-         d += dD[x * (c.H + 1) + y];
-         slot_cnt[slot_of(y * c.W + x, P_UP, IN_S)] += (uint32_t) u;
-         slot_cnt[slot_of(y * c.W + x, P_DOWN, IN_N)] += (uint32_t) d;
-      }
-   }
-}
-
-// Exclusive scan of slot counts (rounded up to 64 records, so every slot starts
-// on a 1 KiB boundary and its 1-in-64 key samples index as base/64) -> bases.
-// Single 1024-thread block; nslots = 30 N is small.
-__global__ __launch_bounds__(1024) void k_scan_slots(uint32_t nslots, const uint32_t* __restrict__ cnt,
-                                                     uint64_t* __restrict__ base)
-{
-   __shared__ uint64_t part[1024];
-   const uint32_t per = (nslots + 1023) / 1024;
-   const uint32_t lo = threadIdx.x * per, hi = min(lo + per, nslots);
-   uint64_t s = 0;
-   for (uint32_t i = lo; i < hi; i++) s += (cnt[i] + 63) & ~63u;   // slots start 64-record aligned (1 KiB)
-   part[threadIdx.x] = s;
-   __syncthreads();
-   for (uint32_t off = 1; off < 1024; off <<= 1)
-   {
-      uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-      __syncthreads();
-      part[threadIdx.x] += v;
-      __syncthreads();
-   }
-   uint64_t run = part[threadIdx.x] - s;
-   for (uint32_t i = lo; i < hi; i++) { base[i] = run; run += (cnt[i] + 63) & ~63u; }
-   if (threadIdx.x == 1023) base[nslots] = part[1023];
-}
-
-// ----------------------------------------------------------------------------
-// Injection grouping: stable partition of the (t, id)-ordered trace by source
-// tile into the injection-port input slots.  One wave per chunk; ranks among
-// equal sources inside a wave come from a ballot-built match mask.
-// ----------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t match_mask(uint32_t key, bool valid, int nbits)
-{
-   uint64_t m = __ballot(valid);
-   for (int b = 0; b < nbits; b++)
-   {
-      const bool bit = (key >> b) & 1u;
-      const uint64_t bb = __ballot(bit && valid);
-      m &= bit ? bb : ~bb;
-   }
-   return m;
-}
-
-template <bool SCATTER>
-__global__ __launch_bounds__(64) void k_inj_group(uint64_t n, uint32_t chunk, uint32_t N, int nbits,
-                                                  const uint32_t* __restrict__ src, const uint8_t* __restrict__ routed,
-                                                  const uint64_t* __restrict__ inj, const uint32_t* __restrict__ aux,
-                                                  uint32_t* __restrict__ hist, const uint64_t* __restrict__ offs,
-                                                  Rec* __restrict__ recs, uint32_t nchunks)
-{
-   extern __shared__ uint32_t h[];   // N counters
-   const uint32_t lane = threadIdx.x;
-   for (uint32_t s = lane; s < N; s += 64) h[s] = 0;
-   __syncthreads();
-   const uint64_t lo = (uint64_t) blockIdx.x * chunk;
-   const uint64_t hi = min(lo + chunk, n);
-   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-   for (uint64_t k = lo; k < hi; k += 64)
-   {
-      const uint64_t i = k + lane;
-      const bool valid = i < hi && routed[i];
-      const uint32_t s = valid ? src[i] : 0u;
-      const uint64_t m = match_mask(s, valid, nbits);
-      uint32_t old = valid ? h[s] : 0u;
-      __syncthreads();
-      const uint32_t rank = old + (uint32_t) __popcll(m & lt);
-      if (valid && (63 - __clzll(m)) == (int) lane) h[s] = old + (uint32_t) __popcll(m);
-      if (SCATTER && valid)
-      {
-         const uint64_t pos = offs[(uint64_t) s * nchunks + blockIdx.x] + rank;
-         Rec r;
-         r.t = inj[i];
-         r.id = (uint32_t) i;
-         r.aux = aux[i];
-         recs[pos] = r;
-      }
-      __syncthreads();
-   }
-   if (!SCATTER)
-      for (uint32_t s = lane; s < N; s += 64) hist[(uint64_t) s * nchunks + blockIdx.x] = h[s];
-}
-
-// Per source tile: exclusive scan over chunks, offset by the slot base.
-__global__ __launch_bounds__(256) void k_inj_offsets(uint32_t nchunks, const uint32_t* __restrict__ hist,
-                                                     const uint64_t* __restrict__ slot_base, uint64_t* __restrict__ offs)
-{
-   __shared__ uint64_t part[256];
-   const uint32_t s = blockIdx.x;
-   const uint32_t per = (nchunks + 255) / 256;
-   const uint32_t lo = threadIdx.x * per, hi = min(lo + per, nchunks);
-   const uint32_t* hrow = hist + (uint64_t) s * nchunks;
-   uint64_t sum = 0;
-   for (uint32_t i = lo; i < hi; i++) sum += hrow[i];
-   part[threadIdx.x] = sum;
-   __syncthreads();
-   for (uint32_t off = 1; off < 256; off <<= 1)
-   {
-      uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-      __syncthreads();
-      part[threadIdx.x] += v;
-      __syncthreads();
-   }
-   uint64_t run = part[threadIdx.x] - sum + slot_base[slot_of(s, P_INJ, IN_LOCAL)];
-   for (uint32_t i = lo; i < hi; i++) { offs[(uint64_t) s * nchunks + i] = run; run += hrow[i]; }
-}
-
-// ----------------------------------------------------------------------------
 // Port stream kernel: one workgroup owns one output-port queue and streams its
 // whole arrival history.  Per round: load up to T records of each input
 // stream into LDS, merge the prefix that is provably complete ((t,id) <= the
@@ -658,9 +441,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
             uint32_t ndir = 0;
             if (dir != P_SELF)
             {
-               uint32_t dx, dy;
-               tile_xy(aux_dst(sm.m_aux[e]), c.W, c.magicW, dx, dy);
-               ndir = xy_dir(nx, ny, dx, dy);
+               ndir = xy_dir(nx, ny, aux_dx(sm.m_aux[e]), aux_dy(sm.m_aux[e]));
             }
             packed += 1ull << (12 * ndir);
          }
@@ -689,9 +470,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
                final_ps[id] = tn + ps_of<F1>(aux_F(ax), c.f);
                continue;
             }
-            uint32_t dx, dy;
-            tile_xy(aux_dst(ax), c.W, c.magicW, dx, dy);
-            const uint32_t ndir = xy_dir(nx, ny, dx, dy);
+            const uint32_t ndir = xy_dir(nx, ny, aux_dx(ax), aux_dy(ax));
             const uint32_t r = (uint32_t) ((pre >> (12 * ndir)) & 0xFFF);
             pre += 1ull << (12 * ndir);
             if (ocur[ndir] + r >= ocap[ndir])
@@ -746,9 +525,9 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
    for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
    {
       if (!routed[i]) { zl[i] = 0; cont[i] = 0; continue; }
-      uint32_t sx, sy, dx, dy;
+      uint32_t sx, sy;
       tile_xy(src[i], c.W, c.magicW, sx, sy);
-      tile_xy(aux_dst(aux[i]), c.W, c.magicW, dx, dy);
+      const uint32_t dx = aux_dx(aux[i]), dy = aux_dy(aux[i]);
       const uint64_t hops = (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
       // Hop::Hop accumulates Latency(0) at injection, Latency(R+Lk) per mesh router,
       // Latency(F) at receive (network_model.cc:142-150, 556-563).
@@ -760,10 +539,6 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
 }
 
 // explicit instantiations
-template __global__ void k_inj_group<false>(uint64_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
-                                            const uint64_t*, const uint32_t*, uint32_t*, const uint64_t*, Rec*, uint32_t);
-template __global__ void k_inj_group<true>(uint64_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
-                                           const uint64_t*, const uint32_t*, uint32_t*, const uint64_t*, Rec*, uint32_t);
 template __global__ void k_port_stream<true>(DevCfg, const uint32_t*, const uint32_t*, const uint64_t*, Rec*, uint64_t*,
                                              uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
 template __global__ void k_port_stream<false>(DevCfg, const uint32_t*, const uint32_t*, const uint64_t*, Rec*, uint64_t*,

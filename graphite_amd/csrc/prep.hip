@@ -1,0 +1,361 @@
+// prep.hip -- per-run preprocessing of the packet batch (gfx950).
+//
+// 1. k_classify:   per packet F = computeNumFlits (network_model.cc:202-212),
+//                  the corner cases of processCornerCases / isModelEnabled
+//                  (network_model.cc:171-183, 413-468: self-sends and unmodeled
+//                  packets bypass the mesh), aux = (dx, dy, F), and a per-chunk
+//                  histogram of source tiles in LDS (no global atomics).
+// 2. k_src_tot / k_inj_base / k_src_offs: injection-slot layout.  The trace is
+//                  (t, id)-ordered; grouping it stably by source tile gives every
+//                  injection queue (emesh_hop_by_hop.cc:109-112, 151-159) its
+//                  arrivals in service order.
+// 3. k_scatter:    the stable group-by-source into the injection slots, one wave
+//                  per chunk, ranks from ballot match masks.
+// 4. k_row_hist:   per (source row, group of sources) LDS histograms of the
+//                  grouped records: per source (dx, y-class) and per destination.
+// 5. k_prow / k_slot_counts: every output-port input slot's record count, in
+//                  closed form from those histograms (XY routing is static:
+//                  emesh_hop_by_hop.cc:229-240).  Deterministic, atomic-free.
+// 6. k_scan_slots: slot bases (64-record aligned, so a slot's 1-in-64 key
+//                  samples index as base/64).
+// 7. k_plan_*:     per-port descriptors and the chunk -> port map of every level,
+//                  on device, so a run needs no host round trip.
+#include "common.h"
+
+namespace gnoc {
+
+// ---------------------------------------------------------------------------
+// 1. classify
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, uint32_t pch, const uint64_t* __restrict__ inj,
+                                                  const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                                                  const uint32_t* __restrict__ bits, const uint32_t* __restrict__ flags,
+                                                  uint32_t* __restrict__ aux, uint8_t* __restrict__ routed,
+                                                  uint64_t* __restrict__ final_ps, uint32_t* __restrict__ hist,
+                                                  unsigned long long* __restrict__ counters)
+{
+   extern __shared__ uint32_t h[];   // N source counters
+   const uint32_t N = c.N;
+   for (uint32_t s = threadIdx.x; s < N; s += blockDim.x) h[s] = 0;
+   __syncthreads();
+   const uint64_t lo = (uint64_t) blockIdx.x * pch;
+   const uint64_t hi = min(lo + pch, n);
+   uint64_t hops = 0, nrouted = 0;
+   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
+   {
+      const uint32_t s = src[i], d = dst[i];
+      const uint32_t fl = flags ? flags[i] : 0u;
+      const uint32_t b = bits[i];
+      const uint32_t F = (b % c.flit_width) ? b / c.flit_width + 1 : b / c.flit_width;
+      const bool bypass = (s == d) || (fl & 1u);
+      uint32_t sx, sy, dx, dy;
+      tile_xy(s, c.W, c.magicW, sx, sy);
+      tile_xy(d, c.W, c.magicW, dx, dy);
+      aux[i] = aux_pack(dx, dy, F);
+      routed[i] = bypass ? 0 : 1;
+      if (bypass)
+      {
+         final_ps[i] = inj[i];
+         continue;
+      }
+      atomicAdd(&h[s], 1u);
+      nrouted++;
+      hops += (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
+   }
+   __syncthreads();
+   uint32_t* hrow = hist + (uint64_t) blockIdx.x * N;
+   for (uint32_t s = threadIdx.x; s < N; s += blockDim.x) hrow[s] = h[s];
+   __shared__ unsigned long long red[2][4];
+   for (int off = 32; off > 0; off >>= 1)
+   {
+      hops += __shfl_down(hops, off);
+      nrouted += __shfl_down(nrouted, off);
+   }
+   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+   if (l == 0) { red[0][w] = hops; red[1][w] = nrouted; }
+   __syncthreads();
+   if (threadIdx.x == 0)
+   {
+      unsigned long long a = 0, r = 0;
+      for (int k = 0; k < (int) (blockDim.x >> 6); k++) { a += red[0][k]; r += red[1][k]; }
+      atomicAdd(&counters[0], a);
+      atomicAdd(&counters[1], r);
+   }
+}
+
+// ---------------------------------------------------------------------------
+// 2. injection-slot layout
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_src_tot(uint32_t N, uint32_t nch, const uint32_t* __restrict__ hist,
+                                                 uint32_t* __restrict__ tot)
+{
+   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+   if (s >= N) return;
+   uint32_t t = 0;
+   for (uint32_t ch = 0; ch < nch; ch++) t += hist[(uint64_t) ch * N + s];
+   tot[s] = t;
+}
+
+// Single block: injection slot bases (64-aligned) in front of every other slot.
+__global__ __launch_bounds__(1024) void k_inj_base(uint32_t N, const uint32_t* __restrict__ tot,
+                                                   uint32_t* __restrict__ slot_cnt, uint64_t* __restrict__ slot_base,
+                                                   uint64_t* __restrict__ inj_total)
+{
+   __shared__ uint64_t part[1024];
+   const uint32_t per = (N + 1023) / 1024;
+   const uint32_t lo = threadIdx.x * per, hi = min(lo + per, N);
+   uint64_t s = 0;
+   for (uint32_t i = lo; i < hi; i++) s += (tot[i] + 63) & ~63u;
+   part[threadIdx.x] = s;
+   __syncthreads();
+   for (uint32_t off = 1; off < 1024; off <<= 1)
+   {
+      const uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+   }
+   uint64_t run = part[threadIdx.x] - s;
+   for (uint32_t i = lo; i < hi; i++)
+   {
+      const uint32_t sl = slot_of(i, P_INJ, IN_LOCAL);
+      slot_base[sl] = run;
+      slot_cnt[sl] = tot[i];
+      run += (tot[i] + 63) & ~63u;
+   }
+   if (threadIdx.x == 1023) *inj_total = part[1023];
+}
+
+// hist[ch][s] (counts) -> absolute record offsets of chunk ch's first record of source s.
+__global__ __launch_bounds__(256) void k_src_offs(uint32_t N, uint32_t nch, uint32_t* __restrict__ hist,
+                                                  const uint64_t* __restrict__ slot_base)
+{
+   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+   if (s >= N) return;
+   uint32_t run = (uint32_t) slot_base[slot_of(s, P_INJ, IN_LOCAL)];   // < 2^32 records (checked at submit)
+   for (uint32_t ch = 0; ch < nch; ch++)
+   {
+      const uint64_t k = (uint64_t) ch * N + s;
+      const uint32_t v = hist[k];
+      hist[k] = run;
+      run += v;
+   }
+}
+
+// ---------------------------------------------------------------------------
+// 3. stable scatter into the injection slots (one wave per chunk)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t match_mask(uint32_t key, bool valid, int nbits)
+{
+   uint64_t m = __ballot(valid);
+   for (int b = 0; b < nbits; b++)
+   {
+      const bool bit = (key >> b) & 1u;
+      const uint64_t bb = __ballot(bit && valid);
+      m &= bit ? bb : ~bb;
+   }
+   return m;
+}
+
+__global__ __launch_bounds__(64) void k_scatter(uint64_t n, uint32_t pch, uint32_t N, int nbits,
+                                                const uint32_t* __restrict__ src, const uint8_t* __restrict__ routed,
+                                                const uint64_t* __restrict__ inj, const uint32_t* __restrict__ aux,
+                                                const uint32_t* __restrict__ offs, Rec* __restrict__ recs,
+                                                uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id)
+{
+   extern __shared__ uint32_t h[];   // N rank counters
+   const uint32_t lane = threadIdx.x;
+   for (uint32_t s = lane; s < N; s += 64) h[s] = 0;
+   __syncthreads();
+   const uint64_t lo = (uint64_t) blockIdx.x * pch;
+   const uint64_t hi = min(lo + pch, n);
+   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+   const uint32_t* orow = offs + (uint64_t) blockIdx.x * N;
+   for (uint64_t k = lo; k < hi; k += 64)
+   {
+      const uint64_t i = k + lane;
+      const bool valid = i < hi && routed[i];
+      const uint32_t s = valid ? src[i] : 0u;
+      const uint64_t m = match_mask(s, valid, nbits);
+      const uint32_t old = valid ? h[s] : 0u;
+      __syncthreads();
+      if (valid)
+      {
+         const uint32_t rank = old + (uint32_t) __popcll(m & lt);
+         if ((63 - __clzll(m)) == (int) lane) h[s] = old + (uint32_t) __popcll(m);
+         const uint64_t pos = (uint64_t) orow[s] + rank;
+         Rec r;
+         r.t = inj[i];
+         r.id = (uint32_t) i;
+         r.aux = aux[i];
+         recs[pos] = r;
+         if ((pos & 63) == 0)
+         {
+            samp_t[pos >> 6] = r.t;
+            samp_id[pos >> 6] = r.id;
+         }
+      }
+      __syncthreads();
+   }
+}
+
+// ---------------------------------------------------------------------------
+// 4. per-row histograms of the grouped injection records
+//    Hs[s][dx][c]   c = 0 (dy < sy), 1 (dy == sy), 2 (dy > sy)      N x W x 3
+//    Pp[y][g][dst]  destinations of row y, source group g            H x G x N
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_row_hist(DevCfg c, uint32_t G, const Rec* __restrict__ recs,
+                                                  const uint32_t* __restrict__ slot_cnt,
+                                                  const uint64_t* __restrict__ slot_base, uint32_t* __restrict__ Hs,
+                                                  uint32_t* __restrict__ Pp, int pp_lds)
+{
+   extern __shared__ uint32_t sm[];
+   const uint32_t W = c.W, N = c.N;
+   const uint32_t y = blockIdx.y, g = blockIdx.x;
+   const uint32_t x0 = (uint32_t) (((uint64_t) g * W) / G), x1 = (uint32_t) (((uint64_t) (g + 1) * W) / G);
+   const uint32_t nhs = (x1 - x0) * W * 3;
+   uint32_t* hs = sm;
+   uint32_t* ph = sm + nhs;
+   uint32_t* pg = Pp + ((uint64_t) y * G + g) * N;
+   for (uint32_t k = threadIdx.x; k < nhs; k += blockDim.x) hs[k] = 0;
+   if (pp_lds)
+      for (uint32_t k = threadIdx.x; k < N; k += blockDim.x) ph[k] = 0;
+   __syncthreads();
+   for (uint32_t x = x0; x < x1; x++)
+   {
+      const uint32_t s = y * W + x;
+      const uint32_t sl = slot_of(s, P_INJ, IN_LOCAL);
+      const uint32_t cnt = slot_cnt[sl];
+      const Rec* r = recs + slot_base[sl];
+      uint32_t* hrow = hs + (x - x0) * W * 3;
+      for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x)
+      {
+         const uint32_t a = r[i].aux;
+         const uint32_t dx = aux_dx(a), dy = aux_dy(a);
+         const uint32_t cl = dy < y ? 0u : dy == y ? 1u : 2u;
+         atomicAdd(&hrow[dx * 3 + cl], 1u);
+         if (pp_lds) atomicAdd(&ph[dy * W + dx], 1u);
+         else atomicAdd(&pg[dy * W + dx], 1u);
+      }
+   }
+   __syncthreads();
+   for (uint32_t k = threadIdx.x; k < nhs; k += blockDim.x) Hs[(uint64_t) (y * W + x0) * W * 3 + k] = hs[k];
+   if (pp_lds)
+      for (uint32_t k = threadIdx.x; k < N; k += blockDim.x) pg[k] = ph[k];
+}
+
+// Prow[y][dst] = sum over groups.
+__global__ __launch_bounds__(256) void k_prow(uint32_t N, uint32_t H, uint32_t G, const uint32_t* __restrict__ Pp,
+                                              uint32_t* __restrict__ Prow)
+{
+   const uint64_t k = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+   if (k >= (uint64_t) H * N) return;
+   const uint64_t y = k / N, d = k % N;
+   uint32_t s = 0;
+   for (uint32_t g = 0; g < G; g++) s += Pp[(y * G + g) * N + d];
+   Prow[k] = s;
+}
+
+// One thread per (tile, dir) computes the 5 input-side counts of that output port.
+// Packets follow XY routing: X leg in the source row, Y leg in the destination column.
+__global__ __launch_bounds__(256) void k_slot_counts(DevCfg c, const uint32_t* __restrict__ Hs,
+                                                     const uint32_t* __restrict__ Prow, uint32_t* __restrict__ slot_cnt)
+{
+   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+   const uint32_t W = c.W, H = c.H, N = c.N;
+   if (k >= N * 5) return;
+   const uint32_t tile = k / 5, dir = k % 5;
+   const uint32_t x = tile % W, y = tile / W;
+   auto hs = [&](uint32_t sx, uint32_t sy, uint32_t dx, uint32_t cl) -> uint32_t {
+      return Hs[((uint64_t) (sy * W + sx) * W + dx) * 3 + cl];
+   };
+   auto prow = [&](uint32_t sy, uint32_t dx, uint32_t dy) -> uint32_t { return Prow[(uint64_t) sy * N + dy * W + dx]; };
+   uint32_t cl = 0, cw = 0, ce = 0, cs = 0, cn = 0;
+   // IN_LOCAL: packets injected here whose first hop leaves through `dir`
+   if (dir == P_RIGHT) { for (uint32_t dx = x + 1; dx < W; dx++) cl += hs(x, y, dx, 0) + hs(x, y, dx, 1) + hs(x, y, dx, 2); }
+   else if (dir == P_LEFT) { for (uint32_t dx = 0; dx < x; dx++) cl += hs(x, y, dx, 0) + hs(x, y, dx, 1) + hs(x, y, dx, 2); }
+   else if (dir == P_UP) cl = hs(x, y, x, 2);
+   else if (dir == P_DOWN) cl = hs(x, y, x, 0);
+   // IN_W: X leg moving right through x (sx < x <= dx) in row y
+   if (dir == P_RIGHT)
+   {
+      for (uint32_t sx = 0; sx < x; sx++)
+         for (uint32_t dx = x + 1; dx < W; dx++) cw += hs(sx, y, dx, 0) + hs(sx, y, dx, 1) + hs(sx, y, dx, 2);
+   }
+   else if (dir != P_LEFT)
+   {
+      const uint32_t want = dir == P_UP ? 2u : dir == P_DOWN ? 0u : 1u;
+      for (uint32_t sx = 0; sx < x; sx++) cw += hs(sx, y, x, want);
+   }
+   // IN_E: X leg moving left (dx <= x < sx)
+   if (dir == P_LEFT)
+   {
+      for (uint32_t sx = x + 1; sx < W; sx++)
+         for (uint32_t dx = 0; dx < x; dx++) ce += hs(sx, y, dx, 0) + hs(sx, y, dx, 1) + hs(sx, y, dx, 2);
+   }
+   else if (dir != P_RIGHT)
+   {
+      const uint32_t want = dir == P_UP ? 2u : dir == P_DOWN ? 0u : 1u;
+      for (uint32_t sx = x + 1; sx < W; sx++) ce += hs(sx, y, x, want);
+   }
+   // IN_S: Y leg moving up in column x (sy < y <= dy)
+   if (dir == P_UP)
+   {
+      for (uint32_t sy = 0; sy < y; sy++)
+         for (uint32_t dy = y + 1; dy < H; dy++) cs += prow(sy, x, dy);
+   }
+   else if (dir == P_SELF)
+   {
+      for (uint32_t sy = 0; sy < y; sy++) cs += prow(sy, x, y);
+   }
+   // IN_N: Y leg moving down (dy <= y < sy)
+   if (dir == P_DOWN)
+   {
+      for (uint32_t sy = y + 1; sy < H; sy++)
+         for (uint32_t dy = 0; dy < y; dy++) cn += prow(sy, x, dy);
+   }
+   else if (dir == P_SELF)
+   {
+      for (uint32_t sy = y + 1; sy < H; sy++) cn += prow(sy, x, y);
+   }
+   slot_cnt[slot_of(tile, dir, IN_LOCAL)] = cl;
+   slot_cnt[slot_of(tile, dir, IN_W)] = cw;
+   slot_cnt[slot_of(tile, dir, IN_E)] = ce;
+   slot_cnt[slot_of(tile, dir, IN_S)] = cs;
+   slot_cnt[slot_of(tile, dir, IN_N)] = cn;
+}
+
+// ---------------------------------------------------------------------------
+// 6. bases of the non-injection slots, after the injection region (single block)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_scan_slots(uint32_t N, const uint32_t* __restrict__ cnt,
+                                                     uint64_t* __restrict__ base, const uint64_t* __restrict__ inj_total,
+                                                     uint64_t* __restrict__ total)
+{
+   __shared__ uint64_t part[1024];
+   // enumerate the 5 mesh directions x 5 inputs of every tile: q -> slot (tile*6 + dir)*5 + in, dir < 5
+   const uint32_t nq = N * 25;
+   const uint32_t per = (nq + 1023) / 1024;
+   const uint32_t lo = threadIdx.x * per, hi = min(lo + per, nq);
+   auto slot = [](uint32_t q) { return (q / 25) * (PORTS * INS) + (q % 25); };
+   uint64_t s = 0;
+   for (uint32_t q = lo; q < hi; q++) s += (cnt[slot(q)] + 63) & ~63u;
+   part[threadIdx.x] = s;
+   __syncthreads();
+   for (uint32_t off = 1; off < 1024; off <<= 1)
+   {
+      const uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+   }
+   uint64_t run = *inj_total + part[threadIdx.x] - s;
+   for (uint32_t q = lo; q < hi; q++)
+   {
+      base[slot(q)] = run;
+      run += (cnt[slot(q)] + 63) & ~63u;
+   }
+   if (threadIdx.x == 1023) *total = *inj_total + part[1023];
+}
+
+}  // namespace gnoc
