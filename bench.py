@@ -116,9 +116,9 @@ def main():
     if rank == 0:
         value = hops_all * a.steps / elapsed_max
         ms_step = elapsed_max / a.steps * 1e3
-        dom = max(("k_chunk", "k_port_stream"), key=lambda k: kst.get(k, (0.0, 0))[0])
+        dom = max(("k_level", "k_port_stream"), key=lambda k: kst.get(k, (0.0, 0))[0])
         port_ms, port_launches = kst.get(dom, (0.0, 0))
-        # dominant kernel: the per-port merge/queue/route stream (k_chunk, or k_port_stream on the v1 path).
+        # dominant kernel: the per-level chunk kernel (k_level, or k_port_stream on the v1 path).
         # Algorithmic bytes over all its launches: 32 B per mesh hop + 24 B per packet.
         alg_bytes = hops * BYTES_PER_HOP + pkts * BYTES_PER_PKT
         achieved = alg_bytes / (port_ms * 1e-3) / 1e9 if port_ms > 0 else 0.0

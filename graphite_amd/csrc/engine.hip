@@ -90,7 +90,8 @@ struct gnoc_engine
    DevBuf hist, tot, slot_cnt, slot_base, counters, gtot;
    DevBuf recs, samp_t, samp_id, Hs, Pp, Prow, nexc, dirty;
    DevBuf pio, pnc, pgb, lvl_cbase, chunk_port, flags, st, lvl_ctr;
-   DevBuf port_sum, port_cnt, port_mg1, plan_ports;
+   DevBuf port_sum, port_cnt, port_mg1, plan_ports, stamps;
+   uint64_t h_chunk_bound = 0;
    int force_v1 = 0;
    int used_v3 = 0;
    std::vector<uint32_t> h_slot_cnt;
@@ -285,7 +286,7 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    if (he == hipSuccess)
    {
       int per_cu = 0, cus = 0;
-      he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_level, LV_T, 0);
+      he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_level<false>, LV_T, 0);
       if (he == hipSuccess) he = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
       e->level_grid = std::max(1, per_cu) * std::max(1, cus);
    }
@@ -497,13 +498,31 @@ static int run_levels_v3(gnoc_engine* e)
    GNOC_LAUNCH(e, KC_PLAN, k_plan_expand, dim3(pg), dim3(256), 0, s, P, e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
                e->pgb.as<uint32_t>(), e->chunk_port.as<uint32_t>());
    e->h_levels = L;
+   const char* stv = std::getenv("GNOC_STAMPS");
+   const bool stamps = stv && *stv == '1';
+   e->h_chunk_bound = chunk_bound;
+   if (stamps)
+   {
+      GNOC_HIP(e, e->stamps.ensure(chunk_bound * 16 * 8));
+      GNOC_HIP(e, hipMemsetAsync(e->stamps.p, 0, chunk_bound * 16 * 8, s));
+   }
    for (uint32_t l = 0; l < L; l++)
-      GNOC_LAUNCH(e, KC_LEVEL, k_level, dim3(e->level_grid), dim3(LV_T), 0, s, c, l, e->lvl_cbase.as<uint32_t>(),
-                  e->lvl_ctr.as<unsigned>(), e->chunk_port.as<uint32_t>(), e->pio.as<PortIO3>(), e->recs.as<Rec>(),
-                  e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(), e->flags.as<uint32_t>(),
-                  e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
-                  e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
-                  e->counters.as<unsigned>() + 8);
+   {
+      if (stamps)
+         GNOC_LAUNCH(e, KC_LEVEL, k_level<true>, dim3(e->level_grid), dim3(LV_T), 0, s, c, l, e->lvl_cbase.as<uint32_t>(),
+                     e->lvl_ctr.as<unsigned>(), e->chunk_port.as<uint32_t>(), e->pio.as<PortIO3>(), e->recs.as<Rec>(),
+                     e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(), e->flags.as<uint32_t>(),
+                     e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
+                     e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
+                     e->counters.as<unsigned>() + 8, e->stamps.as<uint64_t>());
+      else
+         GNOC_LAUNCH(e, KC_LEVEL, k_level<false>, dim3(e->level_grid), dim3(LV_T), 0, s, c, l, e->lvl_cbase.as<uint32_t>(),
+                     e->lvl_ctr.as<unsigned>(), e->chunk_port.as<uint32_t>(), e->pio.as<PortIO3>(), e->recs.as<Rec>(),
+                     e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(), e->flags.as<uint32_t>(),
+                     e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
+                     e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
+                     e->counters.as<unsigned>() + 8, (uint64_t*) nullptr);
+   }
    return GNOC_OK;
 }
 
@@ -749,6 +768,17 @@ int gnoc_get_kernel_stats(gnoc_engine* e, const char** names, double* total_ms, 
       if (total_ms) total_ms[k] = e->kms[k];
       if (launches) launches[k] = e->klaunch[k];
    }
+   return GNOC_OK;
+}
+
+// Debug (tools/stamps.py, GNOC_STAMPS=1): per-chunk phase stamps of the last run.
+__attribute__((visibility("default"))) int gnoc_debug_stamps(gnoc_engine* e, uint64_t* out, size_t cap, size_t* nchunks)
+{
+   if (!e || !nchunks) return GNOC_EINVAL;
+   *nchunks = e->h_chunk_bound;
+   if (!out || !e->stamps.p) return GNOC_OK;
+   const size_t n = std::min(cap, (size_t) e->h_chunk_bound * 16);
+   GNOC_HIP(e, hipMemcpy(out, e->stamps.p, n * 8, hipMemcpyDeviceToHost));
    return GNOC_OK;
 }
 

@@ -31,11 +31,11 @@
 namespace gnoc {
 
 constexpr int LV_T = 256;          // threads per workgroup
-constexpr int LV_CAP = 1024;       // records one leaf holds in LDS
+constexpr int LV_CAP = 2048;       // records one leaf holds in LDS
 constexpr int LV_IN = 4;           // input slots per port (SELF, UP, DOWN have 4)
 constexpr int LV_SEG = LV_IN + 1;  // + the exception segment
 constexpr int LV_MAXLEAF = 32;     // leaves per chunk (bursts); beyond -> errflag, v1 rerun
-constexpr uint32_t LV_CTGT = 640;  // target records per chunk
+constexpr uint32_t LV_CTGT = 1200; // target records per chunk
 constexpr uint32_t LV_SPIN_LIMIT = 1u << 24;
 
 // Per-port descriptor, built on device by k_plan_ports from the slot layout.
@@ -657,6 +657,13 @@ __device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint32
 // ---------------------------------------------------------------------------
 // the level kernel: a persistent grid pulls the level's chunks in order
 // ---------------------------------------------------------------------------
+#define LV_STAMP(k)                                                                                          \
+   do                                                                                                       \
+   {                                                                                                        \
+      if (STAMPS && stamps && tid == 0) stamps[(uint64_t) g * 16 + (k)] = __builtin_amdgcn_s_memtime();     \
+   } while (0)
+
+template <bool STAMPS>
 __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const uint32_t* __restrict__ lvl_cbase,
                                                 unsigned* __restrict__ ctr, const uint32_t* __restrict__ chunk_port,
                                                 const PortIO3* __restrict__ pio, Rec* __restrict__ recs,
@@ -665,7 +672,8 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
                                                 uint64_t* __restrict__ st, uint64_t* __restrict__ final_ps,
                                                 unsigned long long* __restrict__ port_sum,
                                                 unsigned long long* __restrict__ port_cnt,
-                                                unsigned long long* __restrict__ port_mg1, unsigned* __restrict__ errflag)
+                                                unsigned long long* __restrict__ port_mg1, unsigned* __restrict__ errflag,
+                                                uint64_t* __restrict__ stamps)
 {
    __shared__ LvSmem sm;
    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -687,6 +695,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
       __syncthreads();
       if (!sm.j) return;
       const uint32_t g = sm.g;
+      LV_STAMP(0);
       const uint32_t pk = chunk_port[g];
       {
          const uint32_t* srcw = reinterpret_cast<const uint32_t*>(pio + pk);
@@ -709,6 +718,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
          for (int k = 0; k < 5; k++) sm.cy.cnt[k] = 0;
       }
       __syncthreads();
+      LV_STAMP(1);
 
       // ---- chunk key range: exact index split of the largest input
       const uint32_t sb = sm.io.sb;
@@ -722,6 +732,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
       if (has_lo) { const Rec r = recs[sm.io.base[sb] + ilo]; klo_t = r.t; klo_i = r.id; }
       if (has_hi) { const Rec r = recs[sm.io.base[sb] + ihi]; khi_t = r.t; khi_i = r.id; }
 
+      LV_STAMP(2);
       // ---- main ranges of the other inputs (waves search in parallel)
       for (uint32_t q = wv; q < 2 * (uint32_t) LV_IN; q += LV_T / 64)
       {
@@ -751,6 +762,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
          total += rhi[s] - rlo[s];
          totexc += s < nin ? sm.nxe[s] : 0;
       }
+      LV_STAMP(3);
       if (empty) totexc = 0;
       if (totexc) totexc = lv_count_exc(sm, recs, klo_t, klo_i, khi_t, khi_i, has_lo, has_hi);
 
@@ -760,6 +772,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
          if (tid < (uint32_t) LV_IN) { sm.lo[tid] = rlo[tid]; sm.hi[tid] = rhi[tid]; }
          __syncthreads();
          lv_load_merge(sm, recs, klo_t, klo_i, khi_t, khi_i, has_lo, has_hi, !empty);
+         LV_STAMP(4);
          if (j == 0)
          {
             if (tid == 0 && c.analytical && sm.E > 0 && cyc1(sm.r[sm.perm[0]].t) == 0) sm.cy.mode = 1;
@@ -772,12 +785,14 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
          {
             so = lv_scan(sm, 0, sm.E);
             have = true;
+            LV_STAMP(5);
             if (j > 0)
             {
                if (tid == 0) lv_publish_agg(st, flags, g, so);
                if (wv == 0) lv_lookback(sm, sm.io.gbase, j, flags, st, errflag);
                __syncthreads();
             }
+            LV_STAMP(6);
             // FIFO: the inclusive state is (carry) x (aggregate); publish before the outputs
             if (tid == 0 && !sm.cy.mode)
             {
@@ -791,6 +806,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
             __syncthreads();
          }
          lv_process(sm, c, have, so, recs, samp_t, samp_id, nexc, final_ps, errflag);
+         LV_STAMP(7);
       }
       else
       {
@@ -891,6 +907,12 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
       if (tid == 0)
       {
          if (!sm.published) lv_publish_inc(st, flags, g, sm.cy);
+         if (STAMPS && stamps)
+         {
+            stamps[(uint64_t) g * 16 + 8] = __builtin_amdgcn_s_memtime();
+            stamps[(uint64_t) g * 16 + 9] = (uint64_t) j | ((uint64_t) sm.io.dir << 32);
+            stamps[(uint64_t) g * 16 + 10] = sm.st_cnt;
+         }
          atomicAdd(&port_sum[sm.io.port], (unsigned long long) sm.st_sum);
          atomicAdd(&port_cnt[sm.io.port], (unsigned long long) sm.st_cnt);
          if (sm.st_mg1) atomicAdd(&port_mg1[sm.io.port], (unsigned long long) sm.st_mg1);

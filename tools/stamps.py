@@ -1,4 +1,4 @@
-"""Diagnostic: per-phase s_memtime stamps of the chunk kernel (GNOC_STAMPS=1).
+"""Diagnostic: per-phase s_memtime stamps of the v3 level kernel (GNOC_STAMPS=1).
 Prints median cycles per phase by port direction. Dev tool, not a test."""
 import ctypes
 import os
@@ -23,21 +23,16 @@ lib.gnoc_debug_stamps(eng._h, None, 0, ctypes.byref(n))
 buf = np.zeros(n.value * 16, np.uint64)
 lib.gnoc_debug_stamps(eng._h, buf.ctypes.data, buf.size, ctypes.byref(n))
 st = buf.reshape(-1, 16).astype(np.int64)
+st = st[st[:, 8] > 0]
 j = st[:, 9] & 0xFFFFFFFF
 d = st[:, 9] >> 32
-names = ["dq->desc", "keys", "search", "load+merge", "aggscan", "publish_agg", "lookback", "process", "publish_inc"]
-print("chunks", st.shape[0], "summary", eng.summary())
+names = ["", "desc", "keys", "search", "load+merge", "scan", "pub+lookback", "process", "tail"]
+print("chunks", st.shape[0], "summary", eng.summary(), "records/chunk median", int(np.median(st[:, 10])))
 for dirn, label in ((5, "INJ"), (2, "RIGHT"), (1, "LEFT"), (4, "UP"), (3, "DOWN"), (0, "SELF")):
     m = (d == dirn) & (j > 0) & (st[:, 7] > 0)
     if not m.any():
         continue
     s = st[m]
-    out = []
-    for k in range(1, 9):
-        prev = k - 1
-        if k == 7 and True:
-            prev = 6
-        dd = s[:, k] - s[:, prev]
-        out.append(f"{names[k]}={int(np.median(dd))}")
+    out = [f"{names[k]}={int(np.median(s[:, k] - s[:, k - 1]))}" for k in range(1, 9)]
     tot = np.median(s[:, 8] - s[:, 0])
     print(f"{label:6s} n={m.sum():6d} total={int(tot)} " + " ".join(out))
