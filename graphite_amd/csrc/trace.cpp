@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -134,4 +135,77 @@ extern "C" int gnoc_trace_synthetic(int32_t W, int32_t H, double f, double load,
          bits[pos] = nbits;
       }
    return GNOC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// on-disk trace format (include/gnoc.h, gnoc_trace_header)
+// ---------------------------------------------------------------------------
+static_assert(sizeof(gnoc_trace_header) == 128, "trace header is 128 bytes");
+
+extern "C" int gnoc_trace_file_write(const char* path, const gnoc_config* cfg, const gnoc_packets* pk, size_t n)
+{
+   if (!path || !cfg || !pk) return GNOC_EINVAL;
+   if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return GNOC_EINVAL;
+   FILE* f = std::fopen(path, "wb");
+   if (!f) return GNOC_EINVAL;
+   gnoc_trace_header h;
+   std::memset(&h, 0, sizeof(h));
+   std::memcpy(h.magic, GNOC_TRACE_MAGIC, 8);
+   h.version = 1;
+   h.header_bytes = sizeof(h);
+   h.num_packets = n;
+   h.cfg = *cfg;
+   bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1;
+   ok = ok && (n == 0 || std::fwrite(pk->inject_ps, 8, n, f) == n);
+   ok = ok && (n == 0 || std::fwrite(pk->src, 4, n, f) == n);
+   ok = ok && (n == 0 || std::fwrite(pk->dst, 4, n, f) == n);
+   ok = ok && (n == 0 || std::fwrite(pk->bits, 4, n, f) == n);
+   if (pk->flags) ok = ok && (n == 0 || std::fwrite(pk->flags, 4, n, f) == n);
+   else
+   {
+      std::vector<uint32_t> z(std::min<size_t>(n, 1 << 20), 0);
+      for (size_t done = 0; ok && done < n; done += z.size())
+      {
+         const size_t k = std::min(z.size(), n - done);
+         ok = std::fwrite(z.data(), 4, k, f) == k;
+      }
+   }
+   ok = (std::fclose(f) == 0) && ok;
+   return ok ? GNOC_OK : GNOC_EINVAL;
+}
+
+extern "C" int gnoc_trace_file_read(const char* path, gnoc_config* cfg_out, uint64_t* inject_ps, uint32_t* src,
+                                    uint32_t* dst, uint32_t* bits, uint32_t* flags, size_t capacity, size_t* n_out)
+{
+   if (!path || !n_out) return GNOC_EINVAL;
+   FILE* f = std::fopen(path, "rb");
+   if (!f) return GNOC_EINVAL;
+   gnoc_trace_header h;
+   bool ok = std::fread(&h, sizeof(h), 1, f) == 1;
+   ok = ok && std::memcmp(h.magic, GNOC_TRACE_MAGIC, 8) == 0 && h.version == 1 && h.header_bytes == sizeof(h);
+   if (!ok)
+   {
+      std::fclose(f);
+      return GNOC_ETRACE;
+   }
+   const size_t n = (size_t) h.num_packets;
+   *n_out = n;
+   if (cfg_out) *cfg_out = h.cfg;
+   if (!inject_ps)
+   {
+      std::fclose(f);
+      return GNOC_OK;
+   }
+   if (capacity < n || !src || !dst || !bits)
+   {
+      std::fclose(f);
+      return GNOC_EINVAL;
+   }
+   ok = n == 0 || std::fread(inject_ps, 8, n, f) == n;
+   ok = ok && (n == 0 || std::fread(src, 4, n, f) == n);
+   ok = ok && (n == 0 || std::fread(dst, 4, n, f) == n);
+   ok = ok && (n == 0 || std::fread(bits, 4, n, f) == n);
+   if (flags) ok = ok && (n == 0 || std::fread(flags, 4, n, f) == n);
+   std::fclose(f);
+   return ok ? GNOC_OK : GNOC_ETRACE;
 }

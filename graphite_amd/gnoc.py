@@ -33,7 +33,7 @@ EXPORTED = (
     "gnoc_config_default", "gnoc_create", "gnoc_submit", "gnoc_submit_device", "gnoc_run",
     "gnoc_get_packet_results", "gnoc_get_port_stats", "gnoc_get_summary", "gnoc_device_final_ps",
     "gnoc_last_error", "gnoc_destroy", "gnoc_trace_synthetic", "gnoc_abi_version",
-    "gnoc_set_profiling", "gnoc_get_kernel_stats",
+    "gnoc_set_profiling", "gnoc_get_kernel_stats", "gnoc_trace_file_write", "gnoc_trace_file_read",
 )
 
 
@@ -109,6 +109,9 @@ def load() -> ctypes.CDLL:
         ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_uint64, ctypes.c_double, ctypes.c_int32, vp, vp, vp, vp, sz, ctypes.POINTER(sz)]
     lib.gnoc_abi_version.argtypes = []
+    lib.gnoc_trace_file_write.argtypes = [ctypes.c_char_p, ctypes.POINTER(GnocConfig), ctypes.POINTER(GnocPackets), sz]
+    lib.gnoc_trace_file_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(GnocConfig), vp, vp, vp, vp, vp, sz,
+                                         ctypes.POINTER(sz)]
     lib.gnoc_set_profiling.argtypes = [vp, ctypes.c_int]
     lib.gnoc_get_kernel_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(sz)]
@@ -194,6 +197,39 @@ def synthetic_trace(width: int, height: int, offered_load: float, packets_per_ti
     if rc:
         raise GnocError(rc, "synthetic trace generation failed (invalid LCG schedule for this tile count?)")
     return t
+
+
+def write_trace_file(path: str, cfg: "EngineConfig", tr: Trace) -> None:
+    """The on-disk trace format of include/gnoc.h (gnoc_trace_header + SoA)."""
+    lib = load()
+    tr = tr.normalized()
+    c = cfg.to_c()
+    pk = GnocPackets(tr.inject_ps.ctypes.data, tr.src.ctypes.data, tr.dst.ctypes.data, tr.bits.ctypes.data,
+                     tr.flags.ctypes.data)
+    rc = lib.gnoc_trace_file_write(path.encode(), ctypes.byref(c), ctypes.byref(pk), len(tr))
+    if rc:
+        raise GnocError(rc, f"cannot write trace {path}")
+
+
+def read_trace_file(path: str):
+    """-> (EngineConfig, Trace)"""
+    lib = load()
+    c = GnocConfig()
+    n = ctypes.c_size_t(0)
+    rc = lib.gnoc_trace_file_read(path.encode(), ctypes.byref(c), None, None, None, None, None, 0, ctypes.byref(n))
+    if rc:
+        raise GnocError(rc, f"cannot read trace {path}")
+    N = n.value
+    t = Trace(np.empty(N, np.uint64), np.empty(N, np.uint32), np.empty(N, np.uint32), np.empty(N, np.uint32),
+              np.empty(N, np.uint32))
+    rc = lib.gnoc_trace_file_read(path.encode(), None, t.inject_ps.ctypes.data, t.src.ctypes.data, t.dst.ctypes.data,
+                                  t.bits.ctypes.data, t.flags.ctypes.data, N, ctypes.byref(n))
+    if rc:
+        raise GnocError(rc, f"corrupt trace {path}")
+    cfg = EngineConfig(**{f[0]: getattr(c, f[0]) for f in GnocConfig._fields_})
+    for k in ("contention_enabled", "analytical_enabled", "broadcast_tree_enabled"):
+        setattr(cfg, k, bool(getattr(cfg, k)))
+    return cfg, t
 
 
 @dataclass

@@ -1,0 +1,276 @@
+// network_model_emesh_hop_by_hop_hip.cc -- see the header for the reference
+// interface each member mirrors.  Host C++ only; all timing runs behind the
+// C ABI in libgnoc.so (include/gnoc.h).
+#include "network_model_emesh_hop_by_hop_hip.h"
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+namespace graphite_amd {
+
+// ---------------------------------------------------------------------------
+// CfgView: Sim()->getCfg()->get{Int,Bool,Float,String}(key, default)
+// ---------------------------------------------------------------------------
+int CfgView::getInt(const std::string& key, int dflt) const
+{
+   auto it = _kv.find(key);
+   return it == _kv.end() ? dflt : (int) std::strtol(it->second.c_str(), nullptr, 0);
+}
+
+bool CfgView::getBool(const std::string& key, bool dflt) const
+{
+   auto it = _kv.find(key);
+   if (it == _kv.end()) return dflt;
+   const std::string& v = it->second;
+   return v == "true" || v == "1" || v == "yes";
+}
+
+double CfgView::getFloat(const std::string& key, double dflt) const
+{
+   auto it = _kv.find(key);
+   return it == _kv.end() ? dflt : std::strtod(it->second.c_str(), nullptr);
+}
+
+std::string CfgView::getString(const std::string& key, const std::string& dflt) const
+{
+   auto it = _kv.find(key);
+   return it == _kv.end() ? dflt : it->second;
+}
+
+gnoc_config CfgView::toEngineConfig() const
+{
+   gnoc_config c;
+   const int tiles = getInt("general/total_cores", 64);                         // carbon_sim.cfg:34
+   gnoc_config_default(&c, tiles);
+   c.flit_width = getInt("network/emesh_hop_by_hop/flit_width", 64);             // emesh_hop_by_hop.cc:22
+   c.broadcast_tree_enabled = getBool("network/emesh_hop_by_hop/broadcast_tree_enabled", true);   // :25
+   c.router_delay = (uint64_t) getInt("network/emesh_hop_by_hop/router/delay", 1);                // :95
+   c.link_delay = (uint64_t) getInt("network/emesh_hop_by_hop/link/delay", 1);                    // :96
+   c.contention_enabled = getBool("network/emesh_hop_by_hop/queue_model/enabled", true);          // :97
+   const std::string qt = getString("network/emesh_hop_by_hop/queue_model/type", "history_tree"); // :98
+   c.queue_type = qt == "history_tree" ? GNOC_QUEUE_HISTORY_TREE : -1;
+   c.analytical_enabled = getBool("queue_model/history_tree/analytical_model_enabled", true);    // carbon_sim.cfg:392
+   c.max_list_size = getInt("queue_model/history_tree/max_list_size", 100);                     // carbon_sim.cfg:391
+   c.tile_width_mm = getFloat("general/tile_width", 1.0);                                        // carbon_sim.cfg:64
+   c.frequency_ghz = getFloat("network/frequency", 1.0);   // the network's DVFS domain (dvfs_manager.cc:243-250)
+   return c;
+}
+
+// ---------------------------------------------------------------------------
+// NetworkModelEMeshHopByHopHIP
+// ---------------------------------------------------------------------------
+NetworkModelEMeshHopByHopHIP::NetworkModelEMeshHopByHopHIP(const CfgView& cfg, int device)
+   : NetworkModelEMeshHopByHopHIP([&] {
+        gnoc_config c = cfg.toEngineConfig();
+        c.device = device;
+        return c;
+     }())
+{
+}
+
+NetworkModelEMeshHopByHopHIP::NetworkModelEMeshHopByHopHIP(const gnoc_config& cfg) : _cfg(cfg)
+{
+   if (_cfg.queue_type != GNOC_QUEUE_HISTORY_TREE)
+      throw NetworkModelError(GNOC_EUNSUPPORTED, "queue_model/type: only history_tree is implemented");
+   const int rc = gnoc_create(&_cfg, &_eng);
+   if (rc)
+      throw NetworkModelError(rc, "gnoc_create rejected the emesh_hop_by_hop configuration (status " +
+                                      std::to_string(rc) + ")");
+   // derived topology (initializeEMeshTopologyParams, emesh_hop_by_hop.cc:47-70)
+   if (_cfg.mesh_width <= 0 || _cfg.mesh_height <= 0)
+   {
+      _cfg.mesh_width = (int32_t) std::floor(std::sqrt((double) _cfg.num_tiles));
+      _cfg.mesh_height = (int32_t) std::ceil(1.0 * _cfg.num_tiles / _cfg.mesh_width);
+   }
+}
+
+NetworkModelEMeshHopByHopHIP::~NetworkModelEMeshHopByHopHIP() { gnoc_destroy(_eng); }
+
+void NetworkModelEMeshHopByHopHIP::check(int status, const char* what) const
+{
+   if (status) throw NetworkModelError(status, std::string(what) + ": " + gnoc_last_error(_eng));
+}
+
+void NetworkModelEMeshHopByHopHIP::reserve(size_t n)
+{
+   _inj.reserve(n);
+   _src.reserve(n);
+   _dst.reserve(n);
+   _bits.reserve(n);
+   _flags.reserve(n);
+}
+
+uint32_t NetworkModelEMeshHopByHopHIP::routePacket(const NetPacket& pkt)
+{
+   // NetworkModel::__routePacket asserts (network_model.cc:109-113), here as errors
+   if (pkt.sender < 0 || pkt.sender >= _cfg.num_tiles || pkt.receiver < 0 || pkt.receiver >= _cfg.num_tiles)
+      throw NetworkModelError(GNOC_ETRACE, "pkt_sender/pkt_receiver outside the application tiles");
+   if (!_inj.empty() && pkt.time < _inj.back())
+      throw NetworkModelError(GNOC_ETRACE, "packets must be routed in time order");
+   _inj.push_back(pkt.time);
+   _src.push_back((uint32_t) pkt.sender);
+   _dst.push_back((uint32_t) pkt.receiver);
+   _bits.push_back(pkt.modeled_bits);
+   _flags.push_back(pkt.modeled ? 0u : GNOC_PKT_UNMODELED);
+   _ran = false;
+   return (uint32_t) (_inj.size() - 1);
+}
+
+void NetworkModelEMeshHopByHopHIP::run()
+{
+   gnoc_packets pk;
+   pk.inject_ps = _inj.data();
+   pk.src = _src.data();
+   pk.dst = _dst.data();
+   pk.bits = _bits.data();
+   pk.flags = _flags.data();
+   const size_t n = _inj.size();
+   check(gnoc_submit(_eng, &pk, n), "gnoc_submit");
+   check(gnoc_run(_eng), "gnoc_run");
+   _final.resize(n);
+   _zl.resize(n);
+   _ct.resize(n);
+   check(gnoc_get_packet_results(_eng, _final.data(), _zl.data(), _ct.data(), n), "gnoc_get_packet_results");
+   const size_t np = (size_t) _cfg.num_tiles * GNOC_PORTS_PER_TILE;
+   _psum.resize(np);
+   _pcnt.resize(np);
+   _pmg1.resize(np);
+   check(gnoc_get_port_stats(_eng, _psum.data(), _pcnt.data(), _pmg1.data(), np), "gnoc_get_port_stats");
+   _ran = true;
+}
+
+gnoc_summary NetworkModelEMeshHopByHopHIP::summary() const
+{
+   gnoc_summary s;
+   check(gnoc_get_summary(_eng, &s), "gnoc_get_summary");
+   return s;
+}
+
+// Time::toCycles / toNanosec (common/misc/time_types.h:99-109)
+static uint64_t ps_to_cycles(uint64_t ps, double f) { return (uint64_t) std::ceil(((double) ps * f) / 1.0e3); }
+static uint64_t ps_to_ns(uint64_t ps) { return (uint64_t) std::ceil(((double) ps) / 1.0e3); }
+
+void NetworkModelEMeshHopByHopHIP::outputSummary(std::ostream& out, int tile) const
+{
+   if (!_ran) throw NetworkModelError(GNOC_ESTATE, "outputSummary before run()");
+   if (tile < 0 || tile >= _cfg.num_tiles) throw NetworkModelError(GNOC_EINVAL, "tile outside the mesh");
+   const uint32_t fw = (uint32_t) _cfg.flit_width;
+   auto flits = [&](uint32_t bits) -> uint64_t { return (bits % fw) ? bits / fw + 1 : bits / fw; };
+   // updateSendCounters / updateReceiveCounters (network_model.cc:229-272): modeled,
+   // non-self packets; broadcast is not produced by this path.
+   uint64_t ps = 0, fs = 0, bs = 0, pr = 0, fr = 0, br = 0, lat = 0, cont = 0;
+   for (size_t i = 0; i < _inj.size(); i++)
+   {
+      if (_src[i] == _dst[i] || _flags[i]) continue;
+      if ((int) _src[i] == tile) { ps++; fs += flits(_bits[i]); bs += _bits[i]; }
+      if ((int) _dst[i] == tile)
+      {
+         pr++;
+         fr += flits(_bits[i]);
+         br += _bits[i];
+         lat += _zl[i] + _ct[i];
+         cont += _ct[i];
+      }
+   }
+   const double f = _cfg.frequency_ghz;
+   out << "    Total Packets Sent: " << ps << "\n";
+   out << "    Total Flits Sent: " << fs << "\n";
+   out << "    Total Bits Sent: " << bs << "\n";
+   out << "    Total Packets Broadcasted: 0\n";
+   out << "    Total Flits Broadcasted: 0\n";
+   out << "    Total Bits Broadcasted: 0\n";
+   out << "    Total Packets Received: " << pr << "\n";
+   out << "    Total Flits Received: " << fr << "\n";
+   out << "    Total Bits Received: " << br << "\n";
+   if (pr > 0)
+   {
+      out << "    Average Packet Latency (in clock cycles): " << ((float) ps_to_cycles(lat, f)) / pr << "\n";
+      out << "    Average Packet Latency (in nanoseconds): " << ((float) ps_to_ns(lat)) / pr << "\n";
+      out << "    Average Contention Delay (in clock cycles): " << ((float) ps_to_cycles(cont, f)) / pr << "\n";
+      out << "    Average Contention Delay (in nanoseconds): " << ((float) ps_to_ns(cont)) / pr << "\n";
+   }
+   else
+   {
+      out << "    Average Packet Latency (in clock cycles): 0\n";
+      out << "    Average Packet Latency (in nanoseconds): 0\n";
+      out << "    Average Contention Delay (in clock cycles): 0\n";
+      out << "    Average Contention Delay (in nanoseconds): 0\n";
+   }
+   // outputContentionModelsSummary: the mesh router's 5 output ports
+   uint64_t sd = 0, sp = 0, sa = 0;
+   for (int p = 0; p < 5; p++)
+   {
+      const size_t k = (size_t) tile * GNOC_PORTS_PER_TILE + p;
+      sd += _psum[k];
+      sp += _pcnt[k];
+      sa += _pmg1[k];
+   }
+   out << "    Contention Counters:\n";
+   out << "      Average EMesh Router Contention Delay: " << (sp > 0 ? ((float) sd) / sp : 0.0f) << "\n";
+   out << "      Average EMesh Router Link Utilization: 0\n";
+   out << "      Analytical Models Used (%): " << (sp > 0 ? ((float) sa * 100) / sp : 0.0f) << "\n";
+}
+
+bool NetworkModelEMeshHopByHopHIP::isTileCountPermissible(int tile_count)
+{
+   const int w = (int) std::floor(std::sqrt((double) tile_count));
+   const int h = (int) std::ceil(1.0 * tile_count / w);
+   return tile_count == w * h;
+}
+
+std::vector<int> NetworkModelEMeshHopByHopHIP::computeMemoryControllerPositions(int num, int tile_count)
+{
+   const int W = (int) std::floor(std::sqrt((double) tile_count));
+   const int H = (int) std::ceil(1.0 * tile_count / W);
+   const int mw = (int) std::floor(std::sqrt((double) num));
+   const int mh = (int) std::ceil(1.0 * num / mw);
+   std::vector<int> out;
+   for (int j = 0; j < mh && (int) out.size() < num; j++)
+      for (int i = 0; i < mw && (int) out.size() < num; i++)
+      {
+         int sx = W / mw, sy = H / mh;
+         const int bx = i * sx, by = j * sy;
+         if (i == mw - 1) sx = W - (mw - 1) * sx;
+         if (j == mh - 1) sy = H - (mh - 1) * sy;
+         out.push_back((bx + sx / 2) + (by + sy / 2) * W);
+      }
+   return out;
+}
+
+void NetworkModelEMeshHopByHopHIP::writeTrace(const std::string& path) const
+{
+   gnoc_packets pk;
+   pk.inject_ps = _inj.data();
+   pk.src = _src.data();
+   pk.dst = _dst.data();
+   pk.bits = _bits.data();
+   pk.flags = _flags.data();
+   const int rc = gnoc_trace_file_write(path.c_str(), &_cfg, &pk, _inj.size());
+   if (rc) throw NetworkModelError(rc, "cannot write trace " + path);
+}
+
+NetworkModelEMeshHopByHopHIP* NetworkModelEMeshHopByHopHIP::fromTraceFile(const std::string& path, int device)
+{
+   gnoc_config cfg;
+   size_t n = 0;
+   int rc = gnoc_trace_file_read(path.c_str(), &cfg, nullptr, nullptr, nullptr, nullptr, nullptr, 0, &n);
+   if (rc) throw NetworkModelError(rc, "cannot read trace " + path);
+   cfg.device = device;
+   auto* m = new NetworkModelEMeshHopByHopHIP(cfg);
+   m->_inj.resize(n);
+   m->_src.resize(n);
+   m->_dst.resize(n);
+   m->_bits.resize(n);
+   m->_flags.resize(n);
+   rc = gnoc_trace_file_read(path.c_str(), nullptr, m->_inj.data(), m->_src.data(), m->_dst.data(), m->_bits.data(),
+                             m->_flags.data(), n, &n);
+   if (rc)
+   {
+      delete m;
+      throw NetworkModelError(rc, "corrupt trace " + path);
+   }
+   return m;
+}
+
+}  // namespace graphite_amd

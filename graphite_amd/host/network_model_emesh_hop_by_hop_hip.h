@@ -1,0 +1,143 @@
+// network_model_emesh_hop_by_hop_hip.h -- C++ host side of the MI355X
+// emesh_hop_by_hop timing engine, shaped like the reference's network-model
+// plug-in so a Graphite maintainer can register it next to the CPU model.
+//
+// Reference interface it mirrors (INTEGRATION.md shows the registration):
+//   NetworkModel                          common/network/network_model.h:39-207
+//     createModel / parseNetworkType       network_model.cc:50-71, 318-335
+//     __routePacket (SEND_TILE)            network_model.cc:87-116
+//     processReceivedPacket                network_model.cc:142-150
+//     outputSummary                        network_model.cc:274-316
+//     isTileCountPermissible, computeMemoryControllerPositions
+//                                          network_model.cc:337-411
+//   NetworkModelEMeshHopByHop             common/network/models/network_model_emesh_hop_by_hop.{h,cc}
+//     ctor config reads                    :16-38  (network/emesh_hop_by_hop/...)
+//     routePacket                          :146-264
+//     outputContentionModelsSummary        :471-493
+//   RouterModel contention counters       common/network/components/router/router_model.cc:136-215
+//
+// Trace mode: the reference routes one packet per call and returns its hops;
+// the engine times a whole batch at once.  routePacket() records a packet
+// (what Network::netSend hands the model at SEND_TILE), run() times every hop
+// of every recorded packet on the GPU through the C ABI (include/gnoc.h), and
+// the results carry the three NetPacket fields the reference updates
+// (time, zero_load_delay, contention_delay; network.h:27-55).
+//
+// Errors: the reference aborts through LOG_PRINT_ERROR (common/misc/log.cc:
+// 360-362); this layer throws NetworkModelError carrying the C ABI's status
+// and message (uncaught, that terminates the process like the reference).
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <ostream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "gnoc.h"
+
+namespace graphite_amd {
+
+class NetworkModelError : public std::runtime_error
+{
+public:
+   NetworkModelError(int status, const std::string& msg) : std::runtime_error(msg), status(status) {}
+   int status;
+};
+
+// The Sim()->getCfg() view of carbon_sim.cfg keys the path reads (SURVEY.md
+// section 5), with the reference's defaults (carbon_sim.cfg:276-313, 375-392).
+class CfgView
+{
+public:
+   void set(const std::string& key, const std::string& value) { _kv[key] = value; }
+   int getInt(const std::string& key, int dflt) const;
+   bool getBool(const std::string& key, bool dflt) const;
+   double getFloat(const std::string& key, double dflt) const;
+   std::string getString(const std::string& key, const std::string& dflt) const;
+   // gnoc_config for general/total_cores tiles, as NetworkModelEMeshHopByHop's ctor reads it
+   gnoc_config toEngineConfig() const;
+
+private:
+   std::map<std::string, std::string> _kv;
+};
+
+// Trace-mode NetPacket: the fields this path reads (network.h:27-55).
+struct NetPacket
+{
+   uint64_t time = 0;          // NetPacket::time at netSend, picoseconds
+   int32_t sender = 0;         // TILE_ID(pkt.sender)
+   int32_t receiver = 0;       // TILE_ID(pkt.receiver)
+   uint32_t modeled_bits = 0;  // NetworkModel::getModeledLength(pkt)
+   bool modeled = true;        // NetworkModel::isModelEnabled(pkt)
+   // outputs, filled by run(): NetPacket fields after processReceivedPacket
+   uint64_t zero_load_delay = 0;
+   uint64_t contention_delay = 0;
+};
+
+class NetworkModelEMeshHopByHopHIP
+{
+public:
+   static constexpr const char* kTypeName = "emesh_hop_by_hop_hip";
+
+   explicit NetworkModelEMeshHopByHopHIP(const CfgView& cfg, int device = 0);
+   explicit NetworkModelEMeshHopByHopHIP(const gnoc_config& cfg);
+   ~NetworkModelEMeshHopByHopHIP();
+   NetworkModelEMeshHopByHopHIP(const NetworkModelEMeshHopByHopHIP&) = delete;
+   NetworkModelEMeshHopByHopHIP& operator=(const NetworkModelEMeshHopByHopHIP&) = delete;
+
+   // NetworkModel::__routePacket at SEND_TILE, trace mode: record one packet.
+   // Packets must arrive in (time, id) order, as the reference's event loop
+   // hands them to the model.  Returns the packet id (its index).
+   uint32_t routePacket(const NetPacket& pkt);
+   void reserve(size_t n);
+
+   // Time every hop of every recorded packet (one gnoc_submit + gnoc_run).
+   void run();
+
+   // Results of the last run(), indexed by packet id: NetPacket::time,
+   // zero_load_delay, contention_delay after processReceivedPacket.
+   const std::vector<uint64_t>& packetTime() const { return _final; }
+   const std::vector<uint64_t>& packetZeroLoadDelay() const { return _zl; }
+   const std::vector<uint64_t>& packetContentionDelay() const { return _ct; }
+
+   // RouterModel::_total_contention_delay / _total_packets per output port
+   // (index tile*6 + GNOC_PORT_*; GNOC_PORT_INJ = the injection router) and
+   // QueueModelHistoryTree::getTotalRequestsUsingAnalyticalModel.
+   const std::vector<uint64_t>& portContentionDelay() const { return _psum; }
+   const std::vector<uint64_t>& portPackets() const { return _pcnt; }
+   const std::vector<uint64_t>& portAnalyticalRequests() const { return _pmg1; }
+
+   // The per-tile sim.out network section: NetworkModel::outputSummary
+   // (network_model.cc:274-316) followed by the emesh contention counters
+   // (network_model_emesh_hop_by_hop.cc:471-493, router_model.cc:146-215;
+   // link utilization is not modelled here and printed as 0).
+   void outputSummary(std::ostream& out, int tile) const;
+
+   gnoc_summary summary() const;
+   int numTiles() const { return _cfg.num_tiles; }
+   int meshWidth() const { return _cfg.mesh_width; }
+   int meshHeight() const { return _cfg.mesh_height; }
+   size_t numPackets() const { return _inj.size(); }
+
+   // Static capability hooks (network_model_emesh_hop_by_hop.cc:309-364).
+   static bool isTileCountPermissible(int tile_count);
+   static std::vector<int> computeMemoryControllerPositions(int num_memory_controllers, int tile_count);
+
+   // On-disk traces (include/gnoc.h, gnoc_trace_header).
+   void writeTrace(const std::string& path) const;
+   static NetworkModelEMeshHopByHopHIP* fromTraceFile(const std::string& path, int device = 0);
+
+private:
+   void check(int status, const char* what) const;
+
+   gnoc_config _cfg;
+   gnoc_engine* _eng = nullptr;
+   std::vector<uint64_t> _inj;
+   std::vector<uint32_t> _src, _dst, _bits, _flags;
+   std::vector<uint64_t> _final, _zl, _ct, _psum, _pcnt, _pmg1;
+   bool _ran = false;
+};
+
+}  // namespace graphite_amd

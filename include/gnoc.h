@@ -181,6 +181,30 @@ int gnoc_trace_synthetic(int32_t mesh_width, int32_t mesh_height, double frequen
                          uint64_t *inject_ps, uint32_t *src, uint32_t *dst, uint32_t *bits,
                          size_t capacity, size_t *n_out);
 
+/* ---- on-disk trace format ----------------------------
+ * A batch captured at Network::netSend / NetworkModel::__routePacket(SEND_TILE)
+ * (network.cc:174-215, network_model.cc:95-107), with the configuration it was
+ * captured under:  gnoc_trace_header (128 bytes, little endian), then the SoA
+ * arrays inject_ps[n] (u64), src[n], dst[n], bits[n], flags[n] (u32 each).   */
+#define GNOC_TRACE_MAGIC "GNOCTRC1"
+typedef struct gnoc_trace_header
+{
+   char     magic[8];            /* GNOC_TRACE_MAGIC                                  */
+   uint32_t version;             /* 1                                                  */
+   uint32_t header_bytes;        /* 128                                                */
+   uint64_t num_packets;
+   gnoc_config cfg;              /* the configuration the trace was captured under     */
+   uint8_t  reserved[128 - 24 - sizeof(gnoc_config)];
+} gnoc_trace_header;
+
+/* Write a (inject_ps, id)-ordered batch and its configuration to `path`. */
+int gnoc_trace_file_write(const char *path, const gnoc_config *cfg, const gnoc_packets *pk, size_t n);
+
+/* Read `path`: with NULL arrays, fills *cfg_out and *n_out only; then call
+ * again with arrays of capacity >= *n_out. */
+int gnoc_trace_file_read(const char *path, gnoc_config *cfg_out, uint64_t *inject_ps, uint32_t *src, uint32_t *dst,
+                         uint32_t *bits, uint32_t *flags, size_t capacity, size_t *n_out);
+
 int gnoc_abi_version(void);
 
 #ifdef __cplusplus
