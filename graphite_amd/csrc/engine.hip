@@ -353,7 +353,7 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    uint64_t records = 0;
    int rc = validate_host_trace(e, pk, n, &records);
    if (rc) return rc;
-   if (record_bound(e, records) >= (1ull << 32)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32 hop records");
+   if (record_bound(e, records) >= (1ull << 31)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^31 hop records");
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    GNOC_HIP(e, e->t_inj.ensure(n * 8));
    GNOC_HIP(e, e->t_src.ensure(n * 4));
@@ -413,7 +413,7 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 16, hipMemcpyDeviceToHost, e->stream));
    GNOC_HIP(e, hipStreamSynchronize(e->stream));
    const uint64_t records = e->h_pinned[0] + e->h_pinned[1];
-   if (record_bound(e, records) >= (1ull << 32)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32 hop records");
+   if (record_bound(e, records) >= (1ull << 31)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^31 hop records");
    e->rec_bound = record_bound(e, records);
    e->submitted = true;
    e->ran = false;
@@ -484,10 +484,9 @@ static int run_levels_v3(gnoc_engine* e)
    GNOC_HIP(e, e->pgb.ensure((size_t) P * 4));
    GNOC_HIP(e, e->lvl_cbase.ensure((size_t) (L + 1) * 4));
    GNOC_HIP(e, e->chunk_port.ensure(chunk_bound * 4));
-   GNOC_HIP(e, e->flags.ensure(chunk_bound * 4));
-   GNOC_HIP(e, e->st.ensure(chunk_bound * 16 * 8));
+   GNOC_HIP(e, e->st.ensure(chunk_bound * LV_STATE_WORDS * 8));
    GNOC_HIP(e, e->lvl_ctr.ensure((size_t) L * 4));
-   GNOC_HIP(e, hipMemsetAsync(e->flags.p, 0, chunk_bound * 4, s));
+   GNOC_HIP(e, hipMemsetAsync(e->st.p, 0, chunk_bound * LV_STATE_WORDS * 8, s));   // look-back granules
    GNOC_HIP(e, hipMemsetAsync(e->lvl_ctr.p, 0, (size_t) L * 4, s));
    const uint32_t pg = (P + 255) / 256;
    GNOC_LAUNCH(e, KC_PLAN, k_plan_ports, dim3(pg), dim3(256), 0, s, c, P, e->d_lvl_ports.as<uint32_t>(),
@@ -511,14 +510,14 @@ static int run_levels_v3(gnoc_engine* e)
       if (stamps)
          GNOC_LAUNCH(e, KC_LEVEL, k_level<true>, dim3(e->level_grid), dim3(LV_T), 0, s, c, l, e->lvl_cbase.as<uint32_t>(),
                      e->lvl_ctr.as<unsigned>(), e->chunk_port.as<uint32_t>(), e->pio.as<PortIO3>(), e->recs.as<Rec>(),
-                     e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(), e->flags.as<uint32_t>(),
+                     e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(),
                      e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
                      e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
                      e->counters.as<unsigned>() + 8, e->stamps.as<uint64_t>());
       else
          GNOC_LAUNCH(e, KC_LEVEL, k_level<false>, dim3(e->level_grid), dim3(LV_T), 0, s, c, l, e->lvl_cbase.as<uint32_t>(),
                      e->lvl_ctr.as<unsigned>(), e->chunk_port.as<uint32_t>(), e->pio.as<PortIO3>(), e->recs.as<Rec>(),
-                     e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(), e->flags.as<uint32_t>(),
+                     e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(),
                      e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
                      e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
                      e->counters.as<unsigned>() + 8, (uint64_t*) nullptr);

@@ -15,28 +15,30 @@
 // One workgroup per chunk:
 //   1. key range: an exact index split of the port's largest input; the other
 //      inputs are searched with a 64-ary wave search over 1-in-64 key samples
-//   2. load the ranges (16-B records) into LDS; merge by galloping
+//   2. load the ranges (16-B records) into LDS as SoA keys; merge by galloping
 //      co-iteration (rank = own index + lower bounds in the other inputs)
-//   3. block max-plus scan of the chunk: element map X -> max(X + F, t + F),
+//   3. each thread pulls its contiguous merged segment (<= 8 records) into
+//      registers; block max-plus scan: element map X -> max(X + F, t + F),
 //      composition (a1,b1).(a2,b2) = (a1 + a2, max(b1 + a2, b2)), plus per
 //      next-direction record counts (output positions)
-//   4. decoupled look-back over the port's earlier chunks for the carried queue
-//      state (aggregate published first, inclusive state right after)
-//   5. recurrence per thread segment, departure times written back into LDS
-//   6. output pass, lanes over consecutive merged positions, so each wave's
-//      records for one next direction land at consecutive HBM addresses
+//   4. decoupled look-back over the port's earlier chunks in ONE round trip:
+//      every state word is an 8-byte self-validating granule (zeroed per run)
+//   5. recurrence and stores straight from registers
 // Only f == 1 GHz and max_list_size >= 3 take this path (engine.hip).
 #include "common.h"
 
 namespace gnoc {
 
-constexpr int LV_T = 256;          // threads per workgroup
-constexpr int LV_CAP = 2048;       // records one leaf holds in LDS
-constexpr int LV_IN = 4;           // input slots per port (SELF, UP, DOWN have 4)
-constexpr int LV_SEG = LV_IN + 1;  // + the exception segment
-constexpr int LV_MAXLEAF = 32;     // leaves per chunk (bursts); beyond -> errflag, v1 rerun
-constexpr uint32_t LV_CTGT = 1200; // target records per chunk
+constexpr int LV_T = 256;                // threads per workgroup
+constexpr int LV_CAP = 1792;             // records one leaf holds in LDS
+constexpr int LV_PER = LV_CAP / LV_T;    // records per thread in the scan
+constexpr int LV_IN = 4;                 // input slots per port (SELF, UP, DOWN have 4)
+constexpr int LV_SEG = LV_IN + 1;        // + the exception segment
+constexpr int LV_MAXLEAF = 32;           // leaves per chunk (bursts); beyond -> errflag, v1 rerun
+constexpr uint32_t LV_CTGT = 1200;       // target records per chunk
 constexpr uint32_t LV_SPIN_LIMIT = 1u << 24;
+constexpr uint64_t LV_TAG = 1ull << 63;
+constexpr int LV_STATE_WORDS = 16;       // u64 per chunk state
 
 // Per-port descriptor, built on device by k_plan_ports from the slot layout.
 struct __attribute__((aligned(16))) PortIO3
@@ -64,8 +66,11 @@ struct Carry3
 
 struct LvSmem
 {
-   Rec r[LV_CAP];
-   uint16_t perm[LV_CAP];
+   uint64_t kt[LV_CAP];      // arrival time (ps)
+   uint32_t ki[LV_CAP];      // packet id
+   uint32_t ka[LV_CAP];      // aux: dx | dy << 10 | F << 20
+   uint16_t perm[LV_CAP];    // merged position -> record slot
+   uint16_t tmp[LV_CAP];     // intermediate merge lists
    PortIO3 io;
    Carry3 cy;
    uint64_t wA[LV_T / 64], wB[LV_T / 64], wC[LV_T / 64];
@@ -80,14 +85,19 @@ struct LvSmem
    uint32_t g, j, E, s0;
    uint32_t nexc_leaf, published, nleaf, st_cnt;
    uint32_t st_mg1, pad0, pad1, pad2;
+   uint64_t tm[4];           // debug phase stamps inside a leaf (GNOC_STAMPS)
 };
 
 // ---------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lv_ld_flag(const uint32_t* p)
+// Workgroup barrier for LDS only.  __syncthreads() is a workgroup fence and
+// drains every outstanding global store first (s_waitcnt vmcnt(0)); no thread
+// of a chunk reads global data another thread of it wrote, so the chunk
+// kernel's barriers only need the LDS counter.
+__device__ __forceinline__ void lv_bar()
 {
-   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 __device__ __forceinline__ uint64_t lv_ld(const uint64_t* p)
 {
@@ -101,6 +111,11 @@ __device__ __forceinline__ void lv_st(uint64_t* p, uint64_t v)
 __device__ __forceinline__ bool rlt(const Rec& a, uint64_t t, uint32_t id)
 {
    return a.t < t || (a.t == t && a.id < id);
+}
+__device__ __forceinline__ bool klt(const LvSmem& sm, uint32_t k, uint64_t t, uint32_t id)
+{
+   const uint64_t kt = sm.kt[k];
+   return kt < t || (kt == t && sm.ki[k] < id);
 }
 
 __device__ __forceinline__ uint64_t cyc1(uint64_t ps) { return (ps + 999ull) / 1000ull; }
@@ -120,32 +135,31 @@ __device__ __forceinline__ uint32_t next_dir(uint32_t ax, uint32_t dir, uint32_t
 
 __device__ __forceinline__ uint32_t cfield(uint64_t c, uint32_t d) { return (uint32_t) ((c >> (12 * d)) & 0xFFFu); }
 
-// lower bound of (t,id) in LDS records [lo, hi)
-__device__ __forceinline__ uint32_t lds_lb(const Rec* __restrict__ r, uint32_t lo, uint32_t hi, uint64_t t, uint32_t id)
+// lower bound of (t,id) in LDS keys [lo, hi)
+__device__ __forceinline__ uint32_t lds_lb(const LvSmem& sm, uint32_t lo, uint32_t hi, uint64_t t, uint32_t id)
 {
    while (lo < hi)
    {
       const uint32_t mid = (lo + hi) >> 1;
-      if (rlt(r[mid], t, id)) lo = mid + 1;
+      if (klt(sm, mid, t, id)) lo = mid + 1;
       else hi = mid;
    }
    return lo;
 }
 
-// lower bound of (t,id) in [lo, end), knowing every record before lo is smaller
-__device__ __forceinline__ uint32_t lds_gallop(const Rec* __restrict__ r, uint32_t lo, uint32_t end, uint64_t t,
-                                               uint32_t id)
+// lower bound of (t,id) in [lo, end), knowing every key before lo is smaller
+__device__ __forceinline__ uint32_t lds_gallop(const LvSmem& sm, uint32_t lo, uint32_t end, uint64_t t, uint32_t id)
 {
    uint32_t step = 1, hi;
    for (;;)
    {
       const uint32_t pr = lo + step - 1;
       if (pr >= end) { hi = end; break; }
-      if (!rlt(r[pr], t, id)) { hi = pr; break; }
+      if (!klt(sm, pr, t, id)) { hi = pr; break; }
       lo = pr + 1;
       step <<= 1;
    }
-   return lds_lb(r, lo, hi, t, id);
+   return lds_lb(sm, lo, hi, t, id);
 }
 
 // 64-ary lower_bound of key (kt,ki) in the sorted main part [0,n) of a slot,
@@ -184,9 +198,9 @@ __device__ uint32_t lv_count_exc(LvSmem& sm, const Rec* __restrict__ recs, uint6
                                  uint64_t khi_t, uint32_t khi_i, bool has_lo, bool has_hi)
 {
    const uint32_t tid = threadIdx.x;
-   __syncthreads();
+   lv_bar();
    if (tid == 0) sm.nexc_leaf = 0;
-   __syncthreads();
+   lv_bar();
    uint32_t mine = 0;
    for (uint32_t s = 0; s < sm.io.nin; s++)
    {
@@ -200,10 +214,131 @@ __device__ uint32_t lv_count_exc(LvSmem& sm, const Rec* __restrict__ recs, uint6
       }
    }
    if (mine) atomicAdd(&sm.nexc_leaf, mine);
-   __syncthreads();
+   lv_bar();
    const uint32_t n = sm.nexc_leaf;
-   __syncthreads();
+   lv_bar();
    return n;
+}
+
+// ---------------------------------------------------------------------------
+// merge-path merging of sorted segments in LDS
+// A list is a sorted run of record slots: the identity range [off, off+n) of
+// the loaded records (idx == nullptr) or idx[off .. off+n).
+// ---------------------------------------------------------------------------
+struct MList
+{
+   const uint16_t* idx;
+   uint32_t off, n;
+};
+
+__device__ __forceinline__ uint32_t ml_at(const MList& l, uint32_t i) { return l.idx ? l.idx[l.off + i] : l.off + i; }
+
+// Output positions [d0, d1) of merge(A, B) -> out[d] (d relative to the job).
+// One diagonal binary search, then a sequential merge with the two head keys in
+// registers: one dependent LDS read per output.
+__device__ void mp_merge_part(const LvSmem& sm, const MList& A, const MList& B, uint16_t* out, uint32_t d0, uint32_t d1)
+{
+   if (d0 >= d1) return;
+   uint32_t lo = d0 > B.n ? d0 - B.n : 0, hi = min(d0, A.n);
+   while (lo < hi)
+   {
+      const uint32_t m = (lo + hi) >> 1;
+      const uint32_t sa = ml_at(A, m), sb = ml_at(B, d0 - 1 - m);
+      const uint64_t ta = sm.kt[sa], tb = sm.kt[sb];
+      if (ta < tb || (ta == tb && sm.ki[sa] < sm.ki[sb])) lo = m + 1;
+      else hi = m;
+   }
+   uint32_t i = lo, j = d0 - lo;
+   uint32_t sa = 0, sb = 0;
+   uint64_t ta = ~0ull, tb = ~0ull;
+   uint32_t ia = ~0u, ib = ~0u;
+   if (i < A.n) { sa = ml_at(A, i); ta = sm.kt[sa]; ia = sm.ki[sa]; }
+   if (j < B.n) { sb = ml_at(B, j); tb = sm.kt[sb]; ib = sm.ki[sb]; }
+   for (uint32_t d = d0; d < d1; d++)
+   {
+      if (ta < tb || (ta == tb && ia < ib))
+      {
+         out[d] = (uint16_t) sa;
+         if (++i < A.n) { sa = ml_at(A, i); ta = sm.kt[sa]; ia = sm.ki[sa]; }
+         else { ta = ~0ull; ia = ~0u; }
+      }
+      else
+      {
+         out[d] = (uint16_t) sb;
+         if (++j < B.n) { sb = ml_at(B, j); tb = sm.kt[sb]; ib = sm.ki[sb]; }
+         else { tb = ~0ull; ib = ~0u; }
+      }
+   }
+}
+
+// One merge round: job 1 = merge(A1, B1) -> out1[0, n1), job 2 (optional) =
+// merge(A2, B2) -> out2[0, n2); threads split the n1 + n2 outputs evenly.
+__device__ void mp_round(const LvSmem& sm, const MList& A1, const MList& B1, uint16_t* out1, const MList& A2,
+                         const MList& B2, uint16_t* out2)
+{
+   const uint32_t n1 = A1.n + B1.n, n2 = A2.n + B2.n, n = n1 + n2;
+   const uint32_t per = (n + LV_T - 1) / LV_T;
+   const uint32_t d0 = min(threadIdx.x * per, n), d1 = min(d0 + per, n);
+   mp_merge_part(sm, A1, B1, out1, min(d0, n1), min(d1, n1));
+   if (n2) mp_merge_part(sm, A2, B2, out2, max(d0, n1) - n1, max(d1, n1) - n1);
+}
+
+// Merge the non-empty segments sm.off/len (<= 4 inputs + exceptions) into sm.perm.
+__device__ void lv_merge(LvSmem& sm)
+{
+   const uint32_t tid = threadIdx.x;
+   MList S[LV_SEG];
+   uint32_t ns = 0, E = 0;
+#pragma unroll
+   for (int q = 0; q < LV_SEG; q++)
+   {
+      const uint32_t len = sm.len[q];
+      E += len;
+      MList l;
+      l.idx = nullptr;
+      l.off = sm.off[q];
+      l.n = len;
+      // compact non-empty segments to the front (unrolled selects, no scratch)
+#pragma unroll
+      for (int r = 0; r < LV_SEG; r++)
+         if (len && (uint32_t) r == ns) S[r] = l;
+      ns += len ? 1u : 0u;
+   }
+   const MList none = { nullptr, 0, 0 };
+   if (ns <= 1)
+   {
+      const uint32_t base = ns ? S[0].off : 0;
+      for (uint32_t d = tid; d < E; d += LV_T) sm.perm[d] = (uint16_t) (base + d);
+   }
+   else if (ns == 2)
+   {
+      mp_round(sm, S[0], S[1], sm.perm, none, none, nullptr);
+   }
+   else if (ns == 3)
+   {
+      mp_round(sm, S[0], S[1], sm.tmp, none, none, nullptr);
+      lv_bar();
+      const MList T01 = { sm.tmp, 0, S[0].n + S[1].n };
+      mp_round(sm, T01, S[2], sm.perm, none, none, nullptr);
+   }
+   else
+   {
+      const uint32_t n01 = S[0].n + S[1].n, n23 = S[2].n + S[3].n;
+      mp_round(sm, S[0], S[1], sm.tmp, S[2], S[3], sm.tmp + n01);
+      lv_bar();
+      const MList T01 = { sm.tmp, 0, n01 }, T23 = { sm.tmp, n01, n23 };
+      mp_round(sm, T01, T23, sm.perm, none, none, nullptr);
+      if (ns == 5)
+      {
+         lv_bar();
+         const MList P4 = { sm.perm, 0, n01 + n23 };
+         mp_round(sm, P4, S[4], sm.tmp, none, none, nullptr);
+         lv_bar();
+         for (uint32_t d = tid; d < E; d += LV_T) sm.perm[d] = sm.tmp[d];
+      }
+   }
+   if (tid == 0) sm.E = E;
+   lv_bar();
 }
 
 // ---------------------------------------------------------------------------
@@ -228,13 +363,40 @@ __device__ void lv_load_merge(LvSmem& sm, const Rec* __restrict__ recs, uint64_t
       sm.len[LV_IN] = 0;
       sm.nexc_leaf = 0;
    }
-   __syncthreads();
-   for (uint32_t s = 0; s < nin; s++)
+   lv_bar();
    {
-      const Rec* r = recs + sm.io.base[s] + sm.lo[s];
-      const uint32_t L = sm.len[s], o = sm.off[s];
-      for (uint32_t i = tid; i < L; i += LV_T) sm.r[o + i] = r[i];
+      // all of this thread's (<= LV_PER) records in flight at once, then to LDS
+      const uint32_t tot = sm.off[LV_IN];
+      uint32_t o1 = sm.off[1], o2 = sm.off[2], o3 = sm.off[3];
+      const Rec* r0 = recs + sm.io.base[0] + sm.lo[0];
+      const Rec* r1 = recs + sm.io.base[1] + sm.lo[1] - o1;
+      const Rec* r2 = recs + sm.io.base[2] + sm.lo[2] - o2;
+      const Rec* r3 = recs + sm.io.base[3] + sm.lo[3] - o3;
+      Rec v[LV_PER];
+#pragma unroll
+      for (int k = 0; k < LV_PER; k++)
+      {
+         const uint32_t idx = tid + (uint32_t) k * LV_T;
+         if (idx < tot)
+         {
+            const Rec* r = idx >= o3 ? r3 : idx >= o2 ? r2 : idx >= o1 ? r1 : r0;
+            v[k] = r[idx];
+         }
+      }
+#pragma unroll
+      for (int k = 0; k < LV_PER; k++)
+      {
+         const uint32_t idx = tid + (uint32_t) k * LV_T;
+         if (idx < tot)
+         {
+            sm.kt[idx] = v[k].t;
+            sm.ki[idx] = v[k].id;
+            sm.ka[idx] = v[k].aux;
+         }
+      }
    }
+   lv_bar();
+   if (tid == 0) sm.tm[0] = __builtin_amdgcn_s_memtime();
    bool anyexc = false;
    for (uint32_t s = 0; s < nin; s++) anyexc |= sm.nxe[s] > 0;
    if (anyexc && take_exc)
@@ -251,94 +413,91 @@ __device__ void lv_load_merge(LvSmem& sm, const Rec* __restrict__ recs, uint64_t
             if (ge && lt)
             {
                const uint32_t k = atomicAdd(&sm.nexc_leaf, 1u);
-               if (o + k < (uint32_t) LV_CAP) sm.r[o + k] = v;
+               if (o + k < (uint32_t) LV_CAP)
+               {
+                  sm.kt[o + k] = v.t;
+                  sm.ki[o + k] = v.id;
+                  sm.ka[o + k] = v.aux;
+               }
             }
          }
       }
-      __syncthreads();
+      lv_bar();
       const uint32_t ne = min(sm.nexc_leaf, (uint32_t) LV_CAP - o);
       // odd-even transposition sort of the (few) exceptions
       for (uint32_t ph = 0; ph < ne; ph++)
       {
          for (uint32_t i = 2 * tid + (ph & 1); i + 1 < ne; i += 2 * LV_T)
          {
-            const Rec a = sm.r[o + i], b = sm.r[o + i + 1];
-            if (rlt(b, a.t, a.id)) { sm.r[o + i] = b; sm.r[o + i + 1] = a; }
+            const uint32_t a = o + i, b = o + i + 1;
+            if (klt(sm, b, sm.kt[a], sm.ki[a]))
+            {
+               const uint64_t t = sm.kt[a]; sm.kt[a] = sm.kt[b]; sm.kt[b] = t;
+               uint32_t x = sm.ki[a]; sm.ki[a] = sm.ki[b]; sm.ki[b] = x;
+               x = sm.ka[a]; sm.ka[a] = sm.ka[b]; sm.ka[b] = x;
+            }
          }
-         __syncthreads();
+         lv_bar();
       }
       if (tid == 0) sm.len[LV_IN] = ne;
    }
-   __syncthreads();
-   // merge: rank = own index + lower bounds in every other segment
-   uint32_t off[LV_SEG], end[LV_SEG], p[LV_SEG];
-#pragma unroll
-   for (int s = 0; s < LV_SEG; s++)
-   {
-      off[s] = sm.off[s];
-      end[s] = off[s] + sm.len[s];
-      p[s] = off[s];
-   }
-   const uint32_t E = end[LV_SEG - 1];
-   const uint32_t per = (E + LV_T - 1) / LV_T;
-   const uint32_t k0 = min(tid * per, E), k1 = min(k0 + per, E);
-   int cur = -1;
-   for (uint32_t k = k0; k < k1; k++)
-   {
-      int s = 0;
-#pragma unroll
-      for (int q = 0; q < LV_SEG - 1; q++) s += (k >= end[q]) ? 1 : 0;
-      const Rec me = sm.r[k];
-      uint32_t own = k;
-#pragma unroll
-      for (int q = 0; q < LV_SEG; q++) own -= (q == s) ? off[q] : 0u;
-      uint32_t rank = own;
-#pragma unroll
-      for (int o = 0; o < LV_SEG; o++)
-      {
-         if (o == s || off[o] == end[o]) continue;
-         const uint32_t q = (s != cur) ? lds_lb(sm.r, off[o], end[o], me.t, me.id)
-                                       : lds_gallop(sm.r, p[o], end[o], me.t, me.id);
-         p[o] = q;
-         rank += q - off[o];
-      }
-      cur = s;
-      sm.perm[rank] = (uint16_t) k;
-   }
-   if (tid == 0) sm.E = E;
-   __syncthreads();
+   lv_bar();
+   if (tid == 0) sm.tm[1] = __builtin_amdgcn_s_memtime();
+   lv_merge(sm);
 }
 
 // ---------------------------------------------------------------------------
-// block scan of merged positions [s0, E): per-thread contiguous segments
+// per-thread merged segment in registers + block scan
 // ---------------------------------------------------------------------------
+struct Seg
+{
+   uint64_t t[LV_PER];
+   uint32_t id[LV_PER];
+   uint32_t ax[LV_PER];
+   uint32_t a, n;            // first merged position, records
+};
+
 struct Scan3
 {
    uint64_t eA, eB, eC;   // exclusive prefix of this thread
    uint64_t tA, tB, tC;   // block totals
 };
 
-__device__ __forceinline__ void lv_seg(uint32_t s0, uint32_t E, uint32_t& a, uint32_t& b)
+__device__ __forceinline__ void lv_load_seg(const LvSmem& sm, uint32_t s0, uint32_t E, Seg& sg)
 {
    const uint32_t cnt = E - s0;
-   const uint32_t per = (cnt + LV_T - 1) / LV_T;
-   a = s0 + min(threadIdx.x * per, cnt);
-   b = s0 + min((threadIdx.x + 1) * per, cnt);
+   const uint32_t per = (cnt + LV_T - 1) / LV_T;   // <= LV_PER since E <= LV_CAP
+   const uint32_t a = s0 + min(threadIdx.x * per, cnt);
+   const uint32_t b = s0 + min((threadIdx.x + 1) * per, cnt);
+   sg.a = a;
+   sg.n = b - a;
+#pragma unroll
+   for (int i = 0; i < LV_PER; i++)
+   {
+      if ((uint32_t) i < sg.n)
+      {
+         const uint32_t k = sm.perm[a + i];
+         sg.t[i] = sm.kt[k];
+         sg.id[i] = sm.ki[k];
+         sg.ax[i] = sm.ka[k];
+      }
+   }
 }
 
-__device__ Scan3 lv_scan(LvSmem& sm, uint32_t s0, uint32_t E)
+__device__ Scan3 lv_scan(LvSmem& sm, const Seg& sg)
 {
    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
    const uint32_t dir = sm.io.dir, nx = sm.io.nx, ny = sm.io.ny;
-   uint32_t a, b;
-   lv_seg(s0, E, a, b);
    uint64_t A = 0, B = 0, C = 0;
-   for (uint32_t e = a; e < b; e++)
+#pragma unroll
+   for (int i = 0; i < LV_PER; i++)
    {
-      const Rec rc = sm.r[sm.perm[e]];
-      const uint64_t p = aux_F(rc.aux);
-      mp_comp(A, B, p, cyc1(rc.t) + p);
-      C += 1ull << (12 * next_dir(rc.aux, dir, nx, ny));
+      if ((uint32_t) i < sg.n)
+      {
+         const uint64_t p = aux_F(sg.ax[i]);
+         mp_comp(A, B, p, cyc1(sg.t[i]) + p);
+         C += 1ull << (12 * next_dir(sg.ax[i], dir, nx, ny));
+      }
    }
    uint64_t iA = A, iB = B, iC = C;
    for (int off = 1; off < 64; off <<= 1)
@@ -353,9 +512,9 @@ __device__ Scan3 lv_scan(LvSmem& sm, uint32_t s0, uint32_t E)
          iC += pC;
       }
    }
-   __syncthreads();
+   lv_bar();
    if (lane == 63) { sm.wA[wv] = iA; sm.wB[wv] = iB; sm.wC[wv] = iC; }
-   __syncthreads();
+   lv_bar();
    Scan3 o;
    uint64_t PA = 0, PB = 0, PC = 0;
    for (uint32_t w = 0; w < wv; w++)
@@ -381,191 +540,212 @@ __device__ Scan3 lv_scan(LvSmem& sm, uint32_t s0, uint32_t E)
    return o;
 }
 
-// ---------------------------------------------------------------------------
-// process a merged leaf from carry sm.cy; write outputs; advance sm.cy
-// ---------------------------------------------------------------------------
-__device__ void lv_process(LvSmem& sm, const DevCfg& c, bool have_scan, Scan3 so, Rec* __restrict__ recs,
-                           uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id, uint32_t* __restrict__ nexc,
-                           uint64_t* __restrict__ final_ps, unsigned* __restrict__ errflag)
+// Serial prefix while the queue has never idled (history tree + M/G/1), one
+// thread, from merged position 0; outputs written directly.  -> sm.s0
+__device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, uint64_t* __restrict__ samp_t,
+                          uint32_t* __restrict__ samp_id, uint32_t* __restrict__ nexc, uint64_t* __restrict__ final_ps,
+                          unsigned* __restrict__ errflag)
 {
-   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-   const uint32_t E = sm.E;
-   const uint32_t dir = sm.io.dir, nx = sm.io.nx, ny = sm.io.ny;
-   const uint64_t rl = dir == P_INJ ? 0ull : c.rl_ps;
-   // ---- serial prefix while the queue has never idled (history tree + M/G/1)
-   if (sm.cy.mode)
+   if (threadIdx.x == 0)
    {
-      if (tid == 0)
-      {
-         SerialState s;
-         s.X = sm.cy.X; s.g = (int) sm.cy.g; s.mode = 1; s.s1 = sm.cy.s1; s.s2 = sm.cy.s2;
-         s.narr = sm.cy.narr; s.newest = sm.cy.newest; s.mg1 = 0;
-         uint32_t e = 0;
-         uint64_t ssum = 0;
-         for (; e < E && s.mode; e++)
-         {
-            const Rec rc = sm.r[sm.perm[e]];
-            const uint64_t mg_before = s.mg1;
-            const uint64_t cc = serial_step(s, cyc1(rc.t), aux_F(rc.aux), c.max_list, c.analytical);
-            if (s.g >= 1) s.mode = 0;
-            ssum += cc;
-            const uint64_t tn = rc.t + cc * 1000ull + rl;
-            if (dir == P_SELF) { final_ps[rc.id] = tn + 1000ull * aux_F(rc.aux); continue; }
-            const uint32_t nd = next_dir(rc.aux, dir, nx, ny);
-            Rec o;
-            o.t = tn;
-            o.id = rc.id;
-            o.aux = rc.aux;
-            if (s.mg1 != mg_before)
-            {
-               // M/G/1-served: may leave FIFO order -> exception tail of the slot
-               const uint32_t x = atomicAdd(&nexc[sm.io.oslot[nd]], 1u);
-               if (x >= sm.io.ocnt[nd]) { atomicOr(errflag, 1u); continue; }
-               recs[sm.io.obase[nd] + sm.io.ocnt[nd] - 1 - x] = o;
-            }
-            else
-            {
-               const uint32_t pos = sm.cy.cnt[nd]++;
-               if (pos >= sm.io.ocnt[nd]) { atomicOr(errflag, 1u); continue; }
-               recs[sm.io.obase[nd] + pos] = o;
-               if ((pos & 63) == 0)
-               {
-                  samp_t[(sm.io.obase[nd] + pos) >> 6] = tn;
-                  samp_id[(sm.io.obase[nd] + pos) >> 6] = rc.id;
-               }
-            }
-         }
-         sm.s0 = e;
-         sm.cy.X = s.X; sm.cy.g = (uint32_t) s.g; sm.cy.mode = s.mode; sm.cy.s1 = s.s1; sm.cy.s2 = s.s2;
-         sm.cy.narr = s.narr; sm.cy.newest = s.newest;
-         sm.st_sum += ssum;
-         sm.st_cnt += e;
-         sm.st_mg1 += (uint32_t) s.mg1;
-      }
-      __syncthreads();
-      have_scan = false;
-   }
-   else if (tid == 0)
-   {
-      sm.s0 = 0;
-   }
-   __syncthreads();
-   const uint32_t s0 = sm.s0;
-   if (!have_scan) so = lv_scan(sm, s0, E);
-   const uint64_t X0 = sm.cy.X;
-   // ---- recurrence per thread segment; departure time back into LDS
-   uint32_t a, b;
-   lv_seg(s0, E, a, b);
-   {
-      uint64_t X = X0 + so.eA;
-      X = X > so.eB ? X : so.eB;
+      const uint32_t E = sm.E;
+      const uint32_t dir = sm.io.dir, nx = sm.io.nx, ny = sm.io.ny;
+      const uint64_t rl = dir == P_INJ ? 0ull : c.rl_ps;
+      SerialState s;
+      s.X = sm.cy.X; s.g = (int) sm.cy.g; s.mode = 1; s.s1 = sm.cy.s1; s.s2 = sm.cy.s2;
+      s.narr = sm.cy.narr; s.newest = sm.cy.newest; s.mg1 = 0;
+      uint32_t e = 0;
       uint64_t ssum = 0;
-      for (uint32_t e = a; e < b; e++)
+      for (; e < E && s.mode; e++)
       {
          const uint32_t k = sm.perm[e];
-         const uint64_t t = sm.r[k].t;
+         const uint64_t t = sm.kt[k];
+         const uint32_t id = sm.ki[k], ax = sm.ka[k];
+         const uint64_t mg_before = s.mg1;
+         const uint64_t cc = serial_step(s, cyc1(t), aux_F(ax), c.max_list, c.analytical);
+         if (s.g >= 1) s.mode = 0;
+         ssum += cc;
+         const uint64_t tn = t + cc * 1000ull + rl;
+         if (dir == P_SELF) { final_ps[id] = tn + 1000ull * aux_F(ax); continue; }
+         const uint32_t nd = next_dir(ax, dir, nx, ny);
+         Rec o;
+         o.t = tn;
+         o.id = id;
+         o.aux = ax;
+         if (s.mg1 != mg_before)
+         {
+            // M/G/1-served: may leave FIFO order -> exception tail of the slot
+            const uint32_t x = atomicAdd(&nexc[sm.io.oslot[nd]], 1u);
+            if (x >= sm.io.ocnt[nd]) { atomicOr(errflag, 1u); continue; }
+            recs[sm.io.obase[nd] + sm.io.ocnt[nd] - 1 - x] = o;
+         }
+         else
+         {
+            const uint32_t pos = sm.cy.cnt[nd]++;
+            if (pos >= sm.io.ocnt[nd]) { atomicOr(errflag, 1u); continue; }
+            const uint64_t gp = sm.io.obase[nd] + pos;
+            recs[gp] = o;
+            if ((gp & 63) == 0)
+            {
+               samp_t[gp >> 6] = tn;
+               samp_id[gp >> 6] = id;
+            }
+         }
+      }
+      sm.s0 = e;
+      sm.cy.X = s.X; sm.cy.g = (uint32_t) s.g; sm.cy.mode = s.mode; sm.cy.s1 = s.s1; sm.cy.s2 = s.s2;
+      sm.cy.narr = s.narr; sm.cy.newest = s.newest;
+      sm.st_sum += ssum;
+      sm.st_cnt += e;
+      sm.st_mg1 += (uint32_t) s.mg1;
+   }
+   lv_bar();
+}
+
+// Recurrence + stores of this thread's segment from carry sm.cy; then the
+// carry advances by the block totals.
+__device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3& so, Rec* __restrict__ recs,
+                        uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id, uint64_t* __restrict__ final_ps,
+                        unsigned* __restrict__ errflag)
+{
+   const uint32_t lane = threadIdx.x & 63;
+   const uint32_t dir = sm.io.dir, nx = sm.io.nx, ny = sm.io.ny;
+   const uint64_t rl = dir == P_INJ ? 0ull : c.rl_ps;
+   const uint64_t X0 = sm.cy.X;
+   uint64_t X = X0 + so.eA;
+   X = X > so.eB ? X : so.eB;
+   uint64_t ssum = 0;
+   uint32_t run[5];
+#pragma unroll
+   for (int d = 0; d < 5; d++) run[d] = sm.cy.cnt[d] + cfield(so.eC, d);
+#pragma unroll
+   for (int i = 0; i < LV_PER; i++)
+   {
+      if ((uint32_t) i < sg.n)
+      {
+         const uint64_t t = sg.t[i];
          const uint64_t tc = cyc1(t);
          const uint64_t cc = X > tc ? X - tc : 0;
-         X = (X > tc ? X : tc) + aux_F(sm.r[k].aux);
+         const uint32_t ax = sg.ax[i];
+         X = (X > tc ? X : tc) + aux_F(ax);
          ssum += cc;
-         sm.r[k].t = t + cc * 1000ull + rl;
-      }
-      for (int off = 32; off > 0; off >>= 1) ssum += __shfl_down(ssum, off);
-      if (lane == 0 && ssum) atomicAdd((unsigned long long*) &sm.st_sum, (unsigned long long) ssum);
-   }
-   __syncthreads();
-   // ---- output pass: wave w owns the merged range of its 64 threads' segments
-   {
-      const uint32_t cnt = E - s0;
-      const uint32_t per = (cnt + LV_T - 1) / LV_T;
-      const uint32_t wa = s0 + min(wv * 64 * per, cnt), wb = s0 + min((wv + 1) * 64 * per, cnt);
-      const uint64_t wpre = __shfl(so.eC, 0);   // counts before this wave's range
-      const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-      uint32_t run[5] = { 0, 0, 0, 0, 0 };
-      for (uint32_t e0 = wa; e0 < wb; e0 += 64)
-      {
-         const uint32_t e = e0 + lane;
-         const bool valid = e < wb;
-         Rec rc;
-         rc.t = 0; rc.id = 0; rc.aux = 0;
-         if (valid) rc = sm.r[sm.perm[e]];
+         const uint64_t tn = t + cc * 1000ull + rl;
          if (dir == P_SELF)
          {
             // NetworkModel::processReceivedPacket: + serialization (network_model.cc:142-150)
-            if (valid) final_ps[rc.id] = rc.t + 1000ull * aux_F(rc.aux);
+            final_ps[sg.id[i]] = tn + 1000ull * aux_F(ax);
             continue;
          }
-         const uint32_t nd = next_dir(rc.aux, dir, nx, ny);
+         const uint32_t nd = next_dir(ax, dir, nx, ny);
          uint32_t pos = 0;
 #pragma unroll
-         for (uint32_t d = 0; d < 5; d++)
-         {
-            const uint64_t m = __ballot(valid && nd == d);
-            if (nd == d) pos = sm.cy.cnt[d] + cfield(wpre, d) + run[d] + (uint32_t) __popcll(m & lt);
-            run[d] += (uint32_t) __popcll(m);
-         }
-         if (valid && pos >= sm.io.ocnt[nd])
+         for (int d = 0; d < 5; d++)
+            if (nd == (uint32_t) d) pos = run[d]++;
+         if (pos >= sm.io.ocnt[nd])
          {
             atomicOr(errflag, 1u);   // route-count invariant broken: never write outside the slot
+            continue;
          }
-         else if (valid)
+         const uint64_t gp = sm.io.obase[nd] + pos;
+         Rec o;
+         o.t = tn;
+         o.id = sg.id[i];
+         o.aux = ax;
+         recs[gp] = o;
+         if ((gp & 63) == 0)
          {
-            const uint64_t gp = sm.io.obase[nd] + pos;
-            recs[gp] = rc;
-            if ((gp & 63) == 0)
-            {
-               samp_t[gp >> 6] = rc.t;
-               samp_id[gp >> 6] = rc.id;
-            }
+            samp_t[gp >> 6] = tn;
+            samp_id[gp >> 6] = o.id;
          }
       }
    }
-   __syncthreads();
-   if (tid == 0)
+   for (int off = 32; off > 0; off >>= 1) ssum += __shfl_down(ssum, off);
+   if (lane == 0 && ssum) atomicAdd((unsigned long long*) &sm.st_sum, (unsigned long long) ssum);
+   lv_bar();
+   if (threadIdx.x == 0)
    {
-      sm.st_cnt += E - s0;
+      sm.st_cnt += sm.E - sm.s0;
       const uint64_t nx0 = X0 + so.tA;
       sm.cy.X = nx0 > so.tB ? nx0 : so.tB;
       for (uint32_t d = 0; d < 5; d++) sm.cy.cnt[d] += cfield(so.tC, d);
    }
-   __syncthreads();
+   lv_bar();
+}
+
+// A whole merged leaf from carry sm.cy (serial prefix if needed).
+__device__ void lv_leaf(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, uint64_t* __restrict__ samp_t,
+                        uint32_t* __restrict__ samp_id, uint32_t* __restrict__ nexc, uint64_t* __restrict__ final_ps,
+                        unsigned* __restrict__ errflag)
+{
+   if (threadIdx.x == 0) sm.s0 = 0;
+   lv_bar();
+   if (sm.cy.mode) lv_serial(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);
+   Seg sg;
+   lv_load_seg(sm, sm.s0, sm.E, sg);
+   const Scan3 so = lv_scan(sm, sg);
+   lv_emit(sm, c, sg, so, recs, samp_t, samp_id, final_ps, errflag);
 }
 
 // ---------------------------------------------------------------------------
-// decoupled look-back (wave 0): state layout per chunk (16 x u64)
-//   [0] A  [1] B  [2] aggregate counts (5 x 12 bit)
-//   [3] cnt0|cnt1<<32  [4] cnt2|cnt3<<32  [5] cnt4  [6] X  [7] mode|g<<32
-//   [8] s1  [9] s2  [10] narr  [11] newest
-// flags: 1 = aggregate published, 2 = inclusive state published
+// decoupled look-back (wave 0).  Chunk state: 16 x u64, zeroed before the run;
+// every word validates itself (8-byte sc1 granules), so one load round trip
+// returns flags and data together.
+//   [0] A+1  [1] B+1  [2] counts(5 x 12 bit) | TAG                 aggregate
+//   [3] X+1  [4] c0 | c1<<31 | TAG  [5] c2 | c3<<31 | TAG
+//   [6] c4 | mode<<31 | g<<32 | TAG                                  inclusive
+//   [7] s1 [8] s2 [9] narr [10] newest  (serial M/G/1 state, stored before
+//   [3..6] and drained, read only when mode == 1)
 // ---------------------------------------------------------------------------
-__device__ void lv_publish_agg(uint64_t* __restrict__ st, uint32_t* __restrict__ flags, uint32_t g, const Scan3& so)
+__device__ void lv_publish_agg(uint64_t* __restrict__ st, uint32_t g, const Scan3& so)
 {
-   uint64_t* w = st + (uint64_t) g * 16;
-   lv_st(w + 0, so.tA);
-   lv_st(w + 1, so.tB);
-   lv_st(w + 2, so.tC);
-   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-   __hip_atomic_store(&flags[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+   uint64_t* w = st + (uint64_t) g * LV_STATE_WORDS;
+   lv_st(w + 0, so.tA + 1);
+   lv_st(w + 1, so.tB + 1);
+   lv_st(w + 2, so.tC | LV_TAG);
 }
 
-__device__ void lv_publish_inc(uint64_t* __restrict__ st, uint32_t* __restrict__ flags, uint32_t g, const Carry3& cy)
+__device__ void lv_publish_inc(uint64_t* __restrict__ st, uint32_t g, const Carry3& cy)
 {
-   uint64_t* w = st + (uint64_t) g * 16;
-   lv_st(w + 3, (uint64_t) cy.cnt[0] | ((uint64_t) cy.cnt[1] << 32));
-   lv_st(w + 4, (uint64_t) cy.cnt[2] | ((uint64_t) cy.cnt[3] << 32));
-   lv_st(w + 5, (uint64_t) cy.cnt[4]);
-   lv_st(w + 6, cy.X);
-   lv_st(w + 7, (uint64_t) cy.mode | ((uint64_t) cy.g << 32));
-   lv_st(w + 8, (uint64_t) __double_as_longlong(cy.s1));
-   lv_st(w + 9, (uint64_t) __double_as_longlong(cy.s2));
-   lv_st(w + 10, cy.narr);
-   lv_st(w + 11, cy.newest);
-   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-   __hip_atomic_store(&flags[g], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+   uint64_t* w = st + (uint64_t) g * LV_STATE_WORDS;
+   if (cy.mode)
+   {
+      lv_st(w + 7, (uint64_t) __double_as_longlong(cy.s1));
+      lv_st(w + 8, (uint64_t) __double_as_longlong(cy.s2));
+      lv_st(w + 9, cy.narr);
+      lv_st(w + 10, cy.newest);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+   }
+   lv_st(w + 3, cy.X + 1);
+   lv_st(w + 4, LV_TAG | (uint64_t) cy.cnt[0] | ((uint64_t) cy.cnt[1] << 31));
+   lv_st(w + 5, LV_TAG | (uint64_t) cy.cnt[2] | ((uint64_t) cy.cnt[3] << 31));
+   lv_st(w + 6, LV_TAG | (uint64_t) cy.cnt[4] | ((uint64_t) (cy.mode & 1u) << 31) | ((uint64_t) cy.g << 32));
 }
 
-__device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint32_t* __restrict__ flags,
-                            const uint64_t* __restrict__ st, unsigned* __restrict__ errflag)
+__device__ __forceinline__ void lv_take_inc(LvSmem& sm, const uint64_t* __restrict__ w, uint64_t X1, uint64_t c01,
+                                            uint64_t c23, uint64_t c4m, uint64_t accA, uint64_t accB,
+                                            const uint32_t* accC)
+{
+   const uint64_t X = X1 - 1;
+   const uint64_t nx = X + accA;
+   sm.cy.X = nx > accB ? nx : accB;
+   sm.cy.mode = (uint32_t) ((c4m >> 31) & 1u);
+   sm.cy.g = (uint32_t) ((c4m >> 32) & 0x7FFFFFFFu);
+   sm.cy.cnt[0] = (uint32_t) (c01 & 0x7FFFFFFFu) + accC[0];
+   sm.cy.cnt[1] = (uint32_t) ((c01 >> 31) & 0x7FFFFFFFu) + accC[1];
+   sm.cy.cnt[2] = (uint32_t) (c23 & 0x7FFFFFFFu) + accC[2];
+   sm.cy.cnt[3] = (uint32_t) ((c23 >> 31) & 0x7FFFFFFFu) + accC[3];
+   sm.cy.cnt[4] = (uint32_t) (c4m & 0x7FFFFFFFu) + accC[4];
+   if (sm.cy.mode)
+   {
+      sm.cy.s1 = __longlong_as_double((long long) lv_ld(w + 7));
+      sm.cy.s2 = __longlong_as_double((long long) lv_ld(w + 8));
+      sm.cy.narr = lv_ld(w + 9);
+      sm.cy.newest = lv_ld(w + 10);
+   }
+}
+
+__device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint64_t* __restrict__ st,
+                            unsigned* __restrict__ errflag)
 {
    const uint32_t lane = threadIdx.x & 63;
    uint64_t accA = 0, accB = 0;
@@ -575,28 +755,28 @@ __device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint32
    for (;;)
    {
       const int32_t ck = look - (int32_t) lane;
-      uint32_t f = 2;
-      if (ck >= 0) f = lv_ld_flag(&flags[gbase + ck]);
-      const uint64_t inc = __ballot(ck >= 0 && f == 2);
-      const uint64_t zero = __ballot(ck >= 0 && f == 0);
+      uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0, w6 = 0;
+      if (ck >= 0)
+      {
+         const uint64_t* w = st + (uint64_t) (gbase + ck) * LV_STATE_WORDS;
+         w0 = lv_ld(w + 0); w1 = lv_ld(w + 1); w2 = lv_ld(w + 2);
+         w3 = lv_ld(w + 3); w4 = lv_ld(w + 4); w5 = lv_ld(w + 5); w6 = lv_ld(w + 6);
+      }
+      const bool aggv = w0 && w1 && (w2 & LV_TAG);
+      const bool incv = w3 && (w4 & LV_TAG) && (w5 & LV_TAG) && (w6 & LV_TAG);
+      const uint64_t inc = __ballot(ck >= 0 && incv);
+      const uint64_t bad = __ballot(ck >= 0 && !incv && !aggv);
       const uint64_t stop = inc | __ballot(ck < 0);
       const int L = stop ? __ffsll((long long) stop) - 1 : 64;
       const uint64_t need = L >= 64 ? ~0ull : ((1ull << L) - 1);
-      if (zero & need)
+      if (bad & need)
       {
          if (++spins > LV_SPIN_LIMIT) { if (lane == 0) atomicOr(errflag, 2u); return false; }
          __builtin_amdgcn_s_sleep(1);
          continue;
       }
-      uint64_t a = 0, b = 0, q = 0;
-      if ((int) lane < L)
-      {
-         const uint64_t* w = st + (uint64_t) (gbase + ck) * 16;
-         a = lv_ld(w + 0);
-         b = lv_ld(w + 1);
-         q = lv_ld(w + 2);
-      }
-      // compose in chunk order: earliest (lane L-1) first ... lane 0 last, then the tail so far
+      // compose aggregates in chunk order: earliest (lane L-1) first ... lane 0 last, then the tail so far
+      const uint64_t a = (int) lane < L ? w0 - 1 : 0, b = (int) lane < L ? w1 - 1 : 0;
       uint64_t wa = 0, wb = 0;
       for (int l = L - 1; l >= 0; l--) mp_comp(wa, wb, __shfl(a, l), __shfl(b, l));
       mp_comp(wa, wb, accA, accB);
@@ -605,48 +785,34 @@ __device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint32
 #pragma unroll
       for (uint32_t d = 0; d < 5; d++)
       {
-         uint32_t v = (int) lane < L ? cfield(q, d) : 0u;
+         uint32_t v = (int) lane < L ? cfield(w2, d) : 0u;
          for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
          accC[d] += v;
       }
       if (L < 64)
       {
          const int32_t sc = look - L;   // chunk holding an inclusive state (chunk 0 always publishes one)
-         const uint64_t* w = st + (uint64_t) (gbase + sc) * 16;
-         const uint32_t mode = (uint32_t) (lv_ld(w + 7) & 0xFFFFFFFFull);
+         const uint64_t X1 = __shfl(w3, L), c01 = __shfl(w4, L), c23 = __shfl(w5, L), c4m = __shfl(w6, L);
+         const uint32_t mode = (uint32_t) ((c4m >> 31) & 1u);
          if (mode && sc != (int32_t) j - 1)
          {
             // the queue was still in its serial prefix: FIFO aggregates after it are invalid;
             // wait for the immediate predecessor's inclusive state instead.
-            const uint32_t pj = gbase + j - 1;
-            while (lv_ld_flag(&flags[pj]) != 2)
+            const uint64_t* w = st + (uint64_t) (gbase + j - 1) * LV_STATE_WORDS;
+            uint64_t p3, p4, p5, p6;
+            for (;;)
             {
+               p3 = lv_ld(w + 3); p4 = lv_ld(w + 4); p5 = lv_ld(w + 5); p6 = lv_ld(w + 6);
+               if (p3 && (p4 & LV_TAG) && (p5 & LV_TAG) && (p6 & LV_TAG)) break;
                if (++spins > LV_SPIN_LIMIT) { if (lane == 0) atomicOr(errflag, 2u); return false; }
                __builtin_amdgcn_s_sleep(1);
             }
-            w = st + (uint64_t) pj * 16;
-            accA = 0;
-            accB = 0;
-            for (int d = 0; d < 5; d++) accC[d] = 0;
+            const uint32_t zero[5] = { 0, 0, 0, 0, 0 };
+            if (lane == 0) lv_take_inc(sm, w, p3, p4, p5, p6, 0, 0, zero);
          }
-         if (lane == 0)
+         else if (lane == 0)
          {
-            const uint64_t X = lv_ld(w + 6);
-            const uint64_t mg = lv_ld(w + 7);
-            const uint64_t c01 = lv_ld(w + 3), c23 = lv_ld(w + 4), c4 = lv_ld(w + 5);
-            const uint64_t nx = X + accA;
-            sm.cy.X = nx > accB ? nx : accB;
-            sm.cy.mode = (uint32_t) (mg & 0xFFFFFFFFull);
-            sm.cy.g = (uint32_t) (mg >> 32);
-            sm.cy.s1 = __longlong_as_double((long long) lv_ld(w + 8));
-            sm.cy.s2 = __longlong_as_double((long long) lv_ld(w + 9));
-            sm.cy.narr = lv_ld(w + 10);
-            sm.cy.newest = lv_ld(w + 11);
-            sm.cy.cnt[0] = (uint32_t) (c01 & 0xFFFFFFFFull) + accC[0];
-            sm.cy.cnt[1] = (uint32_t) (c01 >> 32) + accC[1];
-            sm.cy.cnt[2] = (uint32_t) (c23 & 0xFFFFFFFFull) + accC[2];
-            sm.cy.cnt[3] = (uint32_t) (c23 >> 32) + accC[3];
-            sm.cy.cnt[4] = (uint32_t) c4 + accC[4];
+            lv_take_inc(sm, st + (uint64_t) (gbase + sc) * LV_STATE_WORDS, X1, c01, c23, c4m, accA, accB, accC);
          }
          return true;
       }
@@ -663,13 +829,17 @@ __device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint32
       if (STAMPS && stamps && tid == 0) stamps[(uint64_t) g * 16 + (k)] = __builtin_amdgcn_s_memtime();     \
    } while (0)
 
+#ifndef LV_MIN_WAVES
+#define LV_MIN_WAVES 4   // waves per SIMD the register allocation must leave room for
+#endif
+
 template <bool STAMPS>
-__global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const uint32_t* __restrict__ lvl_cbase,
+__global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t level, const uint32_t* __restrict__ lvl_cbase,
                                                 unsigned* __restrict__ ctr, const uint32_t* __restrict__ chunk_port,
                                                 const PortIO3* __restrict__ pio, Rec* __restrict__ recs,
                                                 uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id,
-                                                uint32_t* __restrict__ nexc, uint32_t* __restrict__ flags,
-                                                uint64_t* __restrict__ st, uint64_t* __restrict__ final_ps,
+                                                uint32_t* __restrict__ nexc, uint64_t* __restrict__ st,
+                                                uint64_t* __restrict__ final_ps,
                                                 unsigned long long* __restrict__ port_sum,
                                                 unsigned long long* __restrict__ port_cnt,
                                                 unsigned long long* __restrict__ port_mg1, unsigned* __restrict__ errflag,
@@ -681,7 +851,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
    const uint32_t nch = lvl_cbase[level + 1] - cb0;
    for (;;)
    {
-      __syncthreads();
+      lv_bar();
       if (tid == 0)
       {
          const uint32_t cid = atomicAdd(&ctr[level], 1u);   // in order: every predecessor chunk is running
@@ -692,7 +862,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
          sm.st_mg1 = 0;
          sm.published = 0;
       }
-      __syncthreads();
+      lv_bar();
       if (!sm.j) return;
       const uint32_t g = sm.g;
       LV_STAMP(0);
@@ -702,7 +872,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
          uint32_t* dstw = reinterpret_cast<uint32_t*>(&sm.io);
          for (uint32_t k = tid; k < (uint32_t) (sizeof(PortIO3) / 4); k += LV_T) dstw[k] = srcw[k];
       }
-      __syncthreads();
+      lv_bar();
       const uint32_t j = g - sm.io.gbase, nc = sm.io.nc;
       const uint32_t nin = sm.io.nin;
       if (tid < nin)
@@ -717,7 +887,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
          sm.cy.X = 0; sm.cy.mode = 0; sm.cy.g = 0; sm.cy.s1 = 0; sm.cy.s2 = 0; sm.cy.narr = 0; sm.cy.newest = 0;
          for (int k = 0; k < 5; k++) sm.cy.cnt[k] = 0;
       }
-      __syncthreads();
+      lv_bar();
       LV_STAMP(1);
 
       // ---- chunk key range: exact index split of the largest input
@@ -751,16 +921,16 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
          }
          if (lane == 0) sm.search[q] = v;
       }
-      __syncthreads();
+      lv_bar();
       uint32_t total = 0, totexc = 0;
-      uint32_t rlo[LV_IN], rhi[LV_IN];
 #pragma unroll
       for (uint32_t s = 0; s < (uint32_t) LV_IN; s++)
       {
-         rlo[s] = s < nin ? sm.search[2 * s] : 0;
-         rhi[s] = s < nin ? sm.search[2 * s + 1] : 0;
-         total += rhi[s] - rlo[s];
-         totexc += s < nin ? sm.nxe[s] : 0;
+         if (s < nin)
+         {
+            total += sm.search[2 * s + 1] - sm.search[2 * s];
+            totexc += sm.nxe[s];
+         }
       }
       LV_STAMP(3);
       if (empty) totexc = 0;
@@ -769,57 +939,72 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
       if (total + totexc <= (uint32_t) LV_CAP)
       {
          // ---------------- single leaf
-         if (tid < (uint32_t) LV_IN) { sm.lo[tid] = rlo[tid]; sm.hi[tid] = rhi[tid]; }
-         __syncthreads();
+         if (tid < (uint32_t) LV_IN)
+         {
+            sm.lo[tid] = tid < nin ? sm.search[2 * tid] : 0;
+            sm.hi[tid] = tid < nin ? sm.search[2 * tid + 1] : 0;
+         }
+         lv_bar();
          lv_load_merge(sm, recs, klo_t, klo_i, khi_t, khi_i, has_lo, has_hi, !empty);
          LV_STAMP(4);
          if (j == 0)
          {
-            if (tid == 0 && c.analytical && sm.E > 0 && cyc1(sm.r[sm.perm[0]].t) == 0) sm.cy.mode = 1;
-            __syncthreads();
+            if (tid == 0 && c.analytical && sm.E > 0 && cyc1(sm.kt[sm.perm[0]]) == 0) sm.cy.mode = 1;
+            if (tid == 0) sm.s0 = 0;
+            lv_bar();
          }
-         bool have = false;
-         Scan3 so;
-         so.eA = so.eB = so.eC = so.tA = so.tB = so.tC = 0;
          if (j > 0 || !sm.cy.mode)
          {
-            so = lv_scan(sm, 0, sm.E);
-            have = true;
+            if (tid == 0) sm.s0 = 0;
+            Seg sg;
+            lv_load_seg(sm, 0, sm.E, sg);
+            const Scan3 so = lv_scan(sm, sg);
             LV_STAMP(5);
             if (j > 0)
             {
-               if (tid == 0) lv_publish_agg(st, flags, g, so);
-               if (wv == 0) lv_lookback(sm, sm.io.gbase, j, flags, st, errflag);
-               __syncthreads();
+               if (tid == 0) lv_publish_agg(st, g, so);
+               if (wv == 0) lv_lookback(sm, sm.io.gbase, j, st, errflag);
+               lv_bar();
             }
             LV_STAMP(6);
-            // FIFO: the inclusive state is (carry) x (aggregate); publish before the outputs
-            if (tid == 0 && !sm.cy.mode)
+            if (!sm.cy.mode)
             {
-               Carry3 inc = sm.cy;
-               const uint64_t nx0 = inc.X + so.tA;
-               inc.X = nx0 > so.tB ? nx0 : so.tB;
-               for (uint32_t d = 0; d < 5; d++) inc.cnt[d] += cfield(so.tC, d);
-               lv_publish_inc(st, flags, g, inc);
-               sm.published = 1;
+               // FIFO: the inclusive state is (carry) x (aggregate); publish before the outputs
+               if (tid == 0)
+               {
+                  Carry3 inc = sm.cy;
+                  const uint64_t nx0 = inc.X + so.tA;
+                  inc.X = nx0 > so.tB ? nx0 : so.tB;
+                  for (uint32_t d = 0; d < 5; d++) inc.cnt[d] += cfield(so.tC, d);
+                  lv_publish_inc(st, g, inc);
+                  sm.published = 1;
+               }
+               lv_emit(sm, c, sg, so, recs, samp_t, samp_id, final_ps, errflag);
             }
-            __syncthreads();
+            else
+            {
+               lv_leaf(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);   // serial prefix continues
+            }
          }
-         lv_process(sm, c, have, so, recs, samp_t, samp_id, nexc, final_ps, errflag);
+         else
+         {
+            lv_leaf(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);
+         }
          LV_STAMP(7);
       }
       else
       {
          // ---------------- burst: split the key range into leaves that fit LDS
-         if (j > 0 && wv == 0) lv_lookback(sm, sm.io.gbase, j, flags, st, errflag);
+         if (j > 0 && wv == 0) lv_lookback(sm, sm.io.gbase, j, st, errflag);
          if (tid == 0)
          {
             sm.nleaf = 1;
             sm.lk_t[0] = klo_t; sm.lk_i[0] = klo_i;
             sm.lk_t[1] = khi_t; sm.lk_i[1] = khi_i;
-            for (uint32_t s = 0; s < (uint32_t) LV_IN; s++) sm.lr_lo[0][s] = rlo[s];
+            for (uint32_t s = 0; s < (uint32_t) LV_IN; s++) sm.lr_lo[0][s] = s < nin ? sm.search[2 * s] : 0;
+            for (uint32_t s = 0; s < (uint32_t) LV_IN; s++) sm.hi[s] = s < nin ? sm.search[2 * s + 1] : 0;
          }
-         __syncthreads();
+         lv_bar();
          bool ok = true;
          for (uint32_t iter = 0; iter < 4 * (uint32_t) LV_MAXLEAF && ok; iter++)
          {
@@ -830,7 +1015,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
                uint32_t sz = 0, bn = 0, best = 0;
                for (uint32_t s = 0; s < nin; s++)
                {
-                  const uint32_t h = (L + 1 < sm.nleaf) ? sm.lr_lo[L + 1][s] : rhi[s];
+                  const uint32_t h = (L + 1 < sm.nleaf) ? sm.lr_lo[L + 1][s] : sm.hi[s];
                   const uint32_t n = h - sm.lr_lo[L][s];
                   sz += n;
                   if (n > bn) { bn = n; best = s; }
@@ -846,7 +1031,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
             // no progress possible (the leaf is exceptions, or one key) -> exact v1 rerun
             if (sm.nleaf >= (uint32_t) LV_MAXLEAF || bestn < 2) { ok = false; break; }
             const uint32_t L = (uint32_t) bad;
-            const uint32_t hL = (L + 1 < sm.nleaf) ? sm.lr_lo[L + 1][bs] : rhi[bs];
+            const uint32_t hL = (L + 1 < sm.nleaf) ? sm.lr_lo[L + 1][bs] : sm.hi[bs];
             const uint32_t mid = (sm.lr_lo[L][bs] + hL) / 2;
             const Rec mr = recs[sm.io.base[bs] + mid];
             for (uint32_t q = wv; q < (uint32_t) LV_IN; q += LV_T / 64)
@@ -860,7 +1045,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
                }
                if (lane == 0) sm.search[q] = v;
             }
-            __syncthreads();
+            lv_bar();
             if (tid == 0)
             {
                for (uint32_t M = sm.nleaf; M > L + 1; M--)
@@ -871,7 +1056,7 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
                for (uint32_t s = 0; s < (uint32_t) LV_IN; s++) sm.lr_lo[L + 1][s] = s < nin ? sm.search[s] : 0;
                sm.nleaf++;
             }
-            __syncthreads();
+            lv_bar();
          }
          if (!ok)
          {
@@ -880,38 +1065,44 @@ __global__ __launch_bounds__(LV_T) void k_level(DevCfg c, uint32_t level, const 
          else
          {
             const uint32_t nleaf = sm.nleaf;
+            uint32_t rhi[LV_IN];
+#pragma unroll
+            for (uint32_t s = 0; s < (uint32_t) LV_IN; s++) rhi[s] = sm.hi[s];
             for (uint32_t L = 0; L < nleaf; L++)
             {
-               if (tid < (uint32_t) LV_IN)
-               {
-                  sm.lo[tid] = sm.lr_lo[L][tid];
-                  sm.hi[tid] = (L + 1 < nleaf) ? sm.lr_lo[L + 1][tid] : rhi[tid];
-               }
-               __syncthreads();
+               lv_bar();
+#pragma unroll
+               for (uint32_t s = 0; s < (uint32_t) LV_IN; s++)
+                  if (tid == s)
+                  {
+                     sm.lo[s] = sm.lr_lo[L][s];
+                     sm.hi[s] = (L + 1 < nleaf) ? sm.lr_lo[L + 1][s] : rhi[s];
+                  }
+               lv_bar();
                const bool hl = has_lo || L > 0, hh = has_hi || L + 1 < nleaf;
                lv_load_merge(sm, recs, sm.lk_t[L], sm.lk_i[L], sm.lk_t[L + 1], sm.lk_i[L + 1], hl, hh, true);
                if (j == 0 && L == 0)
                {
-                  if (tid == 0 && c.analytical && sm.E > 0 && cyc1(sm.r[sm.perm[0]].t) == 0) sm.cy.mode = 1;
-                  __syncthreads();
+                  if (tid == 0 && c.analytical && sm.E > 0 && cyc1(sm.kt[sm.perm[0]]) == 0) sm.cy.mode = 1;
+                  lv_bar();
                }
-               Scan3 so;
-               so.eA = so.eB = so.eC = so.tA = so.tB = so.tC = 0;
-               lv_process(sm, c, false, so, recs, samp_t, samp_id, nexc, final_ps, errflag);
+               lv_leaf(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);
             }
          }
       }
 
       // ---- inclusive state (if not yet), per-port counters
-      __syncthreads();
+      lv_bar();
       if (tid == 0)
       {
-         if (!sm.published) lv_publish_inc(st, flags, g, sm.cy);
+         if (!sm.published) lv_publish_inc(st, g, sm.cy);
          if (STAMPS && stamps)
          {
             stamps[(uint64_t) g * 16 + 8] = __builtin_amdgcn_s_memtime();
             stamps[(uint64_t) g * 16 + 9] = (uint64_t) j | ((uint64_t) sm.io.dir << 32);
             stamps[(uint64_t) g * 16 + 10] = sm.st_cnt;
+            stamps[(uint64_t) g * 16 + 11] = sm.tm[0];
+            stamps[(uint64_t) g * 16 + 12] = sm.tm[1];
          }
          atomicAdd(&port_sum[sm.io.port], (unsigned long long) sm.st_sum);
          atomicAdd(&port_cnt[sm.io.port], (unsigned long long) sm.st_cnt);

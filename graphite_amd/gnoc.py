@@ -14,7 +14,7 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libgnoc.so")
+LIB_PATH = os.environ.get("GNOC_LIB", os.path.join(_HERE, "_build", "libgnoc.so"))
 
 GNOC_OK = 0
 GNOC_EINVAL = -1

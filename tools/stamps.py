@@ -35,4 +35,6 @@ for dirn, label in ((5, "INJ"), (2, "RIGHT"), (1, "LEFT"), (4, "UP"), (3, "DOWN"
     s = st[m]
     out = [f"{names[k]}={int(np.median(s[:, k] - s[:, k - 1]))}" for k in range(1, 9)]
     tot = np.median(s[:, 8] - s[:, 0])
+    out.append(f"[load={int(np.median(s[:, 11] - s[:, 3]))} exc={int(np.median(s[:, 12] - s[:, 11]))} "
+               f"merge={int(np.median(s[:, 4] - s[:, 12]))}]")
     print(f"{label:6s} n={m.sum():6d} total={int(tot)} " + " ".join(out))
