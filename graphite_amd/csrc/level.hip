@@ -449,12 +449,11 @@ __device__ void lv_load_merge(LvSmem& sm, const Rec* __restrict__ recs, uint64_t
 // ---------------------------------------------------------------------------
 // per-thread merged segment in registers + block scan
 // ---------------------------------------------------------------------------
+// This thread's contiguous merged segment [a, a+n) of positions [s0, E);
+// its records are read from LDS where used (not held across the look-back).
 struct Seg
 {
-   uint64_t t[LV_PER];
-   uint32_t id[LV_PER];
-   uint32_t ax[LV_PER];
-   uint32_t a, n;            // first merged position, records
+   uint32_t a, n;
 };
 
 struct Scan3
@@ -471,17 +470,6 @@ __device__ __forceinline__ void lv_load_seg(const LvSmem& sm, uint32_t s0, uint3
    const uint32_t b = s0 + min((threadIdx.x + 1) * per, cnt);
    sg.a = a;
    sg.n = b - a;
-#pragma unroll
-   for (int i = 0; i < LV_PER; i++)
-   {
-      if ((uint32_t) i < sg.n)
-      {
-         const uint32_t k = sm.perm[a + i];
-         sg.t[i] = sm.kt[k];
-         sg.id[i] = sm.ki[k];
-         sg.ax[i] = sm.ka[k];
-      }
-   }
 }
 
 __device__ Scan3 lv_scan(LvSmem& sm, const Seg& sg)
@@ -489,15 +477,13 @@ __device__ Scan3 lv_scan(LvSmem& sm, const Seg& sg)
    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
    const uint32_t dir = sm.io.dir, nx = sm.io.nx, ny = sm.io.ny;
    uint64_t A = 0, B = 0, C = 0;
-#pragma unroll
-   for (int i = 0; i < LV_PER; i++)
+   for (uint32_t i = 0; i < sg.n; i++)
    {
-      if ((uint32_t) i < sg.n)
-      {
-         const uint64_t p = aux_F(sg.ax[i]);
-         mp_comp(A, B, p, cyc1(sg.t[i]) + p);
-         C += 1ull << (12 * next_dir(sg.ax[i], dir, nx, ny));
-      }
+      const uint32_t k = sm.perm[sg.a + i];
+      const uint32_t ax = sm.ka[k];
+      const uint64_t p = aux_F(ax);
+      mp_comp(A, B, p, cyc1(sm.kt[k]) + p);
+      C += 1ull << (12 * next_dir(ax, dir, nx, ny));
    }
    uint64_t iA = A, iB = B, iC = C;
    for (int off = 1; off < 64; off <<= 1)
@@ -618,22 +604,22 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
    uint32_t run[5];
 #pragma unroll
    for (int d = 0; d < 5; d++) run[d] = sm.cy.cnt[d] + cfield(so.eC, d);
-#pragma unroll
-   for (int i = 0; i < LV_PER; i++)
+   for (uint32_t i = 0; i < sg.n; i++)
    {
-      if ((uint32_t) i < sg.n)
       {
-         const uint64_t t = sg.t[i];
+         const uint32_t k = sm.perm[sg.a + i];
+         const uint64_t t = sm.kt[k];
+         const uint32_t id = sm.ki[k];
          const uint64_t tc = cyc1(t);
          const uint64_t cc = X > tc ? X - tc : 0;
-         const uint32_t ax = sg.ax[i];
+         const uint32_t ax = sm.ka[k];
          X = (X > tc ? X : tc) + aux_F(ax);
          ssum += cc;
          const uint64_t tn = t + cc * 1000ull + rl;
          if (dir == P_SELF)
          {
             // NetworkModel::processReceivedPacket: + serialization (network_model.cc:142-150)
-            final_ps[sg.id[i]] = tn + 1000ull * aux_F(ax);
+            final_ps[id] = tn + 1000ull * aux_F(ax);
             continue;
          }
          const uint32_t nd = next_dir(ax, dir, nx, ny);
@@ -649,7 +635,7 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
          const uint64_t gp = sm.io.obase[nd] + pos;
          Rec o;
          o.t = tn;
-         o.id = sg.id[i];
+         o.id = id;
          o.aux = ax;
          recs[gp] = o;
          if ((gp & 63) == 0)
