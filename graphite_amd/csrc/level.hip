@@ -86,6 +86,19 @@ struct LvSmem
    uint32_t nexc_leaf, published, nleaf, st_cnt;
    uint32_t st_mg1, pad0, pad1, pad2;
    uint64_t tm[4];           // debug phase stamps inside a leaf (GNOC_STAMPS)
+   // current chunk's key range
+   uint64_t klo_t, khi_t;
+   uint32_t klo_i, khi_i, has_lo, has_hi, empty, nc;
+   // next chunk, prefetched by waves 1-3 while wave 0 looks back
+   struct
+   {
+      PortIO3 io;
+      uint64_t klo_t, khi_t;
+      uint32_t klo_i, khi_i;
+      uint32_t g, valid, has_lo, has_hi, empty, ready;
+      uint32_t nmain[LV_IN], nxe[LV_IN];
+      uint32_t search[2 * LV_IN];
+   } nx;
 };
 
 // ---------------------------------------------------------------------------
@@ -777,6 +790,7 @@ __device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint64
       }
       if (L < 64)
       {
+         if (lane == 0) { sm.tm[2] = __builtin_amdgcn_s_memtime(); sm.tm[3] = spins | ((uint64_t) (j - (look - L)) << 32); }
          const int32_t sc = look - L;   // chunk holding an inclusive state (chunk 0 always publishes one)
          const uint64_t X1 = __shfl(w3, L), c01 = __shfl(w4, L), c23 = __shfl(w5, L), c4m = __shfl(w6, L);
          const uint32_t mode = (uint32_t) ((c4m >> 31) & 1u);
@@ -809,6 +823,94 @@ __device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint64
 // ---------------------------------------------------------------------------
 // the level kernel: a persistent grid pulls the level's chunks in order
 // ---------------------------------------------------------------------------
+// Waves 1..3 fetch the next chunk of the level: dynamic chunk id, its port
+// descriptor, exception counts, split keys (wave 1), then the sample searches
+// of the other inputs (all three waves).  Results in sm.nx.
+__device__ __noinline__ void lv_fetch(LvSmem& sm, uint32_t level, uint32_t cb0, uint32_t nch, unsigned* __restrict__ ctr,
+                                      const uint32_t* __restrict__ chunk_port, const PortIO3* __restrict__ pio,
+                                      const Rec* __restrict__ recs, const uint64_t* __restrict__ samp_t,
+                                      const uint32_t* __restrict__ samp_id, const uint32_t* __restrict__ nexc)
+{
+   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+   auto& d = sm.nx;
+   if (wv == 1)
+   {
+      uint32_t cid = 0;
+      if (lane == 0) cid = atomicAdd(&ctr[level], 1u);   // in order: every predecessor chunk is running
+      cid = __shfl(cid, 0);
+      const uint32_t valid = cid < nch ? 1u : 0u;
+      const uint32_t g = cb0 + cid;
+      if (valid)
+      {
+         const uint32_t pk = chunk_port[g];
+         const uint32_t* srcw = reinterpret_cast<const uint32_t*>(pio + pk);
+         uint32_t* dstw = reinterpret_cast<uint32_t*>(&d.io);
+         if (lane < (uint32_t) (sizeof(PortIO3) / 4)) dstw[lane] = srcw[lane];
+         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+         const uint32_t nin = d.io.nin;
+         if (lane < nin)
+         {
+            const uint32_t x = nexc[d.io.slot[lane]];
+            d.nxe[lane] = x;
+            d.nmain[lane] = d.io.cnt[lane] - x;
+         }
+         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+         const uint32_t j = g - d.io.gbase, nc = d.io.nc, sb = d.io.sb;
+         const uint32_t nb = d.nmain[sb];
+         uint32_t has_lo = j > 0, has_hi = j + 1 < nc, empty = 0;
+         if (nb == 0) { empty = j > 0; has_lo = has_hi = 0; }   // only exceptions: chunk 0 takes all
+         const uint32_t ilo = (uint32_t) (((uint64_t) j * nb) / nc);
+         const uint32_t ihi = (uint32_t) (((uint64_t) (j + 1) * nb) / nc);
+         if (lane == 0)
+         {
+            d.klo_t = 0; d.klo_i = 0;
+            if (has_lo) { const Rec r = recs[d.io.base[sb] + ilo]; d.klo_t = r.t; d.klo_i = r.id; }
+         }
+         if (lane == 1)
+         {
+            d.khi_t = ~0ull; d.khi_i = ~0u;
+            if (has_hi) { const Rec r = recs[d.io.base[sb] + ihi]; d.khi_t = r.t; d.khi_i = r.id; }
+         }
+         if (lane == 2)
+         {
+            d.has_lo = has_lo; d.has_hi = has_hi; d.empty = empty;
+            for (uint32_t q = 0; q < 2 * (uint32_t) LV_IN; q++) d.search[q] = 0;
+            if (!empty)
+            {
+               d.search[2 * sb] = has_lo ? ilo : 0;
+               d.search[2 * sb + 1] = has_hi ? ihi : nb;
+               for (uint32_t s = 0; s < nin; s++)
+                  if (s != sb)
+                  {
+                     if (!has_lo) d.search[2 * s] = 0;
+                     if (!has_hi) d.search[2 * s + 1] = d.nmain[s];
+                  }
+            }
+         }
+      }
+      if (lane == 3) { d.g = g; d.valid = valid; }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(&d.ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+   }
+   else
+   {
+      while (__hip_atomic_load(&d.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+         __builtin_amdgcn_s_sleep(1);
+   }
+   if (!d.valid || d.empty) return;
+   const uint32_t nin = d.io.nin, sb = d.io.sb;
+   for (uint32_t q = wv - 1; q < 2 * (uint32_t) LV_IN; q += 3)
+   {
+      const uint32_t s = q >> 1, which = q & 1;
+      if (s >= nin || s == sb) continue;
+      if ((which == 0 && !d.has_lo) || (which == 1 && !d.has_hi)) continue;
+      const uint64_t sbase = d.io.base[s] >> 6;
+      const uint32_t v = wave_lb(recs + d.io.base[s], samp_t + sbase, samp_id + sbase, d.nmain[s],
+                                 which ? d.khi_t : d.klo_t, which ? d.khi_i : d.klo_i, lane);
+      if (lane == 0) d.search[q] = v;
+   }
+}
+
 #define LV_STAMP(k)                                                                                          \
    do                                                                                                       \
    {                                                                                                        \
@@ -835,79 +937,49 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
    const uint32_t cb0 = lvl_cbase[level];
    const uint32_t nch = lvl_cbase[level + 1] - cb0;
+   if (tid == 0) sm.nx.ready = 0;
+   lv_bar();
+   if (wv >= 1) lv_fetch(sm, level, cb0, nch, ctr, chunk_port, pio, recs, samp_t, samp_id, nexc);
+   lv_bar();
    for (;;)
    {
-      lv_bar();
-      if (tid == 0)
-      {
-         const uint32_t cid = atomicAdd(&ctr[level], 1u);   // in order: every predecessor chunk is running
-         sm.g = cb0 + cid;
-         sm.j = cid < nch ? 1u : 0u;   // temporarily: "valid"
-         sm.st_sum = 0;
-         sm.st_cnt = 0;
-         sm.st_mg1 = 0;
-         sm.published = 0;
-      }
-      lv_bar();
-      if (!sm.j) return;
-      const uint32_t g = sm.g;
+      // ---- take the prefetched chunk
+      if (!sm.nx.valid) return;
+      const uint32_t g = sm.nx.g;
       LV_STAMP(0);
-      const uint32_t pk = chunk_port[g];
       {
-         const uint32_t* srcw = reinterpret_cast<const uint32_t*>(pio + pk);
+         const uint32_t* srcw = reinterpret_cast<const uint32_t*>(&sm.nx.io);
          uint32_t* dstw = reinterpret_cast<uint32_t*>(&sm.io);
          for (uint32_t k = tid; k < (uint32_t) (sizeof(PortIO3) / 4); k += LV_T) dstw[k] = srcw[k];
-      }
-      lv_bar();
-      const uint32_t j = g - sm.io.gbase, nc = sm.io.nc;
-      const uint32_t nin = sm.io.nin;
-      if (tid < nin)
-      {
-         const uint32_t x = nexc[sm.io.slot[tid]];
-         sm.nxe[tid] = x;
-         sm.nmain[tid] = sm.io.cnt[tid] - x;
-      }
-      if (tid == 0)
-      {
-         sm.j = j;
-         sm.cy.X = 0; sm.cy.mode = 0; sm.cy.g = 0; sm.cy.s1 = 0; sm.cy.s2 = 0; sm.cy.narr = 0; sm.cy.newest = 0;
-         for (int k = 0; k < 5; k++) sm.cy.cnt[k] = 0;
-      }
-      lv_bar();
-      LV_STAMP(1);
-
-      // ---- chunk key range: exact index split of the largest input
-      const uint32_t sb = sm.io.sb;
-      const uint32_t nb = sm.nmain[sb];
-      bool has_lo = j > 0, has_hi = j + 1 < nc, empty = false;
-      if (nb == 0) { empty = j > 0; has_lo = has_hi = false; }   // only exceptions: chunk 0 takes all
-      const uint32_t ilo = (uint32_t) (((uint64_t) j * nb) / nc);
-      const uint32_t ihi = (uint32_t) (((uint64_t) (j + 1) * nb) / nc);
-      uint64_t klo_t = 0, khi_t = ~0ull;
-      uint32_t klo_i = 0, khi_i = ~0u;
-      if (has_lo) { const Rec r = recs[sm.io.base[sb] + ilo]; klo_t = r.t; klo_i = r.id; }
-      if (has_hi) { const Rec r = recs[sm.io.base[sb] + ihi]; khi_t = r.t; khi_i = r.id; }
-
-      LV_STAMP(2);
-      // ---- main ranges of the other inputs (waves search in parallel)
-      for (uint32_t q = wv; q < 2 * (uint32_t) LV_IN; q += LV_T / 64)
-      {
-         const uint32_t s = q >> 1, which = q & 1;
-         if (s >= nin) continue;
-         uint32_t v;
-         if (empty) v = 0;
-         else if (s == sb) v = which ? (has_hi ? ihi : nb) : (has_lo ? ilo : 0);
-         else if (which == 0 && !has_lo) v = 0;
-         else if (which == 1 && !has_hi) v = sm.nmain[s];
-         else
+         if (tid < (uint32_t) LV_IN)
          {
-            const uint64_t sbase = sm.io.base[s] >> 6;
-            v = wave_lb(recs + sm.io.base[s], samp_t + sbase, samp_id + sbase, sm.nmain[s], which ? khi_t : klo_t,
-                        which ? khi_i : klo_i, lane);
+            sm.nmain[tid] = sm.nx.nmain[tid];
+            sm.nxe[tid] = sm.nx.nxe[tid];
          }
-         if (lane == 0) sm.search[q] = v;
+         if (tid < 2 * (uint32_t) LV_IN) sm.search[tid] = sm.nx.search[tid];
+         if (tid == 0)
+         {
+            sm.klo_t = sm.nx.klo_t; sm.klo_i = sm.nx.klo_i; sm.khi_t = sm.nx.khi_t; sm.khi_i = sm.nx.khi_i;
+            sm.has_lo = sm.nx.has_lo; sm.has_hi = sm.nx.has_hi; sm.empty = sm.nx.empty;
+            sm.g = g;
+            sm.st_sum = 0;
+            sm.st_cnt = 0;
+            sm.st_mg1 = 0;
+            sm.published = 0;
+            sm.cy.X = 0; sm.cy.mode = 0; sm.cy.g = 0; sm.cy.s1 = 0; sm.cy.s2 = 0; sm.cy.narr = 0; sm.cy.newest = 0;
+            for (int k = 0; k < 5; k++) sm.cy.cnt[k] = 0;
+         }
       }
       lv_bar();
+      if (tid == 0) sm.nx.ready = 0;
+      bool fetched = false;
+      const uint32_t j = g - sm.io.gbase;
+      const uint32_t nin = sm.io.nin;
+      const bool has_lo = sm.has_lo, has_hi = sm.has_hi, empty = sm.empty;
+      const uint64_t klo_t = sm.klo_t, khi_t = sm.khi_t;
+      const uint32_t klo_i = sm.klo_i, khi_i = sm.khi_i;
+      LV_STAMP(1);
+      LV_STAMP(2);
       uint32_t total = 0, totexc = 0;
 #pragma unroll
       for (uint32_t s = 0; s < (uint32_t) LV_IN; s++)
@@ -950,6 +1022,8 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
             {
                if (tid == 0) lv_publish_agg(st, g, so);
                if (wv == 0) lv_lookback(sm, sm.io.gbase, j, st, errflag);
+               else lv_fetch(sm, level, cb0, nch, ctr, chunk_port, pio, recs, samp_t, samp_id, nexc);
+               fetched = true;
                lv_bar();
             }
             LV_STAMP(6);
@@ -1077,8 +1151,12 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
          }
       }
 
-      // ---- inclusive state (if not yet), per-port counters
+      // ---- next chunk (if not prefetched), inclusive state (if not yet), per-port counters
       lv_bar();
+      if (!fetched)
+      {
+         if (wv >= 1) lv_fetch(sm, level, cb0, nch, ctr, chunk_port, pio, recs, samp_t, samp_id, nexc);
+      }
       if (tid == 0)
       {
          if (!sm.published) lv_publish_inc(st, g, sm.cy);
@@ -1089,11 +1167,14 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
             stamps[(uint64_t) g * 16 + 10] = sm.st_cnt;
             stamps[(uint64_t) g * 16 + 11] = sm.tm[0];
             stamps[(uint64_t) g * 16 + 12] = sm.tm[1];
+            stamps[(uint64_t) g * 16 + 13] = sm.tm[2];
+            stamps[(uint64_t) g * 16 + 14] = sm.tm[3];
          }
          atomicAdd(&port_sum[sm.io.port], (unsigned long long) sm.st_sum);
          atomicAdd(&port_cnt[sm.io.port], (unsigned long long) sm.st_cnt);
          if (sm.st_mg1) atomicAdd(&port_mg1[sm.io.port], (unsigned long long) sm.st_mg1);
       }
+      lv_bar();
    }
 }
 

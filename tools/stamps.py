@@ -35,6 +35,11 @@ for dirn, label in ((5, "INJ"), (2, "RIGHT"), (1, "LEFT"), (4, "UP"), (3, "DOWN"
     s = st[m]
     out = [f"{names[k]}={int(np.median(s[:, k] - s[:, k - 1]))}" for k in range(1, 9)]
     tot = np.median(s[:, 8] - s[:, 0])
+    lb = s[:, 13] - s[:, 5]
+    spins = s[:, 14] & 0xFFFFFFFF
+    dist = s[:, 14] >> 32
+    out.append(f"[lookback={int(np.median(lb))} p90={int(np.percentile(lb, 90))} spins med={int(np.median(spins))} "
+               f"p90={int(np.percentile(spins, 90))} incl-dist med={int(np.median(dist))} p90={int(np.percentile(dist, 90))}]")
     out.append(f"[load={int(np.median(s[:, 11] - s[:, 3]))} exc={int(np.median(s[:, 12] - s[:, 11]))} "
                f"merge={int(np.median(s[:, 4] - s[:, 12]))}]")
     print(f"{label:6s} n={m.sum():6d} total={int(tot)} " + " ".join(out))
