@@ -74,8 +74,8 @@ struct gnoc_engine
    int level_grid = 0;
 
    // static level plan of the port DAG (host + device copies)
-   std::vector<uint32_t> lvl_ports, lvl_off;
-   DevBuf d_lvl_ports, d_lvl_off;
+   std::vector<uint32_t> lvl_ports, lvl_off, port_k;
+   DevBuf d_lvl_ports, d_lvl_off, d_port_k;
 
    // trace
    size_t n = 0;
@@ -90,7 +90,7 @@ struct gnoc_engine
    DevBuf hist, tot, slot_cnt, slot_base, counters, gtot;
    DevBuf recs, samp_t, samp_id, Hs, Pp, Prow, nexc, dirty;
    DevBuf pio, pnc, pgb, lvl_cbase, chunk_port, flags, st, lvl_ctr;
-   DevBuf port_sum, port_cnt, port_mg1, plan_ports, stamps;
+   DevBuf port_sum, port_cnt, port_mg1, plan_ports, stamps, done;
    uint64_t h_chunk_bound = 0;
    int force_v1 = 0;
    int used_v3 = 0;
@@ -204,6 +204,8 @@ static void build_static_levels(gnoc_engine* e)
    }
    for (uint32_t t = 0; t < N; t++) P.push_back(t * PORTS + P_SELF);
    O.push_back((uint32_t) P.size());
+   e->port_k.assign((size_t) N * PORTS, 0xFFFFFFFFu);   // port id -> plan index
+   for (uint32_t k = 0; k < (uint32_t) P.size(); k++) e->port_k[P[k]] = k;
 }
 
 extern "C" {
@@ -280,13 +282,15 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    if (he == hipSuccess) he = hipHostMalloc((void**) &e->h_pinned, 64, hipHostMallocDefault);
    if (he == hipSuccess) he = e->d_lvl_ports.ensure(e->lvl_ports.size() * 4);
    if (he == hipSuccess) he = e->d_lvl_off.ensure(e->lvl_off.size() * 4);
+   if (he == hipSuccess) he = e->d_port_k.ensure(e->port_k.size() * 4);
+   if (he == hipSuccess) he = hipMemcpy(e->d_port_k.p, e->port_k.data(), e->port_k.size() * 4, hipMemcpyHostToDevice);
    if (he == hipSuccess)
       he = hipMemcpy(e->d_lvl_ports.p, e->lvl_ports.data(), e->lvl_ports.size() * 4, hipMemcpyHostToDevice);
    if (he == hipSuccess) he = hipMemcpy(e->d_lvl_off.p, e->lvl_off.data(), e->lvl_off.size() * 4, hipMemcpyHostToDevice);
    if (he == hipSuccess)
    {
       int per_cu = 0, cus = 0;
-      he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_level<false>, LV_T, 0);
+      he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_level<false, true>, LV_T, 0);
       if (he == hipSuccess) he = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
       e->level_grid = std::max(1, per_cu) * std::max(1, cus);
    }
@@ -490,7 +494,7 @@ static int run_levels_v3(gnoc_engine* e)
    GNOC_HIP(e, hipMemsetAsync(e->lvl_ctr.p, 0, (size_t) L * 4, s));
    const uint32_t pg = (P + 255) / 256;
    GNOC_LAUNCH(e, KC_PLAN, k_plan_ports, dim3(pg), dim3(256), 0, s, c, P, e->d_lvl_ports.as<uint32_t>(),
-               e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
+               e->d_port_k.as<uint32_t>(), e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
                LV_CTGT);
    GNOC_LAUNCH(e, KC_PLAN, k_plan_scan, dim3(1), dim3(1024), 0, s, P, L, e->d_lvl_off.as<uint32_t>(),
                e->pnc.as<uint32_t>(), e->pgb.as<uint32_t>(), e->lvl_cbase.as<uint32_t>());
@@ -505,23 +509,35 @@ static int run_levels_v3(gnoc_engine* e)
       GNOC_HIP(e, e->stamps.ensure(chunk_bound * 16 * 8));
       GNOC_HIP(e, hipMemsetAsync(e->stamps.p, 0, chunk_bound * 16 * 8, s));
    }
-   for (uint32_t l = 0; l < L; l++)
+   GNOC_HIP(e, e->done.ensure((size_t) P * 4));
+   GNOC_HIP(e, hipMemsetAsync(e->done.p, 0, (size_t) P * 4, s));
+   // default: one launch per level (the launch boundary is the level barrier).
+   // GNOC_XLEVEL=1: one persistent launch over every level with port-level
+   // release/acquire hand-offs -- exact, but a consumer still waits for whole
+   // producer ports and every chunk pays an L2 write-back: 2.8x slower on 32x32.
+   const char* xlv = std::getenv("GNOC_XLEVEL");
+   const bool xl = xlv && *xlv == '1';
+   uint64_t* stp = stamps ? e->stamps.as<uint64_t>() : nullptr;
+#define GNOC_LEVEL_ARGS(lvl)                                                                                         \
+   c, (lvl), e->lvl_cbase.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->chunk_port.as<uint32_t>(), e->pio.as<PortIO3>(), \
+      e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(),                 \
+      e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),                          \
+      e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(), e->counters.as<unsigned>() + 8,     \
+      e->done.as<uint32_t>(), stp
+   if (xl)
    {
-      if (stamps)
-         GNOC_LAUNCH(e, KC_LEVEL, k_level<true>, dim3(e->level_grid), dim3(LV_T), 0, s, c, l, e->lvl_cbase.as<uint32_t>(),
-                     e->lvl_ctr.as<unsigned>(), e->chunk_port.as<uint32_t>(), e->pio.as<PortIO3>(), e->recs.as<Rec>(),
-                     e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(),
-                     e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
-                     e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
-                     e->counters.as<unsigned>() + 8, e->stamps.as<uint64_t>());
-      else
-         GNOC_LAUNCH(e, KC_LEVEL, k_level<false>, dim3(e->level_grid), dim3(LV_T), 0, s, c, l, e->lvl_cbase.as<uint32_t>(),
-                     e->lvl_ctr.as<unsigned>(), e->chunk_port.as<uint32_t>(), e->pio.as<PortIO3>(), e->recs.as<Rec>(),
-                     e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(),
-                     e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),
-                     e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
-                     e->counters.as<unsigned>() + 8, (uint64_t*) nullptr);
+      if (stamps) GNOC_LAUNCH(e, KC_LEVEL, (k_level<true, true>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(L));
+      else GNOC_LAUNCH(e, KC_LEVEL, (k_level<false, true>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(L));
    }
+   else
+   {
+      for (uint32_t l = 0; l < L; l++)
+      {
+         if (stamps) GNOC_LAUNCH(e, KC_LEVEL, (k_level<true, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
+         else GNOC_LAUNCH(e, KC_LEVEL, (k_level<false, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
+      }
+   }
+#undef GNOC_LEVEL_ARGS
    return GNOC_OK;
 }
 

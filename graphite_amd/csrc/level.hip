@@ -36,7 +36,7 @@ constexpr int LV_IN = 4;                 // input slots per port (SELF, UP, DOWN
 constexpr int LV_SEG = LV_IN + 1;        // + the exception segment
 constexpr int LV_MAXLEAF = 32;           // leaves per chunk (bursts); beyond -> errflag, v1 rerun
 constexpr uint32_t LV_CTGT = 1200;       // target records per chunk
-constexpr uint32_t LV_SPIN_LIMIT = 1u << 24;
+constexpr uint64_t LV_SPIN_CYCLES = 1ull << 31;   // give up a wait after ~1 s (errflag -> exact v1 rerun)
 constexpr uint64_t LV_TAG = 1ull << 63;
 constexpr int LV_STATE_WORDS = 16;       // u64 per chunk state
 
@@ -51,8 +51,11 @@ struct __attribute__((aligned(16))) PortIO3
    uint32_t oslot[5];        // output slot ids
    uint32_t port, dir, nin, sb;
    uint32_t nx, ny, gbase, nc;
+   uint32_t prod[LV_IN];     // plan index of each input's producer port (LV_NO_PROD: the trace)
+   uint32_t prod_nc[LV_IN];  // that producer's chunk count: complete when done[prod] == prod_nc
 };
 static_assert(sizeof(PortIO3) % 16 == 0, "PortIO3 copy granularity");
+constexpr uint32_t LV_NO_PROD = 0xFFFFFFFFu;
 
 // Carried queue state (exclusive prefix of a chunk / leaf).
 struct Carry3
@@ -89,6 +92,7 @@ struct LvSmem
    // current chunk's key range
    uint64_t klo_t, khi_t;
    uint32_t klo_i, khi_i, has_lo, has_hi, empty, nc;
+   uint32_t pk, pad3, pad4, pad5;
    // next chunk, prefetched by waves 1-3 while wave 0 looks back
    struct
    {
@@ -96,6 +100,7 @@ struct LvSmem
       uint64_t klo_t, khi_t;
       uint32_t klo_i, khi_i;
       uint32_t g, valid, has_lo, has_hi, empty, ready;
+      uint32_t pk, deferred, pad0, pad1;
       uint32_t nmain[LV_IN], nxe[LV_IN];
       uint32_t search[2 * LV_IN];
    } nx;
@@ -751,6 +756,7 @@ __device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint64
    uint32_t accC[5] = { 0, 0, 0, 0, 0 };
    int32_t look = (int32_t) j - 1;
    uint32_t spins = 0;
+   const uint64_t t_start = __builtin_amdgcn_s_memtime();
    for (;;)
    {
       const int32_t ck = look - (int32_t) lane;
@@ -770,7 +776,9 @@ __device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint64
       const uint64_t need = L >= 64 ? ~0ull : ((1ull << L) - 1);
       if (bad & need)
       {
-         if (++spins > LV_SPIN_LIMIT) { if (lane == 0) atomicOr(errflag, 2u); return false; }
+         ++spins;
+         if (__builtin_amdgcn_s_memtime() - t_start > LV_SPIN_CYCLES) { if (lane == 0) atomicOr(errflag, 2u); return false; }
+         if (__hip_atomic_load(errflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 6u) return false;   // another chunk gave up
          __builtin_amdgcn_s_sleep(1);
          continue;
       }
@@ -804,7 +812,8 @@ __device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint64
             {
                p3 = lv_ld(w + 3); p4 = lv_ld(w + 4); p5 = lv_ld(w + 5); p6 = lv_ld(w + 6);
                if (p3 && (p4 & LV_TAG) && (p5 & LV_TAG) && (p6 & LV_TAG)) break;
-               if (++spins > LV_SPIN_LIMIT) { if (lane == 0) atomicOr(errflag, 2u); return false; }
+               if (__builtin_amdgcn_s_memtime() - t_start > LV_SPIN_CYCLES) { if (lane == 0) atomicOr(errflag, 2u); return false; }
+               if (__hip_atomic_load(errflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 6u) return false;
                __builtin_amdgcn_s_sleep(1);
             }
             const uint32_t zero[5] = { 0, 0, 0, 0, 0 };
@@ -823,31 +832,47 @@ __device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint64
 // ---------------------------------------------------------------------------
 // the level kernel: a persistent grid pulls the level's chunks in order
 // ---------------------------------------------------------------------------
-// Waves 1..3 fetch the next chunk of the level: dynamic chunk id, its port
-// descriptor, exception counts, split keys (wave 1), then the sample searches
-// of the other inputs (all three waves).  Results in sm.nx.
-__device__ __noinline__ void lv_fetch(LvSmem& sm, uint32_t level, uint32_t cb0, uint32_t nch, unsigned* __restrict__ ctr,
-                                      const uint32_t* __restrict__ chunk_port, const PortIO3* __restrict__ pio,
-                                      const Rec* __restrict__ recs, const uint64_t* __restrict__ samp_t,
-                                      const uint32_t* __restrict__ samp_id, const uint32_t* __restrict__ nexc)
+// Next-chunk prefetch, by waves 1..3 of the workgroup (results in sm.nx).
+// lv_fetch_keys: input exception counts, split keys (wave 1), then the sample
+// searches of the other inputs (all three waves).  In the cross-level launch
+// (XL) it first needs every producer port of the chunk complete: blocking, it
+// waits; otherwise it returns false and leaves the work to the take.
+template <bool XL>
+__device__ __noinline__ bool lv_fetch_keys(LvSmem& sm, bool block, const Rec* __restrict__ recs,
+                                           const uint64_t* __restrict__ samp_t, const uint32_t* __restrict__ samp_id,
+                                           const uint32_t* __restrict__ nexc, const uint32_t* __restrict__ done,
+                                           unsigned* __restrict__ errflag)
 {
    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
    auto& d = sm.nx;
    if (wv == 1)
    {
-      uint32_t cid = 0;
-      if (lane == 0) cid = atomicAdd(&ctr[level], 1u);   // in order: every predecessor chunk is running
-      cid = __shfl(cid, 0);
-      const uint32_t valid = cid < nch ? 1u : 0u;
-      const uint32_t g = cb0 + cid;
-      if (valid)
+      const uint32_t nin = d.io.nin;
+      bool go = true;
+      if (XL)
       {
-         const uint32_t pk = chunk_port[g];
-         const uint32_t* srcw = reinterpret_cast<const uint32_t*>(pio + pk);
-         uint32_t* dstw = reinterpret_cast<uint32_t*>(&d.io);
-         if (lane < (uint32_t) (sizeof(PortIO3) / 4)) dstw[lane] = srcw[lane];
-         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-         const uint32_t nin = d.io.nin;
+         // producer ports complete?  (release: end of every producer chunk)
+         const uint64_t t_start = __builtin_amdgcn_s_memtime();
+         for (;;)
+         {
+            bool ok = true;
+            if (lane < nin && d.io.prod[lane] != LV_NO_PROD)
+               ok = __hip_atomic_load(&done[d.io.prod[lane]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                    d.io.prod_nc[lane];
+            if (__all(ok)) break;
+            if (!block) { go = false; break; }
+            if (__builtin_amdgcn_s_memtime() - t_start > LV_SPIN_CYCLES) { if (lane == 0) atomicOr(errflag, 2u); break; }
+            if (__hip_atomic_load(errflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 6u) break;
+            __builtin_amdgcn_s_sleep(2);
+         }
+         if (go)
+         {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // this CU's L1 may hold stale lines
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+         }
+      }
+      if (go)
+      {
          if (lane < nin)
          {
             const uint32_t x = nexc[d.io.slot[lane]];
@@ -855,7 +880,7 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, uint32_t level, uint32_t cb0, 
             d.nmain[lane] = d.io.cnt[lane] - x;
          }
          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-         const uint32_t j = g - d.io.gbase, nc = d.io.nc, sb = d.io.sb;
+         const uint32_t j = d.g - d.io.gbase, nc = d.io.nc, sb = d.io.sb;
          const uint32_t nb = d.nmain[sb];
          uint32_t has_lo = j > 0, has_hi = j + 1 < nc, empty = 0;
          if (nb == 0) { empty = j > 0; has_lo = has_hi = 0; }   // only exceptions: chunk 0 takes all
@@ -888,7 +913,7 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, uint32_t level, uint32_t cb0, 
             }
          }
       }
-      if (lane == 3) { d.g = g; d.valid = valid; }
+      if (lane == 3) d.deferred = go ? 0u : 1u;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_store(&d.ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
    }
@@ -897,7 +922,8 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, uint32_t level, uint32_t cb0, 
       while (__hip_atomic_load(&d.ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
          __builtin_amdgcn_s_sleep(1);
    }
-   if (!d.valid || d.empty) return;
+   if (d.deferred) return false;
+   if (d.empty) return true;
    const uint32_t nin = d.io.nin, sb = d.io.sb;
    for (uint32_t q = wv - 1; q < 2 * (uint32_t) LV_IN; q += 3)
    {
@@ -909,6 +935,50 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, uint32_t level, uint32_t cb0, 
                                  which ? d.khi_t : d.klo_t, which ? d.khi_i : d.klo_i, lane);
       if (lane == 0) d.search[q] = v;
    }
+   return true;
+}
+
+// lv_fetch: dynamic chunk id and its port descriptor (wave 1), then the keys
+// if they can be had without blocking.  Waves 1..3 call it.
+template <bool XL>
+__device__ __noinline__ void lv_fetch(LvSmem& sm, uint32_t cb0, uint32_t nch, unsigned* __restrict__ ctr,
+                                      const uint32_t* __restrict__ chunk_port, const PortIO3* __restrict__ pio,
+                                      const Rec* __restrict__ recs, const uint64_t* __restrict__ samp_t,
+                                      const uint32_t* __restrict__ samp_id, const uint32_t* __restrict__ nexc,
+                                      const uint32_t* __restrict__ done, unsigned* __restrict__ errflag)
+{
+   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+   auto& d = sm.nx;
+   if (wv == 1)
+   {
+      uint32_t cid = 0;
+      if (lane == 0) cid = atomicAdd(ctr, 1u);   // in order: every predecessor chunk is running or held
+      cid = __shfl(cid, 0);
+      const uint32_t valid = cid < nch ? 1u : 0u;
+      const uint32_t g = cb0 + cid;
+      if (valid)
+      {
+         const uint32_t pk = chunk_port[g];
+         const uint32_t* srcw = reinterpret_cast<const uint32_t*>(pio + pk);
+         uint32_t* dstw = reinterpret_cast<uint32_t*>(&d.io);
+         if (lane < (uint32_t) (sizeof(PortIO3) / 4)) dstw[lane] = srcw[lane];
+         if (lane == 4) d.pk = pk;
+      }
+      if (lane == 3) { d.g = g; d.valid = valid; }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+   }
+   // waves 2, 3 wait inside lv_fetch_keys for wave 1's ready flag
+   if (wv == 1 && !d.valid)
+   {
+      if (lane == 0)
+      {
+         d.deferred = 0;
+         d.empty = 1;
+         __hip_atomic_store(&d.ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      return;
+   }
+   lv_fetch_keys<XL>(sm, false, recs, samp_t, samp_id, nexc, done, errflag);
 }
 
 #define LV_STAMP(k)                                                                                          \
@@ -921,7 +991,7 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, uint32_t level, uint32_t cb0, 
 #define LV_MIN_WAVES 4   // waves per SIMD the register allocation must leave room for
 #endif
 
-template <bool STAMPS>
+template <bool STAMPS, bool XL>
 __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t level, const uint32_t* __restrict__ lvl_cbase,
                                                 unsigned* __restrict__ ctr, const uint32_t* __restrict__ chunk_port,
                                                 const PortIO3* __restrict__ pio, Rec* __restrict__ recs,
@@ -931,20 +1001,30 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
                                                 unsigned long long* __restrict__ port_sum,
                                                 unsigned long long* __restrict__ port_cnt,
                                                 unsigned long long* __restrict__ port_mg1, unsigned* __restrict__ errflag,
-                                                uint64_t* __restrict__ stamps)
+                                                uint32_t* __restrict__ done, uint64_t* __restrict__ stamps)
 {
    __shared__ LvSmem sm;
    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-   const uint32_t cb0 = lvl_cbase[level];
-   const uint32_t nch = lvl_cbase[level + 1] - cb0;
+   // per-level launch: chunks of `level`; cross-level launch (XL, level = number of levels): all chunks
+   const uint32_t cb0 = XL ? 0u : lvl_cbase[level];
+   const uint32_t nch = XL ? lvl_cbase[level] : lvl_cbase[level + 1] - cb0;
+   unsigned* const cctr = XL ? ctr : ctr + level;
    if (tid == 0) sm.nx.ready = 0;
    lv_bar();
-   if (wv >= 1) lv_fetch(sm, level, cb0, nch, ctr, chunk_port, pio, recs, samp_t, samp_id, nexc);
+   if (wv >= 1) lv_fetch<XL>(sm, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
    lv_bar();
    for (;;)
    {
-      // ---- take the prefetched chunk
+      // ---- take the prefetched chunk (its keys first, if they had to wait for producers)
       if (!sm.nx.valid) return;
+      if (__hip_atomic_load(errflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 6u) return;   // rerun on v1 follows
+      if (sm.nx.deferred)
+      {
+         if (tid == 0) sm.nx.ready = 0;
+         lv_bar();
+         if (wv >= 1) lv_fetch_keys<XL>(sm, true, recs, samp_t, samp_id, nexc, done, errflag);
+         lv_bar();
+      }
       const uint32_t g = sm.nx.g;
       LV_STAMP(0);
       {
@@ -962,6 +1042,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
             sm.klo_t = sm.nx.klo_t; sm.klo_i = sm.nx.klo_i; sm.khi_t = sm.nx.khi_t; sm.khi_i = sm.nx.khi_i;
             sm.has_lo = sm.nx.has_lo; sm.has_hi = sm.nx.has_hi; sm.empty = sm.nx.empty;
             sm.g = g;
+            sm.pk = sm.nx.pk;
             sm.st_sum = 0;
             sm.st_cnt = 0;
             sm.st_mg1 = 0;
@@ -1022,7 +1103,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
             {
                if (tid == 0) lv_publish_agg(st, g, so);
                if (wv == 0) lv_lookback(sm, sm.io.gbase, j, st, errflag);
-               else lv_fetch(sm, level, cb0, nch, ctr, chunk_port, pio, recs, samp_t, samp_id, nexc);
+               else lv_fetch<XL>(sm, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
                fetched = true;
                lv_bar();
             }
@@ -1155,7 +1236,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
       lv_bar();
       if (!fetched)
       {
-         if (wv >= 1) lv_fetch(sm, level, cb0, nch, ctr, chunk_port, pio, recs, samp_t, samp_id, nexc);
+         if (wv >= 1) lv_fetch<XL>(sm, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
       }
       if (tid == 0)
       {
@@ -1174,6 +1255,20 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
          atomicAdd(&port_cnt[sm.io.port], (unsigned long long) sm.st_cnt);
          if (sm.st_mg1) atomicAdd(&port_mg1[sm.io.port], (unsigned long long) sm.st_mg1);
       }
+      if (XL)
+      {
+         // this chunk's records, samples and exception counts, released to the
+         // consumer ports (MI355X_MICROARCH.md, inter-workgroup visibility):
+         // every wave drains its stores, one lane releases at agent scope, then counts
+         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+         lv_bar();
+         if (tid == 0)
+         {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(&done[sm.pk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+         }
+      }
       lv_bar();
    }
 }
@@ -1182,7 +1277,19 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
 // device-side plan
 // ---------------------------------------------------------------------------
 // One thread per port (level order): input slots, output slots, chunk count.
+__device__ __forceinline__ uint32_t plan_nc(const uint32_t* __restrict__ slot_cnt, uint32_t port, uint32_t ctgt)
+{
+   uint32_t tot = 0, nin = 0;
+   for (uint32_t in = 0; in < INS; in++)
+   {
+      const uint32_t n = slot_cnt[port * INS + in];
+      if (n && nin < (uint32_t) LV_IN) { tot += n; nin++; }
+   }
+   return tot ? (tot + ctgt - 1) / ctgt : 0;
+}
+
 __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const uint32_t* __restrict__ lvl_ports,
+                                                    const uint32_t* __restrict__ port_k,
                                                     const uint32_t* __restrict__ slot_cnt,
                                                     const uint64_t* __restrict__ slot_base, PortIO3* __restrict__ pio,
                                                     uint32_t* __restrict__ pnc, uint32_t ctgt)
@@ -1197,7 +1304,10 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
    io.nin = 0;
    io.sb = 0;
    uint32_t tot = 0, best = 0;
-   for (uint32_t s = 0; s < (uint32_t) LV_IN; s++) { io.base[s] = 0; io.slot[s] = 0; io.cnt[s] = 0; }
+   for (uint32_t s = 0; s < (uint32_t) LV_IN; s++)
+   {
+      io.base[s] = 0; io.slot[s] = 0; io.cnt[s] = 0; io.prod[s] = LV_NO_PROD; io.prod_nc[s] = 0;
+   }
    for (uint32_t in = 0; in < INS; in++)
    {
       const uint32_t sl = port * INS + in;
@@ -1207,6 +1317,15 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
          io.slot[io.nin] = sl;
          io.base[io.nin] = slot_base[sl];
          io.cnt[io.nin] = n;
+         // the port that writes this slot (XY routing, emesh_hop_by_hop.cc:229-240)
+         uint32_t pp = LV_NO_PROD;
+         if (in == IN_LOCAL) pp = dir == P_INJ ? LV_NO_PROD : tile * PORTS + P_INJ;
+         else if (in == IN_W) pp = (tile - 1) * PORTS + P_RIGHT;
+         else if (in == IN_E) pp = (tile + 1) * PORTS + P_LEFT;
+         else if (in == IN_S) pp = (tile - c.W) * PORTS + P_UP;
+         else if (in == IN_N) pp = (tile + c.W) * PORTS + P_DOWN;
+         io.prod[io.nin] = pp == LV_NO_PROD ? LV_NO_PROD : port_k[pp];
+         io.prod_nc[io.nin] = pp == LV_NO_PROD ? 0u : plan_nc(slot_cnt, pp, ctgt);
          if (n > best) { best = n; io.sb = io.nin; }
          io.nin++;
          tot += n;
