@@ -30,12 +30,18 @@
 namespace gnoc {
 
 constexpr int LV_T = 256;                // threads per workgroup
-constexpr int LV_CAP = 1792;             // records one leaf holds in LDS
-constexpr int LV_PER = LV_CAP / LV_T;    // records per thread in the scan
+#ifndef LV_CAP_V
+#define LV_CAP_V 1888
+#endif
+constexpr int LV_CAP = LV_CAP_V;         // records one leaf holds in LDS
+constexpr int LV_PER = (LV_CAP + LV_T - 1) / LV_T;   // records per thread (load phase)
 constexpr int LV_IN = 4;                 // input slots per port (SELF, UP, DOWN have 4)
 constexpr int LV_SEG = LV_IN + 1;        // + the exception segment
 constexpr int LV_MAXLEAF = 32;           // leaves per chunk (bursts); beyond -> errflag, v1 rerun
-constexpr uint32_t LV_CTGT = 1200;       // target records per chunk
+#ifndef LV_CTGT_V
+#define LV_CTGT_V 1600
+#endif
+constexpr uint32_t LV_CTGT = LV_CTGT_V;  // target records per chunk
 constexpr uint64_t LV_SPIN_CYCLES = 1ull << 31;   // give up a wait after ~1 s (errflag -> exact v1 rerun)
 constexpr uint64_t LV_TAG = 1ull << 63;
 constexpr int LV_STATE_WORDS = 16;       // u64 per chunk state
@@ -100,7 +106,7 @@ struct LvSmem
       uint64_t klo_t, khi_t;
       uint32_t klo_i, khi_i;
       uint32_t g, valid, has_lo, has_hi, empty, ready;
-      uint32_t pk, deferred, pad0, pad1;
+      uint32_t pk, deferred, ilo, ihi;
       uint32_t nmain[LV_IN], nxe[LV_IN];
       uint32_t search[2 * LV_IN];
    } nx;
@@ -187,6 +193,56 @@ __device__ uint32_t wave_lb(const Rec* __restrict__ r, const uint64_t* __restric
 {
    if (n == 0) return 0;
    uint32_t lo = 0, hi = (n + 63) / 64;
+   while (lo < hi)
+   {
+      const uint32_t step = (hi - lo + 63) / 64;
+      const uint32_t i = lo + lane * step;
+      bool t = false;
+      if (i < hi) t = sp_t[i] < kt || (sp_t[i] == kt && sp_i[i] < ki);
+      const uint32_t c = (uint32_t) __popcll(__ballot(t));
+      if (c == 0) hi = lo;
+      else
+      {
+         const uint32_t nh = min(lo + c * step, hi);
+         lo = lo + (c - 1) * step + 1;
+         hi = nh;
+      }
+   }
+   if (lo == 0) return 0;
+   const uint32_t base = (lo - 1) * 64;
+   const uint32_t k = base + lane;
+   bool t = false;
+   if (k < n) t = rlt(r[k], kt, ki);
+   return base + (uint32_t) __popcll(__ballot(t));
+}
+
+// wave_lb with the key itself read from memory (a sample of the split input):
+// the key load and the first level of sample reads are independent, so they
+// share one round trip.
+__device__ uint32_t wave_lb2(const Rec* __restrict__ r, const uint64_t* __restrict__ sp_t,
+                             const uint32_t* __restrict__ sp_i, uint32_t n, const uint64_t* __restrict__ key_t,
+                             const uint32_t* __restrict__ key_i, uint32_t lane)
+{
+   if (n == 0) return 0;
+   uint32_t lo = 0, hi = (n + 63) / 64;
+   const uint32_t step0 = (hi + 63) / 64;
+   const uint32_t i0 = lane * step0;
+   uint64_t s0t = 0;
+   uint32_t s0i = 0;
+   if (i0 < hi) { s0t = sp_t[i0]; s0i = sp_i[i0]; }
+   const uint64_t kt = *key_t;
+   const uint32_t ki = *key_i;
+   {
+      const bool t = i0 < hi && (s0t < kt || (s0t == kt && s0i < ki));
+      const uint32_t c = (uint32_t) __popcll(__ballot(t));
+      if (c == 0) hi = lo;
+      else
+      {
+         const uint32_t nh = min(lo + c * step0, hi);
+         lo = lo + (c - 1) * step0 + 1;
+         hi = nh;
+      }
+   }
    while (lo < hi)
    {
       const uint32_t step = (hi - lo + 63) / 64;
@@ -580,6 +636,7 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
          {
             // M/G/1-served: may leave FIFO order -> exception tail of the slot
             const uint32_t x = atomicAdd(&nexc[sm.io.oslot[nd]], 1u);
+            atomicOr(errflag + 2, 1u);   // "some slot has exceptions": later levels read nexc
             if (x >= sm.io.ocnt[nd]) { atomicOr(errflag, 1u); continue; }
             recs[sm.io.obase[nd] + sm.io.ocnt[nd] - 1 - x] = o;
          }
@@ -838,7 +895,7 @@ __device__ bool lv_lookback(LvSmem& sm, uint32_t gbase, uint32_t j, const uint64
 // (XL) it first needs every producer port of the chunk complete: blocking, it
 // waits; otherwise it returns false and leaves the work to the take.
 template <bool XL>
-__device__ __noinline__ bool lv_fetch_keys(LvSmem& sm, bool block, const Rec* __restrict__ recs,
+__device__ __noinline__ bool lv_fetch_keys(LvSmem& sm, bool block, bool anyexc, const Rec* __restrict__ recs,
                                            const uint64_t* __restrict__ samp_t, const uint32_t* __restrict__ samp_id,
                                            const uint32_t* __restrict__ nexc, const uint32_t* __restrict__ done,
                                            unsigned* __restrict__ errflag)
@@ -875,7 +932,8 @@ __device__ __noinline__ bool lv_fetch_keys(LvSmem& sm, bool block, const Rec* __
       {
          if (lane < nin)
          {
-            const uint32_t x = nexc[d.io.slot[lane]];
+            // exception counts only if some earlier level wrote exceptions (rare)
+            const uint32_t x = anyexc ? nexc[d.io.slot[lane]] : 0u;
             d.nxe[lane] = x;
             d.nmain[lane] = d.io.cnt[lane] - x;
          }
@@ -884,21 +942,13 @@ __device__ __noinline__ bool lv_fetch_keys(LvSmem& sm, bool block, const Rec* __
          const uint32_t nb = d.nmain[sb];
          uint32_t has_lo = j > 0, has_hi = j + 1 < nc, empty = 0;
          if (nb == 0) { empty = j > 0; has_lo = has_hi = 0; }   // only exceptions: chunk 0 takes all
-         const uint32_t ilo = (uint32_t) (((uint64_t) j * nb) / nc);
-         const uint32_t ihi = (uint32_t) (((uint64_t) (j + 1) * nb) / nc);
-         if (lane == 0)
-         {
-            d.klo_t = 0; d.klo_i = 0;
-            if (has_lo) { const Rec r = recs[d.io.base[sb] + ilo]; d.klo_t = r.t; d.klo_i = r.id; }
-         }
-         if (lane == 1)
-         {
-            d.khi_t = ~0ull; d.khi_i = ~0u;
-            if (has_hi) { const Rec r = recs[d.io.base[sb] + ihi]; d.khi_t = r.t; d.khi_i = r.id; }
-         }
+         // split indices on 64-record boundaries: the split key is a sample
+         const uint32_t ilo = (uint32_t) (((uint64_t) j * nb) / nc) & ~63u;
+         const uint32_t ihi = (uint32_t) (((uint64_t) (j + 1) * nb) / nc) & ~63u;
          if (lane == 2)
          {
             d.has_lo = has_lo; d.has_hi = has_hi; d.empty = empty;
+            d.ilo = ilo; d.ihi = ihi;
             for (uint32_t q = 0; q < 2 * (uint32_t) LV_IN; q++) d.search[q] = 0;
             if (!empty)
             {
@@ -923,16 +973,33 @@ __device__ __noinline__ bool lv_fetch_keys(LvSmem& sm, bool block, const Rec* __
          __builtin_amdgcn_s_sleep(1);
    }
    if (d.deferred) return false;
+   const uint32_t sb = d.io.sb;
+   const uint64_t kb = d.io.base[sb] >> 6;   // sample index of the split input's first record
+   if (wv == 1)
+   {
+      // the chunk's own key range (exception filter, leaf splits)
+      if (lane == 0)
+      {
+         d.klo_t = 0; d.klo_i = 0;
+         if (!d.empty && d.has_lo) { d.klo_t = samp_t[kb + d.ilo / 64]; d.klo_i = samp_id[kb + d.ilo / 64]; }
+      }
+      if (lane == 1)
+      {
+         d.khi_t = ~0ull; d.khi_i = ~0u;
+         if (!d.empty && d.has_hi) { d.khi_t = samp_t[kb + d.ihi / 64]; d.khi_i = samp_id[kb + d.ihi / 64]; }
+      }
+   }
    if (d.empty) return true;
-   const uint32_t nin = d.io.nin, sb = d.io.sb;
+   const uint32_t nin = d.io.nin;
    for (uint32_t q = wv - 1; q < 2 * (uint32_t) LV_IN; q += 3)
    {
       const uint32_t s = q >> 1, which = q & 1;
       if (s >= nin || s == sb) continue;
       if ((which == 0 && !d.has_lo) || (which == 1 && !d.has_hi)) continue;
       const uint64_t sbase = d.io.base[s] >> 6;
-      const uint32_t v = wave_lb(recs + d.io.base[s], samp_t + sbase, samp_id + sbase, d.nmain[s],
-                                 which ? d.khi_t : d.klo_t, which ? d.khi_i : d.klo_i, lane);
+      const uint64_t ks = kb + (which ? d.ihi : d.ilo) / 64;
+      const uint32_t v = wave_lb2(recs + d.io.base[s], samp_t + sbase, samp_id + sbase, d.nmain[s], samp_t + ks,
+                                  samp_id + ks, lane);
       if (lane == 0) d.search[q] = v;
    }
    return true;
@@ -941,7 +1008,7 @@ __device__ __noinline__ bool lv_fetch_keys(LvSmem& sm, bool block, const Rec* __
 // lv_fetch: dynamic chunk id and its port descriptor (wave 1), then the keys
 // if they can be had without blocking.  Waves 1..3 call it.
 template <bool XL>
-__device__ __noinline__ void lv_fetch(LvSmem& sm, uint32_t cb0, uint32_t nch, unsigned* __restrict__ ctr,
+__device__ __noinline__ void lv_fetch(LvSmem& sm, bool anyexc, uint32_t cb0, uint32_t nch, unsigned* __restrict__ ctr,
                                       const uint32_t* __restrict__ chunk_port, const PortIO3* __restrict__ pio,
                                       const Rec* __restrict__ recs, const uint64_t* __restrict__ samp_t,
                                       const uint32_t* __restrict__ samp_id, const uint32_t* __restrict__ nexc,
@@ -978,7 +1045,7 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, uint32_t cb0, uint32_t nch, un
       }
       return;
    }
-   lv_fetch_keys<XL>(sm, false, recs, samp_t, samp_id, nexc, done, errflag);
+   lv_fetch_keys<XL>(sm, false, anyexc, recs, samp_t, samp_id, nexc, done, errflag);
 }
 
 #define LV_STAMP(k)                                                                                          \
@@ -1009,9 +1076,12 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
    const uint32_t cb0 = XL ? 0u : lvl_cbase[level];
    const uint32_t nch = XL ? lvl_cbase[level] : lvl_cbase[level + 1] - cb0;
    unsigned* const cctr = XL ? ctr : ctr + level;
+   // exception tails exist only if an earlier level's M/G/1 path wrote one (flag set
+   // before this launch); the cross-level launch always reads the counts
+   const bool anyexc = XL || errflag[2] != 0;
    if (tid == 0) sm.nx.ready = 0;
    lv_bar();
-   if (wv >= 1) lv_fetch<XL>(sm, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
+   if (wv >= 1) lv_fetch<XL>(sm, anyexc, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
    lv_bar();
    for (;;)
    {
@@ -1022,11 +1092,12 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
       {
          if (tid == 0) sm.nx.ready = 0;
          lv_bar();
-         if (wv >= 1) lv_fetch_keys<XL>(sm, true, recs, samp_t, samp_id, nexc, done, errflag);
+         if (wv >= 1) lv_fetch_keys<XL>(sm, true, anyexc, recs, samp_t, samp_id, nexc, done, errflag);
          lv_bar();
       }
       const uint32_t g = sm.nx.g;
       LV_STAMP(0);
+      if (STAMPS && stamps && tid == 0) stamps[(uint64_t) g * 16 + 1] = __builtin_amdgcn_s_memrealtime();
       {
          const uint32_t* srcw = reinterpret_cast<const uint32_t*>(&sm.nx.io);
          uint32_t* dstw = reinterpret_cast<uint32_t*>(&sm.io);
@@ -1059,7 +1130,6 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
       const bool has_lo = sm.has_lo, has_hi = sm.has_hi, empty = sm.empty;
       const uint64_t klo_t = sm.klo_t, khi_t = sm.khi_t;
       const uint32_t klo_i = sm.klo_i, khi_i = sm.khi_i;
-      LV_STAMP(1);
       LV_STAMP(2);
       uint32_t total = 0, totexc = 0;
 #pragma unroll
@@ -1102,8 +1172,9 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
             if (j > 0)
             {
                if (tid == 0) lv_publish_agg(st, g, so);
+               if (STAMPS && stamps && tid == 0) stamps[(uint64_t) g * 16 + 15] = __builtin_amdgcn_s_memrealtime();
                if (wv == 0) lv_lookback(sm, sm.io.gbase, j, st, errflag);
-               else lv_fetch<XL>(sm, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
+               else lv_fetch<XL>(sm, anyexc, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
                fetched = true;
                lv_bar();
             }
@@ -1236,7 +1307,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
       lv_bar();
       if (!fetched)
       {
-         if (wv >= 1) lv_fetch<XL>(sm, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
+         if (wv >= 1) lv_fetch<XL>(sm, anyexc, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
       }
       if (tid == 0)
       {

@@ -33,7 +33,7 @@ for dirn, label in ((5, "INJ"), (2, "RIGHT"), (1, "LEFT"), (4, "UP"), (3, "DOWN"
     if not m.any():
         continue
     s = st[m]
-    out = [f"{names[k]}={int(np.median(s[:, k] - s[:, k - 1]))}" for k in range(1, 9)]
+    out = [f"{names[k]}={int(np.median(s[:, k] - s[:, k - 1]))}" for k in range(3, 9)]
     tot = np.median(s[:, 8] - s[:, 0])
     lb = s[:, 13] - s[:, 5]
     spins = s[:, 14] & 0xFFFFFFFF
@@ -43,3 +43,15 @@ for dirn, label in ((5, "INJ"), (2, "RIGHT"), (1, "LEFT"), (4, "UP"), (3, "DOWN"
     out.append(f"[load={int(np.median(s[:, 11] - s[:, 3]))} exc={int(np.median(s[:, 12] - s[:, 11]))} "
                f"merge={int(np.median(s[:, 4] - s[:, 12]))}]")
     print(f"{label:6s} n={m.sum():6d} total={int(tot)} " + " ".join(out))
+
+# predecessor timing (s_memrealtime, 100 MHz -> ns x10): take and aggregate publish of chunk g-1 vs g
+gi = np.nonzero((j > 0) & (st[:, 15] > 0))[0]
+prev = gi - 1
+okp = st[prev, 15] > 0
+gi, prev = gi[okp], prev[okp]
+dt_take = (st[prev, 1] - st[gi, 1]) * 10
+dt_pub = (st[prev, 15] - st[gi, 15]) * 10
+print("pred take - own take (ns): med", int(np.median(dt_take)), "p10", int(np.percentile(dt_take, 10)), "p90", int(np.percentile(dt_take, 90)), "frac pred later", round(float((dt_take > 0).mean()), 3))
+print("pred pub  - own pub  (ns): med", int(np.median(dt_pub)), "p10", int(np.percentile(dt_pub, 10)), "p90", int(np.percentile(dt_pub, 90)), "frac pred later", round(float((dt_pub > 0).mean()), 3))
+own = (st[gi, 15] - st[gi, 1]) * 10
+print("own take->pub (ns): med", int(np.median(own)), "p90", int(np.percentile(own, 90)))
