@@ -482,20 +482,22 @@ static int run_levels_v3(gnoc_engine* e)
    hipStream_t s = e->stream;
    const uint32_t P = (uint32_t) e->lvl_ports.size();
    const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
-   const uint64_t chunk_bound = e->rec_bound / LV_CTGT + P + 1;
+   const uint64_t chunk_bound = e->rec_bound / ((LV_CTGT + 1) / 2) + P + 1;   // guided tails use half-size chunks
    GNOC_HIP(e, e->pio.ensure((size_t) P * sizeof(PortIO3)));
    GNOC_HIP(e, e->pnc.ensure((size_t) P * 4));
    GNOC_HIP(e, e->pgb.ensure((size_t) P * 4));
    GNOC_HIP(e, e->lvl_cbase.ensure((size_t) (L + 1) * 4));
    GNOC_HIP(e, e->chunk_port.ensure(chunk_bound * 4));
    GNOC_HIP(e, e->st.ensure(chunk_bound * LV_STATE_WORDS * 8));
-   GNOC_HIP(e, e->lvl_ctr.ensure((size_t) L * 4));
+   GNOC_HIP(e, e->lvl_ctr.ensure((size_t) L * LV_QUEUES * 4));
    GNOC_HIP(e, hipMemsetAsync(e->st.p, 0, chunk_bound * LV_STATE_WORDS * 8, s));   // look-back granules
-   GNOC_HIP(e, hipMemsetAsync(e->lvl_ctr.p, 0, (size_t) L * 4, s));
+   GNOC_HIP(e, hipMemsetAsync(e->lvl_ctr.p, 0, (size_t) L * LV_QUEUES * 4, s));
    const uint32_t pg = (P + 255) / 256;
    GNOC_LAUNCH(e, KC_PLAN, k_plan_ports, dim3(pg), dim3(256), 0, s, c, P, e->d_lvl_ports.as<uint32_t>(),
                e->d_port_k.as<uint32_t>(), e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
                LV_CTGT);
+   GNOC_LAUNCH(e, KC_PLAN, k_plan_guided, dim3(L), dim3(1024), 0, s, e->d_lvl_off.as<uint32_t>(), e->pnc.as<uint32_t>(),
+               LV_CTGT, (uint64_t) e->level_grid * LV_CTGT * LV_TAIL_ROUNDS_NUM / LV_TAIL_ROUNDS_DEN);
    GNOC_LAUNCH(e, KC_PLAN, k_plan_scan, dim3(1), dim3(1024), 0, s, P, L, e->d_lvl_off.as<uint32_t>(),
                e->pnc.as<uint32_t>(), e->pgb.as<uint32_t>(), e->lvl_cbase.as<uint32_t>());
    GNOC_LAUNCH(e, KC_PLAN, k_plan_expand, dim3(pg), dim3(256), 0, s, P, e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
@@ -639,7 +641,11 @@ static int run_once(gnoc_engine* e)
                e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>());
    GNOC_LAUNCH(e, KC_SRC_OFFS, k_src_offs, dim3(ng), dim3(256), 0, s, N, nch, e->hist.as<uint32_t>(),
                e->slot_base.as<uint64_t>());
-   if (n)
+   if (n && N <= SC4_MAXN)
+      GNOC_LAUNCH(e, KC_SCATTER, k_scatter4, dim3(nch), dim3(256), 4 * N * 4, s, (uint64_t) n, pch, N, nbits, e->d_src,
+                  e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(), e->recs.as<Rec>(),
+                  e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>());
+   else if (n)
       GNOC_LAUNCH(e, KC_SCATTER, k_scatter, dim3(nch), dim3(64), N * 4, s, (uint64_t) n, pch, N, nbits, e->d_src,
                   e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(), e->recs.as<Rec>(),
                   e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>());
@@ -647,8 +653,16 @@ static int run_once(gnoc_engine* e)
                e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->Hs.as<uint32_t>(), e->Pp.as<uint32_t>(), pp_lds);
    GNOC_LAUNCH(e, KC_PROW, k_prow, dim3((uint32_t) (((uint64_t) H * N + 255) / 256)), dim3(256), 0, s, N, H, G,
                e->Pp.as<uint32_t>(), e->Prow.as<uint32_t>());
-   GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts, dim3((N * 5 + 255) / 256), dim3(256), 0, s, c, e->Hs.as<uint32_t>(),
-               e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>());
+   if (W <= 64 && H <= 64)
+   {
+      GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_x, dim3(H), dim3(256), (size_t) W * W * 3 * 4, s, c,
+                  e->Hs.as<uint32_t>(), e->slot_cnt.as<uint32_t>());
+      GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_y, dim3(W), dim3(256), (size_t) H * H * 4, s, c,
+                  e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>());
+   }
+   else
+      GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts, dim3((N * 5 + 255) / 256), dim3(256), 0, s, c, e->Hs.as<uint32_t>(),
+                  e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>());
    GNOC_LAUNCH(e, KC_SCAN, k_scan_slots, dim3(1), dim3(1024), 0, s, N, e->slot_cnt.as<uint32_t>(),
                e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>(), e->gtot.as<uint64_t>() + 1);
 

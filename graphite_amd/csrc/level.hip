@@ -42,8 +42,13 @@ constexpr int LV_MAXLEAF = 32;           // leaves per chunk (bursts); beyond ->
 #define LV_CTGT_V 1600
 #endif
 constexpr uint32_t LV_CTGT = LV_CTGT_V;  // target records per chunk
+#ifndef LV_TAIL_ROUNDS_NUM
+#define LV_TAIL_ROUNDS_NUM 0   // records at the end of a level cut into half-size chunks (0: off, measured slower),
+#define LV_TAIL_ROUNDS_DEN 1   // in rounds of the persistent grid (NUM / DEN)
+#endif
 constexpr uint64_t LV_SPIN_CYCLES = 1ull << 31;   // give up a wait after ~1 s (errflag -> exact v1 rerun)
 constexpr uint64_t LV_TAG = 1ull << 63;
+constexpr uint32_t LV_QUEUES = 8;        // chunk dequeue heads per level (power of two)
 constexpr int LV_STATE_WORDS = 16;       // u64 per chunk state
 
 // Per-port descriptor, built on device by k_plan_ports from the slot layout.
@@ -130,6 +135,30 @@ __device__ __forceinline__ uint64_t lv_ld(const uint64_t* p)
 __device__ __forceinline__ void lv_st(uint64_t* p, uint64_t v)
 {
    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Hop-record stores are plain stores: a wave's 16-B records for one next port
+// land on nearby lines and combine in L2 before they reach HBM (write-through
+// sc1 stores measured 37% slower on 32x32).
+__device__ __forceinline__ void lv_store_rec(Rec* p, uint64_t t, uint32_t id, uint32_t aux)
+{
+   Rec o;
+   o.t = t;
+   o.id = id;
+   o.aux = aux;
+   *p = o;
+}
+
+// A record at slot position gp, plus its key sample when gp is a multiple of 64.
+__device__ __forceinline__ void lv_put(Rec* __restrict__ recs, uint64_t* __restrict__ samp_t,
+                                       uint32_t* __restrict__ samp_id, uint64_t gp, uint64_t tn, uint32_t id, uint32_t ax)
+{
+   lv_store_rec(recs + gp, tn, id, ax);
+   if ((gp & 63) == 0)
+   {
+      samp_t[gp >> 6] = tn;
+      samp_id[gp >> 6] = id;
+   }
 }
 
 __device__ __forceinline__ bool rlt(const Rec& a, uint64_t t, uint32_t id)
@@ -638,19 +667,13 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
             const uint32_t x = atomicAdd(&nexc[sm.io.oslot[nd]], 1u);
             atomicOr(errflag + 2, 1u);   // "some slot has exceptions": later levels read nexc
             if (x >= sm.io.ocnt[nd]) { atomicOr(errflag, 1u); continue; }
-            recs[sm.io.obase[nd] + sm.io.ocnt[nd] - 1 - x] = o;
+            lv_store_rec(recs + sm.io.obase[nd] + sm.io.ocnt[nd] - 1 - x, o.t, o.id, o.aux);
          }
          else
          {
             const uint32_t pos = sm.cy.cnt[nd]++;
             if (pos >= sm.io.ocnt[nd]) { atomicOr(errflag, 1u); continue; }
-            const uint64_t gp = sm.io.obase[nd] + pos;
-            recs[gp] = o;
-            if ((gp & 63) == 0)
-            {
-               samp_t[gp >> 6] = tn;
-               samp_id[gp >> 6] = id;
-            }
+            lv_put(recs, samp_t, samp_id, sm.io.obase[nd] + pos, tn, id, ax);
          }
       }
       sm.s0 = e;
@@ -708,16 +731,7 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
             continue;
          }
          const uint64_t gp = sm.io.obase[nd] + pos;
-         Rec o;
-         o.t = tn;
-         o.id = id;
-         o.aux = ax;
-         recs[gp] = o;
-         if ((gp & 63) == 0)
-         {
-            samp_t[gp >> 6] = tn;
-            samp_id[gp >> 6] = o.id;
-         }
+         lv_put(recs, samp_t, samp_id, gp, tn, id, ax);
       }
    }
    for (int off = 32; off > 0; off >>= 1) ssum += __shfl_down(ssum, off);
@@ -1018,11 +1032,16 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, bool anyexc, uint32_t cb0, uin
    auto& d = sm.nx;
    if (wv == 1)
    {
+      // 8 dequeue heads (one word saturates near 90 dequeues/us): group q = blockIdx % 8
+      // takes chunks q, q+8, q+16, ... in order, so every predecessor of a chunk
+      // is held by a running workgroup or done
+      const uint32_t q = blockIdx.x & (LV_QUEUES - 1);
       uint32_t cid = 0;
-      if (lane == 0) cid = atomicAdd(ctr, 1u);   // in order: every predecessor chunk is running or held
+      if (lane == 0) cid = atomicAdd(ctr + q, 1u);
       cid = __shfl(cid, 0);
-      const uint32_t valid = cid < nch ? 1u : 0u;
-      const uint32_t g = cb0 + cid;
+      const uint32_t idx = q + LV_QUEUES * cid;
+      const uint32_t valid = idx < nch ? 1u : 0u;
+      const uint32_t g = cb0 + idx;
       if (valid)
       {
          const uint32_t pk = chunk_port[g];
@@ -1075,7 +1094,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
    // per-level launch: chunks of `level`; cross-level launch (XL, level = number of levels): all chunks
    const uint32_t cb0 = XL ? 0u : lvl_cbase[level];
    const uint32_t nch = XL ? lvl_cbase[level] : lvl_cbase[level + 1] - cb0;
-   unsigned* const cctr = XL ? ctr : ctr + level;
+   unsigned* const cctr = XL ? ctr : ctr + level * LV_QUEUES;
    // exception tails exist only if an earlier level's M/G/1 path wrote one (flag set
    // before this launch); the cross-level launch always reads the counts
    const bool anyexc = XL || errflag[2] != 0;
@@ -1315,9 +1334,9 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
          if (STAMPS && stamps)
          {
             stamps[(uint64_t) g * 16 + 8] = __builtin_amdgcn_s_memtime();
-            stamps[(uint64_t) g * 16 + 9] = (uint64_t) j | ((uint64_t) sm.io.dir << 32);
+            stamps[(uint64_t) g * 16 + 9] = (uint64_t) j | ((uint64_t) sm.io.dir << 32) | ((uint64_t) level << 40);
+            stamps[(uint64_t) g * 16 + 11] = __builtin_amdgcn_s_memrealtime();
             stamps[(uint64_t) g * 16 + 10] = sm.st_cnt;
-            stamps[(uint64_t) g * 16 + 11] = sm.tm[0];
             stamps[(uint64_t) g * 16 + 12] = sm.tm[1];
             stamps[(uint64_t) g * 16 + 13] = sm.tm[2];
             stamps[(uint64_t) g * 16 + 14] = sm.tm[3];
@@ -1348,17 +1367,6 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
 // device-side plan
 // ---------------------------------------------------------------------------
 // One thread per port (level order): input slots, output slots, chunk count.
-__device__ __forceinline__ uint32_t plan_nc(const uint32_t* __restrict__ slot_cnt, uint32_t port, uint32_t ctgt)
-{
-   uint32_t tot = 0, nin = 0;
-   for (uint32_t in = 0; in < INS; in++)
-   {
-      const uint32_t n = slot_cnt[port * INS + in];
-      if (n && nin < (uint32_t) LV_IN) { tot += n; nin++; }
-   }
-   return tot ? (tot + ctgt - 1) / ctgt : 0;
-}
-
 __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const uint32_t* __restrict__ lvl_ports,
                                                     const uint32_t* __restrict__ port_k,
                                                     const uint32_t* __restrict__ slot_cnt,
@@ -1396,7 +1404,7 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
          else if (in == IN_S) pp = (tile - c.W) * PORTS + P_UP;
          else if (in == IN_N) pp = (tile + c.W) * PORTS + P_DOWN;
          io.prod[io.nin] = pp == LV_NO_PROD ? LV_NO_PROD : port_k[pp];
-         io.prod_nc[io.nin] = pp == LV_NO_PROD ? 0u : plan_nc(slot_cnt, pp, ctgt);
+         io.prod_nc[io.nin] = 0;   // k_plan_expand: the producer's chunk count
          if (n > best) { best = n; io.sb = io.nin; }
          io.nin++;
          tot += n;
@@ -1416,38 +1424,70 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
       io.obase[d] = dir == P_SELF ? 0 : slot_base[os];
       io.ocnt[d] = dir == P_SELF ? 0 : slot_cnt[os];
    }
-   const uint32_t nc = tot ? (tot + ctgt - 1) / ctgt : 0;
    io.gbase = 0;
-   io.nc = nc;
+   io.nc = 0;     // k_plan_scan decides, k_plan_expand writes
    pio[k] = io;
-   pnc[k] = nc;
+   pnc[k] = tot;  // records of the port (k_plan_scan turns it into a chunk count)
 }
 
-// Single block: global exclusive scan of chunk counts (ports are in level order),
-// per-level chunk bases.
-__global__ __launch_bounds__(1024) void k_plan_scan(uint32_t P, uint32_t L, const uint32_t* __restrict__ lvl_off,
-                                                    const uint32_t* __restrict__ pnc, uint32_t* __restrict__ pgb,
-                                                    uint32_t* __restrict__ lvl_cbase)
+// One block per level.  Records -> chunk counts with guided sizes: ports whose
+// records fall in the level's last `tail_rec` records (about one round of the
+// persistent grid) use half-size chunks, so the level ends with a short round.
+__global__ __launch_bounds__(1024) void k_plan_guided(const uint32_t* __restrict__ lvl_off, uint32_t* __restrict__ pnc,
+                                                      uint32_t ctgt, uint64_t tail_rec)
 {
-   __shared__ uint32_t part[1024];
-   const uint32_t per = (P + 1023) / 1024;
-   const uint32_t lo = threadIdx.x * per, hi = min(lo + per, P);
-   uint32_t s = 0;
+   __shared__ uint64_t part[1024];
+   const uint32_t l = blockIdx.x;
+   const uint32_t a = lvl_off[l], b = lvl_off[l + 1], np = b - a;
+   const uint32_t per = (np + 1023) / 1024;
+   const uint32_t lo = a + min(threadIdx.x * per, np), hi = a + min((threadIdx.x + 1) * per, np);
+   uint64_t s = 0;
    for (uint32_t i = lo; i < hi; i++) s += pnc[i];
    part[threadIdx.x] = s;
    __syncthreads();
    for (uint32_t off = 1; off < 1024; off <<= 1)
    {
-      const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      const uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
       __syncthreads();
       part[threadIdx.x] += v;
       __syncthreads();
    }
-   uint32_t run = part[threadIdx.x] - s;
+   const uint64_t total = part[1023];
+   const uint64_t tail_start = total > tail_rec ? total - tail_rec : 0;
+   uint64_t run = part[threadIdx.x] - s;
+   for (uint32_t i = lo; i < hi; i++)
+   {
+      const uint32_t tot = pnc[i];
+      const uint32_t tg = run + tot > tail_start ? (ctgt + 1) / 2 : ctgt;
+      pnc[i] = tot ? (tot + tg - 1) / tg : 0;
+      run += tot;
+   }
+}
+
+// Single block: global exclusive scan of chunk counts (ports are in level
+// order), per-level chunk bases.
+__global__ __launch_bounds__(1024) void k_plan_scan(uint32_t P, uint32_t L, const uint32_t* __restrict__ lvl_off,
+                                                    const uint32_t* __restrict__ pnc, uint32_t* __restrict__ pgb,
+                                                    uint32_t* __restrict__ lvl_cbase)
+{
+   __shared__ uint64_t part[1024];
+   const uint32_t per = (P + 1023) / 1024;
+   const uint32_t lo = threadIdx.x * per, hi = min(lo + per, P);
+   uint64_t s = 0;
+   for (uint32_t i = lo; i < hi; i++) s += pnc[i];
+   part[threadIdx.x] = s;
+   __syncthreads();
+   for (uint32_t off = 1; off < 1024; off <<= 1)
+   {
+      const uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+   }
+   uint32_t run = (uint32_t) (part[threadIdx.x] - s);
    for (uint32_t i = lo; i < hi; i++) { pgb[i] = run; run += pnc[i]; }
    __syncthreads();
-   for (uint32_t l = threadIdx.x; l <= L; l += 1024) lvl_cbase[l] = l < L ? pgb[lvl_off[l]] : part[1023];
-   // pgb of an empty trailing level equals the total: lvl_off[L] == P handled by the total above
+   for (uint32_t l = threadIdx.x; l <= L; l += 1024) lvl_cbase[l] = l < L ? pgb[lvl_off[l]] : (uint32_t) part[1023];
 }
 
 __global__ __launch_bounds__(256) void k_plan_expand(uint32_t P, PortIO3* __restrict__ pio, const uint32_t* __restrict__ pnc,
@@ -1457,6 +1497,9 @@ __global__ __launch_bounds__(256) void k_plan_expand(uint32_t P, PortIO3* __rest
    if (k >= P) return;
    const uint32_t gb = pgb[k], nc = pnc[k];
    pio[k].gbase = gb;
+   pio[k].nc = nc;
+   for (uint32_t s = 0; s < (uint32_t) LV_IN; s++)
+      if (pio[k].prod[s] != LV_NO_PROD) pio[k].prod_nc[s] = pnc[pio[k].prod[s]];
    for (uint32_t j = 0; j < nc; j++) chunk_port[gb + j] = k;
 }
 

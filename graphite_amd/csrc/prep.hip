@@ -92,6 +92,7 @@ __global__ __launch_bounds__(256) void k_src_tot(uint32_t N, uint32_t nch, const
    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
    if (s >= N) return;
    uint32_t t = 0;
+#pragma unroll 16
    for (uint32_t ch = 0; ch < nch; ch++) t += hist[(uint64_t) ch * N + s];
    tot[s] = t;
 }
@@ -133,6 +134,7 @@ __global__ __launch_bounds__(256) void k_src_offs(uint32_t N, uint32_t nch, uint
    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
    if (s >= N) return;
    uint32_t run = (uint32_t) slot_base[slot_of(s, P_INJ, IN_LOCAL)];   // < 2^32 records (checked at submit)
+#pragma unroll 16
    for (uint32_t ch = 0; ch < nch; ch++)
    {
       const uint64_t k = (uint64_t) ch * N + s;
@@ -196,6 +198,85 @@ __global__ __launch_bounds__(64) void k_scatter(uint64_t n, uint32_t pch, uint32
          }
       }
       __syncthreads();
+   }
+}
+
+// Same contract with 4 waves per chunk (N <= SC4_MAXN): each wave owns a
+// contiguous quarter; per-wave source counts in LDS give each wave its
+// starting rank, then every wave ranks its quarter in order, with the next
+// 64 packets' loads in flight while the current ones are placed.
+constexpr uint32_t SC4_MAXN = 4096;
+
+__global__ __launch_bounds__(256) void k_scatter4(uint64_t n, uint32_t pch, uint32_t N, int nbits,
+                                                  const uint32_t* __restrict__ src, const uint8_t* __restrict__ routed,
+                                                  const uint64_t* __restrict__ inj, const uint32_t* __restrict__ aux,
+                                                  const uint32_t* __restrict__ offs, Rec* __restrict__ recs,
+                                                  uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id)
+{
+   extern __shared__ uint32_t h4[];   // [4][N] per-wave counts -> running ranks
+   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+   for (uint32_t k = threadIdx.x; k < 4 * N; k += 256) h4[k] = 0;
+   __syncthreads();
+   const uint64_t c0 = (uint64_t) blockIdx.x * pch;
+   const uint64_t c1 = min(c0 + pch, n);
+   const uint64_t q = (c1 - c0 + 3) / 4;
+   const uint64_t lo = min(c0 + w * q, c1), hi = min(lo + q, c1);
+   uint32_t* hw = h4 + w * N;
+   for (uint64_t i = lo + lane; i < hi; i += 64)
+      if (routed[i]) atomicAdd(&hw[src[i]], 1u);
+   __syncthreads();
+   // exclusive prefix over waves, plus the chunk's offset for the source
+   const uint32_t* orow = offs + (uint64_t) blockIdx.x * N;
+   for (uint32_t s2 = threadIdx.x; s2 < N; s2 += 256)
+   {
+      uint32_t run = orow[s2];
+      for (uint32_t ww = 0; ww < 4; ww++)
+      {
+         const uint32_t v = h4[ww * N + s2];
+         h4[ww * N + s2] = run;
+         run += v;
+      }
+   }
+   __syncthreads();
+   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+   // software pipeline: loads of the next 64 packets issued before placing these
+   uint64_t i = lo + lane;
+   bool nv = false;
+   uint32_t ns = 0, na = 0;
+   uint64_t nt = 0;
+   if (i < hi) { nv = routed[i] != 0; ns = src[i]; nt = inj[i]; na = aux[i]; }   // independent loads
+   for (uint64_t k = lo; k < hi; k += 64)
+   {
+      const bool valid = nv;
+      const uint32_t sidx = ns;
+      const uint64_t t = nt;
+      const uint32_t a = na;
+      const uint64_t id = k + lane;
+      const uint64_t i2 = k + 64 + lane;
+      nv = false;
+      if (i2 < hi) { nv = routed[i2] != 0; ns = src[i2]; nt = inj[i2]; na = aux[i2]; }
+      if (!nv) ns = 0;
+      const uint64_t m = match_mask(sidx, valid, nbits);
+      const uint32_t old = valid ? hw[sidx] : 0u;
+      __builtin_amdgcn_wave_barrier();
+      if (valid)
+      {
+         const uint32_t rank = old + (uint32_t) __popcll(m & lt);
+         if ((63 - __clzll(m)) == (int) lane) hw[sidx] = old + (uint32_t) __popcll(m);
+         const uint64_t pos = rank;
+         Rec r;
+         r.t = t;
+         r.id = (uint32_t) id;
+         r.aux = a;
+         recs[pos] = r;
+         if ((pos & 63) == 0)
+         {
+            samp_t[pos >> 6] = r.t;
+            samp_id[pos >> 6] = r.id;
+         }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
    }
 }
 
@@ -323,6 +404,90 @@ __global__ __launch_bounds__(256) void k_slot_counts(DevCfg c, const uint32_t* _
    slot_cnt[slot_of(tile, dir, IN_E)] = ce;
    slot_cnt[slot_of(tile, dir, IN_S)] = cs;
    slot_cnt[slot_of(tile, dir, IN_N)] = cn;
+}
+
+// The same counts, split by leg with the histograms cached in LDS: one block
+// per row for the X-leg inputs (LOCAL, W, E), one per column for the Y-leg
+// inputs (S, N).  Used when W*W*3 and H*H words fit (W, H <= 64).
+__global__ __launch_bounds__(256) void k_slot_counts_x(DevCfg c, const uint32_t* __restrict__ Hs,
+                                                       uint32_t* __restrict__ slot_cnt)
+{
+   extern __shared__ uint32_t hr[];   // Hs rows of this mesh row: [sx][dx][cl]
+   const uint32_t W = c.W, y = blockIdx.x;
+   const uint32_t nw = W * W * 3;
+   for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x) hr[k] = Hs[(uint64_t) y * W * W * 3 + k];
+   __syncthreads();
+   auto hs = [&](uint32_t sx, uint32_t dx, uint32_t cl) -> uint32_t { return hr[(sx * W + dx) * 3 + cl]; };
+   for (uint32_t q = threadIdx.x; q < W * 5; q += blockDim.x)
+   {
+      const uint32_t x = q / 5, dir = q % 5, tile = y * W + x;
+      uint32_t cl = 0, cw = 0, ce = 0;
+      if (dir == P_RIGHT) { for (uint32_t dx = x + 1; dx < W; dx++) cl += hs(x, dx, 0) + hs(x, dx, 1) + hs(x, dx, 2); }
+      else if (dir == P_LEFT) { for (uint32_t dx = 0; dx < x; dx++) cl += hs(x, dx, 0) + hs(x, dx, 1) + hs(x, dx, 2); }
+      else if (dir == P_UP) cl = hs(x, x, 2);
+      else if (dir == P_DOWN) cl = hs(x, x, 0);
+      if (dir == P_RIGHT)
+      {
+         for (uint32_t sx = 0; sx < x; sx++)
+            for (uint32_t dx = x + 1; dx < W; dx++) cw += hs(sx, dx, 0) + hs(sx, dx, 1) + hs(sx, dx, 2);
+      }
+      else if (dir != P_LEFT)
+      {
+         const uint32_t want = dir == P_UP ? 2u : dir == P_DOWN ? 0u : 1u;
+         for (uint32_t sx = 0; sx < x; sx++) cw += hs(sx, x, want);
+      }
+      if (dir == P_LEFT)
+      {
+         for (uint32_t sx = x + 1; sx < W; sx++)
+            for (uint32_t dx = 0; dx < x; dx++) ce += hs(sx, dx, 0) + hs(sx, dx, 1) + hs(sx, dx, 2);
+      }
+      else if (dir != P_RIGHT)
+      {
+         const uint32_t want = dir == P_UP ? 2u : dir == P_DOWN ? 0u : 1u;
+         for (uint32_t sx = x + 1; sx < W; sx++) ce += hs(sx, x, want);
+      }
+      slot_cnt[slot_of(tile, dir, IN_LOCAL)] = cl;
+      slot_cnt[slot_of(tile, dir, IN_W)] = cw;
+      slot_cnt[slot_of(tile, dir, IN_E)] = ce;
+   }
+}
+
+__global__ __launch_bounds__(256) void k_slot_counts_y(DevCfg c, const uint32_t* __restrict__ Prow,
+                                                       uint32_t* __restrict__ slot_cnt)
+{
+   extern __shared__ uint32_t pc[];   // column x of Prow: [sy][dy]
+   const uint32_t W = c.W, H = c.H, N = c.N, x = blockIdx.x;
+   for (uint32_t k = threadIdx.x; k < H * H; k += blockDim.x)
+   {
+      const uint32_t sy = k / H, dy = k % H;
+      pc[k] = Prow[(uint64_t) sy * N + dy * W + x];
+   }
+   __syncthreads();
+   for (uint32_t q = threadIdx.x; q < H * 5; q += blockDim.x)
+   {
+      const uint32_t y = q / 5, dir = q % 5, tile = y * W + x;
+      uint32_t cs = 0, cn = 0;
+      if (dir == P_UP)
+      {
+         for (uint32_t sy = 0; sy < y; sy++)
+            for (uint32_t dy = y + 1; dy < H; dy++) cs += pc[sy * H + dy];
+      }
+      else if (dir == P_SELF)
+      {
+         for (uint32_t sy = 0; sy < y; sy++) cs += pc[sy * H + y];
+      }
+      if (dir == P_DOWN)
+      {
+         for (uint32_t sy = y + 1; sy < H; sy++)
+            for (uint32_t dy = 0; dy < y; dy++) cn += pc[sy * H + dy];
+      }
+      else if (dir == P_SELF)
+      {
+         for (uint32_t sy = y + 1; sy < H; sy++) cn += pc[sy * H + y];
+      }
+      slot_cnt[slot_of(tile, dir, IN_S)] = cs;
+      slot_cnt[slot_of(tile, dir, IN_N)] = cn;
+   }
 }
 
 // ---------------------------------------------------------------------------

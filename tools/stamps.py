@@ -25,7 +25,8 @@ lib.gnoc_debug_stamps(eng._h, buf.ctypes.data, buf.size, ctypes.byref(n))
 st = buf.reshape(-1, 16).astype(np.int64)
 st = st[st[:, 8] > 0]
 j = st[:, 9] & 0xFFFFFFFF
-d = st[:, 9] >> 32
+d = (st[:, 9] >> 32) & 0xFF
+lev = st[:, 9] >> 40
 names = ["", "desc", "keys", "search", "load+merge", "scan", "pub+lookback", "process", "tail"]
 print("chunks", st.shape[0], "summary", eng.summary(), "records/chunk median", int(np.median(st[:, 10])))
 for dirn, label in ((5, "INJ"), (2, "RIGHT"), (1, "LEFT"), (4, "UP"), (3, "DOWN"), (0, "SELF")):
@@ -40,8 +41,7 @@ for dirn, label in ((5, "INJ"), (2, "RIGHT"), (1, "LEFT"), (4, "UP"), (3, "DOWN"
     dist = s[:, 14] >> 32
     out.append(f"[lookback={int(np.median(lb))} p90={int(np.percentile(lb, 90))} spins med={int(np.median(spins))} "
                f"p90={int(np.percentile(spins, 90))} incl-dist med={int(np.median(dist))} p90={int(np.percentile(dist, 90))}]")
-    out.append(f"[load={int(np.median(s[:, 11] - s[:, 3]))} exc={int(np.median(s[:, 12] - s[:, 11]))} "
-               f"merge={int(np.median(s[:, 4] - s[:, 12]))}]")
+    out.append(f"[merge={int(np.median(s[:, 4] - s[:, 12]))}]")
     print(f"{label:6s} n={m.sum():6d} total={int(tot)} " + " ".join(out))
 
 # predecessor timing (s_memrealtime, 100 MHz -> ns x10): take and aggregate publish of chunk g-1 vs g
@@ -55,3 +55,23 @@ print("pred take - own take (ns): med", int(np.median(dt_take)), "p10", int(np.p
 print("pred pub  - own pub  (ns): med", int(np.median(dt_pub)), "p10", int(np.percentile(dt_pub, 10)), "p90", int(np.percentile(dt_pub, 90)), "frac pred later", round(float((dt_pub > 0).mean()), 3))
 own = (st[gi, 15] - st[gi, 1]) * 10
 print("own take->pub (ns): med", int(np.median(own)), "p90", int(np.percentile(own, 90)))
+
+# per-level timeline (s_memrealtime: 100 MHz)
+rows = []
+for L in np.unique(lev):
+    m = lev == L
+    t0, t1 = st[m, 1].min(), st[m, 11].max()
+    span = (t1 - t0) * 10
+    busy = ((st[m, 11] - st[m, 1]) * 10).sum()
+    rows.append((int(L), int(m.sum()), span / 1000, busy / 1000 / max(span, 1) * 1000))
+rows = np.array(rows)
+print("levels", len(rows), "sum of spans (us)", round(rows[:, 2].sum(), 1), "mean busy WGs", round(rows[:, 3].mean(), 1))
+gaps = []
+order = np.argsort([r[0] for r in rows])
+ends = {int(L): st[lev == L, 11].max() for L in np.unique(lev)}
+starts = {int(L): st[lev == L, 1].min() for L in np.unique(lev)}
+ks = sorted(ends)
+gap = [(starts[b] - ends[a]) * 10 / 1000 for a, b in zip(ks[:-1], ks[1:])]
+print("inter-level gap (us): med", round(float(np.median(gap)), 2), "sum", round(float(np.sum(gap)), 1))
+for r in rows[::8]:
+    print("  level %2d chunks %5d span %7.1f us  mean busy WGs %6.1f" % tuple(r))
