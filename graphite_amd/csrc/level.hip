@@ -64,6 +64,7 @@ struct __attribute__((aligned(16))) PortIO3
    uint32_t nx, ny, gbase, nc;
    uint32_t prod[LV_IN];     // plan index of each input's producer port (LV_NO_PROD: the trace)
    uint32_t prod_nc[LV_IN];  // that producer's chunk count: complete when done[prod] == prod_nc
+   uint32_t pk, pad0, pad1, pad2;  // plan index of the port itself
 };
 static_assert(sizeof(PortIO3) % 16 == 0, "PortIO3 copy granularity");
 constexpr uint32_t LV_NO_PROD = 0xFFFFFFFFu;
@@ -1022,8 +1023,8 @@ __device__ __noinline__ bool lv_fetch_keys(LvSmem& sm, bool block, bool anyexc, 
 // lv_fetch: dynamic chunk id and its port descriptor (wave 1), then the keys
 // if they can be had without blocking.  Waves 1..3 call it.
 template <bool XL>
-__device__ __noinline__ void lv_fetch(LvSmem& sm, bool anyexc, uint32_t cb0, uint32_t nch, unsigned* __restrict__ ctr,
-                                      const uint32_t* __restrict__ chunk_port, const PortIO3* __restrict__ pio,
+__device__ __noinline__ void lv_fetch(LvSmem& sm, bool first, bool anyexc, uint32_t cb0, uint32_t nch, unsigned* __restrict__ ctr,
+                                      const PortIO3* __restrict__ cdesc,
                                       const Rec* __restrict__ recs, const uint64_t* __restrict__ samp_t,
                                       const uint32_t* __restrict__ samp_id, const uint32_t* __restrict__ nexc,
                                       const uint32_t* __restrict__ done, unsigned* __restrict__ errflag)
@@ -1034,21 +1035,30 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, bool anyexc, uint32_t cb0, uin
    {
       // 8 dequeue heads (one word saturates near 90 dequeues/us): group q = blockIdx % 8
       // takes chunks q, q+8, q+16, ... in order, so every predecessor of a chunk
-      // is held by a running workgroup or done
+      // is held by a running workgroup or done.  The first chunk of each
+      // workgroup is static (blockIdx / 8), so a level starts without the atomic.
       const uint32_t q = blockIdx.x & (LV_QUEUES - 1);
-      uint32_t cid = 0;
-      if (lane == 0) cid = atomicAdd(ctr + q, 1u);
-      cid = __shfl(cid, 0);
+      uint32_t cid = blockIdx.x / LV_QUEUES;
+      if (!first)
+      {
+         if (lane == 0) cid = atomicAdd(ctr + q, 1u) + (gridDim.x - q + LV_QUEUES - 1) / LV_QUEUES;
+         cid = __shfl(cid, 0);
+      }
       const uint32_t idx = q + LV_QUEUES * cid;
       const uint32_t valid = idx < nch ? 1u : 0u;
       const uint32_t g = cb0 + idx;
       if (valid)
       {
-         const uint32_t pk = chunk_port[g];
-         const uint32_t* srcw = reinterpret_cast<const uint32_t*>(pio + pk);
+         // the chunk's own copy of its port descriptor (k_plan_fill): one load
+         const uint32_t* srcw = reinterpret_cast<const uint32_t*>(cdesc + g);
          uint32_t* dstw = reinterpret_cast<uint32_t*>(&d.io);
-         if (lane < (uint32_t) (sizeof(PortIO3) / 4)) dstw[lane] = srcw[lane];
-         if (lane == 4) d.pk = pk;
+         constexpr uint32_t PKW = offsetof(PortIO3, pk) / 4;
+         if (lane < (uint32_t) (sizeof(PortIO3) / 4))
+         {
+            const uint32_t v = srcw[lane];
+            dstw[lane] = v;
+            if (lane == PKW) d.pk = v;
+         }
       }
       if (lane == 3) { d.g = g; d.valid = valid; }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1079,8 +1089,8 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, bool anyexc, uint32_t cb0, uin
 
 template <bool STAMPS, bool XL>
 __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t level, const uint32_t* __restrict__ lvl_cbase,
-                                                unsigned* __restrict__ ctr, const uint32_t* __restrict__ chunk_port,
-                                                const PortIO3* __restrict__ pio, Rec* __restrict__ recs,
+                                                unsigned* __restrict__ ctr, const PortIO3* __restrict__ cdesc,
+                                                Rec* __restrict__ recs,
                                                 uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id,
                                                 uint32_t* __restrict__ nexc, uint64_t* __restrict__ st,
                                                 uint64_t* __restrict__ final_ps,
@@ -1100,7 +1110,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
    const bool anyexc = XL || errflag[2] != 0;
    if (tid == 0) sm.nx.ready = 0;
    lv_bar();
-   if (wv >= 1) lv_fetch<XL>(sm, anyexc, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
+   if (wv >= 1) lv_fetch<XL>(sm, true, anyexc, cb0, nch, cctr, cdesc, recs, samp_t, samp_id, nexc, done, errflag);
    lv_bar();
    for (;;)
    {
@@ -1193,7 +1203,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
                if (tid == 0) lv_publish_agg(st, g, so);
                if (STAMPS && stamps && tid == 0) stamps[(uint64_t) g * 16 + 15] = __builtin_amdgcn_s_memrealtime();
                if (wv == 0) lv_lookback(sm, sm.io.gbase, j, st, errflag);
-               else lv_fetch<XL>(sm, anyexc, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
+               else lv_fetch<XL>(sm, false, anyexc, cb0, nch, cctr, cdesc, recs, samp_t, samp_id, nexc, done, errflag);
                fetched = true;
                lv_bar();
             }
@@ -1326,7 +1336,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
       lv_bar();
       if (!fetched)
       {
-         if (wv >= 1) lv_fetch<XL>(sm, anyexc, cb0, nch, cctr, chunk_port, pio, recs, samp_t, samp_id, nexc, done, errflag);
+         if (wv >= 1) lv_fetch<XL>(sm, false, anyexc, cb0, nch, cctr, cdesc, recs, samp_t, samp_id, nexc, done, errflag);
       }
       if (tid == 0)
       {
@@ -1426,6 +1436,8 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
    }
    io.gbase = 0;
    io.nc = 0;     // k_plan_scan decides, k_plan_expand writes
+   io.pk = k;
+   io.pad0 = io.pad1 = io.pad2 = 0;
    pio[k] = io;
    pnc[k] = tot;  // records of the port (k_plan_scan turns it into a chunk count)
 }
@@ -1491,16 +1503,27 @@ __global__ __launch_bounds__(1024) void k_plan_scan(uint32_t P, uint32_t L, cons
 }
 
 __global__ __launch_bounds__(256) void k_plan_expand(uint32_t P, PortIO3* __restrict__ pio, const uint32_t* __restrict__ pnc,
-                                                     const uint32_t* __restrict__ pgb, uint32_t* __restrict__ chunk_port)
+                                                     const uint32_t* __restrict__ pgb)
 {
    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
    if (k >= P) return;
-   const uint32_t gb = pgb[k], nc = pnc[k];
-   pio[k].gbase = gb;
-   pio[k].nc = nc;
+   pio[k].gbase = pgb[k];
+   pio[k].nc = pnc[k];
    for (uint32_t s = 0; s < (uint32_t) LV_IN; s++)
       if (pio[k].prod[s] != LV_NO_PROD) pio[k].prod_nc[s] = pnc[pio[k].prod[s]];
-   for (uint32_t j = 0; j < nc; j++) chunk_port[gb + j] = k;
+}
+
+// One wave per port: every chunk gets its own copy of the port descriptor, so
+// a dequeue is one dependent load (chunk id -> descriptor) instead of two.
+__global__ __launch_bounds__(64) void k_plan_fill(const PortIO3* __restrict__ pio, PortIO3* __restrict__ cdesc)
+{
+   const uint32_t k = blockIdx.x, lane = threadIdx.x;
+   constexpr uint32_t WORDS = sizeof(PortIO3) / 4;
+   const uint32_t* src = reinterpret_cast<const uint32_t*>(pio + k);
+   const uint32_t v = lane < WORDS ? src[lane] : 0u;
+   const uint32_t gb = pio[k].gbase, nc = pio[k].nc;
+   for (uint32_t j = 0; j < nc; j++)
+      if (lane < WORDS) reinterpret_cast<uint32_t*>(cdesc + gb + j)[lane] = v;
 }
 
 }  // namespace gnoc
