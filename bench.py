@@ -149,7 +149,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": pmc_traffic(f"emesh_hop_by_hop {W}x{H} {a.mix} load={a.load} pkts/tile={a.ppt}", dom),
+                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/" + PMC_FILE + ")",
+                "algorithmic_bytes_per_launch": alg_bytes / max(port_launches, 1),
                 "kernel": dom,
                 "kernel_launches": port_launches,
                 "kernel_avg_us": port_ms * 1e3 / max(port_launches, 1),
@@ -165,6 +167,24 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+PMC_FILE = "r1_pmc.json"
+
+
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of the dominant kernel, from the committed PMC passes
+    (tools/gpu_round.sh -> tools/prof_summary.py) of this same workload; None if
+    no profile of this workload and kernel is committed."""
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", PMC_FILE)
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload or d.get("kernel") != kernel:
+        return None
+    return d.get("traffic_bytes_per_launch")
 
 
 def cpu_baseline(a, W, H, hot):

@@ -1,0 +1,87 @@
+"""Summarise a tools/gpu_round.sh profile directory: per-kernel time, the
+per-level k_level durations and launch gaps (kernel trace), and HBM bytes per
+k_level launch from the FETCH_SIZE / WRITE_SIZE passes.  Writes pmc.json next
+to the CSVs (bench.py reads the committed copy for roofline.traffic).
+
+FETCH_SIZE is doubled per MI355X_MICROARCH.md "HBM [CDNA4]" (gfx950 tallies
+128-B fabric reads at 64 B); WRITE_SIZE is taken as is."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+d = sys.argv[1]
+
+
+def rows(pattern):
+    out = []
+    for f in sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True)):
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("gnoc::", "").split("<")[0]
+
+
+kt = rows("run_kernel_trace.csv")
+kt.sort(key=lambda r: int(r["Start_Timestamp"]))
+per = defaultdict(list)
+for r in kt:
+    per[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+print("kernel                calls   avg_us   total_ms")
+for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+    print(f"{k:20s} {len(v):6d} {sum(v) / len(v) / 1e3:8.2f} {sum(v) / 1e6:10.3f}")
+
+# one step = the run of k_level launches between two k_classify launches; use the last step
+steps, cur = [], None
+for r in kt:
+    n = short(r["Kernel_Name"])
+    if n == "k_classify":
+        cur = []
+        steps.append(cur)
+    if cur is not None:
+        cur.append(r)
+if steps:
+    last = steps[-1]
+    lv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in last if short(r["Kernel_Name"]) == "k_level"]
+    if lv:
+        dur = [e - s for s, e in lv]
+        gaps = [lv[i + 1][0] - lv[i][1] for i in range(len(lv) - 1)]
+        gaps.sort()
+        print(f"\nlast step: {len(lv)} k_level launches, busy {sum(dur) / 1e6:.3f} ms, span {(lv[-1][1] - lv[0][0]) / 1e6:.3f} ms, "
+              f"launch gaps total {sum(gaps) / 1e6:.3f} ms (median {gaps[len(gaps) // 2] / 1e3:.2f} us)")
+        print("level durations (us):", " ".join(f"{x / 1e3:.0f}" for x in dur))
+        s0, e1 = int(last[0]["Start_Timestamp"]), int(last[-1]["End_Timestamp"])
+        print(f"step span (first to last kernel) {(e1 - s0) / 1e6:.3f} ms")
+
+
+def pmc(pattern, counter):
+    vals = defaultdict(list)
+    for r in rows(pattern):
+        if r.get("Counter_Name") == counter and short(r["Kernel_Name"]) == "k_level":
+            vals[r["Dispatch_Id"]].append(float(r["Counter_Value"]))
+    return [sum(v) for v in vals.values()]
+
+
+fe = pmc("fetch_counter_collection.csv", "FETCH_SIZE")
+wr = pmc("write_counter_collection.csv", "WRITE_SIZE")
+if fe and wr:
+    # counters are in KB (rocprofv3 derived FETCH_SIZE / WRITE_SIZE)
+    fb = 2 * 1024 * sum(fe) / len(fe)
+    wb = 1024 * sum(wr) / len(wr)
+    wl = None
+    for f in glob.glob(os.path.join(d, "bench_fetch.json")):
+        for ln in open(f):
+            if ln.startswith("{"):
+                wl = json.loads(ln)["config"]["workload"]
+    out = {"kernel": "k_level", "workload": wl, "launches_fetch": len(fe), "launches_write": len(wr),
+           "fetch_bytes_per_launch_corrected": fb, "write_bytes_per_launch": wb,
+           "traffic_bytes_per_launch": fb + wb,
+           "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); KB units x1024"}
+    print("\nPMC per k_level launch: fetch %.1f MB (corrected), write %.1f MB, total %.1f MB" % (fb / 1e6, wb / 1e6, (fb + wb) / 1e6))
+    with open(os.path.join(d, "pmc.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
