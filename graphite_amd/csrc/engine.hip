@@ -24,6 +24,7 @@
 #include "kernels.hip"
 #include "level.hip"
 #include "prep.hip"
+#include "shard.hip"
 
 using namespace gnoc;
 
@@ -101,6 +102,18 @@ struct gnoc_engine
    double last_ms = 0.0;
    uint64_t* h_pinned = nullptr;
 
+   // one mesh over several GPUs (gnoc_shard): this rank's row band (X phase)
+   // and column band (Y phase), the turn-record exchange layout per peer
+   int rank = 0, nranks = 1;
+   uint32_t ry0 = 0, ry1 = 0, cx0 = 0, cx1 = 0;
+   uint32_t lvl_y0 = 0;                     // index of the first Y level
+   std::vector<uint64_t> x_cnt;             // [r * n + d]: turn records row band r -> column band d
+   std::vector<XPair> xs_pairs, xr_pairs;   // send / receive layouts (peers in rank order)
+   uint32_t xs_slots = 0, xr_slots = 0;
+   std::vector<uint64_t> xs_units, xr_units;
+   DevBuf d_xs_pairs, d_xr_pairs, xs_off, xr_off;
+   bool begun = false;
+
    // kernel profiling (gnoc_set_profiling)
    bool prof = false;
    std::vector<hipEvent_t> evpool;
@@ -174,38 +187,62 @@ static int fail(gnoc_engine* e, int code, const std::string& msg)
 // Levels of the output-port DAG under XY routing: injection ports; X levels
 // (RIGHT at x = l-1, LEFT at x = W-l, every row); Y levels (UP at y = k, DOWN at
 // y = H-1-k, every column); SELF ports.  Every port's producers sit in earlier levels.
+// A sharded engine keeps the injection and X ports of its row band and the Y and
+// SELF ports of its column band (shard.hip); the level sequence stays the same.
+static uint32_t band_lo(uint32_t b, uint32_t n, uint32_t D) { return (uint32_t) ((uint64_t) b * D / n); }
+
 static void build_static_levels(gnoc_engine* e)
 {
    const uint32_t W = e->dc.W, H = e->dc.H, N = e->dc.N;
+   const uint32_t n = (uint32_t) e->nranks, r = (uint32_t) e->rank;
+   e->ry0 = band_lo(r, n, H);
+   e->ry1 = band_lo(r + 1, n, H);
+   e->cx0 = band_lo(r, n, W);
+   e->cx1 = band_lo(r + 1, n, W);
    auto& P = e->lvl_ports;
    auto& O = e->lvl_off;
    P.clear();
    O.clear();
    O.push_back(0);
-   for (uint32_t t = 0; t < N; t++) P.push_back(t * PORTS + P_INJ);
+   for (uint32_t y = e->ry0; y < e->ry1; y++)
+      for (uint32_t x = 0; x < W; x++) P.push_back((y * W + x) * PORTS + P_INJ);
    O.push_back((uint32_t) P.size());
    for (uint32_t l = 1; l < W; l++)
    {
-      for (uint32_t y = 0; y < H; y++)
+      for (uint32_t y = e->ry0; y < e->ry1; y++)
       {
          P.push_back((y * W + (l - 1)) * PORTS + P_RIGHT);
          P.push_back((y * W + (W - l)) * PORTS + P_LEFT);
       }
       O.push_back((uint32_t) P.size());
    }
+   e->lvl_y0 = (uint32_t) O.size() - 1;
    for (uint32_t k = 0; k + 1 < H; k++)
    {
-      for (uint32_t x = 0; x < W; x++)
+      for (uint32_t x = e->cx0; x < e->cx1; x++)
       {
          P.push_back((k * W + x) * PORTS + P_UP);
          P.push_back(((H - 1 - k) * W + x) * PORTS + P_DOWN);
       }
       O.push_back((uint32_t) P.size());
    }
-   for (uint32_t t = 0; t < N; t++) P.push_back(t * PORTS + P_SELF);
+   for (uint32_t y = 0; y < H; y++)
+      for (uint32_t x = e->cx0; x < e->cx1; x++) P.push_back((y * W + x) * PORTS + P_SELF);
    O.push_back((uint32_t) P.size());
-   e->port_k.assign((size_t) N * PORTS, 0xFFFFFFFFu);   // port id -> plan index
+   e->port_k.assign((size_t) N * PORTS, 0xFFFFFFFFu);   // port id -> plan index (none: another rank's port)
    for (uint32_t k = 0; k < (uint32_t) P.size(); k++) e->port_k[P[k]] = k;
+}
+
+static hipError_t upload_levels(gnoc_engine* e)
+{
+   hipError_t he = e->d_lvl_ports.ensure(std::max<size_t>(1, e->lvl_ports.size()) * 4);
+   if (he == hipSuccess) he = e->d_lvl_off.ensure(e->lvl_off.size() * 4);
+   if (he == hipSuccess) he = e->d_port_k.ensure(e->port_k.size() * 4);
+   if (he == hipSuccess) he = hipMemcpy(e->d_port_k.p, e->port_k.data(), e->port_k.size() * 4, hipMemcpyHostToDevice);
+   if (he == hipSuccess && !e->lvl_ports.empty())
+      he = hipMemcpy(e->d_lvl_ports.p, e->lvl_ports.data(), e->lvl_ports.size() * 4, hipMemcpyHostToDevice);
+   if (he == hipSuccess) he = hipMemcpy(e->d_lvl_off.p, e->lvl_off.data(), e->lvl_off.size() * 4, hipMemcpyHostToDevice);
+   return he;
 }
 
 extern "C" {
@@ -280,13 +317,7 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    if (he == hipSuccess) he = hipEventCreate(&e->ev0);
    if (he == hipSuccess) he = hipEventCreate(&e->ev1);
    if (he == hipSuccess) he = hipHostMalloc((void**) &e->h_pinned, 64, hipHostMallocDefault);
-   if (he == hipSuccess) he = e->d_lvl_ports.ensure(e->lvl_ports.size() * 4);
-   if (he == hipSuccess) he = e->d_lvl_off.ensure(e->lvl_off.size() * 4);
-   if (he == hipSuccess) he = e->d_port_k.ensure(e->port_k.size() * 4);
-   if (he == hipSuccess) he = hipMemcpy(e->d_port_k.p, e->port_k.data(), e->port_k.size() * 4, hipMemcpyHostToDevice);
-   if (he == hipSuccess)
-      he = hipMemcpy(e->d_lvl_ports.p, e->lvl_ports.data(), e->lvl_ports.size() * 4, hipMemcpyHostToDevice);
-   if (he == hipSuccess) he = hipMemcpy(e->d_lvl_off.p, e->lvl_off.data(), e->lvl_off.size() * 4, hipMemcpyHostToDevice);
+   if (he == hipSuccess) he = upload_levels(e);
    if (he == hipSuccess)
    {
       int per_cu = 0, cus = 0;
@@ -327,8 +358,17 @@ static uint64_t record_bound(const gnoc_engine* e, uint64_t records)
 
 static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n, uint64_t* records)
 {
-   const uint32_t N = e->dc.N, W = e->dc.W;
+   const uint32_t N = e->dc.N, W = e->dc.W, H = e->dc.H;
+   const uint32_t nr = (uint32_t) e->nranks;
    uint64_t rec = 0;
+   // turn records per (row band of sy, column band of dx), shard.hip
+   e->x_cnt.assign((size_t) nr * nr, 0);
+   std::vector<uint32_t> rb(H), cb(W);
+   for (uint32_t b = 0; b < nr; b++)
+   {
+      for (uint32_t y = band_lo(b, nr, H); y < band_lo(b + 1, nr, H); y++) rb[y] = b;
+      for (uint32_t x = band_lo(b, nr, W); x < band_lo(b + 1, nr, W); x++) cb[x] = b;
+   }
    for (size_t i = 0; i < n; i++)
    {
       const uint32_t s = pk->src[i], d = pk->dst[i];
@@ -342,10 +382,56 @@ static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n,
       {
          const int64_t sx = s % W, sy = s / W, dx = d % W, dy = d / W;
          rec += 2 + (uint64_t) (std::llabs(sx - dx) + std::llabs(sy - dy));
+         if (nr > 1 && e->dc.contention) e->x_cnt[(size_t) rb[sy] * nr + cb[dx]]++;
       }
    }
    if (n && pk->inject_ps[n - 1] >= (1ull << 50)) return fail(e, GNOC_EUNSUPPORTED, "inject time beyond 2^50 ps");
    *records = rec;
+   return GNOC_OK;
+}
+
+// Send / receive layouts of the turn exchange (shard.hip), from x_cnt.
+static int build_exchange(gnoc_engine* e)
+{
+   const uint32_t nr = (uint32_t) e->nranks, me = (uint32_t) e->rank, W = e->dc.W, H = e->dc.H;
+   e->xs_pairs.clear();
+   e->xr_pairs.clear();
+   e->xs_units.assign(nr, 0);
+   e->xr_units.assign(nr, 0);
+   e->xs_slots = e->xr_slots = 0;
+   if (nr <= 1 || !e->dc.contention) return GNOC_OK;
+   uint64_t su = 0, ru = 0;
+   for (uint32_t q = 0; q < nr; q++)
+   {
+      if (q == me) continue;
+      for (int side = 0; side < 2; side++)
+      {
+         // side 0: my rows -> q's columns (send); side 1: q's rows -> my columns (receive)
+         const uint32_t rr = side ? q : me, cc = side ? me : q;
+         XPair p{};
+         p.x0 = band_lo(cc, nr, W);
+         p.nx = band_lo(cc + 1, nr, W) - p.x0;
+         p.y0 = band_lo(rr, nr, H);
+         p.ny = band_lo(rr + 1, nr, H) - p.y0;
+         p.nslots = p.nx * p.ny * XS_PER_TILE;
+         p.expect = e->x_cnt[(size_t) rr * nr + cc];
+         const uint64_t hdr = (p.nslots + 3) / 4;
+         uint64_t& u = side ? ru : su;
+         p.hdr_unit = u;
+         p.rec_unit = u + hdr;
+         u += hdr + p.expect;
+         (side ? e->xr_units : e->xs_units)[q] = hdr + p.expect;
+         p.slot0 = side ? e->xr_slots : e->xs_slots;
+         (side ? e->xr_slots : e->xs_slots) += p.nslots;
+         (side ? e->xr_pairs : e->xs_pairs).push_back(p);
+      }
+   }
+   GNOC_HIP(e, e->d_xs_pairs.ensure(e->xs_pairs.size() * sizeof(XPair)));
+   GNOC_HIP(e, e->d_xr_pairs.ensure(e->xr_pairs.size() * sizeof(XPair)));
+   GNOC_HIP(e, hipMemcpy(e->d_xs_pairs.p, e->xs_pairs.data(), e->xs_pairs.size() * sizeof(XPair), hipMemcpyHostToDevice));
+   GNOC_HIP(e, hipMemcpy(e->d_xr_pairs.p, e->xr_pairs.data(), e->xr_pairs.size() * sizeof(XPair), hipMemcpyHostToDevice));
+   GNOC_HIP(e, e->xs_off.ensure((size_t) e->xs_slots * 8));
+   GNOC_HIP(e, e->xr_off.ensure((size_t) e->xr_slots * 8));
    return GNOC_OK;
 }
 
@@ -383,8 +469,11 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    e->d_flags = e->t_flags.as<uint32_t>();
    e->n = n;
    e->rec_bound = record_bound(e, records);
+   rc = build_exchange(e);
+   if (rc) return rc;
    e->submitted = true;
    e->ran = false;
+   e->begun = false;
    return GNOC_OK;
 }
 
@@ -393,6 +482,7 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    if (!e || !pk) return GNOC_EINVAL;
    if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return fail(e, GNOC_EINVAL, "null trace array");
    if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
+   if (e->nranks > 1) return fail(e, GNOC_EUNSUPPORTED, "a sharded engine takes host traces (gnoc_submit)");
    e->d_inj = pk->inject_ps;
    e->d_src = pk->src;
    e->d_dst = pk->dst;
@@ -476,7 +566,7 @@ static int run_levels_v1(gnoc_engine* e)
 // ---------------------------------------------------------------------------
 // v3: device-planned chunked levels
 // ---------------------------------------------------------------------------
-static int run_levels_v3(gnoc_engine* e)
+static int run_plan_v3(gnoc_engine* e)
 {
    const DevCfg& c = e->dc;
    hipStream_t s = e->stream;
@@ -504,22 +594,36 @@ static int run_levels_v3(gnoc_engine* e)
                e->pgb.as<uint32_t>());
    GNOC_LAUNCH(e, KC_PLAN, k_plan_fill, dim3(P), dim3(64), 0, s, e->pio.as<PortIO3>(), e->cdesc.as<PortIO3>());
    e->h_levels = L;
+   return GNOC_OK;
+}
+
+// Levels [l0, l1) of the plan built by run_plan_v3.
+static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
+{
+   const DevCfg& c = e->dc;
+   hipStream_t s = e->stream;
+   const uint32_t P = (uint32_t) e->lvl_ports.size();
+   const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
+   const uint64_t chunk_bound = e->rec_bound / ((LV_CTGT + 1) / 2) + P + 1;
    const char* stv = std::getenv("GNOC_STAMPS");
    const bool stamps = stv && *stv == '1';
    e->h_chunk_bound = chunk_bound;
-   if (stamps)
+   if (stamps && l0 == 0)
    {
       GNOC_HIP(e, e->stamps.ensure(chunk_bound * 16 * 8));
       GNOC_HIP(e, hipMemsetAsync(e->stamps.p, 0, chunk_bound * 16 * 8, s));
    }
-   GNOC_HIP(e, e->done.ensure((size_t) P * 4));
-   GNOC_HIP(e, hipMemsetAsync(e->done.p, 0, (size_t) P * 4, s));
+   if (l0 == 0)
+   {
+      GNOC_HIP(e, e->done.ensure((size_t) std::max<uint32_t>(P, 1) * 4));
+      GNOC_HIP(e, hipMemsetAsync(e->done.p, 0, (size_t) std::max<uint32_t>(P, 1) * 4, s));
+   }
    // default: one launch per level (the launch boundary is the level barrier).
    // GNOC_XLEVEL=1: one persistent launch over every level with port-level
    // release/acquire hand-offs -- exact, but a consumer still waits for whole
    // producer ports and every chunk pays an L2 write-back: 2.8x slower on 32x32.
    const char* xlv = std::getenv("GNOC_XLEVEL");
-   const bool xl = xlv && *xlv == '1';
+   const bool xl = xlv && *xlv == '1' && e->nranks == 1;
    uint64_t* stp = stamps ? e->stamps.as<uint64_t>() : nullptr;
 #define GNOC_LEVEL_ARGS(lvl)                                                                                         \
    c, (lvl), e->lvl_cbase.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
@@ -527,14 +631,14 @@ static int run_levels_v3(gnoc_engine* e)
       e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),                          \
       e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(), e->counters.as<unsigned>() + 8,     \
       e->done.as<uint32_t>(), stp
-   if (xl)
+   if (xl && l0 == 0)
    {
       if (stamps) GNOC_LAUNCH(e, KC_LEVEL, (k_level<true, true>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(L));
       else GNOC_LAUNCH(e, KC_LEVEL, (k_level<false, true>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(L));
    }
    else
    {
-      for (uint32_t l = 0; l < L; l++)
+      for (uint32_t l = l0; l < l1 && l < L; l++)
       {
          if (stamps) GNOC_LAUNCH(e, KC_LEVEL, (k_level<true, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
          else GNOC_LAUNCH(e, KC_LEVEL, (k_level<false, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
@@ -546,9 +650,14 @@ static int run_levels_v3(gnoc_engine* e)
 
 constexpr int GNOC_V3_RETRY = 1000;
 
-static int run_once(gnoc_engine* e)
+static int run_post(gnoc_engine* e, bool closed_form);
+
+// Phase 1 of a run: per-run buffers, classification, injection-slot layout,
+// stable scatter, closed-form slot counts and bases.  Queue models disabled
+// (router_model.cc:86): the closed form finishes the run here (*done = true).
+static int run_prep(gnoc_engine* e, bool* done)
 {
-   if (!e) return GNOC_EINVAL;
+   *done = false;
    if (!e->submitted) return fail(e, GNOC_ESTATE, "gnoc_run before gnoc_submit");
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    const DevCfg& c = e->dc;
@@ -604,35 +713,16 @@ static int run_once(gnoc_engine* e)
    GNOC_LAUNCH(e, KC_CLASSIFY, k_classify, dim3(nch), dim3(256), N * 4, s, c, (uint64_t) n, pch, e->d_inj, e->d_src,
                   e->d_dst, e->d_bits, e->d_flags, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(),
                   e->final_ps.as<uint64_t>(), e->hist.as<uint32_t>(), e->counters.as<unsigned long long>());
-   const uint32_t fin_grid = (uint32_t) std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 8192));
 
    if (!c.contention)
    {
       // Queue models disabled (router_model.cc:86): latency is zero-load; no contention counters.
-      if (n)
-      {
-         if (e->f1)
-            GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<true>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
-                        e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
-                        e->cont.as<uint64_t>(), 1);
-         else
-            GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<false>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj,
-                        e->d_src, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
-                        e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), 1);
-      }
-      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 16, hipMemcpyDeviceToHost, s));
-      GNOC_HIP(e, hipEventRecord(e->ev1, s));
-      GNOC_HIP(e, hipStreamSynchronize(s));
-      e->h_counters[0] = e->h_pinned[0];
-      e->h_counters[1] = e->h_pinned[1];
+      int rc = run_post(e, true);
+      if (rc) return rc;
       e->h_records = 0;
       e->h_levels = 0;
-      float ms = 0;
-      GNOC_HIP(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
-      e->last_ms = ms;
-      GNOC_HIP(e, prof_collect(e));
       e->used_v3 = 0;
-      e->ran = true;
+      *done = true;
       return GNOC_OK;
    }
 
@@ -666,50 +756,85 @@ static int run_once(gnoc_engine* e)
                   e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>());
    GNOC_LAUNCH(e, KC_SCAN, k_scan_slots, dim3(1), dim3(1024), 0, s, N, e->slot_cnt.as<uint32_t>(),
                e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>(), e->gtot.as<uint64_t>() + 1);
+   return GNOC_OK;
+}
 
-   const bool v3 = e->f1 && c.max_list >= 3 && !e->force_v1;
-   e->used_v3 = v3;
-   {
-      int rc = v3 ? run_levels_v3(e) : run_levels_v1(e);
-      if (rc) return rc;
-   }
-
+// Last phase: per-packet zero-load / contention (packets this rank delivers:
+// destination in its column band), end event, counters and flags to the host.
+static int run_post(gnoc_engine* e, bool closed_form)
+{
+   const DevCfg& c = e->dc;
+   const size_t n = e->n;
+   hipStream_t s = e->stream;
+   const uint32_t fin_grid = (uint32_t) std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 8192));
    if (n)
    {
       if (e->f1)
          GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<true>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
                      e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
-                     e->cont.as<uint64_t>(), 0);
+                     e->cont.as<uint64_t>(), (int) closed_form, e->cx0, e->cx1);
       else
-         GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<false>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
-                     e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
-                     e->cont.as<uint64_t>(), 0);
+         GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<false>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj,
+                     e->d_src, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
+                     e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), (int) closed_form, e->cx0, e->cx1);
    }
    GNOC_HIP(e, hipEventRecord(e->ev1, s));
    GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 16, hipMemcpyDeviceToHost, s));
-   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 2, e->gtot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
-   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 4, e->counters.as<unsigned int>() + 8, 4, hipMemcpyDeviceToHost, s));
+   if (!closed_form)
+   {
+      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 2, e->gtot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
+      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 4, e->counters.as<unsigned int>() + 8, 4, hipMemcpyDeviceToHost, s));
+   }
    GNOC_HIP(e, hipStreamSynchronize(s));
    e->h_counters[0] = e->h_pinned[0];
    e->h_counters[1] = e->h_pinned[1];
-   e->h_records = e->h_counters[0] + e->h_counters[1];
-   if (e->h_pinned[2] > e->rec_bound) return fail(e, GNOC_EHIP, "internal: slot layout exceeds the record bound");
    float ms = 0;
    GNOC_HIP(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
    e->last_ms = ms;
    GNOC_HIP(e, prof_collect(e));
+   if (closed_form)
+   {
+      e->ran = true;
+      return GNOC_OK;
+   }
+   e->h_records = e->h_counters[0] + e->h_counters[1];
+   if (e->h_pinned[2] > e->rec_bound) return fail(e, GNOC_EHIP, "internal: slot layout exceeds the record bound");
    const unsigned errf = *(unsigned int*) (e->h_pinned + 4);
    // a leaf the splitter could not cut (or a look-back timeout) leaves garbage
    // downstream, so it takes precedence: rerun exactly on the v1 path
-   if (errf & 6u) return GNOC_V3_RETRY;
+   if (errf & 6u)
+   {
+      if (e->nranks > 1) return fail(e, GNOC_EUNSUPPORTED, "sharded run hit a burst the chunked path cannot split");
+      return GNOC_V3_RETRY;
+   }
    if (errf & 1u) return fail(e, GNOC_EHIP, "internal: route-count invariant violated");
    e->ran = true;
    return GNOC_OK;
 }
 
+static int run_once(gnoc_engine* e)
+{
+   if (!e) return GNOC_EINVAL;
+   bool done = false;
+   int rc = run_prep(e, &done);
+   if (rc || done) return rc;
+   const bool v3 = e->f1 && e->dc.max_list >= 3 && !e->force_v1;
+   e->used_v3 = v3;
+   if (v3)
+   {
+      rc = run_plan_v3(e);
+      if (!rc) rc = run_levels_v3(e, 0, (uint32_t) e->lvl_off.size() - 1);
+   }
+   else
+      rc = run_levels_v1(e);
+   if (rc) return rc;
+   return run_post(e, false);
+}
+
 int gnoc_run(gnoc_engine* e)
 {
    if (!e) return GNOC_EINVAL;
+   if (e->nranks > 1) return fail(e, GNOC_ESTATE, "sharded engine: use gnoc_run_begin / exchange / gnoc_run_finish");
    const char* env = std::getenv("GNOC_ENGINE");
    const int forced = env && std::strcmp(env, "v1") == 0;
    e->force_v1 = forced;
@@ -722,6 +847,101 @@ int gnoc_run(gnoc_engine* e)
       if (rc == GNOC_V3_RETRY) rc = fail(e, GNOC_EHIP, "internal: v1 path reported overflow");
    }
    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// one mesh over several GPUs (shard.hip)
+// ---------------------------------------------------------------------------
+int gnoc_shard(gnoc_engine* e, int32_t rank, int32_t nranks)
+{
+   if (!e) return GNOC_EINVAL;
+   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(e, GNOC_EINVAL, "bad rank / nranks");
+   if ((uint32_t) nranks > std::min(e->dc.W, e->dc.H)) return fail(e, GNOC_EINVAL, "more ranks than mesh rows or columns");
+   if (nranks > 1 && e->dc.contention && !(e->f1 && e->dc.max_list >= 3))
+      return fail(e, GNOC_EUNSUPPORTED, "sharding needs the chunked path (f = 1 GHz, max_list_size >= 3)");
+   e->rank = rank;
+   e->nranks = nranks;
+   build_static_levels(e);
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   GNOC_HIP(e, upload_levels(e));
+   e->submitted = false;
+   e->ran = false;
+   e->begun = false;
+   return GNOC_OK;
+}
+
+int gnoc_exchange_counts(gnoc_engine* e, uint64_t* send_units, uint64_t* recv_units, size_t nranks)
+{
+   if (!e) return GNOC_EINVAL;
+   if (!e->submitted) return fail(e, GNOC_ESTATE, "exchange layout is known after gnoc_submit");
+   if (nranks != (size_t) e->nranks) return fail(e, GNOC_EINVAL, "nranks != the engine's shard count");
+   for (size_t q = 0; q < nranks; q++)
+   {
+      if (send_units) send_units[q] = q < e->xs_units.size() ? e->xs_units[q] : 0;
+      if (recv_units) recv_units[q] = q < e->xr_units.size() ? e->xr_units[q] : 0;
+   }
+   return GNOC_OK;
+}
+
+int gnoc_run_begin(gnoc_engine* e, void* send_buf)
+{
+   if (!e) return GNOC_EINVAL;
+   e->ran = false;
+   e->begun = false;
+   bool done = false;
+   int rc = run_prep(e, &done);
+   if (rc) return rc;
+   if (done)
+   {
+      e->begun = true;
+      return GNOC_OK;
+   }
+   e->used_v3 = 1;
+   rc = run_plan_v3(e);
+   if (!rc) rc = run_levels_v3(e, 0, e->lvl_y0);
+   if (rc) return rc;
+   hipStream_t s = e->stream;
+   if (e->xs_slots)
+   {
+      if (!send_buf) return fail(e, GNOC_EINVAL, "null send buffer");
+      const uint32_t np = (uint32_t) e->xs_pairs.size();
+      hipLaunchKernelGGL(k_x_layout, dim3(np), dim3(1024), 0, s, e->dc.W, e->d_xs_pairs.as<XPair>(),
+                         e->slot_cnt.as<uint32_t>(), e->xs_off.as<uint64_t>(), e->counters.as<unsigned>() + 8);
+      GNOC_HIP(e, hipGetLastError());
+      hipLaunchKernelGGL(k_x_pack, dim3((e->xs_slots + 3) / 4), dim3(256), 0, s, e->dc.W, e->d_xs_pairs.as<XPair>(), np,
+                         e->xs_slots, e->xs_off.as<uint64_t>(), e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(),
+                         e->nexc.as<uint32_t>(), e->recs.as<Rec>(), reinterpret_cast<uint4*>(send_buf));
+      GNOC_HIP(e, hipGetLastError());
+   }
+   GNOC_HIP(e, hipStreamSynchronize(s));   // the send buffer is complete when this returns
+   e->begun = true;
+   return GNOC_OK;
+}
+
+int gnoc_run_finish(gnoc_engine* e, const void* recv_buf)
+{
+   if (!e) return GNOC_EINVAL;
+   if (!e->begun) return fail(e, GNOC_ESTATE, "gnoc_run_finish without gnoc_run_begin");
+   e->begun = false;
+   if (!e->dc.contention) return GNOC_OK;   // closed form finished in gnoc_run_begin
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   hipStream_t s = e->stream;
+   if (e->xr_slots)
+   {
+      if (!recv_buf) return fail(e, GNOC_EINVAL, "null receive buffer");
+      const uint32_t np = (uint32_t) e->xr_pairs.size();
+      hipLaunchKernelGGL(k_x_layout, dim3(np), dim3(1024), 0, s, e->dc.W, e->d_xr_pairs.as<XPair>(),
+                         e->slot_cnt.as<uint32_t>(), e->xr_off.as<uint64_t>(), e->counters.as<unsigned>() + 8);
+      GNOC_HIP(e, hipGetLastError());
+      hipLaunchKernelGGL(k_x_unpack, dim3((e->xr_slots + 3) / 4), dim3(256), 0, s, e->dc.W, e->d_xr_pairs.as<XPair>(), np,
+                         e->xr_slots, e->xr_off.as<uint64_t>(), e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(),
+                         e->nexc.as<uint32_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(),
+                         reinterpret_cast<const uint4*>(recv_buf), e->counters.as<unsigned>() + 8);
+      GNOC_HIP(e, hipGetLastError());
+   }
+   int rc = run_levels_v3(e, e->lvl_y0, (uint32_t) e->lvl_off.size() - 1);
+   if (rc) return rc;
+   return run_post(e, false);
 }
 
 int gnoc_get_packet_results(gnoc_engine* e, uint64_t* final_ps, uint64_t* zero_load_ps, uint64_t* contention_ps, size_t n)

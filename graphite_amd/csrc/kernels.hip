@@ -520,14 +520,17 @@ template <bool F1>
 __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const uint64_t* __restrict__ inj,
                                                   const uint32_t* __restrict__ src, const uint32_t* __restrict__ aux,
                                                   const uint8_t* __restrict__ routed, uint64_t* __restrict__ final_ps,
-                                                  uint64_t* __restrict__ zl, uint64_t* __restrict__ cont, int closed_form)
+                                                  uint64_t* __restrict__ zl, uint64_t* __restrict__ cont, int closed_form,
+                                                  uint32_t cx0, uint32_t cx1)
 {
    for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
    {
+      const uint32_t dx = aux_dx(aux[i]), dy = aux_dy(aux[i]);
+      // a sharded engine delivers the packets of its column band (shard.hip); others read 0
+      if (dx < cx0 || dx >= cx1) { final_ps[i] = 0; zl[i] = 0; cont[i] = 0; continue; }
       if (!routed[i]) { zl[i] = 0; cont[i] = 0; continue; }
       uint32_t sx, sy;
       tile_xy(src[i], c.W, c.magicW, sx, sy);
-      const uint32_t dx = aux_dx(aux[i]), dy = aux_dy(aux[i]);
       const uint64_t hops = (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
       // Hop::Hop accumulates Latency(0) at injection, Latency(R+Lk) per mesh router,
       // Latency(F) at receive (network_model.cc:142-150, 556-563).
@@ -544,8 +547,8 @@ template __global__ void k_port_stream<true>(DevCfg, const uint32_t*, const uint
 template __global__ void k_port_stream<false>(DevCfg, const uint32_t*, const uint32_t*, const uint64_t*, Rec*, uint64_t*,
                                               uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
 template __global__ void k_finalize<true>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,
-                                          const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int);
+                                          const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int, uint32_t, uint32_t);
 template __global__ void k_finalize<false>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,
-                                           const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int);
+                                           const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int, uint32_t, uint32_t);
 
 }  // namespace gnoc

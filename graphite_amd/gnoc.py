@@ -34,6 +34,7 @@ EXPORTED = (
     "gnoc_get_packet_results", "gnoc_get_port_stats", "gnoc_get_summary", "gnoc_device_final_ps",
     "gnoc_last_error", "gnoc_destroy", "gnoc_trace_synthetic", "gnoc_abi_version",
     "gnoc_set_profiling", "gnoc_get_kernel_stats", "gnoc_trace_file_write", "gnoc_trace_file_read",
+    "gnoc_shard", "gnoc_exchange_counts", "gnoc_run_begin", "gnoc_run_finish",
 )
 
 
@@ -115,6 +116,10 @@ def load() -> ctypes.CDLL:
     lib.gnoc_set_profiling.argtypes = [vp, ctypes.c_int]
     lib.gnoc_get_kernel_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(sz)]
+    lib.gnoc_shard.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
+    lib.gnoc_exchange_counts.argtypes = [vp, vp, vp, sz]
+    lib.gnoc_run_begin.argtypes = [vp, vp]
+    lib.gnoc_run_finish.argtypes = [vp, vp]
     _lib = lib
     return lib
 
@@ -320,3 +325,96 @@ class Engine:
         p = ctypes.c_void_p()
         self._check(self.lib.gnoc_device_final_ps(self._h, ctypes.byref(p)))
         return int(p.value)
+
+
+def band(b: int, n: int, dim: int) -> range:
+    """Rows (or columns) of band b of n: [b*dim/n, (b+1)*dim/n) -- gnoc_shard's split."""
+    return range(b * dim // n, (b + 1) * dim // n)
+
+
+def turn_counts(tr: Trace, width: int, height: int, nranks: int) -> np.ndarray:
+    """[r, d]: routed packets whose turn record moves from row band r (source row)
+    to column band d (destination column): what gnoc_exchange_counts is built from."""
+    tr = tr.normalized()
+    routed = (tr.src != tr.dst) & ((tr.flags & PKT_UNMODELED) == 0)
+    sy = (tr.src[routed] // width).astype(np.int64)
+    dx = (tr.dst[routed] % width).astype(np.int64)
+    rb = np.empty(height, np.int64)
+    cb = np.empty(width, np.int64)
+    for b in range(nranks):
+        rb[band(b, nranks, height).start:band(b, nranks, height).stop] = b
+        cb[band(b, nranks, width).start:band(b, nranks, width).stop] = b
+    m = np.zeros((nranks, nranks), np.int64)
+    np.add.at(m, (rb[sy], cb[dx]), 1)
+    return m
+
+
+def exchange_units(send, recv, send_units, recv_units, group=None) -> None:
+    """The turn-record all-to-all: send[: sum(send_units)] (16-byte units, peers in
+    rank order) -> recv[: sum(recv_units)].  "nccl" (RCCL over xGMI): device to
+    device on torch's current stream, then synchronised so the engine's stream can
+    read it; "gloo": staged through host memory (CPU tensors pass straight through)."""
+    import torch
+    import torch.distributed as dist
+    s = send[:sum(send_units)]
+    r = recv[:sum(recv_units)]
+    if dist.get_backend(group) == "nccl":
+        dist.all_to_all_single(r, s, output_split_sizes=recv_units, input_split_sizes=send_units, group=group)
+        torch.cuda.current_stream().synchronize()
+        return
+    rh = r if r.device.type == "cpu" else torch.empty(r.shape, dtype=r.dtype)
+    dist.all_to_all_single(rh, s.cpu(), output_split_sizes=recv_units, input_split_sizes=send_units, group=group)
+    if rh is not r:
+        r.copy_(rh)
+        torch.cuda.synchronize()
+
+
+class ShardedEngine(Engine):
+    """One rank's share of a mesh sharded over torch.distributed ranks (gnoc_shard):
+    row band for the X phase, column band for the Y phase, one all-to-all of the
+    turn records in between.  With the "nccl" backend (RCCL over xGMI) the
+    exchange runs device to device; with "gloo" it is staged through host memory
+    (multi-process tests on one GPU or on CPU hosts)."""
+
+    def __init__(self, cfg: EngineConfig, rank: int, nranks: int, group=None):
+        super().__init__(cfg)
+        self.rank, self.nranks, self.group = rank, nranks, group
+        self._check(self.lib.gnoc_shard(self._h, rank, nranks))
+        self._send = self._recv = None
+
+    def submit(self, tr: Trace) -> None:
+        import torch
+        super().submit(tr)
+        s = np.zeros(self.nranks, np.uint64)
+        r = np.zeros(self.nranks, np.uint64)
+        self._check(self.lib.gnoc_exchange_counts(self._h, s.ctypes.data, r.ctypes.data, self.nranks))
+        self.send_units, self.recv_units = [int(v) for v in s], [int(v) for v in r]
+        dev = torch.device("cuda", self.cfg.device)
+        # 16-byte units as int32 x 4 (one Rec per unit)
+        self._send = torch.empty((max(1, sum(self.send_units)), 4), dtype=torch.int32, device=dev)
+        self._recv = torch.empty((max(1, sum(self.recv_units)), 4), dtype=torch.int32, device=dev)
+
+    def exchange(self) -> None:
+        if self.nranks > 1:
+            exchange_units(self._send, self._recv, self.send_units, self.recv_units, self.group)
+
+    def run(self) -> None:
+        self._check(self.lib.gnoc_run_begin(self._h, self._send.data_ptr()))
+        self.exchange()
+        self._check(self.lib.gnoc_run_finish(self._h, self._recv.data_ptr()))
+
+    def gathered_results(self) -> Results:
+        """The whole mesh's results on every rank: element-wise sum over ranks
+        (each entry is non-zero on the one rank that owns it)."""
+        import torch
+        import torch.distributed as dist
+        r = self.results()
+        parts = [r.final_ps, r.zero_load_ps, r.contention_ps, r.port_sum_delay, r.port_count, r.port_mg1]
+        flat = torch.from_numpy(np.concatenate(parts).view(np.int64).copy())
+        if dist.get_backend(self.group) == "nccl":
+            flat = flat.cuda(self.cfg.device)
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        out = flat.cpu().numpy().view(np.uint64)
+        n, npt = self._n, r.port_sum_delay.shape[0]
+        o = [0, n, 2 * n, 3 * n, 3 * n + npt, 3 * n + 2 * npt, 3 * n + 3 * npt]
+        return Results(*(out[o[k]:o[k + 1]].copy() for k in range(6)), summary=r.summary)

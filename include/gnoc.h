@@ -160,6 +160,32 @@ int gnoc_set_profiling(gnoc_engine *eng, int enable);
 int gnoc_get_kernel_stats(gnoc_engine *eng, const char **names, double *total_ms,
                           uint32_t *launches, size_t cap, size_t *count);
 
+/* ---- one mesh over several GPUs ---------------------------
+ * XY routing (emesh_hop_by_hop.cc:229-240) sends a packet along its source
+ * row, then along its destination column.  Rank r of n owns the injection and
+ * LEFT/RIGHT ports of mesh rows [r*H/n, (r+1)*H/n) (its row band: the X phase)
+ * and the UP/DOWN/SELF ports of columns [r*W/n, (r+1)*W/n) (its column band:
+ * the Y phase).  Between the phases every routed packet's one "turn" record
+ * moves from the row-band owner of its source to the column-band owner of its
+ * destination: one all-to-all, done by the caller (RCCL all_to_all over xGMI,
+ * or any transport) on buffers of 16-byte units:
+ *   gnoc_shard(eng, rank, n)            before gnoc_submit (same trace on every rank)
+ *   gnoc_submit(eng, ...)               host trace; fixes the exchange sizes
+ *   gnoc_exchange_counts(eng, s, r, n)  units to send to / receive from each peer
+ *   gnoc_run_begin(eng, send_dev)       prep + X phase + pack; the send buffer is
+ *                                       complete when it returns
+ *   (caller) all_to_all(send_dev -> recv_dev, split sizes s / r)
+ *   gnoc_run_finish(eng, recv_dev)      unpack + Y phase + per-packet results
+ * Results are bit-identical to an unsharded run.  A rank reports the packets it
+ * delivers (destination column in its band) and the ports it owns; every other
+ * entry reads 0, so an element-wise sum over ranks is the whole mesh's result.
+ * gnoc_run is refused on an engine with n > 1.  Needs f = 1 GHz and
+ * max_list_size >= 3 when contention is enabled. */
+int gnoc_shard(gnoc_engine *eng, int32_t rank, int32_t nranks);
+int gnoc_exchange_counts(gnoc_engine *eng, uint64_t *send_units, uint64_t *recv_units, size_t nranks);
+int gnoc_run_begin(gnoc_engine *eng, void *send_dev);
+int gnoc_run_finish(gnoc_engine *eng, const void *recv_dev);
+
 const char *gnoc_last_error(const gnoc_engine *eng);
 void gnoc_destroy(gnoc_engine *eng);
 
