@@ -8,10 +8,14 @@ reference model (tests/test_gpu_parity.py).  Default workload = BASELINE.json
 configs[1]: 32x32 (1024 tiles), uniform_random traffic, offered load 0.005
 pkt/tile/cycle, 10,000 packets per tile (10.24 M packets, ~229 M mesh hops).
 
-Multi-GPU (torchrun, one rank per GPU): each rank simulates its own independent
-32x32 trace (seed + rank) -- the sweep-style sharding of SURVEY.md 8(e); there is
-no collective on the data path, so scaling is "weak".  Ranks synchronise only
-for the barrier and the max-over-ranks time.
+Multi-GPU (torchrun, one rank per GPU; default workload for N > 1 =
+BASELINE.json configs[2]): ONE 64x64 mesh (4096 tiles, offered load 0.002,
+10,000 packets per tile: 40.96 M packets, ~1.79 G mesh hops) sharded over the N
+ranks (gnoc_shard, shard.hip): rank r runs the injection + X-direction ports of
+its row band, one RCCL all-to-all over xGMI moves every packet's turn record to
+the owner of its destination column band, and rank r runs the Y-direction and
+SELF ports of its column band.  Total work is fixed, so scaling is "strong".
+`--workload replicas` instead runs an independent 32x32 batch per rank (weak).
 
 Prints ONE JSON line on rank 0.
 """
@@ -40,14 +44,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--mesh", type=int, default=32)
-    ap.add_argument("--load", type=float, default=0.005)
+    ap.add_argument("--mesh", type=int, default=0, help="mesh side (default: 32, or 64 when sharded)")
+    ap.add_argument("--load", type=float, default=0.0, help="offered load (default: 0.005 at 32x32, 0.002 at 64x64)")
     ap.add_argument("--ppt", type=int, default=10000, help="packets per tile")
     ap.add_argument("--mix", choices=("uniform", "hotspot"), default="uniform")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-sample-ppt", type=int, default=1000)
     ap.add_argument("--verify", type=int, default=0, help="also check the GPU result vs the oracle (slow)")
+    ap.add_argument("--workload", choices=("auto", "mesh", "sharded", "replicas"), default="auto",
+                    help="auto: one 32x32 mesh at N=1, one 64x64 mesh sharded over N ranks at N>1")
     return ap.parse_args()
 
 
@@ -63,14 +69,22 @@ def main():
         torch.cuda.set_device(0)
 
     from graphite_amd import gnoc
+    import numpy as np
 
-    W = H = a.mesh
+    wl = a.workload if a.workload != "auto" else ("mesh" if world == 1 else "sharded")
+    if wl == "mesh" and world > 1:
+        wl = "replicas"
+    sharded = wl == "sharded"
+    # BASELINE.json configs[1] (32x32, load 0.005) / configs[2] (64x64, load 0.002)
+    W = H = a.mesh or (64 if sharded else 32)
+    load = a.load or (0.002 if W == 64 else 0.005)
     hot = 0.2 if a.mix == "hotspot" else 0.0
     t0 = time.time()
-    tr = gnoc.synthetic_trace(W, H, a.load, a.ppt, seed=a.seed + rank, hotspot_fraction=hot, num_hotspots=16)
+    seed = a.seed + (rank if wl == "replicas" else 0)      # a sharded mesh: the same trace on every rank
+    tr = gnoc.synthetic_trace(W, H, load, a.ppt, seed=seed, hotspot_fraction=hot, num_hotspots=16)
     gen_s = time.time() - t0
     cfg = gnoc.EngineConfig(num_tiles=W * H, device=local)
-    eng = gnoc.Engine(cfg)
+    eng = gnoc.ShardedEngine(cfg, rank, world) if sharded else gnoc.Engine(cfg)
     eng.submit(tr)          # trace now resident in HBM; steps start from there
 
     def barrier_sync():
@@ -96,22 +110,27 @@ def main():
     kst = eng.kernel_stats()
     eng.set_profiling(False)
 
+    # this rank's share: mesh hops through the ports it owns, packets it delivers
+    res = eng.results()
+    pc = res.port_count.reshape(-1, 6)
+    my_hops, my_pkts = int(pc[:, :5].sum()), int(pc[:, 0].sum())
     hops = int(summ["mesh_hops"])
     pkts = int(summ["routed_packets"])
     t = torch.tensor([elapsed, float(hops), float(pkts)], dtype=torch.float64, device="cuda")
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:3], op=dist.ReduceOp.SUM)
+        if not sharded:   # replicas: every rank simulated its own batch
+            dist.all_reduce(t[1:3], op=dist.ReduceOp.SUM)
         t[0] = tmax[0]
     elapsed_max, hops_all, pkts_all = float(t[0]), float(t[1]), float(t[2])
 
     if a.verify:
         from oracle import oracle
-        import numpy as np
-        got = eng.results()
-        ref = oracle.run(cfg, tr)
-        assert np.array_equal(got.final_ps, ref.final_ps), "GPU result differs from oracle"
+        got = eng.gathered_results() if sharded else res
+        if rank == 0:
+            ref = oracle.run(cfg, tr)
+            assert np.array_equal(got.final_ps, ref.final_ps), "GPU result differs from oracle"
 
     if rank == 0:
         value = hops_all * a.steps / elapsed_max
@@ -119,10 +138,11 @@ def main():
         dom = max(("k_level", "k_port_stream"), key=lambda k: kst.get(k, (0.0, 0))[0])
         port_ms, port_launches = kst.get(dom, (0.0, 0))
         # dominant kernel: the per-level chunk kernel (k_level, or k_port_stream on the v1 path).
-        # Algorithmic bytes over all its launches: 32 B per mesh hop + 24 B per packet.
-        alg_bytes = hops * BYTES_PER_HOP + pkts * BYTES_PER_PKT
+        # Algorithmic bytes over all its launches on this rank: 32 B per mesh hop + 24 B per delivered packet.
+        alg_bytes = my_hops * BYTES_PER_HOP + my_pkts * BYTES_PER_PKT
         achieved = alg_bytes / (port_ms * 1e-3) / 1e9 if port_ms > 0 else 0.0
-        whole_job_gbs = value * (BYTES_PER_HOP + BYTES_PER_PKT * pkts / max(hops, 1)) / 1e9
+        whole_job_gbs = value * (BYTES_PER_HOP + BYTES_PER_PKT * pkts / max(hops, 1)) / 1e9 / world
+        workload = f"emesh_hop_by_hop {W}x{H} {a.mix} load={load} pkts/tile={a.ppt}"
         line = {
             "metric": "packet-hops simulated/sec (node) + % HBM roofline, 1024-tile emesh",
             "value": value,
@@ -132,15 +152,16 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (synthetic_network.cc uniform_random restated, fixed seeds)",
             "config": {
-                "workload": f"emesh_hop_by_hop {W}x{H} {a.mix} load={a.load} pkts/tile={a.ppt}",
-                "tiles": W * H, "packets_per_rank": len(tr), "mesh_hops_per_rank": hops,
+                "workload": workload,
+                "tiles": W * H, "packets": len(tr) * (world if wl == "replicas" else 1), "mesh_hops": int(hops_all),
                 "flit_width": 64, "router_delay": 1, "link_delay": 1, "queue": "history_tree+mg1",
-                "parallelism": f"replicas{world}" if world > 1 else "single",
+                "parallelism": (f"rowband/colband{world} + RCCL all-to-all" if sharded and world > 1 else
+                                f"replicas{world}" if world > 1 else "single"),
                 "engine_path": int(summ.get("engine_path", -1)),
             },
             "roofline": {
@@ -149,19 +170,20 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": pmc_traffic(f"emesh_hop_by_hop {W}x{H} {a.mix} load={a.load} pkts/tile={a.ppt}", dom),
+                "traffic": pmc_traffic(workload, dom) if world == 1 else None,
                 "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/" + PMC_FILE + ")",
                 "algorithmic_bytes_per_launch": alg_bytes / max(port_launches, 1),
                 "kernel": dom,
                 "kernel_launches": port_launches,
                 "kernel_avg_us": port_ms * 1e3 / max(port_launches, 1),
-                "whole_job_frac": whole_job_gbs / HBM_PEAK_GBS,
+                "whole_job_frac_per_gpu": whole_job_gbs / HBM_PEAK_GBS,
+                "scope": "rank 0's launches and its share of the hops",
             },
             "kernel_ms": {k: round(v[0], 4) for k, v in kst.items()},
             "trace_gen_s": round(gen_s, 2),
         }
         if a.cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(a, W, H, hot)
+            line["cpu_baseline"] = cpu_baseline(a, W, H, load, hot)
         print(json.dumps(line), flush=True)
 
     eng.close()
@@ -187,19 +209,19 @@ def pmc_traffic(workload, kernel):
     return d.get("traffic_bytes_per_launch")
 
 
-def cpu_baseline(a, W, H, hot):
+def cpu_baseline(a, W, H, load, hot):
     """The CPU oracle (event-driven restatement of the reference path) timed on
     one host core over a bounded sample of the same workload."""
     from graphite_amd import gnoc
     from oracle import oracle
-    tr = gnoc.synthetic_trace(W, H, a.load, a.cpu_sample_ppt, seed=a.seed, hotspot_fraction=hot, num_hotspots=16)
+    tr = gnoc.synthetic_trace(W, H, load, a.cpu_sample_ppt, seed=a.seed, hotspot_fraction=hot, num_hotspots=16)
     cfg = gnoc.EngineConfig(num_tiles=W * H)
     t0 = time.perf_counter()
     r = oracle.run(cfg, tr)
     dt = time.perf_counter() - t0
     hops = int(r.port_count.reshape(-1, 6)[:, :5].sum())
     return {"value": hops / dt, "unit": "packet-hops/s", "cores": 1, "kind": "port",
-            "sample": f"{W}x{H} {a.mix} load={a.load} pkts/tile={a.cpu_sample_ppt}: {len(tr)} packets, "
+            "sample": f"{W}x{H} {a.mix} load={load} pkts/tile={a.cpu_sample_ppt}: {len(tr)} packets, "
                       f"{hops} mesh hops in {dt:.2f} s"}
 
 

@@ -90,7 +90,7 @@ struct gnoc_engine
    DevBuf aux, routed, final_ps, zl, cont;
    DevBuf hist, tot, slot_cnt, slot_base, counters, gtot;
    DevBuf recs, samp_t, samp_id, Hs, Pp, Prow, nexc, dirty;
-   DevBuf pio, pnc, pgb, lvl_cbase, cdesc, flags, st, lvl_ctr;
+   DevBuf pio, pnc, pgb, lvl_cbase, lvl_qb, cdesc, flags, st, lvl_ctr;
    DevBuf port_sum, port_cnt, port_mg1, plan_ports, stamps, done;
    uint64_t h_chunk_bound = 0;
    int force_v1 = 0;
@@ -580,6 +580,7 @@ static int run_plan_v3(gnoc_engine* e)
    GNOC_HIP(e, e->cdesc.ensure(chunk_bound * sizeof(PortIO3)));
    GNOC_HIP(e, e->st.ensure(chunk_bound * LV_STATE_WORDS * 8));
    GNOC_HIP(e, e->lvl_ctr.ensure((size_t) L * LV_QUEUES * 4));
+   GNOC_HIP(e, e->lvl_qb.ensure((size_t) L * LV_QB * 4));
    GNOC_HIP(e, hipMemsetAsync(e->st.p, 0, chunk_bound * LV_STATE_WORDS * 8, s));   // look-back granules
    GNOC_HIP(e, hipMemsetAsync(e->lvl_ctr.p, 0, (size_t) L * LV_QUEUES * 4, s));
    const uint32_t pg = (P + 255) / 256;
@@ -590,6 +591,8 @@ static int run_plan_v3(gnoc_engine* e)
                LV_CTGT, (uint64_t) e->level_grid * LV_CTGT * LV_TAIL_ROUNDS_NUM / LV_TAIL_ROUNDS_DEN);
    GNOC_LAUNCH(e, KC_PLAN, k_plan_scan, dim3(1), dim3(1024), 0, s, P, L, e->d_lvl_off.as<uint32_t>(),
                e->pnc.as<uint32_t>(), e->pgb.as<uint32_t>(), e->lvl_cbase.as<uint32_t>());
+   GNOC_LAUNCH(e, KC_PLAN, k_plan_queues, dim3(L), dim3(64), 0, s, e->d_lvl_off.as<uint32_t>(), e->pgb.as<uint32_t>(),
+               e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), (uint32_t) e->level_grid);
    GNOC_LAUNCH(e, KC_PLAN, k_plan_expand, dim3(pg), dim3(256), 0, s, P, e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
                e->pgb.as<uint32_t>());
    GNOC_LAUNCH(e, KC_PLAN, k_plan_fill, dim3(P), dim3(64), 0, s, e->pio.as<PortIO3>(), e->cdesc.as<PortIO3>());
@@ -626,7 +629,7 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
    const bool xl = xlv && *xlv == '1' && e->nranks == 1;
    uint64_t* stp = stamps ? e->stamps.as<uint64_t>() : nullptr;
 #define GNOC_LEVEL_ARGS(lvl)                                                                                         \
-   c, (lvl), e->lvl_cbase.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
+   c, (lvl), e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
       e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(),                 \
       e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),                          \
       e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(), e->counters.as<unsigned>() + 8,     \

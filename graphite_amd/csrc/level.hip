@@ -48,7 +48,17 @@ constexpr uint32_t LV_CTGT = LV_CTGT_V;  // target records per chunk
 #endif
 constexpr uint64_t LV_SPIN_CYCLES = 1ull << 31;   // give up a wait after ~1 s (errflag -> exact v1 rerun)
 constexpr uint64_t LV_TAG = 1ull << 63;
-constexpr uint32_t LV_QUEUES = 8;        // chunk dequeue heads per level (power of two)
+#ifndef LV_QUEUES_V
+#define LV_QUEUES_V 1
+#endif
+#ifndef LV_LATE_ROUNDS
+#define LV_LATE_ROUNDS 4   // levels with more chunks than this many rounds of the grid fetch the next chunk late
+#endif
+#ifndef LV_PORT_QUEUES
+#define LV_PORT_QUEUES 1   // 1: port-aligned queue ranges (+ stealing); 0: chunk-interleaved queues
+#endif
+constexpr uint32_t LV_QUEUES = LV_QUEUES_V;   // chunk dequeue heads per level (power of two)
+constexpr uint32_t LV_QB = LV_QUEUES + 2;     // per-level plan words: queue bases, then the late-fetch flag
 constexpr int LV_STATE_WORDS = 16;       // u64 per chunk state
 
 // Per-port descriptor, built on device by k_plan_ports from the slot layout.
@@ -116,6 +126,10 @@ struct LvSmem
       uint32_t nmain[LV_IN], nxe[LV_IN];
       uint32_t search[2 * LV_IN];
    } nx;
+   // this level's dequeue heads: queue q owns chunks [qb[q], qb[q+1]) (level-relative,
+   // port-aligned, so a chunk's look-back predecessor is always in its own queue)
+   uint32_t qb[LV_QB];        // [LV_QUEUES + 1]: fetch the next chunk after the look-back (long ports)
+   uint32_t qdone;            // bit q: queue q handed out its last chunk
 };
 
 // ---------------------------------------------------------------------------
@@ -1037,14 +1051,54 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, bool first, bool anyexc, uint3
       // takes chunks q, q+8, q+16, ... in order, so every predecessor of a chunk
       // is held by a running workgroup or done.  The first chunk of each
       // workgroup is static (blockIdx / 8), so a level starts without the atomic.
-      const uint32_t q = blockIdx.x & (LV_QUEUES - 1);
-      uint32_t cid = blockIdx.x / LV_QUEUES;
-      if (!first)
+      uint32_t idx = 0xFFFFFFFFu;
+#ifdef LV_QSPREAD
+      const uint32_t q0 = (blockIdx.x / 8) & (LV_QUEUES - 1);   // a queue's workgroups on every XCD
+#else
+      const uint32_t q0 = blockIdx.x & (LV_QUEUES - 1);
+#endif
+      if (XL || !LV_PORT_QUEUES)
       {
-         if (lane == 0) cid = atomicAdd(ctr + q, 1u) + (gridDim.x - q + LV_QUEUES - 1) / LV_QUEUES;
-         cid = __shfl(cid, 0);
+         uint32_t cid = blockIdx.x / LV_QUEUES;
+         if (!first)
+         {
+            if (lane == 0) cid = atomicAdd(ctr + q0, 1u) + (gridDim.x - q0 + LV_QUEUES - 1) / LV_QUEUES;
+            cid = __shfl(cid, 0);
+         }
+         idx = q0 + LV_QUEUES * cid;
       }
-      const uint32_t idx = q + LV_QUEUES * cid;
+      else
+      {
+         // Port-aligned queues: every chunk of a port sits in one queue and is
+         // handed out in order, so its predecessor is already held by a running
+         // workgroup (or done).  Group q starts with chunk blockIdx/8 of queue q
+         // (static), then takes from its queue's head; a drained queue sends its
+         // workgroups on to the next queues (still in-order within each queue).
+         if (first)
+         {
+#ifdef LV_QSPREAD
+            const uint32_t k = (blockIdx.x & 7) + 8 * (blockIdx.x / (8 * LV_QUEUES));
+#else
+            const uint32_t k = blockIdx.x / LV_QUEUES;
+#endif
+            if (k < sm.qb[q0 + 1] - sm.qb[q0]) idx = sm.qb[q0] + k;
+         }
+         for (uint32_t t = 0; t < LV_QUEUES && idx == 0xFFFFFFFFu; t++)
+         {
+            const uint32_t q = (q0 + t) & (LV_QUEUES - 1);
+            if ((sm.qdone >> q) & 1u) continue;
+            const uint32_t size = sm.qb[q + 1] - sm.qb[q];
+            const uint32_t nst = (gridDim.x - q + LV_QUEUES - 1) / LV_QUEUES;   // taken statically
+            uint32_t cid = 0xFFFFFFFFu;
+            if (size > nst)
+            {
+               if (lane == 0) cid = atomicAdd(ctr + q, 1u) + nst;
+               cid = __shfl(cid, 0);
+            }
+            if (cid < size) idx = sm.qb[q] + cid;
+            else if (lane == 0) sm.qdone |= 1u << q;
+         }
+      }
       const uint32_t valid = idx < nch ? 1u : 0u;
       const uint32_t g = cb0 + idx;
       if (valid)
@@ -1089,6 +1143,7 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, bool first, bool anyexc, uint3
 
 template <bool STAMPS, bool XL>
 __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t level, const uint32_t* __restrict__ lvl_cbase,
+                                                const uint32_t* __restrict__ lvl_qb,
                                                 unsigned* __restrict__ ctr, const PortIO3* __restrict__ cdesc,
                                                 Rec* __restrict__ recs,
                                                 uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id,
@@ -1108,7 +1163,9 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
    // exception tails exist only if an earlier level's M/G/1 path wrote one (flag set
    // before this launch); the cross-level launch always reads the counts
    const bool anyexc = XL || errflag[2] != 0;
-   if (tid == 0) sm.nx.ready = 0;
+   if (tid == 0) { sm.nx.ready = 0; sm.qdone = 0; }
+   if (!XL && tid < LV_QB) sm.qb[tid] = lvl_qb[level * LV_QB + tid];
+   if (XL && tid == 0) sm.qb[LV_QUEUES + 1] = 0;
    lv_bar();
    if (wv >= 1) lv_fetch<XL>(sm, true, anyexc, cb0, nch, cctr, cdesc, recs, samp_t, samp_id, nexc, done, errflag);
    lv_bar();
@@ -1202,9 +1259,13 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
             {
                if (tid == 0) lv_publish_agg(st, g, so);
                if (STAMPS && stamps && tid == 0) stamps[(uint64_t) g * 16 + 15] = __builtin_amdgcn_s_memrealtime();
+               // Long ports: a chunk prefetched here waits for this chunk's look-back and
+               // emit, and its successors wait on it in turn (a convoy along the port);
+               // those levels fetch after the emit instead.
+               const bool late = sm.qb[LV_QUEUES + 1] != 0;
                if (wv == 0) lv_lookback(sm, sm.io.gbase, j, st, errflag);
-               else lv_fetch<XL>(sm, false, anyexc, cb0, nch, cctr, cdesc, recs, samp_t, samp_id, nexc, done, errflag);
-               fetched = true;
+               else if (!late) lv_fetch<XL>(sm, false, anyexc, cb0, nch, cctr, cdesc, recs, samp_t, samp_id, nexc, done, errflag);
+               fetched = !late;
                lv_bar();
             }
             LV_STAMP(6);
@@ -1500,6 +1561,36 @@ __global__ __launch_bounds__(1024) void k_plan_scan(uint32_t P, uint32_t L, cons
    for (uint32_t i = lo; i < hi; i++) { pgb[i] = run; run += pnc[i]; }
    __syncthreads();
    for (uint32_t l = threadIdx.x; l <= L; l += 1024) lvl_cbase[l] = l < L ? pgb[lvl_off[l]] : (uint32_t) part[1023];
+}
+
+// One wave per level: split the level's chunks into LV_QUEUES port-aligned
+// ranges of about equal size (a port's chunks never straddle two queues).
+__global__ __launch_bounds__(64) void k_plan_queues(const uint32_t* __restrict__ lvl_off,
+                                                    const uint32_t* __restrict__ pgb,
+                                                    const uint32_t* __restrict__ lvl_cbase, uint32_t* __restrict__ lvl_qb,
+                                                    uint32_t grid)
+{
+   const uint32_t l = blockIdx.x, q = threadIdx.x;
+   const uint32_t a = lvl_off[l], b = lvl_off[l + 1];
+   const uint32_t cb = lvl_cbase[l], T = lvl_cbase[l + 1] - cb;
+   if (q == LV_QUEUES + 1)
+   {
+      // measured (32x32 vs 64x64): prefetching during the look-back pays while a level
+      // is a few grid rounds; over many rounds the held chunks build a convoy
+      lvl_qb[l * LV_QB + q] = T > (uint64_t) LV_LATE_ROUNDS * grid ? 1u : 0u;
+      return;
+   }
+   if (q > LV_QUEUES) return;
+   const uint32_t target = (uint32_t) (((uint64_t) q * T) / LV_QUEUES);
+   // first port k of the level with pgb[k] - cb >= target
+   uint32_t lo = a, hi = b;
+   while (lo < hi)
+   {
+      const uint32_t m = (lo + hi) / 2;
+      if (pgb[m] - cb >= target) hi = m;
+      else lo = m + 1;
+   }
+   lvl_qb[l * LV_QB + q] = q == LV_QUEUES || lo == b ? T : pgb[lo] - cb;
 }
 
 __global__ __launch_bounds__(256) void k_plan_expand(uint32_t P, PortIO3* __restrict__ pio, const uint32_t* __restrict__ pnc,

@@ -12,7 +12,8 @@ from graphite_amd import gnoc  # noqa: E402
 
 mesh = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 ppt = int(sys.argv[2]) if len(sys.argv) > 2 else 10000
-tr = gnoc.synthetic_trace(mesh, mesh, 0.005, ppt, seed=1)
+load = float(sys.argv[3]) if len(sys.argv) > 3 else 0.005
+tr = gnoc.synthetic_trace(mesh, mesh, load, ppt, seed=1)
 eng = gnoc.Engine(gnoc.EngineConfig(num_tiles=mesh * mesh))
 eng.submit(tr)
 eng.run()
