@@ -89,7 +89,7 @@ struct gnoc_engine
    // work
    DevBuf aux, routed, final_ps, zl, cont;
    DevBuf hist, tot, slot_cnt, slot_base, counters, gtot;
-   DevBuf recs, samp_t, samp_id, Hs, Pp, Prow, nexc, dirty;
+   DevBuf recs, samp_t, samp_id, Hs, Pp, Prow, pcol, nexc, dirty;
    DevBuf pio, pnc, pgb, lvl_cbase, lvl_qb, cdesc, flags, st, lvl_ctr;
    DevBuf port_sum, port_cnt, port_mg1, plan_ports, stamps, done;
    uint64_t h_chunk_bound = 0;
@@ -381,8 +381,18 @@ static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n,
       if (!bypass)
       {
          const int64_t sx = s % W, sy = s / W, dx = d % W, dy = d / W;
-         rec += 2 + (uint64_t) (std::llabs(sx - dx) + std::llabs(sy - dy));
-         if (nr > 1 && e->dc.contention) e->x_cnt[(size_t) rb[sy] * nr + cb[dx]]++;
+         const uint64_t ax = (uint64_t) std::llabs(sx - dx), ay = (uint64_t) std::llabs(sy - dy);
+         if (nr <= 1) rec += 2 + ax + ay;
+         else
+         {
+            // records this rank materialises: injection + X leg in its row band (all
+            // injections when prep is not band-local), the turn record on either side,
+            // the Y leg in its column band
+            const bool r_own = rb[sy] == (uint32_t) e->rank, c_own = cb[dx] == (uint32_t) e->rank;
+            const bool band_prep = W <= 64 && H <= 64;
+            rec += (r_own ? 1 + ax : 0) + (!r_own && !band_prep ? 1 : 0) + (r_own || c_own ? 1 : 0) + (c_own ? ay : 0);
+            if (e->dc.contention) e->x_cnt[(size_t) rb[sy] * nr + cb[dx]]++;
+         }
       }
    }
    if (n && pk->inject_ps[n - 1] >= (1ull << 50)) return fail(e, GNOC_EUNSUPPORTED, "inject time beyond 2^50 ps");
@@ -502,7 +512,8 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    GNOC_HIP(e, hipMemsetAsync(e->counters.p, 0, 64, e->stream));
    hipLaunchKernelGGL(k_classify, dim3(nch), dim3(256), N * 4, e->stream, e->dc, (uint64_t) n, pch, e->d_inj, e->d_src,
                          e->d_dst, e->d_bits, e->d_flags, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(),
-                         e->final_ps.as<uint64_t>(), e->hist.as<uint32_t>(), e->counters.as<unsigned long long>());
+                         e->final_ps.as<uint64_t>(), e->hist.as<uint32_t>(), e->counters.as<unsigned long long>(),
+                         0u, e->dc.H, 0u, e->dc.W, nullptr, nullptr);
    GNOC_HIP(e, hipGetLastError());
    GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 16, hipMemcpyDeviceToHost, e->stream));
    GNOC_HIP(e, hipStreamSynchronize(e->stream));
@@ -566,13 +577,29 @@ static int run_levels_v1(gnoc_engine* e)
 // ---------------------------------------------------------------------------
 // v3: device-planned chunked levels
 // ---------------------------------------------------------------------------
+// Records per chunk: LV_CTGT, or GNOC_CHUNK (test knob: small chunks put serial
+// M/G/1 prefixes and exception tails across many chunk boundaries).
+static uint32_t chunk_target()
+{
+   const char* v = std::getenv("GNOC_CHUNK");
+   const long t = v ? std::atol(v) : 0;
+   return t > 0 ? (uint32_t) std::min<long>(std::max<long>(t, 64), LV_CMAX) : LV_CTGT;
+}
+static uint64_t chunk_bound_of(const gnoc_engine* e, uint32_t P)
+{
+   const uint32_t tgt = chunk_target();
+   const uint32_t cmin = LV_ROUNDS_FIT ? std::min<uint32_t>(LV_CMIN, tgt) : tgt;   // smallest chunk a level can get
+   return e->rec_bound / cmin + P + 1;
+}
+
 static int run_plan_v3(gnoc_engine* e)
 {
    const DevCfg& c = e->dc;
    hipStream_t s = e->stream;
    const uint32_t P = (uint32_t) e->lvl_ports.size();
    const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
-   const uint64_t chunk_bound = e->rec_bound / ((LV_CTGT + 1) / 2) + P + 1;   // guided tails use half-size chunks
+   const uint64_t chunk_bound = chunk_bound_of(e, P);
+   const uint32_t ctgt = chunk_target();
    GNOC_HIP(e, e->pio.ensure((size_t) P * sizeof(PortIO3)));
    GNOC_HIP(e, e->pnc.ensure((size_t) P * 4));
    GNOC_HIP(e, e->pgb.ensure((size_t) P * 4));
@@ -581,16 +608,17 @@ static int run_plan_v3(gnoc_engine* e)
    GNOC_HIP(e, e->st.ensure(chunk_bound * LV_STATE_WORDS * 8));
    GNOC_HIP(e, e->lvl_ctr.ensure((size_t) L * LV_QUEUES * 4));
    GNOC_HIP(e, e->lvl_qb.ensure((size_t) L * LV_QB * 4));
-   GNOC_HIP(e, hipMemsetAsync(e->st.p, 0, chunk_bound * LV_STATE_WORDS * 8, s));   // look-back granules
    GNOC_HIP(e, hipMemsetAsync(e->lvl_ctr.p, 0, (size_t) L * LV_QUEUES * 4, s));
    const uint32_t pg = (P + 255) / 256;
    GNOC_LAUNCH(e, KC_PLAN, k_plan_ports, dim3(pg), dim3(256), 0, s, c, P, e->d_lvl_ports.as<uint32_t>(),
                e->d_port_k.as<uint32_t>(), e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
-               LV_CTGT);
+               ctgt);
    GNOC_LAUNCH(e, KC_PLAN, k_plan_guided, dim3(L), dim3(1024), 0, s, e->d_lvl_off.as<uint32_t>(), e->pnc.as<uint32_t>(),
-               LV_CTGT, (uint64_t) e->level_grid * LV_CTGT * LV_TAIL_ROUNDS_NUM / LV_TAIL_ROUNDS_DEN);
+               ctgt, (uint64_t) e->level_grid);
    GNOC_LAUNCH(e, KC_PLAN, k_plan_scan, dim3(1), dim3(1024), 0, s, P, L, e->d_lvl_off.as<uint32_t>(),
                e->pnc.as<uint32_t>(), e->pgb.as<uint32_t>(), e->lvl_cbase.as<uint32_t>());
+   GNOC_LAUNCH(e, KC_PLAN, k_zero_state, dim3(1024), dim3(256), 0, s, e->lvl_cbase.as<uint32_t>(), L,
+               e->st.as<uint64_t>());   // look-back granules
    GNOC_LAUNCH(e, KC_PLAN, k_plan_queues, dim3(L), dim3(64), 0, s, e->d_lvl_off.as<uint32_t>(), e->pgb.as<uint32_t>(),
                e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), (uint32_t) e->level_grid);
    GNOC_LAUNCH(e, KC_PLAN, k_plan_expand, dim3(pg), dim3(256), 0, s, P, e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
@@ -607,7 +635,7 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
    hipStream_t s = e->stream;
    const uint32_t P = (uint32_t) e->lvl_ports.size();
    const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
-   const uint64_t chunk_bound = e->rec_bound / ((LV_CTGT + 1) / 2) + P + 1;
+   const uint64_t chunk_bound = chunk_bound_of(e, P);
    const char* stv = std::getenv("GNOC_STAMPS");
    const bool stamps = stv && *stv == '1';
    e->h_chunk_bound = chunk_bound;
@@ -673,8 +701,14 @@ static int run_prep(gnoc_engine* e, bool* done)
    const uint32_t nch = (uint32_t) std::max<uint64_t>(1, (n + pch - 1) / pch);
    int nbits = 0;
    while ((1u << nbits) < N) nbits++;
+   // Sharded runs prepare only this rank's share: the injection slots and X-leg
+   // counts of its row band [pr0, pr1), and (counted in k_classify) the Y-leg and
+   // turn-slot counts of its column band.  Meshes over 64 on a side prepare everything.
+   const bool band_prep = e->nranks > 1 && W <= 64 && H <= 64;
+   const uint32_t pr0 = band_prep ? e->ry0 : 0u, pr1 = band_prep ? e->ry1 : H, nR = pr1 - pr0;
+   const uint32_t nC = e->cx1 - e->cx0;
    // row-histogram grouping: ~512 workgroups, LDS per group <= 32 KiB of source bins
-   uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(W, 512 / H));
+   uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(W, 512 / nR));
    while (G < W && (W / G + 1) * W * 3 > 8192) G++;
    const int pp_lds = N <= 8192;
    size_t rh_lds = (size_t) ((W + G - 1) / G) * W * 3 * 4 + (pp_lds ? (size_t) N * 4 : 0);
@@ -700,6 +734,7 @@ static int run_prep(gnoc_engine* e, bool* done)
    GNOC_HIP(e, e->port_sum.ensure(nports * 8));
    GNOC_HIP(e, e->port_cnt.ensure(nports * 8));
    GNOC_HIP(e, e->port_mg1.ensure(nports * 8));
+   if (band_prep) GNOC_HIP(e, e->pcol.ensure((size_t) nC * H * H * 4));
 
    e->evused = 0;
    e->evkid.clear();
@@ -711,11 +746,13 @@ static int run_prep(gnoc_engine* e, bool* done)
    GNOC_HIP(e, hipMemsetAsync(e->port_cnt.p, 0, nports * 8, s));
    GNOC_HIP(e, hipMemsetAsync(e->port_mg1.p, 0, nports * 8, s));
    if (!pp_lds) GNOC_HIP(e, hipMemsetAsync(e->Pp.p, 0, (size_t) H * G * N * 4, s));
+   if (band_prep) GNOC_HIP(e, hipMemsetAsync(e->pcol.p, 0, (size_t) nC * H * H * 4, s));
 
    // always launched: for an empty batch it writes the all-zero source histogram
    GNOC_LAUNCH(e, KC_CLASSIFY, k_classify, dim3(nch), dim3(256), N * 4, s, c, (uint64_t) n, pch, e->d_inj, e->d_src,
                   e->d_dst, e->d_bits, e->d_flags, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(),
-                  e->final_ps.as<uint64_t>(), e->hist.as<uint32_t>(), e->counters.as<unsigned long long>());
+                  e->final_ps.as<uint64_t>(), e->hist.as<uint32_t>(), e->counters.as<unsigned long long>(), pr0, pr1,
+                  e->cx0, e->cx1, band_prep ? e->pcol.as<uint32_t>() : nullptr, e->slot_cnt.as<uint32_t>());
 
    if (!c.contention)
    {
@@ -743,16 +780,22 @@ static int run_prep(gnoc_engine* e, bool* done)
       GNOC_LAUNCH(e, KC_SCATTER, k_scatter, dim3(nch), dim3(64), N * 4, s, (uint64_t) n, pch, N, nbits, e->d_src,
                   e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(), e->recs.as<Rec>(),
                   e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>());
-   GNOC_LAUNCH(e, KC_ROW_HIST, k_row_hist, dim3(G, H), dim3(256), rh_lds, s, c, G, e->recs.as<Rec>(),
-               e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->Hs.as<uint32_t>(), e->Pp.as<uint32_t>(), pp_lds);
-   GNOC_LAUNCH(e, KC_PROW, k_prow, dim3((uint32_t) (((uint64_t) H * N + 255) / 256)), dim3(256), 0, s, N, H, G,
-               e->Pp.as<uint32_t>(), e->Prow.as<uint32_t>());
+   GNOC_LAUNCH(e, KC_ROW_HIST, k_row_hist, dim3(G, nR), dim3(256), rh_lds, s, c, G, e->recs.as<Rec>(),
+               e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->Hs.as<uint32_t>(), e->Pp.as<uint32_t>(), pp_lds,
+               pr0);
+   if (!band_prep)
+      GNOC_LAUNCH(e, KC_PROW, k_prow, dim3((uint32_t) (((uint64_t) H * N + 255) / 256)), dim3(256), 0, s, N, H, G,
+                  e->Pp.as<uint32_t>(), e->Prow.as<uint32_t>());
    if (W <= 64 && H <= 64)
    {
-      GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_x, dim3(H), dim3(256), (size_t) W * W * 3 * 4, s, c,
-                  e->Hs.as<uint32_t>(), e->slot_cnt.as<uint32_t>());
-      GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_y, dim3(W), dim3(256), (size_t) H * H * 4, s, c,
-                  e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>());
+      GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_x, dim3(nR), dim3(256), (size_t) W * W * 3 * 4, s, c,
+                  e->Hs.as<uint32_t>(), e->slot_cnt.as<uint32_t>(), pr0);
+      if (band_prep)
+         GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_y, dim3(nC), dim3(256), (size_t) H * H * 4, s, c,
+                     e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>(), e->cx0, (const uint32_t*) e->pcol.as<uint32_t>());
+      else
+         GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_y, dim3(W), dim3(256), (size_t) H * H * 4, s, c,
+                     e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>(), 0u, (const uint32_t*) nullptr);
    }
    else
       GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts, dim3((N * 5 + 255) / 256), dim3(256), 0, s, c, e->Hs.as<uint32_t>(),

@@ -528,7 +528,7 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
       const uint32_t dx = aux_dx(aux[i]), dy = aux_dy(aux[i]);
       // a sharded engine delivers the packets of its column band (shard.hip); others read 0
       if (dx < cx0 || dx >= cx1) { final_ps[i] = 0; zl[i] = 0; cont[i] = 0; continue; }
-      if (!routed[i]) { zl[i] = 0; cont[i] = 0; continue; }
+      if (!(routed[i] & 1)) { zl[i] = 0; cont[i] = 0; continue; }
       uint32_t sx, sy;
       tile_xy(src[i], c.W, c.magicW, sx, sy);
       const uint64_t hops = (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);

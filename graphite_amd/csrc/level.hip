@@ -42,10 +42,6 @@ constexpr int LV_MAXLEAF = 32;           // leaves per chunk (bursts); beyond ->
 #define LV_CTGT_V 1600
 #endif
 constexpr uint32_t LV_CTGT = LV_CTGT_V;  // target records per chunk
-#ifndef LV_TAIL_ROUNDS_NUM
-#define LV_TAIL_ROUNDS_NUM 0   // records at the end of a level cut into half-size chunks (0: off, measured slower),
-#define LV_TAIL_ROUNDS_DEN 1   // in rounds of the persistent grid (NUM / DEN)
-#endif
 constexpr uint64_t LV_SPIN_CYCLES = 1ull << 31;   // give up a wait after ~1 s (errflag -> exact v1 rerun)
 constexpr uint64_t LV_TAG = 1ull << 63;
 #ifndef LV_QUEUES_V
@@ -1244,7 +1240,11 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
          LV_STAMP(4);
          if (j == 0)
          {
-            if (tid == 0 && c.analytical && sm.E > 0 && cyc1(sm.kt[sm.perm[0]]) == 0) sm.cy.mode = 1;
+            // The port starts in the history tree's serial state (no gap yet); its first
+            // arrival keeps it there only at cycle 0 (queue_model_history_tree.cc:58-99).
+            // An empty chunk 0 (every early record is an exception tail of another
+            // chunk's range) hands the untouched serial state on to its successor.
+            if (tid == 0 && c.analytical && (sm.E == 0 || cyc1(sm.kt[sm.perm[0]]) == 0)) sm.cy.mode = 1;
             if (tid == 0) sm.s0 = 0;
             lv_bar();
          }
@@ -1385,7 +1385,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
                lv_load_merge(sm, recs, sm.lk_t[L], sm.lk_i[L], sm.lk_t[L + 1], sm.lk_i[L + 1], hl, hh, true);
                if (j == 0 && L == 0)
                {
-                  if (tid == 0 && c.analytical && sm.E > 0 && cyc1(sm.kt[sm.perm[0]]) == 0) sm.cy.mode = 1;
+                  if (tid == 0 && c.analytical && (sm.E == 0 || cyc1(sm.kt[sm.perm[0]]) == 0)) sm.cy.mode = 1;
                   lv_bar();
                }
                lv_leaf(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);
@@ -1503,37 +1503,70 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
    pnc[k] = tot;  // records of the port (k_plan_scan turns it into a chunk count)
 }
 
-// One block per level.  Records -> chunk counts with guided sizes: ports whose
-// records fall in the level's last `tail_rec` records (about one round of the
-// persistent grid) use half-size chunks, so the level ends with a short round.
+// One block per level.  Records -> chunk counts.  A level runs in rounds of the
+// persistent grid and ends with its slowest round, so the chunk size is chosen
+// per level to make the chunk count just fit a whole number of rounds:
+// rounds = round(records / (ctgt * grid)) (at least 1), then the smallest size c
+// with sum over ports of ceil(records_p / c) <= rounds * grid, kept within
+// [LV_CMIN, LV_CMAX] (LDS holds LV_CAP records per leaf).
+#ifndef LV_CMAX
+#define LV_CMAX 1700
+#endif
+#ifndef LV_CMIN
+#define LV_CMIN 384
+#endif
+#ifndef LV_ROUNDS_FIT
+#define LV_ROUNDS_FIT 0   // measured: 32x32 6% slower, 64x64 unchanged (dynamic dequeue already fills the tail)
+#endif
 __global__ __launch_bounds__(1024) void k_plan_guided(const uint32_t* __restrict__ lvl_off, uint32_t* __restrict__ pnc,
-                                                      uint32_t ctgt, uint64_t tail_rec)
+                                                      uint32_t ctgt, uint64_t grid)
 {
    __shared__ uint64_t part[1024];
+   __shared__ uint32_t pcnt[1024];
+   __shared__ uint32_t csel;
    const uint32_t l = blockIdx.x;
    const uint32_t a = lvl_off[l], b = lvl_off[l + 1], np = b - a;
    const uint32_t per = (np + 1023) / 1024;
    const uint32_t lo = a + min(threadIdx.x * per, np), hi = a + min((threadIdx.x + 1) * per, np);
    uint64_t s = 0;
-   for (uint32_t i = lo; i < hi; i++) s += pnc[i];
+   uint32_t nz = 0;
+   for (uint32_t i = lo; i < hi; i++) { s += pnc[i]; nz += pnc[i] != 0; }
    part[threadIdx.x] = s;
+   pcnt[threadIdx.x] = nz;
    __syncthreads();
-   for (uint32_t off = 1; off < 1024; off <<= 1)
+   for (uint32_t off = 512; off > 0; off >>= 1)
    {
-      const uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-      __syncthreads();
-      part[threadIdx.x] += v;
+      if (threadIdx.x < off)
+      {
+         part[threadIdx.x] += part[threadIdx.x + off];
+         pcnt[threadIdx.x] += pcnt[threadIdx.x + off];
+      }
       __syncthreads();
    }
-   const uint64_t total = part[1023];
-   const uint64_t tail_start = total > tail_rec ? total - tail_rec : 0;
-   uint64_t run = part[threadIdx.x] - s;
+   if (threadIdx.x == 0)
+   {
+      const uint64_t R = part[0], P = pcnt[0];
+      uint32_t c = ctgt;
+      if (LV_ROUNDS_FIT && R > 0)
+      {
+         uint64_t rounds = (R + ctgt * grid / 2) / (ctgt * grid);
+         if (rounds < 1) rounds = 1;
+         for (;; rounds++)
+         {
+            const uint64_t slots = rounds * grid;
+            if (slots <= P) continue;
+            const uint64_t cc = (R + slots - P - 1) / (slots - P);
+            if (cc <= LV_CMAX) { c = (uint32_t) (cc < LV_CMIN ? LV_CMIN : cc); break; }
+         }
+      }
+      csel = c;
+   }
+   __syncthreads();
+   const uint32_t c = csel;
    for (uint32_t i = lo; i < hi; i++)
    {
       const uint32_t tot = pnc[i];
-      const uint32_t tg = run + tot > tail_start ? (ctgt + 1) / 2 : ctgt;
-      pnc[i] = tot ? (tot + tg - 1) / tg : 0;
-      run += tot;
+      pnc[i] = tot ? (tot + c - 1) / c : 0;
    }
 }
 
@@ -1561,6 +1594,15 @@ __global__ __launch_bounds__(1024) void k_plan_scan(uint32_t P, uint32_t L, cons
    for (uint32_t i = lo; i < hi; i++) { pgb[i] = run; run += pnc[i]; }
    __syncthreads();
    for (uint32_t l = threadIdx.x; l <= L; l += 1024) lvl_cbase[l] = l < L ? pgb[lvl_off[l]] : (uint32_t) part[1023];
+}
+
+// Look-back state of the chunks this run uses (the count is known on device only).
+__global__ __launch_bounds__(256) void k_zero_state(const uint32_t* __restrict__ lvl_cbase, uint32_t L,
+                                                    uint64_t* __restrict__ st)
+{
+   const uint64_t n = (uint64_t) lvl_cbase[L] * LV_STATE_WORDS;
+   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+      st[i] = 0;
 }
 
 // One wave per level: split the level's chunks into LV_QUEUES port-aligned

@@ -32,7 +32,9 @@ __global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, uint32_t
                                                   const uint32_t* __restrict__ bits, const uint32_t* __restrict__ flags,
                                                   uint32_t* __restrict__ aux, uint8_t* __restrict__ routed,
                                                   uint64_t* __restrict__ final_ps, uint32_t* __restrict__ hist,
-                                                  unsigned long long* __restrict__ counters)
+                                                  unsigned long long* __restrict__ counters, uint32_t ry0, uint32_t ry1,
+                                                  uint32_t cx0, uint32_t cx1, uint32_t* __restrict__ pcol,
+                                                  uint32_t* __restrict__ slot_cnt)
 {
    extern __shared__ uint32_t h[];   // N source counters
    const uint32_t N = c.N;
@@ -52,13 +54,24 @@ __global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, uint32_t
       tile_xy(s, c.W, c.magicW, sx, sy);
       tile_xy(d, c.W, c.magicW, dx, dy);
       aux[i] = aux_pack(dx, dy, F);
-      routed[i] = bypass ? 0 : 1;
+      // bit 0: routed through the mesh; bit 1: and injected in this rank's row band
+      const bool mine = sy >= ry0 && sy < ry1;
+      routed[i] = bypass ? 0 : mine ? 3 : 1;
       if (bypass)
       {
          final_ps[i] = inj[i];
          continue;
       }
-      atomicAdd(&h[s], 1u);
+      if (mine) atomicAdd(&h[s], 1u);
+      if (pcol && dx >= cx0 && dx < cx1)
+      {
+         // sharded run, destination in this rank's column band: the Y-leg counts
+         // (source row x destination row, per column) and the turn-slot count
+         atomicAdd(&pcol[((dx - cx0) * c.H + sy) * c.H + dy], 1u);
+         const uint32_t dir = dy > sy ? P_UP : dy < sy ? P_DOWN : P_SELF;
+         const uint32_t in = sx < dx ? IN_W : sx > dx ? IN_E : IN_LOCAL;
+         atomicAdd(&slot_cnt[slot_of(sy * c.W + dx, dir, in)], 1u);
+      }
       nrouted++;
       hops += (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
    }
@@ -176,7 +189,7 @@ __global__ __launch_bounds__(64) void k_scatter(uint64_t n, uint32_t pch, uint32
    for (uint64_t k = lo; k < hi; k += 64)
    {
       const uint64_t i = k + lane;
-      const bool valid = i < hi && routed[i];
+      const bool valid = i < hi && (routed[i] & 2);
       const uint32_t s = valid ? src[i] : 0u;
       const uint64_t m = match_mask(s, valid, nbits);
       const uint32_t old = valid ? h[s] : 0u;
@@ -223,7 +236,7 @@ __global__ __launch_bounds__(256) void k_scatter4(uint64_t n, uint32_t pch, uint
    const uint64_t lo = min(c0 + w * q, c1), hi = min(lo + q, c1);
    uint32_t* hw = h4 + w * N;
    for (uint64_t i = lo + lane; i < hi; i += 64)
-      if (routed[i]) atomicAdd(&hw[src[i]], 1u);
+      if (routed[i] & 2) atomicAdd(&hw[src[i]], 1u);
    __syncthreads();
    // exclusive prefix over waves, plus the chunk's offset for the source
    const uint32_t* orow = offs + (uint64_t) blockIdx.x * N;
@@ -244,7 +257,7 @@ __global__ __launch_bounds__(256) void k_scatter4(uint64_t n, uint32_t pch, uint
    bool nv = false;
    uint32_t ns = 0, na = 0;
    uint64_t nt = 0;
-   if (i < hi) { nv = routed[i] != 0; ns = src[i]; nt = inj[i]; na = aux[i]; }   // independent loads
+   if (i < hi) { nv = (routed[i] & 2) != 0; ns = src[i]; nt = inj[i]; na = aux[i]; }   // independent loads
    for (uint64_t k = lo; k < hi; k += 64)
    {
       const bool valid = nv;
@@ -254,7 +267,7 @@ __global__ __launch_bounds__(256) void k_scatter4(uint64_t n, uint32_t pch, uint
       const uint64_t id = k + lane;
       const uint64_t i2 = k + 64 + lane;
       nv = false;
-      if (i2 < hi) { nv = routed[i2] != 0; ns = src[i2]; nt = inj[i2]; na = aux[i2]; }
+      if (i2 < hi) { nv = (routed[i2] & 2) != 0; ns = src[i2]; nt = inj[i2]; na = aux[i2]; }
       if (!nv) ns = 0;
       const uint64_t m = match_mask(sidx, valid, nbits);
       const uint32_t old = valid ? hw[sidx] : 0u;
@@ -288,11 +301,11 @@ __global__ __launch_bounds__(256) void k_scatter4(uint64_t n, uint32_t pch, uint
 __global__ __launch_bounds__(256) void k_row_hist(DevCfg c, uint32_t G, const Rec* __restrict__ recs,
                                                   const uint32_t* __restrict__ slot_cnt,
                                                   const uint64_t* __restrict__ slot_base, uint32_t* __restrict__ Hs,
-                                                  uint32_t* __restrict__ Pp, int pp_lds)
+                                                  uint32_t* __restrict__ Pp, int pp_lds, uint32_t ry0)
 {
    extern __shared__ uint32_t sm[];
    const uint32_t W = c.W, N = c.N;
-   const uint32_t y = blockIdx.y, g = blockIdx.x;
+   const uint32_t y = ry0 + blockIdx.y, g = blockIdx.x;
    const uint32_t x0 = (uint32_t) (((uint64_t) g * W) / G), x1 = (uint32_t) (((uint64_t) (g + 1) * W) / G);
    const uint32_t nhs = (x1 - x0) * W * 3;
    uint32_t* hs = sm;
@@ -410,10 +423,10 @@ __global__ __launch_bounds__(256) void k_slot_counts(DevCfg c, const uint32_t* _
 // per row for the X-leg inputs (LOCAL, W, E), one per column for the Y-leg
 // inputs (S, N).  Used when W*W*3 and H*H words fit (W, H <= 64).
 __global__ __launch_bounds__(256) void k_slot_counts_x(DevCfg c, const uint32_t* __restrict__ Hs,
-                                                       uint32_t* __restrict__ slot_cnt)
+                                                       uint32_t* __restrict__ slot_cnt, uint32_t ry0)
 {
    extern __shared__ uint32_t hr[];   // Hs rows of this mesh row: [sx][dx][cl]
-   const uint32_t W = c.W, y = blockIdx.x;
+   const uint32_t W = c.W, y = ry0 + blockIdx.x;
    const uint32_t nw = W * W * 3;
    for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x) hr[k] = Hs[(uint64_t) y * W * W * 3 + k];
    __syncthreads();
@@ -452,15 +465,18 @@ __global__ __launch_bounds__(256) void k_slot_counts_x(DevCfg c, const uint32_t*
    }
 }
 
+// Column x = cx0 + blockIdx.x.  pcol == nullptr: read column x of Prow[sy][dst];
+// else pcol[x - cx0][sy][dy] (sharded runs, counted in k_classify).
 __global__ __launch_bounds__(256) void k_slot_counts_y(DevCfg c, const uint32_t* __restrict__ Prow,
-                                                       uint32_t* __restrict__ slot_cnt)
+                                                       uint32_t* __restrict__ slot_cnt, uint32_t cx0,
+                                                       const uint32_t* __restrict__ pcol)
 {
-   extern __shared__ uint32_t pc[];   // column x of Prow: [sy][dy]
-   const uint32_t W = c.W, H = c.H, N = c.N, x = blockIdx.x;
+   extern __shared__ uint32_t pc[];   // column x: [sy][dy]
+   const uint32_t W = c.W, H = c.H, N = c.N, x = cx0 + blockIdx.x;
    for (uint32_t k = threadIdx.x; k < H * H; k += blockDim.x)
    {
       const uint32_t sy = k / H, dy = k % H;
-      pc[k] = Prow[(uint64_t) sy * N + dy * W + x];
+      pc[k] = pcol ? pcol[(uint64_t) blockIdx.x * H * H + k] : Prow[(uint64_t) sy * N + dy * W + x];
    }
    __syncthreads();
    for (uint32_t q = threadIdx.x; q < H * 5; q += blockDim.x)

@@ -90,6 +90,9 @@ def load() -> ctypes.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
+    # torch first, so libgnoc.so binds the HIP runtime torch loaded (one runtime per
+    # process: a second one finds no devices)
+    import torch  # noqa: F401
     lib = ctypes.CDLL(LIB_PATH)
     vp, sz = ctypes.c_void_p, ctypes.c_size_t
     lib.gnoc_config_default.argtypes = [ctypes.POINTER(GnocConfig), ctypes.c_int32]
@@ -418,3 +421,66 @@ class ShardedEngine(Engine):
         n, npt = self._n, r.port_sum_delay.shape[0]
         o = [0, n, 2 * n, 3 * n, 3 * n + npt, 3 * n + 2 * npt, 3 * n + 3 * npt]
         return Results(*(out[o[k]:o[k + 1]].copy() for k in range(6)), summary=r.summary)
+
+
+class LocalShardSet:
+    """Every rank of a sharded mesh in ONE process on one device: the same
+    gnoc_shard engines and device kernels as a multi-GPU run, with the
+    all-to-all done by copies between the ranks' buffers.  For parity tests of
+    any rank count on a single GPU, and for per-rank device timings."""
+
+    def __init__(self, cfg: EngineConfig, nranks: int):
+        self.cfg, self.n = cfg, nranks
+        self.engs = []
+        for r in range(nranks):
+            e = Engine(cfg)
+            e._check(e.lib.gnoc_shard(e._h, r, nranks))
+            self.engs.append(e)
+
+    def submit(self, tr: Trace) -> None:
+        import torch
+        dev = torch.device("cuda", self.cfg.device)
+        self.su, self.ru, self.send, self.recv = [], [], [], []
+        for e in self.engs:
+            e.submit(tr)
+            s = np.zeros(self.n, np.uint64)
+            r = np.zeros(self.n, np.uint64)
+            e._check(e.lib.gnoc_exchange_counts(e._h, s.ctypes.data, r.ctypes.data, self.n))
+            self.su.append([int(v) for v in s])
+            self.ru.append([int(v) for v in r])
+            self.send.append(torch.empty((max(1, int(s.sum())), 4), dtype=torch.int32, device=dev))
+            self.recv.append(torch.empty((max(1, int(r.sum())), 4), dtype=torch.int32, device=dev))
+
+    def exchange(self) -> None:
+        import torch
+        for d in range(self.n):
+            o = 0
+            for r in range(self.n):
+                k = self.ru[d][r]
+                assert k == self.su[r][d], "send/receive sizes disagree"
+                so = sum(self.su[r][:d])
+                self.recv[d][o:o + k].copy_(self.send[r][so:so + k])
+                o += k
+        torch.cuda.synchronize()
+
+    def run(self) -> None:
+        for e, s in zip(self.engs, self.send):
+            e._check(e.lib.gnoc_run_begin(e._h, s.data_ptr()))
+        self.exchange()
+        for e, r in zip(self.engs, self.recv):
+            e._check(e.lib.gnoc_run_finish(e._h, r.data_ptr()))
+
+    def results(self) -> Results:
+        """Whole-mesh results: element-wise sum over ranks."""
+        rs = [e.results() for e in self.engs]
+        f = lambda k: np.sum([getattr(r, k) for r in rs], axis=0, dtype=np.uint64)
+        return Results(f("final_ps"), f("zero_load_ps"), f("contention_ps"), f("port_sum_delay"), f("port_count"),
+                       f("port_mg1"), rs[0].summary)
+
+    def set_profiling(self, on: bool) -> None:
+        for e in self.engs:
+            e.set_profiling(on)
+
+    def close(self) -> None:
+        for e in self.engs:
+            e.close()

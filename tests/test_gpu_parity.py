@@ -208,3 +208,26 @@ def test_engine_paths_agree():
     assert b.summary["engine_path"] == 0
     for k in ("final_ps", "port_sum_delay", "port_count", "port_mg1"):
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
+
+
+@pytest.mark.parametrize("chunk", [64, 200, 400, 800])
+def test_small_chunks_serial_prefix_and_exception_tails(chunk, monkeypatch):
+    """GNOC_CHUNK cuts every port into many chunks: the history tree's serial
+    (M/G/1) prefix, and M/G/1 exception tails whose keys fall before a port's
+    first FIFO record, cross chunk boundaries -- including an empty chunk 0 that
+    must hand the untouched serial state to its successor."""
+    monkeypatch.setenv("GNOC_CHUNK", str(chunk))
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = random_trace(20000, 8, 8, seed=3, max_cycle=300, burst0=400)
+    got, ref = run_both(cfg, tr)
+    assert ref.port_mg1.sum() > 0
+    assert_same(got, ref)
+
+
+@pytest.mark.parametrize("chunk", [128, 512])
+def test_small_chunks_32x32_hotspot(chunk, monkeypatch):
+    monkeypatch.setenv("GNOC_CHUNK", str(chunk))
+    cfg = gnoc.EngineConfig(num_tiles=1024)
+    tr = gnoc.synthetic_trace(32, 32, 0.01, 100, seed=8, hotspot_fraction=0.2, num_hotspots=16)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)

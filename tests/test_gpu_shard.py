@@ -45,3 +45,44 @@ def test_shard_four_ranks():
 
 def test_shard_three_ranks_uneven():
     launch(3, ["shape6", "sat8"])
+
+
+def _local_vs(cfg, tr, n, ref):
+    from graphite_amd import gnoc
+    import numpy as np
+    ss = gnoc.LocalShardSet(cfg, n)
+    ss.submit(tr)
+    ss.run()
+    ss.run()
+    got = ss.results()
+    ss.close()
+    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1"):
+        a, b = getattr(got, k), getattr(ref, k)
+        assert np.array_equal(a, b), f"{k} differs at {n} ranks: first {np.nonzero(a != b)[0][:5]}"
+
+
+@pytest.mark.parametrize("n", [2, 5, 8])
+def test_local_shards_vs_oracle_8x8_saturated(n):
+    """All ranks in one process: M/G/1 tails from the X phase cross ranks."""
+    from graphite_amd import gnoc
+    from oracle import oracle
+    from tests.traces import random_trace
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = random_trace(20000, 8, 8, seed=3, max_cycle=300, burst0=400)
+    ref = oracle.run(cfg, tr)
+    assert ref.port_mg1.sum() > 0
+    _local_vs(cfg, tr, n, ref)
+
+
+@pytest.mark.parametrize("W,n,hot", [(32, 8, 0.0), (32, 7, 0.2), (64, 8, 0.0)])
+def test_local_shards_vs_unsharded(W, n, hot):
+    from graphite_amd import gnoc
+    cfg = gnoc.EngineConfig(num_tiles=W * W)
+    tr = gnoc.synthetic_trace(W, W, 0.005 if W == 32 else 0.002, 300 if W == 32 else 100, seed=4,
+                              hotspot_fraction=hot, num_hotspots=16)
+    e = gnoc.Engine(cfg)
+    e.submit(tr)
+    e.run()
+    ref = e.results()
+    e.close()
+    _local_vs(cfg, tr, n, ref)
