@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-sample-ppt", type=int, default=1000)
     ap.add_argument("--verify", type=int, default=0, help="also check the GPU result vs the oracle (slow)")
-    ap.add_argument("--workload", choices=("auto", "mesh", "sharded", "replicas"), default="auto",
+    ap.add_argument("--workload", choices=("auto", "mesh", "sharded", "replicas", "sweep"), default="auto",
                     help="auto: one 32x32 mesh at N=1, one 64x64 mesh sharded over N ranks at N>1")
     return ap.parse_args()
 
@@ -74,6 +74,8 @@ def main():
     wl = a.workload if a.workload != "auto" else ("mesh" if world == 1 else "sharded")
     if wl == "mesh" and world > 1:
         wl = "replicas"
+    if wl == "sweep":
+        return sweep_bench(a, world, rank, local)
     sharded = wl == "sharded"
     # BASELINE.json configs[1] (32x32, load 0.005) / configs[2] (64x64, load 0.002)
     W = H = a.mesh or (64 if sharded else 32)
@@ -186,6 +188,81 @@ def main():
             line["cpu_baseline"] = cpu_baseline(a, W, H, load, hot)
         print(json.dumps(line), flush=True)
 
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def sweep_points():
+    """BASELINE.json configs[4] / SURVEY.md 8(d) config 5: flit width x router delay
+    x tile width (-> link delay 1..4 at 1 GHz) x offered load = 256 8x8 points."""
+    import itertools
+    from graphite_amd import gnoc
+    out = []
+    for fw, r, tw, load in itertools.product((16, 32, 64, 128), (0, 1, 2, 3), (1.0, 150.0, 250.0, 350.0),
+                                             (0.005, 0.01, 0.015, 0.02)):
+        out.append((gnoc.SweepPoint(fw, r, int(-(-tw // 100)), tw), load))
+    return out
+
+
+def sweep_bench(a, world, rank, local):
+    """Independent sweep points sharded across ranks (no collective on the data
+    path: weak in points); each rank times its slice as ONE batch (gnoc_create_sweep)."""
+    from graphite_amd import gnoc
+    ppt = a.ppt if a.ppt != 10000 else 2000
+    pts = sweep_points()
+    mine = pts[rank::world]
+    base = gnoc.EngineConfig(num_tiles=64, device=local)
+    t0 = time.time()
+    trs = [gnoc.synthetic_trace(8, 8, load, ppt, seed=a.seed + 7919 * i) for i, (_, load) in
+           enumerate(pts) if i % world == rank]
+    gen_s = time.time() - t0
+    eng = gnoc.SweepEngine(base, [q for q, _ in mine])
+    eng.submit(trs)
+    for _ in range(a.warmup):
+        eng.run()
+    summ = eng.summary()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        eng.run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    eng.set_profiling(True)
+    eng.run()
+    kst = eng.kernel_stats()
+    hops, pkts = int(summ["mesh_hops"]), int(summ["routed_packets"])
+    t = torch.tensor([elapsed, float(hops), float(pkts)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:3], op=dist.ReduceOp.SUM)
+        t[0] = tmax[0]
+    if rank == 0:
+        elapsed_max, hops_all = float(t[0]), float(t[1])
+        lv_ms, lv_n = kst.get("k_level", (0.0, 0))
+        alg = hops * BYTES_PER_HOP + pkts * BYTES_PER_PKT
+        ach = alg / (lv_ms * 1e-3) / 1e9 if lv_ms > 0 else 0.0
+        print(json.dumps({
+            "metric": "packet-hops simulated/sec (node) + % HBM roofline, 1024-tile emesh",
+            "value": hops_all * a.steps / elapsed_max, "unit": "packet-hops/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed_max / a.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (synthetic_network.cc uniform_random restated, fixed seeds)",
+            "config": {"workload": f"sweep: {len(pts)} 8x8 points (flit 16-128 x R 0-3 x Lk 1-4 x load "
+                                   f"0.005-0.02), pkts/tile={ppt}", "points_per_rank": len(mine),
+                       "parallelism": f"points/{world}", "mesh_hops": int(hops_all)},
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": "k_level",
+                         "kernel_launches": lv_n, "kernel_avg_us": lv_ms * 1e3 / max(lv_n, 1),
+                         "algorithmic_bytes_per_launch": alg / max(lv_n, 1)},
+            "kernel_ms": {k: round(v[0], 4) for k, v in kst.items()},
+            "trace_gen_s": round(gen_s, 2),
+        }), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()

@@ -63,6 +63,12 @@ struct DevCfg
    int analytical;
    int max_list;
    uint32_t magicW;      // ceil(2^32 / W) style reciprocal for tile -> (x, y)
+   // Design-space sweep (gnoc_create_sweep): the mesh is a BX-wide grid of
+   // independent BW x BH blocks, one per sweep point, each with its own R + Lk
+   // and flit width.  A single mesh is one block (pt_rl == nullptr).
+   uint32_t BW, BH, BX;
+   const uint64_t* pt_rl;   // per point Latency(R + Lk).toPicosec()
+   const uint32_t* pt_fw;   // per point flit width
 };
 
 // Latency::toPicosec, common/misc/time_types.h:81-86.  F1: f == 1.0 exactly,
@@ -91,6 +97,21 @@ __host__ __device__ __forceinline__ void tile_xy(uint32_t tile, uint32_t W, uint
    if (q * W > tile) q--;
    y = q;
    x = tile - q * W;
+}
+
+// Sweep point of a tile, and the per-point delay / flit width (single mesh: the config's).
+__host__ __device__ __forceinline__ uint32_t point_of(const DevCfg& c, uint32_t tile)
+{
+   const uint32_t x = tile % c.W, y = tile / c.W;
+   return (y / c.BH) * c.BX + x / c.BW;
+}
+__host__ __device__ __forceinline__ uint64_t rl_of(const DevCfg& c, uint32_t tile)
+{
+   return c.pt_rl ? c.pt_rl[point_of(c, tile)] : c.rl_ps;
+}
+__host__ __device__ __forceinline__ uint32_t fw_of(const DevCfg& c, uint32_t tile)
+{
+   return c.pt_fw ? c.pt_fw[point_of(c, tile)] : c.flit_width;
 }
 
 // Dimension-ordered XY route step, network_model_emesh_hop_by_hop.cc:229-240.

@@ -114,6 +114,12 @@ struct gnoc_engine
    DevBuf d_xs_pairs, d_xr_pairs, xs_off, xr_off;
    bool begun = false;
 
+   // design-space sweep (gnoc_create_sweep): per-point tables
+   int32_t npoints = 1;
+   std::vector<uint64_t> h_pt_rl;
+   std::vector<uint32_t> h_pt_fw;
+   DevBuf d_pt_rl, d_pt_fw;
+
    // kernel profiling (gnoc_set_profiling)
    bool prof = false;
    std::vector<hipEvent_t> evpool;
@@ -207,23 +213,27 @@ static void build_static_levels(gnoc_engine* e)
    for (uint32_t y = e->ry0; y < e->ry1; y++)
       for (uint32_t x = 0; x < W; x++) P.push_back((y * W + x) * PORTS + P_INJ);
    O.push_back((uint32_t) P.size());
-   for (uint32_t l = 1; l < W; l++)
+   // a sweep mesh is a grid of independent BW x BH blocks: levels by in-block coordinate
+   const uint32_t BW = e->dc.BW, BH = e->dc.BH;
+   for (uint32_t l = 1; l < BW; l++)
    {
       for (uint32_t y = e->ry0; y < e->ry1; y++)
-      {
-         P.push_back((y * W + (l - 1)) * PORTS + P_RIGHT);
-         P.push_back((y * W + (W - l)) * PORTS + P_LEFT);
-      }
+         for (uint32_t b0 = 0; b0 < W; b0 += BW)
+         {
+            P.push_back((y * W + b0 + (l - 1)) * PORTS + P_RIGHT);
+            P.push_back((y * W + b0 + (BW - l)) * PORTS + P_LEFT);
+         }
       O.push_back((uint32_t) P.size());
    }
    e->lvl_y0 = (uint32_t) O.size() - 1;
-   for (uint32_t k = 0; k + 1 < H; k++)
+   for (uint32_t k = 0; k + 1 < BH; k++)
    {
-      for (uint32_t x = e->cx0; x < e->cx1; x++)
-      {
-         P.push_back((k * W + x) * PORTS + P_UP);
-         P.push_back(((H - 1 - k) * W + x) * PORTS + P_DOWN);
-      }
+      for (uint32_t b0 = 0; b0 < H; b0 += BH)
+         for (uint32_t x = e->cx0; x < e->cx1; x++)
+         {
+            P.push_back(((b0 + k) * W + x) * PORTS + P_UP);
+            P.push_back(((b0 + BH - 1 - k) * W + x) * PORTS + P_DOWN);
+         }
       O.push_back((uint32_t) P.size());
    }
    for (uint32_t y = 0; y < H; y++)
@@ -310,6 +320,11 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    d.analytical = c.analytical_enabled;
    d.max_list = c.max_list_size;
    d.magicW = d.W == 1 ? 0xFFFFFFFFu : (uint32_t) ((1ull << 32) / d.W);
+   d.BW = d.W;
+   d.BH = d.H;
+   d.BX = 1;
+   d.pt_rl = nullptr;
+   d.pt_fw = nullptr;
    build_static_levels(e);
 
    hipError_t he = hipSetDevice(c.device);
@@ -331,6 +346,83 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
       return GNOC_EHIP;
    }
    *out = e;
+   return GNOC_OK;
+}
+
+int gnoc_create_sweep(const gnoc_config* base, const gnoc_point* points, int32_t npoints, gnoc_engine** out)
+{
+   if (!base || !points || !out || npoints < 1) return GNOC_EINVAL;
+   *out = nullptr;
+   gnoc_config b = *base;
+   if (b.mesh_width <= 0 || b.mesh_height <= 0)
+   {
+      if (b.num_tiles <= 0) return GNOC_EINVAL;
+      b.mesh_width = (int32_t) std::floor(std::sqrt((double) b.num_tiles));
+      b.mesh_height = (int32_t) std::ceil(1.0 * b.num_tiles / b.mesh_width);
+   }
+   if (b.num_tiles <= 0) b.num_tiles = b.mesh_width * b.mesh_height;
+   if (b.num_tiles != b.mesh_width * b.mesh_height) return GNOC_EINVAL;
+   if (b.frequency_ghz != 1.0 || b.max_list_size < 3) return GNOC_EUNSUPPORTED;   // the chunked path
+   std::vector<uint64_t> rl((size_t) npoints);
+   std::vector<uint32_t> fw((size_t) npoints);
+   for (int32_t p = 0; p < npoints; p++)
+   {
+      const gnoc_point& q = points[p];
+      if (q.flit_width <= 0) return GNOC_EINVAL;
+      // each point's own link delay identity (emesh_hop_by_hop.cc:126, electrical_link_model.cc:13-16)
+      if ((uint64_t) std::ceil(b.frequency_ghz * 0.01 * q.tile_width_mm) != q.link_delay) return GNOC_EINVAL;
+      if (q.router_delay + q.link_delay == 0) return GNOC_EINVAL;
+      rl[p] = ps_of<true>(q.router_delay + q.link_delay, 1.0);
+      fw[p] = (uint32_t) q.flit_width;
+   }
+   // blocks laid out BX wide, BY high (unused trailing blocks carry no packets)
+   int32_t BX = (int32_t) std::ceil(std::sqrt((double) npoints));
+   const int32_t BY = (npoints + BX - 1) / BX;
+   for (int32_t p = npoints; p < BX * BY; p++) { rl.push_back(rl[0]); fw.push_back(fw[0]); }
+   gnoc_config u = b;
+   u.mesh_width = BX * b.mesh_width;
+   u.mesh_height = BY * b.mesh_height;
+   u.num_tiles = u.mesh_width * u.mesh_height;
+   u.flit_width = points[0].flit_width;
+   u.router_delay = points[0].router_delay;
+   u.link_delay = points[0].link_delay;
+   u.tile_width_mm = points[0].tile_width_mm;
+   gnoc_engine* e = nullptr;
+   int rc = gnoc_create(&u, &e);
+   if (rc) return rc;
+   e->npoints = npoints;
+   e->h_pt_rl = rl;
+   e->h_pt_fw = fw;
+   e->dc.BW = (uint32_t) b.mesh_width;
+   e->dc.BH = (uint32_t) b.mesh_height;
+   e->dc.BX = (uint32_t) BX;
+   hipError_t he = e->d_pt_rl.ensure(rl.size() * 8);
+   if (he == hipSuccess) he = e->d_pt_fw.ensure(fw.size() * 4);
+   if (he == hipSuccess) he = hipMemcpy(e->d_pt_rl.p, rl.data(), rl.size() * 8, hipMemcpyHostToDevice);
+   if (he == hipSuccess) he = hipMemcpy(e->d_pt_fw.p, fw.data(), fw.size() * 4, hipMemcpyHostToDevice);
+   if (he != hipSuccess)
+   {
+      gnoc_destroy(e);
+      return GNOC_EHIP;
+   }
+   e->dc.pt_rl = e->d_pt_rl.as<uint64_t>();
+   e->dc.pt_fw = e->d_pt_fw.as<uint32_t>();
+   build_static_levels(e);
+   he = upload_levels(e);
+   if (he != hipSuccess)
+   {
+      gnoc_destroy(e);
+      return GNOC_EHIP;
+   }
+   *out = e;
+   return GNOC_OK;
+}
+
+int gnoc_sweep_layout(const gnoc_engine* e, int32_t* blocks_x, int32_t* blocks_y)
+{
+   if (!e) return GNOC_EINVAL;
+   if (blocks_x) *blocks_x = (int32_t) e->dc.BX;
+   if (blocks_y) *blocks_y = (int32_t) (e->dc.H / e->dc.BH);
    return GNOC_OK;
 }
 
@@ -356,6 +448,11 @@ static uint64_t record_bound(const gnoc_engine* e, uint64_t records)
    return records + 64ull * ((uint64_t) e->dc.N * PORTS * INS) + 64;
 }
 
+static uint32_t fw_host(const gnoc_engine* e, uint32_t tile)
+{
+   return e->npoints > 1 ? e->h_pt_fw[point_of(e->dc, tile)] : (uint32_t) e->cfg.flit_width;
+}
+
 static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n, uint64_t* records)
 {
    const uint32_t N = e->dc.N, W = e->dc.W, H = e->dc.H;
@@ -374,7 +471,10 @@ static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n,
       const uint32_t s = pk->src[i], d = pk->dst[i];
       if (s >= N || d >= N) return fail(e, GNOC_ETRACE, "tile id out of range at packet " + std::to_string(i));
       if (i && pk->inject_ps[i] < pk->inject_ps[i - 1]) return fail(e, GNOC_ETRACE, "trace not ordered by inject_ps at packet " + std::to_string(i));
-      const uint32_t F = (pk->bits[i] + (uint32_t) e->cfg.flit_width - 1) / (uint32_t) e->cfg.flit_width;
+      const uint32_t fw = fw_host(e, s);
+      const uint32_t F = (pk->bits[i] + fw - 1) / fw;
+      if (e->npoints > 1 && point_of(e->dc, s) != point_of(e->dc, d))
+         return fail(e, GNOC_ETRACE, "sweep packet crosses sweep points at packet " + std::to_string(i));
       const bool bypass = s == d || (pk->flags && (pk->flags[i] & GNOC_PKT_UNMODELED));
       if (F == 0 && !bypass) return fail(e, GNOC_ETRACE, "zero-flit packet " + std::to_string(i));
       if (F > AUX_F_MAX) return fail(e, GNOC_EUNSUPPORTED, "packet longer than 4095 flits");
@@ -767,11 +867,12 @@ static int run_prep(gnoc_engine* e, bool* done)
    }
 
    const uint32_t ng = (N + 255) / 256;
-   GNOC_LAUNCH(e, KC_SRC_TOT, k_src_tot, dim3(ng), dim3(256), 0, s, N, nch, e->hist.as<uint32_t>(), e->tot.as<uint32_t>());
+   GNOC_LAUNCH(e, KC_SRC_TOT, k_src_tot, dim3(ng), dim3(256), 0, s, N, nch, e->hist.as<uint32_t>(), e->tot.as<uint32_t>(),
+               pr0 * W, pr1 * W);
    GNOC_LAUNCH(e, KC_INJ_BASE, k_inj_base, dim3(1), dim3(1024), 0, s, N, e->tot.as<uint32_t>(), e->slot_cnt.as<uint32_t>(),
                e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>());
    GNOC_LAUNCH(e, KC_SRC_OFFS, k_src_offs, dim3(ng), dim3(256), 0, s, N, nch, e->hist.as<uint32_t>(),
-               e->slot_base.as<uint64_t>());
+               e->slot_base.as<uint64_t>(), pr0 * W, pr1 * W);
    if (n && N <= SC4_MAXN)
       GNOC_LAUNCH(e, KC_SCATTER, k_scatter4, dim3(nch), dim3(256), 4 * N * 4, s, (uint64_t) n, pch, N, nbits, e->d_src,
                   e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(), e->recs.as<Rec>(),
@@ -903,6 +1004,7 @@ int gnoc_shard(gnoc_engine* e, int32_t rank, int32_t nranks)
    if (!e) return GNOC_EINVAL;
    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(e, GNOC_EINVAL, "bad rank / nranks");
    if ((uint32_t) nranks > std::min(e->dc.W, e->dc.H)) return fail(e, GNOC_EINVAL, "more ranks than mesh rows or columns");
+   if (nranks > 1 && e->npoints > 1) return fail(e, GNOC_EUNSUPPORTED, "a sweep shards by points (one engine per rank)");
    if (nranks > 1 && e->dc.contention && !(e->f1 && e->dc.max_list >= 3))
       return fail(e, GNOC_EUNSUPPORTED, "sharding needs the chunked path (f = 1 GHz, max_list_size >= 3)");
    e->rank = rank;
@@ -997,6 +1099,13 @@ int gnoc_get_packet_results(gnoc_engine* e, uint64_t* final_ps, uint64_t* zero_l
    if (n != e->n) return fail(e, GNOC_EINVAL, "result array length != submitted packet count");
    if (!n) return GNOC_OK;
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   if (e->nranks > 1)
+   {
+      hipLaunchKernelGGL(k_mask_unowned, dim3((uint32_t) std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0, e->stream,
+                         (uint64_t) n, e->aux.as<uint32_t>(), e->cx0, e->cx1, e->final_ps.as<uint64_t>(),
+                         e->zl.as<uint64_t>(), e->cont.as<uint64_t>());
+      GNOC_HIP(e, hipGetLastError());
+   }
    if (final_ps) GNOC_HIP(e, hipMemcpyAsync(final_ps, e->final_ps.p, n * 8, hipMemcpyDeviceToHost, e->stream));
    if (zero_load_ps) GNOC_HIP(e, hipMemcpyAsync(zero_load_ps, e->zl.p, n * 8, hipMemcpyDeviceToHost, e->stream));
    if (contention_ps) GNOC_HIP(e, hipMemcpyAsync(contention_ps, e->cont.p, n * 8, hipMemcpyDeviceToHost, e->stream));

@@ -464,7 +464,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
             const uint64_t cc = sm.m_c[e];
             st_sum += cc;
             st_cnt++;
-            const uint64_t tn = t + ps_of<F1>(cc, c.f) + (dir == P_INJ ? 0ull : c.rl_ps);
+            const uint64_t tn = t + ps_of<F1>(cc, c.f) + (dir == P_INJ ? 0ull : rl_of(c, tile));
             if (dir == P_SELF)
             {
                final_ps[id] = tn + ps_of<F1>(aux_F(ax), c.f);
@@ -526,18 +526,34 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
    for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
    {
       const uint32_t dx = aux_dx(aux[i]), dy = aux_dy(aux[i]);
-      // a sharded engine delivers the packets of its column band (shard.hip); others read 0
-      if (dx < cx0 || dx >= cx1) { final_ps[i] = 0; zl[i] = 0; cont[i] = 0; continue; }
+      // a sharded engine delivers the packets of its column band (shard.hip); the
+      // others are zeroed when results are read (k_mask_unowned), not here
+      if (dx < cx0 || dx >= cx1) continue;
       if (!(routed[i] & 1)) { zl[i] = 0; cont[i] = 0; continue; }
       uint32_t sx, sy;
       tile_xy(src[i], c.W, c.magicW, sx, sy);
       const uint64_t hops = (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
       // Hop::Hop accumulates Latency(0) at injection, Latency(R+Lk) per mesh router,
       // Latency(F) at receive (network_model.cc:142-150, 556-563).
-      const uint64_t z = ps_of<F1>(0, c.f) + hops * c.rl_ps + ps_of<F1>(aux_F(aux[i]), c.f);
+      const uint64_t z = ps_of<F1>(0, c.f) + hops * rl_of(c, src[i]) + ps_of<F1>(aux_F(aux[i]), c.f);
       zl[i] = z;
       if (closed_form) final_ps[i] = inj[i] + z;
       cont[i] = final_ps[i] - inj[i] - z;
+   }
+}
+
+// Results of packets another rank delivers read 0 (gnoc_get_packet_results).
+__global__ __launch_bounds__(256) void k_mask_unowned(uint64_t n, const uint32_t* __restrict__ aux, uint32_t cx0,
+                                                      uint32_t cx1, uint64_t* __restrict__ final_ps,
+                                                      uint64_t* __restrict__ zl, uint64_t* __restrict__ cont)
+{
+   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const uint32_t dx = aux_dx(aux[i]);
+      if (dx >= cx0 && dx < cx1) continue;
+      final_ps[i] = 0;
+      zl[i] = 0;
+      cont[i] = 0;
    }
 }
 

@@ -70,7 +70,7 @@ struct __attribute__((aligned(16))) PortIO3
    uint32_t nx, ny, gbase, nc;
    uint32_t prod[LV_IN];     // plan index of each input's producer port (LV_NO_PROD: the trace)
    uint32_t prod_nc[LV_IN];  // that producer's chunk count: complete when done[prod] == prod_nc
-   uint32_t pk, pad0, pad1, pad2;  // plan index of the port itself
+   uint32_t pk, rl, pad1, pad2;    // plan index of the port itself; R + Lk of its tile (ps)
 };
 static_assert(sizeof(PortIO3) % 16 == 0, "PortIO3 copy granularity");
 constexpr uint32_t LV_NO_PROD = 0xFFFFFFFFu;
@@ -650,7 +650,7 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
    {
       const uint32_t E = sm.E;
       const uint32_t dir = sm.io.dir, nx = sm.io.nx, ny = sm.io.ny;
-      const uint64_t rl = dir == P_INJ ? 0ull : c.rl_ps;
+      const uint64_t rl = dir == P_INJ ? 0ull : (uint64_t) sm.io.rl;
       SerialState s;
       s.X = sm.cy.X; s.g = (int) sm.cy.g; s.mode = 1; s.s1 = sm.cy.s1; s.s2 = sm.cy.s2;
       s.narr = sm.cy.narr; s.newest = sm.cy.newest; s.mg1 = 0;
@@ -705,7 +705,7 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
 {
    const uint32_t lane = threadIdx.x & 63;
    const uint32_t dir = sm.io.dir, nx = sm.io.nx, ny = sm.io.ny;
-   const uint64_t rl = dir == P_INJ ? 0ull : c.rl_ps;
+   const uint64_t rl = dir == P_INJ ? 0ull : (uint64_t) sm.io.rl;
    const uint64_t X0 = sm.cy.X;
    uint64_t X = X0 + so.eA;
    X = X > so.eB ? X : so.eB;
@@ -1498,7 +1498,8 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
    io.gbase = 0;
    io.nc = 0;     // k_plan_scan decides, k_plan_expand writes
    io.pk = k;
-   io.pad0 = io.pad1 = io.pad2 = 0;
+   io.rl = (uint32_t) rl_of(c, tile);
+   io.pad1 = io.pad2 = 0;
    pio[k] = io;
    pnc[k] = tot;  // records of the port (k_plan_scan turns it into a chunk count)
 }

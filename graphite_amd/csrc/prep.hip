@@ -48,7 +48,8 @@ __global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, uint32_t
       const uint32_t s = src[i], d = dst[i];
       const uint32_t fl = flags ? flags[i] : 0u;
       const uint32_t b = bits[i];
-      const uint32_t F = (b % c.flit_width) ? b / c.flit_width + 1 : b / c.flit_width;
+      const uint32_t fw = fw_of(c, s);
+      const uint32_t F = (b % fw) ? b / fw + 1 : b / fw;
       const bool bypass = (s == d) || (fl & 1u);
       uint32_t sx, sy, dx, dy;
       tile_xy(s, c.W, c.magicW, sx, sy);
@@ -99,11 +100,13 @@ __global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, uint32_t
 // ---------------------------------------------------------------------------
 // 2. injection-slot layout
 // ---------------------------------------------------------------------------
+// Sources outside [s0, s1) (another rank's row band) have no injection records here.
 __global__ __launch_bounds__(256) void k_src_tot(uint32_t N, uint32_t nch, const uint32_t* __restrict__ hist,
-                                                 uint32_t* __restrict__ tot)
+                                                 uint32_t* __restrict__ tot, uint32_t s0, uint32_t s1)
 {
    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
    if (s >= N) return;
+   if (s < s0 || s >= s1) { tot[s] = 0; return; }
    uint32_t t = 0;
 #pragma unroll 16
    for (uint32_t ch = 0; ch < nch; ch++) t += hist[(uint64_t) ch * N + s];
@@ -142,10 +145,10 @@ __global__ __launch_bounds__(1024) void k_inj_base(uint32_t N, const uint32_t* _
 
 // hist[ch][s] (counts) -> absolute record offsets of chunk ch's first record of source s.
 __global__ __launch_bounds__(256) void k_src_offs(uint32_t N, uint32_t nch, uint32_t* __restrict__ hist,
-                                                  const uint64_t* __restrict__ slot_base)
+                                                  const uint64_t* __restrict__ slot_base, uint32_t s0, uint32_t s1)
 {
    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-   if (s >= N) return;
+   if (s >= N || s < s0 || s >= s1) return;
    uint32_t run = (uint32_t) slot_base[slot_of(s, P_INJ, IN_LOCAL)];   // < 2^32 records (checked at submit)
 #pragma unroll 16
    for (uint32_t ch = 0; ch < nch; ch++)
@@ -257,7 +260,8 @@ __global__ __launch_bounds__(256) void k_scatter4(uint64_t n, uint32_t pch, uint
    bool nv = false;
    uint32_t ns = 0, na = 0;
    uint64_t nt = 0;
-   if (i < hi) { nv = (routed[i] & 2) != 0; ns = src[i]; nt = inj[i]; na = aux[i]; }   // independent loads
+   if (i < hi) { nv = (routed[i] & 2) != 0; ns = src[i]; }
+   if (nv) { nt = inj[i]; na = aux[i]; }   // a sharded rank places only its row band's packets
    for (uint64_t k = lo; k < hi; k += 64)
    {
       const bool valid = nv;
@@ -267,7 +271,8 @@ __global__ __launch_bounds__(256) void k_scatter4(uint64_t n, uint32_t pch, uint
       const uint64_t id = k + lane;
       const uint64_t i2 = k + 64 + lane;
       nv = false;
-      if (i2 < hi) { nv = (routed[i2] & 2) != 0; ns = src[i2]; nt = inj[i2]; na = aux[i2]; }
+      if (i2 < hi) { nv = (routed[i2] & 2) != 0; ns = src[i2]; }
+      if (nv) { nt = inj[i2]; na = aux[i2]; }
       if (!nv) ns = 0;
       const uint64_t m = match_mask(sidx, valid, nbits);
       const uint32_t old = valid ? hw[sidx] : 0u;
@@ -356,61 +361,63 @@ __global__ __launch_bounds__(256) void k_slot_counts(DevCfg c, const uint32_t* _
                                                      const uint32_t* __restrict__ Prow, uint32_t* __restrict__ slot_cnt)
 {
    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-   const uint32_t W = c.W, H = c.H, N = c.N;
+   const uint32_t W = c.W, N = c.N;
    if (k >= N * 5) return;
    const uint32_t tile = k / 5, dir = k % 5;
    const uint32_t x = tile % W, y = tile / W;
+   // a sweep mesh's packets stay inside their BW x BH block
+   const uint32_t bx0 = x / c.BW * c.BW, bx1 = bx0 + c.BW, by0 = y / c.BH * c.BH, by1 = by0 + c.BH;
    auto hs = [&](uint32_t sx, uint32_t sy, uint32_t dx, uint32_t cl) -> uint32_t {
       return Hs[((uint64_t) (sy * W + sx) * W + dx) * 3 + cl];
    };
    auto prow = [&](uint32_t sy, uint32_t dx, uint32_t dy) -> uint32_t { return Prow[(uint64_t) sy * N + dy * W + dx]; };
    uint32_t cl = 0, cw = 0, ce = 0, cs = 0, cn = 0;
    // IN_LOCAL: packets injected here whose first hop leaves through `dir`
-   if (dir == P_RIGHT) { for (uint32_t dx = x + 1; dx < W; dx++) cl += hs(x, y, dx, 0) + hs(x, y, dx, 1) + hs(x, y, dx, 2); }
-   else if (dir == P_LEFT) { for (uint32_t dx = 0; dx < x; dx++) cl += hs(x, y, dx, 0) + hs(x, y, dx, 1) + hs(x, y, dx, 2); }
+   if (dir == P_RIGHT) { for (uint32_t dx = x + 1; dx < bx1; dx++) cl += hs(x, y, dx, 0) + hs(x, y, dx, 1) + hs(x, y, dx, 2); }
+   else if (dir == P_LEFT) { for (uint32_t dx = bx0; dx < x; dx++) cl += hs(x, y, dx, 0) + hs(x, y, dx, 1) + hs(x, y, dx, 2); }
    else if (dir == P_UP) cl = hs(x, y, x, 2);
    else if (dir == P_DOWN) cl = hs(x, y, x, 0);
    // IN_W: X leg moving right through x (sx < x <= dx) in row y
    if (dir == P_RIGHT)
    {
-      for (uint32_t sx = 0; sx < x; sx++)
-         for (uint32_t dx = x + 1; dx < W; dx++) cw += hs(sx, y, dx, 0) + hs(sx, y, dx, 1) + hs(sx, y, dx, 2);
+      for (uint32_t sx = bx0; sx < x; sx++)
+         for (uint32_t dx = x + 1; dx < bx1; dx++) cw += hs(sx, y, dx, 0) + hs(sx, y, dx, 1) + hs(sx, y, dx, 2);
    }
    else if (dir != P_LEFT)
    {
       const uint32_t want = dir == P_UP ? 2u : dir == P_DOWN ? 0u : 1u;
-      for (uint32_t sx = 0; sx < x; sx++) cw += hs(sx, y, x, want);
+      for (uint32_t sx = bx0; sx < x; sx++) cw += hs(sx, y, x, want);
    }
    // IN_E: X leg moving left (dx <= x < sx)
    if (dir == P_LEFT)
    {
-      for (uint32_t sx = x + 1; sx < W; sx++)
-         for (uint32_t dx = 0; dx < x; dx++) ce += hs(sx, y, dx, 0) + hs(sx, y, dx, 1) + hs(sx, y, dx, 2);
+      for (uint32_t sx = x + 1; sx < bx1; sx++)
+         for (uint32_t dx = bx0; dx < x; dx++) ce += hs(sx, y, dx, 0) + hs(sx, y, dx, 1) + hs(sx, y, dx, 2);
    }
    else if (dir != P_RIGHT)
    {
       const uint32_t want = dir == P_UP ? 2u : dir == P_DOWN ? 0u : 1u;
-      for (uint32_t sx = x + 1; sx < W; sx++) ce += hs(sx, y, x, want);
+      for (uint32_t sx = x + 1; sx < bx1; sx++) ce += hs(sx, y, x, want);
    }
    // IN_S: Y leg moving up in column x (sy < y <= dy)
    if (dir == P_UP)
    {
-      for (uint32_t sy = 0; sy < y; sy++)
-         for (uint32_t dy = y + 1; dy < H; dy++) cs += prow(sy, x, dy);
+      for (uint32_t sy = by0; sy < y; sy++)
+         for (uint32_t dy = y + 1; dy < by1; dy++) cs += prow(sy, x, dy);
    }
    else if (dir == P_SELF)
    {
-      for (uint32_t sy = 0; sy < y; sy++) cs += prow(sy, x, y);
+      for (uint32_t sy = by0; sy < y; sy++) cs += prow(sy, x, y);
    }
    // IN_N: Y leg moving down (dy <= y < sy)
    if (dir == P_DOWN)
    {
-      for (uint32_t sy = y + 1; sy < H; sy++)
-         for (uint32_t dy = 0; dy < y; dy++) cn += prow(sy, x, dy);
+      for (uint32_t sy = y + 1; sy < by1; sy++)
+         for (uint32_t dy = by0; dy < y; dy++) cn += prow(sy, x, dy);
    }
    else if (dir == P_SELF)
    {
-      for (uint32_t sy = y + 1; sy < H; sy++) cn += prow(sy, x, y);
+      for (uint32_t sy = y + 1; sy < by1; sy++) cn += prow(sy, x, y);
    }
    slot_cnt[slot_of(tile, dir, IN_LOCAL)] = cl;
    slot_cnt[slot_of(tile, dir, IN_W)] = cw;
@@ -434,30 +441,31 @@ __global__ __launch_bounds__(256) void k_slot_counts_x(DevCfg c, const uint32_t*
    for (uint32_t q = threadIdx.x; q < W * 5; q += blockDim.x)
    {
       const uint32_t x = q / 5, dir = q % 5, tile = y * W + x;
+      const uint32_t bx0 = x / c.BW * c.BW, bx1 = bx0 + c.BW;
       uint32_t cl = 0, cw = 0, ce = 0;
-      if (dir == P_RIGHT) { for (uint32_t dx = x + 1; dx < W; dx++) cl += hs(x, dx, 0) + hs(x, dx, 1) + hs(x, dx, 2); }
-      else if (dir == P_LEFT) { for (uint32_t dx = 0; dx < x; dx++) cl += hs(x, dx, 0) + hs(x, dx, 1) + hs(x, dx, 2); }
+      if (dir == P_RIGHT) { for (uint32_t dx = x + 1; dx < bx1; dx++) cl += hs(x, dx, 0) + hs(x, dx, 1) + hs(x, dx, 2); }
+      else if (dir == P_LEFT) { for (uint32_t dx = bx0; dx < x; dx++) cl += hs(x, dx, 0) + hs(x, dx, 1) + hs(x, dx, 2); }
       else if (dir == P_UP) cl = hs(x, x, 2);
       else if (dir == P_DOWN) cl = hs(x, x, 0);
       if (dir == P_RIGHT)
       {
-         for (uint32_t sx = 0; sx < x; sx++)
-            for (uint32_t dx = x + 1; dx < W; dx++) cw += hs(sx, dx, 0) + hs(sx, dx, 1) + hs(sx, dx, 2);
+         for (uint32_t sx = bx0; sx < x; sx++)
+            for (uint32_t dx = x + 1; dx < bx1; dx++) cw += hs(sx, dx, 0) + hs(sx, dx, 1) + hs(sx, dx, 2);
       }
       else if (dir != P_LEFT)
       {
          const uint32_t want = dir == P_UP ? 2u : dir == P_DOWN ? 0u : 1u;
-         for (uint32_t sx = 0; sx < x; sx++) cw += hs(sx, x, want);
+         for (uint32_t sx = bx0; sx < x; sx++) cw += hs(sx, x, want);
       }
       if (dir == P_LEFT)
       {
-         for (uint32_t sx = x + 1; sx < W; sx++)
-            for (uint32_t dx = 0; dx < x; dx++) ce += hs(sx, dx, 0) + hs(sx, dx, 1) + hs(sx, dx, 2);
+         for (uint32_t sx = x + 1; sx < bx1; sx++)
+            for (uint32_t dx = bx0; dx < x; dx++) ce += hs(sx, dx, 0) + hs(sx, dx, 1) + hs(sx, dx, 2);
       }
       else if (dir != P_RIGHT)
       {
          const uint32_t want = dir == P_UP ? 2u : dir == P_DOWN ? 0u : 1u;
-         for (uint32_t sx = x + 1; sx < W; sx++) ce += hs(sx, x, want);
+         for (uint32_t sx = x + 1; sx < bx1; sx++) ce += hs(sx, x, want);
       }
       slot_cnt[slot_of(tile, dir, IN_LOCAL)] = cl;
       slot_cnt[slot_of(tile, dir, IN_W)] = cw;
@@ -482,24 +490,25 @@ __global__ __launch_bounds__(256) void k_slot_counts_y(DevCfg c, const uint32_t*
    for (uint32_t q = threadIdx.x; q < H * 5; q += blockDim.x)
    {
       const uint32_t y = q / 5, dir = q % 5, tile = y * W + x;
+      const uint32_t by0 = y / c.BH * c.BH, by1 = by0 + c.BH;
       uint32_t cs = 0, cn = 0;
       if (dir == P_UP)
       {
-         for (uint32_t sy = 0; sy < y; sy++)
-            for (uint32_t dy = y + 1; dy < H; dy++) cs += pc[sy * H + dy];
+         for (uint32_t sy = by0; sy < y; sy++)
+            for (uint32_t dy = y + 1; dy < by1; dy++) cs += pc[sy * H + dy];
       }
       else if (dir == P_SELF)
       {
-         for (uint32_t sy = 0; sy < y; sy++) cs += pc[sy * H + y];
+         for (uint32_t sy = by0; sy < y; sy++) cs += pc[sy * H + y];
       }
       if (dir == P_DOWN)
       {
-         for (uint32_t sy = y + 1; sy < H; sy++)
-            for (uint32_t dy = 0; dy < y; dy++) cn += pc[sy * H + dy];
+         for (uint32_t sy = y + 1; sy < by1; sy++)
+            for (uint32_t dy = by0; dy < y; dy++) cn += pc[sy * H + dy];
       }
       else if (dir == P_SELF)
       {
-         for (uint32_t sy = y + 1; sy < H; sy++) cn += pc[sy * H + y];
+         for (uint32_t sy = y + 1; sy < by1; sy++) cn += pc[sy * H + y];
       }
       slot_cnt[slot_of(tile, dir, IN_S)] = cs;
       slot_cnt[slot_of(tile, dir, IN_N)] = cn;

@@ -35,6 +35,7 @@ EXPORTED = (
     "gnoc_last_error", "gnoc_destroy", "gnoc_trace_synthetic", "gnoc_abi_version",
     "gnoc_set_profiling", "gnoc_get_kernel_stats", "gnoc_trace_file_write", "gnoc_trace_file_read",
     "gnoc_shard", "gnoc_exchange_counts", "gnoc_run_begin", "gnoc_run_finish",
+    "gnoc_create_sweep", "gnoc_sweep_layout",
 )
 
 
@@ -54,6 +55,15 @@ class GnocConfig(ctypes.Structure):
         ("max_list_size", ctypes.c_int32),
         ("broadcast_tree_enabled", ctypes.c_int32),
         ("device", ctypes.c_int32),
+    ]
+
+
+class GnocPoint(ctypes.Structure):
+    _fields_ = [
+        ("flit_width", ctypes.c_int32),
+        ("router_delay", ctypes.c_uint64),
+        ("link_delay", ctypes.c_uint64),
+        ("tile_width_mm", ctypes.c_double),
     ]
 
 
@@ -119,6 +129,9 @@ def load() -> ctypes.CDLL:
     lib.gnoc_set_profiling.argtypes = [vp, ctypes.c_int]
     lib.gnoc_get_kernel_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(ctypes.c_uint32), sz, ctypes.POINTER(sz)]
+    lib.gnoc_create_sweep.argtypes = [ctypes.POINTER(GnocConfig), ctypes.POINTER(GnocPoint), ctypes.c_int32,
+                                      ctypes.POINTER(vp)]
+    lib.gnoc_sweep_layout.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
     lib.gnoc_shard.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
     lib.gnoc_exchange_counts.argtypes = [vp, vp, vp, sz]
     lib.gnoc_run_begin.argtypes = [vp, vp]
@@ -484,3 +497,109 @@ class LocalShardSet:
     def close(self) -> None:
         for e in self.engs:
             e.close()
+
+
+# ---------------------------------------------------------------------------
+# design-space sweep (gnoc_create_sweep)
+# ---------------------------------------------------------------------------
+@dataclass
+class SweepPoint:
+    """The per-point carbon_sim.cfg keys a sweep varies."""
+    flit_width: int = 64
+    router_delay: int = 1
+    link_delay: int = 1
+    tile_width_mm: float = 1.0
+
+    def config(self, base: EngineConfig) -> EngineConfig:
+        """This point as a stand-alone engine / oracle configuration."""
+        from dataclasses import replace
+        return replace(base, flit_width=self.flit_width, router_delay=self.router_delay,
+                       link_delay=self.link_delay, tile_width_mm=self.tile_width_mm)
+
+
+def sweep_global_tile(p, t, W, H, bx):
+    """G(p, t) of include/gnoc.h: local tile t of point p in the blocks_x-wide block grid."""
+    p = np.asarray(p, np.int64)
+    t = np.asarray(t, np.int64)
+    return ((p // bx) * H + t // W) * (bx * W) + (p % bx) * W + t % W
+
+
+def sweep_merge(traces, W, H, bx):
+    """(merged Trace with global tiles, order): the (inject_ps, point, id)-ordered
+    merge; order[k] = (point, local id) of merged packet k as two arrays."""
+    pts = np.concatenate([np.full(len(t), i, np.int64) for i, t in enumerate(traces)]) if traces else np.zeros(0, np.int64)
+    lid = np.concatenate([np.arange(len(t), dtype=np.int64) for t in traces]) if traces else np.zeros(0, np.int64)
+    trs = [t.normalized() for t in traces]
+    inj = np.concatenate([t.inject_ps for t in trs]) if trs else np.zeros(0, np.uint64)
+    order = np.lexsort((lid, pts, inj))
+    p, l = pts[order], lid[order]
+    src = np.concatenate([t.src for t in trs])[order] if trs else np.zeros(0, np.uint32)
+    dst = np.concatenate([t.dst for t in trs])[order] if trs else np.zeros(0, np.uint32)
+    bits = np.concatenate([t.bits for t in trs])[order] if trs else np.zeros(0, np.uint32)
+    flags = np.concatenate([t.flags for t in trs])[order] if trs else np.zeros(0, np.uint32)
+    merged = Trace(inj[order], sweep_global_tile(p, src, W, H, bx).astype(np.uint32),
+                   sweep_global_tile(p, dst, W, H, bx).astype(np.uint32), bits, flags)
+    return merged, (p, l)
+
+
+class SweepEngine:
+    """Many independent design points timed in one batch on one GPU (one engine
+    per rank; ranks take disjoint slices of the points -- no collective)."""
+
+    def __init__(self, base: EngineConfig, points):
+        self.lib = load()
+        self.base, self.points = base, list(points)
+        self.W, self.H = base.width, base.height
+        arr = (GnocPoint * len(self.points))(*[GnocPoint(q.flit_width, q.router_delay, q.link_delay, q.tile_width_mm)
+                                                for q in self.points])
+        self._h = ctypes.c_void_p()
+        c = base.to_c()
+        rc = self.lib.gnoc_create_sweep(ctypes.byref(c), arr, len(self.points), ctypes.byref(self._h))
+        if rc:
+            raise GnocError(rc, "gnoc_create_sweep rejected the configuration")
+        bx, by = ctypes.c_int32(), ctypes.c_int32()
+        self._check(self.lib.gnoc_sweep_layout(self._h, ctypes.byref(bx), ctypes.byref(by)))
+        self.bx, self.by = bx.value, by.value
+        self._n = 0
+
+    _check = Engine._check
+    close = Engine.close
+    run = Engine.run
+    summary = Engine.summary
+    set_profiling = Engine.set_profiling
+    kernel_stats = Engine.kernel_stats
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def submit(self, traces) -> None:
+        assert len(traces) == len(self.points)
+        merged, (self._pt, self._lid) = sweep_merge(traces, self.W, self.H, self.bx)
+        self._counts = [len(t) for t in traces]
+        tr = merged.normalized()
+        pk = GnocPackets(tr.inject_ps.ctypes.data, tr.src.ctypes.data, tr.dst.ctypes.data, tr.bits.ctypes.data,
+                         tr.flags.ctypes.data)
+        self._check(self.lib.gnoc_submit(self._h, ctypes.byref(pk), len(tr)))
+        self._n = len(tr)
+
+    def results(self):
+        """One Results per point, in the point's own packet and port numbering."""
+        n = self._n
+        fin, zl, ct = (np.empty(n, np.uint64) for _ in range(3))
+        self._check(self.lib.gnoc_get_packet_results(self._h, fin.ctypes.data, zl.ctypes.data, ct.ctypes.data, n))
+        npt = self.bx * self.W * self.by * self.H * PORTS_PER_TILE
+        ps, pc, pm = (np.empty(npt, np.uint64) for _ in range(3))
+        self._check(self.lib.gnoc_get_port_stats(self._h, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data, npt))
+        out = []
+        tiles = np.arange(self.W * self.H)
+        for p, cnt in enumerate(self._counts):
+            m = self._pt == p
+            idx = np.empty(cnt, np.int64)
+            idx[self._lid[m]] = np.nonzero(m)[0]
+            g = (sweep_global_tile(p, tiles, self.W, self.H, self.bx)[:, None] * PORTS_PER_TILE +
+                 np.arange(PORTS_PER_TILE)[None, :]).reshape(-1)
+            out.append(Results(fin[idx], zl[idx], ct[idx], ps[g], pc[g], pm[g], {}))
+        return out

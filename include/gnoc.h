@@ -160,6 +160,29 @@ int gnoc_set_profiling(gnoc_engine *eng, int enable);
 int gnoc_get_kernel_stats(gnoc_engine *eng, const char **names, double *total_ms,
                           uint32_t *launches, size_t cap, size_t *count);
 
+/* ---- design-space sweep --------------------------
+ * npoints independent simulations of the same mesh size, each with its own
+ * flit width, router delay and link delay (the carbon_sim.cfg keys a sweep
+ * varies), timed in ONE batch: point p is block p of a grid of blocks_x x
+ * blocks_y meshes laid side by side (gnoc_sweep_layout), and XY routing never
+ * leaves a packet's block.  A packet of point p, local tiles s -> d, is
+ * submitted with global tiles G(p, s) -> G(p, d), where for a W x H point
+ *   G(p, t) = ((p / blocks_x) * H + t / W) * (blocks_x * W) + (p % blocks_x) * W + t % W,
+ * and the trace is the (inject_ps, point, id)-ordered merge of the points'
+ * traces.  Results are per packet and per global port, exactly as each point
+ * alone would give.  Needs f = 1 GHz and max_list_size >= 3 (the base config's
+ * frequency / queue keys apply to every point). */
+typedef struct gnoc_point
+{
+   int32_t  flit_width;      /* network/emesh_hop_by_hop/flit_width                           */
+   uint64_t router_delay;    /* network/emesh_hop_by_hop/router/delay                         */
+   uint64_t link_delay;      /* network/emesh_hop_by_hop/link/delay = ceil(f*0.01*tile_width) */
+   double   tile_width_mm;   /* general/tile_width                                            */
+} gnoc_point;
+
+int gnoc_create_sweep(const gnoc_config *base, const gnoc_point *points, int32_t npoints, gnoc_engine **out);
+int gnoc_sweep_layout(const gnoc_engine *eng, int32_t *blocks_x, int32_t *blocks_y);
+
 /* ---- one mesh over several GPUs ---------------------------
  * XY routing (emesh_hop_by_hop.cc:229-240) sends a packet along its source
  * row, then along its destination column.  Rank r of n owns the injection and

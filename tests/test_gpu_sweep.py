@@ -1,0 +1,56 @@
+"""Design-space sweep (gnoc_create_sweep): many points with their own flit
+width, router delay and link delay in one batch, each bit-exact against the
+oracle run of that point alone."""
+import itertools
+
+import numpy as np
+import pytest
+
+from graphite_amd import gnoc
+from oracle import oracle
+from tests.traces import random_trace
+
+pytestmark = pytest.mark.gpu
+
+
+def check_points(base, pts, traces):
+    eng = gnoc.SweepEngine(base, pts)
+    eng.submit(traces)
+    eng.run()
+    eng.run()
+    got = eng.results()
+    eng.close()
+    for k, (q, tr) in enumerate(zip(pts, traces)):
+        ref = oracle.run(q.config(base), tr)
+        for name in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1"):
+            a, b = getattr(got[k], name), getattr(ref, name)
+            assert np.array_equal(a, b), f"point {k} {q}: {name} differs ({np.sum(a != b)} entries)"
+
+
+def test_sweep_grid_of_config5_axes():
+    """flit width x router delay x tile width (-> link delay 1..4) x load, 8x8 points."""
+    base = gnoc.EngineConfig(num_tiles=64)
+    pts, trs = [], []
+    axes = itertools.product([16, 32, 64, 128], [0, 1, 2, 3], [1.0, 150.0, 250.0, 350.0])
+    for k, (fw, r, tw) in enumerate(axes):
+        if k % 3:
+            continue   # 22 of the 64 combinations keep the test short
+        lk = int(np.ceil(0.01 * tw))
+        pts.append(gnoc.SweepPoint(fw, r, lk, tw))
+        load = (0.005, 0.01, 0.015, 0.02)[k % 4]
+        trs.append(gnoc.synthetic_trace(8, 8, load, 150, seed=100 + k))
+    check_points(base, pts, trs)
+
+
+def test_sweep_saturated_points_with_mg1():
+    base = gnoc.EngineConfig(num_tiles=16)
+    pts = [gnoc.SweepPoint(64, 1, 1, 1.0), gnoc.SweepPoint(16, 2, 2, 150.0), gnoc.SweepPoint(128, 0, 3, 250.0)]
+    trs = [random_trace(3000, 4, 4, seed=s, max_cycle=200, burst0=100, self_frac=0.05) for s in range(3)]
+    check_points(base, pts, trs)
+    assert sum(oracle.run(q.config(base), t).port_mg1.sum() for q, t in zip(pts, trs)) > 0
+
+
+def test_sweep_one_point_is_the_plain_engine():
+    base = gnoc.EngineConfig(num_tiles=64)
+    tr = gnoc.synthetic_trace(8, 8, 0.02, 300, seed=1)
+    check_points(base, [gnoc.SweepPoint()], [tr])
