@@ -91,7 +91,7 @@ struct gnoc_engine
    DevBuf hist, tot, slot_cnt, slot_base, counters, gtot;
    DevBuf recs, samp_t, samp_id, Hs, Pp, Prow, pcol, nexc, dirty;
    DevBuf pio, pnc, pgb, lvl_cbase, lvl_qb, cdesc, flags, st, lvl_ctr;
-   DevBuf port_sum, port_cnt, port_mg1, plan_ports, stamps, done;
+   DevBuf port_sum, port_cnt, port_mg1, port_flit, port_last, plan_ports, stamps, done;
    uint64_t h_chunk_bound = 0;
    int force_v1 = 0;
    int used_v3 = 0;
@@ -664,12 +664,14 @@ static int run_levels_v1(gnoc_engine* e)
          GNOC_LAUNCH(e, KC_PORT, k_port_stream<true>, dim3(cnt), dim3(STHREADS), 0, s, c, pp, e->slot_cnt.as<uint32_t>(),
                      e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
                      e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
-                     e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
+                     e->port_flit.as<uint64_t>(), e->port_last.as<uint64_t>(), e->dirty.as<uint32_t>(),
+                     e->counters.as<unsigned int>() + 8);
       else
          GNOC_LAUNCH(e, KC_PORT, k_port_stream<false>, dim3(cnt), dim3(STHREADS), 0, s, c, pp, e->slot_cnt.as<uint32_t>(),
                      e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
                      e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
-                     e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8);
+                     e->port_flit.as<uint64_t>(), e->port_last.as<uint64_t>(), e->dirty.as<uint32_t>(),
+                     e->counters.as<unsigned int>() + 8);
    }
    return GNOC_OK;
 }
@@ -760,7 +762,8 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
    c, (lvl), e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
       e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(),                 \
       e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),                          \
-      e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(), e->counters.as<unsigned>() + 8,     \
+      e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),                                     \
+      e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>(), e->counters.as<unsigned>() + 8,   \
       e->done.as<uint32_t>(), stp
    if (xl && l0 == 0)
    {
@@ -834,6 +837,8 @@ static int run_prep(gnoc_engine* e, bool* done)
    GNOC_HIP(e, e->port_sum.ensure(nports * 8));
    GNOC_HIP(e, e->port_cnt.ensure(nports * 8));
    GNOC_HIP(e, e->port_mg1.ensure(nports * 8));
+   GNOC_HIP(e, e->port_flit.ensure(nports * 8));
+   GNOC_HIP(e, e->port_last.ensure(nports * 8));
    if (band_prep) GNOC_HIP(e, e->pcol.ensure((size_t) nC * H * H * 4));
 
    e->evused = 0;
@@ -845,6 +850,8 @@ static int run_prep(gnoc_engine* e, bool* done)
    GNOC_HIP(e, hipMemsetAsync(e->port_sum.p, 0, nports * 8, s));
    GNOC_HIP(e, hipMemsetAsync(e->port_cnt.p, 0, nports * 8, s));
    GNOC_HIP(e, hipMemsetAsync(e->port_mg1.p, 0, nports * 8, s));
+   GNOC_HIP(e, hipMemsetAsync(e->port_flit.p, 0, nports * 8, s));
+   GNOC_HIP(e, hipMemsetAsync(e->port_last.p, 0, nports * 8, s));
    if (!pp_lds) GNOC_HIP(e, hipMemsetAsync(e->Pp.p, 0, (size_t) H * G * N * 4, s));
    if (band_prep) GNOC_HIP(e, hipMemsetAsync(e->pcol.p, 0, (size_t) nC * H * H * 4, s));
 
@@ -1130,6 +1137,25 @@ int gnoc_get_port_stats(gnoc_engine* e, uint64_t* sum_delay, uint64_t* count, ui
    if (sum_delay) GNOC_HIP(e, hipMemcpyAsync(sum_delay, e->port_sum.p, np * 8, hipMemcpyDeviceToHost, e->stream));
    if (count) GNOC_HIP(e, hipMemcpyAsync(count, e->port_cnt.p, np * 8, hipMemcpyDeviceToHost, e->stream));
    if (mg1_uses) GNOC_HIP(e, hipMemcpyAsync(mg1_uses, e->port_mg1.p, np * 8, hipMemcpyDeviceToHost, e->stream));
+   GNOC_HIP(e, hipStreamSynchronize(e->stream));
+   return GNOC_OK;
+}
+
+int gnoc_get_port_utilization(gnoc_engine* e, uint64_t* flits, uint64_t* last_cycle, size_t nports)
+{
+   if (!e) return GNOC_EINVAL;
+   if (!e->ran) return fail(e, GNOC_ESTATE, "no results: call gnoc_run first");
+   const size_t np = (size_t) e->dc.N * PORTS;
+   if (nports != np) return fail(e, GNOC_EINVAL, "nports != num_tiles*6");
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   if (!e->dc.contention)
+   {
+      if (flits) std::memset(flits, 0, np * 8);
+      if (last_cycle) std::memset(last_cycle, 0, np * 8);
+      return GNOC_OK;
+   }
+   if (flits) GNOC_HIP(e, hipMemcpyAsync(flits, e->port_flit.p, np * 8, hipMemcpyDeviceToHost, e->stream));
+   if (last_cycle) GNOC_HIP(e, hipMemcpyAsync(last_cycle, e->port_last.p, np * 8, hipMemcpyDeviceToHost, e->stream));
    GNOC_HIP(e, hipStreamSynchronize(e->stream));
    return GNOC_OK;
 }

@@ -186,7 +186,8 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
                                                           const uint64_t* __restrict__ slot_base,
                                                           Rec* __restrict__ recs, uint64_t* __restrict__ final_ps,
                                                           uint64_t* __restrict__ port_sum, uint64_t* __restrict__ port_cnt,
-                                                          uint64_t* __restrict__ port_mg1, uint32_t* __restrict__ dirty,
+                                                          uint64_t* __restrict__ port_mg1, uint64_t* __restrict__ port_flit,
+                                                          uint64_t* __restrict__ port_last, uint32_t* __restrict__ dirty,
                                                           unsigned int* __restrict__ errflag)
 {
    __shared__ __attribute__((aligned(16))) char smraw[sizeof(PortSmem) > sizeof(FixSmem) ? sizeof(PortSmem) : sizeof(FixSmem)];
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
 
    uint32_t cur[SMAXIN] = { 0, 0, 0, 0 };
    uint64_t X0 = 0;                         // carried queue state (cycles)
-   uint64_t st_sum = 0, st_cnt = 0;
+   uint64_t st_sum = 0, st_cnt = 0, st_flit = 0, st_last = 0;
    bool first_round = true;
 
    if (tid == 0)
@@ -464,6 +465,12 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
             const uint64_t cc = sm.m_c[e];
             st_sum += cc;
             st_cnt++;
+            {
+               // QueueModel utilization (queue_model.cc:49-53): F and departure, in cycles
+               const uint64_t p = aux_F(ax), dep = cyc_of<F1>(t, c.f) + cc + p;
+               st_flit += p;
+               st_last = st_last > dep ? st_last : dep;
+            }
             const uint64_t tn = t + ps_of<F1>(cc, c.f) + (dir == P_INJ ? 0ull : rl_of(c, tile));
             if (dir == P_SELF)
             {
@@ -499,10 +506,24 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
    }
    if (lane == 0) { sm.wA[wv] = st_sum; sm.wB[wv] = st_cnt; }
    __syncthreads();
+   uint64_t a = 0, b = 0;
+   if (tid == 0)
+      for (uint32_t w = 0; w < STHREADS / 64; w++) { a += sm.wA[w]; b += sm.wB[w]; }
+   __syncthreads();
+   for (int off = 32; off > 0; off >>= 1)
+   {
+      st_flit += __shfl_down(st_flit, off);
+      const uint64_t o = __shfl_down(st_last, off);
+      st_last = st_last > o ? st_last : o;
+   }
+   if (lane == 0) { sm.wA[wv] = st_flit; sm.wB[wv] = st_last; }
+   __syncthreads();
    if (tid == 0)
    {
-      uint64_t a = 0, b = 0;
-      for (uint32_t w = 0; w < STHREADS / 64; w++) { a += sm.wA[w]; b += sm.wB[w]; }
+      uint64_t fl = 0, la = 0;
+      for (uint32_t w = 0; w < STHREADS / 64; w++) { fl += sm.wA[w]; la = la > sm.wB[w] ? la : sm.wB[w]; }
+      port_flit[port] = fl;
+      port_last[port] = la;
       port_sum[port] = a;
       port_cnt[port] = b;
       port_mg1[port] = sm.ss.mg1;
@@ -559,9 +580,9 @@ __global__ __launch_bounds__(256) void k_mask_unowned(uint64_t n, const uint32_t
 
 // explicit instantiations
 template __global__ void k_port_stream<true>(DevCfg, const uint32_t*, const uint32_t*, const uint64_t*, Rec*, uint64_t*,
-                                             uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
+                                             uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
 template __global__ void k_port_stream<false>(DevCfg, const uint32_t*, const uint32_t*, const uint64_t*, Rec*, uint64_t*,
-                                              uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
+                                              uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
 template __global__ void k_finalize<true>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,
                                           const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int, uint32_t, uint32_t);
 template __global__ void k_finalize<false>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,

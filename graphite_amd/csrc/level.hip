@@ -96,6 +96,7 @@ struct LvSmem
    Carry3 cy;
    uint64_t wA[LV_T / 64], wB[LV_T / 64], wC[LV_T / 64];
    uint64_t st_sum;
+   uint64_t st_flit, st_last;   // sum of F, latest departure (QueueModel utilization, queue_model.cc:49-53)
    uint64_t lk_t[LV_MAXLEAF + 1];
    uint32_t lk_i[LV_MAXLEAF + 1];
    uint32_t lr_lo[LV_MAXLEAF][LV_IN];
@@ -655,7 +656,7 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
       s.X = sm.cy.X; s.g = (int) sm.cy.g; s.mode = 1; s.s1 = sm.cy.s1; s.s2 = sm.cy.s2;
       s.narr = sm.cy.narr; s.newest = sm.cy.newest; s.mg1 = 0;
       uint32_t e = 0;
-      uint64_t ssum = 0;
+      uint64_t ssum = 0, sflit = 0, slast = 0;
       for (; e < E && s.mode; e++)
       {
          const uint32_t k = sm.perm[e];
@@ -665,6 +666,9 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
          const uint64_t cc = serial_step(s, cyc1(t), aux_F(ax), c.max_list, c.analytical);
          if (s.g >= 1) s.mode = 0;
          ssum += cc;
+         sflit += aux_F(ax);
+         const uint64_t dep = cyc1(t) + cc + aux_F(ax);
+         slast = slast > dep ? slast : dep;
          const uint64_t tn = t + cc * 1000ull + rl;
          if (dir == P_SELF) { final_ps[id] = tn + 1000ull * aux_F(ax); continue; }
          const uint32_t nd = next_dir(ax, dir, nx, ny);
@@ -691,6 +695,8 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
       sm.cy.X = s.X; sm.cy.g = (uint32_t) s.g; sm.cy.mode = s.mode; sm.cy.s1 = s.s1; sm.cy.s2 = s.s2;
       sm.cy.narr = s.narr; sm.cy.newest = s.newest;
       sm.st_sum += ssum;
+      sm.st_flit += sflit;
+      sm.st_last = sm.st_last > slast ? sm.st_last : slast;
       sm.st_cnt += e;
       sm.st_mg1 += (uint32_t) s.mg1;
    }
@@ -753,6 +759,12 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
       sm.st_cnt += sm.E - sm.s0;
       const uint64_t nx0 = X0 + so.tA;
       sm.cy.X = nx0 > so.tB ? nx0 : so.tB;
+      if (sm.E > sm.s0)
+      {
+         // FIFO-served: departures increase, the last one is the new queue tail X
+         sm.st_flit += so.tA;
+         sm.st_last = sm.st_last > sm.cy.X ? sm.st_last : sm.cy.X;
+      }
       for (uint32_t d = 0; d < 5; d++) sm.cy.cnt[d] += cfield(so.tC, d);
    }
    lv_bar();
@@ -1147,7 +1159,9 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
                                                 uint64_t* __restrict__ final_ps,
                                                 unsigned long long* __restrict__ port_sum,
                                                 unsigned long long* __restrict__ port_cnt,
-                                                unsigned long long* __restrict__ port_mg1, unsigned* __restrict__ errflag,
+                                                unsigned long long* __restrict__ port_mg1,
+                                                unsigned long long* __restrict__ port_flit,
+                                                unsigned long long* __restrict__ port_last, unsigned* __restrict__ errflag,
                                                 uint32_t* __restrict__ done, uint64_t* __restrict__ stamps)
 {
    __shared__ LvSmem sm;
@@ -1197,6 +1211,8 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
             sm.g = g;
             sm.pk = sm.nx.pk;
             sm.st_sum = 0;
+            sm.st_flit = 0;
+            sm.st_last = 0;
             sm.st_cnt = 0;
             sm.st_mg1 = 0;
             sm.published = 0;
@@ -1415,6 +1431,11 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
          atomicAdd(&port_sum[sm.io.port], (unsigned long long) sm.st_sum);
          atomicAdd(&port_cnt[sm.io.port], (unsigned long long) sm.st_cnt);
          if (sm.st_mg1) atomicAdd(&port_mg1[sm.io.port], (unsigned long long) sm.st_mg1);
+         if (sm.st_flit)
+         {
+            atomicAdd(&port_flit[sm.io.port], (unsigned long long) sm.st_flit);
+            atomicMax(&port_last[sm.io.port], (unsigned long long) sm.st_last);
+         }
       }
       if (XL)
       {

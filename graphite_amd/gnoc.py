@@ -35,7 +35,7 @@ EXPORTED = (
     "gnoc_last_error", "gnoc_destroy", "gnoc_trace_synthetic", "gnoc_abi_version",
     "gnoc_set_profiling", "gnoc_get_kernel_stats", "gnoc_trace_file_write", "gnoc_trace_file_read",
     "gnoc_shard", "gnoc_exchange_counts", "gnoc_run_begin", "gnoc_run_finish",
-    "gnoc_create_sweep", "gnoc_sweep_layout",
+    "gnoc_create_sweep", "gnoc_sweep_layout", "gnoc_get_port_utilization",
 )
 
 
@@ -114,6 +114,7 @@ def load() -> ctypes.CDLL:
     lib.gnoc_get_packet_results.argtypes = [vp, vp, vp, vp, sz]
     lib.gnoc_get_port_stats.argtypes = [vp, vp, vp, vp, sz]
     lib.gnoc_get_summary.argtypes = [vp, ctypes.POINTER(GnocSummary)]
+    lib.gnoc_get_port_utilization.argtypes = [vp, vp, vp, sz]
     lib.gnoc_device_final_ps.argtypes = [vp, ctypes.POINTER(vp)]
     lib.gnoc_last_error.argtypes = [vp]
     lib.gnoc_last_error.restype = ctypes.c_char_p
@@ -262,6 +263,8 @@ class Results:
     port_count: np.ndarray
     port_mg1: np.ndarray
     summary: dict = field(default_factory=dict)
+    port_flit: Optional[np.ndarray] = None   # QueueModel _total_utilized_cycles (gnoc_get_port_utilization)
+    port_last: Optional[np.ndarray] = None   # QueueModel _last_request_time
 
 
 class Engine:
@@ -322,7 +325,9 @@ class Engine:
         npt = self.cfg.width * self.cfg.height * PORTS_PER_TILE
         ps, pc, pm = (np.empty(npt, np.uint64) for _ in range(3))
         self._check(self.lib.gnoc_get_port_stats(self._h, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data, npt))
-        return Results(fin, zl, ct, ps, pc, pm, self.summary())
+        pf, pl = np.empty(npt, np.uint64), np.empty(npt, np.uint64)
+        self._check(self.lib.gnoc_get_port_utilization(self._h, pf.ctypes.data, pl.ctypes.data, npt))
+        return Results(fin, zl, ct, ps, pc, pm, self.summary(), pf, pl)
 
     def set_profiling(self, on: bool) -> None:
         self._check(self.lib.gnoc_set_profiling(self._h, int(on)))
@@ -425,15 +430,17 @@ class ShardedEngine(Engine):
         import torch
         import torch.distributed as dist
         r = self.results()
-        parts = [r.final_ps, r.zero_load_ps, r.contention_ps, r.port_sum_delay, r.port_count, r.port_mg1]
+        parts = [r.final_ps, r.zero_load_ps, r.contention_ps, r.port_sum_delay, r.port_count, r.port_mg1,
+                 r.port_flit, r.port_last]
         flat = torch.from_numpy(np.concatenate(parts).view(np.int64).copy())
         if dist.get_backend(self.group) == "nccl":
             flat = flat.cuda(self.cfg.device)
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
         out = flat.cpu().numpy().view(np.uint64)
         n, npt = self._n, r.port_sum_delay.shape[0]
-        o = [0, n, 2 * n, 3 * n, 3 * n + npt, 3 * n + 2 * npt, 3 * n + 3 * npt]
-        return Results(*(out[o[k]:o[k + 1]].copy() for k in range(6)), summary=r.summary)
+        o = [0, n, 2 * n, 3 * n, 3 * n + npt, 3 * n + 2 * npt, 3 * n + 3 * npt, 3 * n + 4 * npt, 3 * n + 5 * npt]
+        a = [out[o[k]:o[k + 1]].copy() for k in range(8)]
+        return Results(*a[:6], summary=r.summary, port_flit=a[6], port_last=a[7])
 
 
 class LocalShardSet:
@@ -488,7 +495,7 @@ class LocalShardSet:
         rs = [e.results() for e in self.engs]
         f = lambda k: np.sum([getattr(r, k) for r in rs], axis=0, dtype=np.uint64)
         return Results(f("final_ps"), f("zero_load_ps"), f("contention_ps"), f("port_sum_delay"), f("port_count"),
-                       f("port_mg1"), rs[0].summary)
+                       f("port_mg1"), rs[0].summary, f("port_flit"), f("port_last"))
 
     def set_profiling(self, on: bool) -> None:
         for e in self.engs:
@@ -593,6 +600,8 @@ class SweepEngine:
         npt = self.bx * self.W * self.by * self.H * PORTS_PER_TILE
         ps, pc, pm = (np.empty(npt, np.uint64) for _ in range(3))
         self._check(self.lib.gnoc_get_port_stats(self._h, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data, npt))
+        pf, pl = np.empty(npt, np.uint64), np.empty(npt, np.uint64)
+        self._check(self.lib.gnoc_get_port_utilization(self._h, pf.ctypes.data, pl.ctypes.data, npt))
         out = []
         tiles = np.arange(self.W * self.H)
         for p, cnt in enumerate(self._counts):
@@ -601,5 +610,5 @@ class SweepEngine:
             idx[self._lid[m]] = np.nonzero(m)[0]
             g = (sweep_global_tile(p, tiles, self.W, self.H, self.bx)[:, None] * PORTS_PER_TILE +
                  np.arange(PORTS_PER_TILE)[None, :]).reshape(-1)
-            out.append(Results(fin[idx], zl[idx], ct[idx], ps[g], pc[g], pm[g], {}))
+            out.append(Results(fin[idx], zl[idx], ct[idx], ps[g], pc[g], pm[g], {}, pf[g], pl[g]))
         return out

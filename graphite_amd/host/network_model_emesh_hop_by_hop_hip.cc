@@ -137,6 +137,11 @@ void NetworkModelEMeshHopByHopHIP::run()
    _pcnt.resize(np);
    _pmg1.resize(np);
    check(gnoc_get_port_stats(_eng, _psum.data(), _pcnt.data(), _pmg1.data(), np), "gnoc_get_port_stats");
+   _pflit.resize(np);
+   _plast.resize(np);
+   check(gnoc_get_port_utilization(_eng, _pflit.data(), _plast.data(), np), "gnoc_get_port_utilization");
+   _rflit.clear();
+   _rpkt.clear();
    _ran = true;
 }
 
@@ -150,6 +155,72 @@ gnoc_summary NetworkModelEMeshHopByHopHIP::summary() const
 // Time::toCycles / toNanosec (common/misc/time_types.h:99-109)
 static uint64_t ps_to_cycles(uint64_t ps, double f) { return (uint64_t) std::ceil(((double) ps * f) / 1.0e3); }
 static uint64_t ps_to_ns(uint64_t ps) { return (uint64_t) std::ceil(((double) ps) / 1.0e3); }
+
+// Every routed packet traverses the mesh routers of its source row from sx to
+// dx, then of column dx up to dy (XY routing, emesh_hop_by_hop.cc:229-240):
+// segment sums with difference arrays, O(packets + tiles).
+void NetworkModelEMeshHopByHopHIP::buildEventCounters() const
+{
+   const int W = _cfg.mesh_width, H = _cfg.mesh_height;
+   const uint32_t fw = (uint32_t) _cfg.flit_width;
+   std::vector<int64_t> rf((size_t) (W + 1) * H, 0), rp((size_t) (W + 1) * H, 0);
+   std::vector<int64_t> cf((size_t) (H + 1) * W, 0), cp((size_t) (H + 1) * W, 0);
+   for (size_t i = 0; i < _inj.size(); i++)
+   {
+      if (_src[i] == _dst[i] || _flags[i]) continue;
+      const int64_t F = (_bits[i] % fw) ? _bits[i] / fw + 1 : _bits[i] / fw;
+      const int sx = (int) _src[i] % W, sy = (int) _src[i] / W, dx = (int) _dst[i] % W, dy = (int) _dst[i] / W;
+      const int x0 = sx < dx ? sx : dx, x1 = sx < dx ? dx : sx;
+      rf[(size_t) sy * (W + 1) + x0] += F;
+      rf[(size_t) sy * (W + 1) + x1 + 1] -= F;
+      rp[(size_t) sy * (W + 1) + x0] += 1;
+      rp[(size_t) sy * (W + 1) + x1 + 1] -= 1;
+      if (dy != sy)
+      {
+         const int y0 = dy > sy ? sy + 1 : dy, y1 = dy > sy ? dy : sy - 1;
+         cf[(size_t) dx * (H + 1) + y0] += F;
+         cf[(size_t) dx * (H + 1) + y1 + 1] -= F;
+         cp[(size_t) dx * (H + 1) + y0] += 1;
+         cp[(size_t) dx * (H + 1) + y1 + 1] -= 1;
+      }
+   }
+   _rflit.assign((size_t) W * H, 0);
+   _rpkt.assign((size_t) W * H, 0);
+   for (int y = 0; y < H; y++)
+   {
+      int64_t a = 0, b = 0;
+      for (int x = 0; x < W; x++)
+      {
+         a += rf[(size_t) y * (W + 1) + x];
+         b += rp[(size_t) y * (W + 1) + x];
+         _rflit[(size_t) y * W + x] += (uint64_t) a;
+         _rpkt[(size_t) y * W + x] += (uint64_t) b;
+      }
+   }
+   for (int x = 0; x < W; x++)
+   {
+      int64_t a = 0, b = 0;
+      for (int y = 0; y < H; y++)
+      {
+         a += cf[(size_t) x * (H + 1) + y];
+         b += cp[(size_t) x * (H + 1) + y];
+         _rflit[(size_t) y * W + x] += (uint64_t) a;
+         _rpkt[(size_t) y * W + x] += (uint64_t) b;
+      }
+   }
+}
+
+uint64_t NetworkModelEMeshHopByHopHIP::routerFlits(int tile) const
+{
+   if (_rflit.empty()) buildEventCounters();
+   return _rflit.at((size_t) tile);
+}
+
+uint64_t NetworkModelEMeshHopByHopHIP::routerPackets(int tile) const
+{
+   if (_rpkt.empty()) buildEventCounters();
+   return _rpkt.at((size_t) tile);
+}
 
 void NetworkModelEMeshHopByHopHIP::outputSummary(std::ostream& out, int tile) const
 {
@@ -197,18 +268,31 @@ void NetworkModelEMeshHopByHopHIP::outputSummary(std::ostream& out, int tile) co
       out << "    Average Contention Delay (in clock cycles): 0\n";
       out << "    Average Contention Delay (in nanoseconds): 0\n";
    }
+   // outputEventCountSummary (:436-468): unicast traffic uses crossbar[1] only
+   const uint64_t rfl = routerFlits(tile);
+   out << "    Event Counters:\n";
+   out << "      Buffer Writes: " << rfl << "\n";
+   out << "      Buffer Reads: " << rfl << "\n";
+   out << "      Switch Allocator Requests: " << routerPackets(tile) << "\n";
+   for (int i = 1; i <= 5; i++) out << "      Crossbar[" << i << "] Traversals: " << (i == 1 ? rfl : 0) << "\n";
+   out << "      Link Traversals: " << rfl << "\n";
+   if (!_cfg.contention_enabled) return;   // emesh_hop_by_hop.cc:304-305
    // outputContentionModelsSummary: the mesh router's 5 output ports
    uint64_t sd = 0, sp = 0, sa = 0;
+   float lu = 0.0f;
    for (int p = 0; p < 5; p++)
    {
       const size_t k = (size_t) tile * GNOC_PORTS_PER_TILE + p;
       sd += _psum[k];
       sp += _pcnt[k];
       sa += _pmg1[k];
+      // QueueModel::getQueueUtilization (queue_model.cc:56-62)
+      lu += (_plast[k] > 0) ? (((float) _pflit[k]) / _plast[k]) : 0.0f;
    }
+   lu = lu / 5;   // RouterModel::getAverageLinkUtilization (router_model.cc:167-183)
    out << "    Contention Counters:\n";
    out << "      Average EMesh Router Contention Delay: " << (sp > 0 ? ((float) sd) / sp : 0.0f) << "\n";
-   out << "      Average EMesh Router Link Utilization: 0\n";
+   out << "      Average EMesh Router Link Utilization: " << lu << "\n";
    out << "      Analytical Models Used (%): " << (sp > 0 ? ((float) sa * 100) / sp : 0.0f) << "\n";
 }
 

@@ -108,11 +108,24 @@ public:
    const std::vector<uint64_t>& portContentionDelay() const { return _psum; }
    const std::vector<uint64_t>& portPackets() const { return _pcnt; }
    const std::vector<uint64_t>& portAnalyticalRequests() const { return _pmg1; }
+   // QueueModel utilization operands per output port (queue_model.cc:49-53):
+   // _total_utilized_cycles (flits) and _last_request_time (cycles).
+   const std::vector<uint64_t>& portUtilizedCycles() const { return _pflit; }
+   const std::vector<uint64_t>& portLastRequestTime() const { return _plast; }
 
-   // The per-tile sim.out network section: NetworkModel::outputSummary
-   // (network_model.cc:274-316) followed by the emesh contention counters
-   // (network_model_emesh_hop_by_hop.cc:471-493, router_model.cc:146-215;
-   // link utilization is not modelled here and printed as 0).
+   // Mesh-router event counters of a tile (RouterModel::updateEventCounters,
+   // router_model.cc:119-127; ElectricalLinkModel::processPacket,
+   // electrical_link_model.cc:29-45): flits through the router (= buffer
+   // writes = buffer reads = crossbar[1] = link traversals for unicast) and
+   // packets through it (= switch allocator requests).  Route-static.
+   uint64_t routerFlits(int tile) const;
+   uint64_t routerPackets(int tile) const;
+
+   // The per-tile sim.out network section of NetworkModelEMeshHopByHop::outputSummary
+   // (network_model_emesh_hop_by_hop.cc:299-306): NetworkModel::outputSummary
+   // (network_model.cc:274-316), the event counters (:436-468) and, when the
+   // queue models are enabled, the contention counters (:471-493,
+   // router_model.cc:146-215).  Power modelling is off (no power section).
    void outputSummary(std::ostream& out, int tile) const;
 
    gnoc_summary summary() const;
@@ -136,7 +149,9 @@ private:
    gnoc_engine* _eng = nullptr;
    std::vector<uint64_t> _inj;
    std::vector<uint32_t> _src, _dst, _bits, _flags;
-   std::vector<uint64_t> _final, _zl, _ct, _psum, _pcnt, _pmg1;
+   std::vector<uint64_t> _final, _zl, _ct, _psum, _pcnt, _pmg1, _pflit, _plast;
+   mutable std::vector<uint64_t> _rflit, _rpkt;   // event counters, built on first use
+   void buildEventCounters() const;
    bool _ran = false;
 };
 

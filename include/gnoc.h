@@ -145,6 +145,15 @@ int gnoc_get_packet_results(gnoc_engine *eng, uint64_t *final_ps, uint64_t *zero
 int gnoc_get_port_stats(gnoc_engine *eng, uint64_t *sum_delay, uint64_t *count,
                         uint64_t *mg1_uses, size_t nports);
 
+/* Per-output-port utilization counters, arrays of num_tiles*6 like
+ * gnoc_get_port_stats: flits = QueueModel::_total_utilized_cycles (sum of the
+ * requests' flit counts) and last_cycle = _last_request_time (latest
+ * arrival + queue delay + flits), queue_model.cc:49-53.  The reference's
+ * link utilization is flits / last_cycle (QueueModel::getQueueUtilization,
+ * queue_model.cc:56-62), averaged over the router's ports
+ * (RouterModel::getAverageLinkUtilization, router_model.cc:167-183). */
+int gnoc_get_port_utilization(gnoc_engine *eng, uint64_t *flits, uint64_t *last_cycle, size_t nports);
+
 int gnoc_get_summary(gnoc_engine *eng, gnoc_summary *out);
 
 /* Device pointer to the final_ps array (uint64_t[n]) of the last run, for

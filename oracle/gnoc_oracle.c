@@ -280,14 +280,17 @@ static heap_ent heap_pop(heap_t *h)
 
 /* Returns 0 on success, <0 on invalid configuration / trace.
  * Outputs are arrays of n (per packet) or 6*W*H (per port, index tile*6+port,
- * port 0..4 = SELF,LEFT,RIGHT,DOWN,UP of the mesh router, 5 = injection router). */
+ * port 0..4 = SELF,LEFT,RIGHT,DOWN,UP of the mesh router, 5 = injection router).
+ * port_flits / port_last (may be NULL): _total_utilized_cycles and
+ * _last_request_time of each port's queue (queue_model.cc:49-53). */
 ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
                        uint64_t router_delay, uint64_t link_delay, double frequency,
                        int contention_enabled, int analytical_enabled, int max_list_size,
                        size_t n, const uint64_t *inject_ps, const uint32_t *src,
                        const uint32_t *dst, const uint32_t *bits, const uint32_t *flags,
                        uint64_t *final_ps, uint64_t *zero_load_ps, uint64_t *contention_ps,
-                       uint64_t *port_sum_delay, uint64_t *port_count, uint64_t *port_mg1)
+                       uint64_t *port_sum_delay, uint64_t *port_count, uint64_t *port_mg1,
+                       uint64_t *port_flits, uint64_t *port_last)
 {
    const int W = mesh_width, H = mesh_height;
    if (W <= 0 || H <= 0 || flit_width <= 0 || frequency <= 0.0) return -1;
@@ -311,6 +314,8 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
    memset(port_sum_delay, 0, nports * sizeof(uint64_t));
    memset(port_count, 0, nports * sizeof(uint64_t));
    memset(port_mg1, 0, nports * sizeof(uint64_t));
+   if (port_flits) memset(port_flits, 0, nports * sizeof(uint64_t));
+   if (port_last) memset(port_last, 0, nports * sizeof(uint64_t));
 
    /* per-packet running state (NetPacket fields, network.h:27-55) */
    uint64_t *ptime = (uint64_t *) malloc(n * sizeof(uint64_t));
@@ -416,6 +421,9 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
       for (size_t p = 0; p < nports; p++)
       {
          port_mg1[p] = q[p]->mg1_uses;
+         /* QueueModel::getQueueUtilization's operands, queue_model.cc:49-62 */
+         if (port_flits) port_flits[p] = q[p]->util_cycles;
+         if (port_last) port_last[p] = q[p]->last_request_time;
          orc_queue_destroy(q[p]);
       }
       free(q);

@@ -53,7 +53,7 @@ def lib() -> ctypes.CDLL:
         L.orc_time_to_cycles.restype = u64
         L.orc_time_to_cycles.argtypes = [u64, ctypes.c_double]
         L.orc_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u64, u64, ctypes.c_double, ctypes.c_int,
-                              ctypes.c_int, ctypes.c_int, ctypes.c_size_t] + [vp] * 11
+                              ctypes.c_int, ctypes.c_int, ctypes.c_size_t] + [vp] * 13
         _orc = L
     return _orc
 
@@ -115,6 +115,8 @@ class OracleResult:
     port_sum_delay: np.ndarray
     port_count: np.ndarray
     port_mg1: np.ndarray
+    port_flit: np.ndarray = None     # QueueModel _total_utilized_cycles per port
+    port_last: np.ndarray = None     # QueueModel _last_request_time per port
 
 
 def run(cfg, tr) -> OracleResult:
@@ -130,11 +132,12 @@ def run(cfg, tr) -> OracleResult:
     flags = np.ascontiguousarray(tr.flags if tr.flags is not None else np.zeros(n, np.uint32), np.uint32)
     fin, zl, ct = (np.zeros(n, np.uint64) for _ in range(3))
     npt = W * H * 6
-    ps, pc, pm = (np.zeros(npt, np.uint64) for _ in range(3))
+    ps, pc, pm, pf, pl = (np.zeros(npt, np.uint64) for _ in range(5))
     rc = L.orc_run(W, H, cfg.flit_width, cfg.router_delay, cfg.link_delay, cfg.frequency_ghz,
                    int(cfg.contention_enabled), int(cfg.analytical_enabled), cfg.max_list_size, n,
                    inj.ctypes.data, src.ctypes.data, dst.ctypes.data, bits.ctypes.data, flags.ctypes.data,
-                   fin.ctypes.data, zl.ctypes.data, ct.ctypes.data, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data)
+                   fin.ctypes.data, zl.ctypes.data, ct.ctypes.data, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data,
+                   pf.ctypes.data, pl.ctypes.data)
     if rc:
         raise ValueError(f"oracle rejected input (rc={rc})")
-    return OracleResult(fin, zl, ct, ps, pc, pm)
+    return OracleResult(fin, zl, ct, ps, pc, pm, pf, pl)

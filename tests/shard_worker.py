@@ -42,7 +42,7 @@ def case(name):
 
 
 def same(a, b):
-    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1"):
+    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1", "port_flit", "port_last"):
         x, y = getattr(a, k), getattr(b, k)
         if not np.array_equal(x, y):
             bad = np.nonzero(x != y)[0]

@@ -1,0 +1,89 @@
+"""Expected sim.out network section of one tile, restated from the reference
+from per-packet and per-port results (test helper; the oracle supplies the
+results).  Float arithmetic in float32 and C++ ostream formatting (%g, 6
+significant digits), as the reference prints them.
+
+  NetworkModel::outputSummary                     network_model.cc:274-316
+    send / receive counters                       network_model.cc:229-272, 95-140
+  NetworkModelEMeshHopByHop::outputEventCountSummary      network_model_emesh_hop_by_hop.cc:436-468
+    RouterModel::updateEventCounters              router_model.cc:119-127
+    ElectricalLinkModel::processPacket            electrical_link_model.cc:29-45
+  NetworkModelEMeshHopByHop::outputContentionModelsSummary  network_model_emesh_hop_by_hop.cc:471-493
+    RouterModel::getAverage*                      router_model.cc:146-215
+    QueueModel::getQueueUtilization               queue_model.cc:56-62
+"""
+import math
+
+import numpy as np
+
+f32 = np.float32
+
+
+def cfmt(v) -> str:
+    """std::ostream << float (default precision 6)."""
+    return "%g" % float(f32(v))
+
+
+def _ceil_div_1000(ps: int) -> int:
+    return int(math.ceil(float(ps) / 1.0e3))
+
+
+def expected_summary(cfg, tr, res, tile: int) -> str:
+    W, H = cfg.width, cfg.height
+    fw = cfg.flit_width
+    src, dst, bits = tr.src.astype(np.int64), tr.dst.astype(np.int64), tr.bits.astype(np.int64)
+    flags = tr.flags if tr.flags is not None else np.zeros(len(src), np.uint32)
+    F = (bits + fw - 1) // fw
+    live = (src != dst) & (flags == 0)
+    s = live & (src == tile)
+    r = live & (dst == tile)
+    lat = int((res.zero_load_ps[r].astype(np.int64) + res.contention_ps[r].astype(np.int64)).sum())
+    cont = int(res.contention_ps[r].astype(np.int64).sum())
+    pr = int(r.sum())
+    out = []
+    out.append(f"    Total Packets Sent: {int(s.sum())}")
+    out.append(f"    Total Flits Sent: {int(F[s].sum())}")
+    out.append(f"    Total Bits Sent: {int(bits[s].sum())}")
+    out.append("    Total Packets Broadcasted: 0")
+    out.append("    Total Flits Broadcasted: 0")
+    out.append("    Total Bits Broadcasted: 0")
+    out.append(f"    Total Packets Received: {pr}")
+    out.append(f"    Total Flits Received: {int(F[r].sum())}")
+    out.append(f"    Total Bits Received: {int(bits[r].sum())}")
+    if pr > 0:
+        f = cfg.frequency_ghz
+        cyc = lambda ps: int(math.ceil((float(ps) * f) / 1.0e3))
+        out.append("    Average Packet Latency (in clock cycles): " + cfmt(f32(cyc(lat)) / f32(pr)))
+        out.append("    Average Packet Latency (in nanoseconds): " + cfmt(f32(_ceil_div_1000(lat)) / f32(pr)))
+        out.append("    Average Contention Delay (in clock cycles): " + cfmt(f32(cyc(cont)) / f32(pr)))
+        out.append("    Average Contention Delay (in nanoseconds): " + cfmt(f32(_ceil_div_1000(cont)) / f32(pr)))
+    else:
+        out += ["    Average Packet Latency (in clock cycles): 0", "    Average Packet Latency (in nanoseconds): 0",
+                "    Average Contention Delay (in clock cycles): 0", "    Average Contention Delay (in nanoseconds): 0"]
+    # event counters: every routed packet crosses the mesh routers of its XY route
+    tx, ty = tile % W, tile // W
+    sx, sy, dx, dy = src % W, src // W, dst % W, dst // W
+    on_row = live & (sy == ty) & (np.minimum(sx, dx) <= tx) & (tx <= np.maximum(sx, dx))
+    on_col = live & (dx == tx) & (dy != sy) & (((dy > sy) & (sy < ty) & (ty <= dy)) | ((dy < sy) & (dy <= ty) & (ty < sy)))
+    through = on_row | on_col
+    fl = int(F[through].sum())
+    out.append("    Event Counters:")
+    out.append(f"      Buffer Writes: {fl}")
+    out.append(f"      Buffer Reads: {fl}")
+    out.append(f"      Switch Allocator Requests: {int(through.sum())}")
+    for i in range(1, 6):
+        out.append(f"      Crossbar[{i}] Traversals: {fl if i == 1 else 0}")
+    out.append(f"      Link Traversals: {fl}")
+    if cfg.contention_enabled:
+        k = tile * 6 + np.arange(5)
+        sd, sp, sa = (int(a[k].sum()) for a in (res.port_sum_delay, res.port_count, res.port_mg1))
+        lu = f32(0.0)
+        for q in k:
+            last = int(res.port_last[q])
+            lu = f32(lu + (f32(int(res.port_flit[q])) / f32(last) if last > 0 else f32(0.0)))
+        lu = f32(lu / f32(5))
+        out.append("    Contention Counters:")
+        out.append("      Average EMesh Router Contention Delay: " + (cfmt(f32(sd) / f32(sp)) if sp else "0"))
+        out.append("      Average EMesh Router Link Utilization: " + cfmt(lu))
+        out.append("      Analytical Models Used (%): " + (cfmt(f32(f32(sa) * f32(100)) / f32(sp)) if sp else "0"))
+    return "\n".join(out) + "\n"

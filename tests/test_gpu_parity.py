@@ -29,7 +29,7 @@ def assert_same(got, ref, tr=None):
         if not np.array_equal(a, b):
             bad = np.nonzero(a != b)[0]
             raise AssertionError(f"{name}: {bad.size} mismatches, first id {bad[0]}: gpu {a[bad[0]]} oracle {b[bad[0]]}")
-    for name in ("port_sum_delay", "port_count", "port_mg1"):
+    for name in ("port_sum_delay", "port_count", "port_mg1", "port_flit", "port_last"):
         a, b = getattr(got, name), getattr(ref, name)
         if not np.array_equal(a, b):
             bad = np.nonzero(a != b)[0]
@@ -206,7 +206,7 @@ def test_engine_paths_agree():
     finally:
         del os.environ["GNOC_ENGINE"]
     assert b.summary["engine_path"] == 0
-    for k in ("final_ps", "port_sum_delay", "port_count", "port_mg1"):
+    for k in ("final_ps", "port_sum_delay", "port_count", "port_mg1", "port_flit", "port_last"):
         assert np.array_equal(getattr(a, k), getattr(b, k)), k
 
 

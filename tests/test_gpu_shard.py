@@ -56,7 +56,7 @@ def _local_vs(cfg, tr, n, ref):
     ss.run()
     got = ss.results()
     ss.close()
-    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1"):
+    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1", "port_flit", "port_last"):
         a, b = getattr(got, k), getattr(ref, k)
         assert np.array_equal(a, b), f"{k} differs at {n} ranks: first {np.nonzero(a != b)[0][:5]}"
 

@@ -22,7 +22,7 @@ def check_points(base, pts, traces):
     eng.close()
     for k, (q, tr) in enumerate(zip(pts, traces)):
         ref = oracle.run(q.config(base), tr)
-        for name in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1"):
+        for name in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1", "port_flit", "port_last"):
             a, b = getattr(got[k], name), getattr(ref, name)
             assert np.array_equal(a, b), f"point {k} {q}: {name} differs ({np.sum(a != b)} entries)"
 
