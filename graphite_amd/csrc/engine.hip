@@ -300,8 +300,11 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    const uint64_t link = (uint64_t) std::ceil(c.frequency_ghz * 0.01 * c.tile_width_mm);
    if (link != c.link_delay) return GNOC_EINVAL;
    if (c.router_delay + c.link_delay == 0) return GNOC_EINVAL;
-   if (c.queue_type != GNOC_QUEUE_HISTORY_TREE) return GNOC_EUNSUPPORTED;  // basic/history_list: DESIGN.md "next"
-   if (c.contention_enabled && c.max_list_size < 2) return GNOC_EINVAL;    // size-1 tree prunes its only node
+   if (c.queue_type != GNOC_QUEUE_HISTORY_TREE && c.queue_type != GNOC_QUEUE_BASIC &&
+       c.queue_type != GNOC_QUEUE_HISTORY_LIST)
+      return GNOC_EINVAL;                                                   // queue_model.cc:33-36
+   if (c.contention_enabled && c.queue_type != GNOC_QUEUE_BASIC && c.max_list_size < 2)
+      return GNOC_EINVAL;                                                   // size-1 tree prunes its only node
 
    gnoc_engine* e = new (std::nothrow) gnoc_engine;
    if (!e) return GNOC_ENOMEM;
@@ -319,6 +322,19 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    d.contention = c.contention_enabled;
    d.analytical = c.analytical_enabled;
    d.max_list = c.max_list_size;
+   if (c.queue_type == GNOC_QUEUE_BASIC)
+   {
+      // QueueModelBasic without moving average: FIFO, no analytical model, no pruning
+      d.analytical = 0;
+      d.max_list = 1 << 30;
+   }
+   else if (c.queue_type == GNOC_QUEUE_HISTORY_LIST && d.max_list < 3)
+   {
+      // the list prunes after inserting (size > max, history_list.cc:138-141): at
+      // max_list_size 2 a gap, once made, is never the last one removed -- the
+      // tree's behaviour at max_list_size >= 3
+      d.max_list = 3;
+   }
    d.magicW = d.W == 1 ? 0xFFFFFFFFu : (uint32_t) ((1ull << 32) / d.W);
    d.BW = d.W;
    d.BH = d.H;

@@ -25,6 +25,7 @@ GNOC_EUNSUPPORTED = -5
 GNOC_ENOMEM = -6
 
 PORT_SELF, PORT_LEFT, PORT_RIGHT, PORT_DOWN, PORT_UP, PORT_INJ = range(6)
+QUEUE_HISTORY_TREE, QUEUE_BASIC, QUEUE_HISTORY_LIST = 0, 1, 2
 PORTS_PER_TILE = 6
 PKT_UNMODELED = 0x1
 
@@ -159,11 +160,14 @@ class EngineConfig:
     frequency_ghz: float = 1.0              # network DVFS domain
     tile_width_mm: float = 1.0              # general/tile_width
     contention_enabled: bool = True         # network/emesh_hop_by_hop/queue_model/enabled
-    queue_type: int = 0                     # history_tree
+    queue_type: int = 0                     # QUEUE_HISTORY_TREE / QUEUE_BASIC / QUEUE_HISTORY_LIST
     analytical_enabled: bool = True         # queue_model/history_tree/analytical_model_enabled
     max_list_size: int = 100                # queue_model/history_tree/max_list_size
     broadcast_tree_enabled: bool = True
     device: int = 0
+    # queue_model/history_list/interleaving_enabled: no effect on in-order requests
+    # (include/gnoc.h); kept so the oracle can restate the list with it on or off
+    interleaving_enabled: bool = True
 
     @property
     def width(self) -> int:
@@ -177,7 +181,7 @@ class EngineConfig:
 
     def to_c(self) -> GnocConfig:
         c = GnocConfig()
-        for f in GnocConfig._fields_:
+        for f in GnocConfig._fields_:   # interleaving_enabled is not an engine key
             v = getattr(self, f[0])
             setattr(c, f[0], int(v) if not isinstance(v, float) else v)
         return c

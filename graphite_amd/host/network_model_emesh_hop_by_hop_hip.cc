@@ -49,9 +49,15 @@ gnoc_config CfgView::toEngineConfig() const
    c.link_delay = (uint64_t) getInt("network/emesh_hop_by_hop/link/delay", 1);                    // :96
    c.contention_enabled = getBool("network/emesh_hop_by_hop/queue_model/enabled", true);          // :97
    const std::string qt = getString("network/emesh_hop_by_hop/queue_model/type", "history_tree"); // :98
-   c.queue_type = qt == "history_tree" ? GNOC_QUEUE_HISTORY_TREE : -1;
-   c.analytical_enabled = getBool("queue_model/history_tree/analytical_model_enabled", true);    // carbon_sim.cfg:392
-   c.max_list_size = getInt("queue_model/history_tree/max_list_size", 100);                     // carbon_sim.cfg:391
+   // QueueModel::create (queue_model.cc:18-38) and each model's keys (carbon_sim.cfg:376-392)
+   c.queue_type = qt == "history_tree" ? GNOC_QUEUE_HISTORY_TREE
+                : qt == "basic" ? GNOC_QUEUE_BASIC
+                : qt == "history_list" ? GNOC_QUEUE_HISTORY_LIST : -1;
+   const std::string qk = qt == "history_list" ? "queue_model/history_list/" : "queue_model/history_tree/";
+   c.analytical_enabled = getBool(qk + "analytical_model_enabled", true);
+   c.max_list_size = getInt(qk + "max_list_size", 100);
+   if (c.queue_type == GNOC_QUEUE_BASIC && getBool("queue_model/basic/moving_avg_enabled", true))
+      c.queue_type = -2;   // a running FP64 window mean: not implemented (include/gnoc.h)
    c.tile_width_mm = getFloat("general/tile_width", 1.0);                                        // carbon_sim.cfg:64
    c.frequency_ghz = getFloat("network/frequency", 1.0);   // the network's DVFS domain (dvfs_manager.cc:243-250)
    return c;
@@ -71,8 +77,10 @@ NetworkModelEMeshHopByHopHIP::NetworkModelEMeshHopByHopHIP(const CfgView& cfg, i
 
 NetworkModelEMeshHopByHopHIP::NetworkModelEMeshHopByHopHIP(const gnoc_config& cfg) : _cfg(cfg)
 {
-   if (_cfg.queue_type != GNOC_QUEUE_HISTORY_TREE)
-      throw NetworkModelError(GNOC_EUNSUPPORTED, "queue_model/type: only history_tree is implemented");
+   if (_cfg.queue_type == -2)
+      throw NetworkModelError(GNOC_EUNSUPPORTED, "queue_model/basic with moving_avg_enabled is not implemented");
+   if (_cfg.queue_type < 0)
+      throw NetworkModelError(GNOC_EINVAL, "queue_model/type: unrecognized queue model");   // queue_model.cc:33-36
    const int rc = gnoc_create(&_cfg, &_eng);
    if (rc)
       throw NetworkModelError(rc, "gnoc_create rejected the emesh_hop_by_hop configuration (status " +

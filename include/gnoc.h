@@ -48,8 +48,21 @@ extern "C" {
 #define GNOC_EUNSUPPORTED  -5   /* valid for the reference, not implemented here   */
 #define GNOC_ENOMEM        -6
 
-/* queue model types, QueueModel::create (common/shared_models/queue_model.cc:18-38) */
+/* queue model types, QueueModel::create (common/shared_models/queue_model.cc:18-38).
+ * Every queue on this path sees its requests in non-decreasing time order (the
+ * reference's event loop is keyed (time, packet id)), so:
+ *   history_tree  the FIFO recurrence plus the serial M/G/1 prefix
+ *   basic         queue_model_basic.cc:35-61 with moving_avg_enabled = false:
+ *                 the plain FIFO recurrence, no analytical model
+ *   history_list  queue_model_history_list.cc:39-146: the same behaviour as the
+ *                 tree for max_list_size >= 2, with or without interleaving (an
+ *                 in-order request never fits an earlier gap); max_list_size and
+ *                 analytical_model_enabled are read from queue_model/history_list
+ * basic with a moving average (carbon_sim.cfg:376-379) returns GNOC_EUNSUPPORTED
+ * at the plug-in: its reference time is a running FP64 window mean. */
 #define GNOC_QUEUE_HISTORY_TREE 0
+#define GNOC_QUEUE_BASIC        1
+#define GNOC_QUEUE_HISTORY_LIST 2
 
 /* per-packet flags */
 #define GNOC_PKT_UNMODELED  0x1u   /* NetworkModel::isModelEnabled() == false
@@ -79,8 +92,8 @@ typedef struct gnoc_config
    double   tile_width_mm;         /* general/tile_width                                                */
    int32_t  contention_enabled;    /* network/emesh_hop_by_hop/queue_model/enabled                      */
    int32_t  queue_type;            /* network/emesh_hop_by_hop/queue_model/type (GNOC_QUEUE_*)          */
-   int32_t  analytical_enabled;    /* queue_model/history_tree/analytical_model_enabled                 */
-   int32_t  max_list_size;         /* queue_model/history_tree/max_list_size (>= 2)                     */
+   int32_t  analytical_enabled;    /* queue_model/<type>/analytical_model_enabled (tree, list)          */
+   int32_t  max_list_size;         /* queue_model/<type>/max_list_size (>= 2; unused by basic)          */
    int32_t  broadcast_tree_enabled;/* network/emesh_hop_by_hop/broadcast_tree_enabled (parsed only)     */
    int32_t  device;                /* HIP device ordinal                                                */
 } gnoc_config;

@@ -16,6 +16,10 @@
  *     search; DESIGN.md and tests/test_oracle.py pin this equivalence
  *     against the real IntervalTree compiled from the reference
  *     (oracle/_ref, see oracle/Makefile).
+ *   - QueueModelHistoryList::computeQueueDelay / computeUsingHistoryList
+ *       common/shared_models/queue_models/queue_model_history_list.cc:39-146
+ *   - QueueModelBasic::computeQueueDelay (moving average disabled)
+ *       common/shared_models/queue_models/queue_model_basic.cc:35-61
  *   - QueueModelMG1::computeQueueDelay / updateQueue
  *       common/shared_models/queue_models/queue_model_m_g_1.cc:17-56
  *   - Latency::toPicosec / Time::toCycles   common/misc/time_types.h:81-109
@@ -69,8 +73,13 @@ ORC_EXPORT uint64_t orc_time_to_cycles(uint64_t p, double f) { return time_to_cy
 /* ------------------------------------------------------------------------ */
 typedef struct { uint64_t first, second; } orc_interval;
 
+enum { ORC_Q_HISTORY_TREE = 0, ORC_Q_BASIC = 1, ORC_Q_HISTORY_LIST = 2 };   /* include/gnoc.h GNOC_QUEUE_* */
+
 typedef struct
 {
+   int type;              /* QueueModel::Type, queue_model.cc:18-38        */
+   int interleaving;      /* queue_model/history_list/interleaving_enabled */
+   uint64_t queue_time;   /* QueueModelBasic::_queue_time                  */
    orc_interval *iv;      /* free intervals, sorted by .first, disjoint    */
    int n;                 /* IntervalTree::_size                           */
    int max_list_size;     /* queue_model/history_tree/max_list_size        */
@@ -84,12 +93,20 @@ typedef struct
    uint64_t total_requests, util_cycles, last_request_time; /* queue_model.cc:40-53 */
 } orc_queue;
 
-ORC_EXPORT orc_queue *orc_queue_create(int max_list_size, int analytical, uint64_t min_proc)
+/* QueueModel::create(type, min_processing_time), queue_model.cc:18-38.
+ * basic: moving average disabled (queue_model_basic.cc:7-30 with
+ * moving_avg_enabled = false); history_list: queue_model_history_list.cc:10-32. */
+ORC_EXPORT orc_queue *orc_queue_create_type(int type, int max_list_size, int analytical, int interleaving,
+                                            uint64_t min_proc)
 {
-   if (max_list_size < 2 || min_proc < 1)
+   if (type != ORC_Q_BASIC && (max_list_size < 2 || min_proc < 1))
       return NULL; /* reference aborts / corrupts its tree for these */
+   if (type < 0 || type > 2) return NULL;
+   if (type == ORC_Q_BASIC) max_list_size = 1;
    orc_queue *q = (orc_queue *) calloc(1, sizeof(orc_queue));
-   q->iv = (orc_interval *) calloc((size_t) max_list_size + 1, sizeof(orc_interval));
+   q->type = type;
+   q->interleaving = interleaving;
+   q->iv = (orc_interval *) calloc((size_t) max_list_size + 2, sizeof(orc_interval));
    q->max_list_size = max_list_size;
    q->analytical = analytical;
    q->min_proc = min_proc;
@@ -98,6 +115,11 @@ ORC_EXPORT orc_queue *orc_queue_create(int max_list_size, int analytical, uint64
    q->iv[0].second = UINT64_MAX;
    q->n = 1;
    return q;
+}
+
+ORC_EXPORT orc_queue *orc_queue_create(int max_list_size, int analytical, uint64_t min_proc)
+{
+   return orc_queue_create_type(ORC_Q_HISTORY_TREE, max_list_size, analytical, 0, min_proc);
 }
 
 ORC_EXPORT void orc_queue_destroy(orc_queue *q)
@@ -164,9 +186,121 @@ static void mg1_update(orc_queue *q, uint64_t t, uint64_t p, uint64_t d)
    q->newest = (q->newest > nw) ? q->newest : nw;
 }
 
+static void util_update(orc_queue *q, uint64_t t, uint64_t p, uint64_t d)
+{
+   /* queue_model.cc:48-53 updateQueueUtilizationCounters */
+   q->util_cycles += p;
+   uint64_t lr = t + d + p;
+   q->last_request_time = (q->last_request_time > lr) ? q->last_request_time : lr;
+   q->total_requests++;
+}
+
+static void iv_insert_at(orc_queue *q, int i, orc_interval v)
+{
+   memmove(&q->iv[i + 1], &q->iv[i], (size_t) (q->n - i) * sizeof(orc_interval));
+   q->iv[i] = v;
+   q->n++;
+}
+
+/* QueueModelHistoryList::computeUsingHistoryList, queue_model_history_list.cc:70-146.
+ * The std::list walk is restated over the sorted array with an index; after an
+ * erase the reference's iterator steps back (curr_it--), and stepping back
+ * from begin() lands on the list's end sentinel, whose successor is begin(). */
+static uint64_t hl_compute(orc_queue *q, uint64_t pkt_time, uint64_t processing_time)
+{
+   const uint64_t m = q->min_proc;
+   uint64_t queue_delay = 0;
+   for (int i = 0; i < q->n; i++)
+   {
+      const orc_interval iv = q->iv[i];
+      if ((pkt_time >= iv.first) && ((pkt_time + processing_time) <= iv.second))
+      {
+         /* :82-96 no additional delay */
+         iv_remove(q, i);
+         int at = i;
+         if ((pkt_time - iv.first) >= m) { orc_interval a = { iv.first, pkt_time }; iv_insert_at(q, at++, a); }
+         if ((iv.second - (pkt_time + processing_time)) >= m)
+         {
+            orc_interval b = { pkt_time + processing_time, iv.second };
+            iv_insert_at(q, at, b);
+         }
+         break;
+      }
+      else if ((pkt_time < iv.first) && ((iv.first + processing_time) <= iv.second))
+      {
+         /* :97-108 wait for the interval */
+         queue_delay += (iv.first - pkt_time);
+         iv_remove(q, i);
+         if ((iv.second - (iv.first + processing_time)) >= m)
+         {
+            orc_interval b = { iv.first + processing_time, iv.second };
+            iv_insert_at(q, i, b);
+         }
+         break;
+      }
+      else if (q->interleaving)
+      {
+         if ((pkt_time >= iv.first) && (pkt_time < iv.second))
+         {
+            /* :111-123 (processing_time -= 0: pkt_time is reassigned first) */
+            iv_remove(q, i);
+            if ((pkt_time - iv.first) >= m)
+            {
+               orc_interval a = { iv.first, pkt_time };
+               iv_insert_at(q, i, a);
+               /* curr_it-- from the element after the insert: the inserted one */
+            }
+            else
+               i--;
+            pkt_time = iv.second;
+            processing_time -= (iv.second - pkt_time);
+         }
+         else if (pkt_time < iv.first)
+         {
+            /* :124-134 */
+            iv_remove(q, i);
+            i--;
+            queue_delay += (iv.first - pkt_time);
+            pkt_time = iv.second;
+            processing_time -= (iv.second - iv.first);
+         }
+      }
+   }
+   if (q->n > q->max_list_size) iv_remove(q, 0);   /* :138-141 */
+   return queue_delay;
+}
+
+/* QueueModelHistoryList::computeQueueDelay, queue_model_history_list.cc:39-68 */
+static uint64_t hl_queue_delay(orc_queue *q, uint64_t t, uint64_t p)
+{
+   uint64_t d;
+   if (q->analytical && ((t + p) < q->iv[0].first))
+   {
+      q->mg1_uses++;
+      d = mg1_delay(q);
+   }
+   else
+      d = hl_compute(q, t, p);
+   mg1_update(q, t, p, d);
+   util_update(q, t, p, d);
+   return d;
+}
+
+/* QueueModelBasic::computeQueueDelay without moving average, queue_model_basic.cc:35-61 */
+static uint64_t basic_queue_delay(orc_queue *q, uint64_t t, uint64_t p)
+{
+   const uint64_t ref_time = t;
+   const uint64_t d = (q->queue_time > ref_time) ? (q->queue_time - ref_time) : 0;
+   q->queue_time = ((q->queue_time > ref_time) ? q->queue_time : ref_time) + p;
+   util_update(q, ref_time, p, d);
+   return d;
+}
+
 /* QueueModelHistoryTree::computeQueueDelay, queue_model_history_tree.cc:43-126 */
 ORC_EXPORT uint64_t orc_queue_compute(orc_queue *q, uint64_t t, uint64_t p)
 {
+   if (q->type == ORC_Q_BASIC) return basic_queue_delay(q, t, p);
+   if (q->type == ORC_Q_HISTORY_LIST) return hl_queue_delay(q, t, p);
    uint64_t d = UINT64_MAX;
    const uint64_t m = q->min_proc;
 
@@ -219,11 +353,7 @@ ORC_EXPORT uint64_t orc_queue_compute(orc_queue *q, uint64_t t, uint64_t p)
    /* :118  M/G/1 statistics are updated on every request */
    mg1_update(q, t, p, d);
 
-   /* queue_model.cc:48-53 updateQueueUtilizationCounters */
-   q->util_cycles += p;
-   uint64_t lr = t + d + p;
-   q->last_request_time = (q->last_request_time > lr) ? q->last_request_time : lr;
-   q->total_requests++;
+   util_update(q, t, p, d);
    return d;
 }
 
@@ -285,7 +415,8 @@ static heap_ent heap_pop(heap_t *h)
  * _last_request_time of each port's queue (queue_model.cc:49-53). */
 ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
                        uint64_t router_delay, uint64_t link_delay, double frequency,
-                       int contention_enabled, int analytical_enabled, int max_list_size,
+                       int contention_enabled, int queue_type, int interleaving, int analytical_enabled,
+                       int max_list_size,
                        size_t n, const uint64_t *inject_ps, const uint32_t *src,
                        const uint32_t *dst, const uint32_t *bits, const uint32_t *flags,
                        uint64_t *final_ps, uint64_t *zero_load_ps, uint64_t *contention_ps,
@@ -294,7 +425,7 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
 {
    const int W = mesh_width, H = mesh_height;
    if (W <= 0 || H <= 0 || flit_width <= 0 || frequency <= 0.0) return -1;
-   if (contention_enabled && max_list_size < 2) return -1;
+   if (contention_enabled && queue_type != ORC_Q_BASIC && max_list_size < 2) return -1;
    const uint32_t N = (uint32_t) (W * H);
    const size_t nports = (size_t) N * PORTS_PER_TILE;
 
@@ -309,7 +440,10 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
    {
       q = (orc_queue **) calloc(nports, sizeof(orc_queue *));
       for (size_t p = 0; p < nports; p++)
-         q[p] = orc_queue_create(max_list_size, analytical_enabled, 1);
+      {
+         q[p] = orc_queue_create_type(queue_type, max_list_size, analytical_enabled, interleaving, 1);
+         if (!q[p]) return -1;
+      }
    }
    memset(port_sum_delay, 0, nports * sizeof(uint64_t));
    memset(port_count, 0, nports * sizeof(uint64_t));

@@ -52,8 +52,10 @@ def lib() -> ctypes.CDLL:
         L.orc_lat_to_ps.argtypes = [u64, ctypes.c_double]
         L.orc_time_to_cycles.restype = u64
         L.orc_time_to_cycles.argtypes = [u64, ctypes.c_double]
+        L.orc_queue_create_type.restype = vp
+        L.orc_queue_create_type.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, u64]
         L.orc_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u64, u64, ctypes.c_double, ctypes.c_int,
-                              ctypes.c_int, ctypes.c_int, ctypes.c_size_t] + [vp] * 13
+                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t] + [vp] * 13
         _orc = L
     return _orc
 
@@ -85,13 +87,16 @@ def ref_lib() -> ctypes.CDLL | None:
 
 
 class Queue:
-    """QueueModelHistoryTree(min_processing_time=1) restated (oracle)."""
+    """QueueModelHistoryTree / QueueModelHistoryList / QueueModelBasic
+    (min_processing_time=1) restated (oracle).  kind: 0 history_tree, 1 basic
+    (no moving average), 2 history_list."""
 
-    def __init__(self, max_list_size: int = 100, analytical: bool = True, min_proc: int = 1):
+    def __init__(self, max_list_size: int = 100, analytical: bool = True, min_proc: int = 1, kind: int = 0,
+                 interleaving: bool = True):
         self.L = lib()
-        self.h = self.L.orc_queue_create(max_list_size, int(analytical), min_proc)
+        self.h = self.L.orc_queue_create_type(kind, max_list_size, int(analytical), int(interleaving), min_proc)
         if not self.h:
-            raise ValueError("invalid history_tree parameters")
+            raise ValueError("invalid queue model parameters")
 
     def compute(self, t: int, p: int) -> int:
         return int(self.L.orc_queue_compute(self.h, t, p))
@@ -134,7 +139,8 @@ def run(cfg, tr) -> OracleResult:
     npt = W * H * 6
     ps, pc, pm, pf, pl = (np.zeros(npt, np.uint64) for _ in range(5))
     rc = L.orc_run(W, H, cfg.flit_width, cfg.router_delay, cfg.link_delay, cfg.frequency_ghz,
-                   int(cfg.contention_enabled), int(cfg.analytical_enabled), cfg.max_list_size, n,
+                   int(cfg.contention_enabled), int(getattr(cfg, "queue_type", 0)),
+                   int(getattr(cfg, "interleaving_enabled", True)), int(cfg.analytical_enabled), cfg.max_list_size, n,
                    inj.ctypes.data, src.ctypes.data, dst.ctypes.data, bits.ctypes.data, flags.ctypes.data,
                    fin.ctypes.data, zl.ctypes.data, ct.ctypes.data, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data,
                    pf.ctypes.data, pl.ctypes.data)

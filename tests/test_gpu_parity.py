@@ -231,3 +231,18 @@ def test_small_chunks_32x32_hotspot(chunk, monkeypatch):
     tr = gnoc.synthetic_trace(32, 32, 0.01, 100, seed=8, hotspot_fraction=0.2, num_hotspots=16)
     got, ref = run_both(cfg, tr)
     assert_same(got, ref)
+
+
+@pytest.mark.parametrize("qtype,L,inter", [(gnoc.QUEUE_BASIC, 100, True), (gnoc.QUEUE_HISTORY_LIST, 2, True),
+                                           (gnoc.QUEUE_HISTORY_LIST, 3, False), (gnoc.QUEUE_HISTORY_LIST, 100, True)])
+def test_queue_models_basic_and_history_list(qtype, L, inter):
+    """QueueModel::create's other types (queue_model.cc:18-38) against the
+    oracle's restatements of queue_model_basic.cc / queue_model_history_list.cc."""
+    cfg = gnoc.EngineConfig(num_tiles=64, queue_type=qtype, max_list_size=L, interleaving_enabled=inter)
+    tr = random_trace(20000, 8, 8, seed=3, max_cycle=300, burst0=400)
+    got, ref = run_both(cfg, tr)
+    if qtype == gnoc.QUEUE_HISTORY_LIST:
+        assert ref.port_mg1.sum() > 0
+    else:
+        assert ref.port_mg1.sum() == 0
+    assert_same(got, ref)

@@ -90,3 +90,50 @@ def test_network_golden(name):
     res = oracle.run(cfg, tr)
     for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1"):
         assert np.array_equal(getattr(res, k), z[k]), k
+
+
+# --- the other queue models of QueueModel::create (queue_model.cc:18-38) -------------
+
+def _sorted_stream(seed, n=3000, burst=40):
+    rng = np.random.default_rng(seed)
+    t = np.sort(rng.integers(0, n // 3, n))
+    t[:burst] = 0
+    p = rng.integers(1, 12, n)
+    return np.sort(t), p
+
+
+@pytest.mark.parametrize("L", [2, 3, 4, 7, 100])
+@pytest.mark.parametrize("interleaving", [False, True])
+def test_history_list_is_the_tree_on_in_order_requests(L, interleaving):
+    """In-order requests never fit an earlier gap, so the list (with or without
+    interleaving) gives the tree's delays and M/G/1 uses; its after-insert
+    pruning makes max_list_size 2 behave like the tree's >= 3."""
+    for seed in range(4):
+        t, p = _sorted_stream(seed)
+        ql = oracle.Queue(L, True, kind=2, interleaving=interleaving)
+        qt = oracle.Queue(max(L, 3), True, kind=0)
+        dl = [ql.compute(int(a), int(b)) for a, b in zip(t, p)]
+        dt = [qt.compute(int(a), int(b)) for a, b in zip(t, p)]
+        assert dl == dt
+        assert ql.mg1_uses == qt.mg1_uses
+
+
+def test_basic_is_the_fifo_recurrence():
+    for seed in range(4):
+        t, p = _sorted_stream(seed)
+        qb = oracle.Queue(kind=1)
+        X, want = 0, []
+        for a, b in zip(t, p):
+            want.append(max(X - int(a), 0))
+            X = max(X, int(a)) + int(b)
+        assert [qb.compute(int(a), int(b)) for a, b in zip(t, p)] == want
+        assert qb.mg1_uses == 0
+
+
+def test_history_list_out_of_order_uses_gaps():
+    """Out of order (not produced on this path, but the restatement covers it):
+    a request fits an earlier gap, and with interleaving spans gaps."""
+    q = oracle.Queue(100, False, kind=2, interleaving=False)
+    assert q.compute(10, 5) == 0      # busy [10, 15), gap [0, 10)
+    assert q.compute(2, 3) == 0       # fits the gap
+    assert q.compute(12, 4) == 3      # waits for 15
