@@ -151,7 +151,7 @@ __device__ __forceinline__ void lv_st(uint64_t* p, uint64_t v)
 
 // Hop-record stores are plain stores: a wave's 16-B records for one next port
 // land on nearby lines and combine in L2 before they reach HBM (write-through
-// sc1 stores measured 37% slower on 32x32).
+// sc1 stores measured 37% slower on 32x32, nontemporal stores 2x slower).
 __device__ __forceinline__ void lv_store_rec(Rec* p, uint64_t t, uint32_t id, uint32_t aux)
 {
    Rec o;

@@ -1,7 +1,3 @@
 cd /root/repo
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > gpurun_out/pytest_q2.log 2>&1
-rc=$?
-tail -3 gpurun_out/pytest_q2.log
-grep -E "^FAILED|^E " gpurun_out/pytest_q2.log | head -8
-exit $rc
+VTAG=_32 bash tools/bench_variants.sh && VTAG=_64 bash tools/bench_variants.sh --workload sharded
