@@ -67,6 +67,9 @@ struct DevCfg
    // independent BW x BH blocks, one per sweep point, each with its own R + Lk
    // and flit width.  A single mesh is one block (pt_rl == nullptr).
    uint32_t BW, BH, BX;
+   // NetworkModelEMeshHopCounter (network_model_emesh_hop_counter.cc:143-157):
+   // no routers or queues, latency Latency(H * (R + Lk)) in one conversion
+   int hop_counter;
    const uint64_t* pt_rl;   // per point Latency(R + Lk).toPicosec()
    const uint32_t* pt_fw;   // per point flit width
 };

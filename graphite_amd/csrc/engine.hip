@@ -339,6 +339,7 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    d.BW = d.W;
    d.BH = d.H;
    d.BX = 1;
+   d.hop_counter = 0;
    d.pt_rl = nullptr;
    d.pt_fw = nullptr;
    build_static_levels(e);
@@ -430,6 +431,35 @@ int gnoc_create_sweep(const gnoc_config* base, const gnoc_point* points, int32_t
       gnoc_destroy(e);
       return GNOC_EHIP;
    }
+   *out = e;
+   return GNOC_OK;
+}
+
+int gnoc_create_hop_counter(const gnoc_config* cfg, gnoc_engine** out)
+{
+   if (!cfg || !out) return GNOC_EINVAL;
+   *out = nullptr;
+   gnoc_config c = *cfg;
+   // NetworkModelEMeshHopCounter ctor (network_model_emesh_hop_counter.cc:11-41, 50-94)
+   if (c.num_tiles <= 0) return GNOC_EINVAL;
+   if (c.link_delay != 1) return GNOC_EINVAL;   // :77 LOG_ASSERT_ERROR(link_delay == 1)
+   const int32_t w = (int32_t) std::floor(std::sqrt((double) c.num_tiles));
+   const int32_t h = (int32_t) std::ceil(1.0 * c.num_tiles / w);
+   // the engine's arrays cover the whole w x h grid; tiles >= num_tiles carry no packets
+   c.mesh_width = w;
+   c.mesh_height = h;
+   const int32_t app = c.num_tiles;
+   c.num_tiles = w * h;
+   c.tile_width_mm = 1.0 / c.frequency_ghz;   // the link identity gnoc_create checks; the hop counter has none
+   c.link_delay = (uint64_t) std::ceil(c.frequency_ghz * 0.01 * c.tile_width_mm);
+   c.contention_enabled = 0;                   // no queues (:61 "contention is not modeled")
+   gnoc_engine* e = nullptr;
+   int rc = gnoc_create(&c, &e);
+   if (rc) return rc;
+   e->dc.Lk = 1;
+   e->dc.hop_counter = 1;
+   e->cfg.num_tiles = app;
+   e->cfg.link_delay = 1;
    *out = e;
    return GNOC_OK;
 }

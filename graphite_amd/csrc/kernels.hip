@@ -556,7 +556,8 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
       const uint64_t hops = (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
       // Hop::Hop accumulates Latency(0) at injection, Latency(R+Lk) per mesh router,
       // Latency(F) at receive (network_model.cc:142-150, 556-563).
-      const uint64_t z = ps_of<F1>(0, c.f) + hops * rl_of(c, src[i]) + ps_of<F1>(aux_F(aux[i]), c.f);
+      const uint64_t z = c.hop_counter ? ps_of<F1>((hops - 1) * (c.R + c.Lk), c.f) + ps_of<F1>(aux_F(aux[i]), c.f)
+                                       : ps_of<F1>(0, c.f) + hops * rl_of(c, src[i]) + ps_of<F1>(aux_F(aux[i]), c.f);
       zl[i] = z;
       if (closed_form) final_ps[i] = inj[i] + z;
       cont[i] = final_ps[i] - inj[i] - z;

@@ -36,7 +36,7 @@ EXPORTED = (
     "gnoc_last_error", "gnoc_destroy", "gnoc_trace_synthetic", "gnoc_abi_version",
     "gnoc_set_profiling", "gnoc_get_kernel_stats", "gnoc_trace_file_write", "gnoc_trace_file_read",
     "gnoc_shard", "gnoc_exchange_counts", "gnoc_run_begin", "gnoc_run_finish",
-    "gnoc_create_sweep", "gnoc_sweep_layout", "gnoc_get_port_utilization",
+    "gnoc_create_sweep", "gnoc_sweep_layout", "gnoc_get_port_utilization", "gnoc_create_hop_counter",
 )
 
 
@@ -134,6 +134,7 @@ def load() -> ctypes.CDLL:
     lib.gnoc_create_sweep.argtypes = [ctypes.POINTER(GnocConfig), ctypes.POINTER(GnocPoint), ctypes.c_int32,
                                       ctypes.POINTER(vp)]
     lib.gnoc_sweep_layout.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
+    lib.gnoc_create_hop_counter.argtypes = [ctypes.POINTER(GnocConfig), ctypes.POINTER(vp)]
     lib.gnoc_shard.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
     lib.gnoc_exchange_counts.argtypes = [vp, vp, vp, sz]
     lib.gnoc_run_begin.argtypes = [vp, vp]
@@ -272,14 +273,21 @@ class Results:
 
 
 class Engine:
-    """One engine handle per GPU (gnoc_create)."""
+    """One engine handle per GPU (gnoc_create; model="emesh_hop_counter":
+    gnoc_create_hop_counter)."""
 
-    def __init__(self, cfg: EngineConfig):
+    def __init__(self, cfg: EngineConfig, model: str = "emesh_hop_by_hop"):
         self.lib = load()
         self.cfg = cfg
         self._h = ctypes.c_void_p()
         c = cfg.to_c()
-        rc = self.lib.gnoc_create(ctypes.byref(c), ctypes.byref(self._h))
+        create = self.lib.gnoc_create_hop_counter if model == "emesh_hop_counter" else self.lib.gnoc_create
+        rc = create(ctypes.byref(c), ctypes.byref(self._h))
+        if model == "emesh_hop_counter":
+            import math
+            w = int(math.floor(math.sqrt(cfg.num_tiles)))
+            from dataclasses import replace
+            self.cfg = replace(cfg, mesh_width=w, mesh_height=int(math.ceil(cfg.num_tiles / w)))
         if rc:
             raise GnocError(rc, "gnoc_create rejected the configuration")
         self._n = 0

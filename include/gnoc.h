@@ -182,6 +182,14 @@ int gnoc_set_profiling(gnoc_engine *eng, int enable);
 int gnoc_get_kernel_stats(gnoc_engine *eng, const char **names, double *total_ms,
                           uint32_t *launches, size_t cap, size_t *count);
 
+/* ---- emesh_hop_counter (network_model_emesh_hop_counter.cc) ---------------
+ * The contention-free mesh model: a packet's latency is
+ * Latency(H * (router_delay + link_delay)), H = Manhattan distance (:143-157),
+ * plus the receive serialization of NetworkModel::processReceivedPacket; no
+ * per-port counters.  link_delay must be 1 (:77); mesh_width/height and
+ * tile_width are ignored (floor(sqrt(N)) x ceil(N / W), :18-19). */
+int gnoc_create_hop_counter(const gnoc_config *cfg, gnoc_engine **out);
+
 /* ---- design-space sweep --------------------------
  * npoints independent simulations of the same mesh size, each with its own
  * flit width, router delay and link delay (the carbon_sim.cfg keys a sweep

@@ -568,3 +568,33 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
    free(pnode);
    return 0;
 }
+
+/* ------------------------------------------------------------------------ */
+/* NetworkModelEMeshHopCounter::routePacket, network_model_emesh_hop_counter.cc:143-157,
+ * with NetworkModel::__routePacket / __processReceivedPacket (network_model.cc:87-150):
+ * one hop SEND_TILE -> RECEIVE_TILE of Latency(H * (R + Lk)), then + Latency(F). */
+ORC_EXPORT int orc_run_hop_counter(int num_tiles, int flit_width, uint64_t router_delay, uint64_t link_delay,
+                                   double frequency, size_t n, const uint64_t *inject_ps, const uint32_t *src,
+                                   const uint32_t *dst, const uint32_t *bits, const uint32_t *flags,
+                                   uint64_t *final_ps, uint64_t *zero_load_ps, uint64_t *contention_ps)
+{
+   if (num_tiles <= 0 || flit_width <= 0 || link_delay != 1) return -1;
+   const int W = (int) floor(sqrt((double) num_tiles));
+   for (size_t i = 0; i < n; i++)
+   {
+      if (src[i] >= (uint32_t) num_tiles || dst[i] >= (uint32_t) num_tiles) return -2;
+      contention_ps[i] = 0;
+      zero_load_ps[i] = 0;
+      final_ps[i] = inject_ps[i];
+      if (src[i] == dst[i] || (flags[i] & ORC_FLAG_UNMODELED)) continue;   /* corner cases / model disabled */
+      const int sx = (int) src[i] % W, sy = (int) src[i] / W, dx = (int) dst[i] % W, dy = (int) dst[i] / W;
+      const uint64_t hops = (uint64_t) (abs(sx - dx) + abs(sy - dy));
+      const uint32_t F = (bits[i] % (uint32_t) flit_width) ? bits[i] / (uint32_t) flit_width + 1
+                                                           : bits[i] / (uint32_t) flit_width;
+      const uint64_t lat = lat_to_ps(hops * (router_delay + link_delay), frequency);
+      const uint64_t ser = lat_to_ps(F, frequency);
+      zero_load_ps[i] = lat + ser;
+      final_ps[i] = inject_ps[i] + lat + ser;
+   }
+   return 0;
+}

@@ -112,6 +112,25 @@ class Queue:
             pass
 
 
+def run_hop_counter(cfg, tr) -> "OracleResult":
+    """NetworkModelEMeshHopCounter restated (gnoc_oracle.c orc_run_hop_counter)."""
+    L = lib()
+    u64, vp = ctypes.c_uint64, ctypes.c_void_p
+    L.orc_run_hop_counter.argtypes = [ctypes.c_int, ctypes.c_int, u64, u64, ctypes.c_double, ctypes.c_size_t] + [vp] * 8
+    n = int(tr.inject_ps.shape[0])
+    arrs = [np.ascontiguousarray(a, t) for a, t in ((tr.inject_ps, np.uint64), (tr.src, np.uint32),
+                                                    (tr.dst, np.uint32), (tr.bits, np.uint32))]
+    flags = np.ascontiguousarray(tr.flags if tr.flags is not None else np.zeros(n, np.uint32), np.uint32)
+    fin, zl, ct = (np.zeros(n, np.uint64) for _ in range(3))
+    rc = L.orc_run_hop_counter(cfg.num_tiles, cfg.flit_width, cfg.router_delay, cfg.link_delay, cfg.frequency_ghz, n,
+                               *[a.ctypes.data for a in arrs], flags.ctypes.data, fin.ctypes.data, zl.ctypes.data,
+                               ct.ctypes.data)
+    if rc:
+        raise ValueError(f"oracle rejected input (rc={rc})")
+    z = np.zeros(0, np.uint64)
+    return OracleResult(fin, zl, ct, z, z, z)
+
+
 @dataclass
 class OracleResult:
     final_ps: np.ndarray

@@ -246,3 +246,24 @@ def test_queue_models_basic_and_history_list(qtype, L, inter):
     else:
         assert ref.port_mg1.sum() == 0
     assert_same(got, ref)
+
+
+@pytest.mark.parametrize("N,R,f", [(64, 1, 1.0), (12, 0, 1.0), (10, 2, 0.9), (1024, 3, 1.5)])
+def test_emesh_hop_counter_model(N, R, f):
+    """NetworkModelEMeshHopCounter (network_model_emesh_hop_counter.cc:143-157):
+    the contention-free model, including non-rectangular tile counts."""
+    import math
+    cfg = gnoc.EngineConfig(num_tiles=N, router_delay=R, frequency_ghz=f)
+    w = int(math.floor(math.sqrt(N)))
+    tr = random_trace(3000, w, int(math.ceil(N / w)), seed=N + R, max_cycle=500, self_frac=0.05, unmodeled_frac=0.05,
+                      bits_choices=[72, 576, 1088], frequency_ghz=f)
+    ok = (tr.src < N) & (tr.dst < N)
+    tr = gnoc.Trace(tr.inject_ps[ok], tr.src[ok], tr.dst[ok], tr.bits[ok], tr.flags[ok])
+    eng = gnoc.Engine(cfg, model="emesh_hop_counter")
+    eng.submit(tr)
+    eng.run()
+    got = eng.results()
+    eng.close()
+    ref = oracle.run_hop_counter(cfg, tr)
+    for k in ("final_ps", "zero_load_ps", "contention_ps"):
+        assert np.array_equal(getattr(got, k), getattr(ref, k)), k
