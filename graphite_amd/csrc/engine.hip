@@ -89,7 +89,7 @@ struct gnoc_engine
    // work
    DevBuf aux, routed, final_ps, zl, cont;
    DevBuf hist, tot, slot_cnt, slot_base, counters, gtot;
-   DevBuf recs, samp_t, samp_id, Hs, Pp, Prow, pcol, nexc, dirty;
+   DevBuf recs, samp_t, samp_id, Hs, Pp, Prow, pcol, nexc, dirty, span;
    DevBuf pio, pnc, pgb, lvl_cbase, lvl_qb, cdesc, flags, st, lvl_ctr;
    DevBuf port_sum, port_cnt, port_mg1, port_flit, port_last, plan_ports, stamps, done;
    uint64_t h_chunk_bound = 0;
@@ -927,9 +927,16 @@ static int run_prep(gnoc_engine* e, bool* done)
    GNOC_LAUNCH(e, KC_SRC_OFFS, k_src_offs, dim3(ng), dim3(256), 0, s, N, nch, e->hist.as<uint32_t>(),
                e->slot_base.as<uint64_t>(), pr0 * W, pr1 * W);
    if (n && N <= SC4_MAXN)
-      GNOC_LAUNCH(e, KC_SCATTER, k_scatter4, dim3(nch), dim3(256), 4 * N * 4, s, (uint64_t) n, pch, N, nbits, e->d_src,
-                  e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(), e->recs.as<Rec>(),
-                  e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>());
+   {
+      const int nw = scatter_waves(N);
+#define GNOC_SCATTER(NWV)                                                                                                 \
+   GNOC_LAUNCH(e, KC_SCATTER, k_scatter4<NWV>, dim3(nch), dim3(64 * NWV), (size_t) NWV * N * 4, s, (uint64_t) n, pch, N, \
+               nbits, e->d_src, e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(),        \
+               e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>())
+      if (nw == 8) GNOC_SCATTER(8);
+      else GNOC_SCATTER(4);
+#undef GNOC_SCATTER
+   }
    else if (n)
       GNOC_LAUNCH(e, KC_SCATTER, k_scatter, dim3(nch), dim3(64), N * 4, s, (uint64_t) n, pch, N, nbits, e->d_src,
                   e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(), e->recs.as<Rec>(),
@@ -954,8 +961,20 @@ static int run_prep(gnoc_engine* e, bool* done)
    else
       GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts, dim3((N * 5 + 255) / 256), dim3(256), 0, s, c, e->Hs.as<uint32_t>(),
                   e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>());
-   GNOC_LAUNCH(e, KC_SCAN, k_scan_slots, dim3(1), dim3(1024), 0, s, N, e->slot_cnt.as<uint32_t>(),
-               e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>(), e->gtot.as<uint64_t>() + 1);
+   if (N * 25 <= 4 * SCAN_SPAN)
+      GNOC_LAUNCH(e, KC_SCAN, k_scan_slots, dim3(1), dim3(1024), 0, s, N, e->slot_cnt.as<uint32_t>(),
+                  e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>(), e->gtot.as<uint64_t>() + 1);
+   else
+   {
+      const uint32_t nq = N * 25, nspan = (nq + SCAN_SPAN - 1) / SCAN_SPAN;
+      GNOC_HIP(e, e->span.ensure((size_t) nspan * 8));
+      GNOC_LAUNCH(e, KC_SCAN, k_scan_span_sums, dim3(nspan), dim3(256), 0, s, nq, e->slot_cnt.as<uint32_t>(),
+                  e->span.as<uint64_t>());
+      GNOC_LAUNCH(e, KC_SCAN, k_scan_span_offsets, dim3(1), dim3(1024), 0, s, nspan, e->span.as<uint64_t>(),
+                  e->gtot.as<uint64_t>(), e->gtot.as<uint64_t>() + 1);
+      GNOC_LAUNCH(e, KC_SCAN, k_scan_span_bases, dim3(nspan), dim3(256), 0, s, nq, e->slot_cnt.as<uint32_t>(),
+                  e->span.as<uint64_t>(), e->slot_base.as<uint64_t>());
+   }
    return GNOC_OK;
 }
 

@@ -1182,7 +1182,10 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
    for (;;)
    {
       // ---- take the prefetched chunk (its keys first, if they had to wait for producers)
-      if (!sm.nx.valid) return;
+      if (!sm.nx.valid)
+      {
+         return;
+      }
       if (__hip_atomic_load(errflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 6u) return;   // rerun on v1 follows
       if (sm.nx.deferred)
       {

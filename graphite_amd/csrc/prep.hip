@@ -217,25 +217,29 @@ __global__ __launch_bounds__(64) void k_scatter(uint64_t n, uint32_t pch, uint32
    }
 }
 
-// Same contract with 4 waves per chunk (N <= SC4_MAXN): each wave owns a
-// contiguous quarter; per-wave source counts in LDS give each wave its
-// starting rank, then every wave ranks its quarter in order, with the next
-// 64 packets' loads in flight while the current ones are placed.
+// Same contract with NW waves per chunk: each wave owns a contiguous 1/NW of
+// the chunk; per-wave source counts in LDS (NW * N words) give each wave its
+// starting rank, then every wave ranks its part in order, with the next 64
+// packets' loads in flight while the current ones are placed.  NW = 8 for
+// N <= 2048, 4 for N <= 4096 (64 KiB of counters).  Larger meshes (sweeps) use
+// k_scatter: a 2-wave variant needs 65536-packet chunks there and was slower.
 constexpr uint32_t SC4_MAXN = 4096;
+__host__ __device__ inline int scatter_waves(uint32_t N) { return N <= 2048 ? 8 : 4; }
 
-__global__ __launch_bounds__(256) void k_scatter4(uint64_t n, uint32_t pch, uint32_t N, int nbits,
+template <int NW>
+__global__ __launch_bounds__(512) void k_scatter4(uint64_t n, uint32_t pch, uint32_t N, int nbits,
                                                   const uint32_t* __restrict__ src, const uint8_t* __restrict__ routed,
                                                   const uint64_t* __restrict__ inj, const uint32_t* __restrict__ aux,
                                                   const uint32_t* __restrict__ offs, Rec* __restrict__ recs,
                                                   uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id)
 {
-   extern __shared__ uint32_t h4[];   // [4][N] per-wave counts -> running ranks
+   extern __shared__ uint32_t h4[];   // [NW][N] per-wave counts -> running ranks
    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-   for (uint32_t k = threadIdx.x; k < 4 * N; k += 256) h4[k] = 0;
+   for (uint32_t k = threadIdx.x; k < NW * N; k += 64 * NW) h4[k] = 0;
    __syncthreads();
    const uint64_t c0 = (uint64_t) blockIdx.x * pch;
    const uint64_t c1 = min(c0 + pch, n);
-   const uint64_t q = (c1 - c0 + 3) / 4;
+   const uint64_t q = (c1 - c0 + NW - 1) / NW;
    const uint64_t lo = min(c0 + w * q, c1), hi = min(lo + q, c1);
    uint32_t* hw = h4 + w * N;
    for (uint64_t i = lo + lane; i < hi; i += 64)
@@ -243,10 +247,10 @@ __global__ __launch_bounds__(256) void k_scatter4(uint64_t n, uint32_t pch, uint
    __syncthreads();
    // exclusive prefix over waves, plus the chunk's offset for the source
    const uint32_t* orow = offs + (uint64_t) blockIdx.x * N;
-   for (uint32_t s2 = threadIdx.x; s2 < N; s2 += 256)
+   for (uint32_t s2 = threadIdx.x; s2 < N; s2 += 64 * NW)
    {
       uint32_t run = orow[s2];
-      for (uint32_t ww = 0; ww < 4; ww++)
+      for (uint32_t ww = 0; ww < (uint32_t) NW; ww++)
       {
          const uint32_t v = h4[ww * N + s2];
          h4[ww * N + s2] = run;
@@ -546,6 +550,89 @@ __global__ __launch_bounds__(1024) void k_scan_slots(uint32_t N, const uint32_t*
       run += (cnt[slot(q)] + 63) & ~63u;
    }
    if (threadIdx.x == 1023) *total = *inj_total + part[1023];
+}
+
+template __global__ void k_scatter4<4>(uint64_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
+                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
+template __global__ void k_scatter4<8>(uint64_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
+                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
+
+// Multi-block variant for large meshes (sweeps): the same slot order, in
+// SCAN_SPAN-entry spans.  Pass 1: span sums; pass 2 (one block): span offsets;
+// pass 3: bases within each span.
+constexpr uint32_t SCAN_SPAN = 4096;
+
+__device__ __forceinline__ uint32_t scan_slot_of(uint32_t q) { return (q / 25) * (PORTS * INS) + (q % 25); }
+
+__global__ __launch_bounds__(256) void k_scan_span_sums(uint32_t nq, const uint32_t* __restrict__ cnt,
+                                                        uint64_t* __restrict__ span_sum)
+{
+   __shared__ uint64_t red[256];
+   const uint32_t q0 = blockIdx.x * SCAN_SPAN, q1 = min(q0 + SCAN_SPAN, nq);
+   uint64_t a = 0;
+   for (uint32_t q = q0 + threadIdx.x; q < q1; q += 256) a += (cnt[scan_slot_of(q)] + 63) & ~63u;
+   red[threadIdx.x] = a;
+   __syncthreads();
+   for (uint32_t off = 128; off > 0; off >>= 1)
+   {
+      if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+      __syncthreads();
+   }
+   if (threadIdx.x == 0) span_sum[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(1024) void k_scan_span_offsets(uint32_t nspan, uint64_t* __restrict__ span_sum,
+                                                            const uint64_t* __restrict__ inj_total,
+                                                            uint64_t* __restrict__ total)
+{
+   __shared__ uint64_t part[1024];
+   const uint32_t per = (nspan + 1023) / 1024;
+   const uint32_t lo = min(threadIdx.x * per, nspan), hi = min(lo + per, nspan);
+   uint64_t s = 0;
+   for (uint32_t i = lo; i < hi; i++) s += span_sum[i];
+   part[threadIdx.x] = s;
+   __syncthreads();
+   for (uint32_t off = 1; off < 1024; off <<= 1)
+   {
+      const uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+   }
+   uint64_t run = *inj_total + part[threadIdx.x] - s;
+   for (uint32_t i = lo; i < hi; i++)
+   {
+      const uint64_t v = span_sum[i];
+      span_sum[i] = run;
+      run += v;
+   }
+   if (threadIdx.x == 1023) *total = *inj_total + part[1023];
+}
+
+__global__ __launch_bounds__(256) void k_scan_span_bases(uint32_t nq, const uint32_t* __restrict__ cnt,
+                                                         const uint64_t* __restrict__ span_off, uint64_t* __restrict__ base)
+{
+   __shared__ uint64_t part[256];
+   const uint32_t q0 = blockIdx.x * SCAN_SPAN, q1 = min(q0 + SCAN_SPAN, nq);
+   const uint32_t per = SCAN_SPAN / 256;
+   const uint32_t lo = min(q0 + threadIdx.x * per, q1), hi = min(lo + per, q1);
+   uint64_t s = 0;
+   for (uint32_t q = lo; q < hi; q++) s += (cnt[scan_slot_of(q)] + 63) & ~63u;
+   part[threadIdx.x] = s;
+   __syncthreads();
+   for (uint32_t off = 1; off < 256; off <<= 1)
+   {
+      const uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+   }
+   uint64_t run = span_off[blockIdx.x] + part[threadIdx.x] - s;
+   for (uint32_t q = lo; q < hi; q++)
+   {
+      base[scan_slot_of(q)] = run;
+      run += (cnt[scan_slot_of(q)] + 63) & ~63u;
+   }
 }
 
 }  // namespace gnoc

@@ -54,3 +54,15 @@ def test_sweep_one_point_is_the_plain_engine():
     base = gnoc.EngineConfig(num_tiles=64)
     tr = gnoc.synthetic_trace(8, 8, 0.02, 300, seed=1)
     check_points(base, [gnoc.SweepPoint()], [tr])
+
+
+def test_sweep_256_points_full_grid():
+    """All 256 points of SURVEY 8d config 5 in one batch (a 128 x 128 block
+    mesh: the large-mesh scatter and multi-block slot scan), light traffic."""
+    base = gnoc.EngineConfig(num_tiles=64)
+    pts, trs = [], []
+    for k, (fw, r, tw, load) in enumerate(itertools.product([16, 32, 64, 128], [0, 1, 2, 3],
+                                                            [1.0, 150.0, 250.0, 350.0], [0.005, 0.01, 0.015, 0.02])):
+        pts.append(gnoc.SweepPoint(fw, r, int(np.ceil(0.01 * tw)), tw))
+        trs.append(gnoc.synthetic_trace(8, 8, load, 12, seed=1000 + k))
+    check_points(base, pts, trs)
