@@ -262,10 +262,41 @@ def sweep_bench(a, world, rank, local):
                          "algorithmic_bytes_per_launch": alg / max(lv_n, 1)},
             "kernel_ms": {k: round(v[0], 4) for k, v in kst.items()},
             "trace_gen_s": round(gen_s, 2),
+            **({"cpu_baseline": sweep_cpu_baseline(a, pts, ppt)} if a.cpu_baseline and world == 1 else {}),
         }), flush=True)
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _sweep_point_oracle(args):
+    """One sweep point through the CPU oracle (a worker process)."""
+    import sys as _s
+    _s.path.insert(0, ROOT)
+    from graphite_amd import gnoc
+    from oracle import oracle
+    (fw, r, lk, tw), load, ppt, seed = args
+    cfg = gnoc.SweepPoint(fw, r, lk, tw).config(gnoc.EngineConfig(num_tiles=64))
+    tr = gnoc.synthetic_trace(8, 8, load, ppt, seed=seed)
+    t0 = time.perf_counter()
+    res = oracle.run(cfg, tr)
+    return int(res.port_count.reshape(-1, 6)[:, :5].sum()), time.perf_counter() - t0
+
+
+def sweep_cpu_baseline(a, pts, ppt, npts=64, workers=16):
+    """independent single-threaded oracle processes over the
+    host cores (16 workers = the GPU box's CPU share), on the first `npts` points
+    of the same sweep; aggregate hops / wall time."""
+    import multiprocessing as mp
+    jobs = [((q.flit_width, q.router_delay, q.link_delay, q.tile_width_mm), load, ppt, a.seed + 7919 * i)
+            for i, (q, load) in enumerate(pts[:npts])]
+    with mp.get_context("spawn").Pool(workers) as pool:
+        out = pool.map(_sweep_point_oracle, jobs)
+    hops = sum(h for h, _ in out)
+    busy = sum(t for _, t in out) / workers   # oracle time only: worker start-up and trace generation excluded
+    return {"value": hops / busy, "unit": "packet-hops/s", "cores": workers, "kind": "port",
+            "sample": f"{npts} of the {len(pts)} sweep points, pkts/tile={ppt}: {hops} mesh hops, "
+                      f"{busy:.2f} s of oracle time per worker ({workers} single-threaded oracle processes)"}
 
 
 PMC_FILE = "r1_pmc.json"
