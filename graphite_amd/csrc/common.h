@@ -18,7 +18,9 @@ enum : uint32_t { IN_LOCAL = 0, IN_W = 1, IN_E = 2, IN_S = 3, IN_N = 4, INS = 5 
 // One hop record in HBM: the arrival of packet `id` at an output-port queue at
 // time `t` (picoseconds).  aux packs the destination's mesh coordinates and the
 // packet's flit count F, so routing needs no division and no gather downstream:
-//   aux = dx | dy << 10 | F << 20      (W, H <= 1024, F <= 4095; checked at submit)
+//   aux = dx | dy << 10 | F << 20 | BC << 31   (W, H <= 1024, F <= 2047; checked at submit)
+// A broadcast (BC = 1, emesh_hop_by_hop.cc:163-221) carries the SENDER's
+// coordinates in (dx, dy): its tree is a function of the sender.
 struct __attribute__((aligned(16))) Rec
 {
    uint64_t t;
@@ -30,7 +32,8 @@ static_assert(sizeof(Rec) == 16, "Rec must be 16 bytes");
 constexpr uint32_t AUX_C_BITS = 10;
 constexpr uint32_t AUX_C_MASK = (1u << AUX_C_BITS) - 1;
 constexpr uint32_t AUX_F_SHIFT = 2 * AUX_C_BITS;
-constexpr uint32_t AUX_F_MAX = (1u << (32 - AUX_F_SHIFT)) - 1;
+constexpr uint32_t AUX_F_MAX = (1u << (31 - AUX_F_SHIFT)) - 1;
+constexpr uint32_t AUX_BC = 1u << 31;
 constexpr uint32_t MESH_DIM_MAX = 1u << AUX_C_BITS;
 
 __host__ __device__ inline uint32_t aux_pack(uint32_t dx, uint32_t dy, uint32_t F)
@@ -39,7 +42,7 @@ __host__ __device__ inline uint32_t aux_pack(uint32_t dx, uint32_t dy, uint32_t 
 }
 __host__ __device__ inline uint32_t aux_dx(uint32_t a) { return a & AUX_C_MASK; }
 __host__ __device__ inline uint32_t aux_dy(uint32_t a) { return (a >> AUX_C_BITS) & AUX_C_MASK; }
-__host__ __device__ inline uint32_t aux_F(uint32_t a) { return a >> AUX_F_SHIFT; }
+__host__ __device__ inline uint32_t aux_F(uint32_t a) { return (a >> AUX_F_SHIFT) & AUX_F_MAX; }
 
 __host__ __device__ inline uint32_t slot_of(uint32_t tile, uint32_t dir, uint32_t in)
 {
@@ -72,6 +75,15 @@ struct DevCfg
    int hop_counter;
    const uint64_t* pt_rl;   // per point Latency(R + Lk).toPicosec()
    const uint32_t* pt_fw;   // per point flit width
+   // Broadcast tree (emesh_hop_by_hop.cc:163-221), nullptr without broadcasts.
+   // A router visit v = b * N + tile of broadcast b charges the MAX queue delay
+   // over its selected ports (router_model.cc:86-101): a pass reads the maxima
+   // of the previous pass (bc_mprev) and records its own (bc_mcur); passes
+   // repeat until they agree (engine.hip gnoc_run).
+   const uint32_t* bc_idx;  // packet id -> broadcast index
+   const uint64_t* bc_mprev;
+   uint64_t* bc_mcur;
+   uint64_t* bc_fin;        // [b * N + tile] receipt time (ps)
 };
 
 // Latency::toPicosec, common/misc/time_types.h:81-86.  F1: f == 1.0 exactly,
@@ -115,6 +127,30 @@ __host__ __device__ __forceinline__ uint64_t rl_of(const DevCfg& c, uint32_t til
 __host__ __device__ __forceinline__ uint32_t fw_of(const DevCfg& c, uint32_t tile)
 {
    return c.pt_fw ? c.pt_fw[point_of(c, tile)] : c.flit_width;
+}
+
+// Output ports a broadcast from (sx, sy) requests at router (cx, cy),
+// network_model_emesh_hop_by_hop.cc:170-204: UP if cy >= sy, DOWN if cy <= sy,
+// along the sender's row RIGHT if cx >= sx and LEFT if cx <= sx, and SELF;
+// ports towards an off-mesh tile are dropped (computeTileID, :274-280).
+__host__ __device__ __forceinline__ uint32_t bc_mask(uint32_t sx, uint32_t sy, uint32_t cx, uint32_t cy, uint32_t W,
+                                                     uint32_t H)
+{
+   uint32_t m = 1u << P_SELF;
+   if (cy >= sy && cy + 1 < H) m |= 1u << P_UP;
+   if (cy <= sy && cy >= 1) m |= 1u << P_DOWN;
+   if (cy == sy)
+   {
+      if (cx >= sx && cx + 1 < W) m |= 1u << P_RIGHT;
+      if (cx <= sx && cx >= 1) m |= 1u << P_LEFT;
+   }
+   return m;
+}
+
+// Input side of a broadcast's record at router (cx, cy): where its tree edge comes from.
+__host__ __device__ __forceinline__ uint32_t bc_in_side(uint32_t sx, uint32_t sy, uint32_t cx, uint32_t cy)
+{
+   return cy > sy ? IN_S : cy < sy ? IN_N : cx > sx ? IN_W : cx < sx ? IN_E : IN_LOCAL;
 }
 
 // Dimension-ordered XY route step, network_model_emesh_hop_by_hop.cc:229-240.

@@ -58,11 +58,11 @@ struct DevBuf
 enum KernelClass
 {
    KC_CLASSIFY, KC_SRC_TOT, KC_INJ_BASE, KC_SRC_OFFS, KC_SCATTER, KC_ROW_HIST, KC_PROW, KC_SLOT_COUNTS, KC_SCAN,
-   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_N
+   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_BCAST, KC_N
 };
 static const char* const kKernelNames[KC_N] = { "k_classify", "k_src_tot", "k_inj_base", "k_src_offs", "k_scatter",
                                                 "k_row_hist", "k_prow", "k_slot_counts", "k_scan_slots", "k_plan",
-                                                "k_level", "k_port_stream", "k_finalize" };
+                                                "k_level", "k_port_stream", "k_finalize", "k_bcast" };
 
 struct gnoc_engine
 {
@@ -113,6 +113,13 @@ struct gnoc_engine
    std::vector<uint64_t> xs_units, xr_units;
    DevBuf d_xs_pairs, d_xr_pairs, xs_off, xr_off;
    bool begun = false;
+
+   // broadcast tree (emesh_hop_by_hop.cc:163-221): packet id -> broadcast index,
+   // broadcast -> packet id, per-visit max delays (two passes), receipts
+   uint32_t nb = 0;
+   uint32_t bc_passes = 0;
+   std::vector<uint32_t> h_bid;
+   DevBuf d_bidx, d_bid, d_bm0, d_bm1, d_bfin, d_bzl, d_bct, d_bflag;
 
    // design-space sweep (gnoc_create_sweep): per-point tables
    int32_t npoints = 1;
@@ -512,19 +519,34 @@ static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n,
       for (uint32_t y = band_lo(b, nr, H); y < band_lo(b + 1, nr, H); y++) rb[y] = b;
       for (uint32_t x = band_lo(b, nr, W); x < band_lo(b + 1, nr, W); x++) cb[x] = b;
    }
+   e->h_bid.clear();
    for (size_t i = 0; i < n; i++)
    {
-      const uint32_t s = pk->src[i], d = pk->dst[i];
+      const uint32_t s = pk->src[i], fl = pk->flags ? pk->flags[i] : 0u;
+      const bool bc = (fl & GNOC_PKT_BROADCAST) != 0;
+      const uint32_t d = bc ? s : pk->dst[i];   // a broadcast's receiver field is ignored
       if (s >= N || d >= N) return fail(e, GNOC_ETRACE, "tile id out of range at packet " + std::to_string(i));
+      if (bc)
+      {
+         // Network::netSend sends one packet per tile when the model has no broadcast
+         // capability (network.cc:186-195): the caller expands those.
+         if (!e->cfg.broadcast_tree_enabled || e->dc.hop_counter)
+            return fail(e, GNOC_EINVAL, "broadcast packet " + std::to_string(i) +
+                                            " but the model has no broadcast tree (the caller expands it, network.cc:186-195)");
+         if (nr > 1 || e->npoints > 1)
+            return fail(e, GNOC_EUNSUPPORTED, "broadcast packets on a sharded or sweep engine");
+         e->h_bid.push_back((uint32_t) i);
+      }
       if (i && pk->inject_ps[i] < pk->inject_ps[i - 1]) return fail(e, GNOC_ETRACE, "trace not ordered by inject_ps at packet " + std::to_string(i));
       const uint32_t fw = fw_host(e, s);
       const uint32_t F = (pk->bits[i] + fw - 1) / fw;
       if (e->npoints > 1 && point_of(e->dc, s) != point_of(e->dc, d))
          return fail(e, GNOC_ETRACE, "sweep packet crosses sweep points at packet " + std::to_string(i));
-      const bool bypass = s == d || (pk->flags && (pk->flags[i] & GNOC_PKT_UNMODELED));
+      const bool bypass = (!bc && s == d) || (fl & GNOC_PKT_UNMODELED);
       if (F == 0 && !bypass) return fail(e, GNOC_ETRACE, "zero-flit packet " + std::to_string(i));
-      if (F > AUX_F_MAX) return fail(e, GNOC_EUNSUPPORTED, "packet longer than 4095 flits");
-      if (!bypass)
+      if (F > AUX_F_MAX) return fail(e, GNOC_EUNSUPPORTED, "packet longer than 2047 flits");
+      if (!bypass && bc) rec += 2ull * N;   // injection + N SELF + N - 1 tree edges
+      else if (!bypass)
       {
          const int64_t sx = s % W, sy = s / W, dx = d % W, dy = d / W;
          const uint64_t ax = (uint64_t) std::llabs(sx - dx), ay = (uint64_t) std::llabs(sy - dy);
@@ -591,6 +613,35 @@ static int build_exchange(gnoc_engine* e)
    return GNOC_OK;
 }
 
+// Broadcast tables of the submitted trace (h_bid from validate_host_trace).
+static int upload_broadcasts(gnoc_engine* e)
+{
+   e->nb = (uint32_t) e->h_bid.size();
+   e->dc.bc_idx = nullptr;
+   e->dc.bc_mprev = nullptr;
+   e->dc.bc_mcur = nullptr;
+   e->dc.bc_fin = nullptr;
+   if (!e->nb) return GNOC_OK;
+   const size_t nv = (size_t) e->nb * e->dc.N;
+   std::vector<uint32_t> bidx(e->n, 0xFFFFFFFFu);
+   for (uint32_t b = 0; b < e->nb; b++) bidx[e->h_bid[b]] = b;
+   GNOC_HIP(e, e->d_bidx.ensure(e->n * 4));
+   GNOC_HIP(e, e->d_bid.ensure((size_t) e->nb * 4));
+   GNOC_HIP(e, e->d_bm0.ensure(nv * 8));
+   GNOC_HIP(e, e->d_bm1.ensure(nv * 8));
+   GNOC_HIP(e, e->d_bfin.ensure(nv * 8));
+   GNOC_HIP(e, e->d_bzl.ensure(nv * 8));
+   GNOC_HIP(e, e->d_bct.ensure(nv * 8));
+   GNOC_HIP(e, e->d_bflag.ensure(16));
+   GNOC_HIP(e, hipMemcpy(e->d_bidx.p, bidx.data(), e->n * 4, hipMemcpyHostToDevice));
+   GNOC_HIP(e, hipMemcpy(e->d_bid.p, e->h_bid.data(), (size_t) e->nb * 4, hipMemcpyHostToDevice));
+   e->dc.bc_idx = e->d_bidx.as<uint32_t>();
+   e->dc.bc_mprev = e->d_bm0.as<uint64_t>();
+   e->dc.bc_mcur = e->d_bm1.as<uint64_t>();
+   e->dc.bc_fin = e->d_bfin.as<uint64_t>();
+   return GNOC_OK;
+}
+
 int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
 {
    if (!e || !pk) return GNOC_EINVAL;
@@ -625,6 +676,8 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    e->d_flags = e->t_flags.as<uint32_t>();
    e->n = n;
    e->rec_bound = record_bound(e, records);
+   rc = upload_broadcasts(e);
+   if (rc) return rc;
    rc = build_exchange(e);
    if (rc) return rc;
    e->submitted = true;
@@ -645,6 +698,9 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    e->d_bits = pk->bits;
    e->d_flags = pk->flags;
    e->n = n;
+   e->h_bid.clear();
+   int brc = upload_broadcasts(e);
+   if (brc) return brc;
    // size the record buffers from the trace (route-static): classify once now
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    GNOC_HIP(e, e->counters.ensure(64));
@@ -661,8 +717,9 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
                          e->final_ps.as<uint64_t>(), e->hist.as<uint32_t>(), e->counters.as<unsigned long long>(),
                          0u, e->dc.H, 0u, e->dc.W, nullptr, nullptr);
    GNOC_HIP(e, hipGetLastError());
-   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 16, hipMemcpyDeviceToHost, e->stream));
+   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 24, hipMemcpyDeviceToHost, e->stream));
    GNOC_HIP(e, hipStreamSynchronize(e->stream));
+   if (e->h_pinned[2]) return fail(e, GNOC_EUNSUPPORTED, "broadcast packets need a host trace (gnoc_submit)");
    const uint64_t records = e->h_pinned[0] + e->h_pinned[1];
    if (record_bound(e, records) >= (1ull << 31)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^31 hop records");
    e->rec_bound = record_bound(e, records);
@@ -961,6 +1018,9 @@ static int run_prep(gnoc_engine* e, bool* done)
    else
       GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts, dim3((N * 5 + 255) / 256), dim3(256), 0, s, c, e->Hs.as<uint32_t>(),
                   e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>());
+   if (e->nb)
+      GNOC_LAUNCH(e, KC_BCAST, k_bcast_slots, dim3((uint32_t) (((uint64_t) e->nb * N + 255) / 256)), dim3(256), 0, s, c,
+                  e->nb, e->d_bid.as<uint32_t>(), e->d_src, e->routed.as<uint8_t>(), e->slot_cnt.as<uint32_t>());
    if (N * 25 <= 4 * SCAN_SPAN)
       GNOC_LAUNCH(e, KC_SCAN, k_scan_slots, dim3(1), dim3(1024), 0, s, N, e->slot_cnt.as<uint32_t>(),
                   e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>(), e->gtot.as<uint64_t>() + 1);
@@ -997,11 +1057,22 @@ static int run_post(gnoc_engine* e, bool closed_form)
                      e->d_src, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
                      e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), (int) closed_form, e->cx0, e->cx1);
    }
+   if (e->nb)
+   {
+#define GNOC_BFIN(F1V)                                                                                                \
+   GNOC_LAUNCH(e, KC_BCAST, k_bcast_final<F1V>, dim3(e->nb), dim3(256), 0, s, c, e->d_bid.as<uint32_t>(), e->d_inj, \
+               e->d_src, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->d_bfin.as<uint64_t>(),                  \
+               e->d_bzl.as<uint64_t>(), e->d_bct.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),  \
+               e->cont.as<uint64_t>(), (int) closed_form)
+      if (e->f1) GNOC_BFIN(true);
+      else GNOC_BFIN(false);
+#undef GNOC_BFIN
+   }
    GNOC_HIP(e, hipEventRecord(e->ev1, s));
-   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 16, hipMemcpyDeviceToHost, s));
+   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 24, hipMemcpyDeviceToHost, s));
    if (!closed_form)
    {
-      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 2, e->gtot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
+      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 3, e->gtot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 4, e->counters.as<unsigned int>() + 8, 4, hipMemcpyDeviceToHost, s));
    }
    GNOC_HIP(e, hipStreamSynchronize(s));
@@ -1016,8 +1087,8 @@ static int run_post(gnoc_engine* e, bool closed_form)
       e->ran = true;
       return GNOC_OK;
    }
-   e->h_records = e->h_counters[0] + e->h_counters[1];
-   if (e->h_pinned[2] > e->rec_bound) return fail(e, GNOC_EHIP, "internal: slot layout exceeds the record bound");
+   e->h_records = e->h_counters[0] + e->h_counters[1] + e->h_pinned[2];
+   if (e->h_pinned[3] > e->rec_bound) return fail(e, GNOC_EHIP, "internal: slot layout exceeds the record bound");
    const unsigned errf = *(unsigned int*) (e->h_pinned + 4);
    // a leaf the splitter could not cut (or a look-back timeout) leaves garbage
    // downstream, so it takes precedence: rerun exactly on the v1 path
@@ -1037,7 +1108,9 @@ static int run_once(gnoc_engine* e)
    bool done = false;
    int rc = run_prep(e, &done);
    if (rc || done) return rc;
-   const bool v3 = e->f1 && e->dc.max_list >= 3 && !e->force_v1;
+   // broadcast batches take the whole-port streams: their children leave FIFO
+   // order and fan out to several next ports (kernels.hip k_port_stream)
+   const bool v3 = e->f1 && e->dc.max_list >= 3 && !e->force_v1 && !e->nb;
    e->used_v3 = v3;
    if (v3)
    {
@@ -1056,16 +1129,78 @@ int gnoc_run(gnoc_engine* e)
    if (e->nranks > 1) return fail(e, GNOC_ESTATE, "sharded engine: use gnoc_run_begin / exchange / gnoc_run_finish");
    const char* env = std::getenv("GNOC_ENGINE");
    const int forced = env && std::strcmp(env, "v1") == 0;
-   e->force_v1 = forced;
-   int rc = run_once(e);
-   if (rc == GNOC_V3_RETRY)
+   // Broadcast batches run in passes: a router visit of a broadcast charges the
+   // max queue delay over the ports it selects (router_model.cc:86-101), and
+   // those ports sit on different levels of the port DAG, so a pass charges the
+   // maxima the previous pass measured.  The event times are the unique causal
+   // solution exactly when two passes agree.
+   const char* pv = std::getenv("GNOC_BCAST_PASSES");
+   const uint32_t max_passes = pv && std::atol(pv) > 0 ? (uint32_t) std::atol(pv) : 256u;
+   const size_t nv = (size_t) e->nb * e->dc.N;
+   e->bc_passes = 0;
+   if (e->nb && e->submitted)
    {
-      e->force_v1 = 1;   // exact but slower whole-port streams
-      rc = run_once(e);
-      e->force_v1 = forced;
-      if (rc == GNOC_V3_RETRY) rc = fail(e, GNOC_EHIP, "internal: v1 path reported overflow");
+      GNOC_HIP(e, hipSetDevice(e->cfg.device));
+      GNOC_HIP(e, hipMemsetAsync(e->d_bm0.p, 0, nv * 8, e->stream));
    }
-   return rc;
+   double ms = 0.0;
+   for (;;)
+   {
+      if (e->nb && e->submitted) GNOC_HIP(e, hipMemsetAsync(e->d_bm1.p, 0, nv * 8, e->stream));
+      e->force_v1 = forced;
+      int rc = run_once(e);
+      if (rc == GNOC_V3_RETRY)
+      {
+         e->force_v1 = 1;   // exact but slower whole-port streams
+         rc = run_once(e);
+         if (rc == GNOC_V3_RETRY) rc = fail(e, GNOC_EHIP, "internal: v1 path reported overflow");
+      }
+      e->force_v1 = forced;
+      if (rc) return rc;
+      ms += e->last_ms;
+      e->bc_passes++;
+      if (!e->nb || !e->dc.contention) break;
+      GNOC_HIP(e, hipMemsetAsync(e->d_bflag.p, 0, 4, e->stream));
+      hipLaunchKernelGGL(k_bcast_agree, dim3((uint32_t) std::min<size_t>((nv + 255) / 256, 4096)), dim3(256), 0,
+                         e->stream, (uint64_t) nv, e->d_bm0.as<uint64_t>(), (const uint64_t*) e->d_bm1.as<uint64_t>(),
+                         e->d_bflag.as<unsigned>());
+      GNOC_HIP(e, hipGetLastError());
+      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 6, e->d_bflag.p, 4, hipMemcpyDeviceToHost, e->stream));
+      GNOC_HIP(e, hipStreamSynchronize(e->stream));
+      if (!*(unsigned*) (e->h_pinned + 6)) break;
+      if (e->bc_passes >= max_passes)
+      {
+         e->ran = false;
+         return fail(e, GNOC_EUNSUPPORTED, "broadcast passes did not agree within " + std::to_string(max_passes) +
+                                               " (GNOC_BCAST_PASSES)");
+      }
+   }
+   e->last_ms = ms;
+   return GNOC_OK;
+}
+
+int gnoc_get_broadcast_results(gnoc_engine* e, uint64_t* final_ps, uint64_t* zero_load_ps, uint64_t* contention_ps,
+                               size_t n_entries)
+{
+   if (!e) return GNOC_EINVAL;
+   if (!e->ran) return fail(e, GNOC_ESTATE, "no results: call gnoc_run first");
+   const size_t nv = (size_t) e->nb * e->dc.N;
+   if (n_entries != nv) return fail(e, GNOC_EINVAL, "broadcast result length != broadcasts x num_tiles");
+   if (!nv) return GNOC_OK;
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   if (final_ps) GNOC_HIP(e, hipMemcpyAsync(final_ps, e->d_bfin.p, nv * 8, hipMemcpyDeviceToHost, e->stream));
+   if (zero_load_ps) GNOC_HIP(e, hipMemcpyAsync(zero_load_ps, e->d_bzl.p, nv * 8, hipMemcpyDeviceToHost, e->stream));
+   if (contention_ps) GNOC_HIP(e, hipMemcpyAsync(contention_ps, e->d_bct.p, nv * 8, hipMemcpyDeviceToHost, e->stream));
+   GNOC_HIP(e, hipStreamSynchronize(e->stream));
+   return GNOC_OK;
+}
+
+int gnoc_get_broadcast_info(const gnoc_engine* e, uint64_t* nbcast, uint32_t* passes)
+{
+   if (!e) return GNOC_EINVAL;
+   if (nbcast) *nbcast = e->nb;
+   if (passes) *passes = e->bc_passes;
+   return GNOC_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -25,7 +25,7 @@ namespace gnoc {
 // slot (or write the packet's final time at SELF).
 // ----------------------------------------------------------------------------
 constexpr int ST = 256;          // records per input per round
-constexpr int SMAXIN = 4;        // max input streams per port
+constexpr int SMAXIN = INS;      // input streams per port: 4 for unicast, 5 at a broadcast sender's SELF
 constexpr int SMAXE = ST * SMAXIN;
 constexpr int STHREADS = 256;
 
@@ -51,6 +51,7 @@ struct PortSmem
    uint64_t wA[STHREADS / 64], wB[STHREADS / 64], wC[STHREADS / 64];
    uint32_t e_cnt[SMAXIN];
    uint32_t s0;
+   uint32_t bc_late;   // a broadcast child left later than its FIFO departure
    SerialState ss;
 };
 
@@ -240,7 +241,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
    }
    uint32_t ocur[5] = { 0, 0, 0, 0, 0 };   // records written per next-direction
 
-   uint32_t cur[SMAXIN] = { 0, 0, 0, 0 };
+   uint32_t cur[SMAXIN] = {};
    uint64_t X0 = 0;                         // carried queue state (cycles)
    uint64_t st_sum = 0, st_cnt = 0, st_flit = 0, st_last = 0;
    bool first_round = true;
@@ -249,7 +250,15 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
    {
       sm.ss.X = 0; sm.ss.g = 0; sm.ss.mode = 0; sm.ss.s1 = 0; sm.ss.s2 = 0;
       sm.ss.narr = 0; sm.ss.newest = 0; sm.ss.mg1 = 0;
+      sm.bc_late = 0;
    }
+   // Next ports of a record at the next router: the XY step, or a broadcast's
+   // tree ports there (bc_mask); none at SELF (the packet is received).
+   auto next_mask = [&](uint32_t ax) -> uint32_t {
+      if (dir == P_SELF) return 0u;
+      if (ax & AUX_BC) return bc_mask(aux_dx(ax), aux_dy(ax), nx, ny, c.W, c.H);
+      return 1u << xy_dir(nx, ny, aux_dx(ax), aux_dy(ax));
+   };
 
    for (;;)
    {
@@ -439,12 +448,8 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
          uint64_t packed = 0;   // 5 x 12-bit counters
          for (uint32_t e = lo; e < hi; e++)
          {
-            uint32_t ndir = 0;
-            if (dir != P_SELF)
-            {
-               ndir = xy_dir(nx, ny, aux_dx(sm.m_aux[e]), aux_dy(sm.m_aux[e]));
-            }
-            packed += 1ull << (12 * ndir);
+            const uint32_t m = next_mask(sm.m_aux[e]);
+            for (uint32_t d = 0; d < 5; d++) packed += (uint64_t) ((m >> d) & 1u) << (12 * d);
          }
          uint64_t inc = packed;
          for (int off = 1; off < 64; off <<= 1)
@@ -463,7 +468,19 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
             const uint64_t t = sm.m_t[e];
             const uint32_t id = sm.m_id[e], ax = sm.m_aux[e];
             const uint64_t cc = sm.m_c[e];
-            st_sum += cc;
+            // the delay charged: this queue's, or for a broadcast's router visit the
+            // max over the visit's ports (router_model.cc:86-101; previous pass)
+            uint64_t ch = cc;
+            uint64_t* bfin = nullptr;
+            if ((ax & AUX_BC) && dir != P_INJ)
+            {
+               const uint64_t v = (uint64_t) c.bc_idx[id] * c.N + tile;
+               atomicMax((unsigned long long*) (c.bc_mcur + v), (unsigned long long) cc);
+               const uint64_t mp = c.bc_mprev[v];
+               if (mp > cc) { ch = mp; sm.bc_late = 1; }
+               bfin = c.bc_fin + v;
+            }
+            st_sum += ch;
             st_cnt++;
             {
                // QueueModel utilization (queue_model.cc:49-53): F and departure, in cycles
@@ -471,25 +488,31 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
                st_flit += p;
                st_last = st_last > dep ? st_last : dep;
             }
-            const uint64_t tn = t + ps_of<F1>(cc, c.f) + (dir == P_INJ ? 0ull : rl_of(c, tile));
+            const uint64_t tn = t + ps_of<F1>(ch, c.f) + (dir == P_INJ ? 0ull : rl_of(c, tile));
             if (dir == P_SELF)
             {
-               final_ps[id] = tn + ps_of<F1>(aux_F(ax), c.f);
+               const uint64_t fin = tn + ps_of<F1>(aux_F(ax), c.f);
+               if (bfin) *bfin = fin;
+               else final_ps[id] = fin;
                continue;
             }
-            const uint32_t ndir = xy_dir(nx, ny, aux_dx(ax), aux_dy(ax));
-            const uint32_t r = (uint32_t) ((pre >> (12 * ndir)) & 0xFFF);
-            pre += 1ull << (12 * ndir);
-            if (ocur[ndir] + r >= ocap[ndir])
-            {
-               atomicOr(errflag, 1u);   // route-count invariant broken: never write out of the slot
-               continue;
-            }
+            const uint32_t m = next_mask(ax);
             Rec o;
             o.t = tn;
             o.id = id;
             o.aux = ax;
-            recs[obase[ndir] + ocur[ndir] + r] = o;
+            for (uint32_t nd = 0; nd < 5; nd++)
+            {
+               if (!((m >> nd) & 1u)) continue;
+               const uint32_t r = (uint32_t) ((pre >> (12 * nd)) & 0xFFF);
+               pre += 1ull << (12 * nd);
+               if (ocur[nd] + r >= ocap[nd])
+               {
+                  atomicOr(errflag, 1u);   // route-count invariant broken: never write out of the slot
+                  continue;
+               }
+               recs[obase[nd] + ocur[nd] + r] = o;
+            }
          }
          for (uint32_t d = 0; d < 5; d++) ocur[d] += (uint32_t) ((tot >> (12 * d)) & 0xFFF);
       }
@@ -527,9 +550,10 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
       port_sum[port] = a;
       port_cnt[port] = b;
       port_mg1[port] = sm.ss.mg1;
-      // Outputs can leave FIFO order only through M/G/1 requests or, for f != 1,
+      // Outputs can leave FIFO order only through M/G/1 requests, broadcast
+      // children charged a sibling port's larger delay or, for f != 1,
       // equal-time pairs; mark this port's output slots for the fixup sort.
-      if (dir != P_SELF && (sm.ss.mg1 > 0 || !F1))
+      if (dir != P_SELF && (sm.ss.mg1 > 0 || sm.bc_late || !F1))
          for (uint32_t d = 0; d < 5; d++) dirty[slot_of(ntile, d, nin_side)] = 1;
    }
 }
@@ -550,6 +574,7 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
       // a sharded engine delivers the packets of its column band (shard.hip); the
       // others are zeroed when results are read (k_mask_unowned), not here
       if (dx < cx0 || dx >= cx1) continue;
+      if (aux[i] & AUX_BC) continue;   // k_bcast_final
       if (!(routed[i] & 1)) { zl[i] = 0; cont[i] = 0; continue; }
       uint32_t sx, sy;
       tile_xy(src[i], c.W, c.magicW, sx, sy);
@@ -562,6 +587,74 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
       if (closed_form) final_ps[i] = inj[i] + z;
       cont[i] = final_ps[i] - inj[i] - z;
    }
+}
+
+// Broadcast receipts, one block per broadcast: per receiving tile the
+// zero-load delay (H+1 routers of the tree path, then serialization) and the
+// contention; the packet's own entries are those of its latest receipt (lowest
+// tile on ties).  Closed form (queue models off): receipt = inject + zero-load.
+template <bool F1>
+__global__ __launch_bounds__(256) void k_bcast_final(DevCfg c, const uint32_t* __restrict__ bid,
+                                                     const uint64_t* __restrict__ inj, const uint32_t* __restrict__ src,
+                                                     const uint32_t* __restrict__ aux, const uint8_t* __restrict__ routed,
+                                                     uint64_t* __restrict__ bfin, uint64_t* __restrict__ bzl,
+                                                     uint64_t* __restrict__ bct, uint64_t* __restrict__ final_ps,
+                                                     uint64_t* __restrict__ zl, uint64_t* __restrict__ cont, int closed_form)
+{
+   __shared__ uint64_t bf[256];
+   __shared__ uint32_t bt[256];
+   const uint32_t b = blockIdx.x, id = bid[b], N = c.N;
+   const uint64_t t0 = inj[id];
+   const bool mesh = (routed[id] & 1) != 0;
+   uint32_t sx, sy;
+   tile_xy(src[id], c.W, c.magicW, sx, sy);
+   const uint64_t fps = ps_of<F1>(aux_F(aux[id]), c.f);
+   uint64_t best = 0;
+   uint32_t btile = 0xFFFFFFFFu;
+   for (uint32_t tile = threadIdx.x; tile < N; tile += blockDim.x)
+   {
+      const uint64_t k = (uint64_t) b * N + tile;
+      uint64_t f = t0, z = 0;
+      if (mesh)
+      {
+         uint32_t x, y;
+         tile_xy(tile, c.W, c.magicW, x, y);
+         const uint64_t hops = (uint64_t) ((x > sx ? x - sx : sx - x) + (y > sy ? y - sy : sy - y) + 1);
+         z = ps_of<F1>(0, c.f) + hops * c.rl_ps + fps;
+         f = closed_form ? t0 + z : bfin[k];
+      }
+      bfin[k] = f;
+      bzl[k] = z;
+      bct[k] = f - t0 - z;
+      if (btile == 0xFFFFFFFFu || f > best) { best = f; btile = tile; }
+   }
+   bf[threadIdx.x] = best;
+   bt[threadIdx.x] = btile;
+   __syncthreads();
+   if (threadIdx.x == 0)
+   {
+      uint64_t f = 0;
+      uint32_t tb = 0xFFFFFFFFu;
+      for (uint32_t k = 0; k < blockDim.x; k++)
+         if (bt[k] != 0xFFFFFFFFu && (tb == 0xFFFFFFFFu || bf[k] > f || (bf[k] == f && bt[k] < tb))) { f = bf[k]; tb = bt[k]; }
+      final_ps[id] = f;
+      zl[id] = bzl[(uint64_t) b * N + tb];
+      cont[id] = bct[(uint64_t) b * N + tb];
+   }
+}
+
+// Pass agreement: any visit whose max delay changed since the previous pass
+// sets *changed; then the maxima become the next pass's input.
+__global__ __launch_bounds__(256) void k_bcast_agree(uint64_t nv, uint64_t* __restrict__ mprev,
+                                                     const uint64_t* __restrict__ mcur, unsigned* __restrict__ changed)
+{
+   bool ch = false;
+   for (uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; k < nv; k += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const uint64_t v = mcur[k];
+      if (v != mprev[k]) { ch = true; mprev[k] = v; }
+   }
+   if (__ballot(ch) && (threadIdx.x & 63) == 0) atomicOr(changed, 1u);
 }
 
 // Results of packets another rank delivers read 0 (gnoc_get_packet_results).
@@ -584,6 +677,12 @@ template __global__ void k_port_stream<true>(DevCfg, const uint32_t*, const uint
                                              uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
 template __global__ void k_port_stream<false>(DevCfg, const uint32_t*, const uint32_t*, const uint64_t*, Rec*, uint64_t*,
                                               uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
+template __global__ void k_bcast_final<true>(DevCfg, const uint32_t*, const uint64_t*, const uint32_t*, const uint32_t*,
+                                             const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*,
+                                             uint64_t*, int);
+template __global__ void k_bcast_final<false>(DevCfg, const uint32_t*, const uint64_t*, const uint32_t*, const uint32_t*,
+                                              const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*,
+                                              uint64_t*, int);
 template __global__ void k_finalize<true>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,
                                           const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int, uint32_t, uint32_t);
 template __global__ void k_finalize<false>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,

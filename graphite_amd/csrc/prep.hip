@@ -50,11 +50,14 @@ __global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, uint32_t
       const uint32_t b = bits[i];
       const uint32_t fw = fw_of(c, s);
       const uint32_t F = (b % fw) ? b / fw + 1 : b / fw;
-      const bool bypass = (s == d) || (fl & 1u);
+      // a broadcast (flag 2; receiver BROADCAST) is never a self-send (network_model.cc:419)
+      const bool bc = (fl & 2u) != 0;
+      const bool bypass = (!bc && s == d) || (fl & 1u);
       uint32_t sx, sy, dx, dy;
       tile_xy(s, c.W, c.magicW, sx, sy);
-      tile_xy(d, c.W, c.magicW, dx, dy);
-      aux[i] = aux_pack(dx, dy, F);
+      if (bc) { dx = sx; dy = sy; }
+      else tile_xy(d, c.W, c.magicW, dx, dy);
+      aux[i] = aux_pack(dx, dy, F) | (bc ? AUX_BC : 0u);
       // bit 0: routed through the mesh; bit 1: and injected in this rank's row band
       const bool mine = sy >= ry0 && sy < ry1;
       routed[i] = bypass ? 0 : mine ? 3 : 1;
@@ -74,7 +77,10 @@ __global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, uint32_t
          atomicAdd(&slot_cnt[slot_of(sy * c.W + dx, dir, in)], 1u);
       }
       nrouted++;
-      hops += (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
+      // a broadcast visits every router once (N switch-allocator requests)
+      hops += bc ? (uint64_t) N : (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
+      // and materialises 2N records: injection + N SELF + (N - 1) tree edges
+      if (bc) atomicAdd(&counters[2], (unsigned long long) (N - 1));
    }
    __syncthreads();
    uint32_t* hrow = hist + (uint64_t) blockIdx.x * N;
@@ -517,6 +523,26 @@ __global__ __launch_bounds__(256) void k_slot_counts_y(DevCfg c, const uint32_t*
       slot_cnt[slot_of(tile, dir, IN_S)] = cs;
       slot_cnt[slot_of(tile, dir, IN_N)] = cn;
    }
+}
+
+// Broadcast-tree records per input slot, added to the unicast counts: one
+// thread per (broadcast, router).  The tree visits router (cx, cy) once, from
+// side bc_in_side, and requests the ports of bc_mask there.
+__global__ __launch_bounds__(256) void k_bcast_slots(DevCfg c, uint32_t nb, const uint32_t* __restrict__ bid,
+                                                     const uint32_t* __restrict__ src,
+                                                     const uint8_t* __restrict__ routed, uint32_t* __restrict__ slot_cnt)
+{
+   const uint64_t k = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+   if (k >= (uint64_t) nb * c.N) return;
+   const uint32_t b = (uint32_t) (k / c.N), tile = (uint32_t) (k % c.N);
+   const uint32_t id = bid[b];
+   if (!(routed[id] & 1)) return;
+   uint32_t sx, sy, cx, cy;
+   tile_xy(src[id], c.W, c.magicW, sx, sy);
+   tile_xy(tile, c.W, c.magicW, cx, cy);
+   const uint32_t m = bc_mask(sx, sy, cx, cy, c.W, c.H), in = bc_in_side(sx, sy, cx, cy);
+   for (uint32_t d = 0; d < 5; d++)
+      if ((m >> d) & 1u) atomicAdd(&slot_cnt[slot_of(tile, d, in)], 1u);
 }
 
 // ---------------------------------------------------------------------------

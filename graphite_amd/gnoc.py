@@ -28,6 +28,7 @@ PORT_SELF, PORT_LEFT, PORT_RIGHT, PORT_DOWN, PORT_UP, PORT_INJ = range(6)
 QUEUE_HISTORY_TREE, QUEUE_BASIC, QUEUE_HISTORY_LIST = 0, 1, 2
 PORTS_PER_TILE = 6
 PKT_UNMODELED = 0x1
+PKT_BROADCAST = 0x2     # receiver = NetPacket::BROADCAST, routed on the broadcast tree
 
 # Every symbol include/gnoc.h declares (checked by tests/test_abi.py).
 EXPORTED = (
@@ -37,6 +38,7 @@ EXPORTED = (
     "gnoc_set_profiling", "gnoc_get_kernel_stats", "gnoc_trace_file_write", "gnoc_trace_file_read",
     "gnoc_shard", "gnoc_exchange_counts", "gnoc_run_begin", "gnoc_run_finish",
     "gnoc_create_sweep", "gnoc_sweep_layout", "gnoc_get_port_utilization", "gnoc_create_hop_counter",
+    "gnoc_get_broadcast_results", "gnoc_get_broadcast_info",
 )
 
 
@@ -135,6 +137,8 @@ def load() -> ctypes.CDLL:
                                       ctypes.POINTER(vp)]
     lib.gnoc_sweep_layout.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
     lib.gnoc_create_hop_counter.argtypes = [ctypes.POINTER(GnocConfig), ctypes.POINTER(vp)]
+    lib.gnoc_get_broadcast_results.argtypes = [vp, vp, vp, vp, sz]
+    lib.gnoc_get_broadcast_info.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]
     lib.gnoc_shard.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
     lib.gnoc_exchange_counts.argtypes = [vp, vp, vp, sz]
     lib.gnoc_run_begin.argtypes = [vp, vp]
@@ -270,6 +274,26 @@ class Results:
     summary: dict = field(default_factory=dict)
     port_flit: Optional[np.ndarray] = None   # QueueModel _total_utilized_cycles (gnoc_get_port_utilization)
     port_last: Optional[np.ndarray] = None   # QueueModel _last_request_time
+    # broadcast receipts [broadcast in trace order, receiving tile] (gnoc_get_broadcast_results)
+    bcast_final_ps: Optional[np.ndarray] = None
+    bcast_zero_load_ps: Optional[np.ndarray] = None
+    bcast_contention_ps: Optional[np.ndarray] = None
+
+
+def expand_broadcasts(tr: Trace, num_tiles: int) -> Trace:
+    """What Network::netSend does with a broadcast when the model has no
+    broadcast tree (network.cc:186-195): one unicast per tile, in tile order,
+    at the broadcast's place in the trace.  (The reference also sends to the
+    two system tiles; those hops are direct and time nothing, network_model.cc:431-436.)"""
+    tr = tr.normalized()
+    bc = (tr.flags & PKT_BROADCAST) != 0
+    reps = np.where(bc, num_tiles, 1)
+    idx = np.repeat(np.arange(len(tr)), reps)
+    dst = tr.dst[idx].copy()
+    first = np.cumsum(reps) - reps
+    for i in np.nonzero(bc)[0]:
+        dst[first[i]:first[i] + num_tiles] = np.arange(num_tiles, dtype=np.uint32)
+    return Trace(tr.inject_ps[idx], tr.src[idx], dst, tr.bits[idx], tr.flags[idx] & ~np.uint32(PKT_BROADCAST))
 
 
 class Engine:
@@ -339,7 +363,19 @@ class Engine:
         self._check(self.lib.gnoc_get_port_stats(self._h, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data, npt))
         pf, pl = np.empty(npt, np.uint64), np.empty(npt, np.uint64)
         self._check(self.lib.gnoc_get_port_utilization(self._h, pf.ctypes.data, pl.ctypes.data, npt))
-        return Results(fin, zl, ct, ps, pc, pm, self.summary(), pf, pl)
+        nb, _ = self.broadcast_info()
+        N = self.cfg.width * self.cfg.height
+        bf, bz, bt = (np.empty((nb, N), np.uint64) for _ in range(3))
+        if nb:
+            self._check(self.lib.gnoc_get_broadcast_results(self._h, bf.ctypes.data, bz.ctypes.data, bt.ctypes.data,
+                                                            nb * N))
+        return Results(fin, zl, ct, ps, pc, pm, self.summary(), pf, pl, bf, bz, bt)
+
+    def broadcast_info(self):
+        """-> (broadcast packets submitted, passes the last run took)"""
+        nb, passes = ctypes.c_uint64(), ctypes.c_uint32()
+        self._check(self.lib.gnoc_get_broadcast_info(self._h, ctypes.byref(nb), ctypes.byref(passes)))
+        return int(nb.value), int(passes.value)
 
     def set_profiling(self, on: bool) -> None:
         self._check(self.lib.gnoc_set_profiling(self._h, int(on)))

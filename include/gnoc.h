@@ -67,6 +67,11 @@ extern "C" {
 /* per-packet flags */
 #define GNOC_PKT_UNMODELED  0x1u   /* NetworkModel::isModelEnabled() == false
                                       (network_model.cc:171-183): zero delay, no queue update */
+#define GNOC_PKT_BROADCAST  0x2u   /* pkt.receiver == NetPacket::BROADCAST with
+                                      broadcast_tree_enabled: routed on the broadcast tree
+                                      (emesh_hop_by_hop.cc:163-221); dst is ignored.  With the
+                                      tree disabled the caller sends one unicast per tile, as
+                                      Network::netSend does (network.cc:186-195) */
 
 /* output ports per tile: mesh router ports SELF,LEFT,RIGHT,DOWN,UP
  * (network_model_emesh_hop_by_hop.h:43-50) then the injection router's port */
@@ -94,7 +99,7 @@ typedef struct gnoc_config
    int32_t  queue_type;            /* network/emesh_hop_by_hop/queue_model/type (GNOC_QUEUE_*)          */
    int32_t  analytical_enabled;    /* queue_model/<type>/analytical_model_enabled (tree, list)          */
    int32_t  max_list_size;         /* queue_model/<type>/max_list_size (>= 2; unused by basic)          */
-   int32_t  broadcast_tree_enabled;/* network/emesh_hop_by_hop/broadcast_tree_enabled (parsed only)     */
+   int32_t  broadcast_tree_enabled;/* network/emesh_hop_by_hop/broadcast_tree_enabled (GNOC_PKT_BROADCAST) */
    int32_t  device;                /* HIP device ordinal                                                */
 } gnoc_config;
 
@@ -107,7 +112,7 @@ typedef struct gnoc_packets
 {
    const uint64_t *inject_ps;   /* NetPacket::time at Network::netSend                 */
    const uint32_t *src;         /* TILE_ID(pkt.sender)                                  */
-   const uint32_t *dst;         /* TILE_ID(pkt.receiver) (BROADCAST not supported yet)  */
+   const uint32_t *dst;         /* TILE_ID(pkt.receiver); ignored for GNOC_PKT_BROADCAST */
    const uint32_t *bits;        /* NetworkModel::getModeledLength(pkt), bits            */
    const uint32_t *flags;       /* GNOC_PKT_* (may be NULL = all zero)                  */
 } gnoc_packets;
@@ -181,6 +186,22 @@ int gnoc_set_profiling(gnoc_engine *eng, int enable);
  * Fills up to cap entries; *count = number of classes. */
 int gnoc_get_kernel_stats(gnoc_engine *eng, const char **names, double *total_ms,
                           uint32_t *launches, size_t cap, size_t *count);
+
+/* ---- broadcast tree (emesh_hop_by_hop.cc:163-221) ----
+ * A GNOC_PKT_BROADCAST packet leaves the sender's injection port, then at every
+ * router requests UP (cy >= sy), DOWN (cy <= sy), RIGHT (cy == sy, cx >= sx),
+ * LEFT (cy == sy, cx <= sx) and SELF, ports off the mesh dropped; the router
+ * charges the MAX of those queues' delays to the packet and to each port's
+ * contention counters (router_model.cc:86-101, 136-144), and every tile
+ * receives it once.  Results per receipt: row b = the b-th broadcast of the
+ * trace, column = receiving tile (n_entries = broadcasts x num_tiles).  The
+ * packet's own gnoc_get_packet_results entries are those of its latest receipt
+ * (lowest tile on ties).  Batches with broadcasts run in passes until the
+ * visits' max delays repeat (gnoc_get_broadcast_info: count, passes); not on
+ * sharded or sweep engines, and not from device traces. */
+int gnoc_get_broadcast_results(gnoc_engine *eng, uint64_t *final_ps, uint64_t *zero_load_ps,
+                               uint64_t *contention_ps, size_t n_entries);
+int gnoc_get_broadcast_info(const gnoc_engine *eng, uint64_t *nbcast, uint32_t *passes);
 
 /* ---- emesh_hop_counter (network_model_emesh_hop_counter.cc) ---------------
  * The contention-free mesh model: a packet's latency is

@@ -364,12 +364,21 @@ enum { NODE_SEND = 0, NODE_RECEIVE = 1, NODE_EMESH = 2 };   /* network_model.h:1
 enum { PORT_SELF = 0, PORT_LEFT, PORT_RIGHT, PORT_DOWN, PORT_UP, PORT_INJ };  /* emesh .h:43-50 + injection */
 #define PORTS_PER_TILE 6
 #define ORC_FLAG_UNMODELED 1u
+#define ORC_FLAG_BROADCAST 2u   /* pkt.receiver == NetPacket::BROADCAST, broadcast tree enabled */
 
-typedef struct { uint64_t t; uint32_t id; } heap_ent;
+/* One pending Hop.  A unicast packet has one Hop in flight and keeps its state
+ * in the per-packet arrays; a broadcast has one per tree edge, so its EMESH
+ * events carry the tile and the accumulated zero-load delay themselves.  Events
+ * of one packet at one time are at different routers (the tree visits every
+ * router once), so their relative order never reaches a queue. */
+typedef struct { uint64_t t; uint32_t id; uint32_t tile; uint64_t zl; } heap_ent;
 
 typedef struct { heap_ent *a; size_t n, cap; } heap_t;
 
-static int he_less(heap_ent x, heap_ent y) { return x.t < y.t || (x.t == y.t && x.id < y.id); }
+static int he_less(heap_ent x, heap_ent y)
+{
+   return x.t < y.t || (x.t == y.t && (x.id < y.id || (x.id == y.id && x.tile < y.tile)));
+}
 
 static void heap_push(heap_t *h, heap_ent e)
 {
@@ -412,7 +421,12 @@ static heap_ent heap_pop(heap_t *h)
  * Outputs are arrays of n (per packet) or 6*W*H (per port, index tile*6+port,
  * port 0..4 = SELF,LEFT,RIGHT,DOWN,UP of the mesh router, 5 = injection router).
  * port_flits / port_last (may be NULL): _total_utilized_cycles and
- * _last_request_time of each port's queue (queue_model.cc:49-53). */
+ * _last_request_time of each port's queue (queue_model.cc:49-53).
+ * Broadcast packets (flags & ORC_FLAG_BROADCAST; dst ignored) take the tree
+ * branch; bcast_final / bcast_zero_load (may be NULL without broadcasts) get
+ * one row of W*H receipts per broadcast, in trace order, column = receiving
+ * tile.  A broadcast's per-packet entries are those of its latest receipt
+ * (lowest tile on ties). */
 ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
                        uint64_t router_delay, uint64_t link_delay, double frequency,
                        int contention_enabled, int queue_type, int interleaving, int analytical_enabled,
@@ -421,7 +435,8 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
                        const uint32_t *dst, const uint32_t *bits, const uint32_t *flags,
                        uint64_t *final_ps, uint64_t *zero_load_ps, uint64_t *contention_ps,
                        uint64_t *port_sum_delay, uint64_t *port_count, uint64_t *port_mg1,
-                       uint64_t *port_flits, uint64_t *port_last)
+                       uint64_t *port_flits, uint64_t *port_last,
+                       uint64_t *bcast_final, uint64_t *bcast_zero_load)
 {
    const int W = mesh_width, H = mesh_height;
    if (W <= 0 || H <= 0 || flit_width <= 0 || frequency <= 0.0) return -1;
@@ -429,10 +444,19 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
    const uint32_t N = (uint32_t) (W * H);
    const size_t nports = (size_t) N * PORTS_PER_TILE;
 
+   size_t nb = 0;
    for (size_t i = 0; i < n; i++)
    {
-      if (src[i] >= N || dst[i] >= N) return -2;
+      const int bc = (flags[i] & ORC_FLAG_BROADCAST) != 0;
+      if (src[i] >= N || (!bc && dst[i] >= N)) return -2;
       if (i > 0 && inject_ps[i] < inject_ps[i - 1]) return -3; /* must be time ordered */
+      nb += (size_t) bc;
+   }
+   if (nb && (!bcast_final || !bcast_zero_load)) return -1;
+   uint32_t *bidx = (uint32_t *) malloc((n ? n : 1) * sizeof(uint32_t));
+   {
+      uint32_t b = 0;
+      for (size_t i = 0; i < n; i++) bidx[i] = (flags[i] & ORC_FLAG_BROADCAST) ? b++ : 0xFFFFFFFFu;
    }
 
    orc_queue **q = NULL;
@@ -464,7 +488,7 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
       pnode[i] = NODE_SEND;
       zero_load_ps[i] = 0;
       contention_ps[i] = 0;
-      heap_ent e = { inject_ps[i], (uint32_t) i };
+      heap_ent e = { inject_ps[i], (uint32_t) i, src[i], 0 };
       heap_push(&h, e);
    }
 
@@ -474,21 +498,30 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
    {
       heap_ent e = heap_pop(&h);
       const uint32_t id = e.id;
-      const uint64_t t = ptime[id];
+      const uint64_t t = e.t;   /* == ptime[id] for a unicast packet */
       const uint32_t F = (bits[id] % (uint32_t) flit_width) ? bits[id] / (uint32_t) flit_width + 1
                                                            : bits[id] / (uint32_t) flit_width; /* network_model.cc:202-212 */
       const int modeled = !(flags[id] & ORC_FLAG_UNMODELED); /* network_model.cc:171-183 */
 
+      const int bc = (flags[id] & ORC_FLAG_BROADCAST) != 0;
       if (pnode[id] == NODE_SEND)
       {
          /* network_model.cc:413-468 processCornerCases: self-send -> RECEIVE, no delay;
-          * network_model.cc:129-133 __processReceivedPacket returns early for it. */
-         if (src[id] == dst[id] || !modeled)
+          * network_model.cc:129-133 __processReceivedPacket returns early for it.
+          * A broadcast is never a self-send (receiver is BROADCAST); its hops to the
+          * system tiles (:453-459) are direct and touch no queue. */
+         if ((!bc && src[id] == dst[id]) || !modeled)
          {
             /* unmodeled packets traverse with zero router/link delay and no
              * queue interaction (router_model.cc:74-75, electrical_link_model.cc:32-33),
              * and __processReceivedPacket skips serialization. */
             final_ps[id] = t;
+            if (bc)
+               for (uint32_t c = 0; c < N; c++)
+               {
+                  bcast_final[(size_t) bidx[id] * N + c] = t;
+                  bcast_zero_load[(size_t) bidx[id] * N + c] = 0;
+               }
             continue;
          }
          /* emesh routePacket SEND_TILE branch, :151-159: injection router (delay 0) */
@@ -506,8 +539,63 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
          zero_load_ps[id] += zl;
          contention_ps[id] += c0ps;
          pnode[id] = NODE_EMESH;
-         heap_ent ne = { ptime[id], id };
+         heap_ent ne = { ptime[id], id, src[id], zero_load_ps[id] };
          heap_push(&h, ne);
+         continue;
+      }
+
+      if (bc)
+      {
+         /* EMESH broadcast branch, emesh_hop_by_hop.cc:163-221: the tree from the
+          * sender -- UP if cy >= sy, DOWN if cy <= sy, along the sender's row
+          * RIGHT if cx >= sx and LEFT if cx <= sx, then SELF; off-mesh tiles
+          * (computeTileID -> INVALID_TILE_ID, :274-280) are dropped. */
+         const int cur = (int) e.tile;
+         const int cx = cur % W, cy = cur / W;
+         const int sx = (int) (src[id] % (uint32_t) W), sy = (int) (src[id] / (uint32_t) W);
+         int ports[5], nexts[5], np = 0;
+         if (cy >= sy && cy + 1 < H) { ports[np] = PORT_UP; nexts[np++] = cur + W; }
+         if (cy <= sy && cy - 1 >= 0) { ports[np] = PORT_DOWN; nexts[np++] = cur - W; }
+         if (cy == sy)
+         {
+            if (cx >= sx && cx + 1 < W) { ports[np] = PORT_RIGHT; nexts[np++] = cur + 1; }
+            if (cx <= sx && cx - 1 >= 0) { ports[np] = PORT_LEFT; nexts[np++] = cur - 1; }
+         }
+         ports[np] = PORT_SELF;
+         nexts[np++] = cur;
+         /* every selected link adds link_delay: zero_load += max = Lk; the router
+          * adds R (router_model.cc:83) and charges the MAX queue delay over the
+          * selected ports to the packet and to every one of them (:86-101, 136-144) */
+         uint64_t m = 0;
+         if (contention_enabled)
+         {
+            const uint64_t tc = time_to_cycles(t, frequency);
+            for (int k = 0; k < np; k++)
+            {
+               const uint64_t d = orc_queue_compute(q[(size_t) cur * PORTS_PER_TILE + (size_t) ports[k]], tc, F);
+               m = d > m ? d : m;
+            }
+            for (int k = 0; k < np; k++)
+            {
+               port_sum_delay[(size_t) cur * PORTS_PER_TILE + (size_t) ports[k]] += m;
+               port_count[(size_t) cur * PORTS_PER_TILE + (size_t) ports[k]]++;
+            }
+         }
+         const uint64_t tn = t + lat_to_ps(m, frequency) + rl_ps;
+         const uint64_t zn = e.zl + rl_ps;
+         for (int k = 0; k < np; k++)
+         {
+            if (ports[k] == PORT_SELF)
+            {
+               /* RECEIVE_TILE at this tile: + serialization (network_model.cc:142-150) */
+               const uint64_t fps = lat_to_ps(F, frequency);
+               bcast_final[(size_t) bidx[id] * N + (size_t) cur] = tn + fps;
+               bcast_zero_load[(size_t) bidx[id] * N + (size_t) cur] = zn + fps;
+               continue;
+            }
+            heap_ent ne = { tn, id, (uint32_t) nexts[k], zn };
+            heap_push(&h, ne);
+         }
          continue;
       }
 
@@ -546,9 +634,23 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
          continue;
       }
       ptile[id] = (uint32_t) next;
-      heap_ent ne = { ptime[id], id };
+      heap_ent ne = { ptime[id], id, (uint32_t) next, 0 };
       heap_push(&h, ne);
    }
+
+   /* a broadcast's per-packet entries: its latest receipt */
+   for (size_t i = 0; i < n; i++)
+   {
+      if (bidx[i] == 0xFFFFFFFFu || !(pnode[i] == NODE_EMESH)) continue;
+      const uint64_t *bf = bcast_final + (size_t) bidx[i] * N, *bz = bcast_zero_load + (size_t) bidx[i] * N;
+      uint32_t best = 0;
+      for (uint32_t c = 1; c < N; c++)
+         if (bf[c] > bf[best]) best = c;
+      final_ps[i] = bf[best];
+      zero_load_ps[i] = bz[best];
+      contention_ps[i] = bf[best] - inject_ps[i] - bz[best];
+   }
+   free(bidx);
 
    if (contention_enabled)
    {

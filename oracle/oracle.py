@@ -55,7 +55,7 @@ def lib() -> ctypes.CDLL:
         L.orc_queue_create_type.restype = vp
         L.orc_queue_create_type.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, u64]
         L.orc_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u64, u64, ctypes.c_double, ctypes.c_int,
-                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t] + [vp] * 13
+                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t] + [vp] * 15
         _orc = L
     return _orc
 
@@ -141,6 +141,9 @@ class OracleResult:
     port_mg1: np.ndarray
     port_flit: np.ndarray = None     # QueueModel _total_utilized_cycles per port
     port_last: np.ndarray = None     # QueueModel _last_request_time per port
+    # broadcast receipts: [broadcast (trace order), receiving tile]
+    bcast_final_ps: np.ndarray = None
+    bcast_zero_load_ps: np.ndarray = None
 
 
 def run(cfg, tr) -> OracleResult:
@@ -157,12 +160,14 @@ def run(cfg, tr) -> OracleResult:
     fin, zl, ct = (np.zeros(n, np.uint64) for _ in range(3))
     npt = W * H * 6
     ps, pc, pm, pf, pl = (np.zeros(npt, np.uint64) for _ in range(5))
+    nb = int(np.count_nonzero(flags & 2))
+    bf, bz = (np.zeros((nb, W * H), np.uint64) for _ in range(2))
     rc = L.orc_run(W, H, cfg.flit_width, cfg.router_delay, cfg.link_delay, cfg.frequency_ghz,
                    int(cfg.contention_enabled), int(getattr(cfg, "queue_type", 0)),
                    int(getattr(cfg, "interleaving_enabled", True)), int(cfg.analytical_enabled), cfg.max_list_size, n,
                    inj.ctypes.data, src.ctypes.data, dst.ctypes.data, bits.ctypes.data, flags.ctypes.data,
                    fin.ctypes.data, zl.ctypes.data, ct.ctypes.data, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data,
-                   pf.ctypes.data, pl.ctypes.data)
+                   pf.ctypes.data, pl.ctypes.data, bf.ctypes.data if nb else None, bz.ctypes.data if nb else None)
     if rc:
         raise ValueError(f"oracle rejected input (rc={rc})")
-    return OracleResult(fin, zl, ct, ps, pc, pm, pf, pl)
+    return OracleResult(fin, zl, ct, ps, pc, pm, pf, pl, bf, bz)

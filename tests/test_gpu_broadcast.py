@@ -1,0 +1,108 @@
+"""Broadcast tree on the GPU vs the CPU oracle.
+
+emesh_hop_by_hop.cc:163-221 routes a broadcast UP/DOWN from every tile of the
+sender's row and along that row, requesting several output ports per router;
+router_model.cc:86-101 charges the max of their queue delays to the packet and
+to each port.  Bit-exact on every per-packet, per-receipt and per-port output,
+with the pass count reported by gnoc_get_broadcast_info.
+"""
+import numpy as np
+import pytest
+
+from graphite_amd import gnoc
+from oracle import oracle
+from tests.test_gpu_parity import assert_same
+from tests.traces import random_trace
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(cfg, tr):
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    got = eng.results()
+    info = eng.broadcast_info()
+    eng.close()
+    return got, oracle.run(cfg, tr), info
+
+
+def assert_bcast_same(got, ref, tr):
+    assert_same(got, ref)
+    assert np.array_equal(got.bcast_final_ps, ref.bcast_final_ps)
+    assert np.array_equal(got.bcast_zero_load_ps, ref.bcast_zero_load_ps)
+    rows = np.nonzero(tr.flags & gnoc.PKT_BROADCAST)[0]
+    ct = ref.bcast_final_ps - tr.inject_ps[rows][:, None] - ref.bcast_zero_load_ps
+    assert np.array_equal(got.bcast_contention_ps, ct)
+
+
+@pytest.mark.parametrize("W,H", [(4, 4), (3, 5), (1, 6), (6, 1), (8, 8)])
+def test_mixed_unicast_broadcast(W, H):
+    cfg = gnoc.EngineConfig(num_tiles=W * H, mesh_width=W, mesh_height=H)
+    tr = random_trace(3000, W, H, seed=W * 7 + H, max_cycle=3000, bcast_frac=0.02, self_frac=0.03)
+    got, ref, (nb, passes) = run_both(cfg, tr)
+    assert nb == int(((tr.flags & gnoc.PKT_BROADCAST) != 0).sum()) > 0
+    assert_bcast_same(got, ref, tr)
+
+
+def test_contended_needs_several_passes():
+    """Dense broadcasts: sibling ports' maxima feed back across levels."""
+    cfg = gnoc.EngineConfig(num_tiles=16)
+    tr = random_trace(1500, 4, 4, seed=21, max_cycle=600, bcast_frac=0.05)
+    got, ref, (nb, passes) = run_both(cfg, tr)
+    assert_bcast_same(got, ref, tr)
+    assert ref.port_sum_delay.sum() > 0 and passes >= 2
+
+
+def test_saturated_burst_mg1():
+    cfg = gnoc.EngineConfig(num_tiles=16)
+    tr = random_trace(2000, 4, 4, seed=5, max_cycle=100, burst0=300, bcast_frac=0.03)
+    got, ref, _ = run_both(cfg, tr)
+    assert ref.port_mg1.sum() > 0
+    assert_bcast_same(got, ref, tr)
+
+
+def test_only_broadcasts():
+    cfg = gnoc.EngineConfig(num_tiles=25, mesh_width=5, mesh_height=5)
+    tr = random_trace(120, 5, 5, seed=8, max_cycle=2000, bcast_frac=1.0)
+    got, ref, _ = run_both(cfg, tr)
+    assert_bcast_same(got, ref, tr)
+
+
+@pytest.mark.parametrize("kw", [dict(frequency_ghz=0.9), dict(max_list_size=2), dict(analytical_enabled=False),
+                                dict(router_delay=0, flit_width=32), dict(queue_type=gnoc.QUEUE_BASIC)])
+def test_config_variants(kw):
+    cfg = gnoc.EngineConfig(num_tiles=16, **kw)
+    f = kw.get("frequency_ghz", 1.0)
+    tr = random_trace(1500, 4, 4, seed=31, max_cycle=1500, burst0=40, bcast_frac=0.03, frequency_ghz=f,
+                      ps_jitter=f != 1.0, bits_choices=[72, 576, 1088])
+    got, ref, _ = run_both(cfg, tr)
+    assert_bcast_same(got, ref, tr)
+
+
+def test_unmodeled_and_contention_off():
+    tr = random_trace(1000, 4, 4, seed=12, max_cycle=800, unmodeled_frac=0.1, bcast_frac=0.05)
+    for cfg in (gnoc.EngineConfig(num_tiles=16), gnoc.EngineConfig(num_tiles=16, contention_enabled=False)):
+        got, ref, _ = run_both(cfg, tr)
+        assert_bcast_same(got, ref, tr)
+
+
+def test_tree_disabled_means_caller_expands():
+    tr = random_trace(800, 4, 4, seed=13, max_cycle=1500, bcast_frac=0.02)
+    cfg = gnoc.EngineConfig(num_tiles=16, broadcast_tree_enabled=False)
+    eng = gnoc.Engine(cfg)
+    with pytest.raises(gnoc.GnocError):
+        eng.submit(tr)
+    eng.close()
+    ex = gnoc.expand_broadcasts(tr, 16)
+    got, ref, (nb, _) = run_both(cfg, ex)
+    assert nb == 0
+    assert_same(got, ref)
+
+
+def test_broadcast_refused_on_sweep():
+    tr = random_trace(100, 4, 4, seed=1, bcast_frac=0.1)
+    pts = [gnoc.SweepPoint(flit_width=64, router_delay=1, link_delay=1, tile_width_mm=1.0)] * 2
+    with pytest.raises(gnoc.GnocError):
+        sw = gnoc.SweepEngine(gnoc.EngineConfig(num_tiles=16), pts)
+        sw.submit([tr, tr])

@@ -1,11 +1,11 @@
 """Trace builders shared by the tests (small, seeded)."""
 import numpy as np
 
-from graphite_amd.gnoc import Trace, PKT_UNMODELED
+from graphite_amd.gnoc import Trace, PKT_BROADCAST, PKT_UNMODELED
 
 
 def random_trace(n, W, H, seed=0, max_cycle=200, burst0=0, self_frac=0.0, unmodeled_frac=0.0,
-                 bits=576, bits_choices=None, ps_jitter=False, frequency_ghz=1.0):
+                 bits=576, bits_choices=None, ps_jitter=False, frequency_ghz=1.0, bcast_frac=0.0):
     """Random (time, id)-ordered trace; burst0 packets injected at t=0."""
     rng = np.random.default_rng(seed)
     N = W * H
@@ -24,6 +24,8 @@ def random_trace(n, W, H, seed=0, max_cycle=200, burst0=0, self_frac=0.0, unmode
     flags = np.zeros(n, np.uint32)
     if unmodeled_frac:
         flags[rng.random(n) < unmodeled_frac] = PKT_UNMODELED
+    if bcast_frac:
+        flags[rng.random(n) < bcast_frac] |= PKT_BROADCAST
     if bits_choices is not None:
         b = rng.choice(np.asarray(bits_choices, np.uint32), n).astype(np.uint32)
     else:
