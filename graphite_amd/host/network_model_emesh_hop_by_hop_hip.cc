@@ -112,15 +112,20 @@ void NetworkModelEMeshHopByHopHIP::reserve(size_t n)
 uint32_t NetworkModelEMeshHopByHopHIP::routePacket(const NetPacket& pkt)
 {
    // NetworkModel::__routePacket asserts (network_model.cc:109-113), here as errors
-   if (pkt.sender < 0 || pkt.sender >= _cfg.num_tiles || pkt.receiver < 0 || pkt.receiver >= _cfg.num_tiles)
+   const bool bc = pkt.receiver == NetPacket::BROADCAST;
+   if (pkt.sender < 0 || pkt.sender >= _cfg.num_tiles || (!bc && (pkt.receiver < 0 || pkt.receiver >= _cfg.num_tiles)))
       throw NetworkModelError(GNOC_ETRACE, "pkt_sender/pkt_receiver outside the application tiles");
+   // hasBroadcastCapability() is broadcast_tree_enabled (emesh_hop_by_hop.cc:25); without
+   // it Network::netSend hands the model one unicast per tile (network.cc:186-195)
+   if (bc && !_cfg.broadcast_tree_enabled)
+      throw NetworkModelError(GNOC_EINVAL, "broadcast without broadcast_tree_enabled: Network::netSend expands it");
    if (!_inj.empty() && pkt.time < _inj.back())
       throw NetworkModelError(GNOC_ETRACE, "packets must be routed in time order");
    _inj.push_back(pkt.time);
    _src.push_back((uint32_t) pkt.sender);
-   _dst.push_back((uint32_t) pkt.receiver);
+   _dst.push_back(bc ? (uint32_t) pkt.sender : (uint32_t) pkt.receiver);
    _bits.push_back(pkt.modeled_bits);
-   _flags.push_back(pkt.modeled ? 0u : GNOC_PKT_UNMODELED);
+   _flags.push_back((pkt.modeled ? 0u : GNOC_PKT_UNMODELED) | (bc ? GNOC_PKT_BROADCAST : 0u));
    _ran = false;
    return (uint32_t) (_inj.size() - 1);
 }
@@ -148,9 +153,35 @@ void NetworkModelEMeshHopByHopHIP::run()
    _pflit.resize(np);
    _plast.resize(np);
    check(gnoc_get_port_utilization(_eng, _pflit.data(), _plast.data(), np), "gnoc_get_port_utilization");
+   _bidx.assign(n, 0xFFFFFFFFu);
+   uint32_t nb = 0;
+   for (size_t i = 0; i < n; i++)
+      if (_flags[i] & GNOC_PKT_BROADCAST) _bidx[i] = nb++;
+   const size_t nv = (size_t) nb * _cfg.num_tiles;
+   _bfin.resize(nv);
+   _bzl.resize(nv);
+   _bct.resize(nv);
+   check(gnoc_get_broadcast_results(_eng, _bfin.data(), _bzl.data(), _bct.data(), nv), "gnoc_get_broadcast_results");
    _rflit.clear();
    _rpkt.clear();
    _ran = true;
+}
+
+size_t NetworkModelEMeshHopByHopHIP::receipt(uint32_t id, int tile) const
+{
+   if (!_ran) throw NetworkModelError(GNOC_ESTATE, "no results before run()");
+   if (id >= _bidx.size() || _bidx[id] == 0xFFFFFFFFu) throw NetworkModelError(GNOC_EINVAL, "not a broadcast packet");
+   if (tile < 0 || tile >= _cfg.num_tiles) throw NetworkModelError(GNOC_EINVAL, "tile outside the mesh");
+   return (size_t) _bidx[id] * _cfg.num_tiles + (size_t) tile;
+}
+uint64_t NetworkModelEMeshHopByHopHIP::broadcastReceiptTime(uint32_t id, int tile) const { return _bfin[receipt(id, tile)]; }
+uint64_t NetworkModelEMeshHopByHopHIP::broadcastReceiptZeroLoadDelay(uint32_t id, int tile) const
+{
+   return _bzl[receipt(id, tile)];
+}
+uint64_t NetworkModelEMeshHopByHopHIP::broadcastReceiptContentionDelay(uint32_t id, int tile) const
+{
+   return _bct[receipt(id, tile)];
 }
 
 gnoc_summary NetworkModelEMeshHopByHopHIP::summary() const
@@ -173,10 +204,33 @@ void NetworkModelEMeshHopByHopHIP::buildEventCounters() const
    const uint32_t fw = (uint32_t) _cfg.flit_width;
    std::vector<int64_t> rf((size_t) (W + 1) * H, 0), rp((size_t) (W + 1) * H, 0);
    std::vector<int64_t> cf((size_t) (H + 1) * W, 0), cp((size_t) (H + 1) * W, 0);
+   _rxbar.assign((size_t) W * H * 5, 0);
+   _rlink.assign((size_t) W * H, 0);
+   std::vector<uint64_t> bflit((size_t) W * H, 0), bpkt((size_t) W * H, 0);
    for (size_t i = 0; i < _inj.size(); i++)
    {
-      if (_src[i] == _dst[i] || _flags[i]) continue;
+      if (_flags[i] & GNOC_PKT_UNMODELED) continue;
       const int64_t F = (_bits[i] % fw) ? _bits[i] / fw + 1 : _bits[i] / fw;
+      if (_flags[i] & GNOC_PKT_BROADCAST)
+      {
+         // the tree visits every router once, selecting UP/DOWN/RIGHT/LEFT/SELF
+         // (emesh_hop_by_hop.cc:170-204): crossbar[#ports], one link per port
+         const int sx = (int) _src[i] % W, sy = (int) _src[i] / W;
+         for (int t = 0; t < W * H; t++)
+         {
+            const int cx = t % W, cy = t / W;
+            int np = 1;
+            np += (cy >= sy && cy + 1 < H);
+            np += (cy <= sy && cy >= 1);
+            if (cy == sy) np += (cx >= sx && cx + 1 < W) + (cx <= sx && cx >= 1);
+            bflit[t] += (uint64_t) F;
+            bpkt[t] += 1;
+            _rxbar[(size_t) t * 5 + np - 1] += (uint64_t) F;
+            _rlink[t] += (uint64_t) (F * np);
+         }
+         continue;
+      }
+      if (_src[i] == _dst[i]) continue;
       const int sx = (int) _src[i] % W, sy = (int) _src[i] / W, dx = (int) _dst[i] % W, dy = (int) _dst[i] / W;
       const int x0 = sx < dx ? sx : dx, x1 = sx < dx ? dx : sx;
       rf[(size_t) sy * (W + 1) + x0] += F;
@@ -216,6 +270,27 @@ void NetworkModelEMeshHopByHopHIP::buildEventCounters() const
          _rpkt[(size_t) y * W + x] += (uint64_t) b;
       }
    }
+   // a unicast hop crosses the crossbar to one port and one link
+   for (size_t t = 0; t < (size_t) W * H; t++)
+   {
+      _rxbar[t * 5] += _rflit[t];
+      _rlink[t] += _rflit[t];
+      _rflit[t] += bflit[t];
+      _rpkt[t] += bpkt[t];
+   }
+}
+
+uint64_t NetworkModelEMeshHopByHopHIP::routerCrossbarTraversals(int tile, int ports) const
+{
+   if (_rpkt.empty()) buildEventCounters();
+   if (ports < 1 || ports > 5) throw NetworkModelError(GNOC_EINVAL, "crossbar port count outside 1..5");
+   return _rxbar.at((size_t) tile * 5 + ports - 1);
+}
+
+uint64_t NetworkModelEMeshHopByHopHIP::routerLinkTraversals(int tile) const
+{
+   if (_rpkt.empty()) buildEventCounters();
+   return _rlink.at((size_t) tile);
 }
 
 uint64_t NetworkModelEMeshHopByHopHIP::routerFlits(int tile) const
@@ -237,11 +312,28 @@ void NetworkModelEMeshHopByHopHIP::outputSummary(std::ostream& out, int tile) co
    const uint32_t fw = (uint32_t) _cfg.flit_width;
    auto flits = [&](uint32_t bits) -> uint64_t { return (bits % fw) ? bits / fw + 1 : bits / fw; };
    // updateSendCounters / updateReceiveCounters (network_model.cc:229-272): modeled,
-   // non-self packets; broadcast is not produced by this path.
-   uint64_t ps = 0, fs = 0, bs = 0, pr = 0, fr = 0, br = 0, lat = 0, cont = 0;
+   // non-self packets; a broadcast counts as sent and broadcasted at its sender
+   // and as received, with that receipt's delays, at every tile.
+   uint64_t ps = 0, fs = 0, bs = 0, pb = 0, fb = 0, bb = 0, pr = 0, fr = 0, br = 0, lat = 0, cont = 0;
    for (size_t i = 0; i < _inj.size(); i++)
    {
-      if (_src[i] == _dst[i] || _flags[i]) continue;
+      if (_flags[i] & GNOC_PKT_UNMODELED) continue;
+      if (_flags[i] & GNOC_PKT_BROADCAST)
+      {
+         if ((int) _src[i] == tile)
+         {
+            ps++; fs += flits(_bits[i]); bs += _bits[i];
+            pb++; fb += flits(_bits[i]); bb += _bits[i];
+         }
+         const size_t k = receipt((uint32_t) i, tile);
+         pr++;
+         fr += flits(_bits[i]);
+         br += _bits[i];
+         lat += _bzl[k] + _bct[k];
+         cont += _bct[k];
+         continue;
+      }
+      if (_src[i] == _dst[i]) continue;
       if ((int) _src[i] == tile) { ps++; fs += flits(_bits[i]); bs += _bits[i]; }
       if ((int) _dst[i] == tile)
       {
@@ -256,9 +348,9 @@ void NetworkModelEMeshHopByHopHIP::outputSummary(std::ostream& out, int tile) co
    out << "    Total Packets Sent: " << ps << "\n";
    out << "    Total Flits Sent: " << fs << "\n";
    out << "    Total Bits Sent: " << bs << "\n";
-   out << "    Total Packets Broadcasted: 0\n";
-   out << "    Total Flits Broadcasted: 0\n";
-   out << "    Total Bits Broadcasted: 0\n";
+   out << "    Total Packets Broadcasted: " << pb << "\n";
+   out << "    Total Flits Broadcasted: " << fb << "\n";
+   out << "    Total Bits Broadcasted: " << bb << "\n";
    out << "    Total Packets Received: " << pr << "\n";
    out << "    Total Flits Received: " << fr << "\n";
    out << "    Total Bits Received: " << br << "\n";
@@ -276,14 +368,14 @@ void NetworkModelEMeshHopByHopHIP::outputSummary(std::ostream& out, int tile) co
       out << "    Average Contention Delay (in clock cycles): 0\n";
       out << "    Average Contention Delay (in nanoseconds): 0\n";
    }
-   // outputEventCountSummary (:436-468): unicast traffic uses crossbar[1] only
+   // outputEventCountSummary (:436-468)
    const uint64_t rfl = routerFlits(tile);
    out << "    Event Counters:\n";
    out << "      Buffer Writes: " << rfl << "\n";
    out << "      Buffer Reads: " << rfl << "\n";
    out << "      Switch Allocator Requests: " << routerPackets(tile) << "\n";
-   for (int i = 1; i <= 5; i++) out << "      Crossbar[" << i << "] Traversals: " << (i == 1 ? rfl : 0) << "\n";
-   out << "      Link Traversals: " << rfl << "\n";
+   for (int i = 1; i <= 5; i++) out << "      Crossbar[" << i << "] Traversals: " << routerCrossbarTraversals(tile, i) << "\n";
+   out << "      Link Traversals: " << routerLinkTraversals(tile) << "\n";
    if (!_cfg.contention_enabled) return;   // emesh_hop_by_hop.cc:304-305
    // outputContentionModelsSummary: the mesh router's 5 output ports
    uint64_t sd = 0, sp = 0, sa = 0;

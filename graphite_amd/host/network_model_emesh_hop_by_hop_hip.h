@@ -66,6 +66,7 @@ private:
 // Trace-mode NetPacket: the fields this path reads (network.h:27-55).
 struct NetPacket
 {
+   static constexpr int32_t BROADCAST = (int32_t) 0xDEADBABE;   // network.h:54
    uint64_t time = 0;          // NetPacket::time at netSend, picoseconds
    int32_t sender = 0;         // TILE_ID(pkt.sender)
    int32_t receiver = 0;       // TILE_ID(pkt.receiver)
@@ -101,6 +102,11 @@ public:
    const std::vector<uint64_t>& packetTime() const { return _final; }
    const std::vector<uint64_t>& packetZeroLoadDelay() const { return _zl; }
    const std::vector<uint64_t>& packetContentionDelay() const { return _ct; }
+   // A broadcast's receipt at `tile` (processReceivedPacket of the copy the
+   // tree delivers there); the packetTime() entry is its latest receipt.
+   uint64_t broadcastReceiptTime(uint32_t id, int tile) const;
+   uint64_t broadcastReceiptZeroLoadDelay(uint32_t id, int tile) const;
+   uint64_t broadcastReceiptContentionDelay(uint32_t id, int tile) const;
 
    // RouterModel::_total_contention_delay / _total_packets per output port
    // (index tile*6 + GNOC_PORT_*; GNOC_PORT_INJ = the injection router) and
@@ -116,10 +122,13 @@ public:
    // Mesh-router event counters of a tile (RouterModel::updateEventCounters,
    // router_model.cc:119-127; ElectricalLinkModel::processPacket,
    // electrical_link_model.cc:29-45): flits through the router (= buffer
-   // writes = buffer reads = crossbar[1] = link traversals for unicast) and
-   // packets through it (= switch allocator requests).  Route-static.
+   // writes = buffer reads), packets through it (= switch allocator
+   // requests), crossbar traversals by number of output ports (1..5; a
+   // broadcast visit uses several) and flits over its links.  Route-static.
    uint64_t routerFlits(int tile) const;
    uint64_t routerPackets(int tile) const;
+   uint64_t routerCrossbarTraversals(int tile, int ports) const;
+   uint64_t routerLinkTraversals(int tile) const;
 
    // The per-tile sim.out network section of NetworkModelEMeshHopByHop::outputSummary
    // (network_model_emesh_hop_by_hop.cc:299-306): NetworkModel::outputSummary
@@ -150,7 +159,10 @@ private:
    std::vector<uint64_t> _inj;
    std::vector<uint32_t> _src, _dst, _bits, _flags;
    std::vector<uint64_t> _final, _zl, _ct, _psum, _pcnt, _pmg1, _pflit, _plast;
-   mutable std::vector<uint64_t> _rflit, _rpkt;   // event counters, built on first use
+   std::vector<uint32_t> _bidx;                    // packet id -> broadcast index (broadcasts only)
+   std::vector<uint64_t> _bfin, _bzl, _bct;        // broadcast receipts [b * N + tile]
+   mutable std::vector<uint64_t> _rflit, _rpkt, _rxbar, _rlink;   // event counters, built on first use
+   size_t receipt(uint32_t id, int tile) const;
    void buildEventCounters() const;
    bool _ran = false;
 };

@@ -88,6 +88,28 @@ int main()
       EXPECT_EQ(mc.size(), 4);
       EXPECT_EQ(mc[0], 1 + 1 * 4);
    }
+   // 5. broadcast tree (emesh_hop_by_hop.cc:163-221) from tile 5 = (1, 1) of 4x4:
+   //    every tile receives at (H+1)(R+Lk) + F; the sender's router selects all
+   //    5 ports (crossbar[5]), a row router 4 (UP, DOWN, onward, SELF).
+   {
+      NetworkModelEMeshHopByHopHIP m(cfg);
+      m.routePacket(pkt(0, 5, NetPacket::BROADCAST));
+      m.run();
+      EXPECT_EQ(m.broadcastReceiptTime(0, 5), (1 * 2 + 9) * 1000);
+      EXPECT_EQ(m.broadcastReceiptTime(0, 15), (5 * 2 + 9) * 1000);   // H = 4
+      EXPECT_EQ(m.broadcastReceiptContentionDelay(0, 15), 0);
+      EXPECT_EQ(m.packetTime()[0], (5 * 2 + 9) * 1000);                 // latest receipt
+      EXPECT_EQ(m.routerCrossbarTraversals(5, 5), 9);
+      EXPECT_EQ(m.routerCrossbarTraversals(6, 4), 9);
+      EXPECT_EQ(m.routerLinkTraversals(6), 4 * 9);
+      EXPECT_EQ(m.routerPackets(0), 1);
+      CfgView nt = cfg;
+      nt.set("network/emesh_hop_by_hop/broadcast_tree_enabled", "false");
+      NetworkModelEMeshHopByHopHIP m2(nt);
+      bool threw = false;
+      try { m2.routePacket(pkt(0, 5, NetPacket::BROADCAST)); } catch (const NetworkModelError& e) { threw = e.status == GNOC_EINVAL; }
+      EXPECT_EQ(threw, 1);
+   }
    if (failures)
    {
       std::fprintf(stderr, "%d failure(s)\n", failures);

@@ -34,22 +34,38 @@ def expected_summary(cfg, tr, res, tile: int) -> str:
     src, dst, bits = tr.src.astype(np.int64), tr.dst.astype(np.int64), tr.bits.astype(np.int64)
     flags = tr.flags if tr.flags is not None else np.zeros(len(src), np.uint32)
     F = (bits + fw - 1) // fw
-    live = (src != dst) & (flags == 0)
-    s = live & (src == tile)
+    bcast = (flags & 2) != 0
+    modeled = (flags & 1) == 0
+    live = (src != dst) & modeled & ~bcast
+    bc = bcast & modeled                      # routed on the broadcast tree
+    brow = np.cumsum(bcast) - 1               # row of each broadcast in res.bcast_*
+    s = (live | bc) & (src == tile)
+    sb = bc & (src == tile)
     r = live & (dst == tile)
     lat = int((res.zero_load_ps[r].astype(np.int64) + res.contention_ps[r].astype(np.int64)).sum())
     cont = int(res.contention_ps[r].astype(np.int64).sum())
     pr = int(r.sum())
+    fr, br = int(F[r].sum()), int(bits[r].sum())
+    inj = tr.inject_ps.astype(np.int64)
+    for i in np.nonzero(bc)[0]:
+        # every tile receives a broadcast once (NetworkModel::updateReceiveCounters per receipt)
+        zl = int(res.bcast_zero_load_ps[brow[i], tile])
+        ct = int(res.bcast_final_ps[brow[i], tile]) - int(inj[i]) - zl
+        lat += zl + ct
+        cont += ct
+        pr += 1
+        fr += int(F[i])
+        br += int(bits[i])
     out = []
     out.append(f"    Total Packets Sent: {int(s.sum())}")
     out.append(f"    Total Flits Sent: {int(F[s].sum())}")
     out.append(f"    Total Bits Sent: {int(bits[s].sum())}")
-    out.append("    Total Packets Broadcasted: 0")
-    out.append("    Total Flits Broadcasted: 0")
-    out.append("    Total Bits Broadcasted: 0")
+    out.append(f"    Total Packets Broadcasted: {int(sb.sum())}")
+    out.append(f"    Total Flits Broadcasted: {int(F[sb].sum())}")
+    out.append(f"    Total Bits Broadcasted: {int(bits[sb].sum())}")
     out.append(f"    Total Packets Received: {pr}")
-    out.append(f"    Total Flits Received: {int(F[r].sum())}")
-    out.append(f"    Total Bits Received: {int(bits[r].sum())}")
+    out.append(f"    Total Flits Received: {fr}")
+    out.append(f"    Total Bits Received: {br}")
     if pr > 0:
         f = cfg.frequency_ghz
         cyc = lambda ps: int(math.ceil((float(ps) * f) / 1.0e3))
@@ -67,13 +83,27 @@ def expected_summary(cfg, tr, res, tile: int) -> str:
     on_col = live & (dx == tx) & (dy != sy) & (((dy > sy) & (sy < ty) & (ty <= dy)) | ((dy < sy) & (dy <= ty) & (ty < sy)))
     through = on_row | on_col
     fl = int(F[through].sum())
+    xbar = [fl, 0, 0, 0, 0]
+    link = fl
+    sar = int(through.sum())
+    # broadcasts: the tree visits this router once, with UP/DOWN/RIGHT/LEFT/SELF
+    # selected as in emesh_hop_by_hop.cc:170-204 (crossbar[#ports], a link per port)
+    for i in np.nonzero(bc)[0]:
+        bx, by = int(sx[i]), int(sy[i])
+        npt = 1 + int(ty >= by and ty + 1 < H) + int(ty <= by and ty >= 1)
+        if ty == by:
+            npt += int(tx >= bx and tx + 1 < W) + int(tx <= bx and tx >= 1)
+        fl += int(F[i])
+        sar += 1
+        xbar[npt - 1] += int(F[i])
+        link += int(F[i]) * npt
     out.append("    Event Counters:")
     out.append(f"      Buffer Writes: {fl}")
     out.append(f"      Buffer Reads: {fl}")
-    out.append(f"      Switch Allocator Requests: {int(through.sum())}")
+    out.append(f"      Switch Allocator Requests: {sar}")
     for i in range(1, 6):
-        out.append(f"      Crossbar[{i}] Traversals: {fl if i == 1 else 0}")
-    out.append(f"      Link Traversals: {fl}")
+        out.append(f"      Crossbar[{i}] Traversals: {xbar[i - 1]}")
+    out.append(f"      Link Traversals: {link}")
     if cfg.contention_enabled:
         k = tile * 6 + np.arange(5)
         sd, sp, sa = (int(a[k].sum()) for a in (res.port_sum_delay, res.port_count, res.port_mg1))

@@ -26,6 +26,8 @@ def cases():
     yield "flit16", gnoc.EngineConfig(num_tiles=36, flit_width=16, router_delay=2), random_trace(
         3000, 6, 6, seed=4, max_cycle=900, bits_choices=[72, 576, 1088])
     yield "nocont", gnoc.EngineConfig(num_tiles=16, contention_enabled=False), random_trace(1500, 4, 4, seed=5)
+    yield "bcast", gnoc.EngineConfig(num_tiles=20, mesh_width=5, mesh_height=4), random_trace(
+        2000, 5, 4, seed=6, max_cycle=2500, self_frac=0.03, unmodeled_frac=0.03, bcast_frac=0.03)
 
 
 def test_event_counters_match_oracle_requests():
@@ -35,15 +37,19 @@ def test_event_counters_match_oracle_requests():
         ref = oracle.run(cfg, tr)
         for t in range(cfg.width * cfg.height):
             txt = expected_summary(cfg, tr, ref, t)
-            sar = int(txt.split("Switch Allocator Requests: ")[1].split("\n")[0])
-            assert sar == int(ref.port_count[t * 6:t * 6 + 5].sum()), t
-            # utilization operands: flits through the router's ports = its buffer writes
-            bw = int(txt.split("Buffer Writes: ")[1].split("\n")[0])
-            assert bw == int(ref.port_flit[t * 6:t * 6 + 5].sum()), t
+            # one port per unicast visit: requests = switch allocations, flits = buffer writes
+            if not np.any(tr.flags & gnoc.PKT_BROADCAST):
+                sar = int(txt.split("Switch Allocator Requests: ")[1].split("\n")[0])
+                assert sar == int(ref.port_count[t * 6:t * 6 + 5].sum()), t
+                bw = int(txt.split("Buffer Writes: ")[1].split("\n")[0])
+                assert bw == int(ref.port_flit[t * 6:t * 6 + 5].sum()), t
+            # utilization operands: flits over the router's links (a broadcast visit uses several)
+            lt = int(txt.split("Link Traversals: ")[1].split("\n")[0])
+            assert lt == int(ref.port_flit[t * 6:t * 6 + 5].sum()), t
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["sat8", "flit16", "nocont"])
+@pytest.mark.parametrize("name", ["sat8", "flit16", "nocont", "bcast"])
 def test_replay_summary_matches_reference_text(tmp_path, name):
     cfg, tr = next((c, t) for n, c, t in cases() if n == name)
     ref = oracle.run(cfg, tr)
