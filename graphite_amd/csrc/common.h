@@ -77,9 +77,11 @@ struct DevCfg
    const uint32_t* pt_fw;   // per point flit width
    // Broadcast tree (emesh_hop_by_hop.cc:163-221), nullptr without broadcasts.
    // A router visit v = b * N + tile of broadcast b charges the MAX queue delay
-   // over its selected ports (router_model.cc:86-101): a pass reads the maxima
-   // of the previous pass (bc_mprev) and records its own (bc_mcur); passes
-   // repeat until they agree (engine.hip gnoc_run).
+   // over its selected ports (router_model.cc:86-101), i.e. its children leave
+   // at the latest departure max(Xb, tc) of those ports, Xb = a queue's
+   // busy-until time ahead of the request: a pass records max Xb per visit in
+   // bc_mcur (atomicMax) and reads max(bc_mcur so far, bc_mprev of the previous
+   // pass); passes repeat until two agree (engine.hip gnoc_run).
    const uint32_t* bc_idx;  // packet id -> broadcast index
    const uint64_t* bc_mprev;
    uint64_t* bc_mcur;

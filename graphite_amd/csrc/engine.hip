@@ -119,7 +119,7 @@ struct gnoc_engine
    uint32_t nb = 0;
    uint32_t bc_passes = 0;
    std::vector<uint32_t> h_bid;
-   DevBuf d_bidx, d_bid, d_bm0, d_bm1, d_bfin, d_bzl, d_bct, d_bflag;
+   DevBuf d_bidx, d_bid, d_bm0, d_bm1, d_bfin, d_bzl, d_bct, d_bflag, d_bcnt, d_btail;
 
    // design-space sweep (gnoc_create_sweep): per-point tables
    int32_t npoints = 1;
@@ -757,24 +757,34 @@ static int run_levels_v1(gnoc_engine* e)
       GNOC_HIP(e, hipMemcpyAsync(e->plan_ports.p, ports.data(), ports.size() * 4, hipMemcpyHostToDevice, s));
    GNOC_HIP(e, e->dirty.ensure((size_t) nslots * 4));
    GNOC_HIP(e, hipMemsetAsync(e->dirty.p, 0, (size_t) nslots * 4, s));
+   if (e->nb)
+   {
+      GNOC_HIP(e, e->d_btail.ensure((size_t) nslots * 4));
+      GNOC_HIP(e, hipMemsetAsync(e->d_btail.p, 0, (size_t) nslots * 4, s));
+   }
    e->h_levels = (uint32_t) (off.size() - 1);
    for (size_t l = 0; l + 1 < off.size(); l++)
    {
       const uint32_t cnt = off[l + 1] - off[l];
       if (!cnt) continue;
       const uint32_t* pp = e->plan_ports.as<uint32_t>() + off[l];
-      if (e->f1)
-         GNOC_LAUNCH(e, KC_PORT, k_port_stream<true>, dim3(cnt), dim3(STHREADS), 0, s, c, pp, e->slot_cnt.as<uint32_t>(),
-                     e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
-                     e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
-                     e->port_flit.as<uint64_t>(), e->port_last.as<uint64_t>(), e->dirty.as<uint32_t>(),
-                     e->counters.as<unsigned int>() + 8);
+#define GNOC_PORT(F1V, BCV)                                                                                         \
+   GNOC_LAUNCH(e, KC_PORT, (k_port_stream<F1V, BCV>), dim3(cnt), dim3(STHREADS), 0, s, c, pp, e->slot_cnt.as<uint32_t>(), \
+               e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(), e->port_sum.as<uint64_t>(),   \
+               e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(), e->port_flit.as<uint64_t>(),                     \
+               e->port_last.as<uint64_t>(), e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8,                \
+               (const uint32_t*) e->d_bcnt.as<uint32_t>(), e->d_btail.as<uint32_t>())
+      if (e->nb)
+      {
+         if (e->f1) GNOC_PORT(true, true);
+         else GNOC_PORT(false, true);
+      }
       else
-         GNOC_LAUNCH(e, KC_PORT, k_port_stream<false>, dim3(cnt), dim3(STHREADS), 0, s, c, pp, e->slot_cnt.as<uint32_t>(),
-                     e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),
-                     e->port_sum.as<uint64_t>(), e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(),
-                     e->port_flit.as<uint64_t>(), e->port_last.as<uint64_t>(), e->dirty.as<uint32_t>(),
-                     e->counters.as<unsigned int>() + 8);
+      {
+         if (e->f1) GNOC_PORT(true, false);
+         else GNOC_PORT(false, false);
+      }
+#undef GNOC_PORT
    }
    return GNOC_OK;
 }
@@ -1019,8 +1029,13 @@ static int run_prep(gnoc_engine* e, bool* done)
       GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts, dim3((N * 5 + 255) / 256), dim3(256), 0, s, c, e->Hs.as<uint32_t>(),
                   e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>());
    if (e->nb)
+   {
+      GNOC_HIP(e, e->d_bcnt.ensure((size_t) nslots * 4));
+      GNOC_HIP(e, hipMemsetAsync(e->d_bcnt.p, 0, (size_t) nslots * 4, s));
       GNOC_LAUNCH(e, KC_BCAST, k_bcast_slots, dim3((uint32_t) (((uint64_t) e->nb * N + 255) / 256)), dim3(256), 0, s, c,
-                  e->nb, e->d_bid.as<uint32_t>(), e->d_src, e->routed.as<uint8_t>(), e->slot_cnt.as<uint32_t>());
+                  e->nb, e->d_bid.as<uint32_t>(), e->d_src, e->routed.as<uint8_t>(), e->slot_cnt.as<uint32_t>(),
+                  e->d_bcnt.as<uint32_t>());
+   }
    if (N * 25 <= 4 * SCAN_SPAN)
       GNOC_LAUNCH(e, KC_SCAN, k_scan_slots, dim3(1), dim3(1024), 0, s, N, e->slot_cnt.as<uint32_t>(),
                   e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>(), e->gtot.as<uint64_t>() + 1);

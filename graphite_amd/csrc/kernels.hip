@@ -25,9 +25,10 @@ namespace gnoc {
 // slot (or write the packet's final time at SELF).
 // ----------------------------------------------------------------------------
 constexpr int ST = 256;          // records per input per round
-constexpr int SMAXIN = INS;      // input streams per port: 4 for unicast, 5 at a broadcast sender's SELF
-constexpr int SMAXE = ST * SMAXIN;
 constexpr int STHREADS = 256;
+// Broadcast batches (BC): a port's broadcast records (the tails of its input
+// slots, written in any order) are sorted in LDS and merged as one more stream.
+constexpr int BC_CAP = 4096;
 
 struct SerialState
 {
@@ -39,20 +40,29 @@ struct SerialState
    uint64_t mg1;
 };
 
+// NS input streams: the <= 4 non-empty input slots of a unicast port, or the 5
+// slots' unicast parts plus the broadcast stream.
+template <int NS>
 struct PortSmem
 {
-   uint64_t in_t[SMAXIN][ST];
-   uint32_t in_id[SMAXIN][ST];
-   uint32_t in_aux[SMAXIN][ST];
-   uint64_t m_t[SMAXE];
-   uint32_t m_id[SMAXE];
-   uint32_t m_aux[SMAXE];
-   uint64_t m_c[SMAXE];
+   uint64_t in_t[NS][ST];
+   uint32_t in_id[NS][ST];
+   uint32_t in_aux[NS][ST];
+   uint64_t m_t[NS * ST];
+   uint32_t m_id[NS * ST];
+   uint32_t m_aux[NS * ST];
+   uint64_t m_c[NS * ST];
    uint64_t wA[STHREADS / 64], wB[STHREADS / 64], wC[STHREADS / 64];
-   uint32_t e_cnt[SMAXIN];
+   uint32_t e_cnt[NS];
    uint32_t s0;
-   uint32_t bc_late;   // a broadcast child left later than its FIFO departure
    SerialState ss;
+};
+
+struct BcSmem
+{
+   uint64_t t[BC_CAP];
+   uint32_t i[BC_CAP];
+   uint32_t a[BC_CAP];
 };
 
 __device__ __forceinline__ bool key_le(uint64_t t1, uint32_t i1, uint64_t t2, uint32_t i2)
@@ -122,6 +132,34 @@ struct FixSmem
    uint32_t ka[FIX_LDS];
 };
 
+// Block-wide bitonic sort by (t, id) of P (a power of two) LDS entries.
+__device__ void bitonic_lds(uint64_t* kt, uint32_t* ki, uint32_t* ka, uint32_t P)
+{
+   const uint32_t tid = threadIdx.x;
+   for (uint32_t k = 2; k <= P; k <<= 1)
+   {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1)
+      {
+         for (uint32_t i = tid; i < P; i += blockDim.x)
+         {
+            const uint32_t l = i ^ j;
+            if (l > i)
+            {
+               const bool up = (i & k) == 0;
+               const bool gt = key_lt(kt[l], ki[l], kt[i], ki[i]);
+               if (gt == up)
+               {
+                  uint64_t tt = kt[i]; kt[i] = kt[l]; kt[l] = tt;
+                  uint32_t ti = ki[i]; ki[i] = ki[l]; ki[l] = ti;
+                  uint32_t ta = ka[i]; ka[i] = ka[l]; ka[l] = ta;
+               }
+            }
+         }
+         __syncthreads();
+      }
+   }
+}
+
 __device__ void fixup_slot(FixSmem& fx, Rec* __restrict__ r, uint32_t n)
 {
    const uint32_t tid = threadIdx.x;
@@ -136,28 +174,7 @@ __device__ void fixup_slot(FixSmem& fx, Rec* __restrict__ r, uint32_t n)
          else { fx.kt[i] = ~0ull; fx.ki[i] = ~0u; fx.ka[i] = 0; }
       }
       __syncthreads();
-      for (uint32_t k = 2; k <= P; k <<= 1)
-      {
-         for (uint32_t j = k >> 1; j > 0; j >>= 1)
-         {
-            for (uint32_t i = tid; i < P; i += blockDim.x)
-            {
-               const uint32_t l = i ^ j;
-               if (l > i)
-               {
-                  const bool up = (i & k) == 0;
-                  const bool gt = key_lt(fx.kt[l], fx.ki[l], fx.kt[i], fx.ki[i]);
-                  if (gt == up)
-                  {
-                     uint64_t tt = fx.kt[i]; fx.kt[i] = fx.kt[l]; fx.kt[l] = tt;
-                     uint32_t ti = fx.ki[i]; fx.ki[i] = fx.ki[l]; fx.ki[l] = ti;
-                     uint32_t ta = fx.ka[i]; fx.ka[i] = fx.ka[l]; fx.ka[l] = ta;
-                  }
-               }
-            }
-            __syncthreads();
-         }
-      }
+      bitonic_lds(fx.kt, fx.ki, fx.ka, P);
       for (uint32_t i = tid; i < n; i += blockDim.x)
       {
          Rec o;
@@ -181,7 +198,12 @@ __device__ void fixup_slot(FixSmem& fx, Rec* __restrict__ r, uint32_t n)
    __syncthreads();
 }
 
-template <bool F1>
+// BC (batches with broadcasts): each input slot is [unicast part | broadcast
+// tail]; the tail holds slot_cnt - bcnt.. slot_cnt, filled through btail in
+// any order.  Broadcast children are charged the max departure over their
+// router visit's ports (router_model.cc:86-101): this pass's value so far
+// (bc_mcur, atomicMax) or the previous pass's (bc_mprev), whichever is later.
+template <bool F1, bool BC>
 __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32_t* __restrict__ ports,
                                                           const uint32_t* __restrict__ slot_cnt,
                                                           const uint64_t* __restrict__ slot_base,
@@ -189,14 +211,21 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
                                                           uint64_t* __restrict__ port_sum, uint64_t* __restrict__ port_cnt,
                                                           uint64_t* __restrict__ port_mg1, uint64_t* __restrict__ port_flit,
                                                           uint64_t* __restrict__ port_last, uint32_t* __restrict__ dirty,
-                                                          unsigned int* __restrict__ errflag)
+                                                          unsigned int* __restrict__ errflag,
+                                                          const uint32_t* __restrict__ bcnt, uint32_t* __restrict__ btail)
 {
-   __shared__ __attribute__((aligned(16))) char smraw[sizeof(PortSmem) > sizeof(FixSmem) ? sizeof(PortSmem) : sizeof(FixSmem)];
-   PortSmem& sm = *reinterpret_cast<PortSmem*>(smraw);
+   constexpr int SMAXIN = BC ? INS + 1 : 4;   // unicast ports have <= 4 non-empty input sides
+   constexpr int SMAXE = ST * SMAXIN;
+   using Smem = PortSmem<SMAXIN>;
+   __shared__ __attribute__((aligned(16))) char smraw[sizeof(Smem) > sizeof(FixSmem) ? sizeof(Smem) : sizeof(FixSmem)];
+   __shared__ __attribute__((aligned(16))) char bcraw[BC ? sizeof(BcSmem) : 16];
+   Smem& sm = *reinterpret_cast<Smem*>(smraw);
    FixSmem& fx = *reinterpret_cast<FixSmem*>(smraw);
+   BcSmem& bs = *reinterpret_cast<BcSmem*>(bcraw);
    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
    const uint32_t port = ports[blockIdx.x];
    const uint32_t tile = port / PORTS, dir = port % PORTS;
+   auto tail_of = [&](uint32_t sl) -> uint32_t { return BC ? bcnt[sl] : 0u; };
 
    // restore order of input slots a producer flagged (M/G/1 or f != 1 ties)
    for (uint32_t in = 0; in < INS; in++)
@@ -204,11 +233,46 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
       const uint32_t sl = slot_of(tile, dir, in);
       if (dirty[sl])
       {
-         fixup_slot(fx, recs + slot_base[sl], slot_cnt[sl]);
+         fixup_slot(fx, recs + slot_base[sl], slot_cnt[sl] - tail_of(sl));
          if (tid == 0) dirty[sl] = 0;
       }
    }
    __syncthreads();
+
+   // broadcast tails: sorted in LDS as one stream, or (more than BC_CAP) sorted
+   // into their slots, which are then streamed whole
+   uint32_t ntail = 0;
+   bool tails_lds = false;
+   if constexpr (BC)
+   {
+      for (uint32_t in = 0; in < INS; in++) ntail += bcnt[slot_of(tile, dir, in)];
+      tails_lds = ntail <= (uint32_t) BC_CAP;
+      if (ntail && tails_lds)
+      {
+         uint32_t P = 1;
+         while (P < ntail) P <<= 1;
+         uint32_t o = 0;
+         for (uint32_t in = 0; in < INS; in++)
+         {
+            const uint32_t sl = slot_of(tile, dir, in), k = bcnt[sl];
+            const Rec* r = recs + slot_base[sl] + (slot_cnt[sl] - k);
+            for (uint32_t i = tid; i < k; i += STHREADS) { bs.t[o + i] = r[i].t; bs.i[o + i] = r[i].id; bs.a[o + i] = r[i].aux; }
+            o += k;
+         }
+         for (uint32_t i = ntail + tid; i < P; i += STHREADS) { bs.t[i] = ~0ull; bs.i[i] = ~0u; bs.a[i] = 0; }
+         __syncthreads();
+         bitonic_lds(bs.t, bs.i, bs.a, P);
+      }
+      else if (ntail)
+      {
+         for (uint32_t in = 0; in < INS; in++)
+         {
+            const uint32_t sl = slot_of(tile, dir, in);
+            if (bcnt[sl]) fixup_slot(fx, recs + slot_base[sl], slot_cnt[sl]);
+         }
+      }
+      __syncthreads();
+   }
 
    // input streams (non-empty slots of this port), block-uniform
    uint64_t ib[SMAXIN];
@@ -217,10 +281,12 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
    for (uint32_t in = 0; in < INS; in++)
    {
       const uint32_t sl = slot_of(tile, dir, in);
-      const uint32_t k = slot_cnt[sl];
-      if (k && nin < SMAXIN) { ib[nin] = slot_base[sl]; icnt[nin] = k; nin++; }
+      const uint32_t k = slot_cnt[sl] - (tails_lds ? tail_of(sl) : 0u);
+      if (k && nin < (uint32_t) SMAXIN) { ib[nin] = slot_base[sl]; icnt[nin] = k; nin++; }
    }
-   for (uint32_t k = nin; k < SMAXIN; k++) { ib[k] = 0; icnt[k] = 0; }
+   const int lds_stream = (BC && tails_lds && ntail) ? (int) nin : -1;
+   if (lds_stream >= 0) { ib[nin] = 0; icnt[nin] = ntail; nin++; }
+   for (uint32_t k = nin; k < (uint32_t) SMAXIN; k++) { ib[k] = 0; icnt[k] = 0; }
 
    // output: next tile and input side (same for every record of this port)
    uint32_t tx, ty;
@@ -233,11 +299,13 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
    uint32_t nx, ny;
    tile_xy(ntile, c.W, c.magicW, nx, ny);
    uint64_t obase[5];
-   uint32_t ocap[5];
+   uint32_t ocap[5], obc[5];   // unicast capacity, broadcast tail of each next slot
    for (uint32_t d = 0; d < 5; d++)
    {
-      obase[d] = slot_base[slot_of(ntile, d, nin_side)];
-      ocap[d] = slot_cnt[slot_of(ntile, d, nin_side)];
+      const uint32_t sl = slot_of(ntile, d, nin_side);
+      obase[d] = slot_base[sl];
+      obc[d] = tail_of(sl);
+      ocap[d] = slot_cnt[sl] - obc[d];
    }
    uint32_t ocur[5] = { 0, 0, 0, 0, 0 };   // records written per next-direction
 
@@ -250,15 +318,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
    {
       sm.ss.X = 0; sm.ss.g = 0; sm.ss.mode = 0; sm.ss.s1 = 0; sm.ss.s2 = 0;
       sm.ss.narr = 0; sm.ss.newest = 0; sm.ss.mg1 = 0;
-      sm.bc_late = 0;
    }
-   // Next ports of a record at the next router: the XY step, or a broadcast's
-   // tree ports there (bc_mask); none at SELF (the packet is received).
-   auto next_mask = [&](uint32_t ax) -> uint32_t {
-      if (dir == P_SELF) return 0u;
-      if (ax & AUX_BC) return bc_mask(aux_dx(ax), aux_dy(ax), nx, ny, c.W, c.H);
-      return 1u << xy_dir(nx, ny, aux_dx(ax), aux_dy(ax));
-   };
 
    for (;;)
    {
@@ -278,10 +338,19 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
          const uint32_t k = j / ST, i = j % ST;
          if (i < nl[k])
          {
-            const Rec r = recs[ib[k] + cur[k] + i];
-            sm.in_t[k][i] = r.t;
-            sm.in_id[k][i] = r.id;
-            sm.in_aux[k][i] = r.aux;
+            if (BC && (int) k == lds_stream)
+            {
+               sm.in_t[k][i] = bs.t[cur[k] + i];
+               sm.in_id[k][i] = bs.i[cur[k] + i];
+               sm.in_aux[k][i] = bs.a[cur[k] + i];
+            }
+            else
+            {
+               const Rec r = recs[ib[k] + cur[k] + i];
+               sm.in_t[k][i] = r.t;
+               sm.in_id[k][i] = r.id;
+               sm.in_aux[k][i] = r.aux;
+            }
          }
       }
       __syncthreads();
@@ -445,11 +514,15 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
       {
          const uint32_t per = (E + STHREADS - 1) / STHREADS;
          const uint32_t lo = min(tid * per, E), hi = min((tid + 1) * per, E);
-         uint64_t packed = 0;   // 5 x 12-bit counters
+         uint64_t packed = 0;   // 5 x 12-bit counters (unicast children; broadcast ones go to tails)
          for (uint32_t e = lo; e < hi; e++)
          {
-            const uint32_t m = next_mask(sm.m_aux[e]);
-            for (uint32_t d = 0; d < 5; d++) packed += (uint64_t) ((m >> d) & 1u) << (12 * d);
+            uint32_t ndir = 0;
+            if (dir != P_SELF)
+            {
+               ndir = xy_dir(nx, ny, aux_dx(sm.m_aux[e]), aux_dy(sm.m_aux[e]));
+            }
+            if (!(BC && (sm.m_aux[e] & AUX_BC))) packed += 1ull << (12 * ndir);
          }
          uint64_t inc = packed;
          for (int off = 1; off < 64; off <<= 1)
@@ -469,16 +542,24 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
             const uint32_t id = sm.m_id[e], ax = sm.m_aux[e];
             const uint64_t cc = sm.m_c[e];
             // the delay charged: this queue's, or for a broadcast's router visit the
-            // max over the visit's ports (router_model.cc:86-101; previous pass)
+            // max over the visit's ports.  A port's departure is max(Xb, tc) with Xb
+            // the queue's busy-until time ahead of the request (tc + cc when it
+            // waited, 0 when idle), so the visit keeps max Xb over its ports: a
+            // pass that moves the visit's arrival tc reuses the other ports' Xb of
+            // the previous pass, exact unless their queues ahead of it changed.
             uint64_t ch = cc;
-            uint64_t* bfin = nullptr;
-            if ((ax & AUX_BC) && dir != P_INJ)
+            const bool bcr = BC && (ax & AUX_BC);
+            uint64_t v = 0;
+            if (bcr && dir != P_INJ)
             {
-               const uint64_t v = (uint64_t) c.bc_idx[id] * c.N + tile;
-               atomicMax((unsigned long long*) (c.bc_mcur + v), (unsigned long long) cc);
+               v = (uint64_t) c.bc_idx[id] * c.N + tile;
+               const uint64_t tc = cyc_of<F1>(t, c.f), xb = cc ? tc + cc : 0ull;
+               const uint64_t old = atomicMax((unsigned long long*) (c.bc_mcur + v), (unsigned long long) xb);
                const uint64_t mp = c.bc_mprev[v];
-               if (mp > cc) { ch = mp; sm.bc_late = 1; }
-               bfin = c.bc_fin + v;
+               uint64_t u = tc + cc;
+               u = u > old ? u : old;
+               u = u > mp ? u : mp;
+               ch = u - tc;
             }
             st_sum += ch;
             st_cnt++;
@@ -492,27 +573,37 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
             if (dir == P_SELF)
             {
                const uint64_t fin = tn + ps_of<F1>(aux_F(ax), c.f);
-               if (bfin) *bfin = fin;
+               if (bcr) c.bc_fin[v] = fin;
                else final_ps[id] = fin;
                continue;
             }
-            const uint32_t m = next_mask(ax);
             Rec o;
             o.t = tn;
             o.id = id;
             o.aux = ax;
-            for (uint32_t nd = 0; nd < 5; nd++)
+            if (bcr)
             {
-               if (!((m >> nd) & 1u)) continue;
-               const uint32_t r = (uint32_t) ((pre >> (12 * nd)) & 0xFFF);
-               pre += 1ull << (12 * nd);
-               if (ocur[nd] + r >= ocap[nd])
+               // the tree ports at the next router (bc_mask): one record into the
+               // broadcast tail of each
+               const uint32_t m = bc_mask(aux_dx(ax), aux_dy(ax), nx, ny, c.W, c.H);
+               for (uint32_t nd = 0; nd < 5; nd++)
                {
-                  atomicOr(errflag, 1u);   // route-count invariant broken: never write out of the slot
-                  continue;
+                  if (!((m >> nd) & 1u)) continue;
+                  const uint32_t q = atomicAdd(&btail[slot_of(ntile, nd, nin_side)], 1u);
+                  if (q >= obc[nd]) { atomicOr(errflag, 1u); continue; }
+                  recs[obase[nd] + ocap[nd] + q] = o;
                }
-               recs[obase[nd] + ocur[nd] + r] = o;
+               continue;
             }
+            const uint32_t ndir = xy_dir(nx, ny, aux_dx(ax), aux_dy(ax));
+            const uint32_t r = (uint32_t) ((pre >> (12 * ndir)) & 0xFFF);
+            pre += 1ull << (12 * ndir);
+            if (ocur[ndir] + r >= ocap[ndir])
+            {
+               atomicOr(errflag, 1u);   // route-count invariant broken: never write out of the slot
+               continue;
+            }
+            recs[obase[ndir] + ocur[ndir] + r] = o;
          }
          for (uint32_t d = 0; d < 5; d++) ocur[d] += (uint32_t) ((tot >> (12 * d)) & 0xFFF);
       }
@@ -550,10 +641,9 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
       port_sum[port] = a;
       port_cnt[port] = b;
       port_mg1[port] = sm.ss.mg1;
-      // Outputs can leave FIFO order only through M/G/1 requests, broadcast
-      // children charged a sibling port's larger delay or, for f != 1,
-      // equal-time pairs; mark this port's output slots for the fixup sort.
-      if (dir != P_SELF && (sm.ss.mg1 > 0 || sm.bc_late || !F1))
+      // Unicast outputs can leave FIFO order only through M/G/1 requests or, for
+      // f != 1, equal-time pairs; mark this port's output slots for the fixup sort.
+      if (dir != P_SELF && (sm.ss.mg1 > 0 || !F1))
          for (uint32_t d = 0; d < 5; d++) dirty[slot_of(ntile, d, nin_side)] = 1;
    }
 }
@@ -673,10 +763,15 @@ __global__ __launch_bounds__(256) void k_mask_unowned(uint64_t n, const uint32_t
 }
 
 // explicit instantiations
-template __global__ void k_port_stream<true>(DevCfg, const uint32_t*, const uint32_t*, const uint64_t*, Rec*, uint64_t*,
-                                             uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
-template __global__ void k_port_stream<false>(DevCfg, const uint32_t*, const uint32_t*, const uint64_t*, Rec*, uint64_t*,
-                                              uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint32_t*, unsigned int*);
+#define GNOC_PORT_STREAM_INST(F1V, BCV)                                                                              \
+   template __global__ void k_port_stream<F1V, BCV>(DevCfg, const uint32_t*, const uint32_t*, const uint64_t*, Rec*, \
+                                                    uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, \
+                                                    uint32_t*, unsigned int*, const uint32_t*, uint32_t*);
+GNOC_PORT_STREAM_INST(true, false)
+GNOC_PORT_STREAM_INST(false, false)
+GNOC_PORT_STREAM_INST(true, true)
+GNOC_PORT_STREAM_INST(false, true)
+#undef GNOC_PORT_STREAM_INST
 template __global__ void k_bcast_final<true>(DevCfg, const uint32_t*, const uint64_t*, const uint32_t*, const uint32_t*,
                                              const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*,
                                              uint64_t*, int);

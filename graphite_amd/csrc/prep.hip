@@ -530,7 +530,8 @@ __global__ __launch_bounds__(256) void k_slot_counts_y(DevCfg c, const uint32_t*
 // side bc_in_side, and requests the ports of bc_mask there.
 __global__ __launch_bounds__(256) void k_bcast_slots(DevCfg c, uint32_t nb, const uint32_t* __restrict__ bid,
                                                      const uint32_t* __restrict__ src,
-                                                     const uint8_t* __restrict__ routed, uint32_t* __restrict__ slot_cnt)
+                                                     const uint8_t* __restrict__ routed, uint32_t* __restrict__ slot_cnt,
+                                                     uint32_t* __restrict__ bcnt)
 {
    const uint64_t k = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
    if (k >= (uint64_t) nb * c.N) return;
@@ -542,7 +543,11 @@ __global__ __launch_bounds__(256) void k_bcast_slots(DevCfg c, uint32_t nb, cons
    tile_xy(tile, c.W, c.magicW, cx, cy);
    const uint32_t m = bc_mask(sx, sy, cx, cy, c.W, c.H), in = bc_in_side(sx, sy, cx, cy);
    for (uint32_t d = 0; d < 5; d++)
-      if ((m >> d) & 1u) atomicAdd(&slot_cnt[slot_of(tile, d, in)], 1u);
+      if ((m >> d) & 1u)
+      {
+         atomicAdd(&slot_cnt[slot_of(tile, d, in)], 1u);
+         atomicAdd(&bcnt[slot_of(tile, d, in)], 1u);   // the slot's broadcast tail (kernels.hip)
+      }
 }
 
 // ---------------------------------------------------------------------------
