@@ -155,6 +155,15 @@ __host__ __device__ __forceinline__ uint32_t bc_in_side(uint32_t sx, uint32_t sy
    return cy > sy ? IN_S : cy < sy ? IN_N : cx > sx ? IN_W : cx < sx ? IN_E : IN_LOCAL;
 }
 
+// Input slot side of a record entering port d of a router from side `side`.
+// Only a broadcast sender's own SELF request enters SELF from LOCAL (unicast
+// self-sends bypass the mesh); it is kept in the S slot, whose records are
+// merged with the others anyway, so every port has <= 4 input slots.
+__host__ __device__ __forceinline__ uint32_t slot_side(uint32_t d, uint32_t side)
+{
+   return d == P_SELF && side == IN_LOCAL ? IN_S : side;
+}
+
 // Dimension-ordered XY route step, network_model_emesh_hop_by_hop.cc:229-240.
 __host__ __device__ __forceinline__ uint32_t xy_dir(uint32_t cx, uint32_t cy, uint32_t dx, uint32_t dy)
 {

@@ -869,7 +869,7 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
    // release/acquire hand-offs -- exact, but a consumer still waits for whole
    // producer ports and every chunk pays an L2 write-back: 2.8x slower on 32x32.
    const char* xlv = std::getenv("GNOC_XLEVEL");
-   const bool xl = xlv && *xlv == '1' && e->nranks == 1;
+   const bool xl = xlv && *xlv == '1' && e->nranks == 1 && !e->nb;
    uint64_t* stp = stamps ? e->stamps.as<uint64_t>() : nullptr;
 #define GNOC_LEVEL_ARGS(lvl)                                                                                         \
    c, (lvl), e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
@@ -958,6 +958,9 @@ static int run_prep(gnoc_engine* e, bool* done)
    e->evkid.clear();
    GNOC_HIP(e, hipEventRecord(e->ev0, s));
    GNOC_HIP(e, hipMemsetAsync(e->counters.p, 0, 64, s));
+   // broadcast children live in the exception tails of their slots (level.hip
+   // lv_bcast): every level reads the tail counts (errflag word 2)
+   if (e->nb) GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned>() + 8 + 2, 1, 1, s));
    GNOC_HIP(e, hipMemsetAsync(e->slot_cnt.p, 0, (size_t) nslots * 4, s));
    GNOC_HIP(e, hipMemsetAsync(e->nexc.p, 0, (size_t) nslots * 4, s));
    GNOC_HIP(e, hipMemsetAsync(e->port_sum.p, 0, nports * 8, s));
@@ -1123,9 +1126,7 @@ static int run_once(gnoc_engine* e)
    bool done = false;
    int rc = run_prep(e, &done);
    if (rc || done) return rc;
-   // broadcast batches take the whole-port streams: their children leave FIFO
-   // order and fan out to several next ports (kernels.hip k_port_stream)
-   const bool v3 = e->f1 && e->dc.max_list >= 3 && !e->force_v1 && !e->nb;
+   const bool v3 = e->f1 && e->dc.max_list >= 3 && !e->force_v1;
    e->used_v3 = v3;
    if (v3)
    {

@@ -302,7 +302,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
    uint32_t ocap[5], obc[5];   // unicast capacity, broadcast tail of each next slot
    for (uint32_t d = 0; d < 5; d++)
    {
-      const uint32_t sl = slot_of(ntile, d, nin_side);
+      const uint32_t sl = slot_of(ntile, d, slot_side(d, nin_side));
       obase[d] = slot_base[sl];
       obc[d] = tail_of(sl);
       ocap[d] = slot_cnt[sl] - obc[d];
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
                for (uint32_t nd = 0; nd < 5; nd++)
                {
                   if (!((m >> nd) & 1u)) continue;
-                  const uint32_t q = atomicAdd(&btail[slot_of(ntile, nd, nin_side)], 1u);
+                  const uint32_t q = atomicAdd(&btail[slot_of(ntile, nd, slot_side(nd, nin_side))], 1u);
                   if (q >= obc[nd]) { atomicOr(errflag, 1u); continue; }
                   recs[obase[nd] + ocap[nd] + q] = o;
                }
@@ -644,7 +644,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
       // Unicast outputs can leave FIFO order only through M/G/1 requests or, for
       // f != 1, equal-time pairs; mark this port's output slots for the fixup sort.
       if (dir != P_SELF && (sm.ss.mg1 > 0 || !F1))
-         for (uint32_t d = 0; d < 5; d++) dirty[slot_of(ntile, d, nin_side)] = 1;
+         for (uint32_t d = 0; d < 5; d++) dirty[slot_of(ntile, d, slot_side(d, nin_side))] = 1;
    }
 }
 

@@ -598,7 +598,7 @@ __device__ Scan3 lv_scan(LvSmem& sm, const Seg& sg)
       const uint32_t ax = sm.ka[k];
       const uint64_t p = aux_F(ax);
       mp_comp(A, B, p, cyc1(sm.kt[k]) + p);
-      C += 1ull << (12 * next_dir(ax, dir, nx, ny));
+      if (!(ax & AUX_BC)) C += 1ull << (12 * next_dir(ax, dir, nx, ny));   // broadcast children: tails
    }
    uint64_t iA = A, iB = B, iC = C;
    for (int off = 1; off < 64; off <<= 1)
@@ -641,6 +641,46 @@ __device__ Scan3 lv_scan(LvSmem& sm, const Seg& sg)
    return o;
 }
 
+// A broadcast record served with queue delay cc at this port (tc = its arrival
+// cycle): the delay its router visit charges -- the max over the visit's ports,
+// from their busy-until times Xb (this pass so far, or the previous pass; DevCfg
+// bc_*) -- then its receipt (SELF) or one record into the exception tail of
+// each tree port at the next router (bc_mask).  Returns the charged delay.
+__device__ uint64_t lv_bcast(const LvSmem& sm, const DevCfg& c, uint64_t t, uint32_t id, uint32_t ax, uint64_t cc,
+                             uint64_t rl, Rec* __restrict__ recs, uint32_t* __restrict__ nexc,
+                             unsigned* __restrict__ errflag)
+{
+   const uint32_t dir = sm.io.dir;
+   uint64_t ch = cc;
+   uint64_t v = 0;
+   if (dir != P_INJ)
+   {
+      v = (uint64_t) c.bc_idx[id] * c.N + sm.io.port / PORTS;
+      const uint64_t tc = cyc1(t), xb = cc ? tc + cc : 0ull;
+      const uint64_t old = atomicMax((unsigned long long*) (c.bc_mcur + v), (unsigned long long) xb);
+      const uint64_t mp = c.bc_mprev[v];
+      uint64_t u = tc + cc;
+      u = u > old ? u : old;
+      u = u > mp ? u : mp;
+      ch = u - tc;
+   }
+   const uint64_t tn = t + ch * 1000ull + rl;
+   if (dir == P_SELF)
+   {
+      c.bc_fin[v] = tn + 1000ull * aux_F(ax);
+      return ch;
+   }
+   const uint32_t m = bc_mask(aux_dx(ax), aux_dy(ax), sm.io.nx, sm.io.ny, c.W, c.H);
+   for (uint32_t nd = 0; nd < 5; nd++)
+   {
+      if (!((m >> nd) & 1u)) continue;
+      const uint32_t x = atomicAdd(&nexc[sm.io.oslot[nd]], 1u);
+      if (x >= sm.io.ocnt[nd]) { atomicOr(errflag, 1u); continue; }
+      lv_store_rec(recs + sm.io.obase[nd] + sm.io.ocnt[nd] - 1 - x, tn, id, ax);
+   }
+   return ch;
+}
+
 // Serial prefix while the queue has never idled (history tree + M/G/1), one
 // thread, from merged position 0; outputs written directly.  -> sm.s0
 __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, uint64_t* __restrict__ samp_t,
@@ -665,10 +705,15 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
          const uint64_t mg_before = s.mg1;
          const uint64_t cc = serial_step(s, cyc1(t), aux_F(ax), c.max_list, c.analytical);
          if (s.g >= 1) s.mode = 0;
-         ssum += cc;
          sflit += aux_F(ax);
          const uint64_t dep = cyc1(t) + cc + aux_F(ax);
          slast = slast > dep ? slast : dep;
+         if (ax & AUX_BC)
+         {
+            ssum += lv_bcast(sm, c, t, id, ax, cc, rl, recs, nexc, errflag);
+            continue;
+         }
+         ssum += cc;
          const uint64_t tn = t + cc * 1000ull + rl;
          if (dir == P_SELF) { final_ps[id] = tn + 1000ull * aux_F(ax); continue; }
          const uint32_t nd = next_dir(ax, dir, nx, ny);
@@ -707,7 +752,7 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
 // carry advances by the block totals.
 __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3& so, Rec* __restrict__ recs,
                         uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id, uint64_t* __restrict__ final_ps,
-                        unsigned* __restrict__ errflag)
+                        uint32_t* __restrict__ nexc, unsigned* __restrict__ errflag)
 {
    const uint32_t lane = threadIdx.x & 63;
    const uint32_t dir = sm.io.dir, nx = sm.io.nx, ny = sm.io.ny;
@@ -729,6 +774,11 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
          const uint64_t cc = X > tc ? X - tc : 0;
          const uint32_t ax = sm.ka[k];
          X = (X > tc ? X : tc) + aux_F(ax);
+         if (ax & AUX_BC)
+         {
+            ssum += lv_bcast(sm, c, t, id, ax, cc, rl, recs, nexc, errflag);
+            continue;
+         }
          ssum += cc;
          const uint64_t tn = t + cc * 1000ull + rl;
          if (dir == P_SELF)
@@ -781,7 +831,7 @@ __device__ void lv_leaf(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, uin
    Seg sg;
    lv_load_seg(sm, sm.s0, sm.E, sg);
    const Scan3 so = lv_scan(sm, sg);
-   lv_emit(sm, c, sg, so, recs, samp_t, samp_id, final_ps, errflag);
+   lv_emit(sm, c, sg, so, recs, samp_t, samp_id, final_ps, nexc, errflag);
 }
 
 // ---------------------------------------------------------------------------
@@ -1300,7 +1350,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
                   lv_publish_inc(st, g, inc);
                   sm.published = 1;
                }
-               lv_emit(sm, c, sg, so, recs, samp_t, samp_id, final_ps, errflag);
+               lv_emit(sm, c, sg, so, recs, samp_t, samp_id, final_ps, nexc, errflag);
             }
             else
             {
@@ -1498,7 +1548,9 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
          else if (in == IN_E) pp = (tile + 1) * PORTS + P_LEFT;
          else if (in == IN_S) pp = (tile - c.W) * PORTS + P_UP;
          else if (in == IN_N) pp = (tile + c.W) * PORTS + P_DOWN;
-         io.prod[io.nin] = pp == LV_NO_PROD ? LV_NO_PROD : port_k[pp];
+         // (a broadcast sender's own SELF record sits in the S slot of a row-0 tile:
+         // no neighbour below, and the INJ port produced it -- XL is off for broadcasts)
+         io.prod[io.nin] = (pp == LV_NO_PROD || pp >= c.N * PORTS) ? LV_NO_PROD : port_k[pp];
          io.prod_nc[io.nin] = 0;   // k_plan_expand: the producer's chunk count
          if (n > best) { best = n; io.sb = io.nin; }
          io.nin++;
@@ -1514,7 +1566,7 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
    io.ny = ntile / c.W;
    for (uint32_t d = 0; d < 5; d++)
    {
-      const uint32_t os = slot_of(ntile, d, nside);
+      const uint32_t os = slot_of(ntile, d, slot_side(d, nside));
       io.oslot[d] = os;
       io.obase[d] = dir == P_SELF ? 0 : slot_base[os];
       io.ocnt[d] = dir == P_SELF ? 0 : slot_cnt[os];

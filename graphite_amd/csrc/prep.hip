@@ -545,8 +545,9 @@ __global__ __launch_bounds__(256) void k_bcast_slots(DevCfg c, uint32_t nb, cons
    for (uint32_t d = 0; d < 5; d++)
       if ((m >> d) & 1u)
       {
-         atomicAdd(&slot_cnt[slot_of(tile, d, in)], 1u);
-         atomicAdd(&bcnt[slot_of(tile, d, in)], 1u);   // the slot's broadcast tail (kernels.hip)
+         const uint32_t sl = slot_of(tile, d, slot_side(d, in));
+         atomicAdd(&slot_cnt[sl], 1u);
+         atomicAdd(&bcnt[sl], 1u);   // the slot's broadcast tail (kernels.hip, level.hip)
       }
 }
 

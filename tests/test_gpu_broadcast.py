@@ -106,3 +106,16 @@ def test_broadcast_refused_on_sweep():
     with pytest.raises(gnoc.GnocError):
         sw = gnoc.SweepEngine(gnoc.EngineConfig(num_tiles=16), pts)
         sw.submit([tr, tr])
+
+
+@pytest.mark.parametrize("env", [{"GNOC_ENGINE": "v1"}, {"GNOC_CHUNK": "96"}, {"GNOC_CHUNK": "400"}])
+def test_engine_paths_agree(monkeypatch, env):
+    """The whole-port path (v1) and the chunked path with small chunks (broadcast
+    tails spread over many chunk key ranges and leaves) give the same bits."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cfg = gnoc.EngineConfig(num_tiles=36, mesh_width=6, mesh_height=6)
+    tr = random_trace(4000, 6, 6, seed=44, max_cycle=2500, burst0=60, bcast_frac=0.02)
+    got, ref, _ = run_both(cfg, tr)
+    assert_bcast_same(got, ref, tr)
+    assert got.summary["engine_path"] == (0 if "GNOC_ENGINE" in env else 1)
