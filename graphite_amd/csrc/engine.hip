@@ -360,7 +360,7 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    if (he == hipSuccess)
    {
       int per_cu = 0, cus = 0;
-      he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_level<false, true>, LV_T, 0);
+      he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_level<false, true, false>, LV_T, 0);
       if (he == hipSuccess) he = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
       e->level_grid = std::max(1, per_cu) * std::max(1, cus);
    }
@@ -880,15 +880,21 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
       e->done.as<uint32_t>(), stp
    if (xl && l0 == 0)
    {
-      if (stamps) GNOC_LAUNCH(e, KC_LEVEL, (k_level<true, true>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(L));
-      else GNOC_LAUNCH(e, KC_LEVEL, (k_level<false, true>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(L));
+      if (stamps) GNOC_LAUNCH(e, KC_LEVEL, (k_level<true, true, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(L));
+      else GNOC_LAUNCH(e, KC_LEVEL, (k_level<false, true, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(L));
    }
    else
    {
       for (uint32_t l = l0; l < l1 && l < L; l++)
       {
-         if (stamps) GNOC_LAUNCH(e, KC_LEVEL, (k_level<true, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
-         else GNOC_LAUNCH(e, KC_LEVEL, (k_level<false, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
+         // broadcast batches take the variant with the broadcast branches (lv_bcast)
+         if (e->nb)
+         {
+            if (stamps) GNOC_LAUNCH(e, KC_LEVEL, (k_level<true, false, true>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
+            else GNOC_LAUNCH(e, KC_LEVEL, (k_level<false, false, true>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
+         }
+         else if (stamps) GNOC_LAUNCH(e, KC_LEVEL, (k_level<true, false, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
+         else GNOC_LAUNCH(e, KC_LEVEL, (k_level<false, false, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
       }
    }
 #undef GNOC_LEVEL_ARGS

@@ -587,6 +587,7 @@ __device__ __forceinline__ void lv_load_seg(const LvSmem& sm, uint32_t s0, uint3
    sg.n = b - a;
 }
 
+template <bool BC>
 __device__ Scan3 lv_scan(LvSmem& sm, const Seg& sg)
 {
    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -598,7 +599,7 @@ __device__ Scan3 lv_scan(LvSmem& sm, const Seg& sg)
       const uint32_t ax = sm.ka[k];
       const uint64_t p = aux_F(ax);
       mp_comp(A, B, p, cyc1(sm.kt[k]) + p);
-      if (!(ax & AUX_BC)) C += 1ull << (12 * next_dir(ax, dir, nx, ny));   // broadcast children: tails
+      if (!BC || !(ax & AUX_BC)) C += 1ull << (12 * next_dir(ax, dir, nx, ny));   // broadcast children: tails
    }
    uint64_t iA = A, iB = B, iC = C;
    for (int off = 1; off < 64; off <<= 1)
@@ -683,6 +684,7 @@ __device__ uint64_t lv_bcast(const LvSmem& sm, const DevCfg& c, uint64_t t, uint
 
 // Serial prefix while the queue has never idled (history tree + M/G/1), one
 // thread, from merged position 0; outputs written directly.  -> sm.s0
+template <bool BC>
 __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, uint64_t* __restrict__ samp_t,
                           uint32_t* __restrict__ samp_id, uint32_t* __restrict__ nexc, uint64_t* __restrict__ final_ps,
                           unsigned* __restrict__ errflag)
@@ -708,7 +710,7 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
          sflit += aux_F(ax);
          const uint64_t dep = cyc1(t) + cc + aux_F(ax);
          slast = slast > dep ? slast : dep;
-         if (ax & AUX_BC)
+         if (BC && (ax & AUX_BC))
          {
             ssum += lv_bcast(sm, c, t, id, ax, cc, rl, recs, nexc, errflag);
             continue;
@@ -750,6 +752,7 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
 
 // Recurrence + stores of this thread's segment from carry sm.cy; then the
 // carry advances by the block totals.
+template <bool BC>
 __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3& so, Rec* __restrict__ recs,
                         uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id, uint64_t* __restrict__ final_ps,
                         uint32_t* __restrict__ nexc, unsigned* __restrict__ errflag)
@@ -770,11 +773,11 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
          const uint32_t k = sm.perm[sg.a + i];
          const uint64_t t = sm.kt[k];
          const uint32_t id = sm.ki[k];
+         const uint32_t ax = sm.ka[k];
          const uint64_t tc = cyc1(t);
          const uint64_t cc = X > tc ? X - tc : 0;
-         const uint32_t ax = sm.ka[k];
          X = (X > tc ? X : tc) + aux_F(ax);
-         if (ax & AUX_BC)
+         if (BC && (ax & AUX_BC))
          {
             ssum += lv_bcast(sm, c, t, id, ax, cc, rl, recs, nexc, errflag);
             continue;
@@ -821,17 +824,18 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
 }
 
 // A whole merged leaf from carry sm.cy (serial prefix if needed).
+template <bool BC>
 __device__ void lv_leaf(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, uint64_t* __restrict__ samp_t,
                         uint32_t* __restrict__ samp_id, uint32_t* __restrict__ nexc, uint64_t* __restrict__ final_ps,
                         unsigned* __restrict__ errflag)
 {
    if (threadIdx.x == 0) sm.s0 = 0;
    lv_bar();
-   if (sm.cy.mode) lv_serial(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);
+   if (sm.cy.mode) lv_serial<BC>(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);
    Seg sg;
    lv_load_seg(sm, sm.s0, sm.E, sg);
-   const Scan3 so = lv_scan(sm, sg);
-   lv_emit(sm, c, sg, so, recs, samp_t, samp_id, final_ps, nexc, errflag);
+   const Scan3 so = lv_scan<BC>(sm, sg);
+   lv_emit<BC>(sm, c, sg, so, recs, samp_t, samp_id, final_ps, nexc, errflag);
 }
 
 // ---------------------------------------------------------------------------
@@ -1199,7 +1203,7 @@ __device__ __noinline__ void lv_fetch(LvSmem& sm, bool first, bool anyexc, uint3
 #define LV_MIN_WAVES 4   // waves per SIMD the register allocation must leave room for
 #endif
 
-template <bool STAMPS, bool XL>
+template <bool STAMPS, bool XL, bool BC>
 __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t level, const uint32_t* __restrict__ lvl_cbase,
                                                 const uint32_t* __restrict__ lvl_qb,
                                                 unsigned* __restrict__ ctr, const PortIO3* __restrict__ cdesc,
@@ -1322,7 +1326,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
             if (tid == 0) sm.s0 = 0;
             Seg sg;
             lv_load_seg(sm, 0, sm.E, sg);
-            const Scan3 so = lv_scan(sm, sg);
+            const Scan3 so = lv_scan<BC>(sm, sg);
             LV_STAMP(5);
             if (j > 0)
             {
@@ -1350,16 +1354,16 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
                   lv_publish_inc(st, g, inc);
                   sm.published = 1;
                }
-               lv_emit(sm, c, sg, so, recs, samp_t, samp_id, final_ps, nexc, errflag);
+               lv_emit<BC>(sm, c, sg, so, recs, samp_t, samp_id, final_ps, nexc, errflag);
             }
             else
             {
-               lv_leaf(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);   // serial prefix continues
+               lv_leaf<BC>(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);   // serial prefix continues
             }
          }
          else
          {
-            lv_leaf(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);
+            lv_leaf<BC>(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);
          }
          LV_STAMP(7);
       }
@@ -1457,7 +1461,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
                   if (tid == 0 && c.analytical && (sm.E == 0 || cyc1(sm.kt[sm.perm[0]]) == 0)) sm.cy.mode = 1;
                   lv_bar();
                }
-               lv_leaf(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);
+               lv_leaf<BC>(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);
             }
          }
       }
