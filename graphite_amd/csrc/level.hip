@@ -1597,7 +1597,10 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
 #define LV_CMIN 384
 #endif
 #ifndef LV_ROUNDS_FIT
-#define LV_ROUNDS_FIT 0   // measured: 32x32 6% slower, 64x64 unchanged (dynamic dequeue already fills the tail)
+#define LV_ROUNDS_FIT 1   // 1: fit levels of at most LV_FIT_MAX grid rounds (at ctgt); 2: every level; 0: off
+#endif
+#ifndef LV_FIT_MAX
+#define LV_FIT_MAX 5      // in halves of a grid round: 5 = levels of up to 2.5 rounds
 #endif
 __global__ __launch_bounds__(1024) void k_plan_guided(const uint32_t* __restrict__ lvl_off, uint32_t* __restrict__ pnc,
                                                       uint32_t ctgt, uint64_t grid)
@@ -1628,7 +1631,11 @@ __global__ __launch_bounds__(1024) void k_plan_guided(const uint32_t* __restrict
    {
       const uint64_t R = part[0], P = pcnt[0];
       uint32_t c = ctgt;
-      if (LV_ROUNDS_FIT && R > 0)
+      // Fitting every level costs 32x32 (2-3 rounds per level) 7%; levels of about
+      // one round (a mesh sharded over 4-8 ranks) gain 7-14%: a second round of a
+      // few chunks costs a whole chunk latency.
+      const uint64_t nat = R / ctgt + P;   // chunks at the target size (about)
+      if (LV_ROUNDS_FIT && R > 0 && (LV_ROUNDS_FIT > 1 || 2 * nat <= (uint64_t) LV_FIT_MAX * grid))
       {
          uint64_t rounds = (R + ctgt * grid / 2) / (ctgt * grid);
          if (rounds < 1) rounds = 1;
