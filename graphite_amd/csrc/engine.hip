@@ -1005,12 +1005,21 @@ static int run_prep(gnoc_engine* e, bool* done)
    if (n && N <= SC4_MAXN)
    {
       const int nw = scatter_waves(N);
-#define GNOC_SCATTER(NWV)                                                                                                 \
-   GNOC_LAUNCH(e, KC_SCATTER, k_scatter4<NWV>, dim3(nch), dim3(64 * NWV), (size_t) NWV * N * 4, s, (uint64_t) n, pch, N, \
-               nbits, e->d_src, e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(),        \
-               e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>())
-      if (nw == 8) GNOC_SCATTER(8);
-      else GNOC_SCATTER(4);
+      // a sharded rank places only its row band's packets (sources s0 .. s0+S-1):
+      // the compacting variant with counters over those sources only
+      const uint32_t s0 = band_prep ? pr0 * W : 0u, S = band_prep ? nR * W : N;
+      int sbits = 0;
+      while ((1u << sbits) < S) sbits++;
+#define GNOC_SCATTER(NWV, SP)                                                                                               \
+   GNOC_LAUNCH(e, KC_SCATTER, (k_scatter4<NWV, SP>), dim3(nch), dim3(64 * NWV), (size_t) NWV * S * 4 + (SP ? NWV * 2048 : 0), \
+               s, (uint64_t) n, pch, N, s0, S, sbits, e->d_src, e->routed.as<uint8_t>(), e->d_inj,                          \
+               e->aux.as<uint32_t>(), e->hist.as<uint32_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(),                  \
+               e->samp_id.as<uint32_t>())
+      if (band_prep && S <= 1024) GNOC_SCATTER(8, true);
+      else if (band_prep && S <= 2048) GNOC_SCATTER(4, true);
+      else if (band_prep) GNOC_SCATTER(2, true);
+      else if (nw == 8) GNOC_SCATTER(8, false);
+      else GNOC_SCATTER(4, false);
 #undef GNOC_SCATTER
    }
    else if (n)

@@ -232,45 +232,108 @@ __global__ __launch_bounds__(64) void k_scatter(uint64_t n, uint32_t pch, uint32
 constexpr uint32_t SC4_MAXN = 4096;
 __host__ __device__ inline int scatter_waves(uint32_t N) { return N <= 2048 ? 8 : 4; }
 
-template <int NW>
-__global__ __launch_bounds__(512) void k_scatter4(uint64_t n, uint32_t pch, uint32_t N, int nbits,
+//
+// SPARSE (a sharded rank: only its row band's sources, ~1/nranks of the trace):
+// each wave compacts the valid packets of 512 at a time into an LDS buffer, in
+// order, and ranks them 64 at a time, so the ballots run per placed packet
+// rather than per trace packet.  The buffer follows the NW * N counters.
+template <int NW, bool SPARSE>
+__global__ __launch_bounds__(512) void k_scatter4(uint64_t n, uint32_t pch, uint32_t N, uint32_t s0, uint32_t S, int nbits,
                                                   const uint32_t* __restrict__ src, const uint8_t* __restrict__ routed,
                                                   const uint64_t* __restrict__ inj, const uint32_t* __restrict__ aux,
                                                   const uint32_t* __restrict__ offs, Rec* __restrict__ recs,
                                                   uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id)
 {
-   extern __shared__ uint32_t h4[];   // [NW][N] per-wave counts -> running ranks
+   extern __shared__ uint32_t h4[];   // [NW][S] per-wave counts of sources s0 .. s0+S-1 -> running ranks
    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-   for (uint32_t k = threadIdx.x; k < NW * N; k += 64 * NW) h4[k] = 0;
+   for (uint32_t k = threadIdx.x; k < NW * S; k += 64 * NW) h4[k] = 0;
    __syncthreads();
    const uint64_t c0 = (uint64_t) blockIdx.x * pch;
    const uint64_t c1 = min(c0 + pch, n);
    const uint64_t q = (c1 - c0 + NW - 1) / NW;
    const uint64_t lo = min(c0 + w * q, c1), hi = min(lo + q, c1);
-   uint32_t* hw = h4 + w * N;
+   uint32_t* hw = h4 + w * S;
+#pragma unroll 8
    for (uint64_t i = lo + lane; i < hi; i += 64)
-      if (routed[i] & 2) atomicAdd(&hw[src[i]], 1u);
+      if (routed[i] & 2) atomicAdd(&hw[src[i] - s0], 1u);
    __syncthreads();
    // exclusive prefix over waves, plus the chunk's offset for the source
-   const uint32_t* orow = offs + (uint64_t) blockIdx.x * N;
-   for (uint32_t s2 = threadIdx.x; s2 < N; s2 += 64 * NW)
+   const uint32_t* orow = offs + (uint64_t) blockIdx.x * N + s0;
+   for (uint32_t s2 = threadIdx.x; s2 < S; s2 += 64 * NW)
    {
       uint32_t run = orow[s2];
       for (uint32_t ww = 0; ww < (uint32_t) NW; ww++)
       {
-         const uint32_t v = h4[ww * N + s2];
-         h4[ww * N + s2] = run;
+         const uint32_t v = h4[ww * S + s2];
+         h4[ww * S + s2] = run;
          run += v;
       }
    }
    __syncthreads();
    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+   if (SPARSE)
+   {
+      uint32_t* buf = h4 + NW * S + w * 512;
+      for (uint64_t k0 = lo; k0 < hi; k0 += 512)
+      {
+         bool v[8];
+#pragma unroll
+         for (int q = 0; q < 8; q++)
+         {
+            const uint64_t i = k0 + (uint64_t) (q * 64) + lane;
+            v[q] = i < hi && (routed[i] & 2) != 0;
+         }
+         uint32_t tot = 0;
+#pragma unroll
+         for (int q = 0; q < 8; q++)
+         {
+            const uint64_t b = __ballot(v[q]);
+            if (v[q]) buf[tot + (uint32_t) __popcll(b & lt)] = (uint32_t) (q * 64) + lane;
+            tot += (uint32_t) __popcll(b);
+         }
+         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+         __builtin_amdgcn_wave_barrier();
+         for (uint32_t q = 0; q < tot; q += 64)
+         {
+            const bool valid = q + lane < tot;
+            uint64_t i = 0;
+            uint32_t sidx = 0;
+            if (valid)
+            {
+               i = k0 + buf[q + lane];
+               sidx = src[i] - s0;
+            }
+            const uint64_t m = match_mask(sidx, valid, nbits);
+            const uint32_t old = valid ? hw[sidx] : 0u;
+            __builtin_amdgcn_wave_barrier();
+            if (valid)
+            {
+               const uint32_t rank = old + (uint32_t) __popcll(m & lt);
+               if ((63 - __clzll(m)) == (int) lane) hw[sidx] = old + (uint32_t) __popcll(m);
+               const uint64_t pos = rank;
+               Rec r;
+               r.t = inj[i];
+               r.id = (uint32_t) i;
+               r.aux = aux[i];
+               recs[pos] = r;
+               if ((pos & 63) == 0)
+               {
+                  samp_t[pos >> 6] = r.t;
+                  samp_id[pos >> 6] = r.id;
+               }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+         }
+      }
+      return;
+   }
    // software pipeline: loads of the next 64 packets issued before placing these
    uint64_t i = lo + lane;
    bool nv = false;
    uint32_t ns = 0, na = 0;
    uint64_t nt = 0;
-   if (i < hi) { nv = (routed[i] & 2) != 0; ns = src[i]; }
+   if (i < hi) { nv = (routed[i] & 2) != 0; ns = src[i] - s0; }
    if (nv) { nt = inj[i]; na = aux[i]; }   // a sharded rank places only its row band's packets
    for (uint64_t k = lo; k < hi; k += 64)
    {
@@ -281,7 +344,7 @@ __global__ __launch_bounds__(512) void k_scatter4(uint64_t n, uint32_t pch, uint
       const uint64_t id = k + lane;
       const uint64_t i2 = k + 64 + lane;
       nv = false;
-      if (i2 < hi) { nv = (routed[i2] & 2) != 0; ns = src[i2]; }
+      if (i2 < hi) { nv = (routed[i2] & 2) != 0; ns = src[i2] - s0; }
       if (nv) { nt = inj[i2]; na = aux[i2]; }
       if (!nv) ns = 0;
       const uint64_t m = match_mask(sidx, valid, nbits);
@@ -584,9 +647,15 @@ __global__ __launch_bounds__(1024) void k_scan_slots(uint32_t N, const uint32_t*
    if (threadIdx.x == 1023) *total = *inj_total + part[1023];
 }
 
-template __global__ void k_scatter4<4>(uint64_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
+template __global__ void k_scatter4<4, false>(uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
                                        const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
-template __global__ void k_scatter4<8>(uint64_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
+template __global__ void k_scatter4<8, false>(uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
+                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
+template __global__ void k_scatter4<4, true>(uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
+                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
+template __global__ void k_scatter4<8, true>(uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
+                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
+template __global__ void k_scatter4<2, true>(uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
                                        const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
 
 // Multi-block variant for large meshes (sweeps): the same slot order, in
