@@ -89,7 +89,7 @@ struct gnoc_engine
    // work
    DevBuf aux, routed, final_ps, zl, cont;
    DevBuf hist, tot, slot_cnt, slot_base, counters, gtot;
-   DevBuf recs, samp_t, samp_id, Hs, Pp, Prow, pcol, nexc, dirty, span;
+   DevBuf recs, samp_t, samp_id, Hs, Pp, Prow, pcol, nexc, dirty, span, srcseg;
    DevBuf pio, pnc, pgb, lvl_cbase, lvl_qb, cdesc, flags, st, lvl_ctr;
    DevBuf port_sum, port_cnt, port_mg1, port_flit, port_last, plan_ports, stamps, done;
    uint64_t h_chunk_bound = 0;
@@ -958,7 +958,7 @@ static int run_prep(gnoc_engine* e, bool* done)
    GNOC_HIP(e, e->port_mg1.ensure(nports * 8));
    GNOC_HIP(e, e->port_flit.ensure(nports * 8));
    GNOC_HIP(e, e->port_last.ensure(nports * 8));
-   if (band_prep) GNOC_HIP(e, e->pcol.ensure((size_t) nC * H * H * 4));
+   if (band_prep) GNOC_HIP(e, e->pcol.ensure((size_t) nC * H * H * 3 * 4));
 
    e->evused = 0;
    e->evkid.clear();
@@ -975,7 +975,7 @@ static int run_prep(gnoc_engine* e, bool* done)
    GNOC_HIP(e, hipMemsetAsync(e->port_flit.p, 0, nports * 8, s));
    GNOC_HIP(e, hipMemsetAsync(e->port_last.p, 0, nports * 8, s));
    if (!pp_lds) GNOC_HIP(e, hipMemsetAsync(e->Pp.p, 0, (size_t) H * G * N * 4, s));
-   if (band_prep) GNOC_HIP(e, hipMemsetAsync(e->pcol.p, 0, (size_t) nC * H * H * 4, s));
+   if (band_prep) GNOC_HIP(e, hipMemsetAsync(e->pcol.p, 0, (size_t) nC * H * H * 3 * 4, s));
 
    // always launched: for an empty batch it writes the all-zero source histogram
    GNOC_LAUNCH(e, KC_CLASSIFY, k_classify, dim3(nch), dim3(256), N * 4, s, c, (uint64_t) n, pch, e->d_inj, e->d_src,
@@ -996,12 +996,20 @@ static int run_prep(gnoc_engine* e, bool* done)
    }
 
    const uint32_t ng = (N + 255) / 256;
-   GNOC_LAUNCH(e, KC_SRC_TOT, k_src_tot, dim3(ng), dim3(256), 0, s, N, nch, e->hist.as<uint32_t>(), e->tot.as<uint32_t>(),
-               pr0 * W, pr1 * W);
+   // per-source sums and prefixes over the chunk axis, in SRC_SEGS segments
+   const uint32_t nseg = std::min<uint32_t>(SRC_SEGS, nch);
+   const uint32_t ngb = (nR * W + 255) / 256;   // this rank's sources [pr0 * W, pr1 * W)
+   GNOC_HIP(e, e->srcseg.ensure((size_t) nseg * N * 4));
+   if (ngb)
+      GNOC_LAUNCH(e, KC_SRC_TOT, k_src_seg, dim3(ngb, nseg), dim3(256), 0, s, N, nch, nseg, e->hist.as<uint32_t>(),
+                  e->srcseg.as<uint32_t>(), pr0 * W, pr1 * W);
+   GNOC_LAUNCH(e, KC_SRC_TOT, k_src_tot, dim3(ng), dim3(256), 0, s, N, nseg, e->srcseg.as<uint32_t>(),
+               e->tot.as<uint32_t>(), pr0 * W, pr1 * W);
    GNOC_LAUNCH(e, KC_INJ_BASE, k_inj_base, dim3(1), dim3(1024), 0, s, N, e->tot.as<uint32_t>(), e->slot_cnt.as<uint32_t>(),
                e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>());
-   GNOC_LAUNCH(e, KC_SRC_OFFS, k_src_offs, dim3(ng), dim3(256), 0, s, N, nch, e->hist.as<uint32_t>(),
-               e->slot_base.as<uint64_t>(), pr0 * W, pr1 * W);
+   if (ngb)
+      GNOC_LAUNCH(e, KC_SRC_OFFS, k_src_offs, dim3(ngb, nseg), dim3(256), 0, s, N, nch, nseg, e->hist.as<uint32_t>(),
+                  e->srcseg.as<uint32_t>(), e->slot_base.as<uint64_t>(), pr0 * W, pr1 * W);
    if (n && N <= SC4_MAXN)
    {
       const int nw = scatter_waves(N);
@@ -1034,13 +1042,13 @@ static int run_prep(gnoc_engine* e, bool* done)
                   e->Pp.as<uint32_t>(), e->Prow.as<uint32_t>());
    if (W <= 64 && H <= 64)
    {
-      GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_x, dim3(nR), dim3(256), (size_t) W * W * 3 * 4, s, c,
+      GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_x, dim3(nR), dim3(256), (size_t) W * W * 4 * 4, s, c,
                   e->Hs.as<uint32_t>(), e->slot_cnt.as<uint32_t>(), pr0);
       if (band_prep)
-         GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_y, dim3(nC), dim3(256), (size_t) H * H * 4, s, c,
+         GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_y, dim3(nC), dim3(256), (size_t) H * H * 2 * 4, s, c,
                      e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>(), e->cx0, (const uint32_t*) e->pcol.as<uint32_t>());
       else
-         GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_y, dim3(W), dim3(256), (size_t) H * H * 4, s, c,
+         GNOC_LAUNCH(e, KC_SLOT_COUNTS, k_slot_counts_y, dim3(W), dim3(256), (size_t) H * H * 2 * 4, s, c,
                      e->Prow.as<uint32_t>(), e->slot_cnt.as<uint32_t>(), 0u, (const uint32_t*) nullptr);
    }
    else

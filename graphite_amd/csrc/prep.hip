@@ -70,11 +70,10 @@ __global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, uint32_t
       if (pcol && dx >= cx0 && dx < cx1)
       {
          // sharded run, destination in this rank's column band: the Y-leg counts
-         // (source row x destination row, per column) and the turn-slot count
-         atomicAdd(&pcol[((dx - cx0) * c.H + sy) * c.H + dy], 1u);
-         const uint32_t dir = dy > sy ? P_UP : dy < sy ? P_DOWN : P_SELF;
+         // per (column, source row, destination row, side the packet turns from);
+         // k_slot_counts_y derives the Y slots and the turn slots from them
          const uint32_t in = sx < dx ? IN_W : sx > dx ? IN_E : IN_LOCAL;
-         atomicAdd(&slot_cnt[slot_of(sy * c.W + dx, dir, in)], 1u);
+         atomicAdd(&pcol[(((dx - cx0) * c.H + sy) * c.H + dy) * 3 + in], 1u);
       }
       nrouted++;
       // a broadcast visits every router once (N switch-allocator requests)
@@ -107,7 +106,24 @@ __global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, uint32_t
 // 2. injection-slot layout
 // ---------------------------------------------------------------------------
 // Sources outside [s0, s1) (another rank's row band) have no injection records here.
-__global__ __launch_bounds__(256) void k_src_tot(uint32_t N, uint32_t nch, const uint32_t* __restrict__ hist,
+// The chunk axis is cut into SRC_SEGS segments (grid y) so a source's sums and
+// prefix run in parallel: seg[g][s] = chunks of segment g, then tot[s] = sum over g.
+constexpr uint32_t SRC_SEGS = 64;
+__device__ __forceinline__ uint32_t seg_ch(uint32_t g, uint32_t nch, uint32_t ns) { return (uint32_t) ((uint64_t) g * nch / ns); }
+
+__global__ __launch_bounds__(256) void k_src_seg(uint32_t N, uint32_t nch, uint32_t ns, const uint32_t* __restrict__ hist,
+                                                 uint32_t* __restrict__ seg, uint32_t s0, uint32_t s1)
+{
+   const uint32_t s = s0 + blockIdx.x * blockDim.x + threadIdx.x, g = blockIdx.y;
+   if (s >= s1) return;
+   uint32_t t = 0;
+   const uint32_t c1 = seg_ch(g + 1, nch, ns);
+#pragma unroll 16
+   for (uint32_t ch = seg_ch(g, nch, ns); ch < c1; ch++) t += hist[(uint64_t) ch * N + s];
+   seg[(uint64_t) g * N + s] = t;
+}
+
+__global__ __launch_bounds__(256) void k_src_tot(uint32_t N, uint32_t ns, const uint32_t* __restrict__ seg,
                                                  uint32_t* __restrict__ tot, uint32_t s0, uint32_t s1)
 {
    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -115,7 +131,7 @@ __global__ __launch_bounds__(256) void k_src_tot(uint32_t N, uint32_t nch, const
    if (s < s0 || s >= s1) { tot[s] = 0; return; }
    uint32_t t = 0;
 #pragma unroll 16
-   for (uint32_t ch = 0; ch < nch; ch++) t += hist[(uint64_t) ch * N + s];
+   for (uint32_t g = 0; g < ns; g++) t += seg[(uint64_t) g * N + s];
    tot[s] = t;
 }
 
@@ -150,14 +166,18 @@ __global__ __launch_bounds__(1024) void k_inj_base(uint32_t N, const uint32_t* _
 }
 
 // hist[ch][s] (counts) -> absolute record offsets of chunk ch's first record of source s.
-__global__ __launch_bounds__(256) void k_src_offs(uint32_t N, uint32_t nch, uint32_t* __restrict__ hist,
+// Grid y = chunk segment g: the running offset starts after segments 0 .. g-1.
+__global__ __launch_bounds__(256) void k_src_offs(uint32_t N, uint32_t nch, uint32_t ns, uint32_t* __restrict__ hist,
+                                                  const uint32_t* __restrict__ seg,
                                                   const uint64_t* __restrict__ slot_base, uint32_t s0, uint32_t s1)
 {
-   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-   if (s >= N || s < s0 || s >= s1) return;
+   const uint32_t s = s0 + blockIdx.x * blockDim.x + threadIdx.x, g = blockIdx.y;
+   if (s >= s1) return;
    uint32_t run = (uint32_t) slot_base[slot_of(s, P_INJ, IN_LOCAL)];   // < 2^32 records (checked at submit)
+   for (uint32_t q = 0; q < g; q++) run += seg[(uint64_t) q * N + s];
+   const uint32_t c1 = seg_ch(g + 1, nch, ns);
 #pragma unroll 16
-   for (uint32_t ch = 0; ch < nch; ch++)
+   for (uint32_t ch = seg_ch(g, nch, ns); ch < c1; ch++)
    {
       const uint64_t k = (uint64_t) ch * N + s;
       const uint32_t v = hist[k];
@@ -505,36 +525,55 @@ __global__ __launch_bounds__(256) void k_slot_counts(DevCfg c, const uint32_t* _
 __global__ __launch_bounds__(256) void k_slot_counts_x(DevCfg c, const uint32_t* __restrict__ Hs,
                                                        uint32_t* __restrict__ slot_cnt, uint32_t ry0)
 {
-   extern __shared__ uint32_t hr[];   // Hs rows of this mesh row: [sx][dx][cl]
+   extern __shared__ uint32_t hr[];   // Hs rows of this mesh row: [sx][dx][cl], then pt[W][W]
    const uint32_t W = c.W, y = ry0 + blockIdx.x;
    const uint32_t nw = W * W * 3;
+   uint32_t* pt = hr + nw;
    for (uint32_t k = threadIdx.x; k < nw; k += blockDim.x) hr[k] = Hs[(uint64_t) y * W * W * 3 + k];
    __syncthreads();
    auto hs = [&](uint32_t sx, uint32_t dx, uint32_t cl) -> uint32_t { return hr[(sx * W + dx) * 3 + cl]; };
+   // 2-D prefix of T(sx, dx) = all classes: pt[(a-1)W + b-1] = sum over sx < a, dx < b
+   if (threadIdx.x < W)
+   {
+      uint32_t run = 0;
+      for (uint32_t dx = 0; dx < W; dx++)
+      {
+         run += hs(threadIdx.x, dx, 0) + hs(threadIdx.x, dx, 1) + hs(threadIdx.x, dx, 2);
+         pt[threadIdx.x * W + dx] = run;
+      }
+   }
+   __syncthreads();
+   if (threadIdx.x < W)
+   {
+      uint32_t run = 0;
+      for (uint32_t sx = 0; sx < W; sx++)
+      {
+         run += pt[sx * W + threadIdx.x];
+         pt[sx * W + threadIdx.x] = run;
+      }
+   }
+   __syncthreads();
+   auto P = [&](uint32_t a, uint32_t b) -> uint32_t { return (a && b) ? pt[(a - 1) * W + (b - 1)] : 0u; };
+   // sum of T over sx in [a0, a1), dx in [b0, b1)
+   auto rect = [&](uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) -> uint32_t {
+      return (a0 >= a1 || b0 >= b1) ? 0u : P(a1, b1) - P(a0, b1) - P(a1, b0) + P(a0, b0);
+   };
    for (uint32_t q = threadIdx.x; q < W * 5; q += blockDim.x)
    {
       const uint32_t x = q / 5, dir = q % 5, tile = y * W + x;
       const uint32_t bx0 = x / c.BW * c.BW, bx1 = bx0 + c.BW;
       uint32_t cl = 0, cw = 0, ce = 0;
-      if (dir == P_RIGHT) { for (uint32_t dx = x + 1; dx < bx1; dx++) cl += hs(x, dx, 0) + hs(x, dx, 1) + hs(x, dx, 2); }
-      else if (dir == P_LEFT) { for (uint32_t dx = bx0; dx < x; dx++) cl += hs(x, dx, 0) + hs(x, dx, 1) + hs(x, dx, 2); }
+      if (dir == P_RIGHT) cl = rect(x, x + 1, x + 1, bx1);
+      else if (dir == P_LEFT) cl = rect(x, x + 1, bx0, x);
       else if (dir == P_UP) cl = hs(x, x, 2);
       else if (dir == P_DOWN) cl = hs(x, x, 0);
-      if (dir == P_RIGHT)
-      {
-         for (uint32_t sx = bx0; sx < x; sx++)
-            for (uint32_t dx = x + 1; dx < bx1; dx++) cw += hs(sx, dx, 0) + hs(sx, dx, 1) + hs(sx, dx, 2);
-      }
+      if (dir == P_RIGHT) cw = rect(bx0, x, x + 1, bx1);
       else if (dir != P_LEFT)
       {
          const uint32_t want = dir == P_UP ? 2u : dir == P_DOWN ? 0u : 1u;
          for (uint32_t sx = bx0; sx < x; sx++) cw += hs(sx, x, want);
       }
-      if (dir == P_LEFT)
-      {
-         for (uint32_t sx = x + 1; sx < bx1; sx++)
-            for (uint32_t dx = bx0; dx < x; dx++) ce += hs(sx, dx, 0) + hs(sx, dx, 1) + hs(sx, dx, 2);
-      }
+      if (dir == P_LEFT) ce = rect(x + 1, bx1, bx0, x);
       else if (dir != P_RIGHT)
       {
          const uint32_t want = dir == P_UP ? 2u : dir == P_DOWN ? 0u : 1u;
@@ -547,38 +586,71 @@ __global__ __launch_bounds__(256) void k_slot_counts_x(DevCfg c, const uint32_t*
 }
 
 // Column x = cx0 + blockIdx.x.  pcol == nullptr: read column x of Prow[sy][dst];
-// else pcol[x - cx0][sy][dy] (sharded runs, counted in k_classify).
+// else pcol[x - cx0][sy][dy][side] (sharded runs, counted in k_classify), which
+// also gives this column's turn slots (tile (x, sy), dir by dy, side IN_LOCAL/W/E).
 __global__ __launch_bounds__(256) void k_slot_counts_y(DevCfg c, const uint32_t* __restrict__ Prow,
                                                        uint32_t* __restrict__ slot_cnt, uint32_t cx0,
                                                        const uint32_t* __restrict__ pcol)
 {
-   extern __shared__ uint32_t pc[];   // column x: [sy][dy]
+   extern __shared__ uint32_t pc[];   // column x: [sy][dy], then its 2-D prefix pt[H][H]
    const uint32_t W = c.W, H = c.H, N = c.N, x = cx0 + blockIdx.x;
    for (uint32_t k = threadIdx.x; k < H * H; k += blockDim.x)
    {
       const uint32_t sy = k / H, dy = k % H;
-      pc[k] = pcol ? pcol[(uint64_t) blockIdx.x * H * H + k] : Prow[(uint64_t) sy * N + dy * W + x];
+      const uint32_t* p3 = pcol ? pcol + ((uint64_t) blockIdx.x * H * H + k) * 3 : nullptr;
+      pc[k] = pcol ? p3[0] + p3[1] + p3[2] : Prow[(uint64_t) sy * N + dy * W + x];
+   }
+   if (pcol)
+   {
+      for (uint32_t q = threadIdx.x; q < H * 9; q += blockDim.x)
+      {
+         const uint32_t sy = q / 9, dir3 = (q % 9) / 3, in = q % 3;
+         const uint32_t dir = dir3 == 0 ? P_SELF : dir3 == 1 ? P_DOWN : P_UP;
+         const uint32_t d0 = dir == P_UP ? sy + 1 : dir == P_DOWN ? 0u : sy;
+         const uint32_t d1 = dir == P_UP ? H : dir == P_DOWN ? sy : sy + 1;
+         const uint32_t* p3 = pcol + ((uint64_t) blockIdx.x * H + sy) * H * 3 + in;
+         uint32_t cnt = 0;
+         for (uint32_t dy = d0; dy < d1; dy++) cnt += p3[dy * 3];
+         slot_cnt[slot_of(sy * W + x, dir, in)] = cnt;
+      }
    }
    __syncthreads();
+   uint32_t* pt = pc + H * H;   // pt[(a-1)H + b-1] = sum over sy < a, dy < b
+   if (threadIdx.x < H)
+   {
+      uint32_t run = 0;
+      for (uint32_t dy = 0; dy < H; dy++)
+      {
+         run += pc[threadIdx.x * H + dy];
+         pt[threadIdx.x * H + dy] = run;
+      }
+   }
+   __syncthreads();
+   if (threadIdx.x < H)
+   {
+      uint32_t run = 0;
+      for (uint32_t sy = 0; sy < H; sy++)
+      {
+         run += pt[sy * H + threadIdx.x];
+         pt[sy * H + threadIdx.x] = run;
+      }
+   }
+   __syncthreads();
+   auto P = [&](uint32_t a, uint32_t b) -> uint32_t { return (a && b) ? pt[(a - 1) * H + (b - 1)] : 0u; };
+   auto rect = [&](uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) -> uint32_t {
+      return (a0 >= a1 || b0 >= b1) ? 0u : P(a1, b1) - P(a0, b1) - P(a1, b0) + P(a0, b0);
+   };
    for (uint32_t q = threadIdx.x; q < H * 5; q += blockDim.x)
    {
       const uint32_t y = q / 5, dir = q % 5, tile = y * W + x;
       const uint32_t by0 = y / c.BH * c.BH, by1 = by0 + c.BH;
       uint32_t cs = 0, cn = 0;
-      if (dir == P_UP)
-      {
-         for (uint32_t sy = by0; sy < y; sy++)
-            for (uint32_t dy = y + 1; dy < by1; dy++) cs += pc[sy * H + dy];
-      }
+      if (dir == P_UP) cs = rect(by0, y, y + 1, by1);
       else if (dir == P_SELF)
       {
          for (uint32_t sy = by0; sy < y; sy++) cs += pc[sy * H + y];
       }
-      if (dir == P_DOWN)
-      {
-         for (uint32_t sy = y + 1; sy < by1; sy++)
-            for (uint32_t dy = by0; dy < y; dy++) cn += pc[sy * H + dy];
-      }
+      if (dir == P_DOWN) cn = rect(y + 1, by1, by0, y);
       else if (dir == P_SELF)
       {
          for (uint32_t sy = y + 1; sy < by1; sy++) cn += pc[sy * H + y];
