@@ -23,6 +23,8 @@
 #include "gnoc.h"
 #include "kernels.hip"
 #include "level.hip"
+#define LV_GEN 1
+#include "level.hip"   // lvg::k_level: any network frequency
 #include "prep.hip"
 #include "shard.hip"
 
@@ -869,7 +871,7 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
    // release/acquire hand-offs -- exact, but a consumer still waits for whole
    // producer ports and every chunk pays an L2 write-back: 2.8x slower on 32x32.
    const char* xlv = std::getenv("GNOC_XLEVEL");
-   const bool xl = xlv && *xlv == '1' && e->nranks == 1 && !e->nb;
+   const bool xl = xlv && *xlv == '1' && e->nranks == 1 && !e->nb && e->f1;
    uint64_t* stp = stamps ? e->stamps.as<uint64_t>() : nullptr;
 #define GNOC_LEVEL_ARGS(lvl)                                                                                         \
    c, (lvl), e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
@@ -887,8 +889,14 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
    {
       for (uint32_t l = l0; l < l1 && l < L; l++)
       {
-         // broadcast batches take the variant with the broadcast branches (lv_bcast)
-         if (e->nb)
+         // f != 1 GHz: the double-conversion copy (no stamps); broadcast batches
+         // take the variant with the broadcast branches (lv_bcast)
+         if (!e->f1)
+         {
+            if (e->nb) GNOC_LAUNCH(e, KC_LEVEL, (lvg::k_level<false, false, true>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
+            else GNOC_LAUNCH(e, KC_LEVEL, (lvg::k_level<false, false, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
+         }
+         else if (e->nb)
          {
             if (stamps) GNOC_LAUNCH(e, KC_LEVEL, (k_level<true, false, true>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
             else GNOC_LAUNCH(e, KC_LEVEL, (k_level<false, false, true>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(l));
@@ -1149,7 +1157,7 @@ static int run_once(gnoc_engine* e)
    bool done = false;
    int rc = run_prep(e, &done);
    if (rc || done) return rc;
-   const bool v3 = e->f1 && e->dc.max_list >= 3 && !e->force_v1;
+   const bool v3 = e->dc.max_list >= 3 && !e->force_v1;
    e->used_v3 = v3;
    if (v3)
    {
@@ -1251,8 +1259,8 @@ int gnoc_shard(gnoc_engine* e, int32_t rank, int32_t nranks)
    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(e, GNOC_EINVAL, "bad rank / nranks");
    if ((uint32_t) nranks > std::min(e->dc.W, e->dc.H)) return fail(e, GNOC_EINVAL, "more ranks than mesh rows or columns");
    if (nranks > 1 && e->npoints > 1) return fail(e, GNOC_EUNSUPPORTED, "a sweep shards by points (one engine per rank)");
-   if (nranks > 1 && e->dc.contention && !(e->f1 && e->dc.max_list >= 3))
-      return fail(e, GNOC_EUNSUPPORTED, "sharding needs the chunked path (f = 1 GHz, max_list_size >= 3)");
+   if (nranks > 1 && e->dc.contention && e->dc.max_list < 3)
+      return fail(e, GNOC_EUNSUPPORTED, "sharding needs the chunked path (max_list_size >= 3)");
    e->rank = rank;
    e->nranks = nranks;
    build_static_levels(e);

@@ -24,10 +24,19 @@
 //   4. decoupled look-back over the port's earlier chunks in ONE round trip:
 //      every state word is an 8-byte self-validating granule (zeroed per run)
 //   5. recurrence and stores straight from registers
-// Only f == 1 GHz and max_list_size >= 3 take this path (engine.hip).
+// Only max_list_size >= 3 takes this path (engine.hip).  engine.hip includes
+// this file twice: LV_GEN 0 is the f = 1 GHz kernel (integer ps <-> cycle
+// conversions), LV_GEN 1 (namespace lvg) the kernel for any other frequency
+// (Time::toCycles / Latency::toPicosec in double, time_types.h:81-109).  Two
+// copies rather than a template flag: the flag alone changed the inlining of the
+// f = 1 GHz kernel and cost it 3% on 32x32.
+#ifndef LV_GEN
+#define LV_GEN 0
+#endif
 #include "common.h"
 
 namespace gnoc {
+#if !LV_GEN
 
 constexpr int LV_T = 256;                // threads per workgroup
 #ifndef LV_CAP_V
@@ -74,6 +83,17 @@ struct __attribute__((aligned(16))) PortIO3
 };
 static_assert(sizeof(PortIO3) % 16 == 0, "PortIO3 copy granularity");
 constexpr uint32_t LV_NO_PROD = 0xFFFFFFFFu;
+#endif
+
+#if LV_GEN
+namespace lvg {   // (argument-dependent lookup must not see the other copy: each lives in a namespace of its own)
+#define LV_CYC(ps) cyc_of<false>((ps), sm.fq)
+#define LV_PS(cy) ps_of<false>((cy), sm.fq)
+#else
+namespace lvx {
+#define LV_CYC(ps) cyc1(ps)
+#define LV_PS(cy) ((cy) * 1000ull)
+#endif
 
 // Carried queue state (exclusive prefix of a chunk / leaf).
 struct Carry3
@@ -108,6 +128,9 @@ struct LvSmem
    uint32_t nexc_leaf, published, nleaf, st_cnt;
    uint32_t st_mg1, pad0, pad1, pad2;
    uint64_t tm[4];           // debug phase stamps inside a leaf (GNOC_STAMPS)
+#if LV_GEN
+   double fq;                // network frequency (GHz)
+#endif
    // current chunk's key range
    uint64_t klo_t, khi_t;
    uint32_t klo_i, khi_i, has_lo, has_hi, empty, nc;
@@ -598,7 +621,7 @@ __device__ Scan3 lv_scan(LvSmem& sm, const Seg& sg)
       const uint32_t k = sm.perm[sg.a + i];
       const uint32_t ax = sm.ka[k];
       const uint64_t p = aux_F(ax);
-      mp_comp(A, B, p, cyc1(sm.kt[k]) + p);
+      mp_comp(A, B, p, LV_CYC(sm.kt[k]) + p);
       if (!BC || !(ax & AUX_BC)) C += 1ull << (12 * next_dir(ax, dir, nx, ny));   // broadcast children: tails
    }
    uint64_t iA = A, iB = B, iC = C;
@@ -657,7 +680,7 @@ __device__ uint64_t lv_bcast(const LvSmem& sm, const DevCfg& c, uint64_t t, uint
    if (dir != P_INJ)
    {
       v = (uint64_t) c.bc_idx[id] * c.N + sm.io.port / PORTS;
-      const uint64_t tc = cyc1(t), xb = cc ? tc + cc : 0ull;
+      const uint64_t tc = LV_CYC(t), xb = cc ? tc + cc : 0ull;
       const uint64_t old = atomicMax((unsigned long long*) (c.bc_mcur + v), (unsigned long long) xb);
       const uint64_t mp = c.bc_mprev[v];
       uint64_t u = tc + cc;
@@ -665,10 +688,10 @@ __device__ uint64_t lv_bcast(const LvSmem& sm, const DevCfg& c, uint64_t t, uint
       u = u > mp ? u : mp;
       ch = u - tc;
    }
-   const uint64_t tn = t + ch * 1000ull + rl;
+   const uint64_t tn = t + LV_PS(ch) + rl;
    if (dir == P_SELF)
    {
-      c.bc_fin[v] = tn + 1000ull * aux_F(ax);
+      c.bc_fin[v] = tn + LV_PS(aux_F(ax));
       return ch;
    }
    const uint32_t m = bc_mask(aux_dx(ax), aux_dy(ax), sm.io.nx, sm.io.ny, c.W, c.H);
@@ -705,10 +728,10 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
          const uint64_t t = sm.kt[k];
          const uint32_t id = sm.ki[k], ax = sm.ka[k];
          const uint64_t mg_before = s.mg1;
-         const uint64_t cc = serial_step(s, cyc1(t), aux_F(ax), c.max_list, c.analytical);
+         const uint64_t cc = serial_step(s, LV_CYC(t), aux_F(ax), c.max_list, c.analytical);
          if (s.g >= 1) s.mode = 0;
          sflit += aux_F(ax);
-         const uint64_t dep = cyc1(t) + cc + aux_F(ax);
+         const uint64_t dep = LV_CYC(t) + cc + aux_F(ax);
          slast = slast > dep ? slast : dep;
          if (BC && (ax & AUX_BC))
          {
@@ -716,8 +739,8 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
             continue;
          }
          ssum += cc;
-         const uint64_t tn = t + cc * 1000ull + rl;
-         if (dir == P_SELF) { final_ps[id] = tn + 1000ull * aux_F(ax); continue; }
+         const uint64_t tn = t + LV_PS(cc) + rl;
+         if (dir == P_SELF) { final_ps[id] = tn + LV_PS(aux_F(ax)); continue; }
          const uint32_t nd = next_dir(ax, dir, nx, ny);
          Rec o;
          o.t = tn;
@@ -774,7 +797,7 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
          const uint64_t t = sm.kt[k];
          const uint32_t id = sm.ki[k];
          const uint32_t ax = sm.ka[k];
-         const uint64_t tc = cyc1(t);
+         const uint64_t tc = LV_CYC(t);
          const uint64_t cc = X > tc ? X - tc : 0;
          X = (X > tc ? X : tc) + aux_F(ax);
          if (BC && (ax & AUX_BC))
@@ -783,11 +806,11 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
             continue;
          }
          ssum += cc;
-         const uint64_t tn = t + cc * 1000ull + rl;
+         const uint64_t tn = t + LV_PS(cc) + rl;
          if (dir == P_SELF)
          {
             // NetworkModel::processReceivedPacket: + serialization (network_model.cc:142-150)
-            final_ps[id] = tn + 1000ull * aux_F(ax);
+            final_ps[id] = tn + LV_PS(aux_F(ax));
             continue;
          }
          const uint32_t nd = next_dir(ax, dir, nx, ny);
@@ -1228,6 +1251,9 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
    // before this launch); the cross-level launch always reads the counts
    const bool anyexc = XL || errflag[2] != 0;
    if (tid == 0) { sm.nx.ready = 0; sm.qdone = 0; }
+#if LV_GEN
+   if (tid == 0) sm.fq = c.f;
+#endif
    if (!XL && tid < LV_QB) sm.qb[tid] = lvl_qb[level * LV_QB + tid];
    if (XL && tid == 0) sm.qb[LV_QUEUES + 1] = 0;
    lv_bar();
@@ -1317,7 +1343,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
             // arrival keeps it there only at cycle 0 (queue_model_history_tree.cc:58-99).
             // An empty chunk 0 (every early record is an exception tail of another
             // chunk's range) hands the untouched serial state on to its successor.
-            if (tid == 0 && c.analytical && (sm.E == 0 || cyc1(sm.kt[sm.perm[0]]) == 0)) sm.cy.mode = 1;
+            if (tid == 0 && c.analytical && (sm.E == 0 || LV_CYC(sm.kt[sm.perm[0]]) == 0)) sm.cy.mode = 1;
             if (tid == 0) sm.s0 = 0;
             lv_bar();
          }
@@ -1458,7 +1484,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
                lv_load_merge(sm, recs, sm.lk_t[L], sm.lk_i[L], sm.lk_t[L + 1], sm.lk_i[L + 1], hl, hh, true);
                if (j == 0 && L == 0)
                {
-                  if (tid == 0 && c.analytical && (sm.E == 0 || cyc1(sm.kt[sm.perm[0]]) == 0)) sm.cy.mode = 1;
+                  if (tid == 0 && c.analytical && (sm.E == 0 || LV_CYC(sm.kt[sm.perm[0]]) == 0)) sm.cy.mode = 1;
                   lv_bar();
                }
                lv_leaf<BC>(sm, c, recs, samp_t, samp_id, nexc, final_ps, errflag);
@@ -1512,6 +1538,13 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
    }
 }
 
+#undef LV_CYC
+#undef LV_PS
+#if LV_GEN
+}  // namespace lvg
+#else
+}  // namespace lvx
+using namespace lvx;
 // ---------------------------------------------------------------------------
 // device-side plan
 // ---------------------------------------------------------------------------
@@ -1747,4 +1780,6 @@ __global__ __launch_bounds__(64) void k_plan_fill(const PortIO3* __restrict__ pi
       if (lane < WORDS) reinterpret_cast<uint32_t*>(cdesc + gb + j)[lane] = v;
 }
 
+#endif
 }  // namespace gnoc
+#undef LV_GEN

@@ -96,8 +96,26 @@ def test_non_unit_frequency(freq):
     cfg = gnoc.EngineConfig(num_tiles=16, frequency_ghz=freq, link_delay=lk)
     tr = random_trace(3000, 4, 4, seed=int(freq * 10), max_cycle=500, burst0=8, ps_jitter=True,
                       frequency_ghz=freq)
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    got = eng.results()
+    assert eng.summary()["engine_path"] == 1      # the chunked kernel with the double ps <-> cycle conversions
+    eng.close()
+    assert_same(got, oracle.run(cfg, tr))
+
+
+@pytest.mark.parametrize("freq", [0.9, 1.25])
+def test_non_unit_frequency_chunked_8x8(freq):
+    """f != 1 GHz on the chunked path at a size with many chunks per port,
+    M/G/1 bursts included (Time::toCycles / Latency::toPicosec, time_types.h:81-109)."""
+    cfg = gnoc.EngineConfig(num_tiles=64, frequency_ghz=freq)
+    tr = random_trace(40000, 8, 8, seed=int(freq * 100), max_cycle=4000, burst0=300, frequency_ghz=freq)
     got, ref = run_both(cfg, tr)
+    assert ref.port_mg1.sum() > 0
     assert_same(got, ref)
+    for k in ("port_sum_delay", "port_count", "port_mg1", "port_flit", "port_last"):
+        assert np.array_equal(getattr(got, k), getattr(ref, k)), k
 
 
 @pytest.mark.parametrize("max_list,analytical", [(2, 1), (3, 1), (100, 0), (5, 1)])

@@ -74,6 +74,18 @@ def test_local_shards_vs_oracle_8x8_saturated(n):
     _local_vs(cfg, tr, n, ref)
 
 
+@pytest.mark.parametrize("n", [3, 8])
+def test_local_shards_vs_oracle_non_unit_frequency(n):
+    """A sharded mesh at f = 0.9 GHz (the chunked path's double conversions on every rank)."""
+    from graphite_amd import gnoc
+    from oracle import oracle
+    from tests.traces import random_trace
+    cfg = gnoc.EngineConfig(num_tiles=64, frequency_ghz=0.9)
+    tr = random_trace(20000, 8, 8, seed=5, max_cycle=2000, burst0=200, ps_jitter=True, frequency_ghz=0.9)
+    ref = oracle.run(cfg, tr)
+    _local_vs(cfg, tr, n, ref)
+
+
 @pytest.mark.parametrize("W,n,hot", [(32, 8, 0.0), (32, 7, 0.2), (64, 8, 0.0)])
 def test_local_shards_vs_unsharded(W, n, hot):
     from graphite_amd import gnoc
