@@ -24,7 +24,7 @@ def rows(pattern):
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").replace("gnoc::", "").split("<")[0]
+    return name.split("(")[0].replace("void ", "").split("<")[0].split("::")[-1]
 
 
 kt = rows("run_kernel_trace.csv")
