@@ -28,6 +28,14 @@
 #include "prep.hip"
 #include "shard.hip"
 
+namespace gnoc {
+// Packets per prep chunk (k_classify / k_scatter blocks): each chunk keeps an
+// N-entry source histogram (hist = 4 B per packet at most), and more, smaller
+// chunks keep enough waves in flight for the per-packet latency chains of the
+// scatter (16,384-tile sweeps: 65,536 -> 16,384 packets per chunk).
+static inline uint32_t prep_chunk(uint32_t N) { return std::max<uint32_t>(16384u, (N + 63u) & ~63u); }
+}  // namespace gnoc
+
 using namespace gnoc;
 
 namespace {
@@ -710,7 +718,7 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    GNOC_HIP(e, e->routed.ensure(n + 4));
    GNOC_HIP(e, e->final_ps.ensure(n * 8 + 8));
    const uint32_t N = e->dc.N;
-   const uint32_t pch = std::max<uint32_t>(16384u, (4u * N + 63u) & ~63u);
+   const uint32_t pch = prep_chunk(N);
    const uint32_t nch = (uint32_t) std::max<uint64_t>(1, (n + pch - 1) / pch);
    GNOC_HIP(e, e->hist.ensure((size_t) nch * N * 4));
    GNOC_HIP(e, hipMemsetAsync(e->counters.p, 0, 64, e->stream));
@@ -927,7 +935,7 @@ static int run_prep(gnoc_engine* e, bool* done)
    const uint32_t nslots = N * PORTS * INS;
    const size_t nports = (size_t) N * PORTS;
    hipStream_t s = e->stream;
-   const uint32_t pch = std::max<uint32_t>(16384u, (4u * N + 63u) & ~63u);
+   const uint32_t pch = prep_chunk(N);
    const uint32_t nch = (uint32_t) std::max<uint64_t>(1, (n + pch - 1) / pch);
    int nbits = 0;
    while ((1u << nbits) < N) nbits++;

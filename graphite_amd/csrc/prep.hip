@@ -215,31 +215,54 @@ __global__ __launch_bounds__(64) void k_scatter(uint64_t n, uint32_t pch, uint32
    const uint64_t hi = min(lo + pch, n);
    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
    const uint32_t* orow = offs + (uint64_t) blockIdx.x * N;
-   for (uint64_t k = lo; k < hi; k += 64)
+   // 8 groups of 64 packets per batch: their loads (then the source-dependent
+   // offsets) in flight together, so a batch costs two round trips, not sixteen
+   for (uint64_t k0 = lo; k0 < hi; k0 += 512)
    {
-      const uint64_t i = k + lane;
-      const bool valid = i < hi && (routed[i] & 2);
-      const uint32_t s = valid ? src[i] : 0u;
-      const uint64_t m = match_mask(s, valid, nbits);
-      const uint32_t old = valid ? h[s] : 0u;
-      __syncthreads();
-      if (valid)
+      bool vv[8];
+      uint32_t sv[8], av[8], ov[8];
+      uint64_t tv[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++)
       {
-         const uint32_t rank = old + (uint32_t) __popcll(m & lt);
-         if ((63 - __clzll(m)) == (int) lane) h[s] = old + (uint32_t) __popcll(m);
-         const uint64_t pos = (uint64_t) orow[s] + rank;
-         Rec r;
-         r.t = inj[i];
-         r.id = (uint32_t) i;
-         r.aux = aux[i];
-         recs[pos] = r;
-         if ((pos & 63) == 0)
-         {
-            samp_t[pos >> 6] = r.t;
-            samp_id[pos >> 6] = r.id;
-         }
+         const uint64_t i = k0 + (uint64_t) (q * 64) + lane;
+         vv[q] = i < hi && (routed[i] & 2);
+         sv[q] = vv[q] ? src[i] : 0u;
       }
-      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < 8; q++)
+      {
+         const uint64_t i = k0 + (uint64_t) (q * 64) + lane;
+         tv[q] = 0; av[q] = 0; ov[q] = 0;
+         if (vv[q]) { tv[q] = inj[i]; av[q] = aux[i]; ov[q] = orow[sv[q]]; }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; q++)
+      {
+         const bool valid = vv[q];
+         const uint32_t sq = sv[q];
+         const uint64_t m = match_mask(sq, valid, nbits);
+         const uint32_t old = valid ? h[sq] : 0u;
+         __builtin_amdgcn_wave_barrier();
+         if (valid)
+         {
+            const uint32_t rank = old + (uint32_t) __popcll(m & lt);
+            if ((63 - __clzll(m)) == (int) lane) h[sq] = old + (uint32_t) __popcll(m);
+            const uint64_t pos = (uint64_t) ov[q] + rank;
+            Rec r;
+            r.t = tv[q];
+            r.id = (uint32_t) (k0 + (uint64_t) (q * 64) + lane);
+            r.aux = av[q];
+            recs[pos] = r;
+            if ((pos & 63) == 0)
+            {
+               samp_t[pos >> 6] = r.t;
+               samp_id[pos >> 6] = r.id;
+            }
+         }
+         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+         __builtin_amdgcn_wave_barrier();
+      }
    }
 }
 
