@@ -27,6 +27,9 @@
 #include "level.hip"   // lvg::k_level: any network frequency
 #include "prep.hip"
 #include "shard.hip"
+#include "serial.hip"
+
+#include <hipcub/hipcub.hpp>
 
 namespace gnoc {
 // Packets per prep chunk (k_classify / k_scatter blocks): each chunk keeps an
@@ -136,6 +139,11 @@ struct gnoc_engine
    std::vector<uint64_t> h_pt_rl;
    std::vector<uint32_t> h_pt_fw;
    DevBuf d_pt_rl, d_pt_fw;
+
+   // QueueModelBasic with a moving average (gnoc_set_basic_moving_average, serial.hip)
+   int ma_type = 0;
+   uint32_t ma_window = 1;
+   DevBuf ma_t, ma_key, ma_val, ma_key2, ma_val2, ma_lo, ma_hi, ma_ring, ma_tmp;
 
    // kernel profiling (gnoc_set_profiling)
    bool prof = false;
@@ -1178,9 +1186,125 @@ static int run_once(gnoc_engine* e)
    return run_post(e, false);
 }
 
+// ---------------------------------------------------------------------------
+// engine path 3: basic queues with a moving average (serial.hip)
+// ---------------------------------------------------------------------------
+static int run_ma(gnoc_engine* e)
+{
+   if (!e->submitted) return fail(e, GNOC_ESTATE, "gnoc_run before gnoc_submit");
+   if (e->nb) return fail(e, GNOC_EUNSUPPORTED, "broadcast packets with moving-average basic queues");
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   const DevCfg& c = e->dc;
+   const size_t n = e->n;
+   const size_t nports = (size_t) c.N * PORTS;
+   hipStream_t s = e->stream;
+   const uint32_t nlvl = (uint32_t) e->lvl_off.size() - 1;
+   uint32_t maxloc = 1;
+   for (uint32_t l = 0; l < nlvl; l++) maxloc = std::max(maxloc, e->lvl_off[l + 1] - e->lvl_off[l]);
+   GNOC_HIP(e, e->final_ps.ensure(n * 8 + 8));
+   GNOC_HIP(e, e->zl.ensure(n * 8 + 8));
+   GNOC_HIP(e, e->cont.ensure(n * 8 + 8));
+   GNOC_HIP(e, e->ma_t.ensure(n * 8 + 8));
+   GNOC_HIP(e, e->ma_key.ensure(n * 8 + 8));
+   GNOC_HIP(e, e->ma_key2.ensure(n * 8 + 8));
+   GNOC_HIP(e, e->ma_val.ensure(n * 4 + 4));
+   GNOC_HIP(e, e->ma_val2.ensure(n * 4 + 4));
+   GNOC_HIP(e, e->ma_lo.ensure((size_t) maxloc * 4));
+   GNOC_HIP(e, e->ma_hi.ensure((size_t) maxloc * 4));
+   GNOC_HIP(e, e->ma_ring.ensure((size_t) maxloc * (e->ma_window + 1) * 8));
+   GNOC_HIP(e, e->counters.ensure(64));
+   for (DevBuf* b : { &e->port_sum, &e->port_cnt, &e->port_mg1, &e->port_flit, &e->port_last })
+   {
+      GNOC_HIP(e, b->ensure(nports * 8));
+      GNOC_HIP(e, hipMemsetAsync(b->p, 0, nports * 8, s));
+   }
+   size_t tmp_bytes = 0;
+   GNOC_HIP(e, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, e->ma_key.as<uint64_t>(), e->ma_key2.as<uint64_t>(),
+                                                  e->ma_val.as<uint32_t>(), e->ma_val2.as<uint32_t>(), (int) n, 0, 64, s));
+   GNOC_HIP(e, e->ma_tmp.ensure(tmp_bytes + 16));
+   GNOC_HIP(e, hipMemsetAsync(e->counters.p, 0, 64, s));
+   GNOC_HIP(e, hipEventRecord(e->ev0, s));
+   const uint32_t grid = (uint32_t) std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 8192));
+   unsigned* err = e->counters.as<unsigned>() + 8;
+   if (n)
+   {
+      hipLaunchKernelGGL(k_ma_init, dim3(grid), dim3(256), 0, s, (uint64_t) n, c.W, e->d_inj, e->d_src, e->d_dst,
+                         e->d_flags, e->ma_t.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
+                         e->cont.as<uint64_t>(), e->counters.as<unsigned long long>());
+      GNOC_HIP(e, hipGetLastError());
+      for (uint32_t l = 0; l < nlvl; l++)
+      {
+         const uint32_t k0 = e->lvl_off[l], nloc = e->lvl_off[l + 1] - k0;
+         if (!nloc) continue;
+         int lb = 1;
+         while ((1u << lb) <= nloc) lb++;   // nloc < 2^lb: the all-ones port index is free
+         const int end_bit = (int) MA_T_BITS + lb;
+         const uint64_t invalid = end_bit >= 64 ? ~0ull : (1ull << end_bit) - 1;
+         hipLaunchKernelGGL(k_ma_keys, dim3(grid), dim3(256), 0, s, (uint64_t) n, c.W, l, nlvl, k0, invalid, e->d_src,
+                            e->d_dst, e->d_flags, e->d_port_k.as<uint32_t>(), (const uint64_t*) e->ma_t.as<uint64_t>(),
+                            e->ma_key.as<uint64_t>(), e->ma_val.as<uint32_t>(), err);
+         GNOC_HIP(e, hipGetLastError());
+         size_t tb = tmp_bytes;
+         GNOC_HIP(e, hipcub::DeviceRadixSort::SortPairs(e->ma_tmp.p, tb, e->ma_key.as<uint64_t>(), e->ma_key2.as<uint64_t>(),
+                                                        e->ma_val.as<uint32_t>(), e->ma_val2.as<uint32_t>(), (int) n, 0,
+                                                        end_bit, s));
+         GNOC_HIP(e, hipMemsetAsync(e->ma_lo.p, 0, (size_t) nloc * 4, s));
+         GNOC_HIP(e, hipMemsetAsync(e->ma_hi.p, 0, (size_t) nloc * 4, s));
+         hipLaunchKernelGGL(k_ma_bounds, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid,
+                            (const uint64_t*) e->ma_key2.as<uint64_t>(), e->ma_lo.as<uint32_t>(), e->ma_hi.as<uint32_t>());
+         GNOC_HIP(e, hipGetLastError());
+         hipLaunchKernelGGL(k_ma_walk, dim3((nloc + 63) / 64), dim3(64), 0, s, nloc,
+                            e->d_lvl_ports.as<uint32_t>() + k0, e->ma_type, e->ma_window, c.flit_width, c.f, c.rl_ps,
+                            (const uint64_t*) e->ma_key2.as<uint64_t>(), (const uint32_t*) e->ma_val2.as<uint32_t>(),
+                            (const uint32_t*) e->ma_lo.as<uint32_t>(), (const uint32_t*) e->ma_hi.as<uint32_t>(),
+                            e->d_bits, e->ma_ring.as<uint64_t>(), e->ma_t.as<uint64_t>(), e->final_ps.as<uint64_t>(),
+                            e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), e->port_sum.as<uint64_t>(),
+                            e->port_cnt.as<uint64_t>(), e->port_flit.as<uint64_t>(), e->port_last.as<uint64_t>());
+         GNOC_HIP(e, hipGetLastError());
+      }
+   }
+   GNOC_HIP(e, hipEventRecord(e->ev1, s));
+   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 40, hipMemcpyDeviceToHost, s));
+   GNOC_HIP(e, hipStreamSynchronize(s));
+   if (*(const unsigned*) (e->h_pinned + 4)) return fail(e, GNOC_EUNSUPPORTED, "packet time beyond 2^49 ps");
+   e->h_counters[0] = e->h_pinned[0];
+   e->h_counters[1] = e->h_pinned[1];
+   e->h_records = e->h_counters[0] + e->h_counters[1];
+   e->h_levels = nlvl;
+   e->used_v3 = 3;
+   float ms = 0;
+   GNOC_HIP(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+   e->last_ms = ms;
+   e->ran = true;
+   return GNOC_OK;
+}
+
+int gnoc_set_basic_moving_average(gnoc_engine* e, int32_t type, uint32_t window_size)
+{
+   if (!e) return GNOC_EINVAL;
+   if (type < GNOC_MOVING_AVG_NONE || type > GNOC_MOVING_AVG_MEDIAN) return fail(e, GNOC_EINVAL, "unknown moving average type");
+   if (type != GNOC_MOVING_AVG_NONE && e->cfg.queue_type != GNOC_QUEUE_BASIC)
+      return fail(e, GNOC_EINVAL, "moving averages belong to the basic queue model");
+   if (type != GNOC_MOVING_AVG_NONE && (window_size < 1 || window_size > (1u << 16)))
+      return fail(e, GNOC_EINVAL, "moving_avg_window_size must be in [1, 65536]");
+   if (type != GNOC_MOVING_AVG_NONE && (e->nranks > 1 || e->npoints > 1 || e->dc.hop_counter))
+      return fail(e, GNOC_EUNSUPPORTED, "moving-average queues run on one unsharded mesh engine");
+   // MovingGeometricMean::compute is a chain of pow() calls (moving_average.h:124-145):
+   // the device's pow and glibc's differ in the last bit on some operands, and the
+   // running product carries such a bit into the truncated reference time (measured:
+   // 17,670 of 20,000 packets differ on an 8x8 batch).  Refused rather than approximated.
+   if (type == GNOC_MOVING_AVG_GEOMETRIC_MEAN)
+      return fail(e, GNOC_EUNSUPPORTED, "geometric_mean moving average (pow is not bit-reproducible vs glibc)");
+   e->ma_type = type;
+   e->ma_window = type ? window_size : 1;
+   e->ran = false;
+   return GNOC_OK;
+}
+
 int gnoc_run(gnoc_engine* e)
 {
    if (!e) return GNOC_EINVAL;
+   if (e->ma_type && e->dc.contention) return run_ma(e);
    if (e->nranks > 1) return fail(e, GNOC_ESTATE, "sharded engine: use gnoc_run_begin / exchange / gnoc_run_finish");
    const char* env = std::getenv("GNOC_ENGINE");
    const int forced = env && std::strcmp(env, "v1") == 0;
@@ -1267,6 +1391,7 @@ int gnoc_shard(gnoc_engine* e, int32_t rank, int32_t nranks)
    if (nranks < 1 || rank < 0 || rank >= nranks) return fail(e, GNOC_EINVAL, "bad rank / nranks");
    if ((uint32_t) nranks > std::min(e->dc.W, e->dc.H)) return fail(e, GNOC_EINVAL, "more ranks than mesh rows or columns");
    if (nranks > 1 && e->npoints > 1) return fail(e, GNOC_EUNSUPPORTED, "a sweep shards by points (one engine per rank)");
+   if (nranks > 1 && e->ma_type) return fail(e, GNOC_EUNSUPPORTED, "moving-average queues run on one unsharded mesh engine");
    if (nranks > 1 && e->dc.contention && e->dc.max_list < 3)
       return fail(e, GNOC_EUNSUPPORTED, "sharding needs the chunked path (max_list_size >= 3)");
    e->rank = rank;

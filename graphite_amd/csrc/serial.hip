@@ -1,0 +1,216 @@
+// serial.hip -- QueueModelBasic with a moving average (engine path 3).
+//
+// queue_model_basic.cc:35-61 with queue_model/basic/moving_avg_enabled: the
+// queue's reference time is not the packet time but a moving average over the
+// window of packet times it has seen (common/misc/moving_average.h), and the
+// FIFO recurrence runs on that reference time:
+//   ref = MA.compute(t);  d = max(Q - ref, 0);  Q = max(Q, ref) + F.
+// The arithmetic mean is a running FP64 sum whose rounding depends on every
+// earlier request of the queue, so a queue is one serial walk over its requests
+// in (time, packet id) order.  What stays parallel is the port DAG of XY routing
+// (DESIGN.md 2): every port of a level gets its whole request stream from earlier
+// levels.  Unlike the FIFO paths, a port's departures are NOT in arrival order
+// here (ref < t lets a later packet wait less), so the streams are re-sorted:
+//
+//   per level:  k_ma_keys   key = (port index in level, t_ps), value = packet id,
+//                           one entry per packet (non-visitors get the max key)
+//               radix sort  stable, bits [0, 49 + level bits) (ties: packet id)
+//               k_ma_bounds first / last entry of each port
+//               k_ma_walk   one thread per port: the reference's arithmetic, in
+//                           order, updating each packet's time / contention /
+//                           zero-load and the port's counters
+//
+// The geometric mean's branch is kept for completeness but refused by
+// gnoc_set_basic_moving_average: its pow() chain is not bit-reproducible
+// against glibc.  Arithmetic mean and median are bit-exact against
+// oracle/gnoc_oracle.c (orc_ma_compute, pinned against the
+// reference's own moving_average.h compiled in oracle/_ref).  This TU is compiled
+// with -ffp-contract=off (no FMA contraction), like the M/G/1 arithmetic.
+#pragma once
+
+#include "common.h"
+
+namespace gnoc {
+
+enum : int { MA_NONE = 0, MA_ARITHMETIC = 1, MA_GEOMETRIC = 2, MA_MEDIAN = 3 };   // include/gnoc.h
+
+constexpr uint32_t MA_T_BITS = 49;   // packet times < 2^49 ps (checked per level)
+constexpr uint64_t MA_T_MASK = (1ull << MA_T_BITS) - 1;
+
+__device__ __forceinline__ uint32_t ma_flits(uint32_t bits, uint32_t fw)
+{
+   return (bits % fw) ? bits / fw + 1 : bits / fw;   // network_model.cc:202-212
+}
+
+// Packet state before the first level: unrouted packets (self-sends, unmodeled,
+// network_model.cc:413-468) finish at their injection time with no delay.
+__global__ void k_ma_init(uint64_t n, uint32_t W, const uint64_t* __restrict__ inj, const uint32_t* __restrict__ src,
+                          const uint32_t* __restrict__ dst, const uint32_t* __restrict__ flags,
+                          uint64_t* __restrict__ ptime, uint64_t* __restrict__ fin, uint64_t* __restrict__ zl,
+                          uint64_t* __restrict__ cont, unsigned long long* __restrict__ counters)
+{
+   unsigned long long hops = 0, routed = 0;
+   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+   {
+      ptime[i] = inj[i];
+      fin[i] = inj[i];
+      zl[i] = 0;
+      cont[i] = 0;
+      const uint32_t s = src[i], d = dst[i];
+      if (s != d && !(flags && (flags[i] & 1u)))
+      {
+         const uint32_t sx = s % W, sy = s / W, dx = d % W, dy = d / W;
+         routed++;
+         hops += (sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1;   // H + 1 mesh routers
+      }
+   }
+   if (hops) atomicAdd(&counters[0], hops);
+   if (routed) atomicAdd(&counters[1], routed);
+}
+
+// The port a packet src s -> dst d requests at level lvl of the plan (engine.hip
+// build_static_levels), or ~0u when its route has no port there.
+__device__ __forceinline__ uint32_t ma_port_at(uint32_t W, uint32_t s, uint32_t d, uint32_t lvl, uint32_t nlvl)
+{
+   const uint32_t sx = s % W, sy = s / W, dx = d % W, dy = d / W;
+   if (lvl == 0) return s * PORTS + P_INJ;
+   if (lvl == nlvl - 1) return d * PORTS + P_SELF;
+   if (lvl < W)
+   {
+      const uint32_t l = lvl;
+      if (sx < dx && sx <= l - 1 && l - 1 < dx) return (sy * W + l - 1) * PORTS + P_RIGHT;
+      if (sx > dx && dx < W - l && W - l <= sx) return (sy * W + W - l) * PORTS + P_LEFT;
+      return ~0u;
+   }
+   const uint32_t k = lvl - W, H = nlvl - W;   // nlvl = W + H
+   if (sy < dy && sy <= k && k < dy) return (k * W + dx) * PORTS + P_UP;
+   if (sy > dy && dy < H - 1 - k && H - 1 - k <= sy) return ((H - 1 - k) * W + dx) * PORTS + P_DOWN;
+   return ~0u;
+}
+
+__global__ void k_ma_keys(uint64_t n, uint32_t W, uint32_t lvl, uint32_t nlvl, uint32_t k0, uint64_t invalid,
+                          const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                          const uint32_t* __restrict__ flags, const uint32_t* __restrict__ port_k,
+                          const uint64_t* __restrict__ ptime, uint64_t* __restrict__ key, uint32_t* __restrict__ val,
+                          unsigned* __restrict__ err)
+{
+   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+   {
+      uint64_t kv = invalid;
+      const uint32_t s = src[i], d = dst[i];
+      if (s != d && !(flags && (flags[i] & 1u)))
+      {
+         const uint32_t p = ma_port_at(W, s, d, lvl, nlvl);
+         if (p != ~0u)
+         {
+            const uint64_t t = ptime[i];
+            if (t > MA_T_MASK) atomicOr(err, 1u);
+            kv = ((uint64_t) (port_k[p] - k0) << MA_T_BITS) | (t & MA_T_MASK);
+         }
+      }
+      key[i] = kv;
+      val[i] = (uint32_t) i;
+   }
+}
+
+__global__ void k_ma_bounds(uint64_t n, uint64_t invalid, const uint64_t* __restrict__ key, uint32_t* __restrict__ lo,
+                            uint32_t* __restrict__ hi)
+{
+   for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < n; j += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const uint64_t k = key[j];
+      if (k == invalid) continue;
+      const uint32_t p = (uint32_t) (k >> MA_T_BITS);
+      if (j == 0 || (uint32_t) (key[j - 1] >> MA_T_BITS) != p) lo[p] = (uint32_t) j;
+      if (j + 1 == n || key[j + 1] == invalid || (uint32_t) (key[j + 1] >> MA_T_BITS) != p) hi[p] = (uint32_t) (j + 1);
+   }
+}
+
+// One queue: QueueModelBasic::computeQueueDelay (queue_model_basic.cc:35-61) with
+// MovingAverage<UInt64>::compute (moving_average.h:90-110 arithmetic, 124-145
+// geometric, 153-162 median) and RouterModel / Hop bookkeeping per request
+// (router_model.cc:70-108, network_model.cc:556-563, :142-150).
+__global__ void k_ma_walk(uint32_t nloc, const uint32_t* __restrict__ ports, int ma_type, uint32_t ma_max,
+                          uint32_t flit_width, double f, uint64_t rl_ps, const uint64_t* __restrict__ key,
+                          const uint32_t* __restrict__ val, const uint32_t* __restrict__ lo,
+                          const uint32_t* __restrict__ hi, const uint32_t* __restrict__ bits, uint64_t* __restrict__ ring,
+                          uint64_t* __restrict__ ptime, uint64_t* __restrict__ fin, uint64_t* __restrict__ zl,
+                          uint64_t* __restrict__ cont, uint64_t* __restrict__ port_sum, uint64_t* __restrict__ port_cnt,
+                          uint64_t* __restrict__ port_flit, uint64_t* __restrict__ port_last)
+{
+   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+   if (p >= nloc) return;
+   const uint32_t port = ports[p];
+   const uint32_t dir = port % PORTS;
+   const uint32_t M = ma_max + 1;
+   uint64_t* list = ring + (size_t) p * M;
+   uint32_t front = 0, back = 0;
+   double mean = ma_type == MA_GEOMETRIC ? 1.0 : 0.0;
+   uint64_t Q = 0, sum = 0, cnt = 0, flits = 0, last = 0;
+   const uint32_t j0 = lo[p], j1 = hi[p];
+   const uint64_t hop_ps = dir == P_INJ ? ps_of<false>(0, f) : rl_ps;   // injection router: delay 0
+   for (uint32_t j = j0; j < j1; j++)
+   {
+      const uint64_t t = key[j] & MA_T_MASK;
+      const uint32_t id = val[j];
+      const uint32_t F = ma_flits(bits[id], flit_width);
+      const uint64_t tc = cyc_of<false>(t, f);
+      // MovingAverage::compute
+      const uint32_t cw = back >= front ? back - front : back + M - front;
+      uint64_t ref;
+      if (ma_type == MA_MEDIAN)
+      {
+         list[back] = tc;
+         back = (back + 1) % M;
+         if (back == front) front = (front + 1) % M;
+         const uint32_t w = back >= front ? back - front : back + M - front;
+         ref = list[(front + (w / 2) % M) % M];
+      }
+      else
+      {
+         if (ma_type == MA_ARITHMETIC)
+         {
+            if (cw == ma_max)
+               mean += (((double) tc / (double) cw) - ((double) list[front] / (double) cw));
+            else
+               mean = (mean * (double) cw + (double) tc) / (double) (cw + 1);
+         }
+         else
+         {
+            if (cw == ma_max)
+               mean *= (pow((double) tc, (1.0 / (double) cw)) / pow((double) list[front], (1.0 / (double) cw)));
+            else
+               mean = pow(pow(mean, (double) cw) * (double) tc, (1.0 / (double) (cw + 1)));
+         }
+         list[back] = tc;
+         back = (back + 1) % M;
+         if (back == front) front = (front + 1) % M;
+         ref = (uint64_t) mean;
+      }
+      const uint64_t d = Q > ref ? Q - ref : 0;
+      Q = (Q > ref ? Q : ref) + F;
+      // QueueModel::updateQueueUtilizationCounters(ref, F, d), queue_model.cc:48-53
+      flits += F;
+      last = last > ref + d + F ? last : ref + d + F;
+      sum += d;
+      cnt++;
+      const uint64_t cps = ps_of<false>(d, f);
+      uint64_t tn = t + cps + hop_ps;
+      zl[id] += hop_ps;
+      cont[id] += cps;
+      if (dir == P_SELF)
+      {
+         const uint64_t fps = ps_of<false>(F, f);   // receive serialization, network_model.cc:142-150
+         tn += fps;
+         zl[id] += fps;
+         fin[id] = tn;
+      }
+      ptime[id] = tn;
+   }
+   port_sum[port] = sum;
+   port_cnt[port] = cnt;
+   port_flit[port] = flits;
+   port_last[port] = last;
+}
+
+}  // namespace gnoc

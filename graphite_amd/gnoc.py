@@ -26,6 +26,8 @@ GNOC_ENOMEM = -6
 
 PORT_SELF, PORT_LEFT, PORT_RIGHT, PORT_DOWN, PORT_UP, PORT_INJ = range(6)
 QUEUE_HISTORY_TREE, QUEUE_BASIC, QUEUE_HISTORY_LIST = 0, 1, 2
+# queue_model/basic/moving_avg_type (moving_average.h:175-189); NONE = moving_avg_enabled false
+MOVING_AVG_NONE, MOVING_AVG_ARITHMETIC_MEAN, MOVING_AVG_GEOMETRIC_MEAN, MOVING_AVG_MEDIAN = 0, 1, 2, 3
 PORTS_PER_TILE = 6
 PKT_UNMODELED = 0x1
 PKT_BROADCAST = 0x2     # receiver = NetPacket::BROADCAST, routed on the broadcast tree
@@ -38,7 +40,7 @@ EXPORTED = (
     "gnoc_set_profiling", "gnoc_get_kernel_stats", "gnoc_trace_file_write", "gnoc_trace_file_read",
     "gnoc_shard", "gnoc_exchange_counts", "gnoc_run_begin", "gnoc_run_finish",
     "gnoc_create_sweep", "gnoc_sweep_layout", "gnoc_get_port_utilization", "gnoc_create_hop_counter",
-    "gnoc_get_broadcast_results", "gnoc_get_broadcast_info",
+    "gnoc_get_broadcast_results", "gnoc_get_broadcast_info", "gnoc_set_basic_moving_average",
 )
 
 
@@ -143,6 +145,7 @@ def load() -> ctypes.CDLL:
     lib.gnoc_exchange_counts.argtypes = [vp, vp, vp, sz]
     lib.gnoc_run_begin.argtypes = [vp, vp]
     lib.gnoc_run_finish.argtypes = [vp, vp]
+    lib.gnoc_set_basic_moving_average.argtypes = [vp, ctypes.c_int32, ctypes.c_uint32]
     _lib = lib
     return lib
 
@@ -173,6 +176,11 @@ class EngineConfig:
     # queue_model/history_list/interleaving_enabled: no effect on in-order requests
     # (include/gnoc.h); kept so the oracle can restate the list with it on or off
     interleaving_enabled: bool = True
+    # queue_model/basic/moving_avg_{enabled,type,window_size} (queue_model_basic.cc:7-30):
+    # MOVING_AVG_* (NONE = disabled) and the window; only with queue_type QUEUE_BASIC
+    # (set through gnoc_set_basic_moving_average, not part of gnoc_config)
+    moving_avg_type: int = 0
+    moving_avg_window: int = 64
 
     @property
     def width(self) -> int:
@@ -314,6 +322,8 @@ class Engine:
             self.cfg = replace(cfg, mesh_width=w, mesh_height=int(math.ceil(cfg.num_tiles / w)))
         if rc:
             raise GnocError(rc, "gnoc_create rejected the configuration")
+        if cfg.moving_avg_type and model != "emesh_hop_counter":
+            self._check(self.lib.gnoc_set_basic_moving_average(self._h, cfg.moving_avg_type, cfg.moving_avg_window))
         self._n = 0
         self._keep = None
 

@@ -56,8 +56,6 @@ gnoc_config CfgView::toEngineConfig() const
    const std::string qk = qt == "history_list" ? "queue_model/history_list/" : "queue_model/history_tree/";
    c.analytical_enabled = getBool(qk + "analytical_model_enabled", true);
    c.max_list_size = getInt(qk + "max_list_size", 100);
-   if (c.queue_type == GNOC_QUEUE_BASIC && getBool("queue_model/basic/moving_avg_enabled", true))
-      c.queue_type = -2;   // a running FP64 window mean: not implemented (include/gnoc.h)
    c.tile_width_mm = getFloat("general/tile_width", 1.0);                                        // carbon_sim.cfg:64
    c.frequency_ghz = getFloat("network/frequency", 1.0);   // the network's DVFS domain (dvfs_manager.cc:243-250)
    return c;
@@ -73,12 +71,31 @@ NetworkModelEMeshHopByHopHIP::NetworkModelEMeshHopByHopHIP(const CfgView& cfg, i
         return c;
      }())
 {
+   int32_t type = GNOC_MOVING_AVG_NONE;
+   uint32_t window = 1;
+   cfg.basicMovingAverage(&type, &window);
+   if (_cfg.queue_type == GNOC_QUEUE_BASIC && type != GNOC_MOVING_AVG_NONE)
+      check(gnoc_set_basic_moving_average(_eng, type, window), "queue_model/basic moving average");
+}
+
+// QueueModelBasic::QueueModelBasic (queue_model_basic.cc:7-30) with the
+// carbon_sim.cfg values as defaults (carbon_sim.cfg:376-379).  An unknown type
+// string leaves the queue without a moving average, as createAvgType's NULL does
+// (moving_average.h:184-188).
+void CfgView::basicMovingAverage(int32_t* type, uint32_t* window) const
+{
+   *type = GNOC_MOVING_AVG_NONE;
+   *window = 1;
+   if (!getBool("queue_model/basic/moving_avg_enabled", true)) return;
+   const std::string t = getString("queue_model/basic/moving_avg_type", "arithmetic_mean");
+   *type = t == "arithmetic_mean" ? GNOC_MOVING_AVG_ARITHMETIC_MEAN
+         : t == "geometric_mean"  ? GNOC_MOVING_AVG_GEOMETRIC_MEAN
+         : t == "median"          ? GNOC_MOVING_AVG_MEDIAN : GNOC_MOVING_AVG_NONE;
+   *window = (uint32_t) getInt("queue_model/basic/moving_avg_window_size", 64);
 }
 
 NetworkModelEMeshHopByHopHIP::NetworkModelEMeshHopByHopHIP(const gnoc_config& cfg) : _cfg(cfg)
 {
-   if (_cfg.queue_type == -2)
-      throw NetworkModelError(GNOC_EUNSUPPORTED, "queue_model/basic with moving_avg_enabled is not implemented");
    if (_cfg.queue_type < 0)
       throw NetworkModelError(GNOC_EINVAL, "queue_model/type: unrecognized queue model");   // queue_model.cc:33-36
    const int rc = gnoc_create(&_cfg, &_eng);

@@ -58,6 +58,8 @@ public:
    std::string getString(const std::string& key, const std::string& dflt) const;
    // gnoc_config for general/total_cores tiles, as NetworkModelEMeshHopByHop's ctor reads it
    gnoc_config toEngineConfig() const;
+   // queue_model/basic/moving_avg_* -> GNOC_MOVING_AVG_* and window size
+   void basicMovingAverage(int32_t* type, uint32_t* window) const;
 
 private:
    std::map<std::string, std::string> _kv;

@@ -58,11 +58,19 @@ extern "C" {
  *                 tree for max_list_size >= 2, with or without interleaving (an
  *                 in-order request never fits an earlier gap); max_list_size and
  *                 analytical_model_enabled are read from queue_model/history_list
- * basic with a moving average (carbon_sim.cfg:376-379) returns GNOC_EUNSUPPORTED
- * at the plug-in: its reference time is a running FP64 window mean. */
+ * basic with a moving average (carbon_sim.cfg:376-379, the cfg's default for
+ * basic) is set with gnoc_set_basic_moving_average and runs on engine path 3:
+ * its reference time is a running FP64 window mean, one serial walk per queue. */
 #define GNOC_QUEUE_HISTORY_TREE 0
 #define GNOC_QUEUE_BASIC        1
 #define GNOC_QUEUE_HISTORY_LIST 2
+
+/* queue_model/basic/moving_avg_type, MovingAverage<T>::createAvgType
+ * (common/misc/moving_average.h:175-189); NONE = moving_avg_enabled false */
+#define GNOC_MOVING_AVG_NONE            0
+#define GNOC_MOVING_AVG_ARITHMETIC_MEAN 1
+#define GNOC_MOVING_AVG_GEOMETRIC_MEAN  2
+#define GNOC_MOVING_AVG_MEDIAN          3
 
 /* per-packet flags */
 #define GNOC_PKT_UNMODELED  0x1u   /* NetworkModel::isModelEnabled() == false
@@ -128,7 +136,8 @@ typedef struct gnoc_summary
    uint64_t records;            /* hop records materialised (injection + mesh)          */
    uint64_t mg1_uses;           /* requests served by the M/G/1 fallback                */
    uint32_t levels;             /* dependency levels executed                           */
-   uint32_t engine_path;        /* 0 whole-port streams, 1 chunked look-back, 2 closed form */
+   uint32_t engine_path;        /* 0 whole-port streams, 1 chunked look-back, 2 closed form,
+                                   3 serial moving-average queues */
    double   last_run_ms;        /* device time of the last gnoc_run (HIP events)        */
 } gnoc_summary;
 
@@ -138,6 +147,17 @@ typedef struct gnoc_summary
  * Validates what the reference asserts: N == W*H (:56-58, :309-320), the link
  * delay identity (:126), queue type (queue_model.cc:33-36). */
 int gnoc_create(const gnoc_config *cfg, gnoc_engine **out);
+
+/* Replaces the moving-average part of QueueModelBasic's constructor
+ * (queue_model_basic.cc:7-30: queue_model/basic/moving_avg_enabled, _type,
+ * _window_size).  Every basic queue of the engine then computes its reference
+ * time as MovingAverage::compute(packet time) (queue_model_basic.cc:38-46).
+ * Requires queue_type GNOC_QUEUE_BASIC; window_size in [1, 65536] (the
+ * reference divides by zero at 0).  GNOC_MOVING_AVG_GEOMETRIC_MEAN returns
+ * GNOC_EUNSUPPORTED: its pow() chain is not bit-reproducible against glibc.  Single unsharded mesh engines only
+ * (GNOC_EUNSUPPORTED for sharded, sweep and hop-counter engines and, at
+ * gnoc_run, for broadcast packets).  Takes effect at the next gnoc_run. */
+int gnoc_set_basic_moving_average(gnoc_engine *eng, int32_t type, uint32_t window_size);
 
 /* Replaces the stream of Network::netSend/forwardPacket calls
  * (network.cc:174-262): hands the engine one batch.  Host pointers; copied. */

@@ -88,6 +88,12 @@ typedef struct
    /* QueueModelMG1 state, queue_model_m_g_1.cc:8-12 */
    double s2, s1;
    uint64_t narr, newest;
+   /* MovingAverage<UInt64> of QueueModelBasic (moving_average.h), ma_type 0 = none */
+   int ma_type;           /* ORC_MA_*                                      */
+   uint32_t ma_max;       /* _max_window_size                              */
+   uint64_t *ma_list;     /* _num_list, _max_window_size + 1 entries       */
+   uint32_t ma_front, ma_back; /* ModuloNum(_max_window_size + 1) values    */
+   double ma_mean;        /* _arithmetic_mean (0.0) / _geometric_mean (1.0) */
    /* counters */
    uint64_t mg1_uses;     /* _total_requests_using_analytical_model        */
    uint64_t total_requests, util_cycles, last_request_time; /* queue_model.cc:40-53 */
@@ -117,6 +123,71 @@ ORC_EXPORT orc_queue *orc_queue_create_type(int type, int max_list_size, int ana
    return q;
 }
 
+/* MovingAverage<T>::createAvgType, moving_average.h:175-189 (include/gnoc.h GNOC_MOVING_AVG_*) */
+enum { ORC_MA_NONE = 0, ORC_MA_ARITHMETIC_MEAN = 1, ORC_MA_GEOMETRIC_MEAN = 2, ORC_MA_MEDIAN = 3 };
+
+/* QueueModelBasic with queue_model/basic/moving_avg_enabled (queue_model_basic.cc:7-30):
+ * attach a moving average of type ma_type over max_window_size numbers. */
+ORC_EXPORT int orc_queue_set_moving_avg(orc_queue *q, int ma_type, uint32_t max_window_size)
+{
+   if (!q || q->type != ORC_Q_BASIC || ma_type < ORC_MA_NONE || ma_type > ORC_MA_MEDIAN) return -1;
+   if (ma_type != ORC_MA_NONE && max_window_size < 1) return -1;   /* window 0 divides by zero */
+   free(q->ma_list);
+   q->ma_list = NULL;
+   q->ma_type = ma_type;
+   if (ma_type == ORC_MA_NONE) return 0;
+   q->ma_max = max_window_size;
+   q->ma_list = (uint64_t *) calloc((size_t) max_window_size + 1, sizeof(uint64_t));   /* :44-50 */
+   q->ma_front = q->ma_back = 0;
+   q->ma_mean = (ma_type == ORC_MA_GEOMETRIC_MEAN) ? 1.0 : 0.0;   /* :88, :122 */
+   return 0;
+}
+
+/* MovingAverage<T>::addToWindow, moving_average.h:57-66 (ModuloNum arithmetic, modulo_num.cc) */
+static void ma_add(orc_queue *q, uint64_t x)
+{
+   const uint32_t M = q->ma_max + 1;
+   q->ma_list[q->ma_back] = x;
+   q->ma_back = (q->ma_back + 1) % M;
+   if (q->ma_back == q->ma_front) q->ma_front = (q->ma_front + 1) % M;
+}
+
+/* MovingArithmeticMean / MovingGeometricMean / MovingMedian ::compute,
+ * moving_average.h:90-110, 124-145, 153-162 */
+ORC_EXPORT uint64_t orc_ma_compute(orc_queue *q, uint64_t x)
+{
+   const uint32_t M = q->ma_max + 1;
+   const uint32_t cw = (q->ma_back >= q->ma_front) ? q->ma_back - q->ma_front : q->ma_back + M - q->ma_front;
+   if (q->ma_type == ORC_MA_MEDIAN)
+   {
+      ma_add(q, x);
+      const uint32_t w = (q->ma_back >= q->ma_front) ? q->ma_back - q->ma_front : q->ma_back + M - q->ma_front;
+      return q->ma_list[(q->ma_front + (w / 2) % M) % M];
+   }
+   if (q->ma_type == ORC_MA_ARITHMETIC_MEAN)
+   {
+      if (cw == q->ma_max)
+      {
+         const uint64_t old = q->ma_list[q->ma_front];
+         q->ma_mean += (((double) x / (double) cw) - ((double) old / (double) cw));
+      }
+      else
+         q->ma_mean = (q->ma_mean * (double) cw + (double) x) / (double) (cw + 1);
+   }
+   else
+   {
+      if (cw == q->ma_max)
+      {
+         const uint64_t old = q->ma_list[q->ma_front];
+         q->ma_mean *= (pow((double) x, (1.0 / (double) cw)) / pow((double) old, (1.0 / (double) cw)));
+      }
+      else
+         q->ma_mean = pow(pow(q->ma_mean, (double) cw) * (double) x, (1.0 / (double) (cw + 1)));
+   }
+   ma_add(q, x);
+   return (uint64_t) q->ma_mean;
+}
+
 ORC_EXPORT orc_queue *orc_queue_create(int max_list_size, int analytical, uint64_t min_proc)
 {
    return orc_queue_create_type(ORC_Q_HISTORY_TREE, max_list_size, analytical, 0, min_proc);
@@ -125,6 +196,7 @@ ORC_EXPORT orc_queue *orc_queue_create(int max_list_size, int analytical, uint64
 ORC_EXPORT void orc_queue_destroy(orc_queue *q)
 {
    if (!q) return;
+   free(q->ma_list);
    free(q->iv);
    free(q);
 }
@@ -286,10 +358,11 @@ static uint64_t hl_queue_delay(orc_queue *q, uint64_t t, uint64_t p)
    return d;
 }
 
-/* QueueModelBasic::computeQueueDelay without moving average, queue_model_basic.cc:35-61 */
+/* QueueModelBasic::computeQueueDelay, queue_model_basic.cc:35-61: the reference
+ * time is the packet time, or the moving average's value with it added (:38-46) */
 static uint64_t basic_queue_delay(orc_queue *q, uint64_t t, uint64_t p)
 {
-   const uint64_t ref_time = t;
+   const uint64_t ref_time = q->ma_type ? orc_ma_compute(q, t) : t;
    const uint64_t d = (q->queue_time > ref_time) ? (q->queue_time - ref_time) : 0;
    q->queue_time = ((q->queue_time > ref_time) ? q->queue_time : ref_time) + p;
    util_update(q, ref_time, p, d);
@@ -427,6 +500,18 @@ static heap_ent heap_pop(heap_t *h)
  * one row of W*H receipts per broadcast, in trace order, column = receiving
  * tile.  A broadcast's per-packet entries are those of its latest receipt
  * (lowest tile on ties). */
+/* queue_model/basic/moving_avg_{enabled,type,window_size} for the next orc_run
+ * calls (ORC_MA_NONE = moving_avg_enabled false) */
+static int g_ma_type = ORC_MA_NONE;
+static uint32_t g_ma_window = 1;
+ORC_EXPORT int orc_set_basic_moving_avg(int ma_type, uint32_t max_window_size)
+{
+   if (ma_type < ORC_MA_NONE || ma_type > ORC_MA_MEDIAN || (ma_type && max_window_size < 1)) return -1;
+   g_ma_type = ma_type;
+   g_ma_window = max_window_size;
+   return 0;
+}
+
 ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
                        uint64_t router_delay, uint64_t link_delay, double frequency,
                        int contention_enabled, int queue_type, int interleaving, int analytical_enabled,
@@ -467,6 +552,7 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
       {
          q[p] = orc_queue_create_type(queue_type, max_list_size, analytical_enabled, interleaving, 1);
          if (!q[p]) return -1;
+         if (queue_type == ORC_Q_BASIC && orc_queue_set_moving_avg(q[p], g_ma_type, g_ma_window)) return -1;
       }
    }
    memset(port_sum_delay, 0, nports * sizeof(uint64_t));

@@ -54,6 +54,10 @@ def lib() -> ctypes.CDLL:
         L.orc_time_to_cycles.argtypes = [u64, ctypes.c_double]
         L.orc_queue_create_type.restype = vp
         L.orc_queue_create_type.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, u64]
+        L.orc_set_basic_moving_avg.argtypes = [ctypes.c_int, ctypes.c_uint32]
+        L.orc_queue_set_moving_avg.argtypes = [vp, ctypes.c_int, ctypes.c_uint32]
+        L.orc_ma_compute.restype = u64
+        L.orc_ma_compute.argtypes = [vp, u64]
         L.orc_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u64, u64, ctypes.c_double, ctypes.c_int,
                               ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t] + [vp] * 15
         _orc = L
@@ -78,6 +82,12 @@ def ref_lib() -> ctypes.CDLL | None:
         L.ref_queue_size.argtypes = [vp]
         L.ref_queue_destroy.argtypes = [vp]
         L.ref_queue_destroy.restype = None
+        L.ref_ma_create.restype = vp
+        L.ref_ma_create.argtypes = [ctypes.c_int, ctypes.c_uint32]
+        L.ref_ma_compute.restype = u64
+        L.ref_ma_compute.argtypes = [vp, u64]
+        L.ref_ma_destroy.argtypes = [vp]
+        L.ref_ma_destroy.restype = None
         L.ref_lat_to_ps.restype = u64
         L.ref_lat_to_ps.argtypes = [u64, ctypes.c_double]
         L.ref_time_to_cycles.restype = u64
@@ -97,6 +107,15 @@ class Queue:
         self.h = self.L.orc_queue_create_type(kind, max_list_size, int(analytical), int(interleaving), min_proc)
         if not self.h:
             raise ValueError("invalid queue model parameters")
+
+    def set_moving_avg(self, ma_type: int, window: int) -> None:
+        """QueueModelBasic with moving_avg_enabled (queue_model_basic.cc:7-30)."""
+        if self.L.orc_queue_set_moving_avg(self.h, ma_type, window):
+            raise ValueError("invalid moving average")
+
+    def moving_avg(self, x: int) -> int:
+        """MovingAverage::compute on the attached average alone (no queue update)."""
+        return int(self.L.orc_ma_compute(self.h, x))
 
     def compute(self, t: int, p: int) -> int:
         return int(self.L.orc_queue_compute(self.h, t, p))
@@ -162,12 +181,16 @@ def run(cfg, tr) -> OracleResult:
     ps, pc, pm, pf, pl = (np.zeros(npt, np.uint64) for _ in range(5))
     nb = int(np.count_nonzero(flags & 2))
     bf, bz = (np.zeros((nb, W * H), np.uint64) for _ in range(2))
+    ma = int(getattr(cfg, "moving_avg_type", 0)) if int(getattr(cfg, "queue_type", 0)) == 1 else 0
+    if L.orc_set_basic_moving_avg(ma, int(getattr(cfg, "moving_avg_window", 1)) if ma else 1):
+        raise ValueError("invalid moving average")
     rc = L.orc_run(W, H, cfg.flit_width, cfg.router_delay, cfg.link_delay, cfg.frequency_ghz,
                    int(cfg.contention_enabled), int(getattr(cfg, "queue_type", 0)),
                    int(getattr(cfg, "interleaving_enabled", True)), int(cfg.analytical_enabled), cfg.max_list_size, n,
                    inj.ctypes.data, src.ctypes.data, dst.ctypes.data, bits.ctypes.data, flags.ctypes.data,
                    fin.ctypes.data, zl.ctypes.data, ct.ctypes.data, ps.ctypes.data, pc.ctypes.data, pm.ctypes.data,
                    pf.ctypes.data, pl.ctypes.data, bf.ctypes.data if nb else None, bz.ctypes.data if nb else None)
+    L.orc_set_basic_moving_avg(0, 1)
     if rc:
         raise ValueError(f"oracle rejected input (rc={rc})")
     return OracleResult(fin, zl, ct, ps, pc, pm, pf, pl, bf, bz)

@@ -5,6 +5,7 @@
 //   common/misc/interval_tree.cc                          (the AVL free-interval tree)
 //   common/shared_models/queue_models/queue_model_m_g_1.cc (the FP64 M/G/1 model)
 //   common/misc/time_types.h                              (ps <-> cycle conversions)
+//   common/misc/moving_average.h + modulo_num.cc          (QueueModelBasic's moving averages)
 // Those three compile with the reference's real headers and -DNDEBUG; nothing
 // is stubbed.  queue_model_history_tree.cc itself cannot be compiled here (its
 // includes reach common/config/section.hpp -> boost/shared_ptr.hpp, absent), so
@@ -16,7 +17,10 @@
 #include <stdint.h>
 #include <utility>
 
+#include <string>
+
 #include "interval_tree.h"
+#include "moving_average.h"
 #include "queue_model_m_g_1.h"
 #include "time_types.h"
 
@@ -123,6 +127,23 @@ __attribute__((visibility("default"))) void ref_queue_destroy(void* vq)
    delete q->tree;
    delete q;
 }
+
+// The real MovingAverage<UInt64>::createAvgType / compute (moving_average.h),
+// as QueueModelBasic builds it (queue_model_basic.cc:27-30, :38-46).
+// type: 1 arithmetic_mean, 2 geometric_mean, 3 median (include/gnoc.h).
+__attribute__((visibility("default"))) void* ref_ma_create(int type, uint32_t window)
+{
+   static const char* const names[] = { "", "arithmetic_mean", "geometric_mean", "median" };
+   if (type < 1 || type > 3) return 0;
+   return MovingAverage<UInt64>::createAvgType(std::string(names[type]), window);
+}
+
+__attribute__((visibility("default"))) uint64_t ref_ma_compute(void* m, uint64_t x)
+{
+   return ((MovingAverage<UInt64>*) m)->compute(x);
+}
+
+__attribute__((visibility("default"))) void ref_ma_destroy(void* m) { delete (MovingAverage<UInt64>*) m; }
 
 // Real Latency::toPicosec / Time::toCycles (time_types.h:81-109).
 __attribute__((visibility("default"))) uint64_t ref_lat_to_ps(uint64_t cycles, double f)

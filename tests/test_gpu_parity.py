@@ -285,3 +285,58 @@ def test_emesh_hop_counter_model(N, R, f):
     ref = oracle.run_hop_counter(cfg, tr)
     for k in ("final_ps", "zero_load_ps", "contention_ps"):
         assert np.array_equal(getattr(got, k), getattr(ref, k)), k
+
+
+@pytest.mark.parametrize("ma,w", [(gnoc.MOVING_AVG_ARITHMETIC_MEAN, 64), (gnoc.MOVING_AVG_ARITHMETIC_MEAN, 1),
+                                  (gnoc.MOVING_AVG_ARITHMETIC_MEAN, 5), (gnoc.MOVING_AVG_MEDIAN, 64),
+                                  (gnoc.MOVING_AVG_MEDIAN, 4), (gnoc.MOVING_AVG_MEDIAN, 1)])
+def test_basic_moving_average(ma, w):
+    """QueueModelBasic with moving_avg_enabled (queue_model_basic.cc:7-61,
+    moving_average.h; carbon_sim.cfg:376-379 default = arithmetic_mean over 64):
+    engine path 3 bit-exact against the oracle, whose moving averages are pinned
+    against the reference's own moving_average.h (tests/test_oracle.py)."""
+    cfg = gnoc.EngineConfig(num_tiles=64, queue_type=gnoc.QUEUE_BASIC, moving_avg_type=ma, moving_avg_window=w)
+    tr = random_trace(20000, 8, 8, seed=w + 7 * ma, max_cycle=2000, burst0=300, self_frac=0.03, unmodeled_frac=0.03,
+                      bits_choices=[72, 576, 1088])
+    got, ref = run_both(cfg, tr)
+    assert got.summary["engine_path"] == 3
+    assert_same(got, ref)
+
+
+@pytest.mark.parametrize("W,H,f,load", [(32, 32, 1.0, 0.005), (5, 3, 0.9, 0.05), (1, 6, 1.0, 0.05), (6, 1, 1.5, 0.05)])
+def test_basic_moving_average_meshes(W, H, f, load):
+    """Moving-average basic queues on a 32x32 synthetic batch (configs[1]'s
+    traffic, 100 packets per tile), odd and one-wide meshes and f != 1 GHz."""
+    cfg = gnoc.EngineConfig(num_tiles=W * H, mesh_width=W, mesh_height=H, frequency_ghz=f,
+                            queue_type=gnoc.QUEUE_BASIC, moving_avg_type=gnoc.MOVING_AVG_ARITHMETIC_MEAN)
+    if W == H:
+        tr = gnoc.synthetic_trace(W, H, load, 100, seed=5)
+    else:
+        tr = random_trace(6000, W, H, seed=W * 10 + H, max_cycle=1500, burst0=50, frequency_ghz=f,
+                          ps_jitter=True)
+    got, ref = run_both(cfg, tr)
+    assert got.summary["engine_path"] == 3
+    assert_same(got, ref)
+
+
+def test_basic_moving_average_refusals():
+    """Broadcast batches, sharding, the geometric mean (pow is not bit-reproducible
+    against glibc) and non-basic queues are refused, not approximated."""
+    with pytest.raises(gnoc.GnocError) as ex:
+        gnoc.Engine(gnoc.EngineConfig(num_tiles=16, queue_type=gnoc.QUEUE_BASIC,
+                                      moving_avg_type=gnoc.MOVING_AVG_GEOMETRIC_MEAN))
+    assert ex.value.code == -5
+    cfg = gnoc.EngineConfig(num_tiles=16, queue_type=gnoc.QUEUE_BASIC, moving_avg_type=gnoc.MOVING_AVG_MEDIAN)
+    eng = gnoc.Engine(cfg)
+    tr = random_trace(200, 4, 4, seed=1, bcast_frac=0.1)
+    eng.submit(tr)
+    with pytest.raises(gnoc.GnocError) as ex:
+        eng.run()
+    assert ex.value.code == -5
+    with pytest.raises(gnoc.GnocError) as ex:
+        eng._check(eng.lib.gnoc_shard(eng._h, 0, 2))
+    assert ex.value.code == -5
+    eng.close()
+    with pytest.raises(gnoc.GnocError) as ex:
+        gnoc.Engine(gnoc.EngineConfig(num_tiles=16, moving_avg_type=gnoc.MOVING_AVG_MEDIAN))
+    assert ex.value.code == -1

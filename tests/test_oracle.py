@@ -130,6 +130,50 @@ def test_basic_is_the_fifo_recurrence():
         assert qb.mg1_uses == 0
 
 
+@pytest.mark.parametrize("ma", [1, 2, 3])
+@pytest.mark.parametrize("w", [1, 2, 5, 64, 100])
+def test_moving_average_matches_reference_source(ma, w):
+    """MovingAverage<UInt64>::compute (moving_average.h, arithmetic / geometric /
+    median) restated in the oracle == the reference's own header compiled in
+    oracle/_ref, number for number, over cycle streams with repeats, steps and gaps."""
+    r = oracle.ref_lib()
+    if r is None:
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    rng = np.random.default_rng(ma * 1000 + w)
+    steps = rng.choice([0, 0, 1, 2, 3, 9, 40, 1000, 123457], size=20000)
+    xs = (np.cumsum(steps) + int(rng.integers(1, 50))).tolist()
+    q = oracle.Queue(kind=1)
+    q.set_moving_avg(ma, w)
+    h = r.ref_ma_create(ma, w)
+    try:
+        got = [q.moving_avg(x) for x in xs]
+        want = [int(r.ref_ma_compute(h, x)) for x in xs]
+    finally:
+        r.ref_ma_destroy(h)
+    assert got == want
+
+
+def test_basic_with_moving_average_queue():
+    """QueueModelBasic::computeQueueDelay with a moving average
+    (queue_model_basic.cc:35-61): ref = MA(t); d = max(Q - ref, 0);
+    Q = max(Q, ref) + p -- against a direct restatement over the reference's MA."""
+    r = oracle.ref_lib()
+    if r is None:
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    for ma, w in ((1, 64), (3, 8), (2, 4)):
+        t, p = _sorted_stream(ma + w)
+        qb = oracle.Queue(kind=1)
+        qb.set_moving_avg(ma, w)
+        h = r.ref_ma_create(ma, w)
+        Q, want = 0, []
+        for a, b in zip(t.tolist(), p.tolist()):
+            ref = int(r.ref_ma_compute(h, a))
+            want.append(max(Q - ref, 0))
+            Q = max(Q, ref) + b
+        r.ref_ma_destroy(h)
+        assert [qb.compute(int(a), int(b)) for a, b in zip(t, p)] == want
+
+
 def test_history_list_out_of_order_uses_gaps():
     """Out of order (not produced on this path, but the restatement covers it):
     a request fits an earlier gap, and with interleaving spans gaps."""
