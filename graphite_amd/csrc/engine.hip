@@ -143,7 +143,7 @@ struct gnoc_engine
    // QueueModelBasic with a moving average (gnoc_set_basic_moving_average, serial.hip)
    int ma_type = 0;
    uint32_t ma_window = 1;
-   DevBuf ma_t, ma_key, ma_val, ma_key2, ma_val2, ma_lo, ma_hi, ma_ring, ma_tmp;
+   DevBuf ma_t, ma_key, ma_val, ma_key2, ma_val2, ma_lo, ma_hi, ma_d, ma_tmp;
 
    // kernel profiling (gnoc_set_profiling)
    bool prof = false;
@@ -1211,7 +1211,7 @@ static int run_ma(gnoc_engine* e)
    GNOC_HIP(e, e->ma_val2.ensure(n * 4 + 4));
    GNOC_HIP(e, e->ma_lo.ensure((size_t) maxloc * 4));
    GNOC_HIP(e, e->ma_hi.ensure((size_t) maxloc * 4));
-   GNOC_HIP(e, e->ma_ring.ensure((size_t) maxloc * (e->ma_window + 1) * 8));
+   GNOC_HIP(e, e->ma_d.ensure(n * 8 + 8));
    GNOC_HIP(e, e->counters.ensure(64));
    for (DevBuf* b : { &e->port_sum, &e->port_cnt, &e->port_mg1, &e->port_flit, &e->port_last })
    {
@@ -1253,13 +1253,27 @@ static int run_ma(gnoc_engine* e)
          hipLaunchKernelGGL(k_ma_bounds, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid,
                             (const uint64_t*) e->ma_key2.as<uint64_t>(), e->ma_lo.as<uint32_t>(), e->ma_hi.as<uint32_t>());
          GNOC_HIP(e, hipGetLastError());
-         hipLaunchKernelGGL(k_ma_walk, dim3((nloc + 63) / 64), dim3(64), 0, s, nloc,
-                            e->d_lvl_ports.as<uint32_t>() + k0, e->ma_type, e->ma_window, c.flit_width, c.f, c.rl_ps,
+         // the sort's inputs are free now: request cycles into ma_key, flits into ma_val
+         hipLaunchKernelGGL(k_ma_gather, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid, c.flit_width, c.f,
                             (const uint64_t*) e->ma_key2.as<uint64_t>(), (const uint32_t*) e->ma_val2.as<uint32_t>(),
-                            (const uint32_t*) e->ma_lo.as<uint32_t>(), (const uint32_t*) e->ma_hi.as<uint32_t>(),
-                            e->d_bits, e->ma_ring.as<uint64_t>(), e->ma_t.as<uint64_t>(), e->final_ps.as<uint64_t>(),
-                            e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), e->port_sum.as<uint64_t>(),
-                            e->port_cnt.as<uint64_t>(), e->port_flit.as<uint64_t>(), e->port_last.as<uint64_t>());
+                            e->d_bits, e->ma_key.as<uint64_t>(), e->ma_val.as<uint32_t>());
+         GNOC_HIP(e, hipGetLastError());
+#define GNOC_MA_WALK(MT)                                                                                     \
+   hipLaunchKernelGGL(k_ma_walk<MT>, dim3((nloc + 63) / 64), dim3(64), 0, s, nloc,                            \
+                      e->d_lvl_ports.as<uint32_t>() + k0, e->ma_window, (const uint64_t*) e->ma_key.as<uint64_t>(), \
+                      (const uint32_t*) e->ma_val.as<uint32_t>(), (const uint32_t*) e->ma_lo.as<uint32_t>(),      \
+                      (const uint32_t*) e->ma_hi.as<uint32_t>(), e->ma_d.as<uint64_t>(), e->port_sum.as<uint64_t>(), \
+                      e->port_cnt.as<uint64_t>(), e->port_flit.as<uint64_t>(), e->port_last.as<uint64_t>())
+         if (e->ma_type == MA_MEDIAN) GNOC_MA_WALK(MA_MEDIAN);
+         else GNOC_MA_WALK(MA_ARITHMETIC);   // the geometric mean is refused at gnoc_set_basic_moving_average
+#undef GNOC_MA_WALK
+         GNOC_HIP(e, hipGetLastError());
+         hipLaunchKernelGGL(k_ma_apply, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid,
+                            (const uint32_t*) e->d_lvl_ports.as<uint32_t>() + k0, c.f, c.rl_ps,
+                            (const uint64_t*) e->ma_key2.as<uint64_t>(), (const uint32_t*) e->ma_val2.as<uint32_t>(),
+                            (const uint32_t*) e->ma_val.as<uint32_t>(), (const uint64_t*) e->ma_d.as<uint64_t>(),
+                            e->ma_t.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
+                            e->cont.as<uint64_t>());
          GNOC_HIP(e, hipGetLastError());
       }
    }

@@ -16,9 +16,10 @@
 //                           one entry per packet (non-visitors get the max key)
 //               radix sort  stable, bits [0, 49 + level bits) (ties: packet id)
 //               k_ma_bounds first / last entry of each port
+//               k_ma_gather cycles and flits of each sorted request
 //               k_ma_walk   one thread per port: the reference's arithmetic, in
-//                           order, updating each packet's time / contention /
-//                           zero-load and the port's counters
+//                           order -> queue delay per request, port counters
+//               k_ma_apply  each packet's time / contention / zero-load
 //
 // The geometric mean's branch is kept for completeness but refused by
 // gnoc_set_basic_moving_average: its pow() chain is not bit-reproducible
@@ -126,91 +127,157 @@ __global__ void k_ma_bounds(uint64_t n, uint64_t invalid, const uint64_t* __rest
    }
 }
 
+// Per sorted request j: the queue's input in cycles and the packet's flit count
+// (coalesced; takes every load off the serial walk's dependency chain).
+__global__ void k_ma_gather(uint64_t n, uint64_t invalid, uint32_t flit_width, double f,
+                            const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                            const uint32_t* __restrict__ bits, uint64_t* __restrict__ tcs, uint32_t* __restrict__ Fs)
+{
+   for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < n; j += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const uint64_t k = key[j];
+      if (k == invalid) continue;
+      tcs[j] = cyc_of<false>(k & MA_T_MASK, f);   // Time::toCycles, time_types.h:104-109
+      Fs[j] = ma_flits(bits[val[j]], flit_width);
+   }
+}
+
 // One queue: QueueModelBasic::computeQueueDelay (queue_model_basic.cc:35-61) with
 // MovingAverage<UInt64>::compute (moving_average.h:90-110 arithmetic, 124-145
-// geometric, 153-162 median) and RouterModel / Hop bookkeeping per request
-// (router_model.cc:70-108, network_model.cc:556-563, :142-150).
-__global__ void k_ma_walk(uint32_t nloc, const uint32_t* __restrict__ ports, int ma_type, uint32_t ma_max,
-                          uint32_t flit_width, double f, uint64_t rl_ps, const uint64_t* __restrict__ key,
-                          const uint32_t* __restrict__ val, const uint32_t* __restrict__ lo,
-                          const uint32_t* __restrict__ hi, const uint32_t* __restrict__ bits, uint64_t* __restrict__ ring,
-                          uint64_t* __restrict__ ptime, uint64_t* __restrict__ fin, uint64_t* __restrict__ zl,
-                          uint64_t* __restrict__ cont, uint64_t* __restrict__ port_sum, uint64_t* __restrict__ port_cnt,
-                          uint64_t* __restrict__ port_flit, uint64_t* __restrict__ port_last)
+// geometric, 153-162 median), one thread per port over its sorted requests.
+// The window is the port's last `ma_max` inputs, i.e. the previous entries of
+// the same sorted segment, so the ring buffer's reads become plain indexed
+// loads: the arithmetic mean's evicted number is entry j - max, the median the
+// entry front + size / 2 of the window after the add.  Loads run one block of
+// MA_B requests ahead of the FP64 chain (registers, double-buffered).
+constexpr int MA_B = 16;
+
+template <int ma_type>
+__global__ void __launch_bounds__(64) k_ma_walk(uint32_t nloc, const uint32_t* __restrict__ ports,
+                                                uint32_t ma_max, const uint64_t* __restrict__ tcs,
+                                                const uint32_t* __restrict__ Fs, const uint32_t* __restrict__ lo,
+                                                const uint32_t* __restrict__ hi, uint64_t* __restrict__ dout,
+                                                uint64_t* __restrict__ port_sum, uint64_t* __restrict__ port_cnt,
+                                                uint64_t* __restrict__ port_flit, uint64_t* __restrict__ port_last)
 {
    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
    if (p >= nloc) return;
    const uint32_t port = ports[p];
-   const uint32_t dir = port % PORTS;
-   const uint32_t M = ma_max + 1;
-   uint64_t* list = ring + (size_t) p * M;
-   uint32_t front = 0, back = 0;
+   const uint32_t j0 = lo[p], j1 = hi[p];
    double mean = ma_type == MA_GEOMETRIC ? 1.0 : 0.0;
    uint64_t Q = 0, sum = 0, cnt = 0, flits = 0, last = 0;
-   const uint32_t j0 = lo[p], j1 = hi[p];
-   const uint64_t hop_ps = dir == P_INJ ? ps_of<false>(0, f) : rl_ps;   // injection router: delay 0
-   for (uint32_t j = j0; j < j1; j++)
-   {
-      const uint64_t t = key[j] & MA_T_MASK;
-      const uint32_t id = val[j];
-      const uint32_t F = ma_flits(bits[id], flit_width);
-      const uint64_t tc = cyc_of<false>(t, f);
-      // MovingAverage::compute
-      const uint32_t cw = back >= front ? back - front : back + M - front;
-      uint64_t ref;
+   uint64_t cx[MA_B], co[MA_B], nx[MA_B], no[MA_B];
+   uint32_t cf[MA_B], nf[MA_B];
+   // entry j's window partner: evicted number (arithmetic / geometric) or median (median)
+   auto other = [&](uint32_t j) -> uint64_t {
+      const uint32_t seen = j - j0;   // requests before j
       if (ma_type == MA_MEDIAN)
       {
-         list[back] = tc;
-         back = (back + 1) % M;
-         if (back == front) front = (front + 1) % M;
-         const uint32_t w = back >= front ? back - front : back + M - front;
-         ref = list[(front + (w / 2) % M) % M];
+         const uint32_t w = seen + 1 < ma_max ? seen + 1 : ma_max;
+         return tcs[j + 1 - w + w / 2];
       }
-      else
+      return seen >= ma_max ? tcs[j - ma_max] : 0ull;
+   };
+   auto load = [&](uint32_t base, uint64_t* X, uint64_t* O, uint32_t* F) {
+#pragma unroll
+      for (int i = 0; i < MA_B; i++)
       {
-         if (ma_type == MA_ARITHMETIC)
+         const uint32_t j = base + (uint32_t) i;
+         if (j < j1)
          {
-            if (cw == ma_max)
-               mean += (((double) tc / (double) cw) - ((double) list[front] / (double) cw));
-            else
-               mean = (mean * (double) cw + (double) tc) / (double) (cw + 1);
+            X[i] = tcs[j];
+            F[i] = Fs[j];
+            O[i] = other(j);
          }
+      }
+   };
+   load(j0, cx, co, cf);
+   for (uint32_t base = j0; base < j1; base += MA_B)
+   {
+      load(base + MA_B, nx, no, nf);
+#pragma unroll
+      for (int i = 0; i < MA_B; i++)
+      {
+         const uint32_t j = base + (uint32_t) i;
+         if (j >= j1) continue;
+         const uint64_t tc = cx[i];
+         const uint32_t F = cf[i];
+         const uint32_t seen = j - j0;
+         const uint32_t cw = seen < ma_max ? seen : ma_max;   // window size before the add
+         uint64_t ref;
+         if (ma_type == MA_MEDIAN)
+            ref = co[i];
          else
          {
-            if (cw == ma_max)
-               mean *= (pow((double) tc, (1.0 / (double) cw)) / pow((double) list[front], (1.0 / (double) cw)));
+            if (ma_type == MA_ARITHMETIC)
+            {
+               if (cw == ma_max)
+                  mean += (((double) tc / (double) cw) - ((double) co[i] / (double) cw));
+               else
+                  mean = (mean * (double) cw + (double) tc) / (double) (cw + 1);
+            }
             else
-               mean = pow(pow(mean, (double) cw) * (double) tc, (1.0 / (double) (cw + 1)));
+            {
+               if (cw == ma_max)
+                  mean *= (pow((double) tc, (1.0 / (double) cw)) / pow((double) co[i], (1.0 / (double) cw)));
+               else
+                  mean = pow(pow(mean, (double) cw) * (double) tc, (1.0 / (double) (cw + 1)));
+            }
+            ref = (uint64_t) mean;
          }
-         list[back] = tc;
-         back = (back + 1) % M;
-         if (back == front) front = (front + 1) % M;
-         ref = (uint64_t) mean;
+         const uint64_t d = Q > ref ? Q - ref : 0;
+         Q = (Q > ref ? Q : ref) + F;
+         // QueueModel::updateQueueUtilizationCounters(ref, F, d), queue_model.cc:48-53
+         flits += F;
+         last = last > ref + d + F ? last : ref + d + F;
+         sum += d;
+         cnt++;
+         dout[j] = d;
       }
-      const uint64_t d = Q > ref ? Q - ref : 0;
-      Q = (Q > ref ? Q : ref) + F;
-      // QueueModel::updateQueueUtilizationCounters(ref, F, d), queue_model.cc:48-53
-      flits += F;
-      last = last > ref + d + F ? last : ref + d + F;
-      sum += d;
-      cnt++;
-      const uint64_t cps = ps_of<false>(d, f);
-      uint64_t tn = t + cps + hop_ps;
-      zl[id] += hop_ps;
-      cont[id] += cps;
-      if (dir == P_SELF)
+#pragma unroll
+      for (int i = 0; i < MA_B; i++)
       {
-         const uint64_t fps = ps_of<false>(F, f);   // receive serialization, network_model.cc:142-150
-         tn += fps;
-         zl[id] += fps;
-         fin[id] = tn;
+         cx[i] = nx[i];
+         co[i] = no[i];
+         cf[i] = nf[i];
       }
-      ptime[id] = tn;
    }
    port_sum[port] = sum;
    port_cnt[port] = cnt;
    port_flit[port] = flits;
    port_last[port] = last;
+}
+
+// Per request: RouterModel / Hop bookkeeping (router_model.cc:70-108,
+// network_model.cc:556-563) and, at SELF, the receive serialization
+// (network_model.cc:142-150).  Each packet has at most one request per level.
+__global__ void k_ma_apply(uint64_t n, uint64_t invalid, const uint32_t* __restrict__ ports, double f, uint64_t rl_ps,
+                           const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                           const uint32_t* __restrict__ Fs, const uint64_t* __restrict__ dout,
+                           uint64_t* __restrict__ ptime, uint64_t* __restrict__ fin, uint64_t* __restrict__ zl,
+                           uint64_t* __restrict__ cont)
+{
+   for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < n; j += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const uint64_t k = key[j];
+      if (k == invalid) continue;
+      const uint32_t dir = ports[(uint32_t) (k >> MA_T_BITS)] % PORTS;
+      const uint32_t id = val[j];
+      const uint64_t hop_ps = dir == P_INJ ? ps_of<false>(0, f) : rl_ps;   // injection router: delay 0
+      const uint64_t cps = ps_of<false>(dout[j], f);
+      uint64_t tn = (k & MA_T_MASK) + cps + hop_ps;
+      uint64_t z = zl[id] + hop_ps;
+      cont[id] += cps;
+      if (dir == P_SELF)
+      {
+         const uint64_t fps = ps_of<false>(Fs[j], f);
+         tn += fps;
+         z += fps;
+         fin[id] = tn;
+      }
+      zl[id] = z;
+      ptime[id] = tn;
+   }
 }
 
 }  // namespace gnoc
