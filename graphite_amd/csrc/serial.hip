@@ -150,7 +150,7 @@ __global__ void k_ma_gather(uint64_t n, uint64_t invalid, uint32_t flit_width, d
 // loads: the arithmetic mean's evicted number is entry j - max, the median the
 // entry front + size / 2 of the window after the add.  Loads run one block of
 // MA_B requests ahead of the FP64 chain (registers, double-buffered).
-constexpr int MA_B = 16;
+constexpr int MA_B = 32;
 
 template <int ma_type>
 __global__ void __launch_bounds__(64) k_ma_walk(uint32_t nloc, const uint32_t* __restrict__ ports,
@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(64) k_ma_walk(uint32_t nloc, const uint32_t* _
    const uint32_t port = ports[p];
    const uint32_t j0 = lo[p], j1 = hi[p];
    double mean = ma_type == MA_GEOMETRIC ? 1.0 : 0.0;
-   uint64_t Q = 0, sum = 0, cnt = 0, flits = 0, last = 0;
+   uint64_t Q = 0, sum = 0, flits = 0;
    uint64_t cx[MA_B], co[MA_B], nx[MA_B], no[MA_B];
    uint32_t cf[MA_B], nf[MA_B];
    // entry j's window partner: evicted number (arithmetic / geometric) or median (median)
@@ -225,13 +225,14 @@ __global__ void __launch_bounds__(64) k_ma_walk(uint32_t nloc, const uint32_t* _
             }
             ref = (uint64_t) mean;
          }
-         const uint64_t d = Q > ref ? Q - ref : 0;
-         Q = (Q > ref ? Q : ref) + F;
-         // QueueModel::updateQueueUtilizationCounters(ref, F, d), queue_model.cc:48-53
+         // d = max(Q - ref, 0); Q = max(Q, ref) + F.  QueueModel's
+         // _last_request_time = max(ref + d + F) = max over requests of the new Q,
+         // which never decreases: the final Q (queue_model.cc:48-53)
+         const uint64_t top = Q > ref ? Q : ref;
+         const uint64_t d = top - ref;
+         Q = top + F;
          flits += F;
-         last = last > ref + d + F ? last : ref + d + F;
          sum += d;
-         cnt++;
          dout[j] = d;
       }
 #pragma unroll
@@ -243,9 +244,9 @@ __global__ void __launch_bounds__(64) k_ma_walk(uint32_t nloc, const uint32_t* _
       }
    }
    port_sum[port] = sum;
-   port_cnt[port] = cnt;
+   port_cnt[port] = j1 - j0;
    port_flit[port] = flits;
-   port_last[port] = last;
+   port_last[port] = Q;
 }
 
 // Per request: RouterModel / Hop bookkeeping (router_model.cc:70-108,
