@@ -1255,14 +1255,17 @@ static int run_ma(gnoc_engine* e)
          GNOC_HIP(e, hipGetLastError());
          // the sort's inputs are free now: request cycles into ma_key, flits into ma_val
          hipLaunchKernelGGL(k_ma_gather, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid, c.flit_width, c.f,
-                            (const uint64_t*) e->ma_key2.as<uint64_t>(), (const uint32_t*) e->ma_val2.as<uint32_t>(),
-                            e->d_bits, e->ma_key.as<uint64_t>(), e->ma_val.as<uint32_t>());
+                            e->ma_type, e->ma_window, (const uint64_t*) e->ma_key2.as<uint64_t>(),
+                            (const uint32_t*) e->ma_val2.as<uint32_t>(), e->d_bits,
+                            (const uint32_t*) e->ma_lo.as<uint32_t>(), e->ma_key.as<uint64_t>(), e->ma_val.as<uint32_t>(),
+                            e->ma_d.as<double>());
          GNOC_HIP(e, hipGetLastError());
 #define GNOC_MA_WALK(MT)                                                                                     \
    hipLaunchKernelGGL(k_ma_walk<MT>, dim3((nloc + 63) / 64), dim3(64), 0, s, nloc,                            \
                       e->d_lvl_ports.as<uint32_t>() + k0, e->ma_window, (const uint64_t*) e->ma_key.as<uint64_t>(), \
                       (const uint32_t*) e->ma_val.as<uint32_t>(), (const uint32_t*) e->ma_lo.as<uint32_t>(),      \
-                      (const uint32_t*) e->ma_hi.as<uint32_t>(), e->ma_d.as<uint64_t>(), e->port_sum.as<uint64_t>(), \
+                      (const uint32_t*) e->ma_hi.as<uint32_t>(), (const double*) e->ma_d.as<double>(),           \
+                      e->ma_d.as<uint64_t>(), e->port_sum.as<uint64_t>(),                                          \
                       e->port_cnt.as<uint64_t>(), e->port_flit.as<uint64_t>(), e->port_last.as<uint64_t>())
          if (e->ma_type == MA_MEDIAN) GNOC_MA_WALK(MA_MEDIAN);
          else GNOC_MA_WALK(MA_ARITHMETIC);   // the geometric mean is refused at gnoc_set_basic_moving_average

@@ -21,9 +21,9 @@
 //                           order -> queue delay per request, port counters
 //               k_ma_apply  each packet's time / contention / zero-load
 //
-// The geometric mean's branch is kept for completeness but refused by
-// gnoc_set_basic_moving_average: its pow() chain is not bit-reproducible
-// against glibc.  Arithmetic mean and median are bit-exact against
+// The geometric mean is refused by gnoc_set_basic_moving_average: its pow()
+// chain is not bit-reproducible against glibc.  Arithmetic mean and median are
+// bit-exact against
 // oracle/gnoc_oracle.c (orc_ma_compute, pinned against the
 // reference's own moving_average.h compiled in oracle/_ref).  This TU is compiled
 // with -ffp-contract=off (no FMA contraction), like the M/G/1 arithmetic.
@@ -129,25 +129,36 @@ __global__ void k_ma_bounds(uint64_t n, uint64_t invalid, const uint64_t* __rest
 
 // Per sorted request j: the queue's input in cycles and the packet's flit count
 // (coalesced; takes every load off the serial walk's dependency chain).
-__global__ void k_ma_gather(uint64_t n, uint64_t invalid, uint32_t flit_width, double f,
+// For the arithmetic mean with a full window, also the increment
+// (x / w) - (old / w) of moving_average.h:97-98: it depends only on the request
+// and the one w places earlier in the port's segment, so its two FP64 divisions
+// leave the serial walk (which then adds it, in order, exactly as the reference).
+__global__ void k_ma_gather(uint64_t n, uint64_t invalid, uint32_t flit_width, double f, int ma_type, uint32_t ma_max,
                             const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
-                            const uint32_t* __restrict__ bits, uint64_t* __restrict__ tcs, uint32_t* __restrict__ Fs)
+                            const uint32_t* __restrict__ bits, const uint32_t* __restrict__ lo,
+                            uint64_t* __restrict__ tcs, uint32_t* __restrict__ Fs, double* __restrict__ delta)
 {
    for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < n; j += (uint64_t) gridDim.x * blockDim.x)
    {
       const uint64_t k = key[j];
       if (k == invalid) continue;
-      tcs[j] = cyc_of<false>(k & MA_T_MASK, f);   // Time::toCycles, time_types.h:104-109
+      const uint64_t tc = cyc_of<false>(k & MA_T_MASK, f);   // Time::toCycles, time_types.h:104-109
+      tcs[j] = tc;
       Fs[j] = ma_flits(bits[val[j]], flit_width);
+      if (ma_type == MA_ARITHMETIC && j - lo[(uint32_t) (k >> MA_T_BITS)] >= ma_max)
+      {
+         const uint64_t old = cyc_of<false>(key[j - ma_max] & MA_T_MASK, f);
+         delta[j] = ((double) tc / (double) ma_max) - ((double) old / (double) ma_max);
+      }
    }
 }
 
 // One queue: QueueModelBasic::computeQueueDelay (queue_model_basic.cc:35-61) with
-// MovingAverage<UInt64>::compute (moving_average.h:90-110 arithmetic, 124-145
-// geometric, 153-162 median), one thread per port over its sorted requests.
+// MovingAverage<UInt64>::compute (moving_average.h:90-110 arithmetic, 153-162
+// median), one thread per port over its sorted requests.
 // The window is the port's last `ma_max` inputs, i.e. the previous entries of
 // the same sorted segment, so the ring buffer's reads become plain indexed
-// loads: the arithmetic mean's evicted number is entry j - max, the median the
+// loads: the arithmetic mean's increment uses entry j - max (k_ma_gather), the median the
 // entry front + size / 2 of the window after the add.  Loads run one block of
 // MA_B requests ahead of the FP64 chain (registers, double-buffered).
 constexpr int MA_B = 32;
@@ -156,7 +167,7 @@ template <int ma_type>
 __global__ void __launch_bounds__(64) k_ma_walk(uint32_t nloc, const uint32_t* __restrict__ ports,
                                                 uint32_t ma_max, const uint64_t* __restrict__ tcs,
                                                 const uint32_t* __restrict__ Fs, const uint32_t* __restrict__ lo,
-                                                const uint32_t* __restrict__ hi, uint64_t* __restrict__ dout,
+                                                const uint32_t* __restrict__ hi, const double* delta, uint64_t* dout,
                                                 uint64_t* __restrict__ port_sum, uint64_t* __restrict__ port_cnt,
                                                 uint64_t* __restrict__ port_flit, uint64_t* __restrict__ port_last)
 {
@@ -164,11 +175,11 @@ __global__ void __launch_bounds__(64) k_ma_walk(uint32_t nloc, const uint32_t* _
    if (p >= nloc) return;
    const uint32_t port = ports[p];
    const uint32_t j0 = lo[p], j1 = hi[p];
-   double mean = ma_type == MA_GEOMETRIC ? 1.0 : 0.0;
+   double mean = 0.0;   // MovingArithmeticMean's _arithmetic_mean(0.0), moving_average.h:88
    uint64_t Q = 0, sum = 0, flits = 0;
    uint64_t cx[MA_B], co[MA_B], nx[MA_B], no[MA_B];
    uint32_t cf[MA_B], nf[MA_B];
-   // entry j's window partner: evicted number (arithmetic / geometric) or median (median)
+   // entry j's window partner: the mean's gathered increment, or the median
    auto other = [&](uint32_t j) -> uint64_t {
       const uint32_t seen = j - j0;   // requests before j
       if (ma_type == MA_MEDIAN)
@@ -176,7 +187,7 @@ __global__ void __launch_bounds__(64) k_ma_walk(uint32_t nloc, const uint32_t* _
          const uint32_t w = seen + 1 < ma_max ? seen + 1 : ma_max;
          return tcs[j + 1 - w + w / 2];
       }
-      return seen >= ma_max ? tcs[j - ma_max] : 0ull;
+      return seen >= ma_max ? __builtin_bit_cast(uint64_t, delta[j]) : 0ull;   // the gathered increment
    };
    auto load = [&](uint32_t base, uint64_t* X, uint64_t* O, uint32_t* F) {
 #pragma unroll
@@ -205,24 +216,15 @@ __global__ void __launch_bounds__(64) k_ma_walk(uint32_t nloc, const uint32_t* _
          const uint32_t seen = j - j0;
          const uint32_t cw = seen < ma_max ? seen : ma_max;   // window size before the add
          uint64_t ref;
-         if (ma_type == MA_MEDIAN)
+         if constexpr (ma_type == MA_MEDIAN)
             ref = co[i];
          else
          {
-            if (ma_type == MA_ARITHMETIC)
-            {
-               if (cw == ma_max)
-                  mean += (((double) tc / (double) cw) - ((double) co[i] / (double) cw));
-               else
-                  mean = (mean * (double) cw + (double) tc) / (double) (cw + 1);
-            }
+            static_assert(ma_type == MA_ARITHMETIC, "the geometric mean is refused (gnoc_set_basic_moving_average)");
+            if (cw == ma_max)
+               mean += __builtin_bit_cast(double, co[i]);   // (tc / cw) - (old / cw), k_ma_gather
             else
-            {
-               if (cw == ma_max)
-                  mean *= (pow((double) tc, (1.0 / (double) cw)) / pow((double) co[i], (1.0 / (double) cw)));
-               else
-                  mean = pow(pow(mean, (double) cw) * (double) tc, (1.0 / (double) (cw + 1)));
-            }
+               mean = (mean * (double) cw + (double) tc) / (double) (cw + 1);
             ref = (uint64_t) mean;
          }
          // d = max(Q - ref, 0); Q = max(Q, ref) + F.  QueueModel's
