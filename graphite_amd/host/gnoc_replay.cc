@@ -2,6 +2,7 @@
 // gnoc_trace_header) through the C++ host model on the GPU.
 //
 //   gnoc_replay TRACE [--results FILE] [--summary TILE|all] [--device D] [--repeat K]
+//               [--moving-avg arithmetic_mean|median:WINDOW]
 //
 // --results writes final/zero-load/contention picoseconds (u64[n] each) then the
 // per-port contention sum, packet count and analytical-request count
@@ -21,10 +22,11 @@ int main(int argc, char** argv)
 {
    if (argc < 2)
    {
-      std::fprintf(stderr, "usage: %s TRACE [--results FILE] [--summary TILE|all] [--device D] [--repeat K]\n", argv[0]);
+      std::fprintf(stderr, "usage: %s TRACE [--results FILE] [--summary TILE|all] [--device D] [--repeat K] "
+                           "[--moving-avg TYPE:WINDOW]\n", argv[0]);
       return 2;
    }
-   std::string results, summary;
+   std::string results, summary, mavg;
    int device = 0, repeat = 1;
    for (int i = 2; i + 1 < argc; i += 2)
    {
@@ -32,6 +34,7 @@ int main(int argc, char** argv)
       else if (!std::strcmp(argv[i], "--summary")) summary = argv[i + 1];
       else if (!std::strcmp(argv[i], "--device")) device = std::atoi(argv[i + 1]);
       else if (!std::strcmp(argv[i], "--repeat")) repeat = std::atoi(argv[i + 1]);
+      else if (!std::strcmp(argv[i], "--moving-avg")) mavg = argv[i + 1];
       else
       {
          std::fprintf(stderr, "unknown option %s\n", argv[i]);
@@ -41,6 +44,16 @@ int main(int argc, char** argv)
    try
    {
       std::unique_ptr<NetworkModelEMeshHopByHopHIP> m(NetworkModelEMeshHopByHopHIP::fromTraceFile(argv[1], device));
+      if (!mavg.empty())
+      {
+         // queue_model/basic/moving_avg_type:moving_avg_window_size (not in the trace header)
+         const size_t c = mavg.find(':');
+         const std::string t = mavg.substr(0, c);
+         const int32_t type = t == "arithmetic_mean" ? GNOC_MOVING_AVG_ARITHMETIC_MEAN
+                            : t == "geometric_mean"  ? GNOC_MOVING_AVG_GEOMETRIC_MEAN
+                            : t == "median"          ? GNOC_MOVING_AVG_MEDIAN : -1;
+         m->setBasicMovingAverage(type, c == std::string::npos ? 64u : (uint32_t) std::atoi(mavg.c_str() + c + 1));
+      }
       double best_ms = 1e30;
       for (int r = 0; r < repeat; r++)
       {

@@ -112,6 +112,11 @@ NetworkModelEMeshHopByHopHIP::NetworkModelEMeshHopByHopHIP(const gnoc_config& cf
 
 NetworkModelEMeshHopByHopHIP::~NetworkModelEMeshHopByHopHIP() { gnoc_destroy(_eng); }
 
+void NetworkModelEMeshHopByHopHIP::setBasicMovingAverage(int32_t type, uint32_t window)
+{
+   check(gnoc_set_basic_moving_average(_eng, type, window), "queue_model/basic moving average");
+}
+
 void NetworkModelEMeshHopByHopHIP::check(int status, const char* what) const
 {
    if (status) throw NetworkModelError(status, std::string(what) + ": " + gnoc_last_error(_eng));

@@ -97,6 +97,9 @@ public:
    void reserve(size_t n);
 
    // Time every hop of every recorded packet (one gnoc_submit + gnoc_run).
+   // queue_model/basic/moving_avg_* on this model's basic queues (GNOC_MOVING_AVG_*;
+   // queue_model_basic.cc:7-30) -- for a replayed trace, whose header has no such keys
+   void setBasicMovingAverage(int32_t type, uint32_t window);
    void run();
 
    // Results of the last run(), indexed by packet id: NetPacket::time,

@@ -34,8 +34,12 @@ def case(name, cfg, tr):
     print(name, len(tr), "mg1", int(r.port_mg1.sum()))
 
 
-def main():
+def main(only=None):
     E = gnoc.EngineConfig
+    global case
+    if only:
+        full = case
+        case = lambda name, cfg, tr: full(name, cfg, tr) if name.startswith(only) else None  # noqa: E731
     case("g_4x4_burst_mg1", E(num_tiles=16), random_trace(1500, 4, 4, seed=1, max_cycle=200, burst0=60))
     case("g_8x8_synthetic_0p05", E(num_tiles=64), gnoc.synthetic_trace(8, 8, 0.05, 60, seed=3))
     case("g_8x8_saturated", E(num_tiles=64), random_trace(4000, 8, 8, seed=2, max_cycle=150, burst0=100))
@@ -52,7 +56,14 @@ def main():
     case("g_4x4_list2", E(num_tiles=16, max_list_size=2), random_trace(1500, 4, 4, seed=9, max_cycle=200, burst0=30))
     case("g_2x4_noanalytical", E(num_tiles=8, analytical_enabled=False),
          random_trace(1000, 2, 4, seed=10, max_cycle=200, burst0=30))
+    # queue_model/basic with its moving average (queue_model_basic.cc, moving_average.h);
+    # the oracle's moving averages are pinned against the reference's header (test_oracle.py)
+    case("g_4x4_basic_ma_arith_w8", E(num_tiles=16, queue_type=1, moving_avg_type=1, moving_avg_window=8),
+         random_trace(1500, 4, 4, seed=11, max_cycle=300, burst0=20, self_frac=0.05, unmodeled_frac=0.05))
+    case("g_4x4_basic_ma_median_w5", E(num_tiles=16, queue_type=1, moving_avg_type=3, moving_avg_window=5),
+         random_trace(1500, 4, 4, seed=12, max_cycle=300, burst0=20))
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

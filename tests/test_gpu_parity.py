@@ -3,6 +3,8 @@
 Integer/ps arithmetic, so the bar is exact equality (np.array_equal) on every
 output array.  Runs on the MI355X box through the C ABI (libgnoc.so).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -11,6 +13,8 @@ from oracle import oracle
 from tests.traces import random_trace
 
 pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def run_both(cfg, tr):
@@ -340,3 +344,20 @@ def test_basic_moving_average_refusals():
     with pytest.raises(gnoc.GnocError) as ex:
         gnoc.Engine(gnoc.EngineConfig(num_tiles=16, moving_avg_type=gnoc.MOVING_AVG_MEDIAN))
     assert ex.value.code == -1
+
+
+@pytest.mark.parametrize("name", sorted(f[:-4] for f in os.listdir(GOLD) if f.endswith(".npz")))
+def test_engine_matches_golden_fixtures(name):
+    """The engine against every committed golden fixture (tests/golden/*.npz,
+    produced by make_golden.py from the pinned oracle): packets and port counters."""
+    import json
+    z = np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False)
+    cfg = gnoc.EngineConfig(**json.loads(str(z["cfg"])))
+    tr = gnoc.Trace(z["inject_ps"], z["src"], z["dst"], z["bits"], z["flags"])
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    got = eng.results()
+    eng.close()
+    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1"):
+        assert np.array_equal(getattr(got, k), z[k]), k

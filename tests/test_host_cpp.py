@@ -55,7 +55,10 @@ def test_replay_golden_through_cpp_model(tmp_path, name):
     trace = str(tmp_path / "t.gtr")
     out = str(tmp_path / "r.bin")
     gnoc.write_trace_file(trace, cfg, tr)
-    r = subprocess.run([os.path.join(BUILD, "gnoc_replay"), trace, "--results", out, "--summary", "0"],
+    # the trace header holds gnoc_config only: the basic queue's moving average goes on the command line
+    mavg = ["--moving-avg", {1: "arithmetic_mean", 3: "median"}[cfg.moving_avg_type] + f":{cfg.moving_avg_window}"] \
+        if cfg.moving_avg_type else []
+    r = subprocess.run([os.path.join(BUILD, "gnoc_replay"), trace, "--results", out, "--summary", "0"] + mavg,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "Total Packets Received" in r.stdout
