@@ -86,6 +86,7 @@ struct DevCfg
    const uint64_t* bc_mprev;
    uint64_t* bc_mcur;
    uint64_t* bc_fin;        // [b * N + tile] receipt time (ps)
+   uint64_t npk;            // packets of the batch: a SELF port never writes final_ps beyond it
 };
 
 // Latency::toPicosec, common/misc/time_types.h:81-86.  F1: f == 1.0 exactly,

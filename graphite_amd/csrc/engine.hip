@@ -28,6 +28,7 @@
 #include "prep.hip"
 #include "shard.hip"
 #include "serial.hip"
+#include "chain.hip"
 
 #include <hipcub/hipcub.hpp>
 
@@ -71,11 +72,12 @@ struct DevBuf
 enum KernelClass
 {
    KC_CLASSIFY, KC_SRC_TOT, KC_INJ_BASE, KC_SRC_OFFS, KC_SCATTER, KC_ROW_HIST, KC_PROW, KC_SLOT_COUNTS, KC_SCAN,
-   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_BCAST, KC_N
+   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_BCAST, KC_CHAIN, KC_BOUNDS, KC_N
 };
 static const char* const kKernelNames[KC_N] = { "k_classify", "k_src_tot", "k_inj_base", "k_src_offs", "k_scatter",
                                                 "k_row_hist", "k_prow", "k_slot_counts", "k_scan_slots", "k_plan",
-                                                "k_level", "k_port_stream", "k_finalize", "k_bcast" };
+                                                "k_level", "k_port_stream", "k_finalize", "k_bcast",
+                                                "k_chain", "k_win_bounds" };
 
 struct gnoc_engine
 {
@@ -144,6 +146,17 @@ struct gnoc_engine
    int ma_type = 0;
    uint32_t ma_window = 1;
    DevBuf ma_t, ma_key, ma_val, ma_key2, ma_val2, ma_lo, ma_hi, ma_d, ma_tmp;
+
+   // v4 chain engine (chain.hip): windows of 2^ch_shift ps, ch_nw of them (sized at submit)
+   uint32_t ch_shift = 0, ch_nw = 0;
+   uint32_t ch_shift_run = 0, ch_nw_run = 0;   // the attempt in flight
+   uint32_t ch_epoch = 0;
+   int ch_grid = 0;
+   int force_levels = 0;
+   int used_chain = 0;
+   uint32_t ncpx = 0, ncpy = 0;
+   DevBuf ch_cp, ch_bt, ch_st, ch_ctr;
+   uint32_t n_retry = 0, n_fallback = 0;    // reruns of the last gnoc_run (chain -> smaller windows / levels, v3 -> v1)
 
    // kernel profiling (gnoc_set_profiling)
    bool prof = false;
@@ -373,7 +386,7 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
    if (he == hipSuccess) he = hipEventCreate(&e->ev0);
    if (he == hipSuccess) he = hipEventCreate(&e->ev1);
-   if (he == hipSuccess) he = hipHostMalloc((void**) &e->h_pinned, 64, hipHostMallocDefault);
+   if (he == hipSuccess) he = hipHostMalloc((void**) &e->h_pinned, 128, hipHostMallocDefault);
    if (he == hipSuccess) he = upload_levels(e);
    if (he == hipSuccess)
    {
@@ -381,6 +394,11 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
       he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_level<false, true, false>, LV_T, 0);
       if (he == hipSuccess) he = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device);
       e->level_grid = std::max(1, per_cu) * std::max(1, cus);
+      // the chain kernels' residency (a grid beyond it only queues: tasks are handed out in order)
+      int c1 = 0, c3 = 0;
+      if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c1, ch::k_chain<1>, ch::T, 0);
+      if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c3, ch::k_chain<3>, ch::T, 0);
+      e->ch_grid = std::max(1, std::min(c1, c3)) * std::max(1, cus);
    }
    if (he != hipSuccess)
    {
@@ -524,6 +542,34 @@ static uint32_t fw_host(const gnoc_engine* e, uint32_t tile)
    return e->npoints > 1 ? e->h_pt_fw[point_of(e->dc, tile)] : (uint32_t) e->cfg.flit_width;
 }
 
+// Chain-engine windows (chain.hip): D = 2^shift ps with the busiest port's
+// expected records per window near CH_FILL of the LDS stream capacity (and its
+// inserts within the insert buffer), assuming a steady rate over [0, t_last].
+// nW = t_last / D + 1 windows, the last one unbounded.  shift 0 = chain off.
+static constexpr double CH_FILL = 0.5;
+static constexpr uint32_t CH_NW_MAX = 4096;
+static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, uint64_t t_last)
+{
+   const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size
+   const uint64_t span = t_last + 1;
+   double d = 1e300;
+   if (port_max) d = std::min(d, CH_FILL * ch::CAP * (double) span / (double) port_max);
+   if (ins_max) d = std::min(d, CH_FILL * ch::ICAP * (double) span / (double) ins_max);
+   uint32_t sh = 10;
+   while (sh < 40 && (double) (1ull << (sh + 1)) <= d) sh++;
+   if (fv && std::atoi(fv) > 0) sh = (uint32_t) std::atoi(fv);
+   uint64_t nw = (t_last >> sh) + 1;
+   while (nw > CH_NW_MAX && sh < 40) { sh++; nw = (t_last >> sh) + 1; }
+   if (sh > 31)
+   {
+      e->ch_shift = 0;   // windows of 2^32 ps or more do not fit the 32-bit time offsets
+      e->ch_nw = 0;
+      return;
+   }
+   e->ch_shift = sh;
+   e->ch_nw = (uint32_t) nw;
+}
+
 static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n, uint64_t* records)
 {
    const uint32_t N = e->dc.N, W = e->dc.W, H = e->dc.H;
@@ -538,6 +584,12 @@ static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n,
       for (uint32_t x = band_lo(b, nr, W); x < band_lo(b + 1, nr, W); x++) cb[x] = b;
    }
    e->h_bid.clear();
+   // chain engine window sizing (chain.hip): records per port over the batch,
+   // from difference arrays along each row (X ports) and column (Y ports), and
+   // insert records per port (first-hop records of X ports, Y-leg starts)
+   std::vector<int32_t> dxr((size_t) H * (W + 1), 0), dxl((size_t) H * (W + 1), 0);
+   std::vector<int32_t> dyu((size_t) W * (H + 1), 0), dyd((size_t) W * (H + 1), 0);
+   std::vector<uint32_t> insx((size_t) N * 2, 0), insy((size_t) N * 2, 0);
    for (size_t i = 0; i < n; i++)
    {
       const uint32_t s = pk->src[i], fl = pk->flags ? pk->flags[i] : 0u;
@@ -568,6 +620,10 @@ static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n,
       {
          const int64_t sx = s % W, sy = s / W, dx = d % W, dy = d / W;
          const uint64_t ax = (uint64_t) std::llabs(sx - dx), ay = (uint64_t) std::llabs(sy - dy);
+         if (dx > sx) { dxr[sy * (W + 1) + sx]++; dxr[sy * (W + 1) + dx]--; insx[s * 2]++; }
+         else if (dx < sx) { dxl[sy * (W + 1) + dx + 1]++; dxl[sy * (W + 1) + sx + 1]--; insx[s * 2 + 1]++; }
+         if (dy > sy) { dyu[dx * (H + 1) + sy]++; dyu[dx * (H + 1) + dy]--; insy[(sy * W + dx) * 2]++; }
+         else if (dy < sy) { dyd[dx * (H + 1) + dy + 1]++; dyd[dx * (H + 1) + sy + 1]--; insy[(sy * W + dx) * 2 + 1]++; }
          if (nr <= 1) rec += 2 + ax + ay;
          else
          {
@@ -582,6 +638,30 @@ static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n,
       }
    }
    if (n && pk->inject_ps[n - 1] >= (1ull << 50)) return fail(e, GNOC_EUNSUPPORTED, "inject time beyond 2^50 ps");
+   uint64_t pmax = 0, imax = 0;
+   for (uint32_t r = 0; r < H; r++)
+   {
+      int64_t a = 0, b = 0;
+      for (uint32_t x = 0; x <= W; x++)
+      {
+         a += dxr[r * (W + 1) + x];
+         b += dxl[r * (W + 1) + x];
+         pmax = std::max<uint64_t>(pmax, (uint64_t) std::max<int64_t>(a, b));
+      }
+   }
+   for (uint32_t x = 0; x < W; x++)
+   {
+      int64_t a = 0, b = 0;
+      for (uint32_t y = 0; y <= H; y++)
+      {
+         a += dyu[x * (H + 1) + y];
+         b += dyd[x * (H + 1) + y];
+         pmax = std::max<uint64_t>(pmax, (uint64_t) std::max<int64_t>(a, b));
+      }
+   }
+   for (uint32_t v : insx) imax = std::max<uint64_t>(imax, v);
+   for (uint32_t v : insy) imax = std::max<uint64_t>(imax, v);
+   choose_windows(e, pmax, imax, n ? pk->inject_ps[n - 1] : 0);
    *records = rec;
    return GNOC_OK;
 }
@@ -693,6 +773,7 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    e->d_bits = e->t_bits.as<uint32_t>();
    e->d_flags = e->t_flags.as<uint32_t>();
    e->n = n;
+   e->dc.npk = n;
    e->rec_bound = record_bound(e, records);
    rc = upload_broadcasts(e);
    if (rc) return rc;
@@ -716,6 +797,9 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    e->d_bits = pk->bits;
    e->d_flags = pk->flags;
    e->n = n;
+   e->dc.npk = n;
+   e->ch_shift = 0;   // no host trace to size the chain engine's windows: level engine
+   e->ch_nw = 0;
    e->h_bid.clear();
    int brc = upload_broadcasts(e);
    if (brc) return brc;
@@ -926,6 +1010,91 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
 }
 
 constexpr int GNOC_V3_RETRY = 1000;
+constexpr int GNOC_CH_RETRY = 1001;      // a chain window overflowed LDS: smaller windows
+constexpr int GNOC_CH_FALLBACK = 1002;   // the chain engine cannot take this batch: level engine
+
+// ---------------------------------------------------------------------------
+// v4: chain engine for the X and Y phases (chain.hip); INJ and SELF levels on k_level
+// ---------------------------------------------------------------------------
+static bool chain_usable(const gnoc_engine* e)
+{
+   const char* env = std::getenv("GNOC_ENGINE");
+   if (env && (std::strcmp(env, "levels") == 0 || std::strcmp(env, "v1") == 0)) return false;
+   return e->ch_nw > 0 && e->f1 && !e->nb && !e->force_levels && !e->force_v1 && !e->dc.hop_counter &&
+          e->dc.max_list >= 3 && (e->dc.W > 1 || e->dc.H > 1);
+}
+
+// Chain descriptors, state buffers, epoch.  After run_plan_v3 (slot layout known).
+static int chain_setup(gnoc_engine* e)
+{
+   const DevCfg& c = e->dc;
+   hipStream_t s = e->stream;
+   const uint32_t W = c.W, H = c.H;
+   e->ncpx = W > 1 ? 2 * (e->ry1 - e->ry0) * (W - 1) : 0;
+   e->ncpy = H > 1 ? 2 * (e->cx1 - e->cx0) * (H - 1) : 0;
+   const uint32_t ncp = e->ncpx + e->ncpy;
+   const uint32_t nW = e->ch_nw_run;
+   GNOC_HIP(e, e->ch_cp.ensure((size_t) std::max<uint32_t>(ncp, 1) * sizeof(ChainPort)));
+   GNOC_HIP(e, e->ch_bt.ensure(((size_t) e->ncpx + 3ull * e->ncpy + 1) * (nW + 1) * 4));
+   GNOC_HIP(e, e->ch_ctr.ensure(64));
+   const size_t stb = (size_t) std::max<uint32_t>(ncp, 1) * nW * ch::SW * 8;
+   const bool fresh = e->ch_st.bytes < stb;
+   GNOC_HIP(e, e->ch_st.ensure(stb));
+   // hand-off granules carry a 16-bit epoch: a new epoch per attempt, the buffer
+   // zeroed when it is new or the epoch wraps
+   e->ch_epoch = (e->ch_epoch + 1) & 0xFFFFu;
+   if (fresh || e->ch_epoch == 0)
+   {
+      GNOC_HIP(e, hipMemsetAsync(e->ch_st.p, 0, e->ch_st.bytes, s));
+      if (e->ch_epoch == 0) e->ch_epoch = 1;
+   }
+   GNOC_HIP(e, hipMemsetAsync(e->ch_ctr.p, 0, 64, s));
+   if (ncp)
+      GNOC_LAUNCH(e, KC_PLAN, ch::k_chain_plan, dim3((ncp + 255) / 256), dim3(256), 0, s, c, e->ncpx, e->ncpy, e->ry0,
+                  e->cx0, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->ch_cp.as<ChainPort>());
+   return GNOC_OK;
+}
+
+// One phase: 0 = X (rows of this rank), 1 = Y (columns of this rank).
+static int chain_phase(gnoc_engine* e, int phase)
+{
+   const DevCfg& c = e->dc;
+   hipStream_t s = e->stream;
+   const uint32_t ncp = phase ? e->ncpy : e->ncpx;
+   if (!ncp) return GNOC_OK;
+   const uint32_t len = phase ? c.H - 1 : c.W - 1;
+   const uint32_t nl = phase ? 3u : 1u;
+   const uint32_t nW = e->ch_nw_run;
+   const ChainPort* cp = e->ch_cp.as<ChainPort>() + (phase ? e->ncpx : 0);
+   uint32_t* bt = e->ch_bt.as<uint32_t>() + (phase ? (size_t) e->ncpx * (nW + 1) : 0);
+   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, cp, nl, nW, e->ch_shift_run,
+               e->recs.as<Rec>(), bt);
+   ChainArgs a;
+   a.c = c;
+   a.cp = cp;
+   a.bt = bt;
+   a.recs = e->recs.as<Rec>();
+   a.samp_t = e->samp_t.as<uint64_t>();
+   a.samp_id = e->samp_id.as<uint32_t>();
+   a.st = e->ch_st.as<uint64_t>();
+   a.port_sum = e->port_sum.as<unsigned long long>();
+   a.port_cnt = e->port_cnt.as<unsigned long long>();
+   a.port_flit = e->port_flit.as<unsigned long long>();
+   a.port_last = e->port_last.as<unsigned long long>();
+   a.errflag = e->counters.as<unsigned>() + 8;
+   a.ctr = e->ch_ctr.as<unsigned>() + phase;
+   a.nch = ncp / len;
+   a.len = len;
+   a.nW = nW;
+   a.dshift = e->ch_shift_run;
+   a.cp0 = phase ? e->ncpx : 0;
+   a.pad0 = 0;
+   a.etag = (uint64_t) e->ch_epoch << 48;
+   const uint32_t grid = (uint32_t) std::min<uint64_t>((uint64_t) e->ch_grid, (uint64_t) a.nch * nW);
+   if (phase) GNOC_LAUNCH(e, KC_CHAIN, ch::k_chain<3>, dim3(grid), dim3(ch::T), 0, s, a);
+   else GNOC_LAUNCH(e, KC_CHAIN, ch::k_chain<1>, dim3(grid), dim3(ch::T), 0, s, a);
+   return GNOC_OK;
+}
 
 static int run_post(gnoc_engine* e, bool closed_form);
 
@@ -1138,7 +1307,7 @@ static int run_post(gnoc_engine* e, bool closed_form)
    if (!closed_form)
    {
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 3, e->gtot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
-      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 4, e->counters.as<unsigned int>() + 8, 4, hipMemcpyDeviceToHost, s));
+      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
    }
    GNOC_HIP(e, hipStreamSynchronize(s));
    e->h_counters[0] = e->h_pinned[0];
@@ -1154,7 +1323,13 @@ static int run_post(gnoc_engine* e, bool closed_form)
    }
    e->h_records = e->h_counters[0] + e->h_counters[1] + e->h_pinned[2];
    if (e->h_pinned[3] > e->rec_bound) return fail(e, GNOC_EHIP, "internal: slot layout exceeds the record bound");
-   const unsigned errf = *(unsigned int*) (e->h_pinned + 4);
+   const unsigned* ef = (const unsigned*) (e->h_pinned + 8);
+   const unsigned errf = ef[0];
+   if (e->used_chain && (ef[4] & ch::F_ANY))
+   {
+      if (ef[4] & ch::F_ROUTE) return fail(e, GNOC_EHIP, "internal: chain route-count invariant violated");
+      return (ef[4] & (ch::F_FALLBACK | ch::F_TIMEOUT)) ? GNOC_CH_FALLBACK : GNOC_CH_RETRY;
+   }
    // a leaf the splitter could not cut (or a look-back timeout) leaves garbage
    // downstream, so it takes precedence: rerun exactly on the v1 path
    if (errf & 6u)
@@ -1175,7 +1350,21 @@ static int run_once(gnoc_engine* e)
    if (rc || done) return rc;
    const bool v3 = e->dc.max_list >= 3 && !e->force_v1;
    e->used_v3 = v3;
-   if (v3)
+   e->used_chain = 0;
+   if (v3 && chain_usable(e))
+   {
+      // v4: INJ level, X chains, Y chains, SELF level
+      const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
+      e->used_chain = 1;
+      e->used_v3 = 4;
+      rc = run_plan_v3(e);
+      if (!rc) rc = chain_setup(e);
+      if (!rc) rc = run_levels_v3(e, 0, 1);
+      if (!rc) rc = chain_phase(e, 0);
+      if (!rc) rc = chain_phase(e, 1);
+      if (!rc) rc = run_levels_v3(e, L - 1, L);
+   }
+   else if (v3)
    {
       rc = run_plan_v3(e);
       if (!rc) rc = run_levels_v3(e, 0, (uint32_t) e->lvl_off.size() - 1);
@@ -1344,14 +1533,35 @@ int gnoc_run(gnoc_engine* e)
    {
       if (e->nb && e->submitted) GNOC_HIP(e, hipMemsetAsync(e->d_bm1.p, 0, nv * 8, e->stream));
       e->force_v1 = forced;
+      e->force_levels = 0;
+      e->ch_shift_run = e->ch_shift;
+      e->ch_nw_run = e->ch_nw;
+      if (e->bc_passes == 0) { e->n_retry = 0; e->n_fallback = 0; }
       int rc = run_once(e);
+      // chain engine: a window that overflowed LDS reruns with windows half as long
+      // (twice as many), up to 3 times; anything else it cannot take reruns on levels
+      while (rc == GNOC_CH_RETRY && e->ch_shift_run > 10 && e->n_retry < 3 && 2ull * e->ch_nw_run <= CH_NW_MAX)
+      {
+         e->n_retry++;
+         e->ch_shift_run--;
+         e->ch_nw_run = e->ch_nw_run * 2;
+         rc = run_once(e);
+      }
+      if (rc == GNOC_CH_RETRY || rc == GNOC_CH_FALLBACK)
+      {
+         e->n_fallback++;
+         e->force_levels = 1;
+         rc = run_once(e);
+      }
       if (rc == GNOC_V3_RETRY)
       {
+         e->n_fallback++;
          e->force_v1 = 1;   // exact but slower whole-port streams
          rc = run_once(e);
          if (rc == GNOC_V3_RETRY) rc = fail(e, GNOC_EHIP, "internal: v1 path reported overflow");
       }
       e->force_v1 = forced;
+      e->force_levels = 0;
       if (rc) return rc;
       ms += e->last_ms;
       e->bc_passes++;
@@ -1449,10 +1659,50 @@ int gnoc_run_begin(gnoc_engine* e, void* send_buf)
       return GNOC_OK;
    }
    e->used_v3 = 1;
-   rc = run_plan_v3(e);
-   if (!rc) rc = run_levels_v3(e, 0, e->lvl_y0);
-   if (rc) return rc;
+   e->used_chain = 0;
+   e->n_retry = 0;
+   e->n_fallback = 0;
+   e->ch_shift_run = e->ch_shift;
+   e->ch_nw_run = e->ch_nw;
    hipStream_t s = e->stream;
+   rc = run_plan_v3(e);
+   if (!rc && chain_usable(e))
+   {
+      // v4 X phase; a rank whose chains decline the batch reruns its X levels on
+      // k_level before packing (the exchange layout does not depend on the path)
+      e->used_chain = 1;
+      e->used_v3 = 4;
+      rc = chain_setup(e);
+      if (!rc) rc = run_levels_v3(e, 0, 1);
+      if (!rc) rc = chain_phase(e, 0);
+      if (rc) return rc;
+      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
+      GNOC_HIP(e, hipStreamSynchronize(s));
+      const unsigned f4 = ((const unsigned*) (e->h_pinned + 8))[4];
+      if (f4 & ch::F_ROUTE) return fail(e, GNOC_EHIP, "internal: chain route-count invariant violated");
+      if (f4 & ch::F_ANY)
+      {
+         e->n_fallback++;
+         GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, 0, 4, s));
+         const uint32_t np = e->dc.N * PORTS;
+         hipLaunchKernelGGL(ch::k_zero_ports, dim3((np + 255) / 256), dim3(256), 0, s, np,
+                            (1u << P_LEFT) | (1u << P_RIGHT), e->port_sum.as<unsigned long long>(),
+                            e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
+                            e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>());
+         GNOC_HIP(e, hipGetLastError());
+         rc = run_levels_v3(e, 1, e->lvl_y0);
+         if (rc) return rc;
+      }
+   }
+   else if (!rc)
+      rc = run_levels_v3(e, 0, e->lvl_y0);
+   if (rc) return rc;
+   // a look-back timeout or a leaf the splitter could not cut leaves garbage in
+   // the turn slots: fail here, before anything is packed for the peers
+   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
+   GNOC_HIP(e, hipStreamSynchronize(s));
+   if (((const unsigned*) (e->h_pinned + 8))[0] & 6u)
+      return fail(e, GNOC_EUNSUPPORTED, "sharded run hit a burst the chunked path cannot split (X phase)");
    if (e->xs_slots)
    {
       if (!send_buf) return fail(e, GNOC_EINVAL, "null send buffer");
@@ -1491,7 +1741,28 @@ int gnoc_run_finish(gnoc_engine* e, const void* recv_buf)
                          reinterpret_cast<const uint4*>(recv_buf), e->counters.as<unsigned>() + 8);
       GNOC_HIP(e, hipGetLastError());
    }
-   int rc = run_levels_v3(e, e->lvl_y0, (uint32_t) e->lvl_off.size() - 1);
+   const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
+   int rc;
+   if (e->used_chain)
+   {
+      rc = chain_phase(e, 1);
+      if (!rc) rc = run_levels_v3(e, L - 1, L);
+      if (!rc) rc = run_post(e, false);
+      if (rc != GNOC_CH_RETRY && rc != GNOC_CH_FALLBACK) return rc;
+      // the Y chains declined: Y and SELF levels on k_level (fresh look-back state)
+      e->n_fallback++;
+      e->used_chain = 0;
+      GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, 0, 4, s));
+      const uint32_t np = e->dc.N * PORTS;
+      hipLaunchKernelGGL(ch::k_zero_ports, dim3((np + 255) / 256), dim3(256), 0, s, np,
+                         (1u << P_UP) | (1u << P_DOWN) | (1u << P_SELF), e->port_sum.as<unsigned long long>(),
+                         e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
+                         e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>());
+      GNOC_HIP(e, hipGetLastError());
+      rc = run_plan_v3(e);
+      if (rc) return rc;
+   }
+   rc = run_levels_v3(e, e->lvl_y0, L);
    if (rc) return rc;
    return run_post(e, false);
 }

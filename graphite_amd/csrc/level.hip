@@ -740,7 +740,12 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
          }
          ssum += cc;
          const uint64_t tn = t + LV_PS(cc) + rl;
-         if (dir == P_SELF) { final_ps[id] = tn + LV_PS(aux_F(ax)); continue; }
+         if (dir == P_SELF)
+         {
+            if (id < c.npk) final_ps[id] = tn + LV_PS(aux_F(ax));
+            else atomicOr(errflag, 1u);
+            continue;
+         }
          const uint32_t nd = next_dir(ax, dir, nx, ny);
          Rec o;
          o.t = tn;
@@ -810,7 +815,8 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
          if (dir == P_SELF)
          {
             // NetworkModel::processReceivedPacket: + serialization (network_model.cc:142-150)
-            final_ps[id] = tn + LV_PS(aux_F(ax));
+            if (id < c.npk) final_ps[id] = tn + LV_PS(aux_F(ax));
+            else atomicOr(errflag, 1u);
             continue;
          }
          const uint32_t nd = next_dir(ax, dir, nx, ny);
@@ -1250,6 +1256,9 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
    // exception tails exist only if an earlier level's M/G/1 path wrote one (flag set
    // before this launch); the cross-level launch always reads the counts
    const bool anyexc = XL || errflag[2] != 0;
+   // the chain engine (chain.hip) declined this batch: its outputs are incomplete,
+   // the host reruns the batch on the level engine
+   if (errflag[4] != 0) return;
    if (tid == 0) { sm.nx.ready = 0; sm.qdone = 0; }
 #if LV_GEN
    if (tid == 0) sm.fq = c.f;
