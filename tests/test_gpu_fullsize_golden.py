@@ -1,0 +1,88 @@
+"""BASELINE.json headline configurations at FULL size, bit-exact against the
+CPU oracle ("a seed plus a SHA-256 of the results").
+
+tests/golden/fullsize_hashes.json holds, per workload, the SHA-256 of every
+output array of the oracle run (final_ps, zero_load_ps, contention_ps and the
+per-port sum / count / M/G/1 / flit / last arrays), made in the build
+container by tests/golden/make_fullsize.py (the oracle needs 2.5 min for a
+32x32 batch and 25 min for the 64x64 one).  Here the trace is regenerated
+from its seed (its own SHA-256 checked first), run through the engine, and
+every result array must hash identically:
+* configs[1]: 32x32 uniform and hotspot, load 0.005, 10,000 packets per tile
+  (10.24 M packets, 228 M mesh hops) -- the bench workload;
+* configs[2]: 64x64 uniform, load 0.002, 10,000 packets per tile (40.96 M
+  packets, 1.79 G mesh hops), on one engine and sharded over 8 row / column
+  band ranks (gnoc.LocalShardSet, all ranks on the one test GPU).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from graphite_amd import gnoc
+from tests.golden.make_fullsize import RESULT_FIELDS, sha, trace_hash, trace_of
+
+pytestmark = pytest.mark.gpu
+
+with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize_hashes.json")) as _fh:
+    GOLD = json.load(_fh)
+
+
+def _check(name, res):
+    g = GOLD[name]["results"]
+    bad = [f for f in RESULT_FIELDS if sha(getattr(res, f)) != g[f]["sha256"]]
+    sums = {f: (int(getattr(res, f).astype(np.uint64).sum(dtype=np.uint64)), g[f]["sum"]) for f in bad}
+    assert not bad, f"{name}: arrays differ from the oracle: {sums}"
+
+
+def _trace(name):
+    tr = trace_of(name)
+    assert trace_hash(tr) == GOLD[name]["trace_sha256"], "synthetic trace generator changed"
+    return tr
+
+
+@pytest.mark.parametrize("name", ["32x32_uniform_l0.005_ppt10000", "32x32_hotspot_l0.005_ppt10000"])
+def test_configs1_full_size_matches_oracle(name):
+    tr = _trace(name)
+    cfg = gnoc.EngineConfig(num_tiles=1024)
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    s = eng.summary()
+    res = eng.results()
+    eng.close()
+    assert s["mesh_hops"] == GOLD[name]["mesh_hops"]
+    _check(name, res)
+
+
+def test_configs1_full_size_level_engine_matches_oracle(monkeypatch):
+    """The chunked level engine (the chain engine's fallback) on the same batch."""
+    name = "32x32_uniform_l0.005_ppt10000"
+    monkeypatch.setenv("GNOC_ENGINE", "levels")
+    tr = _trace(name)
+    eng = gnoc.Engine(gnoc.EngineConfig(num_tiles=1024))
+    eng.submit(tr)
+    eng.run()
+    assert eng.summary()["engine_path"] == 1
+    res = eng.results()
+    eng.close()
+    _check(name, res)
+
+
+def test_configs2_full_size_matches_oracle_single_and_8_ranks():
+    name = "64x64_uniform_l0.002_ppt10000"
+    tr = _trace(name)
+    cfg = gnoc.EngineConfig(num_tiles=4096)
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    res = eng.results()
+    eng.close()
+    _check(name, res)
+    ss = gnoc.LocalShardSet(cfg, 8)
+    ss.submit(tr)
+    ss.run()
+    got = ss.results()
+    ss.close()
+    _check(name, got)
