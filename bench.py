@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # torch first: libgnoc.so then binds to the same HIP runtime (SONAME libamdhip64.so.7)
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -112,6 +113,21 @@ def main():
     kst = eng.kernel_stats()
     eng.set_profiling(False)
 
+    # end to end (SURVEY.md 8(d) "trace resident in host memory -> results in host
+    # memory"): submit from pinned host arrays (host-side trace validation + H2D),
+    # run, final_ps back into a pinned host array; reported beside the HBM-resident value
+    e2e_ms = None
+    if not sharded:
+        ptr = pinned_trace(tr)
+        fin = torch.empty(len(tr), dtype=torch.int64, pin_memory=True).numpy()
+        barrier_sync()
+        t_e = time.perf_counter()
+        for _ in range(max(1, a.steps // 2)):
+            eng.submit(ptr)
+            eng.run()
+            eng.final_ps_into(fin)
+        e2e_ms = (time.perf_counter() - t_e) / max(1, a.steps // 2) * 1e3
+
     # this rank's share: mesh hops through the ports it owns, packets it delivers
     res = eng.results()
     pc = res.port_count.reshape(-1, 6)
@@ -137,11 +153,20 @@ def main():
     if rank == 0:
         value = hops_all * a.steps / elapsed_max
         ms_step = elapsed_max / a.steps * 1e3
-        dom = max(("k_level", "k_port_stream"), key=lambda k: kst.get(k, (0.0, 0))[0])
+        # dominant kernel (most device time on this rank): k_chain (v4: the X and Y port
+        # chains), k_level (the chunked levels; on v4 the injection and SELF levels only) or
+        # k_port_stream (v1).  Algorithmic bytes of ITS launches: 32 B per
+        # hop record it moves -- k_chain: the mesh hops at RIGHT/LEFT/UP/DOWN ports; the
+        # level kernels: every hop record + 24 B per delivered packet.
+        dom = max(("k_chain", "k_level", "k_port_stream"), key=lambda k: kst.get(k, (0.0, 0))[0])
         port_ms, port_launches = kst.get(dom, (0.0, 0))
-        # dominant kernel: the per-level chunk kernel (k_level, or k_port_stream on the v1 path).
-        # Algorithmic bytes over all its launches on this rank: 32 B per mesh hop + 24 B per delivered packet.
-        alg_bytes = my_hops * BYTES_PER_HOP + my_pkts * BYTES_PER_PKT
+        xy_hops = int(pc[:, 1:5].sum())
+        if dom == "k_chain":
+            alg_bytes = xy_hops * BYTES_PER_HOP
+        elif int(summ.get("engine_path", 0)) == 4:   # v4 but k_level dominant: injection + SELF levels
+            alg_bytes = (int(pc[:, 0].sum()) + int(pc[:, 5].sum())) * BYTES_PER_HOP + my_pkts * BYTES_PER_PKT
+        else:
+            alg_bytes = my_hops * BYTES_PER_HOP + my_pkts * BYTES_PER_PKT
         achieved = alg_bytes / (port_ms * 1e-3) / 1e9 if port_ms > 0 else 0.0
         whole_job_gbs = value * (BYTES_PER_HOP + BYTES_PER_PKT * pkts / max(hops, 1)) / 1e9 / world
         workload = f"emesh_hop_by_hop {W}x{H} {a.mix} load={load} pkts/tile={a.ppt}"
@@ -165,7 +190,14 @@ def main():
                 "parallelism": (f"rowband/colband{world} + RCCL all-to-all" if sharded and world > 1 else
                                 f"replicas{world}" if world > 1 else "single"),
                 "engine_path": int(summ.get("engine_path", -1)),
+                "windows": int(summ.get("windows", 0)), "window_ps": (1 << int(summ.get("window_shift", 0)))
+                if summ.get("windows") else None,
             },
+            # every rerun is exact but slow: reported, and the bench refuses to report a
+            # configs[1] number that needed one
+            "reruns": {"retries": int(summ.get("retries", 0)), "fallbacks": int(summ.get("fallbacks", 0))},
+            "e2e_ms_per_step": e2e_ms,
+            "e2e_note": "submit from pinned host memory (host validation + H2D) + run + final_ps D2H",
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -187,6 +219,9 @@ def main():
         if a.cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(a, W, H, load, hot)
         print(json.dumps(line), flush=True)
+        if wl == "mesh" and (summ.get("fallbacks") or summ.get("retries")):
+            print(f"bench: the batch needed reruns {line['reruns']}", file=sys.stderr)
+            sys.exit(3)
 
     eng.close()
     if world > 1:
@@ -283,11 +318,16 @@ def _sweep_point_oracle(args):
     return int(res.port_count.reshape(-1, 6)[:, :5].sum()), time.perf_counter() - t0
 
 
-def sweep_cpu_baseline(a, pts, ppt, npts=64, workers=16):
+def sweep_cpu_baseline(a, pts, ppt, npts=64, workers=None):
     """independent single-threaded oracle processes over the
-    host cores (16 workers = the GPU box's CPU share), on the first `npts` points
-    of the same sweep; aggregate hops / wall time."""
+    host cores this process may run on (sched_getaffinity; nproc and the
+    affinity are stated in the record, and at most 16 are used: the GPU box's
+    CPU share), on the first `npts` points of the same sweep; aggregate hops /
+    oracle time."""
     import multiprocessing as mp
+    avail = len(os.sched_getaffinity(0))
+    if workers is None:
+        workers = max(1, min(avail, 16))
     jobs = [((q.flit_width, q.router_delay, q.link_delay, q.tile_width_mm), load, ppt, a.seed + 7919 * i)
             for i, (q, load) in enumerate(pts[:npts])]
     with mp.get_context("spawn").Pool(workers) as pool:
@@ -295,8 +335,22 @@ def sweep_cpu_baseline(a, pts, ppt, npts=64, workers=16):
     hops = sum(h for h, _ in out)
     busy = sum(t for _, t in out) / workers   # oracle time only: worker start-up and trace generation excluded
     return {"value": hops / busy, "unit": "packet-hops/s", "cores": workers, "kind": "port",
+            "nproc": os.cpu_count(), "affinity_cpus": avail,
             "sample": f"{npts} of the {len(pts)} sweep points, pkts/tile={ppt}: {hops} mesh hops, "
                       f"{busy:.2f} s of oracle time per worker ({workers} single-threaded oracle processes)"}
+
+
+def pinned_trace(tr):
+    """The trace in page-locked host memory (numpy views of pinned torch tensors)."""
+    from graphite_amd import gnoc
+
+    def pin(x):
+        t = torch.empty(x.shape[0], dtype={8: torch.int64, 4: torch.int32}[x.dtype.itemsize], pin_memory=True)
+        v = t.numpy().view(x.dtype)
+        v[:] = x
+        return v
+    return gnoc.Trace(pin(tr.inject_ps), pin(tr.src), pin(tr.dst), pin(tr.bits),
+                      pin(tr.flags if tr.flags is not None else np.zeros(len(tr), np.uint32)))
 
 
 PMC_FILE = "r1_pmc.json"
@@ -329,8 +383,14 @@ def cpu_baseline(a, W, H, load, hot):
     dt = time.perf_counter() - t0
     hops = int(r.port_count.reshape(-1, 6)[:, :5].sum())
     return {"value": hops / dt, "unit": "packet-hops/s", "cores": 1, "kind": "port",
+            "what": "oracle restatement of the reference path (oracle/gnoc_oracle.c), 1 core, sorted-array "
+                    "free list instead of the reference's AVL tree",
             "sample": f"{W}x{H} {a.mix} load={load} pkts/tile={a.cpu_sample_ppt}: {len(tr)} packets, "
-                      f"{hops} mesh hops in {dt:.2f} s"}
+                      f"{hops} mesh hops in {dt:.2f} s",
+            # the reference itself (compiled from its sources, survey probe): context only,
+            # measured in the build container, not on the GPU box
+            "reference_probe": {"value": 0.58e6, "unit": "packet-hops/s", "cores": 1,
+                                "config": "32x32 emesh_hop_by_hop, 300 pkts/tile at 0.01", "host": "Xeon, survey probe"}}
 
 
 if __name__ == "__main__":

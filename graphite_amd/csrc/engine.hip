@@ -155,7 +155,7 @@ struct gnoc_engine
    int force_levels = 0;
    int used_chain = 0;
    uint32_t ncpx = 0, ncpy = 0;
-   DevBuf ch_cp, ch_bt, ch_st, ch_ctr;
+   DevBuf ch_cp, ch_bt, ch_st, ch_ctr, ch_stamps0, ch_stamps1;
    uint32_t n_retry = 0, n_fallback = 0;    // reruns of the last gnoc_run (chain -> smaller windows / levels, v3 -> v1)
 
    // kernel profiling (gnoc_set_profiling)
@@ -1090,6 +1090,19 @@ static int chain_phase(gnoc_engine* e, int phase)
    a.cp0 = phase ? e->ncpx : 0;
    a.pad0 = 0;
    a.etag = (uint64_t) e->ch_epoch << 48;
+   a.stamps = nullptr;
+   const char* xv = std::getenv("GNOC_CHAIN_EXPERIMENT");
+   a.exp = xv ? (uint32_t) std::atoi(xv) : 0u;
+   a.pad1 = 0;
+   const char* stv = std::getenv("GNOC_STAMPS");
+   if (stv && *stv == '1')
+   {
+      const size_t nst = (size_t) a.nch * nW * len * 16;
+      DevBuf& sb = phase ? e->ch_stamps1 : e->ch_stamps0;
+      GNOC_HIP(e, sb.ensure(nst * 8));
+      GNOC_HIP(e, hipMemsetAsync(sb.p, 0, nst * 8, s));
+      a.stamps = sb.as<uint64_t>();
+   }
    const uint32_t grid = (uint32_t) std::min<uint64_t>((uint64_t) e->ch_grid, (uint64_t) a.nch * nW);
    if (phase) GNOC_LAUNCH(e, KC_CHAIN, ch::k_chain<3>, dim3(grid), dim3(ch::T), 0, s, a);
    else GNOC_LAUNCH(e, KC_CHAIN, ch::k_chain<1>, dim3(grid), dim3(ch::T), 0, s, a);
@@ -1362,6 +1375,19 @@ static int run_once(gnoc_engine* e)
       if (!rc) rc = run_levels_v3(e, 0, 1);
       if (!rc) rc = chain_phase(e, 0);
       if (!rc) rc = chain_phase(e, 1);
+      const char* xv = std::getenv("GNOC_CHAIN_EXPERIMENT");
+      if (!rc && xv && std::atoi(xv))
+      {
+         // timing experiment (results invalid): stop after the chains
+         GNOC_HIP(e, hipEventRecord(e->ev1, e->stream));
+         GNOC_HIP(e, hipStreamSynchronize(e->stream));
+         float ms = 0;
+         GNOC_HIP(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
+         e->last_ms = ms;
+         GNOC_HIP(e, prof_collect(e));
+         e->ran = true;
+         return GNOC_OK;
+      }
       if (!rc) rc = run_levels_v3(e, L - 1, L);
    }
    else if (v3)
@@ -1839,6 +1865,10 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
    out->levels = e->h_levels;
    out->last_run_ms = e->last_ms;
    out->engine_path = e->dc.contention ? (uint32_t) e->used_v3 : 2u;
+   out->retries = e->n_retry;
+   out->fallbacks = e->n_fallback;
+   out->windows = e->used_chain ? e->ch_nw_run : 0u;
+   out->window_shift = e->used_chain ? e->ch_shift_run : 0u;
    if (e->ran && e->dc.contention)
    {
       std::vector<uint64_t> m((size_t) e->dc.N * PORTS);
@@ -1878,6 +1908,22 @@ __attribute__((visibility("default"))) int gnoc_debug_stamps(gnoc_engine* e, uin
    if (!out || !e->stamps.p) return GNOC_OK;
    const size_t n = std::min(cap, (size_t) e->h_chunk_bound * 16);
    GNOC_HIP(e, hipMemcpy(out, e->stamps.p, n * 8, hipMemcpyDeviceToHost));
+   return GNOC_OK;
+}
+
+// Debug (tools/chain_stamps.py, GNOC_STAMPS=1): per-step stamps of the last chain run, phase 0 (X) or 1 (Y).
+__attribute__((visibility("default"))) int gnoc_debug_chain_stamps(gnoc_engine* e, int phase, uint64_t* out, size_t cap,
+                                                                   size_t* count, uint32_t* geom)
+{
+   if (!e || !count) return GNOC_EINVAL;
+   const DevBuf& sb = phase ? e->ch_stamps1 : e->ch_stamps0;
+   const uint32_t len = phase ? e->dc.H - 1 : e->dc.W - 1;
+   const uint32_t ncp = phase ? e->ncpy : e->ncpx;
+   const uint32_t nch = len ? ncp / len : 0;
+   *count = (size_t) nch * e->ch_nw_run * len * 16;
+   if (geom) { geom[0] = nch; geom[1] = e->ch_nw_run; geom[2] = len; geom[3] = e->ch_shift_run; }
+   if (!out || !sb.p) return GNOC_OK;
+   GNOC_HIP(e, hipMemcpy(out, sb.p, std::min(cap, *count) * 8, hipMemcpyDeviceToHost));
    return GNOC_OK;
 }
 

@@ -92,6 +92,10 @@ class GnocSummary(ctypes.Structure):
         ("levels", ctypes.c_uint32),
         ("engine_path", ctypes.c_uint32),
         ("last_run_ms", ctypes.c_double),
+        ("retries", ctypes.c_uint32),
+        ("fallbacks", ctypes.c_uint32),
+        ("windows", ctypes.c_uint32),
+        ("window_shift", ctypes.c_uint32),
     ]
 
 
@@ -363,6 +367,11 @@ class Engine:
         s = GnocSummary()
         self._check(self.lib.gnoc_get_summary(self._h, ctypes.byref(s)))
         return {f[0]: getattr(s, f[0]) for f in GnocSummary._fields_ }
+
+    def final_ps_into(self, out: np.ndarray) -> None:
+        """final_ps only, into a caller's (e.g. pinned) uint64 array of the batch size."""
+        assert out.dtype.itemsize == 8 and out.shape[0] == self._n and out.flags["C_CONTIGUOUS"]
+        self._check(self.lib.gnoc_get_packet_results(self._h, out.ctypes.data, None, None, self._n))
 
     def results(self) -> Results:
         n = self._n

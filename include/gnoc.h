@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GNOC_ABI_VERSION 1
+#define GNOC_ABI_VERSION 2
 
 /* error codes */
 #define GNOC_OK             0
@@ -137,8 +137,18 @@ typedef struct gnoc_summary
    uint64_t mg1_uses;           /* requests served by the M/G/1 fallback                */
    uint32_t levels;             /* dependency levels executed                           */
    uint32_t engine_path;        /* 0 whole-port streams, 1 chunked look-back, 2 closed form,
-                                   3 serial moving-average queues */
+                                   3 serial moving-average queues, 4 port chains in time windows */
    double   last_run_ms;        /* device time of the last gnoc_run (HIP events)        */
+   /* ABI 2: how the last gnoc_run got there.  Every rerun is exact; these count
+      the cost.  retries: chain-engine reruns with windows half as long (a window
+      overflowed LDS); fallbacks: reruns on a slower path (chain -> chunked
+      levels when a request would take the M/G/1 branch or an earlier level
+      wrote exception tails; chunked -> whole-port streams on a look-back
+      timeout or an unsplittable burst). */
+   uint32_t retries;
+   uint32_t fallbacks;
+   uint32_t windows;            /* chain-engine time windows of the last attempt (0 = not used) */
+   uint32_t window_shift;       /* window length 2^window_shift ps                      */
 } gnoc_summary;
 
 /* Replaces NetworkModel::createModel(..., NETWORK_EMESH_HOP_BY_HOP)

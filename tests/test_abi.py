@@ -28,7 +28,7 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_defaults():
     lib = gnoc.load()
-    assert lib.gnoc_abi_version() == 1
+    assert lib.gnoc_abi_version() == 2
     c = gnoc.GnocConfig()
     lib.gnoc_config_default(ctypes.byref(c), 1024)
     assert (c.num_tiles, c.flit_width, c.router_delay, c.link_delay) == (1024, 64, 1, 1)
