@@ -35,27 +35,22 @@
 namespace gnoc {
 namespace ch {
 
-#ifndef CH_T_V
-#define CH_T_V 256
+// One wave per task: the scan, the reductions and the hand-off state stay in
+// registers, and LDS needs no barriers (a wave's LDS operations execute in
+// program order).
+constexpr int T = 64;
+#ifndef CH_PER_V
+#define CH_PER_V 12
 #endif
-constexpr int T = CH_T_V;                 // threads per workgroup
-constexpr int NWV = T / 64;
-// threads that carry the descriptor (32) / insert-bounds (<= 6) prefetches: other
-// waves than wave 0 (which polls) when there are some
-constexpr uint32_t DESC_T0 = NWV >= 2 ? 64u : 0u;
-constexpr uint32_t BND_T0 = NWV >= 3 ? 128u : 32u;
-#ifndef CH_CAP_V
-#define CH_CAP_V (8 * CH_T_V)
+constexpr int PER = CH_PER_V;             // stream records per lane
+constexpr int CAP = PER * T;              // stream records per (port, window)
+#ifndef CH_IPER_V
+#define CH_IPER_V 3
 #endif
-constexpr int CAP = CH_CAP_V;             // stream records per (port, window)
-constexpr int PER = CAP / T;              // records per thread
-#ifndef CH_ICAP_V
-#define CH_ICAP_V (2 * CH_T_V)
-#endif
-constexpr int ICAP = CH_ICAP_V;           // inserts per (port, window), + spill-ins of the slow path
-constexpr int IPER = ICAP / T;
+constexpr int IPER = CH_IPER_V;
+constexpr int ICAP = IPER * T;            // inserts per (port, window), + spill-ins of the slow path
 #ifndef CH_MINW
-#define CH_MINW 3                         // waves per SIMD the registers must leave room for (3 workgroups per CU)
+#define CH_MINW 2                         // waves per SIMD the registers must leave room for
 #endif
 constexpr int NLMAX = 3;                  // local insert lists (Y ports: LOCAL, W, E)
 constexpr int SW = 8;                     // state words per (chain port, window)
@@ -69,10 +64,11 @@ constexpr uint64_t M48 = (1ull << 48) - 1;
 constexpr uint64_t OFF_LIM = (1ull << 32) - 4096;   // time offsets within a window (32-bit cycle math)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 
-// LDS index padding: one u64 per 32 entries, so a thread's contiguous segment
-// (stride PER across lanes) hits distinct banks.
+// LDS index padding of the kept list: one u64 per 32 entries, so the lanes'
+// segments (stride about PER) hit distinct banks.
 __host__ __device__ constexpr uint32_t pad(uint32_t r) { return r + (r >> 5); }
-constexpr int CAPP = CAP + CAP / 32;
+constexpr int CAPP = CAP + CAP / 32 + 1;   // + the ~0 behind a full list
+
 
 // Route-count fields of a chain port's outputs: SELF, the chain direction, UP,
 // DOWN (an X port never sends the opposite X way; a Y port only SELF or on).
@@ -117,33 +113,29 @@ struct ChainArgs
    uint32_t pad0;
    uint64_t etag;                 // epoch << 48
    uint64_t* stamps;              // debug (GNOC_STAMPS=1): [(task * len + i) * 16 + k] phase stamps, else null
-   uint32_t exp;                  // debug (GNOC_CHAIN_EXPERIMENT, timing only, results wrong): 1 no HBM
-                                  // stores, 2 no hand-off waits, 4 no merge searches
+   uint32_t exp;                  // unused
    uint32_t pad1;
 };
+
 
 namespace ch {
 
 struct Smem
 {
-   uint64_t key[CAPP];            // (t - wbase) << 32 | id, sorted
-   uint32_t aux[CAPP];            // dx | dy << 10 | F << 20
-   uint64_t ikey[ICAP];           // next port's inserts, one sorted list; the slow path's spill-ins behind them
-   uint32_t iaux[ICAP];
-   uint64_t rkey[ICAP];           // Y ports: the three insert slots' ranges as fetched (premerge -> ikey)
-   uint32_t raux[ICAP];
+   // Port i's stream is the (t, id)-merge of two sorted lists, never materialised:
+   // the records kept from port i-1 (rewritten in place by port i: every read of
+   // the list precedes every write) and port i's inserts (double buffered by port
+   // parity: port i+1's land while port i runs).  ~0 sits behind each list's end.
+   uint64_t kkey[CAPP];           // kept: (t - wbase) << 32 | id
+   uint32_t kaux[CAPP];           // dx | dy << 10 | F << 20
+   uint64_t ikey[2][ICAP + 1];    // inserts
+   uint32_t iaux[2][ICAP + 1];
+   uint64_t rkey[ICAP + 1];       // Y ports' three fetched slot ranges (premerge -> ikey); the slow
+   uint32_t raux[ICAP + 1];       // path's inserts + spill-ins
+   uint64_t skey[ICAP];           // the slow path's spill-ins as loaded
+   uint32_t saux[ICAP];
    ChainPort cp[3];               // ports i, i+1, i+2 (ring)
    uint32_t blo[2][NLMAX], bhi[2][NLMAX];   // window bounds of ports i+1, i+2 (ring)
-   uint32_t ioff[NLMAX + 1];      // insert list offsets (NL local lists, end)
-   uint32_t ioff_next[NLMAX];
-   uint64_t wA[NWV], wB[NWV], wC[NWV];
-   uint64_t X_in, ssum;
-   uint32_t cnt_in[4];
-   uint32_t mode_in, n, n_inwin, first_gap, first_fire;
-   uint32_t Kpp, Pep;             // predecessor's spill range of this port
-   uint32_t Kout, Pend;           // this window's, after it
-   uint32_t P0cur, nin_prev, ncont_prev;   // this port's chain input: records before / kept / all of this window
-   uint32_t sp_skip, sp_take, abort_, next_task, published;
 };
 
 __device__ __forceinline__ uint64_t ld1(const uint64_t* p)
@@ -154,17 +146,8 @@ __device__ __forceinline__ void st1(uint64_t* p, uint64_t v)
 {
    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// LDS-only workgroup barrier (no global store is read back by the workgroup).
-__device__ __forceinline__ void bar()
-{
-   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-__device__ __forceinline__ void mp(uint64_t& A, uint64_t& B, uint64_t a2, uint64_t b2)
-{
-   const uint64_t nb = B + a2;
-   B = nb > b2 ? nb : b2;
-   A += a2;
-}
+// Compiler-only ordering point between LDS phases of the one wave.
+__device__ __forceinline__ void wsync() { asm volatile("" ::: "memory"); }
 __device__ __forceinline__ uint32_t cf(uint64_t c, uint32_t f) { return (uint32_t) ((c >> (16 * f)) & 0xFFFFu); }
 
 // Max-plus aggregate of a run of requests: X -> max(X + A, B); C = route counts
@@ -242,9 +225,14 @@ __device__ __forceinline__ uint64_t sgpr64(uint64_t v)
 {
    return (uint64_t) sgpr((uint32_t) v) | ((uint64_t) sgpr((uint32_t) (v >> 32)) << 32);
 }
+__device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return (uint32_t) __builtin_amdgcn_readlane((int) v, l); }
+__device__ __forceinline__ uint64_t rdl64(uint64_t v, int l)
+{
+   return (uint64_t) rdl((uint32_t) v, l) | ((uint64_t) rdl((uint32_t) (v >> 32), l) << 32);
+}
 
 // Lower bound (number of entries < k) in the sorted u64 array a[0, n), by
-// binary lifting: n is block-uniform, so every lane runs floor(log2 n) + 1
+// binary lifting: n is wave-uniform, so every lane runs floor(log2 n) + 1
 // iterations with no divergence; one LDS read each.
 __device__ __forceinline__ uint32_t lb(const uint64_t* a, uint32_t n, uint64_t k)
 {
@@ -257,76 +245,41 @@ __device__ __forceinline__ uint32_t lb(const uint64_t* a, uint32_t n, uint64_t k
    }
    return pos;
 }
-// same over the padded stream array
-__device__ __forceinline__ uint32_t lbp(const uint64_t* a, uint32_t n, uint64_t k)
-{
-   uint32_t pos = 0;
-   for (uint32_t step = n ? 1u << (31 - __builtin_clz(n)) : 0u; step; step >>= 1)
-   {
-      const uint32_t q = pos + step;
-      const uint64_t v = a[pad((q <= n ? q : n) - 1)];
-      pos = (q <= n && v < k) ? q : pos;
-   }
-   return pos;
-}
 
-__device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f)
-{
-   if (!a.exp) atomicOr(a.errflag + 4, f);
-}
+__device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f) { atomicOr(a.errflag + 4, f); }
 __device__ __forceinline__ bool flagged(const ChainArgs& a)
 {
    return (__hip_atomic_load(a.errflag + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & F_ANY) != 0;
 }
 
-// One wave copies a 128-B port descriptor.
-__device__ __forceinline__ void load_cp(ChainPort* dst, const ChainPort* src, uint32_t lane)
+// A 128-B port descriptor: 32 lanes, one dword each.  The prefetch splits into
+// the load a step ahead (register) and the LDS store at the next step.
+__device__ __forceinline__ void load_cp(ChainPort* dst, const ChainPort* src, uint32_t l)
 {
-   if (lane < 32) reinterpret_cast<uint32_t*>(dst)[lane] = reinterpret_cast<const uint32_t*>(src)[lane];
+   reinterpret_cast<uint32_t*>(dst)[l] = reinterpret_cast<const uint32_t*>(src)[l];
 }
-// The same in two halves: the load a step ahead into a register, the LDS store later
-// (a store right behind its load would stall the wave for the whole round trip).
-__device__ __forceinline__ uint32_t fetch_cp(const ChainPort* src, uint32_t lane)
+__device__ __forceinline__ uint32_t fetch_cp(const ChainPort* src, uint32_t l)
 {
-   return lane < 32 ? reinterpret_cast<const uint32_t*>(src)[lane] : 0u;
+   return reinterpret_cast<const uint32_t*>(src)[l];
 }
-__device__ __forceinline__ void put_cp(ChainPort* dst, uint32_t v, uint32_t lane)
+__device__ __forceinline__ void put_cp(ChainPort* dst, uint32_t v, uint32_t l) { reinterpret_cast<uint32_t*>(dst)[l] = v; }
+// Window bounds [lo, hi) of the insert slots of chain port cpi (l < 2 nl).
+__device__ __forceinline__ uint32_t fetch_bounds(const ChainArgs& a, uint32_t cpi, uint32_t nl, uint32_t w, uint32_t l)
 {
-   if (lane < 32) reinterpret_cast<uint32_t*>(dst)[lane] = v;
+   if (l >= 2 * nl) return 0u;
+   const uint32_t j = l < nl ? l : l - nl;
+   return a.bt[((uint64_t) cpi * nl + j) * (a.nW + 1) + w + (l < nl ? 0u : 1u)];
 }
-// Window bounds [lo, hi) of the insert slots of chain port cpi (lanes < 2 nl).
-__device__ __forceinline__ void load_bounds(Smem& sm, const ChainArgs& a, uint32_t slot, uint32_t cpi, uint32_t nl,
-                                            uint32_t w, uint32_t lane)
+__device__ __forceinline__ void put_bounds(Smem& sm, uint32_t slot, uint32_t v, uint32_t nl, uint32_t l)
 {
-   if (lane < 2 * nl)
-   {
-      const uint32_t j = lane < nl ? lane : lane - nl;
-      const uint32_t v = a.bt[((uint64_t) cpi * nl + j) * (a.nW + 1) + w + (lane < nl ? 0u : 1u)];
-      if (lane < nl) sm.blo[slot][j] = v;
-      else sm.bhi[slot][j] = v;
-   }
-}
-
-__device__ __forceinline__ uint32_t fetch_bounds(const ChainArgs& a, uint32_t cpi, uint32_t nl, uint32_t w, uint32_t lane)
-{
-   if (lane >= 2 * nl) return 0u;
-   const uint32_t j = lane < nl ? lane : lane - nl;
-   return a.bt[((uint64_t) cpi * nl + j) * (a.nW + 1) + w + (lane < nl ? 0u : 1u)];
-}
-__device__ __forceinline__ void put_bounds(Smem& sm, uint32_t slot, uint32_t v, uint32_t nl, uint32_t lane)
-{
-   if (lane < 2 * nl)
-   {
-      if (lane < nl) sm.blo[slot][lane] = v;
-      else sm.bhi[slot][lane - nl] = v;
-   }
+   if (l < nl) sm.blo[slot][l] = v;
+   else if (l < 2 * nl) sm.bhi[slot][l - nl] = v;
 }
 
 // Poll the state words [0, nw) of block s until all carry the epoch tag (lane
 // q < nw holds word q).  Wave-wide; false on abort.
 __device__ bool poll_words(const ChainArgs& a, const uint64_t* s, uint32_t nw, uint32_t lane, uint64_t& v)
 {
-   if (a.exp & 2u) return true;
    const uint64_t t0 = __builtin_amdgcn_s_memtime();
    for (;;)
    {
@@ -344,30 +297,32 @@ __device__ bool poll_words(const ChainArgs& a, const uint64_t* s, uint32_t nw, u
    }
 }
 
-// Issue the loads of a port's local inserts of this window (registers).
+// Issue the loads of a port's local inserts of this window (registers); off =
+// the lists' offsets in the port's insert list (uniform).
 template <int NL>
-__device__ __forceinline__ uint32_t fetch_inserts(Smem& sm, const ChainArgs& a, uint32_t ring, uint32_t br,
-                                                  Rec (&iv)[IPER])
+__device__ __forceinline__ uint32_t fetch_inserts(const Smem& sm, const ChainArgs& a, uint32_t ring, uint32_t br,
+                                                  Rec (&iv)[IPER], uint32_t (&off)[NLMAX + 1])
 {
-   const uint32_t tid = threadIdx.x;
+   const uint32_t lane = threadIdx.x;
    const ChainPort& P = sm.cp[ring];
-   uint32_t off[NL + 1], lo[NL];
+   uint32_t lo[NL];
+   uint64_t base[NL];
    off[0] = 0;
 #pragma unroll
    for (int j = 0; j < NL; j++)
    {
       // bounds come from sorted slots; clamped so that nothing can load out of range
-      lo[j] = min(sm.blo[br][j], P.icnt[j]);
-      const uint32_t hi = min(max(sm.bhi[br][j], lo[j]), P.icnt[j]);
+      const uint32_t cnt = sgpr(P.icnt[j]);
+      lo[j] = min(sgpr(sm.blo[br][j]), cnt);
+      const uint32_t hi = min(max(sgpr(sm.bhi[br][j]), lo[j]), cnt);
       off[j + 1] = off[j] + (hi - lo[j]);
+      base[j] = sgpr64(P.ibase[j]) + lo[j];
    }
    const uint32_t itot = off[NL];
-   if (tid == 0)
-      for (int j = 1; j < NL; j++) sm.ioff_next[j] = off[j];
 #pragma unroll
    for (int q = 0; q < IPER; q++)
    {
-      const uint32_t g = tid + (uint32_t) q * T;
+      const uint32_t g = lane + (uint32_t) q * T;
       iv[q].t = 0;
       iv[q].id = 0;
       iv[q].aux = 0;
@@ -377,25 +332,25 @@ __device__ __forceinline__ uint32_t fetch_inserts(Smem& sm, const ChainArgs& a, 
 #pragma unroll
          for (int l = 1; l < NL; l++)
             if (g >= off[l]) j = (uint32_t) l;
-         iv[q] = a.recs[P.ibase[j] + lo[j] + (g - off[j])];
+         iv[q] = a.recs[base[j] + (g - off[j])];
       }
    }
    return itot;
 }
 
 // Fetched inserts into LDS as keys relative to wbase: X ports (one slot)
-// straight into the insert list, Y ports into the staging lists (premerge).
+// straight into insert list `buf`, Y ports into the staging lists (premerge).
 template <int NL>
-__device__ __forceinline__ bool store_inserts(Smem& sm, const Rec (&iv)[IPER], uint32_t itot, uint64_t wbase)
+__device__ __forceinline__ bool store_inserts(Smem& sm, const Rec (&iv)[IPER], uint32_t itot, uint64_t wbase, uint32_t buf)
 {
-   const uint32_t tid = threadIdx.x;
+   const uint32_t lane = threadIdx.x;
    bool bad = false;
-   uint64_t* K = NL > 1 ? sm.rkey : sm.ikey;
-   uint32_t* X = NL > 1 ? sm.raux : sm.iaux;
+   uint64_t* K = NL > 1 ? sm.rkey : sm.ikey[buf];
+   uint32_t* X = NL > 1 ? sm.raux : sm.iaux[buf];
 #pragma unroll
    for (int q = 0; q < IPER; q++)
    {
-      const uint32_t g = tid + (uint32_t) q * T;
+      const uint32_t g = lane + (uint32_t) q * T;
       if (g < itot && g < (uint32_t) ICAP)
       {
          const uint64_t dt = iv[q].t - wbase;
@@ -404,30 +359,22 @@ __device__ __forceinline__ bool store_inserts(Smem& sm, const Rec (&iv)[IPER], u
          X[g] = iv[q].aux;
       }
    }
-   if (tid == 0)
-   {
-      sm.ioff[0] = 0;
-      for (int j = 1; j < NL; j++) sm.ioff[j] = sm.ioff_next[j];
-      sm.ioff[NL] = itot;
-   }
-   return bad;
+   if (NL == 1 && lane == 0 && itot <= (uint32_t) ICAP) K[itot] = ~0ull;
+   return __any(bad);
 }
 
-// Y ports: the staged slot ranges (each sorted) merged into one sorted insert
-// list: own index + lower bounds in the other two ranges.  Reads the staging
-// lists (written before the preceding barrier); ikey is read after the next.
+// Y ports: the staged slot ranges (each sorted) merged into insert list `buf`:
+// own index + lower bounds in the other two ranges.
 template <int NL>
-__device__ __forceinline__ void premerge(Smem& sm, uint32_t itot)
+__device__ __forceinline__ void premerge(Smem& sm, uint32_t itot, uint32_t buf, const uint32_t (&o)[NLMAX + 1])
 {
    if (NL == 1) return;
-   const uint32_t tid = threadIdx.x;
-   uint32_t o[NL + 1];
-#pragma unroll
-   for (int l = 0; l <= NL; l++) o[l] = sm.ioff[l];
+   const uint32_t lane = threadIdx.x;
+   wsync();
 #pragma unroll
    for (int q = 0; q < IPER; q++)
    {
-      const uint32_t g = tid + (uint32_t) q * T;
+      const uint32_t g = lane + (uint32_t) q * T;
       if (g >= itot || g >= (uint32_t) ICAP) continue;
       const uint64_t k = sm.rkey[g];
       uint32_t own = 0;
@@ -438,79 +385,11 @@ __device__ __forceinline__ void premerge(Smem& sm, uint32_t itot)
 #pragma unroll
       for (int l = 0; l < NL; l++)
          if ((uint32_t) l != own) pos += lb(sm.rkey + o[l], o[l + 1] - o[l], k);
-      sm.ikey[pos] = k;
-      sm.iaux[pos] = sm.raux[g];
+      sm.ikey[buf][pos] = k;
+      sm.iaux[buf][pos] = sm.raux[g];
    }
-}
-
-// Merge the kept records (registers: keys rk, aux ra, index ci among the kept;
-// bit j of km marks one) with the sorted insert list sm.ikey[0, itot) into the
-// stream sm.key/aux.  Position = own index + entries of the other list below
-// (keys are unique: one record per packet per port).  The kept keys sit at
-// key[pad(ci)], written before the barrier preceding this call.
-__device__ void merge(Smem& sm, uint32_t nkeep, uint32_t itot, const uint64_t (&rk)[PER], const uint32_t (&ra)[PER],
-                      uint32_t (&ci)[PER], uint32_t km, uint32_t exp, uint64_t* stp = nullptr)
-{
-   const uint32_t tid = threadIdx.x;
-   if (exp & 4u)
-   {
-      // timing experiment: kept records then inserts, unsorted
-      bar();
-#pragma unroll
-      for (int j = 0; j < PER; j++)
-         if ((km >> j) & 1u) { sm.key[pad(ci[j])] = rk[j]; sm.aux[pad(ci[j])] = ra[j]; }
-      for (uint32_t g = tid; g < itot; g += T) { sm.key[pad(nkeep + g)] = sm.ikey[g]; sm.aux[pad(nkeep + g)] = sm.iaux[g]; }
-      if (tid == 0) sm.n = nkeep + itot;
-      bar();
-      return;
-   }
-   // kept records: inserts below the first one by search, then by advancing
-   uint32_t cur = 0;
-   bool first = true;
-#pragma unroll
-   for (int j = 0; j < PER; j++)
-   {
-      if (!((km >> j) & 1u)) continue;
-      if (first) cur = lb(sm.ikey, itot, rk[j]);
-      else
-         while (cur < itot && sm.ikey[cur] < rk[j]) cur++;
-      first = false;
-      ci[j] += cur;
-   }
-   // inserts: own index + kept below
-   uint64_t ik[IPER];
-   uint32_t ia[IPER], pi[IPER];
-#pragma unroll
-   for (int q = 0; q < IPER; q++)
-   {
-      const uint32_t g = tid + (uint32_t) q * T;
-      pi[q] = NONE;
-      ik[q] = 0;
-      ia[q] = 0;
-      if (g >= itot) continue;
-      ik[q] = sm.ikey[g];
-      ia[q] = sm.iaux[g];
-      pi[q] = g + lbp(sm.key, nkeep, ik[q]);
-   }
-   if (stp && tid == 0) stp[10] = __builtin_amdgcn_s_memtime();
-   bar();
-   if (stp && tid == 0) stp[11] = __builtin_amdgcn_s_memtime();
-#pragma unroll
-   for (int j = 0; j < PER; j++)
-      if ((km >> j) & 1u)
-      {
-         sm.key[pad(ci[j])] = rk[j];
-         sm.aux[pad(ci[j])] = ra[j];
-      }
-#pragma unroll
-   for (int q = 0; q < IPER; q++)
-      if (pi[q] != NONE)
-      {
-         sm.key[pad(pi[q])] = ik[q];
-         sm.aux[pad(pi[q])] = ia[q];
-      }
-   if (tid == 0) sm.n = nkeep + itot;
-   bar();
+   if (lane == 0 && itot <= (uint32_t) ICAP) sm.ikey[buf][itot] = ~0ull;
+   wsync();
 }
 
 // Cycles of a stream record relative to the window base cycle wb = max(wq - 1, 0):
@@ -521,15 +400,36 @@ __device__ __forceinline__ uint32_t rcyc(uint32_t off, uint32_t wr, uint32_t d0)
    return (wr + off + 999u) / 1000u + d0;
 }
 
-// This thread's segment of the stream into registers and its aggregate.
-__device__ __forceinline__ Agg load_segment(const Smem& sm, uint32_t a0, uint32_t cnt, uint32_t wr, uint32_t d0,
-                                            uint32_t nx, uint32_t ny, uint32_t cont, uint64_t (&rk)[PER],
-                                            uint32_t (&ra)[PER])
+// Merge path: how many inserts are among the first d records of the merged
+// (kept K[0, nK), inserts I[0, nI)) stream.  Binary lifting over the insert
+// list (the short one), no divergence; keys are unique (one record per packet
+// per port).
+__device__ __forceinline__ uint32_t mp_split(const uint64_t* K, uint32_t nK, const uint64_t* I, uint32_t nI, uint32_t d)
+{
+   const uint32_t lo = d > nK ? d - nK : 0u, hi = d < nI ? d : nI;
+   uint32_t pos = lo;
+   for (uint32_t step = nI ? 1u << (31 - __builtin_clz(nI)) : 0u; step; step >>= 1)
+   {
+      const uint32_t q = pos + step;
+      const bool in = q <= hi;
+      // insert q-1 precedes kept record d-q: it is among the first d
+      const uint64_t vi = I[in ? q - 1 : 0u], vk = K[pad(in ? d - q : 0u)];
+      pos = (in && vi < vk) ? q : pos;
+   }
+   return pos;
+}
+
+// This lane's records of the merged stream (kept from x, inserts from y; cnt
+// of them) into registers, and their aggregate.
+__device__ __forceinline__ Agg walk(const uint64_t* K, const uint32_t* KA, const uint64_t* I, const uint32_t* IA,
+                                   uint32_t x, uint32_t y, uint32_t cnt, uint32_t wr, uint32_t d0, uint32_t nx,
+                                   uint32_t ny, uint32_t cont, uint64_t (&rk)[PER], uint32_t (&ra)[PER], uint32_t& yend)
 {
    Agg g;
    g.A = 0;
    g.B = 0;
    g.C = 0;
+   uint64_t kx = K[pad(x)], ky = I[y];   // the heads (~0 behind each list's end)
 #pragma unroll
    for (int j = 0; j < PER; j++)
    {
@@ -537,8 +437,14 @@ __device__ __forceinline__ Agg load_segment(const Smem& sm, uint32_t a0, uint32_
       ra[j] = 0;
       if ((uint32_t) j < cnt)
       {
-         rk[j] = sm.key[pad(a0 + j)];
-         ra[j] = sm.aux[pad(a0 + j)];
+         const bool tk = kx < ky;
+         rk[j] = tk ? kx : ky;
+         ra[j] = *(tk ? KA + pad(x) : IA + y);
+         x += tk ? 1u : 0u;
+         y += tk ? 0u : 1u;
+         const uint64_t h = *(tk ? K + pad(x) : I + y);
+         kx = tk ? h : kx;
+         ky = tk ? ky : h;
          const uint32_t p = aux_F(ra[j]);
          const uint32_t nb = g.B + p, b2 = rcyc((uint32_t) (rk[j] >> 32), wr, d0) + p;
          g.B = nb > b2 ? nb : b2;
@@ -546,54 +452,25 @@ __device__ __forceinline__ Agg load_segment(const Smem& sm, uint32_t a0, uint32_
          g.C += 1ull << (16 * field_of(xy_dir(nx, ny, aux_dx(ra[j]), aux_dy(ra[j])), cont));
       }
    }
+   yend = y;
    return g;
 }
 
-// Block scan: exclusive prefix of this thread, block totals.  One barrier.
-__device__ __forceinline__ void block_scan(Smem& sm, const Agg& g, Agg& ex, Agg& tot)
-{
-   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-   const Agg inc = wave_scan(g);
-   if (lane == 63) { sm.wA[wv] = inc.A; sm.wB[wv] = inc.B; sm.wC[wv] = inc.C; }
-   Agg e;   // exclusive within the wave: the inclusive value of lane - 1 (wave_shr 1)
-   e.A = dpp32<0x138, 0xF, 0xF>(inc.A);
-   e.B = dpp32<0x138, 0xF, 0xF>(inc.B);
-   e.C = dpp64<0x138, 0xF, 0xF>(inc.C);
-   bar();
-   Agg p;
-   p.A = 0;
-   p.B = 0;
-   p.C = 0;
-   Agg t = p;
-#pragma unroll
-   for (int v = 0; v < NWV; v++)
-   {
-      Agg q;
-      q.A = (uint32_t) sm.wA[v];
-      q.B = (uint32_t) sm.wB[v];
-      q.C = sm.wC[v];
-      if ((uint32_t) v < wv) p = agg_op(p, q);
-      t = agg_op(t, q);
-   }
-   ex = agg_op(p, e);
-   tot = t;
-}
-
 // Spill-ins of this port (slow path): [Kpp, Pep) of its chain slot, written by
-// earlier windows at the previous port; those with t in this window are merged
-// into the stream (rk/ra: this thread's current segment [a0, a0 + cnt)).
-// Returns the records taken; sets sm.sp_skip (consumed by earlier windows).
-__device__ uint32_t spill_in(Smem& sm, const ChainArgs& a, uint64_t sbase, uint32_t spn, uint32_t sbuf, uint32_t n,
-                             uint64_t wbase, uint64_t wlen, const uint64_t (&rk)[PER], const uint32_t (&ra)[PER],
-                             uint32_t a0, uint32_t cnt)
+// earlier windows at the previous port (sorted: FIFO departure order).  Those
+// with t in this window join the port's insert list: (I, nI) and they merge into
+// the staging list.  Returns the records taken; skip = those consumed by
+// earlier windows.
+__device__ uint32_t spill_in(Smem& sm, const ChainArgs& a, uint64_t sbase, uint32_t spn, const uint64_t* I,
+                             const uint32_t* IA, uint32_t nI, uint64_t wbase, uint64_t wlen, uint32_t& skip)
 {
-   const uint32_t tid = threadIdx.x;
+   const uint32_t lane = threadIdx.x;
    Rec sv[IPER];
    uint32_t nb = 0, nt = 0;
 #pragma unroll
    for (int q = 0; q < IPER; q++)
    {
-      const uint32_t g = tid + (uint32_t) q * T;
+      const uint32_t g = lane + (uint32_t) q * T;
       sv[q].t = 0;
       sv[q].id = 0;
       sv[q].aux = 0;
@@ -608,77 +485,80 @@ __device__ uint32_t spill_in(Smem& sm, const ChainArgs& a, uint64_t sbase, uint3
          nt += (sv[q].t >= wbase && sv[q].t - wbase < wlen) ? 1u : 0u;
       }
    }
-   if (nb) atomicAdd(&sm.sp_skip, nb);
-   if (nt) atomicAdd(&sm.sp_take, nt);
-   bar();
-   const uint32_t skip = sm.sp_skip, take = sm.sp_take;
-   if (!take || n + take > (uint32_t) CAP) return take;
+   skip = rdl(wave_sum32(nb), 63);
+   const uint32_t take = rdl(wave_sum32(nt), 63);
+   if (!take) return 0;
 #pragma unroll
    for (int q = 0; q < IPER; q++)
    {
-      const uint32_t g = tid + (uint32_t) q * T;
+      const uint32_t g = lane + (uint32_t) q * T;
       if (g < spn && sv[q].t >= wbase && sv[q].t - wbase < wlen)
       {
-         const uint32_t o = sbuf + (g - skip);
-         sm.ikey[o] = ((sv[q].t - wbase) << 32) | sv[q].id;
-         sm.iaux[o] = sv[q].aux;
+         sm.skey[g - skip] = ((sv[q].t - wbase) << 32) | sv[q].id;
+         sm.saux[g - skip] = sv[q].aux;
       }
    }
-   bar();
-   uint32_t ps[PER];
-#pragma unroll
-   for (int j = 0; j < PER; j++) ps[j] = (uint32_t) j < cnt ? a0 + j + lb(sm.ikey + sbuf, take, rk[j]) : NONE;
-   uint32_t pq[IPER];
-   uint64_t qk[IPER];
-   uint32_t qa[IPER];
+   wsync();
 #pragma unroll
    for (int q = 0; q < IPER; q++)
    {
-      const uint32_t g = tid + (uint32_t) q * T;
-      pq[q] = NONE;
-      qk[q] = 0;
-      qa[q] = 0;
+      const uint32_t g = lane + (uint32_t) q * T;
       if (g < take)
       {
-         qk[q] = sm.ikey[sbuf + g];
-         qa[q] = sm.iaux[sbuf + g];
-         pq[q] = g + lbp(sm.key, n, qk[q]);
+         const uint64_t k = sm.skey[g];
+         const uint32_t p = g + lb(I, nI, k);
+         sm.rkey[p] = k;
+         sm.raux[p] = sm.saux[g];
+      }
+      if (g < nI)
+      {
+         const uint64_t k = I[g];
+         const uint32_t p = g + lb(sm.skey, take, k);
+         sm.rkey[p] = k;
+         sm.raux[p] = IA[g];
       }
    }
-   bar();
-#pragma unroll
-   for (int j = 0; j < PER; j++)
-      if (ps[j] != NONE)
-      {
-         sm.key[pad(ps[j])] = rk[j];
-         sm.aux[pad(ps[j])] = ra[j];
-      }
-#pragma unroll
-   for (int q = 0; q < IPER; q++)
-      if (pq[q] != NONE)
-      {
-         sm.key[pad(pq[q])] = qk[q];
-         sm.aux[pad(pq[q])] = qa[q];
-      }
-   if (tid == 0) sm.n = n + take;
-   bar();
+   if (lane == 0) sm.rkey[nI + take] = ~0ull;
+   wsync();
    return take;
 }
 
+// State word `lane` (< SW) of a port after a window: tail X, route counts, "no
+// gap yet", the port's unconsumed spill range.
+__device__ __forceinline__ uint64_t state_word(uint32_t lane, uint64_t Xo, const uint32_t (&cin)[4], uint64_t C,
+                                               uint32_t nogap, uint32_t Kout, uint32_t Pend)
+{
+   uint64_t v = Xo;
+#pragma unroll
+   for (int f = 0; f < 4; f++)
+      if (lane == 1u + f) v = cin[f] + cf(C, f);
+   if (lane == 5) v = nogap;
+   if (lane == 6) v = Kout;
+   if (lane == 7) v = Pend;
+   return v;
+}
+
 // ---------------------------------------------------------------------------
-// one task: chain c, window w
+// one task: chain c, window w (one wave)
 // ---------------------------------------------------------------------------
+// Phase stamps (tools/chain_stamps.py): a -DCH_STAMPS build with GNOC_STAMPS=1.
+#ifdef CH_STAMPS
 #define CH_STAMP(k)                                                                                         \
    do                                                                                                      \
    {                                                                                                       \
-      if (a.stamps && threadIdx.x == 0)                                                                     \
-         a.stamps[((uint64_t) tk * len + i) * 16 + (k)] = __builtin_amdgcn_s_memtime();                     \
+      if (a.stamps && lane == 0) a.stamps[((uint64_t) tk * len + i) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
    } while (0)
+#else
+#define CH_STAMP(k) \
+   do             \
+   {              \
+   } while (0)
+#endif
 
 template <int NL>
 __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
 {
-   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+   const uint32_t lane = threadIdx.x;
    const uint64_t wbase = (uint64_t) w << a.dshift;
    const uint64_t wlen = (w + 1 < a.nW) ? (1ull << a.dshift) : OFF_LIM;   // kept offsets: t' - wbase < wlen
    const uint64_t wq = wbase / 1000ull;
@@ -687,53 +567,46 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
    const uint32_t d0 = (uint32_t) (wq - wb);
    const uint32_t len = a.len, nW = a.nW;
    const uint32_t cpb = c * len;
-   const int analytical = a.c.analytical;
+   const uint32_t mode0 = a.c.analytical ? 1u : 0u;
 
-   // ---- prologue: descriptors and insert bounds of ports 0 and 1, port 0's stream;
+   // ---- prologue: descriptors and insert bounds of ports 0 and 1, port 0's inserts;
    // then the pipeline's first prefetches (port 1's inserts, port 2's descriptor and bounds)
-   for (uint32_t x = tid; x < 64u + 4u * NL; x += T)
-   {
-      if (x < 32) load_cp(&sm.cp[0], a.cp + cpb, x);
-      else if (x < 64) { if (len > 1) load_cp(&sm.cp[1], a.cp + cpb + 1, x - 32); }
-      else if (x < 64u + 2u * NL) load_bounds(sm, a, 0, cpb, NL, w, x - 64);
-      else if (len > 1) load_bounds(sm, a, 1, cpb + 1, NL, w, x - 64 - 2 * NL);
-   }
-   if (tid == 0)
-   {
-      sm.abort_ = 0;
-      sm.P0cur = 0;      // port 0 has no chain input
-      sm.nin_prev = 0;
-      sm.ncont_prev = 0;
-   }
-   bar();
+   if (lane < 32) load_cp(&sm.cp[0], a.cp + cpb, lane);
+   else if (len > 1) load_cp(&sm.cp[1], a.cp + cpb + 1, lane - 32);
+   if (lane < 2 * NL) put_bounds(sm, 0, fetch_bounds(a, cpb, NL, w, lane), NL, lane);
+   else if (lane < 4 * NL && len > 1) put_bounds(sm, 1, fetch_bounds(a, cpb + 1, NL, w, lane - 2 * NL), NL, lane - 2 * NL);
+   if (lane == 0) sm.kkey[0] = ~0ull;
+   wsync();
    uint64_t rk[PER];
-   uint32_t ra[PER], ci[PER];
-   Rec iv[IPER];             // the next port's inserts in flight
-   uint32_t itot_cur = 0;    // their count
-   uint32_t cpv = 0, bv = 0; // descriptor / bounds of the port after next, in flight (waves 1 / 2)
+   uint32_t ra[PER];
+   Rec iv[IPER];                 // the next port's inserts in flight
+   uint32_t off_f[NLMAX + 1];    // their lists' offsets
+   uint32_t itot_f = 0;          // their count
+   uint32_t cpv = 0, bv = 0;     // descriptor / bounds of the port after next, in flight
+   uint32_t nK = 0, nI = 0;      // this port's kept records and inserts
+   uint32_t P0cur = 0, nin_prev = 0, ncont_prev = 0;   // this port's chain input: records before / kept / all of this window
    {
-      const uint32_t itot = fetch_inserts<NL>(sm, a, 0, 0, iv);
-      const bool bad = store_inserts<NL>(sm, iv, itot, wbase);
-      if (itot > (uint32_t) ICAP || itot > (uint32_t) CAP)
+      uint32_t off0[NLMAX + 1];
+      nI = fetch_inserts<NL>(sm, a, 0, 0, iv, off0);
+      if (nI > (uint32_t) ICAP)
       {
-         if (tid == 0) flag(a, F_RETRY);
+         if (lane == 0) flag(a, F_RETRY);
          return;
       }
-      if (bad) flag(a, F_FALLBACK);
-      bar();
-      premerge<NL>(sm, itot);
-      bar();
-#pragma unroll
-      for (int j = 0; j < PER; j++) { rk[j] = 0; ra[j] = 0; ci[j] = 0; }
-      merge(sm, 0, itot, rk, ra, ci, 0u, a.exp);
-      if (len > 1) itot_cur = fetch_inserts<NL>(sm, a, 1, 1, iv);
-      if (tid - DESC_T0 < 32u && len > 2) cpv = fetch_cp(a.cp + cpb + 2, tid - DESC_T0);
-      if (tid - BND_T0 < 32u && len > 2) bv = fetch_bounds(a, cpb + 2, NL, w, tid - BND_T0);
+      if (store_inserts<NL>(sm, iv, nI, wbase, 0) && lane == 0) flag(a, F_FALLBACK);
+      premerge<NL>(sm, nI, 0, off0);
+      if (len > 1) itot_f = fetch_inserts<NL>(sm, a, 1, 1, iv, off_f);
+      if (len > 2)
+      {
+         if (lane < 32) cpv = fetch_cp(a.cp + cpb + 2, lane);
+         else bv = fetch_bounds(a, cpb + 2, NL, w, lane - 32);
+      }
    }
 
    for (uint32_t i = 0; i < len; i++)
    {
       const uint32_t cpi = cpb + i;
+      const uint32_t b = i & 1u, bn = b ^ 1u;
       const ChainPort& P = sm.cp[i % 3];
       const bool has_next = i + 1 < len;
       uint64_t* const stw = a.st + ((uint64_t) (a.cp0 + cpi) * nW + w) * SW;          // this window's state
@@ -742,155 +615,150 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       // ---- [A] land last step's prefetches: port i+1's inserts, port i+2's descriptor and
       // bounds; load the predecessor's state of this port
       CH_STAMP(0);
-      const uint32_t itot = itot_cur;
+      const uint32_t itot = itot_f;
+      uint32_t off_c[NLMAX + 1];
+#pragma unroll
+      for (int l = 0; l <= NLMAX; l++) off_c[l] = off_f[l];
       bool ibad = false;
-      if (has_next) ibad = store_inserts<NL>(sm, iv, itot, wbase);
-      if (tid - DESC_T0 < 32u && i + 2 < len) put_cp(&sm.cp[(i + 2) % 3], cpv, tid - DESC_T0);
-      if (tid - BND_T0 < 32u && i + 2 < len) put_bounds(sm, (i + 2) & 1, bv, NL, tid - BND_T0);
+      if (has_next) ibad = store_inserts<NL>(sm, iv, itot, wbase, bn);
+      if (i + 2 < len)
+      {
+         if (lane < 32) put_cp(&sm.cp[(i + 2) % 3], cpv, lane);
+         else put_bounds(sm, (i + 2) & 1, bv, NL, lane - 32);
+      }
       uint64_t pv = 0;
-      if (wv == 0 && w && lane < (uint32_t) SW) pv = ld1(stp + lane);
+      if (w && lane < (uint32_t) SW) pv = ld1(stp + lane);
+      const uint32_t nx = sgpr(P.nx), ny = sgpr(P.ny), cont = sgpr(P.cont), rl = sgpr(P.rl), port = sgpr(P.port);
+      uint32_t ocap[4];
+      uint64_t obase[4];
+#pragma unroll
+      for (int f = 0; f < 4; f++)
+      {
+         ocap[f] = sgpr(P.ocap[f]);
+         obase[f] = sgpr64(P.obase[f]);
+      }
+      wsync();
       CH_STAMP(7);
 
-      const uint32_t nx = sgpr(P.nx), ny = sgpr(P.ny), cont = sgpr(P.cont);
-      uint32_t n = sgpr(sm.n), k = 0, a0 = 0, cnt = 0;
+      const uint64_t* Ic = sm.ikey[b];
+      const uint32_t* IAc = sm.iaux[b];
+      uint32_t n = nK + nI, a0 = 0, cnt = 0;
       Agg ex, tot;
-      bool first = true;
+      bool first = true, published = false;
+      uint32_t Xr = 0, mode = mode0, Kpp = 0, Pep = 0, Kout = 0, Pend = 0;
+      uint32_t cin[4] = { 0, 0, 0, 0 };
       for (;;)
       {
-         // ---- [B][C] the stream: segments, block scan (first pass: no spill-ins yet)
-         k = (n + T - 1) / T;
-         a0 = min(tid * k, n);
-         cnt = min(k, n - a0);
+         // ---- [B][C] this lane's segment of the merged stream, wave scan (first pass: no
+         // spill-ins yet)
          {
-            const Agg g0 = load_segment(sm, a0, cnt, wr, d0, nx, ny, cont, rk, ra);
+            const uint32_t k = (n + T - 1) / T;
+            a0 = min(lane * k, n);
+            cnt = min(k, n - a0);
+            const uint32_t y = mp_split(sm.kkey, nK, Ic, nI, a0);
+            uint32_t yend = 0;
+            const Agg g0 = walk(sm.kkey, sm.kaux, Ic, IAc, a0 - y, y, cnt, wr, d0, nx, ny, cont, rk, ra, yend);
+#ifdef CH_DEBUG
+            // the next lane's split must be where this one's walk ended
+            const uint32_t ynext = (uint32_t) __shfl_down((int) y, 1);
+            if ((lane < 63 && cnt && a0 + cnt < n && ynext != yend) || yend > nI || a0 + cnt - yend > nK)
+               flag(a, F_ROUTE | 64u);
+#endif
             if (first) CH_STAMP(8);
-            block_scan(sm, g0, ex, tot);   // #1
+            const Agg inc = wave_scan(g0);
+            ex.A = dpp32<0x138, 0xF, 0xF>(inc.A);   // exclusive: wave_shr 1
+            ex.B = dpp32<0x138, 0xF, 0xF>(inc.B);
+            ex.C = dpp64<0x138, 0xF, 0xF>(inc.C);
+            tot.A = rdl(inc.A, 63);
+            tot.B = rdl(inc.B, 63);
+            tot.C = rdl64(inc.C, 63);
          }
          if (!first) break;
          CH_STAMP(1);
          first = false;
-         if (ibad) flag(a, F_FALLBACK);
-         // Y ports: the three insert ranges into one sorted list (read after barrier #3)
-         if (has_next) premerge<NL>(sm, itot);
+         if (ibad && lane == 0) flag(a, F_FALLBACK);
+         // Y ports: the three insert ranges into one sorted list (read at the next step)
+         if (has_next) premerge<NL>(sm, itot, bn, off_c);
 
-         // ---- [D] predecessor's state (wave 0)
-         if (wv == 0)
+         // ---- [D] predecessor's state
+         bool ok = true;
+         uint64_t X_in = 0;
+         if (w)
          {
-            uint64_t X_in = 0;
-            uint32_t cin[4] = { 0, 0, 0, 0 };
-            uint32_t mode = analytical ? 1u : 0u, Kpp = 0, Pep = 0;
-            bool ok = true;
-            if (w)
-            {
-               ok = poll_words(a, stp, SW, lane, pv);
-               if (ok)
-               {
-                  X_in = __shfl(pv, 0) & M48;
+            ok = poll_words(a, stp, SW, lane, pv);
+            X_in = rdl64(pv, 0) & M48;
 #pragma unroll
-                  for (int f = 0; f < 4; f++) cin[f] = (uint32_t) (__shfl(pv, 1 + f) & M48);
-                  mode = (uint32_t) (__shfl(pv, 5) & 1u);
-                  Kpp = (uint32_t) (__shfl(pv, 6) & M48);
-                  Pep = (uint32_t) (__shfl(pv, 7) & M48);
-               }
-            }
-            CH_STAMP(2);
-            // window-relative tail: an earlier tail behaves like the base cycle (every tc > wb)
-            const uint64_t xr = X_in > wb ? X_in - wb : 0;
-            if (xr >= (1ull << 31)) ok = false;
-            const uint32_t Xr = (uint32_t) xr;
-            const uint32_t Kout = sm.nin_prev ? sm.P0cur + sm.nin_prev : Kpp;
-            const uint32_t Pend = sm.P0cur + sm.ncont_prev;
-            if (lane == 0)
-            {
-               if (!ok)
-               {
-                  sm.abort_ = 1;
-                  if (xr >= (1ull << 31)) flag(a, F_FALLBACK);
-               }
-               sm.X_in = Xr;
-               for (int f = 0; f < 4; f++) sm.cnt_in[f] = cin[f];
-               sm.mode_in = mode;
-               sm.Kpp = Kpp;
-               sm.Pep = Pep;
-               sm.ssum = 0;
-               sm.n_inwin = 0;
-               sm.first_gap = NONE;
-               sm.first_fire = NONE;
-               sm.sp_skip = 0;
-               sm.sp_take = 0;
-               sm.Kout = Kout;   // this port's spill range after this window (no spill-ins)
-               sm.Pend = Pend;
-            }
-            const bool early = ok && !mode && Pep == Kpp;
-            if (lane == 0) sm.published = early ? 1u : 0u;
-            if (early && lane < (uint32_t) SW)
-            {
-               // inclusive = carry x aggregate, published before the outputs
-               const uint32_t nx0 = Xr + tot.A;
-               uint64_t v = 0;
-               if (lane == 0) v = wb + (nx0 > tot.B ? nx0 : tot.B);
-               else if (lane < 5) v = (uint64_t) (cin[lane - 1] + cf(tot.C, lane - 1));
-               else if (lane == 6) v = Kout;
-               else if (lane == 7) v = Pend;
-               st1(stw + lane, a.etag | v);
-            }
+            for (int f = 0; f < 4; f++) cin[f] = (uint32_t) (rdl64(pv, 1 + f) & M48);
+            mode = (uint32_t) (rdl64(pv, 5) & 1u);
+            Kpp = (uint32_t) (rdl64(pv, 6) & M48);
+            Pep = (uint32_t) (rdl64(pv, 7) & M48);
          }
-         bar();   // #2
+         CH_STAMP(2);
+         if (!ok) return;
+         // window-relative tail: an earlier tail behaves like the base cycle (every tc > wb)
+         const uint64_t xr = X_in > wb ? X_in - wb : 0;
+         if (xr >= (1ull << 31))
+         {
+            if (lane == 0) flag(a, F_FALLBACK);
+            return;
+         }
+         Xr = (uint32_t) xr;
+         Kout = nin_prev ? P0cur + nin_prev : Kpp;   // this port's spill range after this window
+         Pend = P0cur + ncont_prev;
+         // publish before the outputs unless spill-ins change the stream or the history
+         // tree has had no gap yet (then the outputs decide)
+         published = !mode && Pep == Kpp;
+         if (published && lane < (uint32_t) SW)
+         {
+            const uint32_t nx0 = Xr + tot.A;
+            st1(stw + lane, a.etag | state_word(lane, wb + (nx0 > tot.B ? nx0 : tot.B), cin, tot.C, 0u, Kout, Pend));
+         }
          CH_STAMP(3);
-         if (sm.abort_) return;
          // next prefetches (they land at the next step's [A]): port i+2's inserts (its
          // descriptor and bounds landed at this step's [A]), port i+3's descriptor and bounds
-         if (i + 2 < len) itot_cur = fetch_inserts<NL>(sm, a, (i + 2) % 3, (i + 2) & 1, iv);
-         if (tid - DESC_T0 < 32u && i + 3 < len) cpv = fetch_cp(a.cp + cpi + 3, tid - DESC_T0);
-         if (tid - BND_T0 < 32u && i + 3 < len) bv = fetch_bounds(a, cpi + 3, NL, w, tid - BND_T0);
-         if (sm.Pep == sm.Kpp) break;
-         // ---- slow path: spill-ins (about one step in twenty)
-         const uint32_t Kpp = sm.Kpp, spn = sm.Pep - sm.Kpp;
-         const bool sok = i > 0 && spn + min(itot, (uint32_t) ICAP) <= (uint32_t) ICAP &&
-                          (uint64_t) Kpp + spn <= a.cp[cpi - 1].ocap[1];
+         if (i + 2 < len) itot_f = fetch_inserts<NL>(sm, a, (i + 2) % 3, (i + 2) & 1, iv, off_f);
+         if (i + 3 < len)
+         {
+            if (lane < 32) cpv = fetch_cp(a.cp + cpi + 3, lane);
+            else bv = fetch_bounds(a, cpi + 3, NL, w, lane - 32);
+         }
+         if (Pep == Kpp) break;
+         // ---- slow path: spill-ins join the insert list, then rescan
+         const uint32_t spn = Pep - Kpp;
+         const bool sok = i > 0 && spn + nI <= (uint32_t) ICAP && (uint64_t) Kpp + spn <= a.cp[cpi - 1].ocap[1];
          if (!sok)
          {
-            if (tid == 0) flag(a, F_FALLBACK);
+            if (lane == 0) flag(a, F_FALLBACK);
             return;
          }
-         const uint32_t take = spill_in(sm, a, a.cp[cpi - 1].obase[1] + Kpp, spn, itot, n, wbase, wlen, rk, ra, a0, cnt);
+         uint32_t skip = 0;
+         const uint32_t take = spill_in(sm, a, a.cp[cpi - 1].obase[1] + Kpp, spn, Ic, IAc, nI, wbase, wlen, skip);
          if (n + take > (uint32_t) CAP)
          {
-            if (tid == 0) flag(a, F_RETRY);
+            if (lane == 0) flag(a, F_RETRY);
             return;
          }
-         if (tid == 0 && !sm.nin_prev) sm.Kout = Kpp + sm.sp_skip + take;   // the consumed prefix of the old spills
-         n += take;   // rescan (the stream changed)
-         if (!take) first = true;   // nothing merged: the scan stands
-         if (!take) break;
+         if (!nin_prev) Kout = Kpp + skip + take;   // the consumed prefix of the old spills
+         if (!take) break;   // nothing merged: the scan stands
+         Ic = sm.rkey;
+         IAc = sm.raux;
+         nI += take;
+         n += take;          // rescan (the stream changed)
       }
-      if (!sm.published)
+      // publish now (unless the history tree still has no gap: after the outputs)
+      if (!published && !mode && lane < (uint32_t) SW)
       {
-         bar();
-         // publish now (unless the history tree still has no gap: after the outputs)
-         if (wv == 0 && !sm.mode_in && lane < (uint32_t) SW)
-         {
-            const uint32_t nx0 = sm.X_in + tot.A;
-            uint64_t v = 0;
-            if (lane == 0) v = wb + (nx0 > tot.B ? nx0 : tot.B);
-            else if (lane < 5) v = (uint64_t) (sm.cnt_in[lane - 1] + cf(tot.C, lane - 1));
-            else if (lane == 6) v = sm.Kout;
-            else if (lane == 7) v = sm.Pend;
-            st1(stw + lane, a.etag | v);
-         }
+         const uint32_t nx0 = Xr + tot.A;
+         st1(stw + lane, a.etag | state_word(lane, wb + (nx0 > tot.B ? nx0 : tot.B), cin, tot.C, 0u, Kout, Pend));
       }
 
-      // ---- [E] recurrence, outputs; kept records overwrite rk (new key) in place
-      const uint32_t Xin = sgpr(sm.X_in);
-      const uint32_t mode_in = sgpr(sm.mode_in);
-      uint32_t X = Xin + ex.A;
+      // ---- [E] recurrence, outputs: kept records in place into the kept list
+      uint32_t X = Xr + ex.A;
       X = X > ex.B ? X : ex.B;
       uint32_t run[4];
 #pragma unroll
-      for (int f = 0; f < 4; f++) run[f] = sgpr(sm.cnt_in[f]) + cf(ex.C, f);
-      const uint32_t P0n = sgpr(sm.cnt_in[1]);   // chain-direction records before this window
-      const uint32_t rl = sgpr(P.rl);
-      uint32_t km = 0;
+      for (int f = 0; f < 4; f++) run[f] = cin[f] + cf(ex.C, f);
+      const uint32_t P0n = cin[1];   // chain-direction records before this window
       uint64_t ssum = 0;
       uint32_t nkeep = 0, fgap = NONE, ffire = NONE;
       bool spilled = false, bad = false, route = false;
@@ -907,7 +775,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          const uint32_t Xb = X;
          const uint32_t cc = Xb > tc ? Xb - tc : 0;
          X = (Xb > tc ? Xb : tc) + p;
-         if (mode_in)
+         if (mode)
          {
             // history tree with no gap yet: an idle period makes one (:79-86); the M/G/1
             // branch fires while there is none and the tail lies beyond t + p (:58-64)
@@ -921,17 +789,22 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
 #pragma unroll
          for (int q = 0; q < 4; q++)
             if (f == (uint32_t) q) pos = run[q]++;
-         if (f == 1 && dn < wlen)
+         if (f == 1)
          {
-            km |= 1u << j;
-            rk[j] = (dn << 32) | id;
-            ci[j] = pos - P0n;
-            nkeep++;
-            continue;
+            // continuing: kept (a prefix of the window's continuing records) or spilled;
+            // a spill marks the kept list's end (~0 at its index, the first one counts)
+            const uint32_t ci = pos - P0n;
+            const bool keep = dn < wlen;
+            sm.kkey[pad(ci)] = keep ? ((dn << 32) | id) : ~0ull;
+            if (keep)
+            {
+               sm.kaux[pad(ci)] = ax;
+               nkeep++;
+               continue;
+            }
          }
-         if (pos >= P.ocap[f]) { route = true; continue; }
-         if (a.exp & 1u) continue;
-         const uint64_t gp = P.obase[f] + pos;
+         if (pos >= ocap[f]) { route = true; continue; }
+         const uint64_t gp = obase[f] + pos;
          const uint64_t tn = wbase + dn;
          if (f == 1)
          {
@@ -957,86 +830,66 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          }
       }
       CH_STAMP(13);
-      // kept keys at their index (the search array of the next merge: the stream's
-      // own reads all happened before barrier #1)
-#pragma unroll
-      for (int j = 0; j < PER; j++)
-         if ((km >> j) & 1u) sm.key[pad(ci[j])] = rk[j];
-      if (route) flag(a, F_ROUTE);
-      if (bad) flag(a, F_FALLBACK);
-      // block reductions: queue delay sum, kept records, first gap / M/G/1 condition
-      ssum = wave_sum64(ssum);
-      nkeep = wave_sum32(nkeep);
-      if (lane == 63)
-      {
-         if (ssum) atomicAdd((unsigned long long*) &sm.ssum, (unsigned long long) ssum);
-         if (nkeep) atomicAdd(&sm.n_inwin, nkeep);
-      }
-      if (mode_in)
-      {
-         if (fgap != NONE) atomicMin(&sm.first_gap, fgap);
-         if (ffire != NONE) atomicMin(&sm.first_fire, ffire);
-      }
+      // the kept list's end when nothing spilled
+      if (lane == 0) sm.kkey[pad(cf(tot.C, 1))] = ~0ull;
+      if (__any(route) && lane == 0) flag(a, F_ROUTE);
+      if (__any(bad) && lane == 0) flag(a, F_FALLBACK);
+      // wave reductions: queue delay sum, kept records, first gap / M/G/1 condition
+      const uint64_t ssw = rdl64(wave_sum64(ssum), 63);
+      const uint32_t nin = rdl(wave_sum32(nkeep), 63);
       if (__any(spilled)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drained before the next publish
-      bar();   // #3
+      wsync();
       CH_STAMP(4);
 
-      // ---- [F] late publish (no gap yet), port counters, route check (wave 0)
-      const uint32_t nin = sm.n_inwin;
-      if (wv == 0)
+      // ---- [F] late publish (no gap yet), port counters, route check
+      const uint32_t nx0 = Xr + tot.A;
+      const uint64_t Xo = wb + (nx0 > tot.B ? nx0 : tot.B);
+      if (!published && mode)
       {
-         const uint32_t nx0 = Xin + tot.A;
-         const uint64_t Xo = wb + (nx0 > tot.B ? nx0 : tot.B);
-         if (!sm.published && mode_in && lane < (uint32_t) SW)
+         // the records are in lane order: the first lane with a gap / firing holds the first
+         const uint64_t mg = __ballot(fgap != NONE), mf = __ballot(ffire != NONE);
+         const uint32_t fg = mg ? rdl(fgap, __builtin_ctzll(mg)) : NONE;
+         const uint32_t ff = mf ? rdl(ffire, __builtin_ctzll(mf)) : NONE;
+         // the M/G/1 branch would serve a request that arrives before the first gap
+         if (lane == 0 && ff != NONE && (fg == NONE || ff < fg)) flag(a, F_FALLBACK);
+         if (lane < (uint32_t) SW)
+            st1(stw + lane, a.etag | state_word(lane, Xo, cin, tot.C, fg == NONE ? 1u : 0u, Kout, Pend));
+      }
+      if (lane == 0)
+      {
+         if (w + 1 == nW)
          {
-            const uint32_t fg = sm.first_gap, ff = sm.first_fire;
-            // the M/G/1 branch would serve a request that arrives before the first gap
-            if (lane == 0 && ff != NONE && (fg == NONE || ff < fg)) flag(a, F_FALLBACK);
-            uint64_t v = 0;
-            if (lane == 0) v = Xo;
-            else if (lane < 5) v = (uint64_t) (sm.cnt_in[lane - 1] + cf(tot.C, lane - 1));
-            else if (lane == 5) v = (fg == NONE) ? 1u : 0u;   // still no gap after this window
-            else if (lane == 6) v = sm.Kout;
-            else v = sm.Pend;
-            st1(stw + lane, a.etag | v);
+            // every record of the port has passed: the route counts fill every output slot
+            bool full = true;
+            for (uint32_t f = 0; f < 4; f++) full &= cin[f] + cf(tot.C, f) == ocap[f];
+            if (!full) flag(a, F_ROUTE);
          }
-         if (lane == 0)
+         if (n)
          {
-            if (w + 1 == nW)
-            {
-               // every record of the port has passed: the route counts fill every output slot
-               bool full = true;
-               for (uint32_t f = 0; f < 4; f++) full &= sm.cnt_in[f] + cf(tot.C, f) == P.ocap[f];
-               if (!full) flag(a, F_ROUTE);
-            }
-            if (n)
-            {
-               const uint32_t port = P.port;
-               atomicAdd(&a.port_sum[port], (unsigned long long) sm.ssum);
-               atomicAdd(&a.port_cnt[port], (unsigned long long) n);
-               atomicAdd(&a.port_flit[port], (unsigned long long) tot.A);
-               atomicMax(&a.port_last[port], (unsigned long long) Xo);
-            }
-            // the next port's chain input: records before this window, kept, all of this window
-            sm.P0cur = sm.cnt_in[1];
-            sm.nin_prev = nin;
-            sm.ncont_prev = cf(tot.C, 1);
+            atomicAdd(&a.port_sum[port], (unsigned long long) ssw);
+            atomicAdd(&a.port_cnt[port], (unsigned long long) n);
+            atomicAdd(&a.port_flit[port], (unsigned long long) tot.A);
+            atomicMax(&a.port_last[port], (unsigned long long) Xo);
          }
       }
+      // the next port's chain input: records before this window, kept, all of this window
+      P0cur = cin[1];
+      nin_prev = nin;
+      ncont_prev = cf(tot.C, 1);
       CH_STAMP(9);
+#ifdef CH_STAMPS
+      if (a.stamps && lane == 0)
+         a.stamps[((uint64_t) tk * len + i) * 16 + 6] = (uint64_t) n | ((uint64_t) itot << 16) |
+                                                     ((uint64_t) nin << 32) | ((uint64_t) (Pep != Kpp) << 63);
+#endif
       if (!has_next) break;
-      if (itot > (uint32_t) ICAP || nin + itot > (uint32_t) CAP)   // (every thread knows both)
+      if (itot > (uint32_t) ICAP || nin + itot > (uint32_t) CAP)
       {
-         if (tid == 0) flag(a, F_RETRY);
+         if (lane == 0) flag(a, F_RETRY);
          return;
       }
-      // ---- [G] next port's stream: kept records + its inserts
-      merge(sm, nin, itot, rk, ra, ci, km, a.exp,
-            a.stamps ? a.stamps + ((uint64_t) tk * len + i) * 16 : nullptr);   // #4, #5
-      CH_STAMP(5);
-      if (a.stamps && tid == 0)
-         a.stamps[((uint64_t) tk * len + i) * 16 + 6] = (uint64_t) n | ((uint64_t) itot << 16) |
-                                                     ((uint64_t) nin << 32) | ((uint64_t) (sm.Pep != sm.Kpp) << 63);
+      nK = nin;
+      nI = itot;
    }
 }
 
@@ -1044,25 +897,24 @@ template <int NL>
 __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
 {
    __shared__ Smem sm;
-   const uint32_t tid = threadIdx.x;
    const uint32_t ntasks = a.nch * a.nW;
    // an earlier level served a request by M/G/1 (exception tails): the chain's
    // inputs are not in FIFO order -> the level engine reruns the batch
    if (a.errflag[2] != 0)
    {
-      if (tid == 0 && blockIdx.x == 0) flag(a, F_FALLBACK);
+      if (threadIdx.x == 0 && blockIdx.x == 0) flag(a, F_FALLBACK);
       return;
    }
    for (;;)
    {
       // window-major, strictly in order to running workgroups: a task's predecessor
       // (same chain, window - 1) is always held by a running workgroup or done
-      if (tid == 0) sm.next_task = atomicAdd(a.ctr, 1u);
-      bar();
-      const uint32_t tk = sm.next_task;
+      uint32_t tk = 0;
+      if (threadIdx.x == 0) tk = atomicAdd(a.ctr, 1u);
+      tk = rdl(tk, 0);
       if (tk >= ntasks || flagged(a)) return;
       task<NL>(sm, a, tk % a.nch, tk / a.nch, tk);
-      bar();
+      wsync();
    }
 }
 

@@ -1340,7 +1340,12 @@ static int run_post(gnoc_engine* e, bool closed_form)
    const unsigned errf = ef[0];
    if (e->used_chain && (ef[4] & ch::F_ANY))
    {
-      if (ef[4] & ch::F_ROUTE) return fail(e, GNOC_EHIP, "internal: chain route-count invariant violated");
+      if (ef[4] & ch::F_ROUTE)
+      {
+         char m[96];
+         std::snprintf(m, sizeof m, "internal: chain route-count invariant violated (flags 0x%x)", ef[4]);
+         return fail(e, GNOC_EHIP, m);
+      }
       return (ef[4] & (ch::F_FALLBACK | ch::F_TIMEOUT)) ? GNOC_CH_FALLBACK : GNOC_CH_RETRY;
    }
    // a leaf the splitter could not cut (or a look-back timeout) leaves garbage

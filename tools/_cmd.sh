@@ -1,6 +1,8 @@
 mkdir -p gpurun_out
-for L in libgnoc_64a.so libgnoc_64b.so libgnoc_128.so libgnoc.so; do
-  GNOC_LIB=$PWD/graphite_amd/_build/$L timeout -k 10 120 python -u bench.py --steps 5 --warmup 1 --cpu-baseline 0 > gpurun_out/b_$L.json 2> gpurun_out/b_$L.err || { tail -5 gpurun_out/b_$L.err; exit 1; }
-  python3 -c "import json,sys; d=json.load(open('gpurun_out/b_$L.json')); k=d['kernel_ms']; print('$L', round(d['value']/1e9,2), 'G hops/s', round(d['ms_per_step'],3), 'ms chain', k['k_chain'], 'level', k['k_level'])"
-done
-GNOC_LIB=$PWD/graphite_amd/_build/libgnoc_64a.so timeout -k 10 300 python -u tools/chain_check.py > gpurun_out/cc7.log 2>&1; tail -4 gpurun_out/cc7.log
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_r2a.log 2>&1; rc=$?
+tail -5 gpurun_out/pytest_r2a.log; grep -E "PASSED|FAILED|ERROR" gpurun_out/pytest_r2a.log | awk '{print $NF}' | sort | uniq -c
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u tools/chain_check.py > gpurun_out/cc_r2a.log 2>&1; echo cc rc=$?; tail -1 gpurun_out/cc_r2a.log
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 > gpurun_out/bench_r2a.json 2> gpurun_out/bench_r2a.err; echo bench rc=$?
+cat gpurun_out/bench_r2a.json

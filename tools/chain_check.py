@@ -25,7 +25,12 @@ def check(name, cfg, tr, shift=None):
     eng = gnoc.Engine(cfg)
     eng.submit(tr)
     t0 = time.perf_counter()
-    eng.run()
+    try:
+        eng.run()
+    except gnoc.GnocError as ex:
+        print(f"{name:40s} shift={shift} ERROR {ex}", flush=True)
+        eng.close()
+        return False
     dt = time.perf_counter() - t0
     got = eng.results()
     s = eng.summary()
@@ -39,7 +44,8 @@ def check(name, cfg, tr, shift=None):
             i = np.nonzero(a != b)[0]
             bad.append(f"{f}: {i.size} differ, first {i[0]} gpu {a[i[0]]} ref {b[i[0]]}")
     print(f"{name:40s} shift={shift} path={s['engine_path']} pkts={len(tr)} hops={s['mesh_hops']} "
-          f"gpu_ms={s['last_run_ms']:.2f} wall={dt*1e3:.1f} {'OK' if not bad else 'FAIL'}", flush=True)
+          f"gpu_ms={s['last_run_ms']:.2f} wall={dt*1e3:.1f} W={s['windows']}/{s['window_shift']} "
+          f"retry={s['retries']} fb={s['fallbacks']} {'OK' if not bad else 'FAIL'}", flush=True)
     for b in bad:
         print("   ", b, flush=True)
     return not bad

@@ -7,8 +7,8 @@ stamps and prints where a step's time goes:
   wait  = wave 0 polling the predecessor window's state of this port
   d     = rest of [D] up to barrier 2
   emit  = [E] recurrence + stores + reductions (to barrier 3)
-  merge = [F] + [G] merge into the next port's stream
-  gap   = end of step -> start of the next step
+  F     = [F] wave 0's late publish and port counters
+  gap   = end of [F] -> start of the next step
 Usage: python tools/chain_stamps.py [W] [load] [ppt]
 """
 import ctypes
@@ -53,10 +53,10 @@ def main():
         n = (info & 0xFFFF).astype(np.int64)
         itot = ((info >> 16) & 0xFFFF).astype(np.int64)
         spill = (info >> 63).astype(bool)
-        ok = (t[:, :-1, 5] > 0) & (t[:, :-1, 0] > 0)
+        ok = (st[:, :-1, 9] > 0) & (t[:, :-1, 0] > 0) & (t[:, 1:, 0] > 0)
         d = {
             "A": st[:, :-1, 7] - st[:, :-1, 0],
-            "load": st[:, :-1, 8] - st[:, :-1, 7],
+            "walk": st[:, :-1, 8] - st[:, :-1, 7],
             "bscan": st[:, :-1, 1] - st[:, :-1, 8],
             "wait": t[:, :-1, 2] - t[:, :-1, 1],
             "d": t[:, :-1, 3] - t[:, :-1, 2],
@@ -64,10 +64,7 @@ def main():
             "Eloop": st[:, :-1, 13] - st[:, :-1, 12],
             "Epost": st[:, :-1, 4] - st[:, :-1, 13],
             "F": st[:, :-1, 9] - st[:, :-1, 4],
-            "msrch": st[:, :-1, 10] - st[:, :-1, 9],
-            "mbar": st[:, :-1, 11] - st[:, :-1, 10],
-            "mwrite": st[:, :-1, 5] - st[:, :-1, 11],
-            "gap": t[:, 1:, 0] - t[:, :-1, 5],
+            "gap": t[:, 1:, 0] - st[:, :-1, 9],
         }
         print(f"phase {'XY'[phase]}: chains {nch} windows {nW} len {ln} shift {sh} steps {ok.sum()}")
         tot = np.zeros(ok.sum())
@@ -78,7 +75,7 @@ def main():
         print(f"  step   mean {tot.mean():8.0f}  med {np.median(tot):8.0f}")
         print(f"  records/step mean {n[:, :-1][ok].mean():.0f} max {n.max()}  inserts/step mean {itot[:, :-1][ok].mean():.1f}"
               f"  slow-path steps {spill[:, :-1][ok].mean()*100:.1f}%")
-        task_t = t[:, -1, 4] - t[:, 0, 0]
+        task_t = st[:, -1, 9] - t[:, 0, 0]
         good = t[:, 0, 0] > 0
         print(f"  task duration med {np.median(task_t[good]):.0f} cyc; span of phase {t[good][:, :, 0].max() - t[good][:, 0, 0].min()} cyc")
         # wait vs window index
