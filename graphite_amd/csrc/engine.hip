@@ -100,6 +100,7 @@ struct gnoc_engine
    const uint64_t* d_inj = nullptr;
    const uint32_t *d_src = nullptr, *d_dst = nullptr, *d_bits = nullptr, *d_flags = nullptr;
    DevBuf t_inj, t_src, t_dst, t_bits, t_flags;
+   DevBuf vbuf;                             // submit-time checks and statistics (k_validate)
 
    // work
    DevBuf aux, routed, final_ps, zl, cont;
@@ -570,99 +571,74 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
    e->ch_nw = (uint32_t) nw;
 }
 
-static int validate_host_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n, uint64_t* records)
+// The submitted trace's contract checks and statistics, on the device
+// (prep.hip k_validate over e->d_*): the first offending packet of any check,
+// the hop records this engine materialises, the turn exchange counts of a
+// sharded engine, and the chain engine's window size from the busiest port.
+static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t* nbc)
 {
-   const uint32_t N = e->dc.N, W = e->dc.W, H = e->dc.H;
-   const uint32_t nr = (uint32_t) e->nranks;
-   uint64_t rec = 0;
-   // turn records per (row band of sy, column band of dx), shard.hip
+   const uint32_t N = e->dc.N, W = e->dc.W, H = e->dc.H, nr = (uint32_t) e->nranks;
+   hipStream_t s = e->stream;
+   const size_t nd = (size_t) 2 * H * (W + 1) + (size_t) 2 * W * (H + 1);   // difference arrays (int)
+   const size_t ni = (size_t) 4 * N;                                       // inserts per X / Y port
+   const size_t off_x = (sizeof(ValOut) + (nd + ni) * 4 + 7) / 8 * 8;
+   const size_t bytes = off_x + (size_t) nr * nr * 8;
+   static_assert(sizeof(ValOut) <= 128, "ValOut lands in the 128-B pinned staging");
+   GNOC_HIP(e, e->vbuf.ensure(bytes));
+   GNOC_HIP(e, hipMemsetAsync(e->vbuf.p, 0, bytes, s));
+   GNOC_HIP(e, hipMemsetAsync(e->vbuf.p, 0xFF, sizeof(unsigned long long) * VB_KINDS, s));
+   char* base = static_cast<char*>(e->vbuf.p);
+   ValOut* vo = reinterpret_cast<ValOut*>(base);
+   int* dxr = reinterpret_cast<int*>(base + sizeof(ValOut));
+   int* dxl = dxr + (size_t) H * (W + 1);
+   int* dyu = dxl + (size_t) H * (W + 1);
+   int* dyd = dyu + (size_t) W * (H + 1);
+   uint32_t* insx = reinterpret_cast<uint32_t*>(dyd + (size_t) W * (H + 1));
+   uint32_t* insy = insx + 2 * (size_t) N;
+   unsigned long long* xcnt = reinterpret_cast<unsigned long long*>(base + off_x);
+   if (n)
+   {
+      const uint32_t grid = (uint32_t) std::min<uint64_t>((n + 255) / 256, 4096);
+      const int tree = e->cfg.broadcast_tree_enabled && !e->dc.hop_counter;
+      hipLaunchKernelGGL(k_validate, dim3(grid), dim3(256), 0, s, e->dc, (uint64_t) n, e->d_inj, e->d_src, e->d_dst,
+                         e->d_bits, e->d_flags, tree, e->npoints > 1 ? 1u : 0u, nr, (uint32_t) e->rank, vo, dxr, dxl, dyu,
+                         dyd, insx, insy, xcnt);
+      GNOC_HIP(e, hipGetLastError());
+      hipLaunchKernelGGL(k_validate_max, dim3(1), dim3(1024), 0, s, W, H, dxr, dxl, dyu, dyd, insx, insy, vo);
+      GNOC_HIP(e, hipGetLastError());
+   }
+   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, vo, sizeof(ValOut), hipMemcpyDeviceToHost, s));
    e->x_cnt.assign((size_t) nr * nr, 0);
-   std::vector<uint32_t> rb(H), cb(W);
-   for (uint32_t b = 0; b < nr; b++)
+   if (nr > 1) GNOC_HIP(e, hipMemcpyAsync(e->x_cnt.data(), xcnt, (size_t) nr * nr * 8, hipMemcpyDeviceToHost, s));
+   GNOC_HIP(e, hipStreamSynchronize(s));
+   ValOut v;
+   std::memcpy(&v, e->h_pinned, sizeof v);
+   // the first offending packet (one check per packet: the first that fails)
+   uint32_t k = VB_KINDS;
+   for (uint32_t q = 0; q < VB_KINDS; q++)
+      if (v.bad[q] != ~0ull && (k == VB_KINDS || v.bad[q] < v.bad[k])) k = q;
+   if (k != VB_KINDS)
    {
-      for (uint32_t y = band_lo(b, nr, H); y < band_lo(b + 1, nr, H); y++) rb[y] = b;
-      for (uint32_t x = band_lo(b, nr, W); x < band_lo(b + 1, nr, W); x++) cb[x] = b;
-   }
-   e->h_bid.clear();
-   // chain engine window sizing (chain.hip): records per port over the batch,
-   // from difference arrays along each row (X ports) and column (Y ports), and
-   // insert records per port (first-hop records of X ports, Y-leg starts)
-   std::vector<int32_t> dxr((size_t) H * (W + 1), 0), dxl((size_t) H * (W + 1), 0);
-   std::vector<int32_t> dyu((size_t) W * (H + 1), 0), dyd((size_t) W * (H + 1), 0);
-   std::vector<uint32_t> insx((size_t) N * 2, 0), insy((size_t) N * 2, 0);
-   for (size_t i = 0; i < n; i++)
-   {
-      const uint32_t s = pk->src[i], fl = pk->flags ? pk->flags[i] : 0u;
-      const bool bc = (fl & GNOC_PKT_BROADCAST) != 0;
-      const uint32_t d = bc ? s : pk->dst[i];   // a broadcast's receiver field is ignored
-      if (s >= N || d >= N) return fail(e, GNOC_ETRACE, "tile id out of range at packet " + std::to_string(i));
-      if (bc)
+      const std::string at = std::to_string(v.bad[k]);
+      switch (k)
       {
-         // Network::netSend sends one packet per tile when the model has no broadcast
-         // capability (network.cc:186-195): the caller expands those.
-         if (!e->cfg.broadcast_tree_enabled || e->dc.hop_counter)
-            return fail(e, GNOC_EINVAL, "broadcast packet " + std::to_string(i) +
+         case VB_TILE: return fail(e, GNOC_ETRACE, "tile id out of range at packet " + at);
+         case VB_BC_TREE:
+            // Network::netSend sends one packet per tile when the model has no broadcast
+            // capability (network.cc:186-195): the caller expands those.
+            return fail(e, GNOC_EINVAL, "broadcast packet " + at +
                                             " but the model has no broadcast tree (the caller expands it, network.cc:186-195)");
-         if (nr > 1 || e->npoints > 1)
-            return fail(e, GNOC_EUNSUPPORTED, "broadcast packets on a sharded or sweep engine");
-         e->h_bid.push_back((uint32_t) i);
-      }
-      if (i && pk->inject_ps[i] < pk->inject_ps[i - 1]) return fail(e, GNOC_ETRACE, "trace not ordered by inject_ps at packet " + std::to_string(i));
-      const uint32_t fw = fw_host(e, s);
-      const uint32_t F = (pk->bits[i] + fw - 1) / fw;
-      if (e->npoints > 1 && point_of(e->dc, s) != point_of(e->dc, d))
-         return fail(e, GNOC_ETRACE, "sweep packet crosses sweep points at packet " + std::to_string(i));
-      const bool bypass = (!bc && s == d) || (fl & GNOC_PKT_UNMODELED);
-      if (F == 0 && !bypass) return fail(e, GNOC_ETRACE, "zero-flit packet " + std::to_string(i));
-      if (F > AUX_F_MAX) return fail(e, GNOC_EUNSUPPORTED, "packet longer than 2047 flits");
-      if (!bypass && bc) rec += 2ull * N;   // injection + N SELF + N - 1 tree edges
-      else if (!bypass)
-      {
-         const int64_t sx = s % W, sy = s / W, dx = d % W, dy = d / W;
-         const uint64_t ax = (uint64_t) std::llabs(sx - dx), ay = (uint64_t) std::llabs(sy - dy);
-         if (dx > sx) { dxr[sy * (W + 1) + sx]++; dxr[sy * (W + 1) + dx]--; insx[s * 2]++; }
-         else if (dx < sx) { dxl[sy * (W + 1) + dx + 1]++; dxl[sy * (W + 1) + sx + 1]--; insx[s * 2 + 1]++; }
-         if (dy > sy) { dyu[dx * (H + 1) + sy]++; dyu[dx * (H + 1) + dy]--; insy[(sy * W + dx) * 2]++; }
-         else if (dy < sy) { dyd[dx * (H + 1) + dy + 1]++; dyd[dx * (H + 1) + sy + 1]--; insy[(sy * W + dx) * 2 + 1]++; }
-         if (nr <= 1) rec += 2 + ax + ay;
-         else
-         {
-            // records this rank materialises: injection + X leg in its row band (all
-            // injections when prep is not band-local), the turn record on either side,
-            // the Y leg in its column band
-            const bool r_own = rb[sy] == (uint32_t) e->rank, c_own = cb[dx] == (uint32_t) e->rank;
-            const bool band_prep = W <= 64 && H <= 64;
-            rec += (r_own ? 1 + ax : 0) + (!r_own && !band_prep ? 1 : 0) + (r_own || c_own ? 1 : 0) + (c_own ? ay : 0);
-            if (e->dc.contention) e->x_cnt[(size_t) rb[sy] * nr + cb[dx]]++;
-         }
+         case VB_BC_SHARD: return fail(e, GNOC_EUNSUPPORTED, "broadcast packets on a sharded or sweep engine");
+         case VB_ORDER: return fail(e, GNOC_ETRACE, "trace not ordered by inject_ps at packet " + at);
+         case VB_SWEEP: return fail(e, GNOC_ETRACE, "sweep packet crosses sweep points at packet " + at);
+         case VB_ZERO_F: return fail(e, GNOC_ETRACE, "zero-flit packet " + at);
+         case VB_F_MAX: return fail(e, GNOC_EUNSUPPORTED, "packet longer than 2047 flits (packet " + at + ")");
+         default: return fail(e, GNOC_EUNSUPPORTED, "inject time beyond 2^50 ps at packet " + at);
       }
    }
-   if (n && pk->inject_ps[n - 1] >= (1ull << 50)) return fail(e, GNOC_EUNSUPPORTED, "inject time beyond 2^50 ps");
-   uint64_t pmax = 0, imax = 0;
-   for (uint32_t r = 0; r < H; r++)
-   {
-      int64_t a = 0, b = 0;
-      for (uint32_t x = 0; x <= W; x++)
-      {
-         a += dxr[r * (W + 1) + x];
-         b += dxl[r * (W + 1) + x];
-         pmax = std::max<uint64_t>(pmax, (uint64_t) std::max<int64_t>(a, b));
-      }
-   }
-   for (uint32_t x = 0; x < W; x++)
-   {
-      int64_t a = 0, b = 0;
-      for (uint32_t y = 0; y <= H; y++)
-      {
-         a += dyu[x * (H + 1) + y];
-         b += dyd[x * (H + 1) + y];
-         pmax = std::max<uint64_t>(pmax, (uint64_t) std::max<int64_t>(a, b));
-      }
-   }
-   for (uint32_t v : insx) imax = std::max<uint64_t>(imax, v);
-   for (uint32_t v : insy) imax = std::max<uint64_t>(imax, v);
-   choose_windows(e, pmax, imax, n ? pk->inject_ps[n - 1] : 0);
-   *records = rec;
+   choose_windows(e, v.pmax, v.imax, n ? v.tlast : 0);
+   *records = v.records;
+   *nbc = v.nbc;
    return GNOC_OK;
 }
 
@@ -745,10 +721,7 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    if (!e || !pk) return GNOC_EINVAL;
    if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return fail(e, GNOC_EINVAL, "null trace array");
    if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
-   uint64_t records = 0;
-   int rc = validate_host_trace(e, pk, n, &records);
-   if (rc) return rc;
-   if (record_bound(e, records) >= (1ull << 31)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^31 hop records");
+   e->submitted = false;
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    GNOC_HIP(e, e->t_inj.ensure(n * 8));
    GNOC_HIP(e, e->t_src.ensure(n * 4));
@@ -765,7 +738,6 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
          GNOC_HIP(e, hipMemcpyAsync(e->t_flags.p, pk->flags, n * 4, hipMemcpyHostToDevice, e->stream));
       else
          GNOC_HIP(e, hipMemsetAsync(e->t_flags.p, 0, n * 4, e->stream));
-      GNOC_HIP(e, hipStreamSynchronize(e->stream));
    }
    e->d_inj = e->t_inj.as<uint64_t>();
    e->d_src = e->t_src.as<uint32_t>();
@@ -774,7 +746,15 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    e->d_flags = e->t_flags.as<uint32_t>();
    e->n = n;
    e->dc.npk = n;
+   uint64_t records = 0, nbc = 0;
+   int rc = device_validate(e, n, &records, &nbc);   // (its sync also ends the copies)
+   if (rc) return rc;
+   if (record_bound(e, records) >= (1ull << 31)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^31 hop records");
    e->rec_bound = record_bound(e, records);
+   e->h_bid.clear();
+   if (nbc)
+      for (size_t i = 0; i < n; i++)
+         if (pk->flags[i] & GNOC_PKT_BROADCAST) e->h_bid.push_back((uint32_t) i);
    rc = upload_broadcasts(e);
    if (rc) return rc;
    rc = build_exchange(e);
@@ -791,6 +771,8 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return fail(e, GNOC_EINVAL, "null trace array");
    if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
    if (e->nranks > 1) return fail(e, GNOC_EUNSUPPORTED, "a sharded engine takes host traces (gnoc_submit)");
+   e->submitted = false;
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
    e->d_inj = pk->inject_ps;
    e->d_src = pk->src;
    e->d_dst = pk->dst;
@@ -798,35 +780,19 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    e->d_flags = pk->flags;
    e->n = n;
    e->dc.npk = n;
-   e->ch_shift = 0;   // no host trace to size the chain engine's windows: level engine
-   e->ch_nw = 0;
-   e->h_bid.clear();
-   int brc = upload_broadcasts(e);
-   if (brc) return brc;
-   // size the record buffers from the trace (route-static): classify once now
-   GNOC_HIP(e, hipSetDevice(e->cfg.device));
-   GNOC_HIP(e, e->counters.ensure(64));
-   GNOC_HIP(e, e->aux.ensure(n * 4 + 4));
-   GNOC_HIP(e, e->routed.ensure(n + 4));
-   GNOC_HIP(e, e->final_ps.ensure(n * 8 + 8));
-   const uint32_t N = e->dc.N;
-   const uint32_t pch = prep_chunk(N);
-   const uint32_t nch = (uint32_t) std::max<uint64_t>(1, (n + pch - 1) / pch);
-   GNOC_HIP(e, e->hist.ensure((size_t) nch * N * 4));
-   GNOC_HIP(e, hipMemsetAsync(e->counters.p, 0, 64, e->stream));
-   hipLaunchKernelGGL(k_classify, dim3(nch), dim3(256), N * 4, e->stream, e->dc, (uint64_t) n, pch, e->d_inj, e->d_src,
-                         e->d_dst, e->d_bits, e->d_flags, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(),
-                         e->final_ps.as<uint64_t>(), e->hist.as<uint32_t>(), e->counters.as<unsigned long long>(),
-                         0u, e->dc.H, 0u, e->dc.W, nullptr, nullptr);
-   GNOC_HIP(e, hipGetLastError());
-   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 24, hipMemcpyDeviceToHost, e->stream));
-   GNOC_HIP(e, hipStreamSynchronize(e->stream));
-   if (e->h_pinned[2]) return fail(e, GNOC_EUNSUPPORTED, "broadcast packets need a host trace (gnoc_submit)");
-   const uint64_t records = e->h_pinned[0] + e->h_pinned[1];
+   // the same contract as gnoc_submit, checked on the device
+   uint64_t records = 0, nbc = 0;
+   int rc = device_validate(e, n, &records, &nbc);
+   if (rc) return rc;
+   if (nbc) return fail(e, GNOC_EUNSUPPORTED, "broadcast packets need a host trace (gnoc_submit)");
    if (record_bound(e, records) >= (1ull << 31)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^31 hop records");
    e->rec_bound = record_bound(e, records);
+   e->h_bid.clear();
+   rc = upload_broadcasts(e);
+   if (rc) return rc;
    e->submitted = true;
    e->ran = false;
+   e->begun = false;
    return GNOC_OK;
 }
 

@@ -103,6 +103,171 @@ __global__ __launch_bounds__(256) void k_classify(DevCfg c, uint64_t n, uint32_t
 }
 
 // ---------------------------------------------------------------------------
+// 0. submit-time checks and statistics (gnoc_submit / gnoc_submit_device)
+// ---------------------------------------------------------------------------
+// The trace contract of include/gnoc.h on the device: per check the first
+// offending packet (atomicMin; the host reports the lowest index, ties in check
+// order), the hop records this engine materialises, broadcasts, and for the
+// chain engine's window sizing the records per X / Y port over the batch
+// (difference arrays along each row / column) and the inserts per port.  A
+// sharded engine also counts its turn exchange per (row band, column band).
+enum : uint32_t
+{
+   VB_TILE = 0,      // src or dst out of range
+   VB_BC_TREE,       // broadcast, but the model has no broadcast tree
+   VB_BC_SHARD,      // broadcast on a sharded or sweep engine
+   VB_ORDER,         // inject_ps decreasing
+   VB_SWEEP,         // sweep packet crosses sweep points
+   VB_ZERO_F,        // routed packet of zero flits
+   VB_F_MAX,         // more than AUX_F_MAX flits
+   VB_T_MAX,         // inject time >= 2^50 ps
+   VB_KINDS
+};
+struct ValOut
+{
+   unsigned long long bad[VB_KINDS];
+   unsigned long long records, nbc, pmax, imax, tlast;
+};
+
+__device__ __forceinline__ uint32_t band_of(uint32_t y, uint32_t nr, uint32_t D)
+{
+   return (uint32_t) (((uint64_t) (y + 1) * nr - 1) / D);   // inverse of band_lo(b) = b D / nr
+}
+
+__global__ __launch_bounds__(256) void k_validate(DevCfg c, uint64_t n, const uint64_t* __restrict__ inj,
+                                                  const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                                                  const uint32_t* __restrict__ bits, const uint32_t* __restrict__ flags,
+                                                  int tree, uint32_t sweep, uint32_t nr, uint32_t rank, ValOut* __restrict__ vo,
+                                                  int* __restrict__ dxr, int* __restrict__ dxl, int* __restrict__ dyu,
+                                                  int* __restrict__ dyd, uint32_t* __restrict__ insx,
+                                                  uint32_t* __restrict__ insy, unsigned long long* __restrict__ xcnt)
+{
+   const uint32_t N = c.N, W = c.W, H = c.H;
+   const bool band_prep = W <= 64 && H <= 64;
+   unsigned long long rec = 0, nbc = 0;
+   for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const uint32_t s = src[i], fl = flags ? flags[i] : 0u;
+      const bool bc = (fl & 2u) != 0;
+      const uint32_t d = bc ? s : dst[i];   // a broadcast's receiver field is ignored
+      const uint64_t t = inj[i];
+      if (i == n - 1) vo->tlast = t;
+      uint32_t kind = VB_KINDS;
+      uint32_t F = 0;
+      bool bypass = true;
+      if (s >= N || d >= N) kind = VB_TILE;
+      else if (bc && !tree) kind = VB_BC_TREE;
+      else if (bc && (nr > 1 || sweep)) kind = VB_BC_SHARD;
+      else if (i && t < inj[i - 1]) kind = VB_ORDER;
+      else if (sweep && point_of(c, s) != point_of(c, d)) kind = VB_SWEEP;
+      else
+      {
+         const uint32_t fw = fw_of(c, s), b = bits[i];
+         F = (b % fw) ? b / fw + 1 : b / fw;
+         bypass = (!bc && s == d) || (fl & 1u);
+         if (F == 0 && !bypass) kind = VB_ZERO_F;
+         else if (F > AUX_F_MAX) kind = VB_F_MAX;
+         else if (t >= (1ull << 50)) kind = VB_T_MAX;
+      }
+      if (kind != VB_KINDS)
+      {
+         atomicMin(&vo->bad[kind], (unsigned long long) i);
+         continue;
+      }
+      nbc += bc ? 1u : 0u;
+      if (bypass) continue;
+      if (bc)
+      {
+         rec += 2ull * N;   // injection + N SELF + N - 1 tree edges
+         continue;
+      }
+      uint32_t sx, sy, dx, dy;
+      tile_xy(s, W, c.magicW, sx, sy);
+      tile_xy(d, W, c.magicW, dx, dy);
+      const uint32_t ax = sx > dx ? sx - dx : dx - sx, ay = sy > dy ? sy - dy : dy - sy;
+      if (dx > sx)
+      {
+         atomicAdd(&dxr[sy * (W + 1) + sx], 1);
+         atomicAdd(&dxr[sy * (W + 1) + dx], -1);
+         atomicAdd(&insx[s * 2], 1u);
+      }
+      else if (dx < sx)
+      {
+         atomicAdd(&dxl[sy * (W + 1) + dx + 1], 1);
+         atomicAdd(&dxl[sy * (W + 1) + sx + 1], -1);
+         atomicAdd(&insx[s * 2 + 1], 1u);
+      }
+      if (dy > sy)
+      {
+         atomicAdd(&dyu[dx * (H + 1) + sy], 1);
+         atomicAdd(&dyu[dx * (H + 1) + dy], -1);
+         atomicAdd(&insy[(sy * W + dx) * 2], 1u);
+      }
+      else if (dy < sy)
+      {
+         atomicAdd(&dyd[dx * (H + 1) + dy + 1], 1);
+         atomicAdd(&dyd[dx * (H + 1) + sy + 1], -1);
+         atomicAdd(&insy[(sy * W + dx) * 2 + 1], 1u);
+      }
+      if (nr <= 1) rec += 2 + ax + ay;
+      else
+      {
+         // records this rank materialises: injection + X leg in its row band (all
+         // injections when prep is not band-local), the turn record on either side,
+         // the Y leg in its column band
+         const uint32_t rb = band_of(sy, nr, H), cb = band_of(dx, nr, W);
+         const bool r_own = rb == rank, c_own = cb == rank;
+         rec += (r_own ? 1 + ax : 0) + (!r_own && !band_prep ? 1 : 0) + (r_own || c_own ? 1 : 0) + (c_own ? ay : 0);
+         if (c.contention) atomicAdd(&xcnt[rb * nr + cb], 1ull);
+      }
+   }
+   // wave sums, one atomic per wave
+   for (int off = 32; off > 0; off >>= 1)
+   {
+      rec += __shfl_down(rec, off);
+      nbc += __shfl_down(nbc, off);
+   }
+   if ((threadIdx.x & 63) == 0)
+   {
+      if (rec) atomicAdd(&vo->records, rec);
+      if (nbc) atomicAdd(&vo->nbc, nbc);
+   }
+}
+
+// The busiest X / Y port over the batch (prefix sums of the difference arrays)
+// and the most inserts of any port.  One workgroup.
+__global__ __launch_bounds__(1024) void k_validate_max(uint32_t W, uint32_t H, const int* __restrict__ dxr,
+                                                       const int* __restrict__ dxl, const int* __restrict__ dyu,
+                                                       const int* __restrict__ dyd, const uint32_t* __restrict__ insx,
+                                                       const uint32_t* __restrict__ insy, ValOut* __restrict__ vo)
+{
+   unsigned long long pm = 0, im = 0;
+   for (uint32_t r = threadIdx.x; r < H; r += blockDim.x)
+   {
+      long long a = 0, b = 0;
+      for (uint32_t x = 0; x <= W; x++)
+      {
+         a += dxr[r * (W + 1) + x];
+         b += dxl[r * (W + 1) + x];
+         pm = max(pm, (unsigned long long) max(a, b));
+      }
+   }
+   for (uint32_t x = threadIdx.x; x < W; x += blockDim.x)
+   {
+      long long a = 0, b = 0;
+      for (uint32_t y = 0; y <= H; y++)
+      {
+         a += dyu[x * (H + 1) + y];
+         b += dyd[x * (H + 1) + y];
+         pm = max(pm, (unsigned long long) max(a, b));
+      }
+   }
+   for (uint32_t k = threadIdx.x; k < 2 * W * H; k += blockDim.x) im = max(im, (unsigned long long) max(insx[k], insy[k]));
+   atomicMax(&vo->pmax, pm);
+   atomicMax(&vo->imax, im);
+}
+
+// ---------------------------------------------------------------------------
 // 2. injection-slot layout
 // ---------------------------------------------------------------------------
 // Sources outside [s0, s1) (another rank's row band) have no injection records here.

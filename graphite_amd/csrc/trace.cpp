@@ -54,25 +54,42 @@ extern "C" int gnoc_trace_synthetic(int32_t W, int32_t H, double f, double load,
                                     uint64_t seed, double hot_frac, int32_t num_hot, uint64_t* inject_ps,
                                     uint32_t* src, uint32_t* dst, uint32_t* bits, size_t capacity, size_t* n_out)
 {
+   return gnoc_trace_synthetic_pattern(GNOC_TRAFFIC_UNIFORM_RANDOM, W, H, f, load, ppt, payload, seed, hot_frac,
+                                       num_hot, inject_ps, src, dst, bits, capacity, n_out);
+}
+
+extern "C" int gnoc_trace_synthetic_pattern(int32_t pattern, int32_t W, int32_t H, double f, double load, uint64_t ppt,
+                                            uint32_t payload, uint64_t seed, double hot_frac, int32_t num_hot,
+                                            uint64_t* inject_ps, uint32_t* src, uint32_t* dst, uint32_t* bits,
+                                            size_t capacity, size_t* n_out)
+{
    if (W <= 0 || H <= 0 || !(f > 0) || !(load > 0) || load > 1.0 || !n_out) return GNOC_EINVAL;
+   if (pattern < GNOC_TRAFFIC_UNIFORM_RANDOM || pattern > GNOC_TRAFFIC_NEAREST_NEIGHBOR) return GNOC_EINVAL;
    const int N = W * H;
+   const bool pow2 = (N & (N - 1)) == 0;
+   // bit complement and shuffle assert a power-of-two tile count (synthetic_network.cc:290, 299)
+   if ((pattern == GNOC_TRAFFIC_BIT_COMPLEMENT || pattern == GNOC_TRAFFIC_SHUFFLE) && !pow2) return GNOC_EINVAL;
    const uint64_t total = (uint64_t) N * ppt;
    *n_out = (size_t) total;
    if (!inject_ps) return GNOC_OK;
    if (capacity < total || !src || !dst || !bits) return GNOC_EINVAL;
    if (hot_frac > 0 && num_hot <= 0) return GNOC_EINVAL;
 
-   // uniformRandomTrafficGenerator, synthetic_network.cc:247-301: send_matrix[slot][sender]
-   std::vector<uint32_t> sendm((size_t) N * N);
-   sendm[0] = (uint32_t) (N / 2);
-   for (int i = 0; i < N; i++)
+   // A tile's destination schedule: send_vec[k % size] (synthetic_network.cc:183).
+   // uniformRandomTrafficGenerator (:232-286): send_matrix[slot][sender], an LCG
+   // schedule; the other patterns (:288-341) send every packet to one tile.
+   std::vector<uint32_t> sendm;
+   if (pattern == GNOC_TRAFFIC_UNIFORM_RANDOM)
    {
-      if (i) sendm[(size_t) i * N] = sendm[(size_t) (i - 1) * N + 1 % N];
-      for (int j = 1; j < N; j++)
-         sendm[(size_t) i * N + j] = (uint32_t) ((13ull * sendm[(size_t) i * N + j - 1] + 5) % (uint64_t) N);
-   }
-   // the reference asserts every slot row and sender column is a permutation (:269-293)
-   {
+      sendm.resize((size_t) N * N);
+      sendm[0] = (uint32_t) (N / 2);
+      for (int i = 0; i < N; i++)
+      {
+         if (i) sendm[(size_t) i * N] = sendm[(size_t) (i - 1) * N + 1 % N];
+         for (int j = 1; j < N; j++)
+            sendm[(size_t) i * N + j] = (uint32_t) ((13ull * sendm[(size_t) i * N + j - 1] + 5) % (uint64_t) N);
+      }
+      // the reference asserts every slot row and sender column is a permutation (:254-279)
       std::vector<uint8_t> seen(N);
       for (int i = 0; i < N; i++)
       {
@@ -81,6 +98,28 @@ extern "C" int gnoc_trace_synthetic(int32_t W, int32_t H, double f, double load,
          for (int j = 0; j < N; j++) if (!seen[j]) return GNOC_EINVAL;
       }
    }
+   else
+   {
+      sendm.resize(N);
+      int nbits = 0;
+      while ((1 << (nbits + 1)) <= N) nbits++;   // floorLog2
+      for (int t = 0; t < N; t++)
+      {
+         const int sx = t % W, sy = t / W;   // computeEMeshPosition (:350-354)
+         int64_t d = 0;
+         switch (pattern)
+         {
+            case GNOC_TRAFFIC_BIT_COMPLEMENT: d = (~t) & (N - 1); break;                              // :288-295
+            case GNOC_TRAFFIC_SHUFFLE: d = ((t >> (nbits - 1)) & 1) | ((t << 1) & (N - 1)); break;     // :297-305
+            case GNOC_TRAFFIC_TRANSPOSE: d = (int64_t) sx * W + sy; break;                            // :307-317
+            case GNOC_TRAFFIC_TORNADO: d = (int64_t) ((sy + H / 2) % H) * W + (sx + W / 2) % W; break; // :319-329
+            default: d = (int64_t) ((sy + 1) % H) * W + (sx + 1) % W; break;                          // :331-341
+         }
+         if (d < 0 || d >= N) return GNOC_EINVAL;   // transpose of a non-square mesh
+         sendm[t] = (uint32_t) d;
+      }
+   }
+   const bool fixed = pattern != GNOC_TRAFFIC_UNIFORM_RANDOM;
    const std::vector<uint32_t> hot = hot_frac > 0 ? mc_positions(W, H, num_hot) : std::vector<uint32_t>();
 
    // Per tile: the cycle of each send (Bernoulli per cycle while packets remain,
@@ -101,7 +140,7 @@ extern "C" int gnoc_trace_synthetic(int32_t W, int32_t H, double f, double load,
          {
             if (r.next() * 1.0 < load)
             {
-               uint32_t dd = sendm[(size_t) (sent % (uint64_t) N) * N + t];
+               uint32_t dd = fixed ? sendm[t] : sendm[(size_t) (sent % (uint64_t) N) * N + t];
                if (hot_frac > 0 && rh.next() < hot_frac)
                   dd = hot[(size_t) (rh.next() * (double) hot.size()) % hot.size()];
                c[sent] = cycle;
@@ -144,6 +183,12 @@ static_assert(sizeof(gnoc_trace_header) == 128, "trace header is 128 bytes");
 
 extern "C" int gnoc_trace_file_write(const char* path, const gnoc_config* cfg, const gnoc_packets* pk, size_t n)
 {
+   return gnoc_trace_file_write_q(path, cfg, nullptr, pk, n);
+}
+
+extern "C" int gnoc_trace_file_write_q(const char* path, const gnoc_config* cfg, const gnoc_trace_queue* q,
+                                       const gnoc_packets* pk, size_t n)
+{
    if (!path || !cfg || !pk) return GNOC_EINVAL;
    if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return GNOC_EINVAL;
    FILE* f = std::fopen(path, "wb");
@@ -151,10 +196,12 @@ extern "C" int gnoc_trace_file_write(const char* path, const gnoc_config* cfg, c
    gnoc_trace_header h;
    std::memset(&h, 0, sizeof(h));
    std::memcpy(h.magic, GNOC_TRACE_MAGIC, 8);
-   h.version = 1;
+   h.version = 2;
    h.header_bytes = sizeof(h);
    h.num_packets = n;
    h.cfg = *cfg;
+   h.ma_type = q ? q->ma_type : GNOC_MOVING_AVG_NONE;
+   h.ma_window = q ? q->ma_window : 1u;
    bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1;
    ok = ok && (n == 0 || std::fwrite(pk->inject_ps, 8, n, f) == n);
    ok = ok && (n == 0 || std::fwrite(pk->src, 4, n, f) == n);
@@ -177,12 +224,20 @@ extern "C" int gnoc_trace_file_write(const char* path, const gnoc_config* cfg, c
 extern "C" int gnoc_trace_file_read(const char* path, gnoc_config* cfg_out, uint64_t* inject_ps, uint32_t* src,
                                     uint32_t* dst, uint32_t* bits, uint32_t* flags, size_t capacity, size_t* n_out)
 {
+   return gnoc_trace_file_read_q(path, cfg_out, nullptr, inject_ps, src, dst, bits, flags, capacity, n_out);
+}
+
+extern "C" int gnoc_trace_file_read_q(const char* path, gnoc_config* cfg_out, gnoc_trace_queue* q_out,
+                                      uint64_t* inject_ps, uint32_t* src, uint32_t* dst, uint32_t* bits, uint32_t* flags,
+                                      size_t capacity, size_t* n_out)
+{
    if (!path || !n_out) return GNOC_EINVAL;
    FILE* f = std::fopen(path, "rb");
    if (!f) return GNOC_EINVAL;
    gnoc_trace_header h;
    bool ok = std::fread(&h, sizeof(h), 1, f) == 1;
-   ok = ok && std::memcmp(h.magic, GNOC_TRACE_MAGIC, 8) == 0 && h.version == 1 && h.header_bytes == sizeof(h);
+   ok = ok && std::memcmp(h.magic, GNOC_TRACE_MAGIC, 8) == 0 && (h.version == 1 || h.version == 2) &&
+        h.header_bytes == sizeof(h);
    if (!ok)
    {
       std::fclose(f);
@@ -191,6 +246,12 @@ extern "C" int gnoc_trace_file_read(const char* path, gnoc_config* cfg_out, uint
    const size_t n = (size_t) h.num_packets;
    *n_out = n;
    if (cfg_out) *cfg_out = h.cfg;
+   if (q_out)
+   {
+      // version 1 carried no queue settings: the reference's defaults (no moving average)
+      q_out->ma_type = h.version >= 2 ? h.ma_type : GNOC_MOVING_AVG_NONE;
+      q_out->ma_window = h.version >= 2 ? h.ma_window : 1u;
+   }
    if (!inject_ps)
    {
       std::fclose(f);

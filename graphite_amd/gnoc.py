@@ -38,6 +38,7 @@ EXPORTED = (
     "gnoc_get_packet_results", "gnoc_get_port_stats", "gnoc_get_summary", "gnoc_device_final_ps",
     "gnoc_last_error", "gnoc_destroy", "gnoc_trace_synthetic", "gnoc_abi_version",
     "gnoc_set_profiling", "gnoc_get_kernel_stats", "gnoc_trace_file_write", "gnoc_trace_file_read",
+    "gnoc_trace_file_write_q", "gnoc_trace_file_read_q", "gnoc_trace_synthetic_pattern",
     "gnoc_shard", "gnoc_exchange_counts", "gnoc_run_begin", "gnoc_run_finish",
     "gnoc_create_sweep", "gnoc_sweep_layout", "gnoc_get_port_utilization", "gnoc_create_hop_counter",
     "gnoc_get_broadcast_results", "gnoc_get_broadcast_info", "gnoc_set_basic_moving_average",
@@ -80,6 +81,10 @@ class GnocPackets(ctypes.Structure):
         ("bits", ctypes.c_void_p),
         ("flags", ctypes.c_void_p),
     ]
+
+
+class GnocTraceQueue(ctypes.Structure):
+    _fields_ = [("ma_type", ctypes.c_int32), ("ma_window", ctypes.c_uint32)]
 
 
 class GnocSummary(ctypes.Structure):
@@ -132,8 +137,16 @@ def load() -> ctypes.CDLL:
     lib.gnoc_trace_synthetic.argtypes = [
         ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_uint64, ctypes.c_double, ctypes.c_int32, vp, vp, vp, vp, sz, ctypes.POINTER(sz)]
+    lib.gnoc_trace_synthetic_pattern.argtypes = [
+        ctypes.c_int32,
+        ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint32,
+        ctypes.c_uint64, ctypes.c_double, ctypes.c_int32, vp, vp, vp, vp, sz, ctypes.POINTER(sz)]
     lib.gnoc_abi_version.argtypes = []
     lib.gnoc_trace_file_write.argtypes = [ctypes.c_char_p, ctypes.POINTER(GnocConfig), ctypes.POINTER(GnocPackets), sz]
+    lib.gnoc_trace_file_write_q.argtypes = [ctypes.c_char_p, ctypes.POINTER(GnocConfig), ctypes.POINTER(GnocTraceQueue),
+                                            ctypes.POINTER(GnocPackets), sz]
+    lib.gnoc_trace_file_read_q.argtypes = [ctypes.c_char_p, ctypes.POINTER(GnocConfig), ctypes.POINTER(GnocTraceQueue),
+                                           vp, vp, vp, vp, vp, sz, ctypes.POINTER(sz)]
     lib.gnoc_trace_file_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(GnocConfig), vp, vp, vp, vp, vp, sz,
                                          ctypes.POINTER(sz)]
     lib.gnoc_set_profiling.argtypes = [vp, ctypes.c_int]
@@ -222,44 +235,54 @@ class Trace:
                      np.ascontiguousarray(f, np.uint32))
 
 
+# synthetic_network.cc NetworkTrafficType (:16-24), include/gnoc.h GNOC_TRAFFIC_*
+TRAFFIC_PATTERNS = ("uniform_random", "bit_complement", "shuffle", "transpose", "tornado", "nearest_neighbor")
+
+
 def synthetic_trace(width: int, height: int, offered_load: float, packets_per_tile: int, seed: int = 1,
                     payload_bytes: int = 8, frequency_ghz: float = 1.0, hotspot_fraction: float = 0.0,
-                    num_hotspots: int = 16) -> Trace:
+                    num_hotspots: int = 16, pattern: str = "uniform_random") -> Trace:
     lib = load()
+    pat = TRAFFIC_PATTERNS.index(pattern)
     n = ctypes.c_size_t(0)
-    rc = lib.gnoc_trace_synthetic(width, height, frequency_ghz, offered_load, packets_per_tile, payload_bytes,
-                                  seed, hotspot_fraction, num_hotspots, None, None, None, None, 0, ctypes.byref(n))
+    rc = lib.gnoc_trace_synthetic_pattern(pat, width, height, frequency_ghz, offered_load, packets_per_tile,
+                                          payload_bytes, seed, hotspot_fraction, num_hotspots, None, None, None, None,
+                                          0, ctypes.byref(n))
     if rc:
         raise GnocError(rc, "trace size query failed")
     N = n.value
     t = Trace(np.empty(N, np.uint64), np.empty(N, np.uint32), np.empty(N, np.uint32), np.empty(N, np.uint32),
               np.zeros(N, np.uint32))
-    rc = lib.gnoc_trace_synthetic(width, height, frequency_ghz, offered_load, packets_per_tile, payload_bytes,
-                                  seed, hotspot_fraction, num_hotspots, t.inject_ps.ctypes.data, t.src.ctypes.data,
-                                  t.dst.ctypes.data, t.bits.ctypes.data, N, ctypes.byref(n))
+    rc = lib.gnoc_trace_synthetic_pattern(pat, width, height, frequency_ghz, offered_load, packets_per_tile,
+                                          payload_bytes, seed, hotspot_fraction, num_hotspots, t.inject_ps.ctypes.data,
+                                          t.src.ctypes.data, t.dst.ctypes.data, t.bits.ctypes.data, N, ctypes.byref(n))
     if rc:
-        raise GnocError(rc, "synthetic trace generation failed (invalid LCG schedule for this tile count?)")
+        raise GnocError(rc, f"synthetic trace generation failed ({pattern} on {width}x{height})")
     return t
 
 
 def write_trace_file(path: str, cfg: "EngineConfig", tr: Trace) -> None:
-    """The on-disk trace format of include/gnoc.h (gnoc_trace_header + SoA)."""
+    """The on-disk trace format of include/gnoc.h (gnoc_trace_header v2 + SoA),
+    with the basic queue's moving-average settings of cfg."""
     lib = load()
     tr = tr.normalized()
     c = cfg.to_c()
+    q = GnocTraceQueue(int(cfg.moving_avg_type), int(cfg.moving_avg_window if cfg.moving_avg_type else 1))
     pk = GnocPackets(tr.inject_ps.ctypes.data, tr.src.ctypes.data, tr.dst.ctypes.data, tr.bits.ctypes.data,
                      tr.flags.ctypes.data)
-    rc = lib.gnoc_trace_file_write(path.encode(), ctypes.byref(c), ctypes.byref(pk), len(tr))
+    rc = lib.gnoc_trace_file_write_q(path.encode(), ctypes.byref(c), ctypes.byref(q), ctypes.byref(pk), len(tr))
     if rc:
         raise GnocError(rc, f"cannot write trace {path}")
 
 
 def read_trace_file(path: str):
-    """-> (EngineConfig, Trace)"""
+    """-> (EngineConfig, Trace); a version-1 file reads with no moving average."""
     lib = load()
     c = GnocConfig()
+    q = GnocTraceQueue()
     n = ctypes.c_size_t(0)
-    rc = lib.gnoc_trace_file_read(path.encode(), ctypes.byref(c), None, None, None, None, None, 0, ctypes.byref(n))
+    rc = lib.gnoc_trace_file_read_q(path.encode(), ctypes.byref(c), ctypes.byref(q), None, None, None, None, None, 0,
+                                    ctypes.byref(n))
     if rc:
         raise GnocError(rc, f"cannot read trace {path}")
     N = n.value
@@ -272,6 +295,9 @@ def read_trace_file(path: str):
     cfg = EngineConfig(**{f[0]: getattr(c, f[0]) for f in GnocConfig._fields_})
     for k in ("contention_enabled", "analytical_enabled", "broadcast_tree_enabled"):
         setattr(cfg, k, bool(getattr(cfg, k)))
+    cfg.moving_avg_type = q.ma_type
+    if q.ma_type:
+        cfg.moving_avg_window = q.ma_window
     return cfg, t
 
 

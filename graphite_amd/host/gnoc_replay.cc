@@ -46,7 +46,7 @@ int main(int argc, char** argv)
       std::unique_ptr<NetworkModelEMeshHopByHopHIP> m(NetworkModelEMeshHopByHopHIP::fromTraceFile(argv[1], device));
       if (!mavg.empty())
       {
-         // queue_model/basic/moving_avg_type:moving_avg_window_size (not in the trace header)
+         // queue_model/basic/moving_avg_type:moving_avg_window_size (overrides the trace header's)
          const size_t c = mavg.find(':');
          const std::string t = mavg.substr(0, c);
          const int32_t type = t == "arithmetic_mean" ? GNOC_MOVING_AVG_ARITHMETIC_MEAN

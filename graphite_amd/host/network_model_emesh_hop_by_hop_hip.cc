@@ -74,24 +74,24 @@ NetworkModelEMeshHopByHopHIP::NetworkModelEMeshHopByHopHIP(const CfgView& cfg, i
    int32_t type = GNOC_MOVING_AVG_NONE;
    uint32_t window = 1;
    cfg.basicMovingAverage(&type, &window);
-   if (_cfg.queue_type == GNOC_QUEUE_BASIC && type != GNOC_MOVING_AVG_NONE)
-      check(gnoc_set_basic_moving_average(_eng, type, window), "queue_model/basic moving average");
+   if (_cfg.queue_type == GNOC_QUEUE_BASIC && type != GNOC_MOVING_AVG_NONE) setBasicMovingAverage(type, window);
 }
 
-// QueueModelBasic::QueueModelBasic (queue_model_basic.cc:7-30) with the
-// carbon_sim.cfg values as defaults (carbon_sim.cfg:376-379).  An unknown type
-// string leaves the queue without a moving average, as createAvgType's NULL does
+// QueueModelBasic::QueueModelBasic (queue_model_basic.cc:7-30) with its code
+// defaults: moving_avg_enabled false, window 1, type "none" (:17-19); a
+// carbon_sim.cfg supplies its own values when present.  An unknown type string
+// leaves the queue without a moving average, as createAvgType's NULL does
 // (moving_average.h:184-188).
 void CfgView::basicMovingAverage(int32_t* type, uint32_t* window) const
 {
    *type = GNOC_MOVING_AVG_NONE;
    *window = 1;
-   if (!getBool("queue_model/basic/moving_avg_enabled", true)) return;
-   const std::string t = getString("queue_model/basic/moving_avg_type", "arithmetic_mean");
+   if (!getBool("queue_model/basic/moving_avg_enabled", false)) return;
+   const std::string t = getString("queue_model/basic/moving_avg_type", "none");
    *type = t == "arithmetic_mean" ? GNOC_MOVING_AVG_ARITHMETIC_MEAN
          : t == "geometric_mean"  ? GNOC_MOVING_AVG_GEOMETRIC_MEAN
          : t == "median"          ? GNOC_MOVING_AVG_MEDIAN : GNOC_MOVING_AVG_NONE;
-   *window = (uint32_t) getInt("queue_model/basic/moving_avg_window_size", 64);
+   *window = (uint32_t) getInt("queue_model/basic/moving_avg_window_size", 1);
 }
 
 NetworkModelEMeshHopByHopHIP::NetworkModelEMeshHopByHopHIP(const gnoc_config& cfg) : _cfg(cfg)
@@ -115,6 +115,8 @@ NetworkModelEMeshHopByHopHIP::~NetworkModelEMeshHopByHopHIP() { gnoc_destroy(_en
 void NetworkModelEMeshHopByHopHIP::setBasicMovingAverage(int32_t type, uint32_t window)
 {
    check(gnoc_set_basic_moving_average(_eng, type, window), "queue_model/basic moving average");
+   _queue.ma_type = type;
+   _queue.ma_window = window;
 }
 
 void NetworkModelEMeshHopByHopHIP::check(int status, const char* what) const
@@ -452,18 +454,31 @@ void NetworkModelEMeshHopByHopHIP::writeTrace(const std::string& path) const
    pk.dst = _dst.data();
    pk.bits = _bits.data();
    pk.flags = _flags.data();
-   const int rc = gnoc_trace_file_write(path.c_str(), &_cfg, &pk, _inj.size());
+   const int rc = gnoc_trace_file_write_q(path.c_str(), &_cfg, &_queue, &pk, _inj.size());
    if (rc) throw NetworkModelError(rc, "cannot write trace " + path);
 }
 
 NetworkModelEMeshHopByHopHIP* NetworkModelEMeshHopByHopHIP::fromTraceFile(const std::string& path, int device)
 {
    gnoc_config cfg;
+   gnoc_trace_queue q;
    size_t n = 0;
-   int rc = gnoc_trace_file_read(path.c_str(), &cfg, nullptr, nullptr, nullptr, nullptr, nullptr, 0, &n);
+   int rc = gnoc_trace_file_read_q(path.c_str(), &cfg, &q, nullptr, nullptr, nullptr, nullptr, nullptr, 0, &n);
    if (rc) throw NetworkModelError(rc, "cannot read trace " + path);
    cfg.device = device;
    auto* m = new NetworkModelEMeshHopByHopHIP(cfg);
+   if (cfg.queue_type == GNOC_QUEUE_BASIC && q.ma_type != GNOC_MOVING_AVG_NONE)
+   {
+      try
+      {
+         m->setBasicMovingAverage(q.ma_type, q.ma_window);   // the settings the trace was captured under
+      }
+      catch (...)
+      {
+         delete m;
+         throw;
+      }
+   }
    m->_inj.resize(n);
    m->_src.resize(n);
    m->_dst.resize(n);

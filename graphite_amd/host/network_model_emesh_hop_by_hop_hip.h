@@ -98,7 +98,8 @@ public:
 
    // Time every hop of every recorded packet (one gnoc_submit + gnoc_run).
    // queue_model/basic/moving_avg_* on this model's basic queues (GNOC_MOVING_AVG_*;
-   // queue_model_basic.cc:7-30) -- for a replayed trace, whose header has no such keys
+   // queue_model_basic.cc:7-30).  Written into captured traces (header v2) and
+   // applied by fromTraceFile; a version-1 trace replays with NONE unless set here.
    void setBasicMovingAverage(int32_t type, uint32_t window);
    void run();
 
@@ -160,6 +161,7 @@ private:
    void check(int status, const char* what) const;
 
    gnoc_config _cfg;
+   gnoc_trace_queue _queue{GNOC_MOVING_AVG_NONE, 1};   // basic queues' moving average
    gnoc_engine* _eng = nullptr;
    std::vector<uint64_t> _inj;
    std::vector<uint32_t> _src, _dst, _bits, _flags;

@@ -311,6 +311,23 @@ int gnoc_trace_synthetic(int32_t mesh_width, int32_t mesh_height, double frequen
                          uint64_t *inject_ps, uint32_t *src, uint32_t *dst, uint32_t *bits,
                          size_t capacity, size_t *n_out);
 
+/* The reference generator's other traffic patterns (NetworkTrafficType,
+ * synthetic_network.cc:16-24, 288-341), same timing model as above: every
+ * packet of a tile goes to one destination.  BIT_COMPLEMENT and SHUFFLE need a
+ * power-of-two tile count; TRANSPOSE a destination inside the mesh (GNOC_EINVAL
+ * otherwise, where the reference asserts). */
+#define GNOC_TRAFFIC_UNIFORM_RANDOM    0
+#define GNOC_TRAFFIC_BIT_COMPLEMENT    1
+#define GNOC_TRAFFIC_SHUFFLE           2
+#define GNOC_TRAFFIC_TRANSPOSE         3
+#define GNOC_TRAFFIC_TORNADO           4
+#define GNOC_TRAFFIC_NEAREST_NEIGHBOR  5
+int gnoc_trace_synthetic_pattern(int32_t pattern, int32_t mesh_width, int32_t mesh_height, double frequency_ghz,
+                                 double offered_load, uint64_t packets_per_tile, uint32_t payload_bytes,
+                                 uint64_t seed, double hotspot_fraction, int32_t num_hotspots,
+                                 uint64_t *inject_ps, uint32_t *src, uint32_t *dst, uint32_t *bits,
+                                 size_t capacity, size_t *n_out);
+
 /* ---- on-disk trace format ----------------------------
  * A batch captured at Network::netSend / NetworkModel::__routePacket(SEND_TILE)
  * (network.cc:174-215, network_model.cc:95-107), with the configuration it was
@@ -320,20 +337,38 @@ int gnoc_trace_synthetic(int32_t mesh_width, int32_t mesh_height, double frequen
 typedef struct gnoc_trace_header
 {
    char     magic[8];            /* GNOC_TRACE_MAGIC                                  */
-   uint32_t version;             /* 1                                                  */
+   uint32_t version;             /* 2 (version-1 files read with ma_type = NONE)      */
    uint32_t header_bytes;        /* 128                                                */
    uint64_t num_packets;
    gnoc_config cfg;              /* the configuration the trace was captured under     */
-   uint8_t  reserved[128 - 24 - sizeof(gnoc_config)];
+   int32_t  ma_type;             /* v2: queue_model/basic moving average (GNOC_MOVING_AVG_*) */
+   uint32_t ma_window;           /* v2: its window size                               */
+   uint8_t  reserved[128 - 32 - sizeof(gnoc_config)];
 } gnoc_trace_header;
 
-/* Write a (inject_ps, id)-ordered batch and its configuration to `path`. */
+/* Queue settings outside gnoc_config that a trace carries (header v2): the basic
+ * queue's moving average, gnoc_set_basic_moving_average (queue_model_basic.cc:7-30). */
+typedef struct gnoc_trace_queue
+{
+   int32_t  ma_type;             /* GNOC_MOVING_AVG_NONE = moving_avg_enabled false */
+   uint32_t ma_window;
+} gnoc_trace_queue;
+
+/* Write a (inject_ps, id)-ordered batch and its configuration to `path`
+ * (moving average NONE). */
 int gnoc_trace_file_write(const char *path, const gnoc_config *cfg, const gnoc_packets *pk, size_t n);
+/* The same with the queue settings (q may be NULL: NONE). */
+int gnoc_trace_file_write_q(const char *path, const gnoc_config *cfg, const gnoc_trace_queue *q,
+                            const gnoc_packets *pk, size_t n);
 
 /* Read `path`: with NULL arrays, fills *cfg_out and *n_out only; then call
  * again with arrays of capacity >= *n_out. */
 int gnoc_trace_file_read(const char *path, gnoc_config *cfg_out, uint64_t *inject_ps, uint32_t *src, uint32_t *dst,
                          uint32_t *bits, uint32_t *flags, size_t capacity, size_t *n_out);
+/* The same, also filling *q_out (NONE for a version-1 file) when not NULL. */
+int gnoc_trace_file_read_q(const char *path, gnoc_config *cfg_out, gnoc_trace_queue *q_out, uint64_t *inject_ps,
+                           uint32_t *src, uint32_t *dst, uint32_t *bits, uint32_t *flags, size_t capacity,
+                           size_t *n_out);
 
 int gnoc_abi_version(void);
 

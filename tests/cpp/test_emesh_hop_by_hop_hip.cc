@@ -110,6 +110,25 @@ int main()
       try { m2.routePacket(pkt(0, 5, NetPacket::BROADCAST)); } catch (const NetworkModelError& e) { threw = e.status == GNOC_EINVAL; }
       EXPECT_EQ(threw, 1);
    }
+   // 6. queue_model/basic moving average: the reference's code defaults when the
+   //    section is absent (queue_model_basic.cc:17-19: disabled, window 1, "none")
+   {
+      CfgView empty;
+      int32_t type = -7;
+      uint32_t window = 0;
+      empty.basicMovingAverage(&type, &window);
+      EXPECT_EQ(type, GNOC_MOVING_AVG_NONE);
+      EXPECT_EQ(window, 1);
+      CfgView on = cfg;
+      on.set("queue_model/basic/moving_avg_enabled", "true");
+      on.basicMovingAverage(&type, &window);
+      EXPECT_EQ(type, GNOC_MOVING_AVG_NONE);   // enabled, type "none": createAvgType gives NULL
+      on.set("queue_model/basic/moving_avg_type", "arithmetic_mean");
+      on.set("queue_model/basic/moving_avg_window_size", "8");
+      on.basicMovingAverage(&type, &window);
+      EXPECT_EQ(type, GNOC_MOVING_AVG_ARITHMETIC_MEAN);
+      EXPECT_EQ(window, 8);
+   }
    if (failures)
    {
       std::fprintf(stderr, "%d failure(s)\n", failures);

@@ -1,0 +1,43 @@
+"""The reference generator's non-uniform traffic patterns (synthetic_network.cc
+:288-341) on the GPU engine vs the oracle, bit-exact.  Fixed-destination
+patterns concentrate load on few X / Y chains (transpose, tornado) -- the
+non-uniform port loads the chain engine's window sizing and the level engine's
+chunk splitter see least under uniform traffic."""
+import pytest
+
+from graphite_amd import gnoc
+from tests.test_gpu_parity import assert_same, run_both
+
+pytestmark = pytest.mark.gpu
+
+PATTERNS = ["bit_complement", "shuffle", "transpose", "tornado", "nearest_neighbor"]
+
+
+@pytest.mark.parametrize("pattern", PATTERNS)
+def test_pattern_32x32(pattern):
+    cfg = gnoc.EngineConfig(num_tiles=1024)
+    tr = gnoc.synthetic_trace(32, 32, 0.002, 200, seed=7, pattern=pattern)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+    assert got.summary["mesh_hops"] == int(ref.port_count.reshape(-1, 6)[:, :5].sum())
+
+
+@pytest.mark.parametrize("pattern", PATTERNS)
+@pytest.mark.parametrize("load", [0.01, 0.08])
+def test_pattern_8x8(pattern, load):
+    """Up to saturation (the M/G/1 branch then fires, and the chain engine hands
+    the batch to the level engine)."""
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = gnoc.synthetic_trace(8, 8, load, 300, seed=3, pattern=pattern)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
+
+
+def test_tornado_32x32_hotspot_mix_forced_windows(monkeypatch):
+    """Tornado plus a hotspot fraction, with small forced chain windows (many
+    window edges and spills per chain)."""
+    monkeypatch.setenv("GNOC_WINDOW_SHIFT", "17")
+    cfg = gnoc.EngineConfig(num_tiles=1024)
+    tr = gnoc.synthetic_trace(32, 32, 0.002, 150, seed=9, pattern="tornado", hotspot_fraction=0.1)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)

@@ -42,6 +42,27 @@ def test_trace_file_rejects_garbage(tmp_path):
         gnoc.read_trace_file(str(p))
 
 
+def test_trace_header_carries_moving_average(tmp_path):
+    """Header v2 round trip of the basic queue's moving average; a version-1 file
+    (no such keys) reads with none, as the reference's defaults give."""
+    cfg = gnoc.EngineConfig(num_tiles=16, queue_type=gnoc.QUEUE_BASIC,
+                            moving_avg_type=gnoc.MOVING_AVG_MEDIAN, moving_avg_window=17)
+    tr = gnoc.Trace(np.array([0, 5, 9], np.uint64), np.array([0, 1, 2], np.uint32), np.array([3, 2, 1], np.uint32),
+                    np.array([576, 576, 72], np.uint32))
+    p = str(tmp_path / "q.gtr")
+    gnoc.write_trace_file(p, cfg, tr)
+    c2, t2 = gnoc.read_trace_file(p)
+    assert (c2.moving_avg_type, c2.moving_avg_window) == (gnoc.MOVING_AVG_MEDIAN, 17)
+    assert np.array_equal(t2.inject_ps, tr.inject_ps) and np.array_equal(t2.bits, tr.bits)
+    raw = bytearray(open(p, "rb").read())
+    assert int.from_bytes(raw[8:12], "little") == 2
+    raw[8:12] = (1).to_bytes(4, "little")
+    p1 = str(tmp_path / "v1.gtr")
+    open(p1, "wb").write(bytes(raw))
+    c1, _ = gnoc.read_trace_file(p1)
+    assert c1.moving_avg_type == gnoc.MOVING_AVG_NONE
+
+
 @pytest.mark.gpu
 def test_cpp_known_answers():
     r = subprocess.run([os.path.join(BUILD, "test_emesh_hop_by_hop_hip")], capture_output=True, text=True, timeout=120)
@@ -55,10 +76,8 @@ def test_replay_golden_through_cpp_model(tmp_path, name):
     trace = str(tmp_path / "t.gtr")
     out = str(tmp_path / "r.bin")
     gnoc.write_trace_file(trace, cfg, tr)
-    # the trace header holds gnoc_config only: the basic queue's moving average goes on the command line
-    mavg = ["--moving-avg", {1: "arithmetic_mean", 3: "median"}[cfg.moving_avg_type] + f":{cfg.moving_avg_window}"] \
-        if cfg.moving_avg_type else []
-    r = subprocess.run([os.path.join(BUILD, "gnoc_replay"), trace, "--results", out, "--summary", "0"] + mavg,
+    # the header (v2) carries the basic queue's moving average: no command-line flag
+    r = subprocess.run([os.path.join(BUILD, "gnoc_replay"), trace, "--results", out, "--summary", "0"],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert "Total Packets Received" in r.stdout

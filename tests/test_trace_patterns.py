@@ -1,0 +1,43 @@
+"""Destinations of the synthetic traffic patterns (gnoc_trace_synthetic_pattern)
+against the reference generator's formulas (synthetic_network.cc:288-341),
+restated here independently; the timing model is the uniform case's."""
+import numpy as np
+import pytest
+
+from graphite_amd import gnoc
+
+
+def _expected(pattern, W, H, t):
+    N = W * H
+    sx, sy = t % W, t // W
+    nbits = int(np.log2(N))
+    return {
+        "bit_complement": (~t) & (N - 1),
+        "shuffle": ((t >> (nbits - 1)) & 1) | ((t << 1) & (N - 1)),
+        "transpose": sx * W + sy,
+        "tornado": ((sy + H // 2) % H) * W + (sx + W // 2) % W,
+        "nearest_neighbor": ((sy + 1) % H) * W + (sx + 1) % W,
+    }[pattern]
+
+
+@pytest.mark.parametrize("pattern", ["bit_complement", "shuffle", "transpose", "tornado", "nearest_neighbor"])
+@pytest.mark.parametrize("W,H", [(8, 8), (32, 32), (16, 16)])
+def test_pattern_destinations(pattern, W, H):
+    tr = gnoc.synthetic_trace(W, H, 0.05, 20, seed=2, pattern=pattern)
+    assert len(tr) == W * H * 20
+    assert np.all(np.diff(tr.inject_ps.astype(np.int64)) >= 0)
+    exp = np.array([_expected(pattern, W, H, t) for t in range(W * H)], np.uint32)
+    assert np.array_equal(tr.dst, exp[tr.src])
+    # the same per-tile send times as uniform traffic (the Bernoulli stream is the tile's)
+    u = gnoc.synthetic_trace(W, H, 0.05, 20, seed=2)
+    assert np.array_equal(np.sort(u.inject_ps), np.sort(tr.inject_ps))
+
+
+def test_pattern_refusals():
+    # bit complement / shuffle need 2^k tiles (the reference asserts isPower2)
+    for p in ("bit_complement", "shuffle"):
+        with pytest.raises(gnoc.GnocError) as ex:
+            gnoc.synthetic_trace(6, 6, 0.05, 5, pattern=p)
+        assert ex.value.code == -1
+    with pytest.raises(ValueError):
+        gnoc.synthetic_trace(4, 4, 0.05, 5, pattern="hotspot_storm")
