@@ -1379,6 +1379,8 @@ static int run_ma(gnoc_engine* e)
 {
    if (!e->submitted) return fail(e, GNOC_ESTATE, "gnoc_run before gnoc_submit");
    if (e->nb) return fail(e, GNOC_EUNSUPPORTED, "broadcast packets with moving-average basic queues");
+   // the packet sort takes an int count (self-sends and unmodeled packets count too)
+   if (e->n > (size_t) INT32_MAX) return fail(e, GNOC_EUNSUPPORTED, "more than 2^31-1 packets on the moving-average path");
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    const DevCfg& c = e->dc;
    const size_t n = e->n;
@@ -1700,6 +1702,9 @@ int gnoc_run_begin(gnoc_engine* e, void* send_buf)
    GNOC_HIP(e, hipStreamSynchronize(s));
    if (((const unsigned*) (e->h_pinned + 8))[0] & 6u)
       return fail(e, GNOC_EUNSUPPORTED, "sharded run hit a burst the chunked path cannot split (X phase)");
+   // test knob: this rank reports an X-phase failure (the peers must all abort too)
+   const char* frv = std::getenv("GNOC_FAIL_RANK");
+   if (frv && *frv && std::atoi(frv) == e->rank) return fail(e, GNOC_EHIP, "injected X-phase failure (GNOC_FAIL_RANK)");
    if (e->xs_slots)
    {
       if (!send_buf) return fail(e, GNOC_EINVAL, "null send buffer");

@@ -512,10 +512,24 @@ class ShardedEngine(Engine):
         if self.nranks > 1:
             exchange_units(self._send, self._recv, self.send_units, self.recv_units, self.group)
 
+    def _agree(self, rc: int, what: str) -> None:
+        """Every rank learns whether any rank failed `what`, and all raise together
+        (a rank that raised alone would leave its peers waiting in the exchange or
+        in gathered_results' all-reduce)."""
+        import torch
+        import torch.distributed as dist
+        flag = torch.tensor([1 if rc else 0], dtype=torch.int32)
+        if dist.get_backend(self.group) == "nccl":
+            flag = flag.cuda(self.cfg.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        self._check(rc)
+        if int(flag.item()):
+            raise GnocError(-3, f"{what} failed on another rank")
+
     def run(self) -> None:
-        self._check(self.lib.gnoc_run_begin(self._h, self._send.data_ptr()))
+        self._agree(self.lib.gnoc_run_begin(self._h, self._send.data_ptr()), "gnoc_run_begin")
         self.exchange()
-        self._check(self.lib.gnoc_run_finish(self._h, self._recv.data_ptr()))
+        self._agree(self.lib.gnoc_run_finish(self._h, self._recv.data_ptr()), "gnoc_run_finish")
 
     def gathered_results(self) -> Results:
         """The whole mesh's results on every rank: element-wise sum over ranks

@@ -56,6 +56,27 @@ def main():
     torch.cuda.set_device(0)
     failures = 0
     for name in sys.argv[1:]:
+        if name == "fail":
+            # rank 1's X phase fails: every rank must raise (none may hang in the exchange)
+            os.environ["GNOC_FAIL_RANK"] = "1"
+            eng = gnoc.ShardedEngine(gnoc.EngineConfig(num_tiles=64), rank, world)
+            eng.submit(gnoc.synthetic_trace(8, 8, 0.05, 100, seed=11))
+            try:
+                eng.run()
+                raised = False
+            except gnoc.GnocError:
+                raised = True
+            os.environ.pop("GNOC_FAIL_RANK")
+            eng.close()
+            flag = torch.tensor([1 if raised else 0], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if rank == 0:
+                if int(flag.item()) == 1:
+                    print(f"SHARD OK {name} world={world}", flush=True)
+                else:
+                    failures += 1
+                    print(f"SHARD FAIL {name} world={world}: a rank did not raise", flush=True)
+            continue
         cfg, tr, ref_kind = case(name)
         eng = gnoc.ShardedEngine(cfg, rank, world)
         eng.submit(tr)

@@ -47,6 +47,12 @@ def test_shard_three_ranks_uneven():
     launch(3, ["shape6", "sat8"])
 
 
+def test_shard_failure_on_one_rank_fails_every_rank():
+    """One rank's X phase fails (GNOC_FAIL_RANK): the status all-reduce around the
+    exchange makes every rank raise instead of waiting on the failed one."""
+    launch(3, ["fail", "syn8"])
+
+
 def _local_vs(cfg, tr, n, ref):
     from graphite_amd import gnoc
     import numpy as np
