@@ -76,6 +76,16 @@ __host__ __device__ __forceinline__ uint32_t field_of(uint32_t nd, uint32_t cont
 {
    return nd == cont ? 1u : nd == P_SELF ? 0u : nd == P_UP ? 2u : 3u;
 }
+// The same for a record of an X chain (XC) or a Y chain, from its destination and
+// the next tile (nx, ny): under XY routing an X-chain record has dx at or beyond
+// nx in the chain's direction, a Y-chain record dy at or beyond ny.
+template <bool XC>
+__device__ __forceinline__ uint32_t route_field(uint32_t nx, uint32_t ny, uint32_t aux)
+{
+   const uint32_t dx = aux & AUX_C_MASK, dy = (aux >> AUX_C_BITS) & AUX_C_MASK;
+   if (!XC) return dy != ny ? 1u : 0u;
+   return dx != nx ? 1u : dy > ny ? 2u : dy < ny ? 3u : 0u;
+}
 
 }  // namespace ch
 
@@ -136,6 +146,7 @@ struct Smem
    uint32_t saux[ICAP];
    ChainPort cp[3];               // ports i, i+1, i+2 (ring)
    uint32_t blo[2][NLMAX], bhi[2][NLMAX];   // window bounds of ports i+1, i+2 (ring)
+   uint32_t ioffs[2][NLMAX + 1];  // offsets of a port's local insert lists (by port parity)
 };
 
 __device__ __forceinline__ uint64_t ld1(const uint64_t* p)
@@ -300,12 +311,12 @@ __device__ bool poll_words(const ChainArgs& a, const uint64_t* s, uint32_t nw, u
 // Issue the loads of a port's local inserts of this window (registers); off =
 // the lists' offsets in the port's insert list (uniform).
 template <int NL>
-__device__ __forceinline__ uint32_t fetch_inserts(const Smem& sm, const ChainArgs& a, uint32_t ring, uint32_t br,
-                                                  Rec (&iv)[IPER], uint32_t (&off)[NLMAX + 1])
+__device__ __forceinline__ uint32_t fetch_inserts(Smem& sm, const ChainArgs& a, uint32_t ring, uint32_t br,
+                                                  Rec (&iv)[IPER], uint32_t parity)
 {
    const uint32_t lane = threadIdx.x;
    const ChainPort& P = sm.cp[ring];
-   uint32_t lo[NL];
+   uint32_t lo[NL], off[NL + 1];
    uint64_t base[NL];
    off[0] = 0;
 #pragma unroll
@@ -319,6 +330,8 @@ __device__ __forceinline__ uint32_t fetch_inserts(const Smem& sm, const ChainArg
       base[j] = sgpr64(P.ibase[j]) + lo[j];
    }
    const uint32_t itot = off[NL];
+   // the lists' offsets, for premerge (LDS: no scalar registers held across the step)
+   if (NL > 1 && lane <= (uint32_t) NL) sm.ioffs[parity][lane] = off[lane < (uint32_t) NL ? lane : NL];
 #pragma unroll
    for (int q = 0; q < IPER; q++)
    {
@@ -366,11 +379,14 @@ __device__ __forceinline__ bool store_inserts(Smem& sm, const Rec (&iv)[IPER], u
 // Y ports: the staged slot ranges (each sorted) merged into insert list `buf`:
 // own index + lower bounds in the other two ranges.
 template <int NL>
-__device__ __forceinline__ void premerge(Smem& sm, uint32_t itot, uint32_t buf, const uint32_t (&o)[NLMAX + 1])
+__device__ __forceinline__ void premerge(Smem& sm, uint32_t itot, uint32_t buf, uint32_t parity)
 {
    if (NL == 1) return;
    const uint32_t lane = threadIdx.x;
    wsync();
+   uint32_t o[NL + 1];
+#pragma unroll
+   for (int l = 0; l <= NL; l++) o[l] = sm.ioffs[parity][l];
 #pragma unroll
    for (int q = 0; q < IPER; q++)
    {
@@ -421,6 +437,7 @@ __device__ __forceinline__ uint32_t mp_split(const uint64_t* K, uint32_t nK, con
 
 // This lane's records of the merged stream (kept from x, inserts from y; cnt
 // of them) into registers, and their aggregate.
+template <bool XC>
 __device__ __forceinline__ Agg walk(const uint64_t* K, const uint32_t* KA, const uint64_t* I, const uint32_t* IA,
                                    uint32_t x, uint32_t y, uint32_t cnt, uint32_t wr, uint32_t d0, uint32_t nx,
                                    uint32_t ny, uint32_t cont, uint64_t (&rk)[PER], uint32_t (&ra)[PER], uint32_t& yend)
@@ -449,7 +466,7 @@ __device__ __forceinline__ Agg walk(const uint64_t* K, const uint32_t* KA, const
          const uint32_t nb = g.B + p, b2 = rcyc((uint32_t) (rk[j] >> 32), wr, d0) + p;
          g.B = nb > b2 ? nb : b2;
          g.A += p;
-         g.C += 1ull << (16 * field_of(xy_dir(nx, ny, aux_dx(ra[j]), aux_dy(ra[j])), cont));
+         g.C += 1ull << (16 * route_field<XC>(nx, ny, ra[j]));
       }
    }
    yend = y;
@@ -580,22 +597,20 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
    uint64_t rk[PER];
    uint32_t ra[PER];
    Rec iv[IPER];                 // the next port's inserts in flight
-   uint32_t off_f[NLMAX + 1];    // their lists' offsets
    uint32_t itot_f = 0;          // their count
    uint32_t cpv = 0, bv = 0;     // descriptor / bounds of the port after next, in flight
    uint32_t nK = 0, nI = 0;      // this port's kept records and inserts
    uint32_t P0cur = 0, nin_prev = 0, ncont_prev = 0;   // this port's chain input: records before / kept / all of this window
    {
-      uint32_t off0[NLMAX + 1];
-      nI = fetch_inserts<NL>(sm, a, 0, 0, iv, off0);
+      nI = fetch_inserts<NL>(sm, a, 0, 0, iv, 0);
       if (nI > (uint32_t) ICAP)
       {
          if (lane == 0) flag(a, F_RETRY);
          return;
       }
       if (store_inserts<NL>(sm, iv, nI, wbase, 0) && lane == 0) flag(a, F_FALLBACK);
-      premerge<NL>(sm, nI, 0, off0);
-      if (len > 1) itot_f = fetch_inserts<NL>(sm, a, 1, 1, iv, off_f);
+      premerge<NL>(sm, nI, 0, 0);
+      if (len > 1) itot_f = fetch_inserts<NL>(sm, a, 1, 1, iv, 1);
       if (len > 2)
       {
          if (lane < 32) cpv = fetch_cp(a.cp + cpb + 2, lane);
@@ -616,9 +631,6 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       // bounds; load the predecessor's state of this port
       CH_STAMP(0);
       const uint32_t itot = itot_f;
-      uint32_t off_c[NLMAX + 1];
-#pragma unroll
-      for (int l = 0; l <= NLMAX; l++) off_c[l] = off_f[l];
       bool ibad = false;
       if (has_next) ibad = store_inserts<NL>(sm, iv, itot, wbase, bn);
       if (i + 2 < len)
@@ -629,14 +641,6 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       uint64_t pv = 0;
       if (w && lane < (uint32_t) SW) pv = ld1(stp + lane);
       const uint32_t nx = sgpr(P.nx), ny = sgpr(P.ny), cont = sgpr(P.cont), rl = sgpr(P.rl), port = sgpr(P.port);
-      uint32_t ocap[4];
-      uint64_t obase[4];
-#pragma unroll
-      for (int f = 0; f < 4; f++)
-      {
-         ocap[f] = sgpr(P.ocap[f]);
-         obase[f] = sgpr64(P.obase[f]);
-      }
       wsync();
       CH_STAMP(7);
 
@@ -657,7 +661,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
             cnt = min(k, n - a0);
             const uint32_t y = mp_split(sm.kkey, nK, Ic, nI, a0);
             uint32_t yend = 0;
-            const Agg g0 = walk(sm.kkey, sm.kaux, Ic, IAc, a0 - y, y, cnt, wr, d0, nx, ny, cont, rk, ra, yend);
+            const Agg g0 = walk<NL == 1>(sm.kkey, sm.kaux, Ic, IAc, a0 - y, y, cnt, wr, d0, nx, ny, cont, rk, ra, yend);
 #ifdef CH_DEBUG
             // the next lane's split must be where this one's walk ended
             const uint32_t ynext = (uint32_t) __shfl_down((int) y, 1);
@@ -678,7 +682,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          first = false;
          if (ibad && lane == 0) flag(a, F_FALLBACK);
          // Y ports: the three insert ranges into one sorted list (read at the next step)
-         if (has_next) premerge<NL>(sm, itot, bn, off_c);
+         if (has_next) premerge<NL>(sm, itot, bn, (i + 1) & 1);
 
          // ---- [D] predecessor's state
          bool ok = true;
@@ -716,7 +720,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          CH_STAMP(3);
          // next prefetches (they land at the next step's [A]): port i+2's inserts (its
          // descriptor and bounds landed at this step's [A]), port i+3's descriptor and bounds
-         if (i + 2 < len) itot_f = fetch_inserts<NL>(sm, a, (i + 2) % 3, (i + 2) & 1, iv, off_f);
+         if (i + 2 < len) itot_f = fetch_inserts<NL>(sm, a, (i + 2) % 3, (i + 2) & 1, iv, (i + 2) & 1);
          if (i + 3 < len)
          {
             if (lane < 32) cpv = fetch_cp(a.cp + cpi + 3, lane);
@@ -784,7 +788,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          }
          ssum += cc;
          const uint64_t dn = (uint64_t) off + (uint64_t) cc * 1000ull + rl;   // t' - wbase
-         const uint32_t f = field_of(xy_dir(nx, ny, aux_dx(ax), aux_dy(ax)), cont);
+         const uint32_t f = route_field<NL == 1>(nx, ny, ax);
          uint32_t pos = 0;
 #pragma unroll
          for (int q = 0; q < 4; q++)
@@ -803,8 +807,10 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
                continue;
             }
          }
-         if (pos >= ocap[f]) { route = true; continue; }
-         const uint64_t gp = obase[f] + pos;
+         // the output slot of field f: read per record from the descriptor (no scalar
+         // registers held across the step; the next prefetch lands in another slot)
+         if (pos >= P.ocap[f]) { route = true; continue; }
+         const uint64_t gp = P.obase[f] + pos;
          const uint64_t tn = wbase + dn;
          if (f == 1)
          {
@@ -861,7 +867,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          {
             // every record of the port has passed: the route counts fill every output slot
             bool full = true;
-            for (uint32_t f = 0; f < 4; f++) full &= cin[f] + cf(tot.C, f) == ocap[f];
+            for (uint32_t f = 0; f < 4; f++) full &= cin[f] + cf(tot.C, f) == P.ocap[f];
             if (!full) flag(a, F_ROUTE);
          }
          if (n)

@@ -538,10 +538,6 @@ static uint64_t record_bound(const gnoc_engine* e, uint64_t records)
    return records + 64ull * ((uint64_t) e->dc.N * PORTS * INS) + 64;
 }
 
-static uint32_t fw_host(const gnoc_engine* e, uint32_t tile)
-{
-   return e->npoints > 1 ? e->h_pt_fw[point_of(e->dc, tile)] : (uint32_t) e->cfg.flit_width;
-}
 
 // Chain-engine windows (chain.hip): D = 2^shift ps with the busiest port's
 // expected records per window near CH_FILL of the LDS stream capacity (and its
