@@ -20,6 +20,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "gnoc.h"
 #include "kernels.hip"
 #include "level.hip"
@@ -101,6 +103,10 @@ struct gnoc_engine
    const uint32_t *d_src = nullptr, *d_dst = nullptr, *d_bits = nullptr, *d_flags = nullptr;
    DevBuf t_inj, t_src, t_dst, t_bits, t_flags;
    DevBuf vbuf;                             // submit-time checks and statistics (k_validate)
+   // gnoc_run_sharded: the engine's own exchange buffers and transport
+   DevBuf xsend, xrecv, xflag;
+   gnoc_transport tp{};
+   void* nccl = nullptr;                    // ncclComm_t (gnoc_shard_set_comm)
 
    // work
    DevBuf aux, routed, final_ps, zl, cont;
@@ -1638,6 +1644,110 @@ int gnoc_exchange_counts(gnoc_engine* e, uint64_t* send_units, uint64_t* recv_un
       if (recv_units) recv_units[q] = q < e->xr_units.size() ? e->xr_units[q] : 0;
    }
    return GNOC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// gnoc_run_sharded: begin -> all-to-all (RCCL or the caller's transport) -> finish
+// ---------------------------------------------------------------------------
+static int rccl_exchange(gnoc_engine* e, const void* send, const uint64_t* su, void* recv, const uint64_t* ru)
+{
+   ncclComm_t comm = static_cast<ncclComm_t>(e->nccl);
+   const int nr = e->nranks;
+   // grouped point-to-point: every peer pair is one xGMI transfer (no ring relay)
+   if (ncclGroupStart() != ncclSuccess) return fail(e, GNOC_EHIP, "ncclGroupStart");
+   uint64_t so = 0, ro = 0;
+   for (int q = 0; q < nr; q++)
+   {
+      if (su[q] && ncclSend(static_cast<const char*>(send) + so * 16, su[q] * 16, ncclChar, q, comm, e->stream) != ncclSuccess)
+         return fail(e, GNOC_EHIP, "ncclSend");
+      if (ru[q] && ncclRecv(static_cast<char*>(recv) + ro * 16, ru[q] * 16, ncclChar, q, comm, e->stream) != ncclSuccess)
+         return fail(e, GNOC_EHIP, "ncclRecv");
+      so += su[q];
+      ro += ru[q];
+   }
+   if (ncclGroupEnd() != ncclSuccess) return fail(e, GNOC_EHIP, "ncclGroupEnd");
+   GNOC_HIP(e, hipStreamSynchronize(e->stream));
+   return GNOC_OK;
+}
+
+static int rccl_agree(gnoc_engine* e, int32_t status, int32_t* out)
+{
+   ncclComm_t comm = static_cast<ncclComm_t>(e->nccl);
+   GNOC_HIP(e, e->xflag.ensure(16));
+   int32_t* h = reinterpret_cast<int32_t*>(e->h_pinned + 15);
+   *h = status;
+   GNOC_HIP(e, hipMemcpyAsync(e->xflag.p, h, 4, hipMemcpyHostToDevice, e->stream));
+   if (ncclAllReduce(e->xflag.p, e->xflag.p, 1, ncclInt32, ncclMax, comm, e->stream) != ncclSuccess)
+      return fail(e, GNOC_EHIP, "ncclAllReduce (status)");
+   GNOC_HIP(e, hipMemcpyAsync(h, e->xflag.p, 4, hipMemcpyDeviceToHost, e->stream));
+   GNOC_HIP(e, hipStreamSynchronize(e->stream));
+   *out = *h;
+   return GNOC_OK;
+}
+
+int gnoc_shard_set_comm(gnoc_engine* e, void* nccl_comm)
+{
+   if (!e) return GNOC_EINVAL;
+   if (!nccl_comm) return fail(e, GNOC_EINVAL, "null ncclComm_t");
+   int nr = 0, rk = 0, dev = -1;
+   if (ncclCommCount(static_cast<ncclComm_t>(nccl_comm), &nr) != ncclSuccess ||
+       ncclCommUserRank(static_cast<ncclComm_t>(nccl_comm), &rk) != ncclSuccess ||
+       ncclCommCuDevice(static_cast<ncclComm_t>(nccl_comm), &dev) != ncclSuccess)
+      return fail(e, GNOC_EINVAL, "not a valid ncclComm_t");
+   if (nr != e->nranks || rk != e->rank)
+      return fail(e, GNOC_EINVAL, "communicator rank / size differ from gnoc_shard's");
+   if (dev != e->cfg.device) return fail(e, GNOC_EINVAL, "communicator on another device than the engine's");
+   e->nccl = nccl_comm;
+   e->tp = gnoc_transport{};
+   return GNOC_OK;
+}
+
+int gnoc_shard_set_transport(gnoc_engine* e, const gnoc_transport* tp)
+{
+   if (!e || !tp) return GNOC_EINVAL;
+   if (!tp->exchange || !tp->agree) return fail(e, GNOC_EINVAL, "transport needs exchange and agree");
+   e->tp = *tp;
+   e->nccl = nullptr;
+   return GNOC_OK;
+}
+
+static int shard_agree(gnoc_engine* e, int rc, const char* what)
+{
+   int32_t any = 0;
+   const int32_t mine = rc ? 1 : 0;
+   int trc = e->nccl ? rccl_agree(e, mine, &any) : (e->tp.agree(e->tp.ctx, mine, &any) ? GNOC_EHIP : GNOC_OK);
+   if (trc) return rc ? rc : (e->nccl ? trc : fail(e, GNOC_EHIP, std::string("transport agree failed after ") + what));
+   if (rc) return rc;
+   if (any) return fail(e, GNOC_EHIP, std::string(what) + " failed on another rank");
+   return GNOC_OK;
+}
+
+int gnoc_run_sharded(gnoc_engine* e)
+{
+   if (!e) return GNOC_EINVAL;
+   if (e->nranks <= 1) return gnoc_run(e);
+   if (!e->nccl && !e->tp.exchange) return fail(e, GNOC_ESTATE, "gnoc_run_sharded needs gnoc_shard_set_comm or a transport");
+   if (!e->submitted) return fail(e, GNOC_ESTATE, "gnoc_run_sharded before gnoc_submit");
+   uint64_t ns = 0, nrv = 0;
+   for (uint64_t u : e->xs_units) ns += u;
+   for (uint64_t u : e->xr_units) nrv += u;
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   GNOC_HIP(e, e->xsend.ensure(std::max<uint64_t>(ns, 1) * 16));
+   GNOC_HIP(e, e->xrecv.ensure(std::max<uint64_t>(nrv, 1) * 16));
+   std::vector<uint64_t> su((size_t) e->nranks, 0), ru((size_t) e->nranks, 0);
+   for (size_t q = 0; q < su.size(); q++)
+   {
+      su[q] = q < e->xs_units.size() ? e->xs_units[q] : 0;
+      ru[q] = q < e->xr_units.size() ? e->xr_units[q] : 0;
+   }
+   int rc = shard_agree(e, gnoc_run_begin(e, e->xsend.p), "gnoc_run_begin");
+   if (rc) return rc;
+   if (e->nccl) rc = rccl_exchange(e, e->xsend.p, su.data(), e->xrecv.p, ru.data());
+   else if (e->tp.exchange(e->tp.ctx, e->xsend.p, su.data(), e->xrecv.p, ru.data(), e->stream))
+      rc = fail(e, GNOC_EHIP, "transport exchange failed");
+   rc = shard_agree(e, rc, "the turn exchange");
+   if (rc) return rc;
+   return shard_agree(e, gnoc_run_finish(e, e->xrecv.p), "gnoc_run_finish");
 }
 
 int gnoc_run_begin(gnoc_engine* e, void* send_buf)

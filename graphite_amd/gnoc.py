@@ -39,6 +39,7 @@ EXPORTED = (
     "gnoc_last_error", "gnoc_destroy", "gnoc_trace_synthetic", "gnoc_abi_version",
     "gnoc_set_profiling", "gnoc_get_kernel_stats", "gnoc_trace_file_write", "gnoc_trace_file_read",
     "gnoc_trace_file_write_q", "gnoc_trace_file_read_q", "gnoc_trace_synthetic_pattern",
+    "gnoc_shard_set_comm", "gnoc_shard_set_transport", "gnoc_run_sharded",
     "gnoc_shard", "gnoc_exchange_counts", "gnoc_run_begin", "gnoc_run_finish",
     "gnoc_create_sweep", "gnoc_sweep_layout", "gnoc_get_port_utilization", "gnoc_create_hop_counter",
     "gnoc_get_broadcast_results", "gnoc_get_broadcast_info", "gnoc_set_basic_moving_average",

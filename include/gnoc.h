@@ -290,6 +290,30 @@ int gnoc_exchange_counts(gnoc_engine *eng, uint64_t *send_units, uint64_t *recv_
 int gnoc_run_begin(gnoc_engine *eng, void *send_dev);
 int gnoc_run_finish(gnoc_engine *eng, const void *recv_dev);
 
+/* The same run without a caller-side harness (SURVEY.md 8b:
+ * gnoc_create_sharded(cfg, rank, nranks, ncclComm_t)): the engine keeps the
+ * send / receive buffers and does the all-to-all itself, either over RCCL
+ * (gnoc_shard_set_comm: an ncclComm_t of the shard count, this engine's rank,
+ * on this engine's device; grouped ncclSend / ncclRecv over xGMI) or through a
+ * caller transport (gnoc_shard_set_transport; in-process tests, other fabrics).
+ * Around the exchange every rank's status is max-reduced, so a failure on one
+ * rank fails every rank's gnoc_run_sharded (none waits on a failed peer). */
+typedef struct gnoc_transport
+{
+   /* Move send_units[q] 16-byte units to rank q and receive recv_units[q] from it
+    * (rank q's block starts at the sum of the units of ranks < q; own entry 0).
+    * Device buffers; `stream` (a hipStream_t) holds the producing work.
+    * Return 0 when the receive buffer is complete. */
+   int (*exchange)(void *ctx, const void *send_dev, const uint64_t *send_units, void *recv_dev,
+                   const uint64_t *recv_units, void *stream);
+   /* *out = max over ranks of `status` (0 = ok); return 0 on success. */
+   int (*agree)(void *ctx, int32_t status, int32_t *out);
+   void *ctx;
+} gnoc_transport;
+int gnoc_shard_set_comm(gnoc_engine *eng, void *nccl_comm);
+int gnoc_shard_set_transport(gnoc_engine *eng, const gnoc_transport *tp);
+int gnoc_run_sharded(gnoc_engine *eng);
+
 const char *gnoc_last_error(const gnoc_engine *eng);
 void gnoc_destroy(gnoc_engine *eng);
 

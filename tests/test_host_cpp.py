@@ -64,6 +64,33 @@ def test_trace_header_carries_moving_average(tmp_path):
 
 
 @pytest.mark.gpu
+def test_cpp_sharded_run_through_c_transport():
+    """gnoc_run_sharded over the in-process C transport (2, 3, 5 ranks == unsharded;
+    a failure on one rank fails all): multi-GPU without Python or torch."""
+    r = subprocess.run([os.path.join(BUILD, "test_shard_transport")], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert "every rank failed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_replay_sharded_matches_unsharded(tmp_path):
+    """gnoc_replay --shards 4 (C ABI, in-process transport) writes the same results
+    file as the unsharded replay."""
+    cfg = gnoc.EngineConfig(num_tiles=256)
+    tr = gnoc.synthetic_trace(16, 16, 0.01, 200, seed=4)
+    trace = str(tmp_path / "t.gtr")
+    gnoc.write_trace_file(trace, cfg, tr)
+    outs = []
+    for extra in ([], ["--shards", "4"]):
+        out = str(tmp_path / f"r{len(outs)}.bin")
+        r = subprocess.run([os.path.join(BUILD, "gnoc_replay"), trace, "--results", out] + extra, capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stderr
+        outs.append(np.fromfile(out, np.uint64))
+    assert outs[0].size == outs[1].size and np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
 def test_cpp_known_answers():
     r = subprocess.run([os.path.join(BUILD, "test_emesh_hop_by_hop_hip")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
