@@ -63,9 +63,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (a one-GPU box): every rank on device 0, exchange over gloo
+    if os.environ.get("GNOC_BENCH_ONE_GPU"):
+        local = 0
+    backend = os.environ.get("GNOC_BENCH_BACKEND", "nccl")   # nccl = RCCL over xGMI
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
 
@@ -197,7 +204,7 @@ def main():
             # configs[1] number that needed one
             "reruns": {"retries": int(summ.get("retries", 0)), "fallbacks": int(summ.get("fallbacks", 0))},
             "e2e_ms_per_step": e2e_ms,
-            "e2e_note": "submit from pinned host memory (host validation + H2D) + run + final_ps D2H",
+            "e2e_note": "submit from pinned host memory (H2D + device-side trace checks) + run + final_ps D2H",
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
