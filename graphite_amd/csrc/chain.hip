@@ -40,17 +40,17 @@ namespace ch {
 // program order).
 constexpr int T = 64;
 #ifndef CH_PER_V
-#define CH_PER_V 12
+#define CH_PER_V 11
 #endif
 constexpr int PER = CH_PER_V;             // stream records per lane
 constexpr int CAP = PER * T;              // stream records per (port, window)
 #ifndef CH_IPER_V
-#define CH_IPER_V 3
+#define CH_IPER_V 2
 #endif
 constexpr int IPER = CH_IPER_V;
 constexpr int ICAP = IPER * T;            // inserts per (port, window), + spill-ins of the slow path
 #ifndef CH_MINW
-#define CH_MINW 2                         // waves per SIMD the registers must leave room for
+#define CH_MINW 3                         // waves per SIMD the registers must leave room for
 #endif
 constexpr int NLMAX = 3;                  // local insert lists (Y ports: LOCAL, W, E)
 constexpr int SW = 8;                     // state words per (chain port, window)
@@ -142,8 +142,6 @@ struct Smem
    uint32_t iaux[2][ICAP + 1];
    uint64_t rkey[ICAP + 1];       // Y ports' three fetched slot ranges (premerge -> ikey); the slow
    uint32_t raux[ICAP + 1];       // path's inserts + spill-ins
-   uint64_t skey[ICAP];           // the slow path's spill-ins as loaded
-   uint32_t saux[ICAP];
    ChainPort cp[3];               // ports i, i+1, i+2 (ring)
    uint32_t blo[2][NLMAX], bhi[2][NLMAX];   // window bounds of ports i+1, i+2 (ring)
    uint32_t ioffs[2][NLMAX + 1];  // offsets of a port's local insert lists (by port parity)
@@ -479,7 +477,7 @@ __device__ __forceinline__ Agg walk(const uint64_t* K, const uint32_t* KA, const
 // the staging list.  Returns the records taken; skip = those consumed by
 // earlier windows.
 __device__ uint32_t spill_in(Smem& sm, const ChainArgs& a, uint64_t sbase, uint32_t spn, const uint64_t* I,
-                             const uint32_t* IA, uint32_t nI, uint64_t wbase, uint64_t wlen, uint32_t& skip)
+                             const uint32_t* IA, uint32_t nI, uint32_t nK, uint64_t wbase, uint64_t wlen, uint32_t& skip)
 {
    const uint32_t lane = threadIdx.x;
    Rec sv[IPER];
@@ -505,14 +503,17 @@ __device__ uint32_t spill_in(Smem& sm, const ChainArgs& a, uint64_t sbase, uint3
    skip = rdl(wave_sum32(nb), 63);
    const uint32_t take = rdl(wave_sum32(nt), 63);
    if (!take) return 0;
+   // staged right behind the kept list's end (the caller checked the room)
+   uint64_t* const sk = sm.kkey + pad(nK) + 1;
+   uint32_t* const sa = sm.kaux + pad(nK) + 1;
 #pragma unroll
    for (int q = 0; q < IPER; q++)
    {
       const uint32_t g = lane + (uint32_t) q * T;
       if (g < spn && sv[q].t >= wbase && sv[q].t - wbase < wlen)
       {
-         sm.skey[g - skip] = ((sv[q].t - wbase) << 32) | sv[q].id;
-         sm.saux[g - skip] = sv[q].aux;
+         sk[g - skip] = ((sv[q].t - wbase) << 32) | sv[q].id;
+         sa[g - skip] = sv[q].aux;
       }
    }
    wsync();
@@ -522,15 +523,15 @@ __device__ uint32_t spill_in(Smem& sm, const ChainArgs& a, uint64_t sbase, uint3
       const uint32_t g = lane + (uint32_t) q * T;
       if (g < take)
       {
-         const uint64_t k = sm.skey[g];
+         const uint64_t k = sk[g];
          const uint32_t p = g + lb(I, nI, k);
          sm.rkey[p] = k;
-         sm.raux[p] = sm.saux[g];
+         sm.raux[p] = sa[g];
       }
       if (g < nI)
       {
          const uint64_t k = I[g];
-         const uint32_t p = g + lb(sm.skey, take, k);
+         const uint32_t p = g + lb(sk, take, k);
          sm.rkey[p] = k;
          sm.raux[p] = IA[g];
       }
@@ -729,14 +730,15 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          if (Pep == Kpp) break;
          // ---- slow path: spill-ins join the insert list, then rescan
          const uint32_t spn = Pep - Kpp;
-         const bool sok = i > 0 && spn + nI <= (uint32_t) ICAP && (uint64_t) Kpp + spn <= a.cp[cpi - 1].ocap[1];
+         const bool sok = i > 0 && spn + nI <= (uint32_t) ICAP && (uint64_t) Kpp + spn <= a.cp[cpi - 1].ocap[1] &&
+                          pad(nK) + 1 + spn <= (uint32_t) CAPP;   // room to stage the spills behind the kept list
          if (!sok)
          {
             if (lane == 0) flag(a, F_FALLBACK);
             return;
          }
          uint32_t skip = 0;
-         const uint32_t take = spill_in(sm, a, a.cp[cpi - 1].obase[1] + Kpp, spn, Ic, IAc, nI, wbase, wlen, skip);
+         const uint32_t take = spill_in(sm, a, a.cp[cpi - 1].obase[1] + Kpp, spn, Ic, IAc, nI, nK, wbase, wlen, skip);
          if (n + take > (uint32_t) CAP)
          {
             if (lane == 0) flag(a, F_RETRY);

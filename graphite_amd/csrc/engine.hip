@@ -549,7 +549,7 @@ static uint64_t record_bound(const gnoc_engine* e, uint64_t records)
 // expected records per window near CH_FILL of the LDS stream capacity (and its
 // inserts within the insert buffer), assuming a steady rate over [0, t_last].
 // nW = t_last / D + 1 windows, the last one unbounded.  shift 0 = chain off.
-static constexpr double CH_FILL = 0.5;
+static constexpr double CH_FILL = 0.55;
 static constexpr uint32_t CH_NW_MAX = 4096;
 static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, uint64_t t_last)
 {
