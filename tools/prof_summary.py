@@ -1,6 +1,7 @@
 """Summarise a tools/gpu_round.sh profile directory: per-kernel time, the
 per-level k_level durations and launch gaps (kernel trace), and HBM bytes per
-k_level launch from the FETCH_SIZE / WRITE_SIZE passes.  Writes pmc.json next
+launch of the dominant kernel (k_chain on v4, k_level on v3) and of k_level,
+from the FETCH_SIZE / WRITE_SIZE passes.  Writes pmc.json next
 to the CSVs (bench.py reads the committed copy for roofline.traffic).
 
 FETCH_SIZE is doubled per MI355X_MICROARCH.md "HBM [CDNA4]" (gfx950 tallies
@@ -59,29 +60,38 @@ if steps:
         print(f"step span (first to last kernel) {(e1 - s0) / 1e6:.3f} ms")
 
 
-def pmc(pattern, counter):
+def pmc(pattern, counter, kernel):
     vals = defaultdict(list)
     for r in rows(pattern):
-        if r.get("Counter_Name") == counter and short(r["Kernel_Name"]) == "k_level":
+        if r.get("Counter_Name") == counter and short(r["Kernel_Name"]) == kernel:
             vals[r["Dispatch_Id"]].append(float(r["Counter_Value"]))
     return [sum(v) for v in vals.values()]
 
 
-fe = pmc("fetch_counter_collection.csv", "FETCH_SIZE")
-wr = pmc("write_counter_collection.csv", "WRITE_SIZE")
-if fe and wr:
+# the dominant kernel (most device time): k_chain on the v4 engine, k_level on v3
+tot = {k: sum(v) for k, v in per.items() if k in ("k_chain", "k_level", "k_port_stream")}
+dom = max(tot, key=tot.get) if tot else "k_level"
+wl = None
+for f in glob.glob(os.path.join(d, "bench_fetch.json")):
+    for ln in open(f):
+        if ln.startswith("{"):
+            wl = json.loads(ln)["config"]["workload"]
+out = {"kernel": dom, "workload": wl,
+       "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); KB units x1024", "per_kernel": {}}
+for k in [dom] + [x for x in ("k_chain", "k_level") if x != dom]:
+    fe = pmc("fetch_counter_collection.csv", "FETCH_SIZE", k)
+    wr = pmc("write_counter_collection.csv", "WRITE_SIZE", k)
+    if not (fe and wr):
+        continue
     # counters are in KB (rocprofv3 derived FETCH_SIZE / WRITE_SIZE)
     fb = 2 * 1024 * sum(fe) / len(fe)
     wb = 1024 * sum(wr) / len(wr)
-    wl = None
-    for f in glob.glob(os.path.join(d, "bench_fetch.json")):
-        for ln in open(f):
-            if ln.startswith("{"):
-                wl = json.loads(ln)["config"]["workload"]
-    out = {"kernel": "k_level", "workload": wl, "launches_fetch": len(fe), "launches_write": len(wr),
-           "fetch_bytes_per_launch_corrected": fb, "write_bytes_per_launch": wb,
-           "traffic_bytes_per_launch": fb + wb,
-           "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section); KB units x1024"}
-    print("\nPMC per k_level launch: fetch %.1f MB (corrected), write %.1f MB, total %.1f MB" % (fb / 1e6, wb / 1e6, (fb + wb) / 1e6))
+    avg_us = sum(per[k]) / len(per[k]) / 1e3 if per.get(k) else None
+    out["per_kernel"][k] = {"launches_fetch": len(fe), "launches_write": len(wr),
+                            "fetch_bytes_per_launch_corrected": fb, "write_bytes_per_launch": wb,
+                            "traffic_bytes_per_launch": fb + wb, "kernel_trace_avg_us": avg_us}
+    print("\nPMC per %s launch: fetch %.1f MB (corrected), write %.1f MB, total %.1f MB" % (k, fb / 1e6, wb / 1e6, (fb + wb) / 1e6))
+if dom in out["per_kernel"]:
+    out.update(out["per_kernel"][dom])
     with open(os.path.join(d, "pmc.json"), "w") as fh:
         json.dump(out, fh, indent=1)
