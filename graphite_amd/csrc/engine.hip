@@ -152,7 +152,7 @@ struct gnoc_engine
    // QueueModelBasic with a moving average (gnoc_set_basic_moving_average, serial.hip)
    int ma_type = 0;
    uint32_t ma_window = 1;
-   DevBuf ma_t, ma_key, ma_val, ma_key2, ma_val2, ma_lo, ma_hi, ma_d, ma_tmp;
+   DevBuf ma_t, ma_key, ma_val, ma_key2, ma_val2, ma_lo, ma_hi, ma_d, ma_tmp, ma_ref, ma_agg, ma_m;
 
    // v4 chain engine (chain.hip): windows of 2^ch_shift ps, ch_nw of them (sized at submit)
    uint32_t ch_shift = 0, ch_nw = 0;
@@ -584,10 +584,17 @@ static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t
    const size_t nd = (size_t) 2 * H * (W + 1) + (size_t) 2 * W * (H + 1);   // difference arrays (int)
    const size_t ni = (size_t) 4 * N;                                       // inserts per X / Y port
    const size_t off_x = (sizeof(ValOut) + (nd + ni) * 4 + 7) / 8 * 8;
-   const size_t bytes = off_x + (size_t) nr * nr * 8;
+   // block-private statistics in LDS when the table (+ the turn counts) fits a
+   // CU's LDS: nblk partial tables behind the turn counts, summed by k_validate_sum
+   const uint32_t ntab = (uint32_t) (nd + ni);
+   const size_t lds = ((size_t) ntab + (size_t) nr * nr) * 4;
+   const bool lh = n && lds <= 150 * 1024;
+   const uint32_t nblk = lh ? (uint32_t) std::min<uint64_t>((n + 4095) / 4096, lds <= 64 * 1024 ? 512 : 256) : 0;
+   const size_t off_p = (off_x + (size_t) nr * nr * 8 + 255) / 256 * 256;
+   const size_t bytes = off_p + (size_t) nblk * ntab * 4;
    static_assert(sizeof(ValOut) <= 128, "ValOut lands in the 128-B pinned staging");
    GNOC_HIP(e, e->vbuf.ensure(bytes));
-   GNOC_HIP(e, hipMemsetAsync(e->vbuf.p, 0, bytes, s));
+   GNOC_HIP(e, hipMemsetAsync(e->vbuf.p, 0, off_p, s));
    GNOC_HIP(e, hipMemsetAsync(e->vbuf.p, 0xFF, sizeof(unsigned long long) * VB_KINDS, s));
    char* base = static_cast<char*>(e->vbuf.p);
    ValOut* vo = reinterpret_cast<ValOut*>(base);
@@ -598,13 +605,27 @@ static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t
    uint32_t* insx = reinterpret_cast<uint32_t*>(dyd + (size_t) W * (H + 1));
    uint32_t* insy = insx + 2 * (size_t) N;
    unsigned long long* xcnt = reinterpret_cast<unsigned long long*>(base + off_x);
+   int* part = reinterpret_cast<int*>(base + off_p);
    if (n)
    {
-      const uint32_t grid = (uint32_t) std::min<uint64_t>((n + 255) / 256, 4096);
       const int tree = e->cfg.broadcast_tree_enabled && !e->dc.hop_counter;
-      hipLaunchKernelGGL(k_validate, dim3(grid), dim3(256), 0, s, e->dc, (uint64_t) n, e->d_inj, e->d_src, e->d_dst,
-                         e->d_bits, e->d_flags, tree, e->npoints > 1 ? 1u : 0u, nr, (uint32_t) e->rank, vo, dxr, dxl, dyu,
-                         dyd, insx, insy, xcnt);
+      const uint32_t sweep = e->npoints > 1 ? 1u : 0u;
+      if (lh)
+      {
+         if (lds > 64 * 1024)
+            GNOC_HIP(e, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_validate<true>),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
+         hipLaunchKernelGGL(k_validate<true>, dim3(nblk), dim3(256), lds, s, e->dc, (uint64_t) n, e->d_inj, e->d_src,
+                            e->d_dst, e->d_bits, e->d_flags, tree, sweep, nr, (uint32_t) e->rank, vo, dxr, ntab, part, xcnt);
+         GNOC_HIP(e, hipGetLastError());
+         hipLaunchKernelGGL(k_validate_sum, dim3((ntab + 255) / 256), dim3(256), 0, s, ntab, nblk, part, dxr);
+      }
+      else
+      {
+         const uint32_t grid = (uint32_t) std::min<uint64_t>((n + 255) / 256, 4096);
+         hipLaunchKernelGGL(k_validate<false>, dim3(grid), dim3(256), 0, s, e->dc, (uint64_t) n, e->d_inj, e->d_src,
+                            e->d_dst, e->d_bits, e->d_flags, tree, sweep, nr, (uint32_t) e->rank, vo, dxr, ntab, part, xcnt);
+      }
       GNOC_HIP(e, hipGetLastError());
       hipLaunchKernelGGL(k_validate_max, dim3(1), dim3(1024), 0, s, W, H, dxr, dxl, dyu, dyd, insx, insy, vo);
       GNOC_HIP(e, hipGetLastError());
@@ -1402,6 +1423,10 @@ static int run_ma(gnoc_engine* e)
    GNOC_HIP(e, e->ma_lo.ensure((size_t) maxloc * 4));
    GNOC_HIP(e, e->ma_hi.ensure((size_t) maxloc * 4));
    GNOC_HIP(e, e->ma_d.ensure(n * 8 + 8));
+   GNOC_HIP(e, e->ma_ref.ensure(n * 8 + 8));
+   const size_t nsb = (n + MS_CH - 1) / MS_CH + 1;   // scan blocks
+   GNOC_HIP(e, e->ma_agg.ensure(nsb * 28 + 64));
+   GNOC_HIP(e, e->ma_m.ensure(64));
    GNOC_HIP(e, e->counters.ensure(64));
    for (DevBuf* b : { &e->port_sum, &e->port_cnt, &e->port_mg1, &e->port_flit, &e->port_last })
    {
@@ -1440,26 +1465,61 @@ static int run_ma(gnoc_engine* e)
                                                         end_bit, s));
          GNOC_HIP(e, hipMemsetAsync(e->ma_lo.p, 0, (size_t) nloc * 4, s));
          GNOC_HIP(e, hipMemsetAsync(e->ma_hi.p, 0, (size_t) nloc * 4, s));
+         GNOC_HIP(e, hipMemsetAsync(e->ma_m.p, 0, 4, s));
+         const uint32_t* mcnt = e->ma_m.as<uint32_t>();
          hipLaunchKernelGGL(k_ma_bounds, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid,
-                            (const uint64_t*) e->ma_key2.as<uint64_t>(), e->ma_lo.as<uint32_t>(), e->ma_hi.as<uint32_t>());
+                            (const uint64_t*) e->ma_key2.as<uint64_t>(), e->ma_lo.as<uint32_t>(), e->ma_hi.as<uint32_t>(),
+                            e->ma_m.as<uint32_t>());
          GNOC_HIP(e, hipGetLastError());
          // the sort's inputs are free now: request cycles into ma_key, flits into ma_val
-         hipLaunchKernelGGL(k_ma_gather, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid, c.flit_width, c.f,
-                            e->ma_type, e->ma_window, (const uint64_t*) e->ma_key2.as<uint64_t>(),
-                            (const uint32_t*) e->ma_val2.as<uint32_t>(), e->d_bits,
-                            (const uint32_t*) e->ma_lo.as<uint32_t>(), e->ma_key.as<uint64_t>(), e->ma_val.as<uint32_t>(),
-                            e->ma_d.as<double>());
+         const uint64_t* skey = e->ma_key2.as<uint64_t>();
+         const uint32_t* lo = e->ma_lo.as<uint32_t>();
+         const uint32_t* hi = e->ma_hi.as<uint32_t>();
+         const uint32_t* ports = e->d_lvl_ports.as<uint32_t>() + k0;
+         uint64_t* tcs = e->ma_key.as<uint64_t>();
+         uint32_t* Fs = e->ma_val.as<uint32_t>();
+         uint64_t* ref = e->ma_ref.as<uint64_t>();
+#define GNOC_MA_GATHER(MT)                                                                                          \
+   hipLaunchKernelGGL(k_ma_gather<MT>, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid, c.flit_width, c.f,        \
+                      e->ma_window, skey, (const uint32_t*) e->ma_val2.as<uint32_t>(), e->d_bits, lo, tcs, Fs,      \
+                      e->ma_d.as<double>(), ref)
+#define GNOC_MA_CHAIN(MT)                                                                                           \
+   hipLaunchKernelGGL(k_ma_chain<MT>, dim3((nloc + 63) / 64), dim3(64), 0, s, nloc, e->ma_window,                  \
+                      (const uint64_t*) tcs, lo, hi, (const double*) e->ma_d.as<double>(), e->ma_ref.as<double>())
+         if (e->ma_type == MA_MEDIAN) GNOC_MA_GATHER(MA_MEDIAN);
+         else if (e->ma_type == MA_GEOMETRIC) GNOC_MA_GATHER(MA_GEOMETRIC);
+         else GNOC_MA_GATHER(MA_ARITHMETIC);
          GNOC_HIP(e, hipGetLastError());
-#define GNOC_MA_WALK(MT)                                                                                     \
-   hipLaunchKernelGGL(k_ma_walk<MT>, dim3((nloc + 63) / 64), dim3(64), 0, s, nloc,                            \
-                      e->d_lvl_ports.as<uint32_t>() + k0, e->ma_window, (const uint64_t*) e->ma_key.as<uint64_t>(), \
-                      (const uint32_t*) e->ma_val.as<uint32_t>(), (const uint32_t*) e->ma_lo.as<uint32_t>(),      \
-                      (const uint32_t*) e->ma_hi.as<uint32_t>(), (const double*) e->ma_d.as<double>(),           \
-                      e->ma_d.as<uint64_t>(), e->port_sum.as<uint64_t>(),                                          \
-                      e->port_cnt.as<uint64_t>(), e->port_flit.as<uint64_t>(), e->port_last.as<uint64_t>())
-         if (e->ma_type == MA_MEDIAN) GNOC_MA_WALK(MA_MEDIAN);
-         else GNOC_MA_WALK(MA_ARITHMETIC);   // the geometric mean is refused at gnoc_set_basic_moving_average
-#undef GNOC_MA_WALK
+         if (e->ma_type == MA_GEOMETRIC) GNOC_MA_CHAIN(MA_GEOMETRIC);
+         else if (e->ma_type == MA_ARITHMETIC) GNOC_MA_CHAIN(MA_ARITHMETIC);
+         GNOC_HIP(e, hipGetLastError());
+#undef GNOC_MA_GATHER
+#undef GNOC_MA_CHAIN
+         // the queue: segmented max-plus scan (delays into ma_d, free once the chain ran)
+         uint64_t* bA = e->ma_agg.as<uint64_t>();
+         uint64_t* bB = bA + nsb;
+         uint64_t* qin = bB + nsb;
+         uint32_t* bR = reinterpret_cast<uint32_t*>(qin + nsb);
+         const uint32_t sgrid = (uint32_t) ((n + MS_CH - 1) / MS_CH);
+         uint64_t* dout = e->ma_d.as<uint64_t>();
+#define GNOC_MA_SCAN(MT)                                                                                            \
+   do                                                                                                               \
+   {                                                                                                                \
+      hipLaunchKernelGGL(k_ma_scan1<MT>, dim3(sgrid), dim3(MS_T), 0, s, mcnt, skey, lo, (const uint64_t*) ref,      \
+                         (const uint32_t*) Fs, bA, bB, bR);                                                         \
+      hipLaunchKernelGGL(k_ma_scan2, dim3(1), dim3(64), 0, s, mcnt, (const uint64_t*) bA, (const uint64_t*) bB,     \
+                         (const uint32_t*) bR, qin);                                                                \
+      hipLaunchKernelGGL(k_ma_scan3<MT>, dim3(sgrid), dim3(MS_T), 0, s, mcnt, skey, lo, hi, ports,                  \
+                         (const uint64_t*) ref, (const uint32_t*) Fs, (const uint64_t*) qin, dout,                  \
+                         e->port_last.as<uint64_t>());                                                              \
+   } while (0)
+         if (e->ma_type == MA_MEDIAN) GNOC_MA_SCAN(MA_MEDIAN);
+         else GNOC_MA_SCAN(MA_ARITHMETIC);   // arithmetic and geometric: ref = (T) mean, the same conversion
+#undef GNOC_MA_SCAN
+         GNOC_HIP(e, hipGetLastError());
+         hipLaunchKernelGGL(k_ma_ports, dim3(nloc, 16), dim3(256), 0, s, ports, lo, hi, (const uint64_t*) dout,
+                            (const uint32_t*) Fs, e->port_sum.as<unsigned long long>(),
+                            e->port_cnt.as<unsigned long long>(), e->port_flit.as<unsigned long long>());
          GNOC_HIP(e, hipGetLastError());
          hipLaunchKernelGGL(k_ma_apply, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid,
                             (const uint32_t*) e->d_lvl_ports.as<uint32_t>() + k0, c.f, c.rl_ps,
@@ -1496,12 +1556,8 @@ int gnoc_set_basic_moving_average(gnoc_engine* e, int32_t type, uint32_t window_
       return fail(e, GNOC_EINVAL, "moving_avg_window_size must be in [1, 65536]");
    if (type != GNOC_MOVING_AVG_NONE && (e->nranks > 1 || e->npoints > 1 || e->dc.hop_counter))
       return fail(e, GNOC_EUNSUPPORTED, "moving-average queues run on one unsharded mesh engine");
-   // MovingGeometricMean::compute is a chain of pow() calls (moving_average.h:124-145):
-   // the device's pow and glibc's differ in the last bit on some operands, and the
-   // running product carries such a bit into the truncated reference time (measured:
-   // 17,670 of 20,000 packets differ on an 8x8 batch).  Refused rather than approximated.
-   if (type == GNOC_MOVING_AVG_GEOMETRIC_MEAN)
-      return fail(e, GNOC_EUNSUPPORTED, "geometric_mean moving average (pow is not bit-reproducible vs glibc)");
+   // MovingGeometricMean::compute is a chain of pow() calls (moving_average.h:119-135):
+   // the engine runs glibc's own pow algorithm and tables (glibc_pow.h), bit-exact.
    e->ma_type = type;
    e->ma_window = type ? window_size : 1;
    e->ran = false;

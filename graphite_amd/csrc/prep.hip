@@ -134,16 +134,37 @@ __device__ __forceinline__ uint32_t band_of(uint32_t y, uint32_t nr, uint32_t D)
    return (uint32_t) (((uint64_t) (y + 1) * nr - 1) / D);   // inverse of band_lo(b) = b D / nr
 }
 
+// The statistics table (ints, in this order): dxr, dxl [H (W + 1)] (X difference
+// arrays), dyu, dyd [W (H + 1)] (Y), insx, insy [2 N] (inserts per X / Y port).
+// LH: the block counts into a private copy in LDS (dynamic shared memory: the
+// table, then nr^2 turn counts) and stores it to part[block] for k_validate_sum
+// -- the per-packet atomics then never meet in L2 (10 M packets on 32x32: 3.5 ms
+// of L2 atomics -> LDS).  Otherwise the atomics go to the global table.
+template <bool LH>
 __global__ __launch_bounds__(256) void k_validate(DevCfg c, uint64_t n, const uint64_t* __restrict__ inj,
                                                   const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
                                                   const uint32_t* __restrict__ bits, const uint32_t* __restrict__ flags,
                                                   int tree, uint32_t sweep, uint32_t nr, uint32_t rank, ValOut* __restrict__ vo,
-                                                  int* __restrict__ dxr, int* __restrict__ dxl, int* __restrict__ dyu,
-                                                  int* __restrict__ dyd, uint32_t* __restrict__ insx,
-                                                  uint32_t* __restrict__ insy, unsigned long long* __restrict__ xcnt)
+                                                  int* __restrict__ gtab, uint32_t ntab, int* __restrict__ part,
+                                                  unsigned long long* __restrict__ xcnt)
 {
+   extern __shared__ int lds_tab[];
    const uint32_t N = c.N, W = c.W, H = c.H;
    const bool band_prep = W <= 64 && H <= 64;
+   const uint32_t nx2 = nr * nr;
+   int* const tab = LH ? lds_tab : gtab;
+   uint32_t* const lx = reinterpret_cast<uint32_t*>(lds_tab + ntab);
+   if (LH)
+   {
+      for (uint32_t k = threadIdx.x; k < ntab + nx2; k += blockDim.x) lds_tab[k] = 0;
+      __syncthreads();
+   }
+   int* const dxr = tab;
+   int* const dxl = dxr + (size_t) H * (W + 1);
+   int* const dyu = dxl + (size_t) H * (W + 1);
+   int* const dyd = dyu + (size_t) W * (H + 1);
+   int* const insx = dyd + (size_t) W * (H + 1);
+   int* const insy = insx + 2 * (size_t) N;
    unsigned long long rec = 0, nbc = 0;
    for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
    {
@@ -189,25 +210,25 @@ __global__ __launch_bounds__(256) void k_validate(DevCfg c, uint64_t n, const ui
       {
          atomicAdd(&dxr[sy * (W + 1) + sx], 1);
          atomicAdd(&dxr[sy * (W + 1) + dx], -1);
-         atomicAdd(&insx[s * 2], 1u);
+         atomicAdd(&insx[s * 2], 1);
       }
       else if (dx < sx)
       {
          atomicAdd(&dxl[sy * (W + 1) + dx + 1], 1);
          atomicAdd(&dxl[sy * (W + 1) + sx + 1], -1);
-         atomicAdd(&insx[s * 2 + 1], 1u);
+         atomicAdd(&insx[s * 2 + 1], 1);
       }
       if (dy > sy)
       {
          atomicAdd(&dyu[dx * (H + 1) + sy], 1);
          atomicAdd(&dyu[dx * (H + 1) + dy], -1);
-         atomicAdd(&insy[(sy * W + dx) * 2], 1u);
+         atomicAdd(&insy[(sy * W + dx) * 2], 1);
       }
       else if (dy < sy)
       {
          atomicAdd(&dyd[dx * (H + 1) + dy + 1], 1);
          atomicAdd(&dyd[dx * (H + 1) + sy + 1], -1);
-         atomicAdd(&insy[(sy * W + dx) * 2 + 1], 1u);
+         atomicAdd(&insy[(sy * W + dx) * 2 + 1], 1);
       }
       if (nr <= 1) rec += 2 + ax + ay;
       else
@@ -218,7 +239,11 @@ __global__ __launch_bounds__(256) void k_validate(DevCfg c, uint64_t n, const ui
          const uint32_t rb = band_of(sy, nr, H), cb = band_of(dx, nr, W);
          const bool r_own = rb == rank, c_own = cb == rank;
          rec += (r_own ? 1 + ax : 0) + (!r_own && !band_prep ? 1 : 0) + (r_own || c_own ? 1 : 0) + (c_own ? ay : 0);
-         if (c.contention) atomicAdd(&xcnt[rb * nr + cb], 1ull);
+         if (c.contention)
+         {
+            if (LH) atomicAdd(&lx[rb * nr + cb], 1u);
+            else atomicAdd(&xcnt[rb * nr + cb], 1ull);
+         }
       }
    }
    // wave sums, one atomic per wave
@@ -232,6 +257,26 @@ __global__ __launch_bounds__(256) void k_validate(DevCfg c, uint64_t n, const ui
       if (rec) atomicAdd(&vo->records, rec);
       if (nbc) atomicAdd(&vo->nbc, nbc);
    }
+   if (LH)
+   {
+      __syncthreads();
+      int* const out = part + (size_t) blockIdx.x * ntab;
+      for (uint32_t k = threadIdx.x; k < ntab; k += blockDim.x) out[k] = lds_tab[k];
+      for (uint32_t k = threadIdx.x; k < nx2; k += blockDim.x)
+         if (lx[k]) atomicAdd(&xcnt[k], (unsigned long long) lx[k]);
+   }
+}
+
+// The blocks' private tables summed into the global one (a column per thread).
+__global__ __launch_bounds__(256) void k_validate_sum(uint32_t ntab, uint32_t nblk, const int* __restrict__ part,
+                                                      int* __restrict__ gtab)
+{
+   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+   if (k >= ntab) return;
+   int acc = 0;
+#pragma unroll 8
+   for (uint32_t b = 0; b < nblk; b++) acc += part[(size_t) b * ntab + k];
+   gtab[k] = acc;
 }
 
 // The busiest X / Y port over the batch (prefix sums of the difference arrays)

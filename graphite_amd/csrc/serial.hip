@@ -16,20 +16,31 @@
 //                           one entry per packet (non-visitors get the max key)
 //               radix sort  stable, bits [0, 49 + level bits) (ties: packet id)
 //               k_ma_bounds first / last entry of each port
-//               k_ma_gather cycles and flits of each sorted request
-//               k_ma_walk   one thread per port: the reference's arithmetic, in
-//                           order -> queue delay per request, port counters
+//               k_ma_gather cycles and flits of each sorted request, and what the
+//                           mean needs that depends on no state: the arithmetic
+//                           mean's increment x/w - old/w, the geometric mean's
+//                           factor pow(x, 1/w) / pow(old, 1/w), or the median itself
+//               k_ma_chain  one lane per port: only the mean's FP64 chain, in order
+//                           (one add / multiply per request once the window is full)
+//               k_ma_scan1/2/3  the queue, QueueModelBasic's d = max(Q - ref, 0),
+//                           Q = max(Q, ref) + F, as a segmented max-plus scan over the
+//                           level's sorted requests (per 1024-entry block, a one-wave
+//                           scan of the block aggregates, then the block again with
+//                           its carry): delay per request, each port's last Q
+//               k_ma_ports  per-port delay / flit sums (blocks of a port's segment)
 //               k_ma_apply  each packet's time / contention / zero-load
 //
-// The geometric mean is refused by gnoc_set_basic_moving_average: its pow()
-// chain is not bit-reproducible against glibc.  Arithmetic mean and median are
-// bit-exact against
-// oracle/gnoc_oracle.c (orc_ma_compute, pinned against the
-// reference's own moving_average.h compiled in oracle/_ref).  This TU is compiled
-// with -ffp-contract=off (no FMA contraction), like the M/G/1 arithmetic.
+// The geometric mean's pow is glibc's (glibc_pow.h, bit-exact with the x86-64
+// FMA build the reference links), and ref = (T) mean is the x86-64 conversion
+// (to_u64_x86: a NaN or inf mean -- a window holding a 0 -- converts as it does
+// there).  Arithmetic mean, geometric mean and median are bit-exact against
+// oracle/gnoc_oracle.c (orc_ma_compute, pinned against the reference's own
+// moving_average.h compiled in oracle/_ref).  This TU is compiled with
+// -ffp-contract=off (no FMA contraction), like the M/G/1 arithmetic.
 #pragma once
 
 #include "common.h"
+#include "glibc_pow.h"
 
 namespace gnoc {
 
@@ -114,29 +125,38 @@ __global__ void k_ma_keys(uint64_t n, uint32_t W, uint32_t lvl, uint32_t nlvl, u
    }
 }
 
+// Each port's segment [lo, hi) of the sorted entries, and the number of valid
+// entries (requests of the level) in *mcount.
 __global__ void k_ma_bounds(uint64_t n, uint64_t invalid, const uint64_t* __restrict__ key, uint32_t* __restrict__ lo,
-                            uint32_t* __restrict__ hi)
+                            uint32_t* __restrict__ hi, uint32_t* __restrict__ mcount)
 {
    for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < n; j += (uint64_t) gridDim.x * blockDim.x)
    {
       const uint64_t k = key[j];
       if (k == invalid) continue;
       const uint32_t p = (uint32_t) (k >> MA_T_BITS);
+      const bool last = j + 1 == n || key[j + 1] == invalid;
       if (j == 0 || (uint32_t) (key[j - 1] >> MA_T_BITS) != p) lo[p] = (uint32_t) j;
-      if (j + 1 == n || key[j + 1] == invalid || (uint32_t) (key[j + 1] >> MA_T_BITS) != p) hi[p] = (uint32_t) (j + 1);
+      if (last || (uint32_t) (key[j + 1] >> MA_T_BITS) != p) hi[p] = (uint32_t) (j + 1);
+      if (last) *mcount = (uint32_t) (j + 1);
    }
 }
 
 // Per sorted request j: the queue's input in cycles and the packet's flit count
-// (coalesced; takes every load off the serial walk's dependency chain).
-// For the arithmetic mean with a full window, also the increment
-// (x / w) - (old / w) of moving_average.h:97-98: it depends only on the request
-// and the one w places earlier in the port's segment, so its two FP64 divisions
-// leave the serial walk (which then adds it, in order, exactly as the reference).
-__global__ void k_ma_gather(uint64_t n, uint64_t invalid, uint32_t flit_width, double f, int ma_type, uint32_t ma_max,
+// (coalesced; takes every load off the serial chain), and the part of the
+// moving average that depends only on the request and the one w places earlier
+// in the port's segment (the window's oldest entry once the window is full,
+// moving_average.h:90-95, 121-126):
+//   arithmetic  delta = (x / w) - (old / w)          (moving_average.h:93-94)
+//   geometric   fac = pow(x, 1 / w) / pow(old, 1 / w)  (:125)
+//   median      ref = the window's middle entry        (:149-153), final
+// The chain adds / multiplies delta / fac in order, exactly as the reference.
+template <int MT>
+__global__ void k_ma_gather(uint64_t n, uint64_t invalid, uint32_t flit_width, double f, uint32_t ma_max,
                             const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
                             const uint32_t* __restrict__ bits, const uint32_t* __restrict__ lo,
-                            uint64_t* __restrict__ tcs, uint32_t* __restrict__ Fs, double* __restrict__ delta)
+                            uint64_t* __restrict__ tcs, uint32_t* __restrict__ Fs, double* __restrict__ delta,
+                            uint64_t* __restrict__ ref)
 {
    for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < n; j += (uint64_t) gridDim.x * blockDim.x)
    {
@@ -145,110 +165,305 @@ __global__ void k_ma_gather(uint64_t n, uint64_t invalid, uint32_t flit_width, d
       const uint64_t tc = cyc_of<false>(k & MA_T_MASK, f);   // Time::toCycles, time_types.h:104-109
       tcs[j] = tc;
       Fs[j] = ma_flits(bits[val[j]], flit_width);
-      if (ma_type == MA_ARITHMETIC && j - lo[(uint32_t) (k >> MA_T_BITS)] >= ma_max)
+      const uint32_t seen = (uint32_t) (j - lo[(uint32_t) (k >> MA_T_BITS)]);   // requests before j
+      if (MT == MA_MEDIAN)
+      {
+         // after the add the window holds the last min(seen + 1, w) requests; the
+         // median index is front + size / 2
+         const uint32_t w = seen + 1 < ma_max ? seen + 1 : ma_max;
+         ref[j] = cyc_of<false>(key[j + 1 - w + w / 2] & MA_T_MASK, f);
+      }
+      else if (seen >= ma_max)
       {
          const uint64_t old = cyc_of<false>(key[j - ma_max] & MA_T_MASK, f);
-         delta[j] = ((double) tc / (double) ma_max) - ((double) old / (double) ma_max);
+         if (MT == MA_ARITHMETIC)
+            delta[j] = ((double) tc / (double) ma_max) - ((double) old / (double) ma_max);
+         else
+         {
+            const double e = 1.0 / (double) ma_max;
+            delta[j] = gpow::pow((double) tc, e) / gpow::pow((double) old, e);
+         }
       }
    }
 }
 
-// One queue: QueueModelBasic::computeQueueDelay (queue_model_basic.cc:35-61) with
-// MovingAverage<UInt64>::compute (moving_average.h:90-110 arithmetic, 153-162
-// median), one thread per port over its sorted requests.
-// The window is the port's last `ma_max` inputs, i.e. the previous entries of
-// the same sorted segment, so the ring buffer's reads become plain indexed
-// loads: the arithmetic mean's increment uses entry j - max (k_ma_gather), the median the
-// entry front + size / 2 of the window after the add.  Loads run one block of
-// MA_B requests ahead of the FP64 chain (registers, double-buffered).
+// The mean's serial chain, one lane per port over its sorted requests
+// (MovingArithmeticMean / MovingGeometricMean::compute, moving_average.h:87-135):
+// while the window fills, the reference's full formula; then one FP64 add or
+// multiply per request with the gathered delta / factor.  Writes the mean of
+// every request (the conversion to the reference time and the queue itself are
+// parallel: k_ma_scan).  Loads run one block of MA_B requests ahead.
 constexpr int MA_B = 32;
 
-template <int ma_type>
-__global__ void __launch_bounds__(64) k_ma_walk(uint32_t nloc, const uint32_t* __restrict__ ports,
-                                                uint32_t ma_max, const uint64_t* __restrict__ tcs,
-                                                const uint32_t* __restrict__ Fs, const uint32_t* __restrict__ lo,
-                                                const uint32_t* __restrict__ hi, const double* delta, uint64_t* dout,
-                                                uint64_t* __restrict__ port_sum, uint64_t* __restrict__ port_cnt,
-                                                uint64_t* __restrict__ port_flit, uint64_t* __restrict__ port_last)
+template <int MT>
+__global__ void __launch_bounds__(64) k_ma_chain(uint32_t nloc, uint32_t ma_max, const uint64_t* __restrict__ tcs,
+                                                 const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi,
+                                                 const double* __restrict__ delta, double* __restrict__ mean_out)
 {
    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
    if (p >= nloc) return;
-   const uint32_t port = ports[p];
    const uint32_t j0 = lo[p], j1 = hi[p];
-   double mean = 0.0;   // MovingArithmeticMean's _arithmetic_mean(0.0), moving_average.h:88
-   uint64_t Q = 0, sum = 0, flits = 0;
-   uint64_t cx[MA_B], co[MA_B], nx[MA_B], no[MA_B];
-   uint32_t cf[MA_B], nf[MA_B];
-   // entry j's window partner: the mean's gathered increment, or the median
-   auto other = [&](uint32_t j) -> uint64_t {
-      const uint32_t seen = j - j0;   // requests before j
-      if (ma_type == MA_MEDIAN)
-      {
-         const uint32_t w = seen + 1 < ma_max ? seen + 1 : ma_max;
-         return tcs[j + 1 - w + w / 2];
-      }
-      return seen >= ma_max ? __builtin_bit_cast(uint64_t, delta[j]) : 0ull;   // the gathered increment
-   };
-   auto load = [&](uint32_t base, uint64_t* X, uint64_t* O, uint32_t* F) {
-#pragma unroll
-      for (int i = 0; i < MA_B; i++)
-      {
-         const uint32_t j = base + (uint32_t) i;
-         if (j < j1)
-         {
-            X[i] = tcs[j];
-            F[i] = Fs[j];
-            O[i] = other(j);
-         }
-      }
-   };
-   load(j0, cx, co, cf);
-   for (uint32_t base = j0; base < j1; base += MA_B)
+   // _arithmetic_mean(0.0) / _geometric_mean(1.0), moving_average.h:84, 116
+   double m = MT == MA_ARITHMETIC ? 0.0 : 1.0;
+   const uint32_t jf = j1 - j0 < ma_max ? j1 : j0 + ma_max;   // end of the filling requests
+   for (uint32_t j = j0; j < jf; j++)
    {
-      load(base + MA_B, nx, no, nf);
-#pragma unroll
-      for (int i = 0; i < MA_B; i++)
-      {
-         const uint32_t j = base + (uint32_t) i;
-         if (j >= j1) continue;
-         const uint64_t tc = cx[i];
-         const uint32_t F = cf[i];
-         const uint32_t seen = j - j0;
-         const uint32_t cw = seen < ma_max ? seen : ma_max;   // window size before the add
-         uint64_t ref;
-         if constexpr (ma_type == MA_MEDIAN)
-            ref = co[i];
-         else
-         {
-            static_assert(ma_type == MA_ARITHMETIC, "the geometric mean is refused (gnoc_set_basic_moving_average)");
-            if (cw == ma_max)
-               mean += __builtin_bit_cast(double, co[i]);   // (tc / cw) - (old / cw), k_ma_gather
-            else
-               mean = (mean * (double) cw + (double) tc) / (double) (cw + 1);
-            ref = (uint64_t) mean;
-         }
-         // d = max(Q - ref, 0); Q = max(Q, ref) + F.  QueueModel's
-         // _last_request_time = max(ref + d + F) = max over requests of the new Q,
-         // which never decreases: the final Q (queue_model.cc:48-53)
-         const uint64_t top = Q > ref ? Q : ref;
-         const uint64_t d = top - ref;
-         Q = top + F;
-         flits += F;
-         sum += d;
-         dout[j] = d;
-      }
-#pragma unroll
-      for (int i = 0; i < MA_B; i++)
-      {
-         cx[i] = nx[i];
-         co[i] = no[i];
-         cf[i] = nf[i];
-      }
+      const uint32_t cw = j - j0;   // window size before the add
+      const double x = (double) tcs[j];
+      if (MT == MA_ARITHMETIC)
+         m = (m * (double) cw + x) / (double) (cw + 1);
+      else
+         m = gpow::pow(gpow::pow(m, (double) cw) * x, 1.0 / (double) (cw + 1));
+      mean_out[j] = m;
    }
-   port_sum[port] = sum;
-   port_cnt[port] = j1 - j0;
-   port_flit[port] = flits;
-   port_last[port] = Q;
+   double cur[MA_B], nxt[MA_B];
+   auto load = [&](uint32_t base, double* D) {
+#pragma unroll
+      for (int i = 0; i < MA_B; i++)
+         if (base + (uint32_t) i < j1) D[i] = delta[base + i];
+   };
+   load(jf, cur);
+   for (uint32_t base = jf; base < j1; base += MA_B)
+   {
+      load(base + MA_B, nxt);
+#pragma unroll
+      for (int i = 0; i < MA_B; i++)
+      {
+         if (base + (uint32_t) i >= j1) break;
+         if (MT == MA_ARITHMETIC) m += cur[i];
+         else m *= cur[i];
+         mean_out[base + i] = m;
+      }
+#pragma unroll
+      for (int i = 0; i < MA_B; i++) cur[i] = nxt[i];
+   }
+}
+
+// ---- the queue as a segmented max-plus scan ----------------------------------
+// QueueModelBasic::computeQueueDelay (queue_model_basic.cc:35-61) on ref:
+//   d = max(Q - ref, 0);  Q = max(Q, ref) + F,  Q = 0 at a port's first request.
+// Request j is the map Q -> max(Q + F, ref + F); a port's first request ignores Q
+// (reset).  Maps compose: (A1, B1) then (A2, B2) = (A1 + A2, max(B1 + A2, B2)).
+// _last_request_time (queue_model.cc:48-53) is the port's final Q (it never
+// decreases).  u64 arithmetic as in the reference: ref may be 2^63 (a NaN mean).
+constexpr uint32_t MS_T = 256, MS_PER = 4, MS_CH = MS_T * MS_PER;   // entries per scan block
+
+struct MaAgg
+{
+   uint64_t A, B;
+   uint32_t reset;
+};
+__device__ __forceinline__ MaAgg ma_op(const MaAgg& x, const MaAgg& y)   // x, then y
+{
+   if (y.reset) return y;
+   MaAgg r;
+   r.A = x.A + y.A;
+   const uint64_t b = x.B + y.A;
+   r.B = b > y.B ? b : y.B;
+   r.reset = x.reset;
+   return r;
+}
+template <int MT>
+__device__ __forceinline__ uint64_t ma_ref(const uint64_t* ref, uint64_t j)
+{
+   if (MT == MA_MEDIAN) return ref[j];
+   return gpow::to_u64_x86(__builtin_bit_cast(double, ref[j]));   // (T) _mean, moving_average.h:103, 134
+}
+__device__ __forceinline__ bool ma_first(const uint64_t* key, const uint32_t* lo, uint64_t j)
+{
+   return lo[(uint32_t) (key[j] >> MA_T_BITS)] == (uint32_t) j;
+}
+
+// Block-wide exclusive scan of one aggregate per thread (LDS, 256 threads); the
+// block's total in `tot`.
+__device__ MaAgg ma_block_scan(MaAgg v, MaAgg& tot)
+{
+   __shared__ uint64_t sA[MS_T], sB[MS_T];
+   __shared__ uint32_t sR[MS_T];
+   const uint32_t t = threadIdx.x;
+   MaAgg inc = v;
+   for (uint32_t off = 1; off < MS_T; off <<= 1)
+   {
+      sA[t] = inc.A;
+      sB[t] = inc.B;
+      sR[t] = inc.reset;
+      __syncthreads();
+      if (t >= off)
+      {
+         MaAgg prev;
+         prev.A = sA[t - off];
+         prev.B = sB[t - off];
+         prev.reset = sR[t - off];
+         inc = ma_op(prev, inc);
+      }
+      __syncthreads();
+   }
+   sA[t] = inc.A;
+   sB[t] = inc.B;
+   sR[t] = inc.reset;
+   __syncthreads();
+   tot.A = sA[MS_T - 1];
+   tot.B = sB[MS_T - 1];
+   tot.reset = sR[MS_T - 1];
+   MaAgg ex;
+   ex.A = t ? sA[t - 1] : 0;
+   ex.B = t ? sB[t - 1] : 0;
+   ex.reset = t ? sR[t - 1] : 0;
+   __syncthreads();
+   return ex;
+}
+
+template <int MT>
+__device__ __forceinline__ MaAgg ma_thread_agg(uint64_t m, const uint64_t* key, const uint32_t* lo, const uint64_t* ref,
+                                               const uint32_t* Fs, uint64_t j0)
+{
+   MaAgg g;
+   g.A = 0;
+   g.B = 0;
+   g.reset = 0;
+#pragma unroll
+   for (uint32_t q = 0; q < MS_PER; q++)
+   {
+      const uint64_t j = j0 + q;
+      if (j >= m) break;
+      const uint64_t F = Fs[j], r = ma_ref<MT>(ref, j);
+      MaAgg e;
+      e.A = F;
+      e.B = r + F;
+      e.reset = ma_first(key, lo, j) ? 1u : 0u;
+      g = ma_op(g, e);
+   }
+   return g;
+}
+
+// 1: the aggregate of each block of MS_CH requests
+template <int MT>
+__global__ __launch_bounds__(MS_T) void k_ma_scan1(const uint32_t* __restrict__ mcount, const uint64_t* __restrict__ key, const uint32_t* __restrict__ lo,
+                                                   const uint64_t* __restrict__ ref, const uint32_t* __restrict__ Fs,
+                                                   uint64_t* __restrict__ bA, uint64_t* __restrict__ bB, uint32_t* __restrict__ bR)
+{
+   const uint64_t m = *mcount;
+   if ((uint64_t) blockIdx.x * MS_CH >= m) return;   // the grid covers every packet; the level has m requests
+   const uint64_t j0 = (uint64_t) blockIdx.x * MS_CH + threadIdx.x * MS_PER;
+   MaAgg tot;
+   ma_block_scan(ma_thread_agg<MT>(m, key, lo, ref, Fs, j0), tot);
+   if (threadIdx.x == 0)
+   {
+      bA[blockIdx.x] = tot.A;
+      bB[blockIdx.x] = tot.B;
+      bR[blockIdx.x] = tot.reset;
+   }
+}
+
+// 2: one wave: the queue value entering each block (exclusive scan of the block
+// aggregates applied to Q = 0; block 0 starts a port)
+__global__ __launch_bounds__(64) void k_ma_scan2(const uint32_t* __restrict__ mcount, const uint64_t* __restrict__ bA, const uint64_t* __restrict__ bB,
+                                                 const uint32_t* __restrict__ bR, uint64_t* __restrict__ qin)
+{
+   const uint32_t lane = threadIdx.x;
+   const uint32_t nb = (*mcount + MS_CH - 1) / MS_CH;
+   MaAgg carry;
+   carry.A = 0;
+   carry.B = 0;
+   carry.reset = 1;
+   for (uint32_t b0 = 0; b0 < nb; b0 += 64)
+   {
+      const uint32_t b = b0 + lane;
+      MaAgg v;
+      v.A = b < nb ? bA[b] : 0;
+      v.B = b < nb ? bB[b] : 0;
+      v.reset = b < nb ? bR[b] : 0;
+      MaAgg inc = v;
+      for (int off = 1; off < 64; off <<= 1)
+      {
+         MaAgg prev;
+         prev.A = __shfl_up(inc.A, off);
+         prev.B = __shfl_up(inc.B, off);
+         prev.reset = __shfl_up(inc.reset, off);
+         if ((int) lane >= off) inc = ma_op(prev, inc);
+      }
+      MaAgg ex;
+      ex.A = __shfl_up(inc.A, 1);
+      ex.B = __shfl_up(inc.B, 1);
+      ex.reset = __shfl_up(inc.reset, 1);
+      if (lane == 0)
+      {
+         ex.A = 0;
+         ex.B = 0;
+         ex.reset = 0;
+      }
+      const MaAgg before = ma_op(carry, ex);   // everything before block b (carry starts with a reset)
+      if (b < nb) qin[b] = before.B > before.A ? before.B : before.A;   // max(0 + A, B)
+      MaAgg last;
+      last.A = __shfl(inc.A, 63);
+      last.B = __shfl(inc.B, 63);
+      last.reset = __shfl(inc.reset, 63);
+      carry = ma_op(carry, last);
+   }
+}
+
+// 3: each block again with its carry: delay per request, each port's final Q
+template <int MT>
+__global__ __launch_bounds__(MS_T) void k_ma_scan3(const uint32_t* __restrict__ mcount, const uint64_t* __restrict__ key, const uint32_t* __restrict__ lo,
+                                                   const uint32_t* __restrict__ hi, const uint32_t* __restrict__ ports,
+                                                   const uint64_t* __restrict__ ref, const uint32_t* __restrict__ Fs,
+                                                   const uint64_t* __restrict__ qin, uint64_t* __restrict__ dout,
+                                                   uint64_t* __restrict__ port_last)
+{
+   const uint64_t m = *mcount;
+   if ((uint64_t) blockIdx.x * MS_CH >= m) return;
+   const uint64_t j0 = (uint64_t) blockIdx.x * MS_CH + threadIdx.x * MS_PER;
+   MaAgg tot;
+   const MaAgg ex = ma_block_scan(ma_thread_agg<MT>(m, key, lo, ref, Fs, j0), tot);
+   // Q before this thread's first request
+   uint64_t Q = qin[blockIdx.x];
+   if (ex.reset) Q = ex.B > ex.A ? ex.B : ex.A;
+   else
+   {
+      const uint64_t b = Q + ex.A;
+      Q = b > ex.B ? b : ex.B;
+   }
+#pragma unroll
+   for (uint32_t q = 0; q < MS_PER; q++)
+   {
+      const uint64_t j = j0 + q;
+      if (j >= m) break;
+      const uint32_t pk = (uint32_t) (key[j] >> MA_T_BITS);
+      if (lo[pk] == (uint32_t) j) Q = 0;
+      const uint64_t r = ma_ref<MT>(ref, j);
+      const uint64_t top = Q > r ? Q : r;
+      dout[j] = top - r;
+      Q = top + Fs[j];
+      if (hi[pk] == (uint32_t) j + 1) port_last[ports[pk]] = Q;
+   }
+}
+
+// Per-port delay and flit sums: grid (ports, blocks per port), integer atomics
+// (deterministic); counts are the segment lengths.
+__global__ __launch_bounds__(256) void k_ma_ports(const uint32_t* __restrict__ ports, const uint32_t* __restrict__ lo,
+                                                  const uint32_t* __restrict__ hi, const uint64_t* __restrict__ dout,
+                                                  const uint32_t* __restrict__ Fs, unsigned long long* __restrict__ port_sum,
+                                                  unsigned long long* __restrict__ port_cnt,
+                                                  unsigned long long* __restrict__ port_flit)
+{
+   const uint32_t p = blockIdx.x, j0 = lo[p], j1 = hi[p];
+   unsigned long long s = 0, fl = 0;
+   for (uint32_t j = j0 + blockIdx.y * blockDim.x + threadIdx.x; j < j1; j += gridDim.y * blockDim.x)
+   {
+      s += dout[j];
+      fl += Fs[j];
+   }
+   for (int off = 32; off > 0; off >>= 1)
+   {
+      s += __shfl_down(s, off);
+      fl += __shfl_down(fl, off);
+   }
+   if ((threadIdx.x & 63) == 0)
+   {
+      if (s) atomicAdd(&port_sum[ports[p]], s);
+      if (fl) atomicAdd(&port_flit[ports[p]], fl);
+   }
+   if (blockIdx.y == 0 && threadIdx.x == 0) port_cnt[ports[p]] = j1 - j0;
 }
 
 // Per request: RouterModel / Hop bookkeeping (router_model.cc:70-108,

@@ -62,6 +62,13 @@ def main(only=None):
          random_trace(1500, 4, 4, seed=11, max_cycle=300, burst0=20, self_frac=0.05, unmodeled_frac=0.05))
     case("g_4x4_basic_ma_median_w5", E(num_tiles=16, queue_type=1, moving_avg_type=3, moving_avg_window=5),
          random_trace(1500, 4, 4, seed=12, max_cycle=300, burst0=20))
+    # geometric mean (moving_average.h:119-135, glibc pow): zeros in the window (the
+    # mean becomes 0, then NaN), and a batch starting at cycle 1000 (finite means)
+    case("g_4x4_basic_ma_geom_w6", E(num_tiles=16, queue_type=1, moving_avg_type=2, moving_avg_window=6),
+         random_trace(1500, 4, 4, seed=13, max_cycle=300, burst0=20))
+    late = random_trace(1500, 4, 4, seed=14, max_cycle=3000, burst0=20)
+    late.inject_ps[:] += 1_000_000
+    case("g_4x4_basic_ma_geom_w16_late", E(num_tiles=16, queue_type=1, moving_avg_type=2, moving_avg_window=16), late)
 
 
 if __name__ == "__main__":
