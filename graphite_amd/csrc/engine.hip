@@ -32,7 +32,6 @@
 #include "serial.hip"
 #include "chain.hip"
 
-#include <hipcub/hipcub.hpp>
 
 namespace gnoc {
 // Packets per prep chunk (k_classify / k_scatter blocks): each chunk keeps an
@@ -152,10 +151,11 @@ struct gnoc_engine
    // QueueModelBasic with a moving average (gnoc_set_basic_moving_average, serial.hip)
    int ma_type = 0;
    uint32_t ma_window = 1;
-   DevBuf ma_t, ma_key, ma_val, ma_key2, ma_val2, ma_lo, ma_hi, ma_d, ma_tmp, ma_ref, ma_agg, ma_m;
+   DevBuf ma_t, ma_key, ma_val, ma_key2, ma_val2, ma_lo, ma_hi, ma_d, ma_ref, ma_agg, ma_m, ma_bcnt, ma_hist;
 
    // v4 chain engine (chain.hip): windows of 2^ch_shift ps, ch_nw of them (sized at submit)
    uint32_t ch_shift = 0, ch_nw = 0;
+   uint64_t h_tlast = 0;                    // last injection time of the batch (k_validate)
    uint32_t ch_shift_run = 0, ch_nw_run = 0;   // the attempt in flight
    uint32_t ch_epoch = 0;
    int ch_grid = 0;
@@ -659,6 +659,7 @@ static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t
          default: return fail(e, GNOC_EUNSUPPORTED, "inject time beyond 2^50 ps at packet " + at);
       }
    }
+   e->h_tlast = n ? v.tlast : 0;
    choose_windows(e, v.pmax, v.imax, n ? v.tlast : 0);
    *records = v.records;
    *nbc = v.nbc;
@@ -1398,13 +1399,9 @@ static int run_once(gnoc_engine* e)
 // ---------------------------------------------------------------------------
 // engine path 3: basic queues with a moving average (serial.hip)
 // ---------------------------------------------------------------------------
-static int run_ma(gnoc_engine* e)
+static int run_ma_tb(gnoc_engine* e, uint32_t tb, bool* wider)
 {
-   if (!e->submitted) return fail(e, GNOC_ESTATE, "gnoc_run before gnoc_submit");
-   if (e->nb) return fail(e, GNOC_EUNSUPPORTED, "broadcast packets with moving-average basic queues");
-   // the packet sort takes an int count (self-sends and unmodeled packets count too)
-   if (e->n > (size_t) INT32_MAX) return fail(e, GNOC_EUNSUPPORTED, "more than 2^31-1 packets on the moving-average path");
-   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   *wider = false;
    const DevCfg& c = e->dc;
    const size_t n = e->n;
    const size_t nports = (size_t) c.N * PORTS;
@@ -1412,6 +1409,7 @@ static int run_ma(gnoc_engine* e)
    const uint32_t nlvl = (uint32_t) e->lvl_off.size() - 1;
    uint32_t maxloc = 1;
    for (uint32_t l = 0; l < nlvl; l++) maxloc = std::max(maxloc, e->lvl_off[l + 1] - e->lvl_off[l]);
+   const uint32_t nbk = (uint32_t) std::max<size_t>(1, (n + RS_CH - 1) / RS_CH);   // compaction / radix blocks
    GNOC_HIP(e, e->final_ps.ensure(n * 8 + 8));
    GNOC_HIP(e, e->zl.ensure(n * 8 + 8));
    GNOC_HIP(e, e->cont.ensure(n * 8 + 8));
@@ -1427,20 +1425,21 @@ static int run_ma(gnoc_engine* e)
    const size_t nsb = (n + MS_CH - 1) / MS_CH + 1;   // scan blocks
    GNOC_HIP(e, e->ma_agg.ensure(nsb * 28 + 64));
    GNOC_HIP(e, e->ma_m.ensure(64));
+   GNOC_HIP(e, e->ma_bcnt.ensure(((size_t) nbk + 1) * 4));
+   GNOC_HIP(e, e->ma_hist.ensure(((size_t) RS_BINS * nbk + RS_BINS) * 4));
    GNOC_HIP(e, e->counters.ensure(64));
    for (DevBuf* b : { &e->port_sum, &e->port_cnt, &e->port_mg1, &e->port_flit, &e->port_last })
    {
       GNOC_HIP(e, b->ensure(nports * 8));
       GNOC_HIP(e, hipMemsetAsync(b->p, 0, nports * 8, s));
    }
-   size_t tmp_bytes = 0;
-   GNOC_HIP(e, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, e->ma_key.as<uint64_t>(), e->ma_key2.as<uint64_t>(),
-                                                  e->ma_val.as<uint32_t>(), e->ma_val2.as<uint32_t>(), (int) n, 0, 64, s));
-   GNOC_HIP(e, e->ma_tmp.ensure(tmp_bytes + 16));
    GNOC_HIP(e, hipMemsetAsync(e->counters.p, 0, 64, s));
    GNOC_HIP(e, hipEventRecord(e->ev0, s));
    const uint32_t grid = (uint32_t) std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 8192));
    unsigned* err = e->counters.as<unsigned>() + 8;
+   uint32_t* mcnt = e->ma_m.as<uint32_t>();
+   uint32_t* hist = e->ma_hist.as<uint32_t>();
+   uint32_t* dtot = hist + (size_t) RS_BINS * nbk;
    if (n)
    {
       hipLaunchKernelGGL(k_ma_init, dim3(grid), dim3(256), 0, s, (uint64_t) n, c.W, e->d_inj, e->d_src, e->d_dst,
@@ -1451,40 +1450,53 @@ static int run_ma(gnoc_engine* e)
       {
          const uint32_t k0 = e->lvl_off[l], nloc = e->lvl_off[l + 1] - k0;
          if (!nloc) continue;
-         int lb = 1;
-         while ((1u << lb) <= nloc) lb++;   // nloc < 2^lb: the all-ones port index is free
-         const int end_bit = (int) MA_T_BITS + lb;
-         const uint64_t invalid = end_bit >= 64 ? ~0ull : (1ull << end_bit) - 1;
-         hipLaunchKernelGGL(k_ma_keys, dim3(grid), dim3(256), 0, s, (uint64_t) n, c.W, l, nlvl, k0, invalid, e->d_src,
+         int lb = 0;
+         while ((1u << lb) < nloc) lb++;   // port indices < 2^lb
+         const uint32_t end_bit = tb + (uint32_t) lb;
+         // the level's requests, compacted in packet order, then sorted by (port, t)
+         hipLaunchKernelGGL(k_ma_count, dim3(nbk), dim3(RS_T), 0, s, (uint64_t) n, c.W, l, nlvl, e->d_src, e->d_dst,
+                            e->d_flags, e->ma_bcnt.as<uint32_t>());
+         hipLaunchKernelGGL(k_ma_scan_counts, dim3(1), dim3(1024), 0, s, nbk, e->ma_bcnt.as<uint32_t>(), mcnt);
+         hipLaunchKernelGGL(k_ma_keys, dim3(nbk), dim3(RS_T), 0, s, (uint64_t) n, c.W, l, nlvl, k0, tb, e->d_src,
                             e->d_dst, e->d_flags, e->d_port_k.as<uint32_t>(), (const uint64_t*) e->ma_t.as<uint64_t>(),
-                            e->ma_key.as<uint64_t>(), e->ma_val.as<uint32_t>(), err);
+                            (const uint32_t*) e->ma_bcnt.as<uint32_t>(), e->ma_key.as<uint64_t>(), e->ma_val.as<uint32_t>(),
+                            err);
          GNOC_HIP(e, hipGetLastError());
-         size_t tb = tmp_bytes;
-         GNOC_HIP(e, hipcub::DeviceRadixSort::SortPairs(e->ma_tmp.p, tb, e->ma_key.as<uint64_t>(), e->ma_key2.as<uint64_t>(),
-                                                        e->ma_val.as<uint32_t>(), e->ma_val2.as<uint32_t>(), (int) n, 0,
-                                                        end_bit, s));
+         uint64_t* kA = e->ma_key.as<uint64_t>();
+         uint64_t* kB = e->ma_key2.as<uint64_t>();
+         uint32_t* vA = e->ma_val.as<uint32_t>();
+         uint32_t* vB = e->ma_val2.as<uint32_t>();
+         for (uint32_t sh = 0; sh < end_bit; sh += 8)
+         {
+            hipLaunchKernelGGL(k_rs_hist, dim3(nbk), dim3(RS_T), 0, s, (const uint32_t*) mcnt, sh, nbk, (const uint64_t*) kA,
+                               hist);
+            hipLaunchKernelGGL(k_rs_offsets, dim3(RS_BINS), dim3(RS_T), 0, s, (const uint32_t*) mcnt, nbk, hist, dtot);
+            hipLaunchKernelGGL(k_rs_scatter, dim3(nbk), dim3(RS_T), 0, s, (const uint32_t*) mcnt, sh, nbk,
+                               (const uint64_t*) kA, (const uint32_t*) vA, (const uint32_t*) hist, (const uint32_t*) dtot,
+                               kB, vB);
+            std::swap(kA, kB);
+            std::swap(vA, vB);
+         }
+         GNOC_HIP(e, hipGetLastError());
+         // sorted requests in (kA, vA); the other pair holds cycles and flits
          GNOC_HIP(e, hipMemsetAsync(e->ma_lo.p, 0, (size_t) nloc * 4, s));
          GNOC_HIP(e, hipMemsetAsync(e->ma_hi.p, 0, (size_t) nloc * 4, s));
-         GNOC_HIP(e, hipMemsetAsync(e->ma_m.p, 0, 4, s));
-         const uint32_t* mcnt = e->ma_m.as<uint32_t>();
-         hipLaunchKernelGGL(k_ma_bounds, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid,
-                            (const uint64_t*) e->ma_key2.as<uint64_t>(), e->ma_lo.as<uint32_t>(), e->ma_hi.as<uint32_t>(),
-                            e->ma_m.as<uint32_t>());
+         hipLaunchKernelGGL(k_ma_bounds, dim3(grid), dim3(256), 0, s, (const uint32_t*) mcnt, tb, (const uint64_t*) kA,
+                            e->ma_lo.as<uint32_t>(), e->ma_hi.as<uint32_t>());
          GNOC_HIP(e, hipGetLastError());
-         // the sort's inputs are free now: request cycles into ma_key, flits into ma_val
-         const uint64_t* skey = e->ma_key2.as<uint64_t>();
+         const uint64_t* skey = kA;
+         const uint32_t* sval = vA;
          const uint32_t* lo = e->ma_lo.as<uint32_t>();
          const uint32_t* hi = e->ma_hi.as<uint32_t>();
          const uint32_t* ports = e->d_lvl_ports.as<uint32_t>() + k0;
-         uint64_t* tcs = e->ma_key.as<uint64_t>();
-         uint32_t* Fs = e->ma_val.as<uint32_t>();
+         uint64_t* tcs = kB;
+         uint32_t* Fs = vB;
          uint64_t* ref = e->ma_ref.as<uint64_t>();
 #define GNOC_MA_GATHER(MT)                                                                                          \
-   hipLaunchKernelGGL(k_ma_gather<MT>, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid, c.flit_width, c.f,        \
-                      e->ma_window, skey, (const uint32_t*) e->ma_val2.as<uint32_t>(), e->d_bits, lo, tcs, Fs,      \
-                      e->ma_d.as<double>(), ref)
+   hipLaunchKernelGGL(k_ma_gather<MT>, dim3(grid), dim3(256), 0, s, (const uint32_t*) mcnt, tb, c.flit_width, c.f,   \
+                      e->ma_window, skey, sval, e->d_bits, lo, tcs, Fs, e->ma_d.as<double>(), ref)
 #define GNOC_MA_CHAIN(MT)                                                                                           \
-   hipLaunchKernelGGL(k_ma_chain<MT>, dim3((nloc + 63) / 64), dim3(64), 0, s, nloc, e->ma_window,                  \
+   hipLaunchKernelGGL(k_ma_chain<MT>, dim3(nloc), dim3(64), 0, s, nloc, e->ma_window,                               \
                       (const uint64_t*) tcs, lo, hi, (const double*) e->ma_d.as<double>(), e->ma_ref.as<double>())
          if (e->ma_type == MA_MEDIAN) GNOC_MA_GATHER(MA_MEDIAN);
          else if (e->ma_type == MA_GEOMETRIC) GNOC_MA_GATHER(MA_GEOMETRIC);
@@ -1505,12 +1517,12 @@ static int run_ma(gnoc_engine* e)
 #define GNOC_MA_SCAN(MT)                                                                                            \
    do                                                                                                               \
    {                                                                                                                \
-      hipLaunchKernelGGL(k_ma_scan1<MT>, dim3(sgrid), dim3(MS_T), 0, s, mcnt, skey, lo, (const uint64_t*) ref,      \
-                         (const uint32_t*) Fs, bA, bB, bR);                                                         \
-      hipLaunchKernelGGL(k_ma_scan2, dim3(1), dim3(64), 0, s, mcnt, (const uint64_t*) bA, (const uint64_t*) bB,     \
-                         (const uint32_t*) bR, qin);                                                                \
-      hipLaunchKernelGGL(k_ma_scan3<MT>, dim3(sgrid), dim3(MS_T), 0, s, mcnt, skey, lo, hi, ports,                  \
-                         (const uint64_t*) ref, (const uint32_t*) Fs, (const uint64_t*) qin, dout,                  \
+      hipLaunchKernelGGL(k_ma_scan1<MT>, dim3(sgrid), dim3(MS_T), 0, s, (const uint32_t*) mcnt, tb, skey, lo,       \
+                         (const uint64_t*) ref, (const uint32_t*) Fs, bA, bB, bR);                                  \
+      hipLaunchKernelGGL(k_ma_scan2, dim3(1), dim3(64), 0, s, (const uint32_t*) mcnt, (const uint64_t*) bA,         \
+                         (const uint64_t*) bB, (const uint32_t*) bR, qin);                                          \
+      hipLaunchKernelGGL(k_ma_scan3<MT>, dim3(sgrid), dim3(MS_T), 0, s, (const uint32_t*) mcnt, tb, skey, lo, hi,   \
+                         ports, (const uint64_t*) ref, (const uint32_t*) Fs, (const uint64_t*) qin, dout,           \
                          e->port_last.as<uint64_t>());                                                              \
    } while (0)
          if (e->ma_type == MA_MEDIAN) GNOC_MA_SCAN(MA_MEDIAN);
@@ -1521,19 +1533,31 @@ static int run_ma(gnoc_engine* e)
                             (const uint32_t*) Fs, e->port_sum.as<unsigned long long>(),
                             e->port_cnt.as<unsigned long long>(), e->port_flit.as<unsigned long long>());
          GNOC_HIP(e, hipGetLastError());
-         hipLaunchKernelGGL(k_ma_apply, dim3(grid), dim3(256), 0, s, (uint64_t) n, invalid,
-                            (const uint32_t*) e->d_lvl_ports.as<uint32_t>() + k0, c.f, c.rl_ps,
-                            (const uint64_t*) e->ma_key2.as<uint64_t>(), (const uint32_t*) e->ma_val2.as<uint32_t>(),
-                            (const uint32_t*) e->ma_val.as<uint32_t>(), (const uint64_t*) e->ma_d.as<uint64_t>(),
-                            e->ma_t.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
-                            e->cont.as<uint64_t>());
+         hipLaunchKernelGGL(k_ma_apply, dim3(grid), dim3(256), 0, s, (const uint32_t*) mcnt, tb, ports, c.f, c.rl_ps, skey,
+                            sval, (const uint32_t*) Fs, (const uint64_t*) dout, e->ma_t.as<uint64_t>(),
+                            e->final_ps.as<uint64_t>());
          GNOC_HIP(e, hipGetLastError());
       }
+   }
+   if (n)
+   {
+      hipLaunchKernelGGL(k_ma_final, dim3(grid), dim3(256), 0, s, (uint64_t) n, c.W, c.flit_width, c.f, c.rl_ps, e->d_inj,
+                         e->d_src, e->d_dst, e->d_bits, e->d_flags, (const uint64_t*) e->final_ps.as<uint64_t>(),
+                         e->zl.as<uint64_t>(), e->cont.as<uint64_t>());
+      GNOC_HIP(e, hipGetLastError());
    }
    GNOC_HIP(e, hipEventRecord(e->ev1, s));
    GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 40, hipMemcpyDeviceToHost, s));
    GNOC_HIP(e, hipStreamSynchronize(s));
-   if (*(const unsigned*) (e->h_pinned + 4)) return fail(e, GNOC_EUNSUPPORTED, "packet time beyond 2^49 ps");
+   if (*(const unsigned*) (e->h_pinned + 4))
+   {
+      if (tb < MA_T_BITS)
+      {
+         *wider = true;
+         return GNOC_OK;
+      }
+      return fail(e, GNOC_EUNSUPPORTED, "packet time beyond 2^49 ps");
+   }
    e->h_counters[0] = e->h_pinned[0];
    e->h_counters[1] = e->h_pinned[1];
    e->h_records = e->h_counters[0] + e->h_counters[1];
@@ -1544,6 +1568,24 @@ static int run_ma(gnoc_engine* e)
    e->last_ms = ms;
    e->ran = true;
    return GNOC_OK;
+}
+
+static int run_ma(gnoc_engine* e)
+{
+   if (!e->submitted) return fail(e, GNOC_ESTATE, "gnoc_run before gnoc_submit");
+   if (e->nb) return fail(e, GNOC_EUNSUPPORTED, "broadcast packets with moving-average basic queues");
+   // request indices are 32-bit (self-sends and unmodeled packets count too)
+   if (e->n > (size_t) INT32_MAX) return fail(e, GNOC_EUNSUPPORTED, "more than 2^31-1 packets on the moving-average path");
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   // 32-bit request times while the batch leaves 2^31 ps of headroom for delays;
+   // a request beyond 2^32 ps reruns the batch with 49-bit times
+   bool wider = false;
+   if (e->h_tlast < (1ull << 31))
+   {
+      const int rc = run_ma_tb(e, 32, &wider);
+      if (rc || !wider) return rc;
+   }
+   return run_ma_tb(e, MA_T_BITS, &wider);
 }
 
 int gnoc_set_basic_moving_average(gnoc_engine* e, int32_t type, uint32_t window_size)

@@ -46,8 +46,13 @@ namespace gnoc {
 
 enum : int { MA_NONE = 0, MA_ARITHMETIC = 1, MA_GEOMETRIC = 2, MA_MEDIAN = 3 };   // include/gnoc.h
 
-constexpr uint32_t MA_T_BITS = 49;   // packet times < 2^49 ps (checked per level)
-constexpr uint64_t MA_T_MASK = (1ull << MA_T_BITS) - 1;
+// Sort keys: (port index in level) << tb | t_ps.  tb = 32 while every request
+// time of the batch is below 2^32 ps (5 radix passes on 32x32), else 49; a
+// request at or beyond 2^tb ps sets a flag and the host reruns with tb = 49
+// (the engine refuses times beyond 2^49 ps).
+constexpr uint32_t MA_T_BITS = 49;
+__device__ __forceinline__ uint32_t kport(uint64_t k, uint32_t tb) { return (uint32_t) (k >> tb); }
+__device__ __forceinline__ uint64_t ktime(uint64_t k, uint32_t tb) { return k & ((1ull << tb) - 1); }
 
 __device__ __forceinline__ uint32_t ma_flits(uint32_t bits, uint32_t fw)
 {
@@ -100,45 +105,230 @@ __device__ __forceinline__ uint32_t ma_port_at(uint32_t W, uint32_t s, uint32_t 
    return ~0u;
 }
 
-__global__ void k_ma_keys(uint64_t n, uint32_t W, uint32_t lvl, uint32_t nlvl, uint32_t k0, uint64_t invalid,
-                          const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
-                          const uint32_t* __restrict__ flags, const uint32_t* __restrict__ port_k,
-                          const uint64_t* __restrict__ ptime, uint64_t* __restrict__ key, uint32_t* __restrict__ val,
-                          unsigned* __restrict__ err)
+// ---- the level's requests in (port, time, packet id) order -----------------
+// Compaction (packet order), then a stable LSD radix sort on 8-bit digits.
+// Blocks of RS_CH entries; the ranking inside a block uses wave ballots (a
+// wave's 64 entries matched on their digit by 8 ballots), so equal keys keep
+// packet order: ties of (port, t) go by packet id as in the reference's event
+// queue.
+constexpr uint32_t RS_T = 256, RS_PER = 8, RS_CH = RS_T * RS_PER, RS_BINS = 256;
+
+__device__ __forceinline__ uint64_t lanes_below() { return (1ull << (threadIdx.x & 63)) - 1; }
+
+// The requests of level lvl: entry i of the compacted list is a (key, packet id)
+// pair.  Pass 1 counts per block; the block offsets are an exclusive scan.
+__device__ __forceinline__ bool ma_visit(uint32_t W, uint32_t lvl, uint32_t nlvl, const uint32_t* src, const uint32_t* dst,
+                                         const uint32_t* flags, uint64_t i, uint32_t& p)
 {
-   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+   const uint32_t s = src[i], d = dst[i];
+   if (s == d || (flags && (flags[i] & 1u))) return false;
+   p = ma_port_at(W, s, d, lvl, nlvl);
+   return p != ~0u;
+}
+
+__global__ __launch_bounds__(RS_T) void k_ma_count(uint64_t n, uint32_t W, uint32_t lvl, uint32_t nlvl,
+                                                   const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                                                   const uint32_t* __restrict__ flags, uint32_t* __restrict__ bcnt)
+{
+   __shared__ uint32_t wc[RS_T / 64];
+   uint32_t c = 0;
+   for (uint32_t q = 0; q < RS_PER; q++)
    {
-      uint64_t kv = invalid;
-      const uint32_t s = src[i], d = dst[i];
-      if (s != d && !(flags && (flags[i] & 1u)))
-      {
-         const uint32_t p = ma_port_at(W, s, d, lvl, nlvl);
-         if (p != ~0u)
-         {
-            const uint64_t t = ptime[i];
-            if (t > MA_T_MASK) atomicOr(err, 1u);
-            kv = ((uint64_t) (port_k[p] - k0) << MA_T_BITS) | (t & MA_T_MASK);
-         }
-      }
-      key[i] = kv;
-      val[i] = (uint32_t) i;
+      const uint64_t i = (uint64_t) blockIdx.x * RS_CH + q * RS_T + threadIdx.x;
+      uint32_t p;
+      if (i < n && ma_visit(W, lvl, nlvl, src, dst, flags, i, p)) c++;
+   }
+   for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
+   if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
+   __syncthreads();
+   if (threadIdx.x == 0)
+   {
+      uint32_t t = 0;
+      for (uint32_t w = 0; w < RS_T / 64; w++) t += wc[w];
+      bcnt[blockIdx.x] = t;
    }
 }
 
-// Each port's segment [lo, hi) of the sorted entries, and the number of valid
-// entries (requests of the level) in *mcount.
-__global__ void k_ma_bounds(uint64_t n, uint64_t invalid, const uint64_t* __restrict__ key, uint32_t* __restrict__ lo,
-                            uint32_t* __restrict__ hi, uint32_t* __restrict__ mcount)
+// Exclusive scan of nb counts in place (one block of 1024); the total in *total.
+__global__ __launch_bounds__(1024) void k_ma_scan_counts(uint32_t nb, uint32_t* __restrict__ cnt, uint32_t* __restrict__ total)
 {
-   for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < n; j += (uint64_t) gridDim.x * blockDim.x)
+   __shared__ uint32_t part[1024];
+   const uint32_t t = threadIdx.x, per = (nb + 1023) / 1024, b0 = t * per, b1 = min(nb, b0 + per);
+   uint32_t sum = 0;
+   for (uint32_t b = b0; b < b1; b++) sum += cnt[b];
+   part[t] = sum;
+   __syncthreads();
+   for (uint32_t off = 1; off < 1024; off <<= 1)
    {
-      const uint64_t k = key[j];
-      if (k == invalid) continue;
-      const uint32_t p = (uint32_t) (k >> MA_T_BITS);
-      const bool last = j + 1 == n || key[j + 1] == invalid;
-      if (j == 0 || (uint32_t) (key[j - 1] >> MA_T_BITS) != p) lo[p] = (uint32_t) j;
-      if (last || (uint32_t) (key[j + 1] >> MA_T_BITS) != p) hi[p] = (uint32_t) (j + 1);
-      if (last) *mcount = (uint32_t) (j + 1);
+      const uint32_t v = t >= off ? part[t - off] : 0u;
+      __syncthreads();
+      part[t] += v;
+      __syncthreads();
+   }
+   uint32_t run = part[t] - sum;
+   for (uint32_t b = b0; b < b1; b++)
+   {
+      const uint32_t c = cnt[b];
+      cnt[b] = run;
+      run += c;
+   }
+   if (t == 1023) *total = part[1023];
+}
+
+// Pass 2: the compacted (key, packet id) list, in packet order.
+__global__ __launch_bounds__(RS_T) void k_ma_keys(uint64_t n, uint32_t W, uint32_t lvl, uint32_t nlvl, uint32_t k0, uint32_t tb,
+                                                  const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
+                                                  const uint32_t* __restrict__ flags, const uint32_t* __restrict__ port_k,
+                                                  const uint64_t* __restrict__ ptime, const uint32_t* __restrict__ boff,
+                                                  uint64_t* __restrict__ key, uint32_t* __restrict__ val,
+                                                  unsigned* __restrict__ err)
+{
+   __shared__ uint32_t wc[RS_T / 64];
+   const uint32_t w = threadIdx.x >> 6;
+   uint32_t run = boff[blockIdx.x];
+   for (uint32_t q = 0; q < RS_PER; q++)
+   {
+      const uint64_t i = (uint64_t) blockIdx.x * RS_CH + q * RS_T + threadIdx.x;
+      uint32_t p = 0;
+      const bool v = i < n && ma_visit(W, lvl, nlvl, src, dst, flags, i, p);
+      const uint64_t bal = __ballot(v);
+      if ((threadIdx.x & 63) == 0) wc[w] = (uint32_t) __popcll(bal);
+      __syncthreads();
+      uint32_t before = run;
+      for (uint32_t u = 0; u < w; u++) before += wc[u];
+      if (v)
+      {
+         const uint64_t t = ptime[i];
+         if (t >> tb) atomicOr(err, 1u);
+         const uint32_t j = before + (uint32_t) __popcll(bal & lanes_below());
+         key[j] = ((uint64_t) (port_k[p] - k0) << tb) | t;
+         val[j] = (uint32_t) i;
+      }
+      for (uint32_t u = 0; u < RS_T / 64; u++) run += wc[u];
+      __syncthreads();
+   }
+}
+
+// Radix pass, 1: per-block digit histograms, digit-major hist[d * nbs + b]
+// (nbs = the host's bound on the block count).
+__global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ mcount, uint32_t shift, uint32_t nbs,
+                                                  const uint64_t* __restrict__ key, uint32_t* __restrict__ hist)
+{
+   __shared__ uint32_t h[RS_BINS];
+   const uint32_t m = *mcount;
+   if ((uint64_t) blockIdx.x * RS_CH >= m) return;
+   h[threadIdx.x] = 0;
+   __syncthreads();
+   for (uint32_t q = 0; q < RS_PER; q++)
+   {
+      const uint32_t i = blockIdx.x * RS_CH + q * RS_T + threadIdx.x;
+      if (i < m) atomicAdd(&h[(uint32_t) (key[i] >> shift) & 0xFFu], 1u);
+   }
+   __syncthreads();
+   hist[(size_t) threadIdx.x * nbs + blockIdx.x] = h[threadIdx.x];
+}
+
+// Block-wide exclusive sum of one value per thread (RS_T threads); total in tot.
+__device__ __forceinline__ uint32_t rs_block_exclusive(uint32_t v, uint32_t& tot)
+{
+   __shared__ uint32_t sc[RS_T];
+   const uint32_t t = threadIdx.x;
+   sc[t] = v;
+   __syncthreads();
+   for (uint32_t off = 1; off < RS_T; off <<= 1)
+   {
+      const uint32_t u = t >= off ? sc[t - off] : 0u;
+      __syncthreads();
+      sc[t] += u;
+      __syncthreads();
+   }
+   const uint32_t inc = sc[t];
+   tot = sc[RS_T - 1];
+   __syncthreads();
+   return inc - v;
+}
+
+// Radix pass, 2: one block per digit: the exclusive scan of its row over the
+// blocks (in place) and the digit's total.
+__global__ __launch_bounds__(RS_T) void k_rs_offsets(const uint32_t* __restrict__ mcount, uint32_t nbs,
+                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ dtot)
+{
+   const uint32_t nb = (*mcount + RS_CH - 1) / RS_CH;
+   uint32_t* row = hist + (size_t) blockIdx.x * nbs;
+   uint32_t carry = 0;
+   for (uint32_t c = 0; c < nb; c += RS_T)
+   {
+      const uint32_t b = c + threadIdx.x;
+      const uint32_t v = b < nb ? row[b] : 0u;
+      uint32_t tot;
+      const uint32_t ex = rs_block_exclusive(v, tot);
+      if (b < nb) row[b] = carry + ex;
+      carry += tot;
+   }
+   if (threadIdx.x == 0) dtot[blockIdx.x] = carry;
+}
+
+// Radix pass, 3: stable scatter.  Sub-round q takes entries [q 256, (q + 1) 256) of
+// the block in thread order; a wave matches its 64 digits with 8 ballots.
+__global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict__ mcount, uint32_t shift, uint32_t nbs,
+                                                     const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                     const uint32_t* __restrict__ offs, const uint32_t* __restrict__ dtot,
+                                                     uint64_t* __restrict__ kout, uint32_t* __restrict__ vout)
+{
+   __shared__ uint32_t run[RS_BINS];
+   __shared__ uint32_t wcnt[RS_T / 64][RS_BINS];
+   const uint32_t m = *mcount;
+   if ((uint64_t) blockIdx.x * RS_CH >= m) return;
+   const uint32_t t = threadIdx.x, w = t >> 6;
+   uint32_t tot;
+   run[t] = rs_block_exclusive(dtot[t], tot) + offs[(size_t) t * nbs + blockIdx.x];   // digit base + this block's offset
+   for (uint32_t u = 0; u < RS_T / 64; u++) wcnt[u][t] = 0;
+   __syncthreads();
+   for (uint32_t q = 0; q < RS_PER; q++)
+   {
+      const uint32_t i = blockIdx.x * RS_CH + q * RS_T + t;
+      const bool v = i < m;
+      const uint64_t k = v ? kin[i] : 0ull;
+      const uint32_t id = v ? vin[i] : 0u;
+      const uint32_t dg = (uint32_t) (k >> shift) & 0xFFu;
+      uint64_t peers = __ballot(v);
+#pragma unroll
+      for (int b = 0; b < 8; b++)
+      {
+         const uint64_t bb = __ballot((dg >> b) & 1u);
+         peers &= ((dg >> b) & 1u) ? bb : ~bb;
+      }
+      const uint32_t rank = (uint32_t) __popcll(peers & lanes_below());
+      const bool leader = v && rank == 0;
+      if (leader) wcnt[w][dg] = (uint32_t) __popcll(peers);
+      __syncthreads();
+      if (v)
+      {
+         uint32_t pos = run[dg] + rank;
+         for (uint32_t u = 0; u < w; u++) pos += wcnt[u][dg];
+         kout[pos] = k;
+         vout[pos] = id;
+      }
+      __syncthreads();
+      if (leader)
+      {
+         atomicAdd(&run[dg], wcnt[w][dg]);
+         wcnt[w][dg] = 0;
+      }
+      __syncthreads();
+   }
+}
+
+// Each port's segment [lo, hi) of the sorted requests.
+__global__ void k_ma_bounds(const uint32_t* __restrict__ mcount, uint32_t tb, const uint64_t* __restrict__ key,
+                            uint32_t* __restrict__ lo, uint32_t* __restrict__ hi)
+{
+   const uint64_t m = *mcount;
+   for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < m; j += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const uint32_t p = kport(key[j], tb);
+      if (j == 0 || kport(key[j - 1], tb) != p) lo[p] = (uint32_t) j;
+      if (j + 1 == m || kport(key[j + 1], tb) != p) hi[p] = (uint32_t) (j + 1);
    }
 }
 
@@ -152,30 +342,30 @@ __global__ void k_ma_bounds(uint64_t n, uint64_t invalid, const uint64_t* __rest
 //   median      ref = the window's middle entry        (:149-153), final
 // The chain adds / multiplies delta / fac in order, exactly as the reference.
 template <int MT>
-__global__ void k_ma_gather(uint64_t n, uint64_t invalid, uint32_t flit_width, double f, uint32_t ma_max,
+__global__ void k_ma_gather(const uint32_t* __restrict__ mcount, uint32_t tb, uint32_t flit_width, double f, uint32_t ma_max,
                             const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
                             const uint32_t* __restrict__ bits, const uint32_t* __restrict__ lo,
                             uint64_t* __restrict__ tcs, uint32_t* __restrict__ Fs, double* __restrict__ delta,
                             uint64_t* __restrict__ ref)
 {
+   const uint64_t n = *mcount;
    for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < n; j += (uint64_t) gridDim.x * blockDim.x)
    {
       const uint64_t k = key[j];
-      if (k == invalid) continue;
-      const uint64_t tc = cyc_of<false>(k & MA_T_MASK, f);   // Time::toCycles, time_types.h:104-109
+      const uint64_t tc = cyc_of<false>(ktime(k, tb), f);   // Time::toCycles, time_types.h:104-109
       tcs[j] = tc;
       Fs[j] = ma_flits(bits[val[j]], flit_width);
-      const uint32_t seen = (uint32_t) (j - lo[(uint32_t) (k >> MA_T_BITS)]);   // requests before j
+      const uint32_t seen = (uint32_t) (j - lo[kport(k, tb)]);   // requests before j
       if (MT == MA_MEDIAN)
       {
          // after the add the window holds the last min(seen + 1, w) requests; the
          // median index is front + size / 2
          const uint32_t w = seen + 1 < ma_max ? seen + 1 : ma_max;
-         ref[j] = cyc_of<false>(key[j + 1 - w + w / 2] & MA_T_MASK, f);
+         ref[j] = cyc_of<false>(ktime(key[j + 1 - w + w / 2], tb), f);
       }
       else if (seen >= ma_max)
       {
-         const uint64_t old = cyc_of<false>(key[j - ma_max] & MA_T_MASK, f);
+         const uint64_t old = cyc_of<false>(ktime(key[j - ma_max], tb), f);
          if (MT == MA_ARITHMETIC)
             delta[j] = ((double) tc / (double) ma_max) - ((double) old / (double) ma_max);
          else
@@ -187,55 +377,78 @@ __global__ void k_ma_gather(uint64_t n, uint64_t invalid, uint32_t flit_width, d
    }
 }
 
-// The mean's serial chain, one lane per port over its sorted requests
+// The mean's serial chain over one port's sorted requests
 // (MovingArithmeticMean / MovingGeometricMean::compute, moving_average.h:87-135):
 // while the window fills, the reference's full formula; then one FP64 add or
 // multiply per request with the gathered delta / factor.  Writes the mean of
 // every request (the conversion to the reference time and the queue itself are
-// parallel: k_ma_scan).  Loads run one block of MA_B requests ahead.
-constexpr int MA_B = 32;
-
+// parallel: k_ma_scan).  One wave per port: the wave moves blocks of 64 deltas
+// and means with coalesced loads / stores (the next block in flight) through
+// LDS, and lane 0 runs only the FP64 chain out of LDS.  (A lane per port with a
+// global store per request waited on its own stores -- gfx9's vmcnt counts
+// stores too -- at ~60 ns per request.)
 template <int MT>
 __global__ void __launch_bounds__(64) k_ma_chain(uint32_t nloc, uint32_t ma_max, const uint64_t* __restrict__ tcs,
                                                  const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi,
                                                  const double* __restrict__ delta, double* __restrict__ mean_out)
 {
-   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+   __shared__ double din[64], dres[64];
+   const uint32_t p = blockIdx.x, lane = threadIdx.x;
    if (p >= nloc) return;
    const uint32_t j0 = lo[p], j1 = hi[p];
    // _arithmetic_mean(0.0) / _geometric_mean(1.0), moving_average.h:84, 116
    double m = MT == MA_ARITHMETIC ? 0.0 : 1.0;
    const uint32_t jf = j1 - j0 < ma_max ? j1 : j0 + ma_max;   // end of the filling requests
-   for (uint32_t j = j0; j < jf; j++)
-   {
-      const uint32_t cw = j - j0;   // window size before the add
-      const double x = (double) tcs[j];
-      if (MT == MA_ARITHMETIC)
-         m = (m * (double) cw + x) / (double) (cw + 1);
-      else
-         m = gpow::pow(gpow::pow(m, (double) cw) * x, 1.0 / (double) (cw + 1));
-      mean_out[j] = m;
-   }
-   double cur[MA_B], nxt[MA_B];
-   auto load = [&](uint32_t base, double* D) {
-#pragma unroll
-      for (int i = 0; i < MA_B; i++)
-         if (base + (uint32_t) i < j1) D[i] = delta[base + i];
-   };
-   load(jf, cur);
-   for (uint32_t base = jf; base < j1; base += MA_B)
-   {
-      load(base + MA_B, nxt);
-#pragma unroll
-      for (int i = 0; i < MA_B; i++)
+   if (lane == 0)
+      for (uint32_t j = j0; j < jf; j++)
       {
-         if (base + (uint32_t) i >= j1) break;
-         if (MT == MA_ARITHMETIC) m += cur[i];
-         else m *= cur[i];
-         mean_out[base + i] = m;
+         const uint32_t cw = j - j0;   // window size before the add
+         const double x = (double) tcs[j];
+         if (MT == MA_ARITHMETIC)
+            m = (m * (double) cw + x) / (double) (cw + 1);
+         else
+            m = gpow::pow(gpow::pow(m, (double) cw) * x, 1.0 / (double) (cw + 1));
+         mean_out[j] = m;
       }
+   double nxt = jf + lane < j1 ? delta[jf + lane] : 0.0;
+   for (uint32_t base = jf; base < j1; base += 64)
+   {
+      const double cur = nxt;
+      if (base + 64 + lane < j1) nxt = delta[base + 64 + lane];   // the next block in flight
+      din[lane] = cur;
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0)
+      {
+         const uint32_t cnt = j1 - base < 64 ? j1 - base : 64;
+         if (cnt == 64)
+         {
+            // full block: the LDS reads of a group issue ahead of its dependent chain
 #pragma unroll
-      for (int i = 0; i < MA_B; i++) cur[i] = nxt[i];
+            for (int g = 0; g < 64; g += 16)
+            {
+               double v[16];
+#pragma unroll
+               for (int k = 0; k < 16; k++) v[k] = din[g + k];
+#pragma unroll
+               for (int k = 0; k < 16; k++)
+               {
+                  if (MT == MA_ARITHMETIC) m += v[k];
+                  else m *= v[k];
+                  dres[g + k] = m;
+               }
+            }
+         }
+         else
+            for (uint32_t i = 0; i < cnt; i++)
+            {
+               if (MT == MA_ARITHMETIC) m += din[i];
+               else m *= din[i];
+               dres[i] = m;
+            }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (base + lane < j1) mean_out[base + lane] = dres[lane];
+      __builtin_amdgcn_wave_barrier();
    }
 }
 
@@ -269,9 +482,9 @@ __device__ __forceinline__ uint64_t ma_ref(const uint64_t* ref, uint64_t j)
    if (MT == MA_MEDIAN) return ref[j];
    return gpow::to_u64_x86(__builtin_bit_cast(double, ref[j]));   // (T) _mean, moving_average.h:103, 134
 }
-__device__ __forceinline__ bool ma_first(const uint64_t* key, const uint32_t* lo, uint64_t j)
+__device__ __forceinline__ bool ma_first(const uint64_t* key, const uint32_t* lo, uint64_t j, uint32_t tb)
 {
-   return lo[(uint32_t) (key[j] >> MA_T_BITS)] == (uint32_t) j;
+   return lo[kport(key[j], tb)] == (uint32_t) j;
 }
 
 // Block-wide exclusive scan of one aggregate per thread (LDS, 256 threads); the
@@ -314,8 +527,8 @@ __device__ MaAgg ma_block_scan(MaAgg v, MaAgg& tot)
 }
 
 template <int MT>
-__device__ __forceinline__ MaAgg ma_thread_agg(uint64_t m, const uint64_t* key, const uint32_t* lo, const uint64_t* ref,
-                                               const uint32_t* Fs, uint64_t j0)
+__device__ __forceinline__ MaAgg ma_thread_agg(uint64_t m, uint32_t tb, const uint64_t* key, const uint32_t* lo,
+                                               const uint64_t* ref, const uint32_t* Fs, uint64_t j0)
 {
    MaAgg g;
    g.A = 0;
@@ -330,7 +543,7 @@ __device__ __forceinline__ MaAgg ma_thread_agg(uint64_t m, const uint64_t* key, 
       MaAgg e;
       e.A = F;
       e.B = r + F;
-      e.reset = ma_first(key, lo, j) ? 1u : 0u;
+      e.reset = ma_first(key, lo, j, tb) ? 1u : 0u;
       g = ma_op(g, e);
    }
    return g;
@@ -338,7 +551,7 @@ __device__ __forceinline__ MaAgg ma_thread_agg(uint64_t m, const uint64_t* key, 
 
 // 1: the aggregate of each block of MS_CH requests
 template <int MT>
-__global__ __launch_bounds__(MS_T) void k_ma_scan1(const uint32_t* __restrict__ mcount, const uint64_t* __restrict__ key, const uint32_t* __restrict__ lo,
+__global__ __launch_bounds__(MS_T) void k_ma_scan1(const uint32_t* __restrict__ mcount, uint32_t tb, const uint64_t* __restrict__ key, const uint32_t* __restrict__ lo,
                                                    const uint64_t* __restrict__ ref, const uint32_t* __restrict__ Fs,
                                                    uint64_t* __restrict__ bA, uint64_t* __restrict__ bB, uint32_t* __restrict__ bR)
 {
@@ -346,7 +559,7 @@ __global__ __launch_bounds__(MS_T) void k_ma_scan1(const uint32_t* __restrict__ 
    if ((uint64_t) blockIdx.x * MS_CH >= m) return;   // the grid covers every packet; the level has m requests
    const uint64_t j0 = (uint64_t) blockIdx.x * MS_CH + threadIdx.x * MS_PER;
    MaAgg tot;
-   ma_block_scan(ma_thread_agg<MT>(m, key, lo, ref, Fs, j0), tot);
+   ma_block_scan(ma_thread_agg<MT>(m, tb, key, lo, ref, Fs, j0), tot);
    if (threadIdx.x == 0)
    {
       bA[blockIdx.x] = tot.A;
@@ -404,7 +617,7 @@ __global__ __launch_bounds__(64) void k_ma_scan2(const uint32_t* __restrict__ mc
 
 // 3: each block again with its carry: delay per request, each port's final Q
 template <int MT>
-__global__ __launch_bounds__(MS_T) void k_ma_scan3(const uint32_t* __restrict__ mcount, const uint64_t* __restrict__ key, const uint32_t* __restrict__ lo,
+__global__ __launch_bounds__(MS_T) void k_ma_scan3(const uint32_t* __restrict__ mcount, uint32_t tb, const uint64_t* __restrict__ key, const uint32_t* __restrict__ lo,
                                                    const uint32_t* __restrict__ hi, const uint32_t* __restrict__ ports,
                                                    const uint64_t* __restrict__ ref, const uint32_t* __restrict__ Fs,
                                                    const uint64_t* __restrict__ qin, uint64_t* __restrict__ dout,
@@ -414,7 +627,7 @@ __global__ __launch_bounds__(MS_T) void k_ma_scan3(const uint32_t* __restrict__ 
    if ((uint64_t) blockIdx.x * MS_CH >= m) return;
    const uint64_t j0 = (uint64_t) blockIdx.x * MS_CH + threadIdx.x * MS_PER;
    MaAgg tot;
-   const MaAgg ex = ma_block_scan(ma_thread_agg<MT>(m, key, lo, ref, Fs, j0), tot);
+   const MaAgg ex = ma_block_scan(ma_thread_agg<MT>(m, tb, key, lo, ref, Fs, j0), tot);
    // Q before this thread's first request
    uint64_t Q = qin[blockIdx.x];
    if (ex.reset) Q = ex.B > ex.A ? ex.B : ex.A;
@@ -428,7 +641,7 @@ __global__ __launch_bounds__(MS_T) void k_ma_scan3(const uint32_t* __restrict__ 
    {
       const uint64_t j = j0 + q;
       if (j >= m) break;
-      const uint32_t pk = (uint32_t) (key[j] >> MA_T_BITS);
+      const uint32_t pk = kport(key[j], tb);
       if (lo[pk] == (uint32_t) j) Q = 0;
       const uint64_t r = ma_ref<MT>(ref, j);
       const uint64_t top = Q > r ? Q : r;
@@ -467,34 +680,52 @@ __global__ __launch_bounds__(256) void k_ma_ports(const uint32_t* __restrict__ p
 }
 
 // Per request: RouterModel / Hop bookkeeping (router_model.cc:70-108,
-// network_model.cc:556-563) and, at SELF, the receive serialization
-// (network_model.cc:142-150).  Each packet has at most one request per level.
-__global__ void k_ma_apply(uint64_t n, uint64_t invalid, const uint32_t* __restrict__ ports, double f, uint64_t rl_ps,
-                           const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
-                           const uint32_t* __restrict__ Fs, const uint64_t* __restrict__ dout,
-                           uint64_t* __restrict__ ptime, uint64_t* __restrict__ fin, uint64_t* __restrict__ zl,
-                           uint64_t* __restrict__ cont)
+// network_model.cc:556-563): the packet leaves the router at t + delay + hop
+// delay (the injection router's is 0), plus, at SELF, the receive serialization
+// (network_model.cc:142-150).  Only the packet's time is carried between levels;
+// zero-load and contention follow in closed form (k_ma_final).
+__global__ void k_ma_apply(const uint32_t* __restrict__ mcount, uint32_t tb, const uint32_t* __restrict__ ports, double f,
+                           uint64_t rl_ps, const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                           const uint32_t* __restrict__ Fs, const uint64_t* __restrict__ dout, uint64_t* __restrict__ ptime,
+                           uint64_t* __restrict__ fin)
 {
+   const uint64_t n = *mcount;   // the level's requests
    for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < n; j += (uint64_t) gridDim.x * blockDim.x)
    {
       const uint64_t k = key[j];
-      if (k == invalid) continue;
-      const uint32_t dir = ports[(uint32_t) (k >> MA_T_BITS)] % PORTS;
+      const uint32_t dir = ports[kport(k, tb)] % PORTS;
       const uint32_t id = val[j];
       const uint64_t hop_ps = dir == P_INJ ? ps_of<false>(0, f) : rl_ps;   // injection router: delay 0
-      const uint64_t cps = ps_of<false>(dout[j], f);
-      uint64_t tn = (k & MA_T_MASK) + cps + hop_ps;
-      uint64_t z = zl[id] + hop_ps;
-      cont[id] += cps;
+      uint64_t tn = ktime(k, tb) + ps_of<false>(dout[j], f) + hop_ps;
       if (dir == P_SELF)
       {
-         const uint64_t fps = ps_of<false>(Fs[j], f);
-         tn += fps;
-         z += fps;
+         tn += ps_of<false>(Fs[j], f);
          fin[id] = tn;
       }
-      zl[id] = z;
-      ptime[id] = tn;
+      else
+         ptime[id] = tn;
+   }
+}
+
+// After the last level: zero-load = the injection router's 0 + (H + 1) router and
+// link delays + the serialization (the per-hop sums k_ma_apply's predecessor kept
+// per packet), contention = final - inject - zero-load (= the sum of the queue
+// delays in ps, exactly).
+__global__ void k_ma_final(uint64_t n, uint32_t W, uint32_t flit_width, double f, uint64_t rl_ps,
+                           const uint64_t* __restrict__ inj, const uint32_t* __restrict__ src,
+                           const uint32_t* __restrict__ dst, const uint32_t* __restrict__ bits,
+                           const uint32_t* __restrict__ flags, const uint64_t* __restrict__ fin, uint64_t* __restrict__ zl,
+                           uint64_t* __restrict__ cont)
+{
+   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const uint32_t s = src[i], d = dst[i];
+      if (s == d || (flags && (flags[i] & 1u))) continue;   // k_ma_init's zeros stand
+      const uint32_t sx = s % W, sy = s / W, dx = d % W, dy = d / W;
+      const uint64_t hops = (sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1;
+      const uint64_t z = ps_of<false>(0, f) + hops * rl_ps + ps_of<false>(ma_flits(bits[i], flit_width), f);
+      zl[i] = z;
+      cont[i] = fin[i] - inj[i] - z;
    }
 }
 

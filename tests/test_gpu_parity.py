@@ -295,7 +295,8 @@ AM, GM, MED = gnoc.MOVING_AVG_ARITHMETIC_MEAN, gnoc.MOVING_AVG_GEOMETRIC_MEAN, g
 
 
 @pytest.mark.parametrize("ma,w,t0", [(AM, 64, 0), (AM, 1, 0), (AM, 5, 0), (MED, 64, 0), (MED, 4, 0), (MED, 1, 0),
-                                     (GM, 64, 0), (GM, 1, 0), (GM, 5, 0), (GM, 64, 1), (GM, 7, 1), (GM, 200, 1)])
+                                     (GM, 64, 0), (GM, 1, 0), (GM, 5, 0), (GM, 64, 1), (GM, 7, 1), (GM, 200, 1),
+                                     (AM, 64, 2), (MED, 4, 2), (GM, 16, 2)])
 def test_basic_moving_average(ma, w, t0):
     """QueueModelBasic with moving_avg_enabled (queue_model_basic.cc:7-61,
     moving_average.h; carbon_sim.cfg:376-379 default = arithmetic_mean over 64):
@@ -304,12 +305,13 @@ def test_basic_moving_average(ma, w, t0):
     The geometric mean runs glibc's pow (glibc_pow.h).  t0 = 0: packets at cycle
     0 put zeros into the windows (the geometric mean becomes 0, then NaN once a
     zero leaves the window: ref = (UInt64) NaN as on x86-64); t0 = 1: every
-    request at cycle >= 1000, so the products stay finite."""
+    request at cycle >= 1000, so the products stay finite; t0 = 2: times beyond
+    2^33 ps (the 49-bit sort keys instead of 32-bit ones)."""
     cfg = gnoc.EngineConfig(num_tiles=64, queue_type=gnoc.QUEUE_BASIC, moving_avg_type=ma, moving_avg_window=w)
     tr = random_trace(20000, 8, 8, seed=w + 7 * ma, max_cycle=2000, burst0=300, self_frac=0.03, unmodeled_frac=0.03,
                       bits_choices=[72, 576, 1088])
     if t0:
-        tr.inject_ps[:] += 1_000_000
+        tr.inject_ps[:] += 1_000_000 if t0 == 1 else (1 << 33)
     got, ref = run_both(cfg, tr)
     assert got.summary["engine_path"] == 3
     assert_same(got, ref)
