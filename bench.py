@@ -226,8 +226,9 @@ def main():
         if a.cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(a, W, H, load, hot)
         print(json.dumps(line), flush=True)
-        if wl == "mesh" and (summ.get("fallbacks") or summ.get("retries")):
-            print(f"bench: the batch needed reruns {line['reruns']}", file=sys.stderr)
+        if wl == "mesh" and (summ.get("fallbacks") or summ.get("retries") or int(summ.get("engine_path", -1)) != 4):
+            print(f"bench: the batch needed reruns {line['reruns']} or left the chain engine "
+                  f"(engine_path {summ.get('engine_path')})", file=sys.stderr)
             sys.exit(3)
 
     eng.close()
@@ -303,6 +304,8 @@ def sweep_bench(a, world, rank, local):
                          "kernel_launches": lv_n, "kernel_avg_us": lv_ms * 1e3 / max(lv_n, 1),
                          "algorithmic_bytes_per_launch": alg / max(lv_n, 1)},
             "kernel_ms": {k: round(v[0], 4) for k, v in kst.items()},
+            "engine_path": int(summ.get("engine_path", -1)),
+            "reruns": {"retries": int(summ.get("retries", 0)), "fallbacks": int(summ.get("fallbacks", 0))},
             "trace_gen_s": round(gen_s, 2),
             **({"cpu_baseline": sweep_cpu_baseline(a, pts, ppt)} if a.cpu_baseline and world == 1 else {}),
         }), flush=True)

@@ -160,6 +160,7 @@ struct gnoc_engine
    uint32_t ch_epoch = 0;
    int ch_grid = 0;
    int force_levels = 0;
+   int ch_declined = 0;                     // this batch fell back from the chain engine: later runs skip it
    int used_chain = 0;
    uint32_t ncpx = 0, ncpy = 0;
    DevBuf ch_cp, ch_bt, ch_st, ch_ctr, ch_stamps0, ch_stamps1;
@@ -554,10 +555,12 @@ static constexpr uint32_t CH_NW_MAX = 4096;
 static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, uint64_t t_last)
 {
    const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size
+   const char* ff = std::getenv("GNOC_CH_FILL");         // experiment knob: the target fill
+   const double fill = ff && std::atof(ff) > 0 ? std::atof(ff) : CH_FILL;
    const uint64_t span = t_last + 1;
    double d = 1e300;
-   if (port_max) d = std::min(d, CH_FILL * ch::CAP * (double) span / (double) port_max);
-   if (ins_max) d = std::min(d, CH_FILL * ch::ICAP * (double) span / (double) ins_max);
+   if (port_max) d = std::min(d, fill * ch::CAP * (double) span / (double) port_max);
+   if (ins_max) d = std::min(d, fill * ch::ICAP * (double) span / (double) ins_max);
    uint32_t sh = 10;
    while (sh < 40 && (double) (1ull << (sh + 1)) <= d) sh++;
    if (fv && std::atoi(fv) > 0) sh = (uint32_t) std::atoi(fv);
@@ -567,10 +570,12 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
    {
       e->ch_shift = 0;   // windows of 2^32 ps or more do not fit the 32-bit time offsets
       e->ch_nw = 0;
+      e->ch_declined = 0;
       return;
    }
    e->ch_shift = sh;
    e->ch_nw = (uint32_t) nw;
+   e->ch_declined = 0;
 }
 
 // The submitted trace's contract checks and statistics, on the device
@@ -1010,7 +1015,7 @@ static bool chain_usable(const gnoc_engine* e)
 {
    const char* env = std::getenv("GNOC_ENGINE");
    if (env && (std::strcmp(env, "levels") == 0 || std::strcmp(env, "v1") == 0)) return false;
-   return e->ch_nw > 0 && e->f1 && !e->nb && !e->force_levels && !e->force_v1 && !e->dc.hop_counter &&
+   return e->ch_nw > 0 && e->f1 && !e->nb && !e->force_levels && !e->ch_declined && !e->force_v1 && !e->dc.hop_counter &&
           e->dc.max_list >= 3 && (e->dc.W > 1 || e->dc.H > 1);
 }
 
@@ -1648,9 +1653,18 @@ int gnoc_run(gnoc_engine* e)
       }
       if (rc == GNOC_CH_RETRY || rc == GNOC_CH_FALLBACK)
       {
+         // the same batch would decline again (deterministic): later runs of it go
+         // straight to the level engine (a new submit clears this)
          e->n_fallback++;
          e->force_levels = 1;
+         e->ch_declined = 1;
          rc = run_once(e);
+      }
+      else if (!rc && e->used_chain && e->n_retry)
+      {
+         // the window size that fit: later runs of this batch start with it
+         e->ch_shift = e->ch_shift_run;
+         e->ch_nw = e->ch_nw_run;
       }
       if (rc == GNOC_V3_RETRY)
       {

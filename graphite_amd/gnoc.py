@@ -519,6 +519,9 @@ class ShardedEngine(Engine):
         in gathered_results' all-reduce)."""
         import torch
         import torch.distributed as dist
+        if self.nranks == 1 and not dist.is_initialized():   # one rank, no process group
+            self._check(rc)
+            return
         flag = torch.tensor([1 if rc else 0], dtype=torch.int32)
         if dist.get_backend(self.group) == "nccl":
             flag = flag.cuda(self.cfg.device)
@@ -538,6 +541,8 @@ class ShardedEngine(Engine):
         import torch
         import torch.distributed as dist
         r = self.results()
+        if self.nranks == 1 and not dist.is_initialized():
+            return r
         parts = [r.final_ps, r.zero_load_ps, r.contention_ps, r.port_sum_delay, r.port_count, r.port_mg1,
                  r.port_flit, r.port_last]
         flat = torch.from_numpy(np.concatenate(parts).view(np.int64).copy())

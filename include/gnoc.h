@@ -163,8 +163,8 @@ int gnoc_create(const gnoc_config *cfg, gnoc_engine **out);
  * _window_size).  Every basic queue of the engine then computes its reference
  * time as MovingAverage::compute(packet time) (queue_model_basic.cc:38-46).
  * Requires queue_type GNOC_QUEUE_BASIC; window_size in [1, 65536] (the
- * reference divides by zero at 0).  GNOC_MOVING_AVG_GEOMETRIC_MEAN returns
- * GNOC_EUNSUPPORTED: its pow() chain is not bit-reproducible against glibc.  Single unsharded mesh engines only
+ * reference divides by zero at 0).  All three averages are bit-exact; the
+ * geometric mean runs glibc's own pow (graphite_amd/csrc/glibc_pow.h).  Single unsharded mesh engines only
  * (GNOC_EUNSUPPORTED for sharded, sweep and hop-counter engines and, at
  * gnoc_run, for broadcast packets).  Takes effect at the next gnoc_run. */
 int gnoc_set_basic_moving_average(gnoc_engine *eng, int32_t type, uint32_t window_size);

@@ -49,6 +49,24 @@ def test_synthetic_8x8(load, ppt):
     assert got.summary["mesh_hops"] == int(ref.port_count.reshape(-1, 6)[:, :5].sum())
 
 
+def test_declined_batch_reruns_identically():
+    """A batch the chain engine declines (saturated bursts: the M/G/1 branch
+    fires) runs on the level engine; later runs of the same batch go there
+    directly (no doomed attempt) and give the same bytes."""
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = random_trace(6000, 8, 8, seed=21, max_cycle=150, burst0=200)
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    a, s1 = eng.results(), eng.summary()
+    eng.run()
+    b, s2 = eng.results(), eng.summary()
+    eng.close()
+    assert s1["fallbacks"] >= 1 and s2["fallbacks"] == 0 and s1["engine_path"] == s2["engine_path"] != 4
+    assert_same(a, b)
+    assert_same(a, oracle.run(cfg, tr))
+
+
 def test_saturated_mg1_is_exercised():
     """Saturated 8x8 from t=0: the M/G/1 fallback fires and must match."""
     cfg = gnoc.EngineConfig(num_tiles=64)
