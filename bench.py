@@ -197,8 +197,8 @@ def main():
                 "parallelism": (f"rowband/colband{world} + RCCL all-to-all" if sharded and world > 1 else
                                 f"replicas{world}" if world > 1 else "single"),
                 "engine_path": int(summ.get("engine_path", -1)),
-                "windows": int(summ.get("windows", 0)), "window_ps": (1 << int(summ.get("window_shift", 0)))
-                if summ.get("windows") else None,
+                "windows": [int(summ.get("windows", 0)), int(summ.get("windows_y", 0))],
+                "window_ps": [int(summ.get("window_ps_x", 0)), int(summ.get("window_ps_y", 0))],
             },
             # every rerun is exact but slow: reported, and the bench refuses to report a
             # configs[1] number that needed one

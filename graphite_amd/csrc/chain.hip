@@ -9,8 +9,9 @@
 // a few "insert" slots written by earlier phases (IN_LOCAL for X ports; IN_LOCAL,
 // IN_W, IN_E for Y ports).
 //
-// Time is cut into windows [w D, (w+1) D), D = 2^dshift ps, the last one
-// unbounded.  One workgroup task = (chain, window): it walks the chain's ports
+// Time is cut into windows [w D, (w+1) D), the last one unbounded; D per phase,
+// sized from the batch's busiest port and then from the fill the previous run
+// measured (engine.hip choose_windows / adapt_windows).  One workgroup task = (chain, window): it walks the chain's ports
 // in order, keeping the window's arrival stream in LDS:
 //   port i:  stream (sorted)  --FIFO max-plus scan-->  departures
 //            continuing departures with t' < window end stay in LDS and are
@@ -118,10 +119,12 @@ struct ChainArgs
    unsigned long long* port_last;
    unsigned* errflag;             // [0] route invariant, [2] exception tails exist, [4] chain flags
    unsigned* ctr;                 // dequeue head
-   uint32_t nch, len, nW, dshift;
+   uint32_t nch, len, nW, pad2;
+   uint64_t D;                    // window length (ps); window w = [w D, (w + 1) D), the last one unbounded
    uint32_t cp0;                  // state index offset of this phase
    uint32_t pad0;
    uint64_t etag;                 // epoch << 48
+   unsigned* nmax;                // [0] the most stream records, [1] the most inserts of any step (window sizing)
    uint64_t* stamps;              // debug (GNOC_STAMPS=1): [(task * len + i) * 16 + k] phase stamps, else null
    uint32_t exp;                  // unused
    uint32_t pad1;
@@ -255,7 +258,11 @@ __device__ __forceinline__ uint32_t lb(const uint64_t* a, uint32_t n, uint64_t k
    return pos;
 }
 
-__device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f) { atomicOr(a.errflag + 4, f); }
+__device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f)
+{
+   atomicOr(a.errflag + 4, f);
+   if (f & F_RETRY) atomicMax(a.nmax, 0xFFFFFFFFu);   // tells the host which phase's windows overflowed
+}
 __device__ __forceinline__ bool flagged(const ChainArgs& a)
 {
    return (__hip_atomic_load(a.errflag + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & F_ANY) != 0;
@@ -577,8 +584,8 @@ template <int NL>
 __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
 {
    const uint32_t lane = threadIdx.x;
-   const uint64_t wbase = (uint64_t) w << a.dshift;
-   const uint64_t wlen = (w + 1 < a.nW) ? (1ull << a.dshift) : OFF_LIM;   // kept offsets: t' - wbase < wlen
+   const uint64_t wbase = (uint64_t) w * a.D;
+   const uint64_t wlen = (w + 1 < a.nW) ? a.D : OFF_LIM;   // kept offsets: t' - wbase < wlen
    const uint64_t wq = wbase / 1000ull;
    const uint32_t wr = (uint32_t) (wbase - wq * 1000ull);
    const uint64_t wb = wq ? wq - 1 : 0;          // base cycle: every request of the window has tc > wb (w > 0)
@@ -602,6 +609,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
    uint32_t cpv = 0, bv = 0;     // descriptor / bounds of the port after next, in flight
    uint32_t nK = 0, nI = 0;      // this port's kept records and inserts
    uint32_t P0cur = 0, nin_prev = 0, ncont_prev = 0;   // this port's chain input: records before / kept / all of this window
+   uint32_t nmax = 0, imax = 0;  // the fullest stream / insert list of this task (window sizing)
    {
       nI = fetch_inserts<NL>(sm, a, 0, 0, iv, 0);
       if (nI > (uint32_t) ICAP)
@@ -880,6 +888,8 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
             atomicMax(&a.port_last[port], (unsigned long long) Xo);
          }
       }
+      nmax = n > nmax ? n : nmax;
+      imax = itot > imax ? itot : imax;   // the next port's inserts (checked against ICAP below)
       // the next port's chain input: records before this window, kept, all of this window
       P0cur = cin[1];
       nin_prev = nin;
@@ -898,6 +908,11 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       }
       nK = nin;
       nI = itot;
+   }
+   if (lane == 0)
+   {
+      atomicMax(a.nmax, nmax);
+      atomicMax(a.nmax + 1, imax);
    }
 }
 
@@ -994,9 +1009,9 @@ __global__ __launch_bounds__(256) void k_chain_plan(DevCfg c, uint32_t ncpx, uin
 
 // One workgroup per (chain port, insert list): bt[w] = first record of the
 // slot with t >= w D (w < nW), bt[nW] = record count.  Window of t:
-// min(t >> dshift, nW - 1) (the last window is unbounded).
+// min(t / D, nW - 1) (the last window is unbounded).
 __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict__ cp, uint32_t nl, uint32_t nW,
-                                                    uint32_t dshift, const Rec* __restrict__ recs,
+                                                    uint64_t D, const Rec* __restrict__ recs,
                                                     uint32_t* __restrict__ bt)
 {
    const uint32_t k = blockIdx.x / nl, j = blockIdx.x % nl;
@@ -1011,12 +1026,12 @@ __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict_
    }
    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
    {
-      uint64_t wi = recs[base + i].t >> dshift;
+      uint64_t wi = recs[base + i].t / D;
       wi = wi < wl ? wi : wl;
       int64_t wp = -1;
       if (i)
       {
-         uint64_t q = recs[base + i - 1].t >> dshift;
+         uint64_t q = recs[base + i - 1].t / D;
          wp = (int64_t) (q < wl ? q : wl);
       }
       for (int64_t v = wp + 1; v <= (int64_t) wi; v++) b[v] = i;

@@ -153,10 +153,14 @@ struct gnoc_engine
    uint32_t ma_window = 1;
    DevBuf ma_t, ma_key, ma_val, ma_key2, ma_val2, ma_lo, ma_hi, ma_d, ma_ref, ma_agg, ma_m, ma_bcnt, ma_hist;
 
-   // v4 chain engine (chain.hip): windows of 2^ch_shift ps, ch_nw of them (sized at submit)
-   uint32_t ch_shift = 0, ch_nw = 0;
+   // v4 chain engine (chain.hip): per phase (X, Y) windows of ch_D ps, ch_nw of them
+   // (sized at submit, then from the fill each run measures)
+   uint64_t ch_D[2] = { 0, 0 };
+   uint32_t ch_nw[2] = { 0, 0 };
+   uint64_t ch_D_cap[2] = { 0, 0 };         // a window length that overflowed LDS (0: none yet)
    uint64_t h_tlast = 0;                    // last injection time of the batch (k_validate)
-   uint32_t ch_shift_run = 0, ch_nw_run = 0;   // the attempt in flight
+   uint64_t ch_D_run[2] = { 0, 0 };         // the attempt in flight
+   uint32_t ch_nw_run[2] = { 0, 0 };
    uint32_t ch_epoch = 0;
    int ch_grid = 0;
    int force_levels = 0;
@@ -546,36 +550,65 @@ static uint64_t record_bound(const gnoc_engine* e, uint64_t records)
 }
 
 
-// Chain-engine windows (chain.hip): D = 2^shift ps with the busiest port's
+// Chain-engine windows (chain.hip), per phase: D ps with the busiest port's
 // expected records per window near CH_FILL of the LDS stream capacity (and its
 // inserts within the insert buffer), assuming a steady rate over [0, t_last].
-// nW = t_last / D + 1 windows, the last one unbounded.  shift 0 = chain off.
-static constexpr double CH_FILL = 0.55;
+// nW = t_last / D + 1 windows, the last one unbounded.  D = 0: chain off.  After
+// each run adapt_windows resizes D from the fullest step the run measured.
+static constexpr double CH_FILL = 0.45;     // first run: the steady-rate estimate (bursts reach ~1.7x on the Y phase)
+static constexpr double CH_TARGET = 0.9;     // adapted windows: the fullest step at 0.9 of capacity
 static constexpr uint32_t CH_NW_MAX = 4096;
+static constexpr uint64_t CH_D_MIN = 1024, CH_D_MAX = 1ull << 31;   // 32-bit time offsets in a window
+static uint32_t windows_of(uint64_t D, uint64_t t_last) { return (uint32_t) (t_last / D + 1); }
+static void set_window(gnoc_engine* e, int p, double d)
+{
+   const uint64_t t_last = e->h_tlast;
+   uint64_t D = d >= (double) CH_D_MAX ? CH_D_MAX : (uint64_t) d;
+   if (D < CH_D_MIN) D = CH_D_MIN;
+   if (windows_of(D, t_last) > CH_NW_MAX) D = t_last / (CH_NW_MAX - 1) + 1;
+   if (D > CH_D_MAX) D = 0;   // windows this long do not fit the 32-bit time offsets: chain off
+   e->ch_D[p] = D;
+   e->ch_nw[p] = D ? windows_of(D, t_last) : 0;
+}
 static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, uint64_t t_last)
 {
-   const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size
-   const char* ff = std::getenv("GNOC_CH_FILL");         // experiment knob: the target fill
-   const double fill = ff && std::atof(ff) > 0 ? std::atof(ff) : CH_FILL;
+   const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size (2^shift ps)
+   const char* pv = std::getenv("GNOC_WINDOW_PS");      // test knob: force the window size (ps)
    const uint64_t span = t_last + 1;
    double d = 1e300;
-   if (port_max) d = std::min(d, fill * ch::CAP * (double) span / (double) port_max);
-   if (ins_max) d = std::min(d, fill * ch::ICAP * (double) span / (double) ins_max);
-   uint32_t sh = 10;
-   while (sh < 40 && (double) (1ull << (sh + 1)) <= d) sh++;
-   if (fv && std::atoi(fv) > 0) sh = (uint32_t) std::atoi(fv);
-   uint64_t nw = (t_last >> sh) + 1;
-   while (nw > CH_NW_MAX && sh < 40) { sh++; nw = (t_last >> sh) + 1; }
-   if (sh > 31)
-   {
-      e->ch_shift = 0;   // windows of 2^32 ps or more do not fit the 32-bit time offsets
-      e->ch_nw = 0;
-      e->ch_declined = 0;
-      return;
-   }
-   e->ch_shift = sh;
-   e->ch_nw = (uint32_t) nw;
+   if (port_max) d = std::min(d, CH_FILL * ch::CAP * (double) span / (double) port_max);
+   if (ins_max) d = std::min(d, CH_FILL * ch::ICAP * (double) span / (double) ins_max);
+   if (fv && std::atoi(fv) > 0) d = (double) (1ull << std::atoi(fv));
+   if (pv && std::atoll(pv) > 0) d = (double) std::atoll(pv);
+   e->h_tlast = t_last;
+   const char* px = std::getenv("GNOC_WINDOW_PS_X");    // experiment knobs: one phase's window size
+   const char* py = std::getenv("GNOC_WINDOW_PS_Y");
+   set_window(e, 0, px && std::atoll(px) > 0 ? (double) std::atoll(px) : d);
+   set_window(e, 1, py && std::atoll(py) > 0 ? (double) std::atoll(py) : d);
+   if (!e->ch_D[0] || !e->ch_D[1]) e->ch_D[0] = e->ch_D[1] = e->ch_nw[0] = e->ch_nw[1] = 0;
+   e->ch_D_cap[0] = e->ch_D_cap[1] = 0;
    e->ch_declined = 0;
+}
+// After a chain run without retries: per phase, scale D so that the fullest step
+// (stream records, inserts) lands near CH_TARGET of its LDS capacity.  Results do
+// not depend on D; a window that overflows later retries with half the length.
+static void adapt_windows(gnoc_engine* e, const unsigned* nmax)
+{
+   if (std::getenv("GNOC_WINDOW_SHIFT") || std::getenv("GNOC_WINDOW_PS") || std::getenv("GNOC_WINDOW_PS_X") ||
+       std::getenv("GNOC_WINDOW_PS_Y"))
+      return;
+   for (int p = 0; p < 2; p++)
+   {
+      const unsigned n = nmax[2 * p], ni = nmax[2 * p + 1];
+      if (!n || !e->ch_D[p]) continue;
+      double r = CH_TARGET * ch::CAP / (double) n;
+      if (ni) r = std::min(r, 0.95 * ch::ICAP / (double) ni);   // inserts are few: only keep them in the buffer
+      if (r > 0.92 && r < 1.08) continue;   // close enough: no churn
+      double d = (double) e->ch_D[p] * r;
+      if (e->ch_D_cap[p]) d = std::min(d, 0.95 * (double) e->ch_D_cap[p]);   // stay below a size that overflowed
+      set_window(e, p, d);
+   }
+   if (!e->ch_D[0] || !e->ch_D[1]) e->ch_D[0] = e->ch_D[1] = e->ch_nw[0] = e->ch_nw[1] = 0;
 }
 
 // The submitted trace's contract checks and statistics, on the device
@@ -664,7 +697,6 @@ static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t
          default: return fail(e, GNOC_EUNSUPPORTED, "inject time beyond 2^50 ps at packet " + at);
       }
    }
-   e->h_tlast = n ? v.tlast : 0;
    choose_windows(e, v.pmax, v.imax, n ? v.tlast : 0);
    *records = v.records;
    *nbc = v.nbc;
@@ -1015,7 +1047,7 @@ static bool chain_usable(const gnoc_engine* e)
 {
    const char* env = std::getenv("GNOC_ENGINE");
    if (env && (std::strcmp(env, "levels") == 0 || std::strcmp(env, "v1") == 0)) return false;
-   return e->ch_nw > 0 && e->f1 && !e->nb && !e->force_levels && !e->ch_declined && !e->force_v1 && !e->dc.hop_counter &&
+   return e->ch_nw[0] > 0 && e->f1 && !e->nb && !e->force_levels && !e->ch_declined && !e->force_v1 && !e->dc.hop_counter &&
           e->dc.max_list >= 3 && (e->dc.W > 1 || e->dc.H > 1);
 }
 
@@ -1028,11 +1060,12 @@ static int chain_setup(gnoc_engine* e)
    e->ncpx = W > 1 ? 2 * (e->ry1 - e->ry0) * (W - 1) : 0;
    e->ncpy = H > 1 ? 2 * (e->cx1 - e->cx0) * (H - 1) : 0;
    const uint32_t ncp = e->ncpx + e->ncpy;
-   const uint32_t nW = e->ch_nw_run;
+   const uint32_t nWx = e->ch_nw_run[0], nWy = e->ch_nw_run[1];
    GNOC_HIP(e, e->ch_cp.ensure((size_t) std::max<uint32_t>(ncp, 1) * sizeof(ChainPort)));
-   GNOC_HIP(e, e->ch_bt.ensure(((size_t) e->ncpx + 3ull * e->ncpy + 1) * (nW + 1) * 4));
-   GNOC_HIP(e, e->ch_ctr.ensure(64));
-   const size_t stb = (size_t) std::max<uint32_t>(ncp, 1) * nW * ch::SW * 8;
+   // window bounds and hand-off state: the X phase's, then the Y phase's
+   GNOC_HIP(e, e->ch_bt.ensure(((size_t) e->ncpx * (nWx + 1) + 3ull * e->ncpy * (nWy + 1) + 1) * 4));
+   GNOC_HIP(e, e->ch_ctr.ensure(256));   // [0, 1] dequeue heads; [32, 36) fill maxima, a line of their own
+   const size_t stb = ((size_t) e->ncpx * nWx + (size_t) e->ncpy * nWy + 1) * ch::SW * 8;
    const bool fresh = e->ch_st.bytes < stb;
    GNOC_HIP(e, e->ch_st.ensure(stb));
    // hand-off granules carry a 16-bit epoch: a new epoch per attempt, the buffer
@@ -1043,7 +1076,7 @@ static int chain_setup(gnoc_engine* e)
       GNOC_HIP(e, hipMemsetAsync(e->ch_st.p, 0, e->ch_st.bytes, s));
       if (e->ch_epoch == 0) e->ch_epoch = 1;
    }
-   GNOC_HIP(e, hipMemsetAsync(e->ch_ctr.p, 0, 64, s));
+   GNOC_HIP(e, hipMemsetAsync(e->ch_ctr.p, 0, 256, s));
    if (ncp)
       GNOC_LAUNCH(e, KC_PLAN, ch::k_chain_plan, dim3((ncp + 255) / 256), dim3(256), 0, s, c, e->ncpx, e->ncpy, e->ry0,
                   e->cx0, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->ch_cp.as<ChainPort>());
@@ -1059,11 +1092,11 @@ static int chain_phase(gnoc_engine* e, int phase)
    if (!ncp) return GNOC_OK;
    const uint32_t len = phase ? c.H - 1 : c.W - 1;
    const uint32_t nl = phase ? 3u : 1u;
-   const uint32_t nW = e->ch_nw_run;
+   const uint32_t nW = e->ch_nw_run[phase];
+   const uint64_t D = e->ch_D_run[phase];
    const ChainPort* cp = e->ch_cp.as<ChainPort>() + (phase ? e->ncpx : 0);
-   uint32_t* bt = e->ch_bt.as<uint32_t>() + (phase ? (size_t) e->ncpx * (nW + 1) : 0);
-   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, cp, nl, nW, e->ch_shift_run,
-               e->recs.as<Rec>(), bt);
+   uint32_t* bt = e->ch_bt.as<uint32_t>() + (phase ? (size_t) e->ncpx * (e->ch_nw_run[0] + 1) : 0);
+   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, cp, nl, nW, D, e->recs.as<Rec>(), bt);
    ChainArgs a;
    a.c = c;
    a.cp = cp;
@@ -1071,7 +1104,7 @@ static int chain_phase(gnoc_engine* e, int phase)
    a.recs = e->recs.as<Rec>();
    a.samp_t = e->samp_t.as<uint64_t>();
    a.samp_id = e->samp_id.as<uint32_t>();
-   a.st = e->ch_st.as<uint64_t>();
+   a.st = e->ch_st.as<uint64_t>() + (phase ? (size_t) e->ncpx * e->ch_nw_run[0] * ch::SW : 0);
    a.port_sum = e->port_sum.as<unsigned long long>();
    a.port_cnt = e->port_cnt.as<unsigned long long>();
    a.port_flit = e->port_flit.as<unsigned long long>();
@@ -1081,8 +1114,12 @@ static int chain_phase(gnoc_engine* e, int phase)
    a.nch = ncp / len;
    a.len = len;
    a.nW = nW;
-   a.dshift = e->ch_shift_run;
-   a.cp0 = phase ? e->ncpx : 0;
+   a.pad2 = 0;
+   a.D = D;
+   a.cp0 = 0;   // st points at this phase's state
+   // away from the flag word every poll reads and from the dequeue heads: task-end
+   // atomics on those lines slowed the hand-off polls by half
+   a.nmax = e->ch_ctr.as<unsigned>() + 32 + 2 * phase;
    a.pad0 = 0;
    a.etag = (uint64_t) e->ch_epoch << 48;
    a.stamps = nullptr;
@@ -1316,6 +1353,8 @@ static int run_post(gnoc_engine* e, bool closed_form)
    {
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 3, e->gtot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
+      if (e->used_chain)
+         GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 14, e->ch_ctr.as<unsigned>() + 32, 16, hipMemcpyDeviceToHost, s));
    }
    GNOC_HIP(e, hipStreamSynchronize(s));
    e->h_counters[0] = e->h_pinned[0];
@@ -1638,17 +1677,29 @@ int gnoc_run(gnoc_engine* e)
       if (e->nb && e->submitted) GNOC_HIP(e, hipMemsetAsync(e->d_bm1.p, 0, nv * 8, e->stream));
       e->force_v1 = forced;
       e->force_levels = 0;
-      e->ch_shift_run = e->ch_shift;
-      e->ch_nw_run = e->ch_nw;
+      for (int p = 0; p < 2; p++)
+      {
+         e->ch_D_run[p] = e->ch_D[p];
+         e->ch_nw_run[p] = e->ch_nw[p];
+      }
       if (e->bc_passes == 0) { e->n_retry = 0; e->n_fallback = 0; }
       int rc = run_once(e);
       // chain engine: a window that overflowed LDS reruns with windows half as long
       // (twice as many), up to 3 times; anything else it cannot take reruns on levels
-      while (rc == GNOC_CH_RETRY && e->ch_shift_run > 10 && e->n_retry < 3 && 2ull * e->ch_nw_run <= CH_NW_MAX)
+      while (rc == GNOC_CH_RETRY && e->n_retry < 3 && e->ch_D_run[0] >= 2 * CH_D_MIN && e->ch_D_run[1] >= 2 * CH_D_MIN &&
+             2ull * std::max(e->ch_nw_run[0], e->ch_nw_run[1]) <= CH_NW_MAX)
       {
          e->n_retry++;
-         e->ch_shift_run--;
-         e->ch_nw_run = e->ch_nw_run * 2;
+         const unsigned* nm = (const unsigned*) (e->h_pinned + 14);   // the failed attempt's maxima
+         const bool known = nm[0] == 0xFFFFFFFFu || nm[2] == 0xFFFFFFFFu;
+         for (int p = 0; p < 2; p++)
+         {
+            // halve the phase that overflowed (both when the kernel could not say)
+            if (known && nm[2 * p] != 0xFFFFFFFFu) continue;
+            if (!e->ch_D_cap[p] || e->ch_D_run[p] < e->ch_D_cap[p]) e->ch_D_cap[p] = e->ch_D_run[p];
+            e->ch_D_run[p] /= 2;
+            e->ch_nw_run[p] = windows_of(e->ch_D_run[p], e->h_tlast);
+         }
          rc = run_once(e);
       }
       if (rc == GNOC_CH_RETRY || rc == GNOC_CH_FALLBACK)
@@ -1663,9 +1714,14 @@ int gnoc_run(gnoc_engine* e)
       else if (!rc && e->used_chain && e->n_retry)
       {
          // the window size that fit: later runs of this batch start with it
-         e->ch_shift = e->ch_shift_run;
-         e->ch_nw = e->ch_nw_run;
+         for (int p = 0; p < 2; p++)
+         {
+            e->ch_D[p] = e->ch_D_run[p];
+            e->ch_nw[p] = e->ch_nw_run[p];
+         }
       }
+      else if (!rc && e->used_chain)
+         adapt_windows(e, (const unsigned*) (e->h_pinned + 14));   // the fill this run measured
       if (rc == GNOC_V3_RETRY)
       {
          e->n_fallback++;
@@ -1879,8 +1935,11 @@ int gnoc_run_begin(gnoc_engine* e, void* send_buf)
    e->used_chain = 0;
    e->n_retry = 0;
    e->n_fallback = 0;
-   e->ch_shift_run = e->ch_shift;
-   e->ch_nw_run = e->ch_nw;
+   for (int p = 0; p < 2; p++)
+   {
+      e->ch_D_run[p] = e->ch_D[p];
+      e->ch_nw_run[p] = e->ch_nw[p];
+   }
    hipStream_t s = e->stream;
    rc = run_plan_v3(e);
    if (!rc && chain_usable(e))
@@ -2061,8 +2120,14 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
    out->engine_path = e->dc.contention ? (uint32_t) e->used_v3 : 2u;
    out->retries = e->n_retry;
    out->fallbacks = e->n_fallback;
-   out->windows = e->used_chain ? e->ch_nw_run : 0u;
-   out->window_shift = e->used_chain ? e->ch_shift_run : 0u;
+   out->windows = e->used_chain ? e->ch_nw_run[0] : 0u;
+   uint32_t sh = 0;
+   while (e->used_chain && sh < 63 && (2ull << sh) <= e->ch_D_run[0]) sh++;
+   out->window_shift = e->used_chain ? sh : 0u;
+   out->windows_y = e->used_chain ? e->ch_nw_run[1] : 0u;
+   out->abi_pad = 0;
+   out->window_ps_x = e->used_chain ? e->ch_D_run[0] : 0u;
+   out->window_ps_y = e->used_chain ? e->ch_D_run[1] : 0u;
    if (e->ran && e->dc.contention)
    {
       std::vector<uint64_t> m((size_t) e->dc.N * PORTS);
@@ -2114,8 +2179,8 @@ __attribute__((visibility("default"))) int gnoc_debug_chain_stamps(gnoc_engine* 
    const uint32_t len = phase ? e->dc.H - 1 : e->dc.W - 1;
    const uint32_t ncp = phase ? e->ncpy : e->ncpx;
    const uint32_t nch = len ? ncp / len : 0;
-   *count = (size_t) nch * e->ch_nw_run * len * 16;
-   if (geom) { geom[0] = nch; geom[1] = e->ch_nw_run; geom[2] = len; geom[3] = e->ch_shift_run; }
+   *count = (size_t) nch * e->ch_nw_run[phase] * len * 16;
+   if (geom) { geom[0] = nch; geom[1] = e->ch_nw_run[phase]; geom[2] = len; geom[3] = (uint32_t) (e->ch_D_run[phase] >> 10); }
    if (!out || !sb.p) return GNOC_OK;
    GNOC_HIP(e, hipMemcpy(out, sb.p, std::min(cap, *count) * 8, hipMemcpyDeviceToHost));
    return GNOC_OK;

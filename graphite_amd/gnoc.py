@@ -102,6 +102,10 @@ class GnocSummary(ctypes.Structure):
         ("fallbacks", ctypes.c_uint32),
         ("windows", ctypes.c_uint32),
         ("window_shift", ctypes.c_uint32),
+        ("windows_y", ctypes.c_uint32),
+        ("abi_pad", ctypes.c_uint32),
+        ("window_ps_x", ctypes.c_uint64),
+        ("window_ps_y", ctypes.c_uint64),
     ]
 
 

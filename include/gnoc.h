@@ -147,8 +147,13 @@ typedef struct gnoc_summary
       timeout or an unsplittable burst). */
    uint32_t retries;
    uint32_t fallbacks;
-   uint32_t windows;            /* chain-engine time windows of the last attempt (0 = not used) */
-   uint32_t window_shift;       /* window length 2^window_shift ps                      */
+   uint32_t windows;            /* chain-engine time windows of the last attempt, X phase (0 = not used) */
+   uint32_t window_shift;       /* floor(log2) of the X phase's window length in ps     */
+   /* ABI 3: windows per phase, any length (sized from each run's measured fill) */
+   uint32_t windows_y;          /* Y phase's windows                                     */
+   uint32_t abi_pad;
+   uint64_t window_ps_x;        /* window length (ps) of the X phase                     */
+   uint64_t window_ps_y;        /* ... of the Y phase                                    */
 } gnoc_summary;
 
 /* Replaces NetworkModel::createModel(..., NETWORK_EMESH_HOP_BY_HOP)

@@ -41,3 +41,41 @@ def test_tornado_32x32_hotspot_mix_forced_windows(monkeypatch):
     tr = gnoc.synthetic_trace(32, 32, 0.002, 150, seed=9, pattern="tornado", hotspot_fraction=0.1)
     got, ref = run_both(cfg, tr)
     assert_same(got, ref)
+
+
+@pytest.mark.parametrize("wps", [98_765, 1_234_567])
+def test_odd_window_lengths(monkeypatch, wps):
+    """Window lengths that are not powers of two (the engine sizes each phase's
+    windows from the fill it measured): records sit on window edges at odd
+    offsets; hotspot mix, bit-exact."""
+    monkeypatch.setenv("GNOC_WINDOW_PS", str(wps))
+    cfg = gnoc.EngineConfig(num_tiles=1024)
+    tr = gnoc.synthetic_trace(32, 32, 0.004, 120, seed=11, hotspot_fraction=0.2)
+    got, ref = run_both(cfg, tr)
+    assert got.summary["engine_path"] == 4 and got.summary["window_ps_x"] == wps
+    assert_same(got, ref)
+
+
+def test_adapted_windows_repeat_exactly():
+    """Runs after the first resize the windows from the measured fill (per phase);
+    every run gives the same bytes as the oracle."""
+    cfg = gnoc.EngineConfig(num_tiles=1024)
+    tr = gnoc.synthetic_trace(32, 32, 0.005, 300, seed=13)
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    sizes, res = [], []
+    for _ in range(3):
+        eng.run()
+        s = eng.summary()
+        sizes.append((s["window_ps_x"], s["window_ps_y"]))
+        res.append(eng.results())
+    eng.close()
+    ref = oracle_run(cfg, tr)
+    for r in res:
+        assert_same(r, ref)
+    assert sizes[1] != sizes[0] or sizes[2] == sizes[1]
+
+
+def oracle_run(cfg, tr):
+    from oracle import oracle
+    return oracle.run(cfg, tr)

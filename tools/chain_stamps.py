@@ -78,6 +78,15 @@ def main():
         task_t = st[:, -1, 9] - t[:, 0, 0]
         good = t[:, 0, 0] > 0
         print(f"  task duration med {np.median(task_t[good]):.0f} cyc; span of phase {t[good][:, :, 0].max() - t[good][:, 0, 0].min()} cyc")
+        # records per step by window: where the LDS capacity is used
+        nw_ = n[:, :-1].reshape(nW, nch, ln - 1)
+        mx = nw_.max(axis=(1, 2))
+        top = np.argsort(mx)[::-1][:8]
+        print("  busiest windows (index: max records/step):", ", ".join(f"{q}: {mx[q]}" for q in top),
+              f"| 99th pct of per-window max {np.percentile(mx, 99):.0f}, median {np.median(mx):.0f}")
+        # per chain: the fullest step (would per-chain windows help?)
+        cm = nw_.max(axis=(0, 2))
+        print("  per-chain max records/step: sorted", np.sort(cm).tolist())
         # wait vs window index
         w_idx = np.repeat(np.arange(nW), nch)
         for q in (0, 1, 2, nW // 2, nW - 1):
