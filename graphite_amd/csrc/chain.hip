@@ -104,27 +104,40 @@ struct __attribute__((aligned(16))) ChainPort
 };
 static_assert(sizeof(ChainPort) == 128, "ChainPort is one 128-B line");
 
+// One chain's windows: length D (ps), nW of them; its hand-off state block and
+// window-bounds block (offsets into ChainArgs::st / bt).  Chains of a phase may
+// have different windows (each is sized from its own measured fill).
+struct ChainWin
+{
+   uint64_t D;
+   uint64_t st_off;               // u64 words: state of (port i, window w) at st_off + (i nW + w) SW
+   uint64_t bt_off;               // u32 words: bounds of (port i, list j) at bt_off + (i nl + j)(nW + 1)
+   uint32_t nW;
+   uint32_t pad;
+};
+
 struct ChainArgs
 {
    DevCfg c;
    const ChainPort* cp;           // [nch * len] (this phase)
-   const uint32_t* bt;            // [(cpi * nl + j) * (nW + 1) + w] window bounds of insert slots
+   const uint32_t* bt;            // window bounds of insert slots (per chain: ChainWin::bt_off)
    Rec* recs;
    uint64_t* samp_t;
    uint32_t* samp_id;
-   uint64_t* st;                  // [(cpi + cp0) * nW + w] * SW  hand-off state
+   uint64_t* st;                  // hand-off state (per chain: ChainWin::st_off)
    unsigned long long* port_sum;
    unsigned long long* port_cnt;
    unsigned long long* port_flit;
    unsigned long long* port_last;
    unsigned* errflag;             // [0] route invariant, [2] exception tails exist, [4] chain flags
    unsigned* ctr;                 // dequeue head
-   uint32_t nch, len, nW, pad2;
-   uint64_t D;                    // window length (ps); window w = [w D, (w + 1) D), the last one unbounded
-   uint32_t cp0;                  // state index offset of this phase
+   uint32_t nch, len, ntasks, pad2;
+   const ChainWin* cw;            // [nch] windows per chain: window w = [w D, (w + 1) D), the last one unbounded
+   const uint32_t* tasks;         // [ntasks] c << 16 | w, ordered by the window's start time w D
+   uint32_t cp0;                  // unused (0)
    uint32_t pad0;
    uint64_t etag;                 // epoch << 48
-   unsigned* nmax;                // [0] the most stream records, [1] the most inserts of any step (window sizing)
+   unsigned* nmax;                // [2 c] the most stream records, [2 c + 1] the most inserts of chain c's steps
    uint64_t* stamps;              // debug (GNOC_STAMPS=1): [(task * len + i) * 16 + k] phase stamps, else null
    uint32_t exp;                  // unused
    uint32_t pad1;
@@ -258,10 +271,12 @@ __device__ __forceinline__ uint32_t lb(const uint64_t* a, uint32_t n, uint64_t k
    return pos;
 }
 
-__device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f)
+__device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f) { atomicOr(a.errflag + 4, f); }
+// A window of chain c overflowed LDS: the run retries, halving that chain's windows.
+__device__ __forceinline__ void flag_overflow(const ChainArgs& a, uint32_t c)
 {
-   atomicOr(a.errflag + 4, f);
-   if (f & F_RETRY) atomicMax(a.nmax, 0xFFFFFFFFu);   // tells the host which phase's windows overflowed
+   flag(a, F_RETRY);
+   atomicMax(a.nmax + 2 * c, 0xFFFFFFFFu);
 }
 __device__ __forceinline__ bool flagged(const ChainArgs& a)
 {
@@ -279,12 +294,14 @@ __device__ __forceinline__ uint32_t fetch_cp(const ChainPort* src, uint32_t l)
    return reinterpret_cast<const uint32_t*>(src)[l];
 }
 __device__ __forceinline__ void put_cp(ChainPort* dst, uint32_t v, uint32_t l) { reinterpret_cast<uint32_t*>(dst)[l] = v; }
-// Window bounds [lo, hi) of the insert slots of chain port cpi (l < 2 nl).
-__device__ __forceinline__ uint32_t fetch_bounds(const ChainArgs& a, uint32_t cpi, uint32_t nl, uint32_t w, uint32_t l)
+// Window bounds [lo, hi) of the insert slots of port i of a chain whose bounds
+// block starts at bt_off (l < 2 nl).
+__device__ __forceinline__ uint32_t fetch_bounds(const ChainArgs& a, uint64_t bt_off, uint32_t nW, uint32_t i, uint32_t nl,
+                                                 uint32_t w, uint32_t l)
 {
    if (l >= 2 * nl) return 0u;
    const uint32_t j = l < nl ? l : l - nl;
-   return a.bt[((uint64_t) cpi * nl + j) * (a.nW + 1) + w + (l < nl ? 0u : 1u)];
+   return a.bt[bt_off + ((uint64_t) i * nl + j) * (nW + 1) + w + (l < nl ? 0u : 1u)];
 }
 __device__ __forceinline__ void put_bounds(Smem& sm, uint32_t slot, uint32_t v, uint32_t nl, uint32_t l)
 {
@@ -584,13 +601,15 @@ template <int NL>
 __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
 {
    const uint32_t lane = threadIdx.x;
-   const uint64_t wbase = (uint64_t) w * a.D;
-   const uint64_t wlen = (w + 1 < a.nW) ? a.D : OFF_LIM;   // kept offsets: t' - wbase < wlen
+   const uint64_t D = a.cw[c].D, st_off = a.cw[c].st_off, bt_off = a.cw[c].bt_off;
+   const uint32_t nW = a.cw[c].nW;
+   const uint64_t wbase = (uint64_t) w * D;
+   const uint64_t wlen = (w + 1 < nW) ? D : OFF_LIM;   // kept offsets: t' - wbase < wlen
    const uint64_t wq = wbase / 1000ull;
    const uint32_t wr = (uint32_t) (wbase - wq * 1000ull);
    const uint64_t wb = wq ? wq - 1 : 0;          // base cycle: every request of the window has tc > wb (w > 0)
    const uint32_t d0 = (uint32_t) (wq - wb);
-   const uint32_t len = a.len, nW = a.nW;
+   const uint32_t len = a.len;
    const uint32_t cpb = c * len;
    const uint32_t mode0 = a.c.analytical ? 1u : 0u;
 
@@ -598,8 +617,8 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
    // then the pipeline's first prefetches (port 1's inserts, port 2's descriptor and bounds)
    if (lane < 32) load_cp(&sm.cp[0], a.cp + cpb, lane);
    else if (len > 1) load_cp(&sm.cp[1], a.cp + cpb + 1, lane - 32);
-   if (lane < 2 * NL) put_bounds(sm, 0, fetch_bounds(a, cpb, NL, w, lane), NL, lane);
-   else if (lane < 4 * NL && len > 1) put_bounds(sm, 1, fetch_bounds(a, cpb + 1, NL, w, lane - 2 * NL), NL, lane - 2 * NL);
+   if (lane < 2 * NL) put_bounds(sm, 0, fetch_bounds(a, bt_off, nW, 0, NL, w, lane), NL, lane);
+   else if (lane < 4 * NL && len > 1) put_bounds(sm, 1, fetch_bounds(a, bt_off, nW, 1, NL, w, lane - 2 * NL), NL, lane - 2 * NL);
    if (lane == 0) sm.kkey[0] = ~0ull;
    wsync();
    uint64_t rk[PER];
@@ -614,7 +633,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       nI = fetch_inserts<NL>(sm, a, 0, 0, iv, 0);
       if (nI > (uint32_t) ICAP)
       {
-         if (lane == 0) flag(a, F_RETRY);
+         if (lane == 0) flag_overflow(a, c);
          return;
       }
       if (store_inserts<NL>(sm, iv, nI, wbase, 0) && lane == 0) flag(a, F_FALLBACK);
@@ -623,7 +642,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       if (len > 2)
       {
          if (lane < 32) cpv = fetch_cp(a.cp + cpb + 2, lane);
-         else bv = fetch_bounds(a, cpb + 2, NL, w, lane - 32);
+         else bv = fetch_bounds(a, bt_off, nW, 2, NL, w, lane - 32);
       }
    }
 
@@ -633,8 +652,8 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       const uint32_t b = i & 1u, bn = b ^ 1u;
       const ChainPort& P = sm.cp[i % 3];
       const bool has_next = i + 1 < len;
-      uint64_t* const stw = a.st + ((uint64_t) (a.cp0 + cpi) * nW + w) * SW;          // this window's state
-      const uint64_t* const stp = w ? a.st + ((uint64_t) (a.cp0 + cpi) * nW + w - 1) * SW : nullptr;   // predecessor's
+      uint64_t* const stw = a.st + st_off + ((uint64_t) i * nW + w) * SW;          // this window's state
+      const uint64_t* const stp = w ? stw - SW : nullptr;                           // predecessor's
 
       // ---- [A] land last step's prefetches: port i+1's inserts, port i+2's descriptor and
       // bounds; load the predecessor's state of this port
@@ -733,7 +752,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          if (i + 3 < len)
          {
             if (lane < 32) cpv = fetch_cp(a.cp + cpi + 3, lane);
-            else bv = fetch_bounds(a, cpi + 3, NL, w, lane - 32);
+            else bv = fetch_bounds(a, bt_off, nW, i + 3, NL, w, lane - 32);
          }
          if (Pep == Kpp) break;
          // ---- slow path: spill-ins join the insert list, then rescan
@@ -749,7 +768,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          const uint32_t take = spill_in(sm, a, a.cp[cpi - 1].obase[1] + Kpp, spn, Ic, IAc, nI, nK, wbase, wlen, skip);
          if (n + take > (uint32_t) CAP)
          {
-            if (lane == 0) flag(a, F_RETRY);
+            if (lane == 0) flag_overflow(a, c);
             return;
          }
          if (!nin_prev) Kout = Kpp + skip + take;   // the consumed prefix of the old spills
@@ -903,7 +922,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       if (!has_next) break;
       if (itot > (uint32_t) ICAP || nin + itot > (uint32_t) CAP)
       {
-         if (lane == 0) flag(a, F_RETRY);
+         if (lane == 0) flag_overflow(a, c);
          return;
       }
       nK = nin;
@@ -911,8 +930,8 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
    }
    if (lane == 0)
    {
-      atomicMax(a.nmax, nmax);
-      atomicMax(a.nmax + 1, imax);
+      atomicMax(a.nmax + 2 * c, nmax);
+      atomicMax(a.nmax + 2 * c + 1, imax);
    }
 }
 
@@ -920,7 +939,7 @@ template <int NL>
 __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
 {
    __shared__ Smem sm;
-   const uint32_t ntasks = a.nch * a.nW;
+   const uint32_t ntasks = a.ntasks;
    // an earlier level served a request by M/G/1 (exception tails): the chain's
    // inputs are not in FIFO order -> the level engine reruns the batch
    if (a.errflag[2] != 0)
@@ -930,13 +949,14 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
    }
    for (;;)
    {
-      // window-major, strictly in order to running workgroups: a task's predecessor
-      // (same chain, window - 1) is always held by a running workgroup or done
+      // in window start-time order, strictly in order to running workgroups: a task's
+      // predecessor (same chain, window - 1) is always held by a running workgroup or done
       uint32_t tk = 0;
       if (threadIdx.x == 0) tk = atomicAdd(a.ctr, 1u);
       tk = rdl(tk, 0);
       if (tk >= ntasks || flagged(a)) return;
-      task<NL>(sm, a, tk % a.nch, tk / a.nch, tk);
+      const uint32_t cw = a.tasks[tk];
+      task<NL>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
       wsync();
    }
 }
@@ -1010,14 +1030,16 @@ __global__ __launch_bounds__(256) void k_chain_plan(DevCfg c, uint32_t ncpx, uin
 // One workgroup per (chain port, insert list): bt[w] = first record of the
 // slot with t >= w D (w < nW), bt[nW] = record count.  Window of t:
 // min(t / D, nW - 1) (the last window is unbounded).
-__global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict__ cp, uint32_t nl, uint32_t nW,
-                                                    uint64_t D, const Rec* __restrict__ recs,
+__global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict__ cp, uint32_t nl, uint32_t len,
+                                                    const ChainWin* __restrict__ cw, const Rec* __restrict__ recs,
                                                     uint32_t* __restrict__ bt)
 {
-   const uint32_t k = blockIdx.x / nl, j = blockIdx.x % nl;
+   const uint32_t k = blockIdx.x / nl, j = blockIdx.x % nl, c = k / len, i = k % len;
+   const uint64_t D = cw[c].D;
+   const uint32_t nW = cw[c].nW;
    const uint64_t base = cp[k].ibase[j];
    const uint32_t n = cp[k].icnt[j];
-   uint32_t* b = bt + (uint64_t) blockIdx.x * (nW + 1);
+   uint32_t* b = bt + cw[c].bt_off + ((uint64_t) i * nl + j) * (nW + 1);
    const uint64_t wl = nW - 1;
    if (n == 0)
    {

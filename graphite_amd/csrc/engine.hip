@@ -153,14 +153,18 @@ struct gnoc_engine
    uint32_t ma_window = 1;
    DevBuf ma_t, ma_key, ma_val, ma_key2, ma_val2, ma_lo, ma_hi, ma_d, ma_ref, ma_agg, ma_m, ma_bcnt, ma_hist;
 
-   // v4 chain engine (chain.hip): per phase (X, Y) windows of ch_D ps, ch_nw of them
-   // (sized at submit, then from the fill each run measures)
-   uint64_t ch_D[2] = { 0, 0 };
-   uint32_t ch_nw[2] = { 0, 0 };
-   uint64_t ch_D_cap[2] = { 0, 0 };         // a window length that overflowed LDS (0: none yet)
-   uint64_t h_tlast = 0;                    // last injection time of the batch (k_validate)
-   uint64_t ch_D_run[2] = { 0, 0 };         // the attempt in flight
-   uint32_t ch_nw_run[2] = { 0, 0 };
+   // v4 chain engine (chain.hip): per phase (X, Y), per chain, windows of chD ps
+   // (sized at submit, then from the fill each run measured per chain)
+   bool ch_on = false;
+   uint64_t h_tlast = 0;                     // last injection time of the batch (k_validate)
+   std::vector<uint64_t> chD[2], chCap[2];   // window length; a length that overflowed LDS (0: none)
+   std::vector<uint64_t> chD_run[2];         // the attempt in flight
+   std::vector<uint64_t> chD_up[2];          // the lengths the device tables hold
+   std::vector<ChainWin> h_cw[2];
+   std::vector<uint32_t> h_tasks[2];
+   uint64_t ch_st_words[2] = { 0, 0 }, ch_bt_words[2] = { 0, 0 };
+   unsigned* h_nmax = nullptr;               // pinned: per chain fill maxima of the last run
+   DevBuf ch_cw, ch_tasks, ch_nmax;
    uint32_t ch_epoch = 0;
    int ch_grid = 0;
    int force_levels = 0;
@@ -399,6 +403,9 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    if (he == hipSuccess) he = hipEventCreate(&e->ev0);
    if (he == hipSuccess) he = hipEventCreate(&e->ev1);
    if (he == hipSuccess) he = hipHostMalloc((void**) &e->h_pinned, 128, hipHostMallocDefault);
+   // per chain fill maxima: 2 u32 for each of the <= 2 (W + H) chains
+   if (he == hipSuccess)
+      he = hipHostMalloc((void**) &e->h_nmax, 16 * ((size_t) e->dc.W + e->dc.H) + 64, hipHostMallocDefault);
    if (he == hipSuccess) he = upload_levels(e);
    if (he == hipSuccess)
    {
@@ -535,6 +542,7 @@ void gnoc_destroy(gnoc_engine* e)
    if (e->ev0) (void) hipEventDestroy(e->ev0);
    if (e->ev1) (void) hipEventDestroy(e->ev1);
    if (e->h_pinned) (void) hipHostFree(e->h_pinned);
+   if (e->h_nmax) (void) hipHostFree(e->h_nmax);
    for (hipEvent_t ev : e->evpool) (void) hipEventDestroy(ev);
    if (e->stream) (void) hipStreamDestroy(e->stream);
    delete e;
@@ -560,15 +568,19 @@ static constexpr double CH_TARGET = 0.9;     // adapted windows: the fullest ste
 static constexpr uint32_t CH_NW_MAX = 4096;
 static constexpr uint64_t CH_D_MIN = 1024, CH_D_MAX = 1ull << 31;   // 32-bit time offsets in a window
 static uint32_t windows_of(uint64_t D, uint64_t t_last) { return (uint32_t) (t_last / D + 1); }
-static void set_window(gnoc_engine* e, int p, double d)
+static uint32_t chain_count(const gnoc_engine* e, int p)
+{
+   return p == 0 ? (e->dc.W > 1 ? 2 * (e->ry1 - e->ry0) : 0u) : (e->dc.H > 1 ? 2 * (e->cx1 - e->cx0) : 0u);
+}
+// A window length from a target: clamped to the 32-bit time offsets and to at
+// most CH_NW_MAX windows; 0 when it cannot fit (chain engine off).
+static uint64_t clamp_window(const gnoc_engine* e, double d)
 {
    const uint64_t t_last = e->h_tlast;
    uint64_t D = d >= (double) CH_D_MAX ? CH_D_MAX : (uint64_t) d;
    if (D < CH_D_MIN) D = CH_D_MIN;
    if (windows_of(D, t_last) > CH_NW_MAX) D = t_last / (CH_NW_MAX - 1) + 1;
-   if (D > CH_D_MAX) D = 0;   // windows this long do not fit the 32-bit time offsets: chain off
-   e->ch_D[p] = D;
-   e->ch_nw[p] = D ? windows_of(D, t_last) : 0;
+   return D > CH_D_MAX ? 0 : D;
 }
 static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, uint64_t t_last)
 {
@@ -583,32 +595,91 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
    e->h_tlast = t_last;
    const char* px = std::getenv("GNOC_WINDOW_PS_X");    // experiment knobs: one phase's window size
    const char* py = std::getenv("GNOC_WINDOW_PS_Y");
-   set_window(e, 0, px && std::atoll(px) > 0 ? (double) std::atoll(px) : d);
-   set_window(e, 1, py && std::atoll(py) > 0 ? (double) std::atoll(py) : d);
-   if (!e->ch_D[0] || !e->ch_D[1]) e->ch_D[0] = e->ch_D[1] = e->ch_nw[0] = e->ch_nw[1] = 0;
-   e->ch_D_cap[0] = e->ch_D_cap[1] = 0;
+   e->ch_on = true;
+   for (int p = 0; p < 2; p++)
+   {
+      const char* k = p ? py : px;
+      const uint64_t D = clamp_window(e, k && std::atoll(k) > 0 ? (double) std::atoll(k) : d);
+      if (!D) e->ch_on = false;
+      e->chD[p].assign(chain_count(e, p), D);
+      e->chCap[p].assign(chain_count(e, p), 0);
+   }
    e->ch_declined = 0;
 }
-// After a chain run without retries: per phase, scale D so that the fullest step
-// (stream records, inserts) lands near CH_TARGET of its LDS capacity.  Results do
-// not depend on D; a window that overflows later retries with half the length.
-static void adapt_windows(gnoc_engine* e, const unsigned* nmax)
+// After a chain run without retries: per chain, scale D so that its fullest step
+// (stream records, inserts) lands near CH_TARGET of the LDS capacity.  Results do
+// not depend on D; a window that overflows later retries with that chain's
+// windows halved, and the overflowing length caps the chain.
+static void adapt_windows(gnoc_engine* e)
 {
    if (std::getenv("GNOC_WINDOW_SHIFT") || std::getenv("GNOC_WINDOW_PS") || std::getenv("GNOC_WINDOW_PS_X") ||
        std::getenv("GNOC_WINDOW_PS_Y"))
       return;
+   const unsigned* nm = e->h_nmax;
    for (int p = 0; p < 2; p++)
    {
-      const unsigned n = nmax[2 * p], ni = nmax[2 * p + 1];
-      if (!n || !e->ch_D[p]) continue;
-      double r = CH_TARGET * ch::CAP / (double) n;
-      if (ni) r = std::min(r, 0.95 * ch::ICAP / (double) ni);   // inserts are few: only keep them in the buffer
-      if (r > 0.92 && r < 1.08) continue;   // close enough: no churn
-      double d = (double) e->ch_D[p] * r;
-      if (e->ch_D_cap[p]) d = std::min(d, 0.95 * (double) e->ch_D_cap[p]);   // stay below a size that overflowed
-      set_window(e, p, d);
+      for (size_t c = 0; c < e->chD[p].size(); c++)
+      {
+         const unsigned n = nm[2 * c], ni = nm[2 * c + 1];
+         if (!n || n == 0xFFFFFFFFu) continue;
+         double r = CH_TARGET * ch::CAP / (double) n;
+         if (ni) r = std::min(r, 0.95 * ch::ICAP / (double) ni);   // inserts are few: only keep them in the buffer
+         if (r > 0.92 && r < 1.08) continue;                        // close enough: no churn
+         double d = (double) e->chD[p][c] * r;
+         if (e->chCap[p][c]) d = std::min(d, 0.95 * (double) e->chCap[p][c]);   // stay below a size that overflowed
+         const uint64_t D = clamp_window(e, d);
+         if (D) e->chD[p][c] = D;
+      }
+      nm += 2 * e->chD[p].size();
    }
-   if (!e->ch_D[0] || !e->ch_D[1]) e->ch_D[0] = e->ch_D[1] = e->ch_nw[0] = e->ch_nw[1] = 0;
+}
+// The device tables of the attempt's windows (chD_run): per chain its windows,
+// state and bounds blocks; the tasks of each phase in window start-time order
+// (so a task's predecessor, same chain and window - 1, is always handed out
+// first).  Rebuilt only when the lengths change.
+static int chain_tables(gnoc_engine* e)
+{
+   if (e->chD_up[0] == e->chD_run[0] && e->chD_up[1] == e->chD_run[1] && e->ch_cw.p) return GNOC_OK;
+   const uint32_t lens[2] = { e->dc.W - 1, e->dc.H - 1 }, nls[2] = { 1u, 3u };
+   std::vector<std::pair<uint64_t, uint32_t>> order;
+   for (int p = 0; p < 2; p++)
+   {
+      auto& cw = e->h_cw[p];
+      cw.assign(e->chD_run[p].size(), ChainWin{});
+      uint64_t st = 0, bt = 0;
+      order.clear();
+      for (size_t c = 0; c < cw.size(); c++)
+      {
+         const uint64_t D = e->chD_run[p][c];
+         const uint32_t nW = windows_of(D, e->h_tlast);
+         cw[c].D = D;
+         cw[c].nW = nW;
+         cw[c].st_off = st;
+         cw[c].bt_off = bt;
+         cw[c].pad = 0;
+         st += (uint64_t) lens[p] * nW * ch::SW;
+         bt += (uint64_t) lens[p] * nls[p] * (nW + 1);
+         for (uint32_t w = 0; w < nW; w++) order.push_back({ (uint64_t) w * D, (uint32_t) (c << 16) | w });
+      }
+      std::stable_sort(order.begin(), order.end(),
+                       [](const std::pair<uint64_t, uint32_t>& x, const std::pair<uint64_t, uint32_t>& y) { return x.first < y.first; });
+      e->h_tasks[p].resize(order.size());
+      for (size_t k = 0; k < order.size(); k++) e->h_tasks[p][k] = order[k].second;
+      e->ch_st_words[p] = st;
+      e->ch_bt_words[p] = bt;
+   }
+   const size_t ncw = e->h_cw[0].size() + e->h_cw[1].size(), nt = e->h_tasks[0].size() + e->h_tasks[1].size();
+   GNOC_HIP(e, e->ch_cw.ensure(std::max<size_t>(ncw, 1) * sizeof(ChainWin)));
+   GNOC_HIP(e, e->ch_tasks.ensure(std::max<size_t>(nt, 1) * 4));
+   GNOC_HIP(e, hipMemcpy(e->ch_cw.p, e->h_cw[0].data(), e->h_cw[0].size() * sizeof(ChainWin), hipMemcpyHostToDevice));
+   GNOC_HIP(e, hipMemcpy(e->ch_cw.as<ChainWin>() + e->h_cw[0].size(), e->h_cw[1].data(), e->h_cw[1].size() * sizeof(ChainWin),
+                         hipMemcpyHostToDevice));
+   GNOC_HIP(e, hipMemcpy(e->ch_tasks.p, e->h_tasks[0].data(), e->h_tasks[0].size() * 4, hipMemcpyHostToDevice));
+   GNOC_HIP(e, hipMemcpy(e->ch_tasks.as<uint32_t>() + e->h_tasks[0].size(), e->h_tasks[1].data(), e->h_tasks[1].size() * 4,
+                         hipMemcpyHostToDevice));
+   e->chD_up[0] = e->chD_run[0];
+   e->chD_up[1] = e->chD_run[1];
+   return GNOC_OK;
 }
 
 // The submitted trace's contract checks and statistics, on the device
@@ -1047,7 +1118,7 @@ static bool chain_usable(const gnoc_engine* e)
 {
    const char* env = std::getenv("GNOC_ENGINE");
    if (env && (std::strcmp(env, "levels") == 0 || std::strcmp(env, "v1") == 0)) return false;
-   return e->ch_nw[0] > 0 && e->f1 && !e->nb && !e->force_levels && !e->ch_declined && !e->force_v1 && !e->dc.hop_counter &&
+   return e->ch_on && e->f1 && !e->nb && !e->force_levels && !e->ch_declined && !e->force_v1 && !e->dc.hop_counter &&
           e->dc.max_list >= 3 && (e->dc.W > 1 || e->dc.H > 1);
 }
 
@@ -1060,12 +1131,18 @@ static int chain_setup(gnoc_engine* e)
    e->ncpx = W > 1 ? 2 * (e->ry1 - e->ry0) * (W - 1) : 0;
    e->ncpy = H > 1 ? 2 * (e->cx1 - e->cx0) * (H - 1) : 0;
    const uint32_t ncp = e->ncpx + e->ncpy;
-   const uint32_t nWx = e->ch_nw_run[0], nWy = e->ch_nw_run[1];
    GNOC_HIP(e, e->ch_cp.ensure((size_t) std::max<uint32_t>(ncp, 1) * sizeof(ChainPort)));
+   int rc = chain_tables(e);
+   if (rc) return rc;
    // window bounds and hand-off state: the X phase's, then the Y phase's
-   GNOC_HIP(e, e->ch_bt.ensure(((size_t) e->ncpx * (nWx + 1) + 3ull * e->ncpy * (nWy + 1) + 1) * 4));
-   GNOC_HIP(e, e->ch_ctr.ensure(256));   // [0, 1] dequeue heads; [32, 36) fill maxima, a line of their own
-   const size_t stb = ((size_t) e->ncpx * nWx + (size_t) e->ncpy * nWy + 1) * ch::SW * 8;
+   GNOC_HIP(e, e->ch_bt.ensure((e->ch_bt_words[0] + e->ch_bt_words[1] + 1) * 4));
+   GNOC_HIP(e, e->ch_ctr.ensure(256));   // [0, 1] dequeue heads
+   // per chain fill maxima, away from the flag word every hand-off poll reads (task-end
+   // atomics next to it slowed the polls by half)
+   const size_t nmx = 2 * (e->h_cw[0].size() + e->h_cw[1].size());
+   GNOC_HIP(e, e->ch_nmax.ensure(std::max<size_t>(nmx, 1) * 4));
+   GNOC_HIP(e, hipMemsetAsync(e->ch_nmax.p, 0, std::max<size_t>(nmx, 1) * 4, s));
+   const size_t stb = (e->ch_st_words[0] + e->ch_st_words[1] + ch::SW) * 8;
    const bool fresh = e->ch_st.bytes < stb;
    GNOC_HIP(e, e->ch_st.ensure(stb));
    // hand-off granules carry a 16-bit epoch: a new epoch per attempt, the buffer
@@ -1092,11 +1169,10 @@ static int chain_phase(gnoc_engine* e, int phase)
    if (!ncp) return GNOC_OK;
    const uint32_t len = phase ? c.H - 1 : c.W - 1;
    const uint32_t nl = phase ? 3u : 1u;
-   const uint32_t nW = e->ch_nw_run[phase];
-   const uint64_t D = e->ch_D_run[phase];
    const ChainPort* cp = e->ch_cp.as<ChainPort>() + (phase ? e->ncpx : 0);
-   uint32_t* bt = e->ch_bt.as<uint32_t>() + (phase ? (size_t) e->ncpx * (e->ch_nw_run[0] + 1) : 0);
-   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, cp, nl, nW, D, e->recs.as<Rec>(), bt);
+   uint32_t* bt = e->ch_bt.as<uint32_t>() + (phase ? e->ch_bt_words[0] : 0);
+   const ChainWin* cw = e->ch_cw.as<ChainWin>() + (phase ? e->h_cw[0].size() : 0);
+   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, cp, nl, len, cw, e->recs.as<Rec>(), bt);
    ChainArgs a;
    a.c = c;
    a.cp = cp;
@@ -1104,7 +1180,7 @@ static int chain_phase(gnoc_engine* e, int phase)
    a.recs = e->recs.as<Rec>();
    a.samp_t = e->samp_t.as<uint64_t>();
    a.samp_id = e->samp_id.as<uint32_t>();
-   a.st = e->ch_st.as<uint64_t>() + (phase ? (size_t) e->ncpx * e->ch_nw_run[0] * ch::SW : 0);
+   a.st = e->ch_st.as<uint64_t>() + (phase ? e->ch_st_words[0] : 0);
    a.port_sum = e->port_sum.as<unsigned long long>();
    a.port_cnt = e->port_cnt.as<unsigned long long>();
    a.port_flit = e->port_flit.as<unsigned long long>();
@@ -1113,13 +1189,12 @@ static int chain_phase(gnoc_engine* e, int phase)
    a.ctr = e->ch_ctr.as<unsigned>() + phase;
    a.nch = ncp / len;
    a.len = len;
-   a.nW = nW;
+   a.ntasks = (uint32_t) e->h_tasks[phase].size();
    a.pad2 = 0;
-   a.D = D;
-   a.cp0 = 0;   // st points at this phase's state
-   // away from the flag word every poll reads and from the dequeue heads: task-end
-   // atomics on those lines slowed the hand-off polls by half
-   a.nmax = e->ch_ctr.as<unsigned>() + 32 + 2 * phase;
+   a.cw = cw;
+   a.tasks = e->ch_tasks.as<uint32_t>() + (phase ? e->h_tasks[0].size() : 0);
+   a.cp0 = 0;
+   a.nmax = e->ch_nmax.as<unsigned>() + (phase ? 2 * e->h_cw[0].size() : 0);
    a.pad0 = 0;
    a.etag = (uint64_t) e->ch_epoch << 48;
    a.stamps = nullptr;
@@ -1129,13 +1204,13 @@ static int chain_phase(gnoc_engine* e, int phase)
    const char* stv = std::getenv("GNOC_STAMPS");
    if (stv && *stv == '1')
    {
-      const size_t nst = (size_t) a.nch * nW * len * 16;
+      const size_t nst = (size_t) a.ntasks * len * 16;
       DevBuf& sb = phase ? e->ch_stamps1 : e->ch_stamps0;
       GNOC_HIP(e, sb.ensure(nst * 8));
       GNOC_HIP(e, hipMemsetAsync(sb.p, 0, nst * 8, s));
       a.stamps = sb.as<uint64_t>();
    }
-   const uint32_t grid = (uint32_t) std::min<uint64_t>((uint64_t) e->ch_grid, (uint64_t) a.nch * nW);
+   const uint32_t grid = (uint32_t) std::min<uint64_t>((uint64_t) e->ch_grid, (uint64_t) a.ntasks);
    if (phase) GNOC_LAUNCH(e, KC_CHAIN, ch::k_chain<3>, dim3(grid), dim3(ch::T), 0, s, a);
    else GNOC_LAUNCH(e, KC_CHAIN, ch::k_chain<1>, dim3(grid), dim3(ch::T), 0, s, a);
    return GNOC_OK;
@@ -1354,7 +1429,8 @@ static int run_post(gnoc_engine* e, bool closed_form)
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 3, e->gtot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
       if (e->used_chain)
-         GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 14, e->ch_ctr.as<unsigned>() + 32, 16, hipMemcpyDeviceToHost, s));
+         GNOC_HIP(e, hipMemcpyAsync(e->h_nmax, e->ch_nmax.p, 8 * (e->h_cw[0].size() + e->h_cw[1].size()),
+                                    hipMemcpyDeviceToHost, s));
    }
    GNOC_HIP(e, hipStreamSynchronize(s));
    e->h_counters[0] = e->h_pinned[0];
@@ -1677,29 +1753,34 @@ int gnoc_run(gnoc_engine* e)
       if (e->nb && e->submitted) GNOC_HIP(e, hipMemsetAsync(e->d_bm1.p, 0, nv * 8, e->stream));
       e->force_v1 = forced;
       e->force_levels = 0;
-      for (int p = 0; p < 2; p++)
-      {
-         e->ch_D_run[p] = e->ch_D[p];
-         e->ch_nw_run[p] = e->ch_nw[p];
-      }
+      e->chD_run[0] = e->chD[0];
+      e->chD_run[1] = e->chD[1];
       if (e->bc_passes == 0) { e->n_retry = 0; e->n_fallback = 0; }
       int rc = run_once(e);
       // chain engine: a window that overflowed LDS reruns with windows half as long
       // (twice as many), up to 3 times; anything else it cannot take reruns on levels
-      while (rc == GNOC_CH_RETRY && e->n_retry < 3 && e->ch_D_run[0] >= 2 * CH_D_MIN && e->ch_D_run[1] >= 2 * CH_D_MIN &&
-             2ull * std::max(e->ch_nw_run[0], e->ch_nw_run[1]) <= CH_NW_MAX)
+      while (rc == GNOC_CH_RETRY && e->n_retry < 3)
       {
-         e->n_retry++;
-         const unsigned* nm = (const unsigned*) (e->h_pinned + 14);   // the failed attempt's maxima
-         const bool known = nm[0] == 0xFFFFFFFFu || nm[2] == 0xFFFFFFFFu;
+         // halve the windows of the chains that overflowed (all, when none is marked)
+         bool any = false, ok = true;
+         const unsigned* nm = e->h_nmax;
+         for (int p = 0; p < 2; p++, nm += 2 * e->chD_run[p - 1].size())
+            for (size_t c = 0; c < e->chD_run[p].size(); c++) any |= nm[2 * c] == 0xFFFFFFFFu;
+         nm = e->h_nmax;
          for (int p = 0; p < 2; p++)
          {
-            // halve the phase that overflowed (both when the kernel could not say)
-            if (known && nm[2 * p] != 0xFFFFFFFFu) continue;
-            if (!e->ch_D_cap[p] || e->ch_D_run[p] < e->ch_D_cap[p]) e->ch_D_cap[p] = e->ch_D_run[p];
-            e->ch_D_run[p] /= 2;
-            e->ch_nw_run[p] = windows_of(e->ch_D_run[p], e->h_tlast);
+            for (size_t c = 0; c < e->chD_run[p].size(); c++)
+            {
+               if (any && nm[2 * c] != 0xFFFFFFFFu) continue;
+               uint64_t& D = e->chD_run[p][c];
+               if (!e->chCap[p][c] || D < e->chCap[p][c]) e->chCap[p][c] = D;
+               if (D < 2 * CH_D_MIN || 2ull * windows_of(D, e->h_tlast) > CH_NW_MAX) ok = false;
+               D /= 2;
+            }
+            nm += 2 * e->chD_run[p].size();
          }
+         if (!ok) break;
+         e->n_retry++;
          rc = run_once(e);
       }
       if (rc == GNOC_CH_RETRY || rc == GNOC_CH_FALLBACK)
@@ -1713,15 +1794,12 @@ int gnoc_run(gnoc_engine* e)
       }
       else if (!rc && e->used_chain && e->n_retry)
       {
-         // the window size that fit: later runs of this batch start with it
-         for (int p = 0; p < 2; p++)
-         {
-            e->ch_D[p] = e->ch_D_run[p];
-            e->ch_nw[p] = e->ch_nw_run[p];
-         }
+         // the window sizes that fit: later runs of this batch start with them
+         e->chD[0] = e->chD_run[0];
+         e->chD[1] = e->chD_run[1];
       }
       else if (!rc && e->used_chain)
-         adapt_windows(e, (const unsigned*) (e->h_pinned + 14));   // the fill this run measured
+         adapt_windows(e);   // the fill this run measured
       if (rc == GNOC_V3_RETRY)
       {
          e->n_fallback++;
@@ -1935,11 +2013,8 @@ int gnoc_run_begin(gnoc_engine* e, void* send_buf)
    e->used_chain = 0;
    e->n_retry = 0;
    e->n_fallback = 0;
-   for (int p = 0; p < 2; p++)
-   {
-      e->ch_D_run[p] = e->ch_D[p];
-      e->ch_nw_run[p] = e->ch_nw[p];
-   }
+   e->chD_run[0] = e->chD[0];
+   e->chD_run[1] = e->chD[1];
    hipStream_t s = e->stream;
    rc = run_plan_v3(e);
    if (!rc && chain_usable(e))
@@ -2120,14 +2195,23 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
    out->engine_path = e->dc.contention ? (uint32_t) e->used_v3 : 2u;
    out->retries = e->n_retry;
    out->fallbacks = e->n_fallback;
-   out->windows = e->used_chain ? e->ch_nw_run[0] : 0u;
+   // per phase: the most windows and the longest window of any chain
+   uint32_t nwm[2] = { 0, 0 };
+   uint64_t dm[2] = { 0, 0 };
+   for (int p = 0; p < 2 && e->used_chain; p++)
+      for (const ChainWin& w : e->h_cw[p])
+      {
+         nwm[p] = std::max(nwm[p], w.nW);
+         dm[p] = std::max(dm[p], w.D);
+      }
+   out->windows = nwm[0];
    uint32_t sh = 0;
-   while (e->used_chain && sh < 63 && (2ull << sh) <= e->ch_D_run[0]) sh++;
+   while (sh < 63 && (2ull << sh) <= dm[0]) sh++;
    out->window_shift = e->used_chain ? sh : 0u;
-   out->windows_y = e->used_chain ? e->ch_nw_run[1] : 0u;
+   out->windows_y = nwm[1];
    out->abi_pad = 0;
-   out->window_ps_x = e->used_chain ? e->ch_D_run[0] : 0u;
-   out->window_ps_y = e->used_chain ? e->ch_D_run[1] : 0u;
+   out->window_ps_x = dm[0];
+   out->window_ps_y = dm[1];
    if (e->ran && e->dc.contention)
    {
       std::vector<uint64_t> m((size_t) e->dc.N * PORTS);
@@ -2179,8 +2263,10 @@ __attribute__((visibility("default"))) int gnoc_debug_chain_stamps(gnoc_engine* 
    const uint32_t len = phase ? e->dc.H - 1 : e->dc.W - 1;
    const uint32_t ncp = phase ? e->ncpy : e->ncpx;
    const uint32_t nch = len ? ncp / len : 0;
-   *count = (size_t) nch * e->ch_nw_run[phase] * len * 16;
-   if (geom) { geom[0] = nch; geom[1] = e->ch_nw_run[phase]; geom[2] = len; geom[3] = (uint32_t) (e->ch_D_run[phase] >> 10); }
+   (void) nch;
+   const size_t nt = e->h_tasks[phase].size();
+   *count = nt * len * 16;
+   if (geom) { geom[0] = 1; geom[1] = (uint32_t) nt; geom[2] = len; geom[3] = 0; }   // tasks in start-time order
    if (!out || !sb.p) return GNOC_OK;
    GNOC_HIP(e, hipMemcpy(out, sb.p, std::min(cap, *count) * 8, hipMemcpyDeviceToHost));
    return GNOC_OK;
