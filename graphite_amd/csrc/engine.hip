@@ -156,6 +156,7 @@ struct gnoc_engine
    // v4 chain engine (chain.hip): per phase (X, Y), per chain, windows of chD ps
    // (sized at submit, then from the fill each run measured per chain)
    bool ch_on = false;
+   uint64_t ch_key[4] = { 0, 0, 0, 0 };      // the shape of the batch the windows were sized for
    uint64_t h_tlast = 0;                     // last injection time of the batch (k_validate)
    std::vector<uint64_t> chD[2], chCap[2];   // window length; a length that overflowed LDS (0: none)
    std::vector<uint64_t> chD_run[2];         // the attempt in flight
@@ -584,6 +585,15 @@ static uint64_t clamp_window(const gnoc_engine* e, double d)
 }
 static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, uint64_t t_last)
 {
+   // A batch with the same shape as the last one (packets, busiest port, inserts,
+   // last injection) keeps the windows the runs of the last one settled on: the
+   // windows change only the schedule, never a result.
+   const uint64_t key[4] = { (uint64_t) e->n, port_max, ins_max, t_last };
+   const bool same = std::equal(key, key + 4, e->ch_key) && e->ch_on && !std::getenv("GNOC_WINDOW_SHIFT") &&
+                     !std::getenv("GNOC_WINDOW_PS") && !std::getenv("GNOC_WINDOW_PS_X") && !std::getenv("GNOC_WINDOW_PS_Y");
+   std::copy(key, key + 4, e->ch_key);
+   e->ch_declined = 0;
+   if (same) return;
    const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size (2^shift ps)
    const char* pv = std::getenv("GNOC_WINDOW_PS");      // test knob: force the window size (ps)
    const uint64_t span = t_last + 1;
