@@ -170,6 +170,7 @@ struct gnoc_engine
    int ch_grid = 0;
    int force_levels = 0;
    int ch_declined = 0;                     // this batch fell back from the chain engine: later runs skip it
+   int ch_resized = 0;                      // the windows were already changed during this (sharded) run
    int used_chain = 0;
    uint32_t ncpx = 0, ncpy = 0;
    DevBuf ch_cp, ch_bt, ch_st, ch_ctr, ch_stamps0, ch_stamps1;
@@ -643,6 +644,34 @@ static void adapt_windows(gnoc_engine* e)
       nm += 2 * e->chD[p].size();
    }
 }
+// After a run that overflowed LDS: halve the windows (in D) of the chains the
+// kernel marked (all chains when none is marked) and cap them at the length that
+// overflowed.  False when a halved window would leave the allowed range.
+static bool halve_overflowed(gnoc_engine* e, std::vector<uint64_t>* D)
+{
+   bool any = false, ok = true;
+   const unsigned* nm = e->h_nmax;
+   for (int p = 0; p < 2; p++)
+   {
+      for (size_t c = 0; c < D[p].size(); c++) any |= nm[2 * c] == 0xFFFFFFFFu;
+      nm += 2 * D[p].size();
+   }
+   nm = e->h_nmax;
+   for (int p = 0; p < 2; p++)
+   {
+      for (size_t c = 0; c < D[p].size(); c++)
+      {
+         if (any && nm[2 * c] != 0xFFFFFFFFu) continue;
+         uint64_t& d = D[p][c];
+         if (!e->chCap[p][c] || d < e->chCap[p][c]) e->chCap[p][c] = d;
+         if (d < 2 * CH_D_MIN || 2ull * windows_of(d, e->h_tlast) > CH_NW_MAX) ok = false;
+         else d /= 2;
+      }
+      nm += 2 * D[p].size();
+   }
+   return ok;
+}
+
 // The device tables of the attempt's windows (chD_run): per chain its windows,
 // state and bounds blocks; the tasks of each phase in window start-time order
 // (so a task's predecessor, same chain and window - 1, is always handed out
@@ -1772,24 +1801,7 @@ int gnoc_run(gnoc_engine* e)
       while (rc == GNOC_CH_RETRY && e->n_retry < 3)
       {
          // halve the windows of the chains that overflowed (all, when none is marked)
-         bool any = false, ok = true;
-         const unsigned* nm = e->h_nmax;
-         for (int p = 0; p < 2; p++, nm += 2 * e->chD_run[p - 1].size())
-            for (size_t c = 0; c < e->chD_run[p].size(); c++) any |= nm[2 * c] == 0xFFFFFFFFu;
-         nm = e->h_nmax;
-         for (int p = 0; p < 2; p++)
-         {
-            for (size_t c = 0; c < e->chD_run[p].size(); c++)
-            {
-               if (any && nm[2 * c] != 0xFFFFFFFFu) continue;
-               uint64_t& D = e->chD_run[p][c];
-               if (!e->chCap[p][c] || D < e->chCap[p][c]) e->chCap[p][c] = D;
-               if (D < 2 * CH_D_MIN || 2ull * windows_of(D, e->h_tlast) > CH_NW_MAX) ok = false;
-               D /= 2;
-            }
-            nm += 2 * e->chD_run[p].size();
-         }
-         if (!ok) break;
+         if (!halve_overflowed(e, e->chD_run)) break;
          e->n_retry++;
          rc = run_once(e);
       }
@@ -2043,6 +2055,14 @@ int gnoc_run_begin(gnoc_engine* e, void* send_buf)
       if (f4 & ch::F_ROUTE) return fail(e, GNOC_EHIP, "internal: chain route-count invariant violated");
       if (f4 & ch::F_ANY)
       {
+         if (f4 & ch::F_RETRY)
+         {
+            // windows of this rank's X chains overflowed: shorter ones at the next run
+            GNOC_HIP(e, hipMemcpy(e->h_nmax, e->ch_nmax.p, 8 * (e->h_cw[0].size() + e->h_cw[1].size()),
+                                  hipMemcpyDeviceToHost));
+            (void) halve_overflowed(e, e->chD);
+            e->ch_resized = 1;
+         }
          e->n_fallback++;
          GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, 0, 4, s));
          const uint32_t np = e->dc.N * PORTS;
@@ -2112,6 +2132,11 @@ int gnoc_run_finish(gnoc_engine* e, const void* recv_buf)
       rc = chain_phase(e, 1);
       if (!rc) rc = run_levels_v3(e, L - 1, L);
       if (!rc) rc = run_post(e, false);
+      // the windows of the next run: from this run's measured fill, or shorter
+      // for the chains that overflowed (results never depend on them)
+      if (!rc && !e->ch_resized) adapt_windows(e);
+      if (rc == GNOC_CH_RETRY) (void) halve_overflowed(e, e->chD);
+      e->ch_resized = 0;
       if (rc != GNOC_CH_RETRY && rc != GNOC_CH_FALLBACK) return rc;
       // the Y chains declined: Y and SELF levels on k_level (fresh look-back state)
       e->n_fallback++;
