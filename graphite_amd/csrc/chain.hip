@@ -1046,16 +1046,24 @@ __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict_
       for (uint32_t v = threadIdx.x; v <= nW; v += blockDim.x) b[v] = 0;
       return;
    }
-   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+   // t / D by a double reciprocal and one correction step (t < 2^50, D >= 1024:
+   // the estimate is off by at most one); the previous record's window comes from
+   // the neighbouring lane
+   const double inv = 1.0 / (double) D;
+   auto win = [&](uint64_t t) -> uint64_t {
+      uint64_t q = (uint64_t) ((double) t * inv);
+      if (q * D > t) q--;
+      else if ((q + 1) * D <= t) q++;
+      return q < wl ? q : wl;
+   };
+   for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x)
    {
-      uint64_t wi = recs[base + i].t / D;
-      wi = wi < wl ? wi : wl;
-      int64_t wp = -1;
-      if (i)
-      {
-         uint64_t q = recs[base + i - 1].t / D;
-         wp = (int64_t) (q < wl ? q : wl);
-      }
+      const uint32_t i = i0 + threadIdx.x;
+      const uint64_t wi = i < n ? win(recs[base + i].t) : wl;
+      uint64_t wprev = (uint64_t) __shfl_up((long long) wi, 1);
+      if ((threadIdx.x & 63) == 0) wprev = i ? win(recs[base + i - 1].t) : 0;
+      if (i >= n) continue;
+      const int64_t wp = i ? (int64_t) wprev : -1;
       for (int64_t v = wp + 1; v <= (int64_t) wi; v++) b[v] = i;
       if (i == n - 1)
          for (uint64_t v = wi + 1; v <= nW; v++) b[v] = n;

@@ -87,7 +87,12 @@ struct DevCfg
    uint64_t* bc_mcur;
    uint64_t* bc_fin;        // [b * N + tile] receipt time (ps)
    uint64_t npk;            // packets of the batch: a SELF port never writes final_ps beyond it
+   // A sharded rank's partitioned trace (gnoc_submit): records carry global packet
+   // ids (their ties order every rank alike); the rank's per-packet arrays are
+   // indexed by its own packet index, g2l[global id].  nullptr: ids are indices.
+   const uint32_t* g2l;
 };
+__device__ __forceinline__ uint64_t pk_index(const DevCfg& c, uint32_t id) { return c.g2l ? c.g2l[id] : id; }
 
 // Latency::toPicosec, common/misc/time_types.h:81-86.  F1: f == 1.0 exactly,
 // where the double expression equals 1000*c for every c < 2^43.

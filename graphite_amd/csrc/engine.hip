@@ -123,6 +123,15 @@ struct gnoc_engine
    double last_ms = 0.0;
    uint64_t* h_pinned = nullptr;
 
+   // a sharded rank's partitioned trace (gnoc_submit): only the packets of its
+   // row band (sources) or column band (destinations), in trace order; gid maps
+   // them to their global index, g2l back
+   bool part = false;
+   size_t n_glob = 0;
+   uint64_t h_glob_hops = 0, h_glob_routed = 0;
+   std::vector<uint32_t> h_gid;
+   DevBuf d_gid, d_g2l;
+
    // one mesh over several GPUs (gnoc_shard): this rank's row band (X phase)
    // and column band (Y phase), the turn-record exchange layout per peer
    int rank = 0, nranks = 1;
@@ -398,6 +407,7 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    d.hop_counter = 0;
    d.pt_rl = nullptr;
    d.pt_fw = nullptr;
+   d.g2l = nullptr;
    build_static_levels(e);
 
    hipError_t he = hipSetDevice(c.device);
@@ -790,7 +800,7 @@ static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t
       if (v.bad[q] != ~0ull && (k == VB_KINDS || v.bad[q] < v.bad[k])) k = q;
    if (k != VB_KINDS)
    {
-      const std::string at = std::to_string(v.bad[k]);
+      const std::string at = std::to_string(e->part && v.bad[k] < e->h_gid.size() ? (uint64_t) e->h_gid[v.bad[k]] : v.bad[k]);
       switch (k)
       {
          case VB_TILE: return fail(e, GNOC_ETRACE, "tile id out of range at packet " + at);
@@ -887,12 +897,85 @@ static int upload_broadcasts(gnoc_engine* e)
    return GNOC_OK;
 }
 
-int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
+__global__ void k_g2l(uint64_t n, const uint32_t* __restrict__ gid, uint32_t* __restrict__ g2l)
 {
-   if (!e || !pk) return GNOC_EINVAL;
-   if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return fail(e, GNOC_EINVAL, "null trace array");
+   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+      g2l[gid[i]] = (uint32_t) i;
+}
+
+// A sharded rank keeps only the packets it touches: sources in its row band
+// (injection, X phase, turn) or destinations in its column band (Y phase, SELF,
+// the results it delivers).  The contract checks a rank could miss on its subset
+// (tile range, order) run here over the whole trace; the totals the summary
+// reports are the whole mesh's.  Row / column band prep (W, H <= 64) only.
+static int partition_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n, gnoc_packets* sub,
+                           std::vector<uint64_t>& inj, std::vector<uint32_t>& src, std::vector<uint32_t>& dst,
+                           std::vector<uint32_t>& bits, std::vector<uint32_t>& flags)
+{
+   const uint32_t N = e->dc.N, W = e->dc.W;
+   uint64_t hops = 0, routed = 0;
+   e->h_gid.clear();
+   for (size_t i = 0; i < n; i++)
+   {
+      const uint32_t s = pk->src[i], d = pk->dst[i], fl = pk->flags ? pk->flags[i] : 0u;
+      if (fl & GNOC_PKT_BROADCAST) return fail(e, GNOC_EUNSUPPORTED, "broadcast packets on a sharded or sweep engine");
+      if (s >= N || d >= N) return fail(e, GNOC_ETRACE, "tile id out of range at packet " + std::to_string(i));
+      if (i && pk->inject_ps[i] < pk->inject_ps[i - 1])
+         return fail(e, GNOC_ETRACE, "trace not ordered by inject_ps at packet " + std::to_string(i));
+      const uint32_t sx = s % W, sy = s / W, dx = d % W, dy = d / W;
+      if (s != d && !(fl & GNOC_PKT_UNMODELED))
+      {
+         routed++;
+         hops += (sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1;
+      }
+      if ((sy >= e->ry0 && sy < e->ry1) || (dx >= e->cx0 && dx < e->cx1)) e->h_gid.push_back((uint32_t) i);
+   }
+   const size_t m = e->h_gid.size();
+   inj.resize(m);
+   src.resize(m);
+   dst.resize(m);
+   bits.resize(m);
+   flags.resize(m);
+   for (size_t k = 0; k < m; k++)
+   {
+      const size_t i = e->h_gid[k];
+      inj[k] = pk->inject_ps[i];
+      src[k] = pk->src[i];
+      dst[k] = pk->dst[i];
+      bits[k] = pk->bits[i];
+      flags[k] = pk->flags ? pk->flags[i] : 0u;
+   }
+   sub->inject_ps = inj.data();
+   sub->src = src.data();
+   sub->dst = dst.data();
+   sub->bits = bits.data();
+   sub->flags = flags.data();
+   e->h_glob_hops = hops;
+   e->h_glob_routed = routed;
+   return GNOC_OK;
+}
+
+int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk_in, size_t n)
+{
+   if (!e || !pk_in) return GNOC_EINVAL;
+   if (n && (!pk_in->inject_ps || !pk_in->src || !pk_in->dst || !pk_in->bits)) return fail(e, GNOC_EINVAL, "null trace array");
    if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
    e->submitted = false;
+   const gnoc_packets* pk = pk_in;
+   gnoc_packets sub{};
+   std::vector<uint64_t> l_inj;
+   std::vector<uint32_t> l_src, l_dst, l_bits, l_flags;
+   e->part = e->nranks > 1 && e->dc.W <= 64 && e->dc.H <= 64 && e->npoints == 1 && !e->dc.hop_counter && e->dc.contention &&
+             !std::getenv("GNOC_NO_PARTITION");
+   e->n_glob = n;
+   e->dc.g2l = nullptr;
+   if (e->part)
+   {
+      const int prc = partition_trace(e, pk_in, n, &sub, l_inj, l_src, l_dst, l_bits, l_flags);
+      if (prc) return prc;
+      pk = &sub;
+      n = e->h_gid.size();
+   }
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    GNOC_HIP(e, e->t_inj.ensure(n * 8));
    GNOC_HIP(e, e->t_src.ensure(n * 4));
@@ -916,7 +999,20 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    e->d_bits = e->t_bits.as<uint32_t>();
    e->d_flags = e->t_flags.as<uint32_t>();
    e->n = n;
-   e->dc.npk = n;
+   e->dc.npk = e->part ? e->n_glob : n;
+   if (e->part)
+   {
+      GNOC_HIP(e, e->d_gid.ensure(n * 4 + 4));
+      GNOC_HIP(e, e->d_g2l.ensure(e->n_glob * 4 + 4));
+      if (n)
+      {
+         GNOC_HIP(e, hipMemcpyAsync(e->d_gid.p, e->h_gid.data(), n * 4, hipMemcpyHostToDevice, e->stream));
+         hipLaunchKernelGGL(k_g2l, dim3((uint32_t) std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0, e->stream,
+                            (uint64_t) n, e->d_gid.as<uint32_t>(), e->d_g2l.as<uint32_t>());
+         GNOC_HIP(e, hipGetLastError());
+      }
+      e->dc.g2l = e->d_g2l.as<uint32_t>();
+   }
    uint64_t records = 0, nbc = 0;
    int rc = device_validate(e, n, &records, &nbc);   // (its sync also ends the copies)
    if (rc) return rc;
@@ -938,6 +1034,12 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk, size_t n)
 
 int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
 {
+   if (e)
+   {
+      e->part = false;   // a device trace is used as is (every rank reads all of it)
+      e->n_glob = n;
+      e->dc.g2l = nullptr;
+   }
    if (!e || !pk) return GNOC_EINVAL;
    if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return fail(e, GNOC_EINVAL, "null trace array");
    if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
@@ -1374,7 +1476,7 @@ static int run_prep(gnoc_engine* e, bool* done)
    GNOC_LAUNCH(e, KC_SCATTER, (k_scatter4<NWV, SP>), dim3(nch), dim3(64 * NWV), (size_t) NWV * S * 4 + (SP ? NWV * 2048 : 0), \
                s, (uint64_t) n, pch, N, s0, S, sbits, e->d_src, e->routed.as<uint8_t>(), e->d_inj,                          \
                e->aux.as<uint32_t>(), e->hist.as<uint32_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(),                  \
-               e->samp_id.as<uint32_t>())
+               e->samp_id.as<uint32_t>(), e->part ? (const uint32_t*) e->d_gid.as<uint32_t>() : nullptr)
       if (band_prep && S <= 1024) GNOC_SCATTER(8, true);
       else if (band_prep && S <= 2048) GNOC_SCATTER(4, true);
       else if (band_prep) GNOC_SCATTER(2, true);
@@ -2160,15 +2262,33 @@ int gnoc_get_packet_results(gnoc_engine* e, uint64_t* final_ps, uint64_t* zero_l
 {
    if (!e) return GNOC_EINVAL;
    if (!e->ran) return fail(e, GNOC_ESTATE, "no results: call gnoc_run first");
-   if (n != e->n) return fail(e, GNOC_EINVAL, "result array length != submitted packet count");
+   if (n != (e->part ? e->n_glob : e->n)) return fail(e, GNOC_EINVAL, "result array length != submitted packet count");
    if (!n) return GNOC_OK;
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
-   if (e->nranks > 1)
+   if (e->nranks > 1 && e->n)
    {
-      hipLaunchKernelGGL(k_mask_unowned, dim3((uint32_t) std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0, e->stream,
-                         (uint64_t) n, e->aux.as<uint32_t>(), e->cx0, e->cx1, e->final_ps.as<uint64_t>(),
+      hipLaunchKernelGGL(k_mask_unowned, dim3((uint32_t) std::min<size_t>((e->n + 255) / 256, 8192)), dim3(256), 0,
+                         e->stream, (uint64_t) e->n, e->aux.as<uint32_t>(), e->cx0, e->cx1, e->final_ps.as<uint64_t>(),
                          e->zl.as<uint64_t>(), e->cont.as<uint64_t>());
       GNOC_HIP(e, hipGetLastError());
+   }
+   if (e->part)
+   {
+      // this rank's packets back to their places in the whole trace; 0 elsewhere
+      const size_t m = e->n;
+      std::vector<uint64_t> tmp(m);
+      uint64_t* outs[3] = { final_ps, zero_load_ps, contention_ps };
+      const DevBuf* srcs[3] = { &e->final_ps, &e->zl, &e->cont };
+      for (int k = 0; k < 3; k++)
+      {
+         if (!outs[k]) continue;
+         std::memset(outs[k], 0, n * 8);
+         if (!m) continue;
+         GNOC_HIP(e, hipMemcpyAsync(tmp.data(), srcs[k]->p, m * 8, hipMemcpyDeviceToHost, e->stream));
+         GNOC_HIP(e, hipStreamSynchronize(e->stream));
+         for (size_t i = 0; i < m; i++) outs[k][e->h_gid[i]] = tmp[i];
+      }
+      return GNOC_OK;
    }
    if (final_ps) GNOC_HIP(e, hipMemcpyAsync(final_ps, e->final_ps.p, n * 8, hipMemcpyDeviceToHost, e->stream));
    if (zero_load_ps) GNOC_HIP(e, hipMemcpyAsync(zero_load_ps, e->zl.p, n * 8, hipMemcpyDeviceToHost, e->stream));
@@ -2221,9 +2341,10 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
 {
    if (!e || !out) return GNOC_EINVAL;
    std::memset(out, 0, sizeof(*out));
-   out->packets = e->n;
-   out->mesh_hops = e->h_counters[0];
-   out->routed_packets = e->h_counters[1];
+   out->packets = e->part ? e->n_glob : e->n;
+   // a partitioned rank reports the whole mesh's totals (as an unpartitioned one does)
+   out->mesh_hops = e->part ? e->h_glob_hops : e->h_counters[0];
+   out->routed_packets = e->part ? e->h_glob_routed : e->h_counters[1];
    out->records = e->h_records;
    out->levels = e->h_levels;
    out->last_run_ms = e->last_ms;
@@ -2311,6 +2432,7 @@ int gnoc_device_final_ps(gnoc_engine* e, void** dptr)
 {
    if (!e || !dptr) return GNOC_EINVAL;
    if (!e->ran) return fail(e, GNOC_ESTATE, "no results: call gnoc_run first");
+   if (e->part) return fail(e, GNOC_EUNSUPPORTED, "a sharded rank holds only its own packets' results (gnoc_get_packet_results)");
    *dptr = e->final_ps.p;
    return GNOC_OK;
 }

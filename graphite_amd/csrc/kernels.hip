@@ -574,7 +574,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
             {
                const uint64_t fin = tn + ps_of<F1>(aux_F(ax), c.f);
                if (bcr) c.bc_fin[v] = fin;
-               else final_ps[id] = fin;
+               else final_ps[pk_index(c, id)] = fin;
                continue;
             }
             Rec o;

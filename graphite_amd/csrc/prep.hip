@@ -495,8 +495,10 @@ __global__ __launch_bounds__(512) void k_scatter4(uint64_t n, uint32_t pch, uint
                                                   const uint32_t* __restrict__ src, const uint8_t* __restrict__ routed,
                                                   const uint64_t* __restrict__ inj, const uint32_t* __restrict__ aux,
                                                   const uint32_t* __restrict__ offs, Rec* __restrict__ recs,
-                                                  uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id)
+                                                  uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id,
+                                                  const uint32_t* __restrict__ gid)
 {
+   // gid: a sharded rank's partitioned trace -- records carry global packet ids
    extern __shared__ uint32_t h4[];   // [NW][S] per-wave counts of sources s0 .. s0+S-1 -> running ranks
    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
    for (uint32_t k = threadIdx.x; k < NW * S; k += 64 * NW) h4[k] = 0;
@@ -566,7 +568,7 @@ __global__ __launch_bounds__(512) void k_scatter4(uint64_t n, uint32_t pch, uint
                const uint64_t pos = rank;
                Rec r;
                r.t = inj[i];
-               r.id = (uint32_t) i;
+               r.id = gid ? gid[i] : (uint32_t) i;
                r.aux = aux[i];
                recs[pos] = r;
                if ((pos & 63) == 0)
@@ -610,7 +612,7 @@ __global__ __launch_bounds__(512) void k_scatter4(uint64_t n, uint32_t pch, uint
          const uint64_t pos = rank;
          Rec r;
          r.t = t;
-         r.id = (uint32_t) id;
+         r.id = gid ? gid[id] : (uint32_t) id;
          r.aux = a;
          recs[pos] = r;
          if ((pos & 63) == 0)
@@ -953,15 +955,20 @@ __global__ __launch_bounds__(1024) void k_scan_slots(uint32_t N, const uint32_t*
 }
 
 template __global__ void k_scatter4<4, false>(uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
-                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
+                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*,
+                                       const uint32_t*);
 template __global__ void k_scatter4<8, false>(uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
-                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
+                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*,
+                                       const uint32_t*);
 template __global__ void k_scatter4<4, true>(uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
-                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
+                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*,
+                                       const uint32_t*);
 template __global__ void k_scatter4<8, true>(uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
-                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
+                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*,
+                                       const uint32_t*);
 template __global__ void k_scatter4<2, true>(uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, int, const uint32_t*, const uint8_t*,
-                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*);
+                                       const uint64_t*, const uint32_t*, const uint32_t*, Rec*, uint64_t*, uint32_t*,
+                                       const uint32_t*);
 
 // Multi-block variant for large meshes (sweeps): the same slot order, in
 // SCAN_SPAN-entry spans.  Pass 1: span sums; pass 2 (one block): span offsets;
