@@ -161,6 +161,7 @@ struct gnoc_engine
    int ma_type = 0;
    uint32_t ma_window = 1;
    DevBuf ma_t, ma_key, ma_val, ma_key2, ma_val2, ma_lo, ma_hi, ma_d, ma_ref, ma_agg, ma_m, ma_bcnt, ma_hist;
+   DevBuf sc_key, sc_rec, sc_hist;          // injection slots of large meshes (radix sort by source)
 
    // v4 chain engine (chain.hip): per phase (X, Y), per chain, windows of chD ps
    // (sized at submit, then from the fill each run measured per chain)
@@ -1461,7 +1462,7 @@ static int run_prep(gnoc_engine* e, bool* done)
                e->tot.as<uint32_t>(), pr0 * W, pr1 * W);
    GNOC_LAUNCH(e, KC_INJ_BASE, k_inj_base, dim3(1), dim3(1024), 0, s, N, e->tot.as<uint32_t>(), e->slot_cnt.as<uint32_t>(),
                e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>());
-   if (ngb)
+   if (ngb && N <= SC4_MAXN)   // per-chunk offsets for the scatter kernels (the sort path needs none)
       GNOC_LAUNCH(e, KC_SRC_OFFS, k_src_offs, dim3(ngb, nseg), dim3(256), 0, s, N, nch, nseg, e->hist.as<uint32_t>(),
                   e->srcseg.as<uint32_t>(), e->slot_base.as<uint64_t>(), pr0 * W, pr1 * W);
    if (n && N <= SC4_MAXN)
@@ -1485,9 +1486,40 @@ static int run_prep(gnoc_engine* e, bool* done)
 #undef GNOC_SCATTER
    }
    else if (n)
-      GNOC_LAUNCH(e, KC_SCATTER, k_scatter, dim3(nch), dim3(64), N * 4, s, (uint64_t) n, pch, N, nbits, e->d_src,
-                  e->routed.as<uint8_t>(), e->d_inj, e->aux.as<uint32_t>(), e->hist.as<uint32_t>(), e->recs.as<Rec>(),
+   {
+      // large meshes (sweeps): the stable group-by-source as a radix sort of
+      // (source, record) pairs, then a coalesced copy into the slots (serial.hip)
+      const uint32_t nbk = (uint32_t) ((n + RS_CH - 1) / RS_CH);
+      GNOC_HIP(e, e->sc_key.ensure(2 * n * 4 + 8));
+      GNOC_HIP(e, e->sc_rec.ensure(2 * n * sizeof(Rec) + 16));
+      GNOC_HIP(e, e->sc_hist.ensure(((size_t) RS_BINS * nbk + RS_BINS + N + 8) * 4));
+      uint32_t* kA = e->sc_key.as<uint32_t>();
+      uint32_t* kB = kA + n;
+      Rec* rA = e->sc_rec.as<Rec>();
+      Rec* rB = rA + n;
+      uint32_t* hist = e->sc_hist.as<uint32_t>();
+      uint32_t* dtot = hist + (size_t) RS_BINS * nbk;
+      uint32_t* first = dtot + RS_BINS;
+      uint32_t* mcnt = first + N;
+      const uint32_t grid = (uint32_t) std::min<size_t>((n + 255) / 256, 8192);
+      GNOC_LAUNCH(e, KC_SCATTER, k_set_u32, dim3(1), dim3(1), 0, s, mcnt, (uint32_t) n);
+      GNOC_LAUNCH(e, KC_SCATTER, k_src_keys, dim3(grid), dim3(256), 0, s, (uint64_t) n, N, e->d_src, e->routed.as<uint8_t>(),
+                  e->d_inj, e->aux.as<uint32_t>(), e->part ? (const uint32_t*) e->d_gid.as<uint32_t>() : nullptr, kA, rA);
+      for (uint32_t sh = 0; (N >> sh) != 0; sh += 8)   // keys 0 .. N
+      {
+         GNOC_LAUNCH(e, KC_SCATTER, k_rs_hist<uint32_t>, dim3(nbk), dim3(RS_T), 0, s, (const uint32_t*) mcnt, sh, nbk,
+                     (const uint32_t*) kA, hist);
+         GNOC_LAUNCH(e, KC_SCATTER, k_rs_offsets, dim3(RS_BINS), dim3(RS_T), 0, s, (const uint32_t*) mcnt, nbk, hist, dtot);
+         GNOC_LAUNCH(e, KC_SCATTER, (k_rs_scatter<uint32_t, Rec>), dim3(nbk), dim3(RS_T), 0, s, (const uint32_t*) mcnt, sh,
+                     nbk, (const uint32_t*) kA, (const Rec*) rA, (const uint32_t*) hist, (const uint32_t*) dtot, kB, rB);
+         std::swap(kA, kB);
+         std::swap(rA, rB);
+      }
+      GNOC_LAUNCH(e, KC_SCATTER, k_src_first, dim3(grid), dim3(256), 0, s, (uint64_t) n, N, (const uint32_t*) kA, first);
+      GNOC_LAUNCH(e, KC_SCATTER, k_src_place, dim3(grid), dim3(256), 0, s, (uint64_t) n, N, (const uint32_t*) kA,
+                  (const Rec*) rA, (const uint32_t*) first, (const uint64_t*) e->slot_base.as<uint64_t>(), e->recs.as<Rec>(),
                   e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>());
+   }
    GNOC_LAUNCH(e, KC_ROW_HIST, k_row_hist, dim3(G, nR), dim3(256), rh_lds, s, c, G, e->recs.as<Rec>(),
                e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->Hs.as<uint32_t>(), e->Pp.as<uint32_t>(), pp_lds,
                pr0);
@@ -1729,10 +1761,10 @@ static int run_ma_tb(gnoc_engine* e, uint32_t tb, bool* wider)
          uint32_t* vB = e->ma_val2.as<uint32_t>();
          for (uint32_t sh = 0; sh < end_bit; sh += 8)
          {
-            hipLaunchKernelGGL(k_rs_hist, dim3(nbk), dim3(RS_T), 0, s, (const uint32_t*) mcnt, sh, nbk, (const uint64_t*) kA,
-                               hist);
+            hipLaunchKernelGGL(k_rs_hist<uint64_t>, dim3(nbk), dim3(RS_T), 0, s, (const uint32_t*) mcnt, sh, nbk,
+                               (const uint64_t*) kA, hist);
             hipLaunchKernelGGL(k_rs_offsets, dim3(RS_BINS), dim3(RS_T), 0, s, (const uint32_t*) mcnt, nbk, hist, dtot);
-            hipLaunchKernelGGL(k_rs_scatter, dim3(nbk), dim3(RS_T), 0, s, (const uint32_t*) mcnt, sh, nbk,
+            hipLaunchKernelGGL((k_rs_scatter<uint64_t, uint32_t>), dim3(nbk), dim3(RS_T), 0, s, (const uint32_t*) mcnt, sh, nbk,
                                (const uint64_t*) kA, (const uint32_t*) vA, (const uint32_t*) hist, (const uint32_t*) dtot,
                                kB, vB);
             std::swap(kA, kB);

@@ -211,8 +211,9 @@ __global__ __launch_bounds__(RS_T) void k_ma_keys(uint64_t n, uint32_t W, uint32
 
 // Radix pass, 1: per-block digit histograms, digit-major hist[d * nbs + b]
 // (nbs = the host's bound on the block count).
+template <typename K>
 __global__ __launch_bounds__(RS_T) void k_rs_hist(const uint32_t* __restrict__ mcount, uint32_t shift, uint32_t nbs,
-                                                  const uint64_t* __restrict__ key, uint32_t* __restrict__ hist)
+                                                  const K* __restrict__ key, uint32_t* __restrict__ hist)
 {
    __shared__ uint32_t h[RS_BINS];
    const uint32_t m = *mcount;
@@ -270,10 +271,11 @@ __global__ __launch_bounds__(RS_T) void k_rs_offsets(const uint32_t* __restrict_
 
 // Radix pass, 3: stable scatter.  Sub-round q takes entries [q 256, (q + 1) 256) of
 // the block in thread order; a wave matches its 64 digits with 8 ballots.
+template <typename K, typename V>
 __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict__ mcount, uint32_t shift, uint32_t nbs,
-                                                     const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                     const K* __restrict__ kin, const V* __restrict__ vin,
                                                      const uint32_t* __restrict__ offs, const uint32_t* __restrict__ dtot,
-                                                     uint64_t* __restrict__ kout, uint32_t* __restrict__ vout)
+                                                     K* __restrict__ kout, V* __restrict__ vout)
 {
    __shared__ uint32_t run[RS_BINS];
    __shared__ uint32_t wcnt[RS_T / 64][RS_BINS];
@@ -288,8 +290,9 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
    {
       const uint32_t i = blockIdx.x * RS_CH + q * RS_T + t;
       const bool v = i < m;
-      const uint64_t k = v ? kin[i] : 0ull;
-      const uint32_t id = v ? vin[i] : 0u;
+      const K k = v ? kin[i] : K(0);
+      V id{};
+      if (v) id = vin[i];
       const uint32_t dg = (uint32_t) (k >> shift) & 0xFFu;
       uint64_t peers = __ballot(v);
 #pragma unroll
@@ -316,6 +319,60 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
          wcnt[w][dg] = 0;
       }
       __syncthreads();
+   }
+}
+
+// ---- injection slots of large meshes (N > 4096: sweeps) ----------------------
+// The stable group-by-source of the trace as a 2-pass LSD radix sort of
+// (source, record) pairs -- the per-chunk source counters of the scatter kernels
+// need N words of LDS per wave, which a 16,384-tile sweep mesh cannot give them.
+// Packets this rank does not place get the key N and sort last.
+__global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
+
+__global__ void k_src_keys(uint64_t n, uint32_t N, const uint32_t* __restrict__ src, const uint8_t* __restrict__ routed,
+                           const uint64_t* __restrict__ inj, const uint32_t* __restrict__ aux,
+                           const uint32_t* __restrict__ gid, uint32_t* __restrict__ key, Rec* __restrict__ rec)
+{
+   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const bool placed = (routed[i] & 2) != 0;
+      key[i] = placed ? src[i] : N;
+      Rec r;
+      r.t = inj[i];
+      r.id = gid ? gid[i] : (uint32_t) i;
+      r.aux = aux[i];
+      rec[i] = r;
+   }
+}
+
+// First sorted position of every present source.
+__global__ void k_src_first(uint64_t m, uint32_t N, const uint32_t* __restrict__ key, uint32_t* __restrict__ first)
+{
+   for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < m; j += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const uint32_t s = key[j];
+      if (s < N && (j == 0 || key[j - 1] != s)) first[s] = (uint32_t) j;
+   }
+}
+
+// The sorted records into their injection slots (coalesced: a source's records
+// are consecutive in both), with the 1-in-64 key samples.
+__global__ void k_src_place(uint64_t m, uint32_t N, const uint32_t* __restrict__ key, const Rec* __restrict__ rec,
+                            const uint32_t* __restrict__ first, const uint64_t* __restrict__ slot_base,
+                            Rec* __restrict__ recs, uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id)
+{
+   for (uint64_t j = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; j < m; j += (uint64_t) gridDim.x * blockDim.x)
+   {
+      const uint32_t s = key[j];
+      if (s >= N) continue;
+      const uint64_t pos = slot_base[slot_of(s, P_INJ, IN_LOCAL)] + (j - first[s]);
+      const Rec r = rec[j];
+      recs[pos] = r;
+      if ((pos & 63) == 0)
+      {
+         samp_t[pos >> 6] = r.t;
+         samp_id[pos >> 6] = r.id;
+      }
    }
 }
 
