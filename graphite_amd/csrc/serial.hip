@@ -269,31 +269,62 @@ __global__ __launch_bounds__(RS_T) void k_rs_offsets(const uint32_t* __restrict_
    if (threadIdx.x == 0) dtot[blockIdx.x] = carry;
 }
 
-// Radix pass, 3: stable scatter.  Sub-round q takes entries [q 256, (q + 1) 256) of
-// the block in thread order; a wave matches its 64 digits with 8 ballots.
+// Radix pass, 3: stable scatter.  Wave w of the block takes the block's entries
+// [w 512, (w + 1) 512) in 8 sub-rounds of 64: first its per-digit counts (LDS
+// atomics), then, after one block-wide prefix of the counts over the waves, its
+// placement with wave-local state only -- a lane's rank among the lanes of the
+// same digit from 8 ballots, its position from the wave's running counter of
+// that digit (read by every lane before the leader advances it: a wave's LDS
+// operations execute in program order).  Two block barriers per 2,048 entries.
 template <typename K, typename V>
 __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict__ mcount, uint32_t shift, uint32_t nbs,
                                                      const K* __restrict__ kin, const V* __restrict__ vin,
                                                      const uint32_t* __restrict__ offs, const uint32_t* __restrict__ dtot,
                                                      K* __restrict__ kout, V* __restrict__ vout)
 {
-   __shared__ uint32_t run[RS_BINS];
-   __shared__ uint32_t wcnt[RS_T / 64][RS_BINS];
+   constexpr uint32_t NW = RS_T / 64, WCH = RS_CH / NW;   // entries per wave
+   __shared__ uint32_t wb[NW][RS_BINS];
    const uint32_t m = *mcount;
    if ((uint64_t) blockIdx.x * RS_CH >= m) return;
-   const uint32_t t = threadIdx.x, w = t >> 6;
-   uint32_t tot;
-   run[t] = rs_block_exclusive(dtot[t], tot) + offs[(size_t) t * nbs + blockIdx.x];   // digit base + this block's offset
-   for (uint32_t u = 0; u < RS_T / 64; u++) wcnt[u][t] = 0;
+   const uint32_t t = threadIdx.x, w = t >> 6, lane = t & 63;
+   for (uint32_t u = 0; u < NW; u++) wb[u][t] = 0;
    __syncthreads();
+   const uint32_t i0 = blockIdx.x * RS_CH + w * WCH;
+   K kr[RS_PER];
+   V vr[RS_PER];
+#pragma unroll
    for (uint32_t q = 0; q < RS_PER; q++)
    {
-      const uint32_t i = blockIdx.x * RS_CH + q * RS_T + t;
+      const uint32_t i = i0 + q * 64 + lane;
+      kr[q] = K(0);
+      vr[q] = V{};
+      if (i < m)
+      {
+         kr[q] = kin[i];
+         vr[q] = vin[i];
+         atomicAdd(&wb[w][(uint32_t) (kr[q] >> shift) & 0xFFu], 1u);
+      }
+   }
+   __syncthreads();
+   {
+      // thread t = digit t: the block's base for it, then each wave's start
+      uint32_t tot;
+      uint32_t run = rs_block_exclusive(dtot[t], tot) + offs[(size_t) t * nbs + blockIdx.x];
+#pragma unroll
+      for (uint32_t u = 0; u < NW; u++)
+      {
+         const uint32_t c = wb[u][t];
+         wb[u][t] = run;
+         run += c;
+      }
+   }
+   __syncthreads();
+#pragma unroll
+   for (uint32_t q = 0; q < RS_PER; q++)
+   {
+      const uint32_t i = i0 + q * 64 + lane;
       const bool v = i < m;
-      const K k = v ? kin[i] : K(0);
-      V id{};
-      if (v) id = vin[i];
-      const uint32_t dg = (uint32_t) (k >> shift) & 0xFFu;
+      const uint32_t dg = (uint32_t) (kr[q] >> shift) & 0xFFu;
       uint64_t peers = __ballot(v);
 #pragma unroll
       for (int b = 0; b < 8; b++)
@@ -302,23 +333,15 @@ __global__ __launch_bounds__(RS_T) void k_rs_scatter(const uint32_t* __restrict_
          peers &= ((dg >> b) & 1u) ? bb : ~bb;
       }
       const uint32_t rank = (uint32_t) __popcll(peers & lanes_below());
-      const bool leader = v && rank == 0;
-      if (leader) wcnt[w][dg] = (uint32_t) __popcll(peers);
-      __syncthreads();
+      const uint32_t pos = v ? wb[w][dg] + rank : 0u;
+      __builtin_amdgcn_wave_barrier();
+      if (v && rank == 0) wb[w][dg] += (uint32_t) __popcll(peers);
+      __builtin_amdgcn_wave_barrier();
       if (v)
       {
-         uint32_t pos = run[dg] + rank;
-         for (uint32_t u = 0; u < w; u++) pos += wcnt[u][dg];
-         kout[pos] = k;
-         vout[pos] = id;
+         kout[pos] = kr[q];
+         vout[pos] = vr[q];
       }
-      __syncthreads();
-      if (leader)
-      {
-         atomicAdd(&run[dg], wcnt[w][dg]);
-         wcnt[w][dg] = 0;
-      }
-      __syncthreads();
    }
 }
 
