@@ -78,13 +78,18 @@ struct DevCfg
    // Broadcast tree (emesh_hop_by_hop.cc:163-221), nullptr without broadcasts.
    // A router visit v = b * N + tile of broadcast b charges the MAX queue delay
    // over its selected ports (router_model.cc:86-101), i.e. its children leave
-   // at the latest departure max(Xb, tc) of those ports, Xb = a queue's
-   // busy-until time ahead of the request: a pass records max Xb per visit in
-   // bc_mcur (atomicMax) and reads max(bc_mcur so far, bc_mprev of the previous
-   // pass); passes repeat until two agree (engine.hip gnoc_run).
+   // at the latest departure tc + c over those ports.  A pass records that max
+   // per visit in bc_mcur (atomicMax) and charges each port's child
+   // u = max(its own departure, bc_mcur so far, the previous pass's busy-until
+   // times ahead of the request (Xb) of the visit's ports that the level order
+   // serves after this one); bc_u keeps min u, max u and this pass's Xb per port
+   // direction.  The pass is exact when every visit's children got u == its
+   // final max (bc_visit, engine.hip gnoc_run).
    const uint32_t* bc_idx;  // packet id -> broadcast index
-   const uint64_t* bc_mprev;
+   const uint64_t* bc_mprev;  // [d * nv + v] Xb of direction d (P_SELF..P_UP), previous pass
    uint64_t* bc_mcur;
+   uint64_t* bc_u;          // [0, nv) min u, [nv, 2nv) max u, [(2 + d) nv, (3 + d) nv) Xb of direction d
+   uint64_t bc_nv;          // broadcasts x N
    uint64_t* bc_fin;        // [b * N + tile] receipt time (ps)
    uint64_t npk;            // packets of the batch: a SELF port never writes final_ps beyond it
    // A sharded rank's partitioned trace (gnoc_submit): records carry global packet
@@ -93,6 +98,40 @@ struct DevCfg
    const uint32_t* g2l;
 };
 __device__ __forceinline__ uint64_t pk_index(const DevCfg& c, uint32_t id) { return c.g2l ? c.g2l[id] : id; }
+
+// One port (direction dir) of broadcast router visit v: arrival cycle tc, own
+// queue delay cc.  Returns the delay the visit charges this port's child
+// (router_model.cc:86-101).  The level order serves X ports, then Y ports, then
+// SELF: a port predicts the ports served after it from their previous-pass Xb,
+// the busy-until time ahead of the request when it waited (tc + cc), else 0 --
+// exact while their queues ahead of the visit are unchanged.  (Keeping the
+// busy-until time of an idle queue too took 34 passes instead of 20 on the
+// 968-broadcast 32x32 batch.)
+__device__ __forceinline__ uint64_t bc_visit(const DevCfg& c, uint64_t v, uint32_t dir, uint64_t tc, uint64_t cc)
+{
+   const uint64_t nv = c.bc_nv;
+   const uint64_t dep = tc + cc;
+   const uint64_t so_far = atomicMax((unsigned long long*) (c.bc_mcur + v), (unsigned long long) dep);
+   uint64_t u = dep > so_far ? dep : so_far;
+   if (dir != P_SELF)
+   {
+      uint64_t p = c.bc_mprev[P_SELF * nv + v];
+      const uint64_t pu = dir == P_UP ? 0 : c.bc_mprev[P_UP * nv + v];
+      const uint64_t pd = dir == P_DOWN ? 0 : c.bc_mprev[P_DOWN * nv + v];
+      p = p > pu ? p : pu;
+      p = p > pd ? p : pd;
+      if (dir == P_LEFT || dir == P_RIGHT)
+      {
+         const uint64_t px = c.bc_mprev[(dir == P_LEFT ? P_RIGHT : P_LEFT) * nv + v];
+         p = p > px ? p : px;
+      }
+      u = u > p ? u : p;
+   }
+   atomicMin((unsigned long long*) (c.bc_u + v), (unsigned long long) u);
+   atomicMax((unsigned long long*) (c.bc_u + nv + v), (unsigned long long) u);
+   if (cc) c.bc_u[(2 + dir) * nv + v] = dep;
+   return u - tc;
+}
 
 // Latency::toPicosec, common/misc/time_types.h:81-86.  F1: f == 1.0 exactly,
 // where the double expression equals 1000*c for every c < 2^43.

@@ -149,7 +149,7 @@ struct gnoc_engine
    uint32_t nb = 0;
    uint32_t bc_passes = 0;
    std::vector<uint32_t> h_bid;
-   DevBuf d_bidx, d_bid, d_bm0, d_bm1, d_bfin, d_bzl, d_bct, d_bflag, d_bcnt, d_btail;
+   DevBuf d_bidx, d_bid, d_bm0, d_bm1, d_bu, d_bfin, d_bzl, d_bct, d_bflag, d_bcnt, d_btail;
 
    // design-space sweep (gnoc_create_sweep): per-point tables
    int32_t npoints = 1;
@@ -876,6 +876,8 @@ static int upload_broadcasts(gnoc_engine* e)
    e->dc.bc_idx = nullptr;
    e->dc.bc_mprev = nullptr;
    e->dc.bc_mcur = nullptr;
+   e->dc.bc_u = nullptr;
+   e->dc.bc_nv = 0;
    e->dc.bc_fin = nullptr;
    if (!e->nb) return GNOC_OK;
    const size_t nv = (size_t) e->nb * e->dc.N;
@@ -883,8 +885,9 @@ static int upload_broadcasts(gnoc_engine* e)
    for (uint32_t b = 0; b < e->nb; b++) bidx[e->h_bid[b]] = b;
    GNOC_HIP(e, e->d_bidx.ensure(e->n * 4));
    GNOC_HIP(e, e->d_bid.ensure((size_t) e->nb * 4));
-   GNOC_HIP(e, e->d_bm0.ensure(nv * 8));
+   GNOC_HIP(e, e->d_bm0.ensure(nv * 40));
    GNOC_HIP(e, e->d_bm1.ensure(nv * 8));
+   GNOC_HIP(e, e->d_bu.ensure(nv * 56));
    GNOC_HIP(e, e->d_bfin.ensure(nv * 8));
    GNOC_HIP(e, e->d_bzl.ensure(nv * 8));
    GNOC_HIP(e, e->d_bct.ensure(nv * 8));
@@ -894,6 +897,8 @@ static int upload_broadcasts(gnoc_engine* e)
    e->dc.bc_idx = e->d_bidx.as<uint32_t>();
    e->dc.bc_mprev = e->d_bm0.as<uint64_t>();
    e->dc.bc_mcur = e->d_bm1.as<uint64_t>();
+   e->dc.bc_u = e->d_bu.as<uint64_t>();
+   e->dc.bc_nv = nv;
    e->dc.bc_fin = e->d_bfin.as<uint64_t>();
    return GNOC_OK;
 }
@@ -1908,9 +1913,10 @@ int gnoc_run(gnoc_engine* e)
    const int forced = env && std::strcmp(env, "v1") == 0;
    // Broadcast batches run in passes: a router visit of a broadcast charges the
    // max queue delay over the ports it selects (router_model.cc:86-101), and
-   // those ports sit on different levels of the port DAG, so a pass charges the
-   // maxima the previous pass measured.  The event times are the unique causal
-   // solution exactly when two passes agree.
+   // those ports sit on different levels of the port DAG, so a pass charges a
+   // visit's ports not yet served this pass their busy-until times of the
+   // previous pass.  The event times are the unique causal solution exactly when
+   // every visit charged all its children its final max.
    const char* pv = std::getenv("GNOC_BCAST_PASSES");
    const uint32_t max_passes = pv && std::atol(pv) > 0 ? (uint32_t) std::atol(pv) : 256u;
    const size_t nv = (size_t) e->nb * e->dc.N;
@@ -1918,12 +1924,17 @@ int gnoc_run(gnoc_engine* e)
    if (e->nb && e->submitted)
    {
       GNOC_HIP(e, hipSetDevice(e->cfg.device));
-      GNOC_HIP(e, hipMemsetAsync(e->d_bm0.p, 0, nv * 8, e->stream));
+      GNOC_HIP(e, hipMemsetAsync(e->d_bm0.p, 0, nv * 40, e->stream));
    }
    double ms = 0.0;
    for (;;)
    {
-      if (e->nb && e->submitted) GNOC_HIP(e, hipMemsetAsync(e->d_bm1.p, 0, nv * 8, e->stream));
+      if (e->nb && e->submitted)
+      {
+         GNOC_HIP(e, hipMemsetAsync(e->d_bm1.p, 0, nv * 8, e->stream));
+         GNOC_HIP(e, hipMemsetAsync(e->d_bu.p, 0xFF, nv * 8, e->stream));
+         GNOC_HIP(e, hipMemsetAsync(e->d_bu.as<uint64_t>() + nv, 0, nv * 48, e->stream));
+      }
       e->force_v1 = forced;
       e->force_levels = 0;
       e->chD_run[0] = e->chD[0];
@@ -1969,13 +1980,22 @@ int gnoc_run(gnoc_engine* e)
       ms += e->last_ms;
       e->bc_passes++;
       if (!e->nb || !e->dc.contention) break;
-      GNOC_HIP(e, hipMemsetAsync(e->d_bflag.p, 0, 4, e->stream));
+      GNOC_HIP(e, hipMemsetAsync(e->d_bflag.p, 0, 8, e->stream));
+      GNOC_HIP(e, hipMemsetAsync(e->d_bflag.as<char>() + 8, 0xFF, 8, e->stream));
       hipLaunchKernelGGL(k_bcast_agree, dim3((uint32_t) std::min<size_t>((nv + 255) / 256, 4096)), dim3(256), 0,
                          e->stream, (uint64_t) nv, e->d_bm0.as<uint64_t>(), (const uint64_t*) e->d_bm1.as<uint64_t>(),
+                         (const uint64_t*) e->d_bu.as<uint64_t>(),
                          e->d_bflag.as<unsigned>());
       GNOC_HIP(e, hipGetLastError());
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 6, e->d_bflag.p, 4, hipMemcpyDeviceToHost, e->stream));
       GNOC_HIP(e, hipStreamSynchronize(e->stream));
+      if (std::getenv("GNOC_BCAST_DEBUG"))
+      {
+         unsigned hb[4];
+         GNOC_HIP(e, hipMemcpy(hb, e->d_bflag.p, 16, hipMemcpyDeviceToHost));
+         std::fprintf(stderr, "bcast pass %u: %.3f ms changed %u min_cycle %llu\n", e->bc_passes, e->last_ms, hb[1],
+                      (unsigned long long) (hb[2] | (uint64_t) hb[3] << 32));
+      }
       if (!*(unsigned*) (e->h_pinned + 6)) break;
       if (e->bc_passes >= max_passes)
       {

@@ -542,24 +542,15 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
             const uint32_t id = sm.m_id[e], ax = sm.m_aux[e];
             const uint64_t cc = sm.m_c[e];
             // the delay charged: this queue's, or for a broadcast's router visit the
-            // max over the visit's ports.  A port's departure is max(Xb, tc) with Xb
-            // the queue's busy-until time ahead of the request (tc + cc when it
-            // waited, 0 when idle), so the visit keeps max Xb over its ports: a
-            // pass that moves the visit's arrival tc reuses the other ports' Xb of
-            // the previous pass, exact unless their queues ahead of it changed.
+            // max over the visit's ports (bc_visit).
             uint64_t ch = cc;
             const bool bcr = BC && (ax & AUX_BC);
             uint64_t v = 0;
             if (bcr && dir != P_INJ)
             {
                v = (uint64_t) c.bc_idx[id] * c.N + tile;
-               const uint64_t tc = cyc_of<F1>(t, c.f), xb = cc ? tc + cc : 0ull;
-               const uint64_t old = atomicMax((unsigned long long*) (c.bc_mcur + v), (unsigned long long) xb);
-               const uint64_t mp = c.bc_mprev[v];
-               uint64_t u = tc + cc;
-               u = u > old ? u : old;
-               u = u > mp ? u : mp;
-               ch = u - tc;
+               const uint64_t tc = cyc_of<F1>(t, c.f);
+               ch = bc_visit(c, v, dir, tc, cc);
             }
             st_sum += ch;
             st_cnt++;
@@ -733,18 +724,34 @@ __global__ __launch_bounds__(256) void k_bcast_final(DevCfg c, const uint32_t* _
    }
 }
 
-// Pass agreement: any visit whose max delay changed since the previous pass
-// sets *changed; then the maxima become the next pass's input.
+// Pass check: a visit whose children were not all charged its final max
+// departure (min u or max u != mcur) sets *changed; the busy-until times of
+// its ports this pass become the next pass's input (mprev).  Visits no port
+// reached (u untouched, mcur 0) are skipped.
 __global__ __launch_bounds__(256) void k_bcast_agree(uint64_t nv, uint64_t* __restrict__ mprev,
-                                                     const uint64_t* __restrict__ mcur, unsigned* __restrict__ changed)
+                                                     const uint64_t* __restrict__ mcur, const uint64_t* __restrict__ u,
+                                                     unsigned* __restrict__ changed)
 {
    bool ch = false;
+   unsigned nch = 0;
+   uint64_t tmin = ~0ull;
    for (uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; k < nv; k += (uint64_t) gridDim.x * blockDim.x)
    {
-      const uint64_t v = mcur[k];
-      if (v != mprev[k]) { ch = true; mprev[k] = v; }
+      const uint64_t m = mcur[k], lo = u[k], hi = u[nv + k];
+      for (uint32_t d = 0; d < 5; d++) mprev[d * nv + k] = u[(2 + d) * nv + k];
+      if ((m || hi) && (lo != m || hi != m))
+      {
+         ch = true;
+         nch++;
+         tmin = m < tmin ? m : tmin;
+      }
    }
    if (__ballot(ch) && (threadIdx.x & 63) == 0) atomicOr(changed, 1u);
+   if (nch)
+   {
+      atomicAdd(changed + 1, nch);
+      atomicMin((unsigned long long*) (changed + 2), (unsigned long long) tmin);
+   }
 }
 
 // Results of packets another rank delivers read 0 (gnoc_get_packet_results).

@@ -666,9 +666,7 @@ __device__ Scan3 lv_scan(LvSmem& sm, const Seg& sg)
 }
 
 // A broadcast record served with queue delay cc at this port (tc = its arrival
-// cycle): the delay its router visit charges -- the max over the visit's ports,
-// from their busy-until times Xb (this pass so far, or the previous pass; DevCfg
-// bc_*) -- then its receipt (SELF) or one record into the exception tail of
+// cycle): the delay its router visit charges -- the max over the visit's ports (bc_visit) -- then its receipt (SELF) or one record into the exception tail of
 // each tree port at the next router (bc_mask).  Returns the charged delay.
 __device__ uint64_t lv_bcast(const LvSmem& sm, const DevCfg& c, uint64_t t, uint32_t id, uint32_t ax, uint64_t cc,
                              uint64_t rl, Rec* __restrict__ recs, uint32_t* __restrict__ nexc,
@@ -680,13 +678,7 @@ __device__ uint64_t lv_bcast(const LvSmem& sm, const DevCfg& c, uint64_t t, uint
    if (dir != P_INJ)
    {
       v = (uint64_t) c.bc_idx[id] * c.N + sm.io.port / PORTS;
-      const uint64_t tc = LV_CYC(t), xb = cc ? tc + cc : 0ull;
-      const uint64_t old = atomicMax((unsigned long long*) (c.bc_mcur + v), (unsigned long long) xb);
-      const uint64_t mp = c.bc_mprev[v];
-      uint64_t u = tc + cc;
-      u = u > old ? u : old;
-      u = u > mp ? u : mp;
-      ch = u - tc;
+      ch = bc_visit(c, v, dir, LV_CYC(t), cc);
    }
    const uint64_t tn = t + LV_PS(ch) + rl;
    if (dir == P_SELF)
