@@ -78,18 +78,16 @@ struct DevCfg
    // Broadcast tree (emesh_hop_by_hop.cc:163-221), nullptr without broadcasts.
    // A router visit v = b * N + tile of broadcast b charges the MAX queue delay
    // over its selected ports (router_model.cc:86-101), i.e. its children leave
-   // at the latest departure tc + c over those ports.  A pass records that max
-   // per visit in bc_mcur (atomicMax) and charges each port's child
-   // u = max(its own departure, bc_mcur so far, the previous pass's busy-until
-   // times ahead of the request (Xb) of the visit's ports that the level order
-   // serves after this one); bc_u keeps min u, max u and this pass's Xb per port
-   // direction.  The pass is exact when every visit's children got u == its
-   // final max (bc_visit, engine.hip gnoc_run).
+   // at the latest departure tc + c over those ports.  A pass keeps per visit
+   // (one BCS-word record, bc_cur) that max, the min and max departure u its
+   // ports' children were charged, and each port's queue neighbourhood
+   // (BcWin); u = max(the port's own departure, the max so far, predictions
+   // for the visit's ports the level order serves after this one from the
+   // previous pass's record, bc_prev).  The pass is exact when every visit's
+   // children got u == its final max (bc_visit, engine.hip gnoc_run).
    const uint32_t* bc_idx;  // packet id -> broadcast index
-   const uint64_t* bc_mprev;  // [d * nv + v] Xb of direction d (P_SELF..P_UP), previous pass
-   uint64_t* bc_mcur;
-   uint64_t* bc_u;          // [0, nv) min u, [nv, 2nv) max u, [(2 + d) nv, (3 + d) nv) Xb of direction d
-   uint64_t bc_nv;          // broadcasts x N
+   const uint64_t* bc_prev; // [v * BCS + ...] previous pass
+   uint64_t* bc_cur;        // [v * BCS + ...] this pass (zeroed before it)
    uint64_t* bc_fin;        // [b * N + tile] receipt time (ps)
    uint64_t npk;            // packets of the batch: a SELF port never writes final_ps beyond it
    // A sharded rank's partitioned trace (gnoc_submit): records carry global packet
@@ -99,38 +97,76 @@ struct DevCfg
 };
 __device__ __forceinline__ uint64_t pk_index(const DevCfg& c, uint32_t id) { return c.g2l ? c.g2l[id] : id; }
 
-// One port (direction dir) of broadcast router visit v: arrival cycle tc, own
-// queue delay cc.  Returns the delay the visit charges this port's child
-// (router_model.cc:86-101).  The level order serves X ports, then Y ports, then
-// SELF: a port predicts the ports served after it from their previous-pass Xb,
-// the busy-until time ahead of the request when it waited (tc + cc), else 0 --
-// exact while their queues ahead of the visit are unchanged.  (Keeping the
-// busy-until time of an idle queue too took 34 passes instead of 20 on the
-// 968-broadcast 32x32 batch.)
-__device__ __forceinline__ uint64_t bc_visit(const DevCfg& c, uint64_t v, uint32_t dir, uint64_t tc, uint64_t cc)
+// A broadcast record's neighbourhood in its port's queue (cycles): the
+// arrivals of the records just before and after it (a_prev, a_next), the
+// busy-until time ahead of it (B), ahead of it were it behind the next record
+// (B_next = max(B, a_next) + F_next) and ahead of the previous record (B_pp).
+// The next pass predicts the wait of the visit at its new arrival tc' from the
+// slot tc' falls in: exact while at most one record is crossed and the
+// queue's other records did not move.  Unknown fields: a_prev = tc (nothing
+// earlier predicted), a_next = ~0, B_pp = 0.
+enum : uint32_t { BCW_AP = 0, BCW_AN = 1, BCW_B = 2, BCW_BN = 3, BCW_BP = 4, BCW = 5 };
+// a visit's record: ~min u, max u, max departure, then BcWin of each direction
+enum : uint32_t { BC_UMIN = 0, BC_UMAX = 1, BC_M = 2, BC_WIN = 3, BCS = BC_WIN + 5 * BCW };
+struct BcWin
 {
-   const uint64_t nv = c.bc_nv;
+   uint64_t ap, an, b, bn, bp;
+};
+__device__ __forceinline__ uint64_t bc_predict(const uint64_t* __restrict__ prev, uint32_t d, uint64_t tc)
+{
+   // (loading all five fields up front measured slower: register pressure)
+   const uint64_t* w = prev + BC_WIN + d * BCW;
+   const uint64_t ap = w[BCW_AP], an = w[BCW_AN];
+   const uint64_t b = tc < ap ? w[BCW_BP] : tc > an ? w[BCW_BN] : w[BCW_B];
+   return b > tc ? b : 0;
+}
+
+// One port (direction dir) of broadcast router visit v (selected ports sel):
+// arrival cycle tc, own queue delay cc, its queue neighbourhood w.  Returns the delay the visit
+// charges this port's child (router_model.cc:86-101).  The level order serves
+// X ports, then Y ports, then SELF: a port predicts the ports served after it
+// (bc_predict); the ports served before it are in the max so far.
+__device__ __forceinline__ uint64_t bc_visit(const DevCfg& c, uint64_t v, uint32_t dir, uint32_t sel, uint64_t tc,
+                                             uint64_t cc, const BcWin& w)
+{
+   uint64_t* r = c.bc_cur + v * BCS;
+   const uint64_t* q = c.bc_prev + v * BCS;
    const uint64_t dep = tc + cc;
-   const uint64_t so_far = atomicMax((unsigned long long*) (c.bc_mcur + v), (unsigned long long) dep);
+   const uint64_t so_far = atomicMax((unsigned long long*) (r + BC_M), (unsigned long long) dep);
    uint64_t u = dep > so_far ? dep : so_far;
    if (dir != P_SELF)
    {
-      uint64_t p = c.bc_mprev[P_SELF * nv + v];
-      const uint64_t pu = dir == P_UP ? 0 : c.bc_mprev[P_UP * nv + v];
-      const uint64_t pd = dir == P_DOWN ? 0 : c.bc_mprev[P_DOWN * nv + v];
-      p = p > pu ? p : pu;
-      p = p > pd ? p : pd;
-      if (dir == P_LEFT || dir == P_RIGHT)
-      {
-         const uint64_t px = c.bc_mprev[(dir == P_LEFT ? P_RIGHT : P_LEFT) * nv + v];
-         p = p > px ? p : px;
-      }
-      u = u > p ? u : p;
+      // the visit's selected ports (sel, bc_mask) served after this one
+      const uint32_t later = sel & ~(1u << dir) & ~(dir == P_UP || dir == P_DOWN ? (1u << P_LEFT) | (1u << P_RIGHT) : 0u);
+      for (uint32_t d = 0; d < 5; d++)
+         if ((later >> d) & 1u)
+         {
+            const uint64_t p = bc_predict(q, d, tc);
+            u = u > p ? u : p;
+         }
    }
-   atomicMin((unsigned long long*) (c.bc_u + v), (unsigned long long) u);
-   atomicMax((unsigned long long*) (c.bc_u + nv + v), (unsigned long long) u);
-   if (cc) c.bc_u[(2 + dir) * nv + v] = dep;
+   atomicMax((unsigned long long*) (r + BC_UMIN), (unsigned long long) ~u);
+   atomicMax((unsigned long long*) (r + BC_UMAX), (unsigned long long) u);
+   uint64_t* o = r + BC_WIN + dir * BCW;
+   o[BCW_AP] = w.ap;
+   o[BCW_AN] = w.an;
+   o[BCW_B] = w.b;
+   o[BCW_BN] = w.bn;
+   o[BCW_BP] = w.bp;
    return u - tc;
+}
+
+// A neighbourhood that only knows the wait itself (serial history-tree mode,
+// whole-port streams): predicts busy-until tc + cc when the queue waited.
+__device__ __forceinline__ BcWin bc_win_wait(uint64_t tc, uint64_t cc)
+{
+   BcWin w;
+   w.ap = 0;
+   w.an = ~0ull;
+   w.b = cc ? tc + cc : 0;
+   w.bn = w.b;
+   w.bp = w.b;
+   return w;
 }
 
 // Latency::toPicosec, common/misc/time_types.h:81-86.  F1: f == 1.0 exactly,

@@ -149,7 +149,7 @@ struct gnoc_engine
    uint32_t nb = 0;
    uint32_t bc_passes = 0;
    std::vector<uint32_t> h_bid;
-   DevBuf d_bidx, d_bid, d_bm0, d_bm1, d_bu, d_bfin, d_bzl, d_bct, d_bflag, d_bcnt, d_btail;
+   DevBuf d_bidx, d_bid, d_bv[2], d_bfin, d_bzl, d_bct, d_bflag, d_bcnt, d_btail;
 
    // design-space sweep (gnoc_create_sweep): per-point tables
    int32_t npoints = 1;
@@ -874,10 +874,8 @@ static int upload_broadcasts(gnoc_engine* e)
 {
    e->nb = (uint32_t) e->h_bid.size();
    e->dc.bc_idx = nullptr;
-   e->dc.bc_mprev = nullptr;
-   e->dc.bc_mcur = nullptr;
-   e->dc.bc_u = nullptr;
-   e->dc.bc_nv = 0;
+   e->dc.bc_prev = nullptr;
+   e->dc.bc_cur = nullptr;
    e->dc.bc_fin = nullptr;
    if (!e->nb) return GNOC_OK;
    const size_t nv = (size_t) e->nb * e->dc.N;
@@ -885,9 +883,8 @@ static int upload_broadcasts(gnoc_engine* e)
    for (uint32_t b = 0; b < e->nb; b++) bidx[e->h_bid[b]] = b;
    GNOC_HIP(e, e->d_bidx.ensure(e->n * 4));
    GNOC_HIP(e, e->d_bid.ensure((size_t) e->nb * 4));
-   GNOC_HIP(e, e->d_bm0.ensure(nv * 40));
-   GNOC_HIP(e, e->d_bm1.ensure(nv * 8));
-   GNOC_HIP(e, e->d_bu.ensure(nv * 56));
+   GNOC_HIP(e, e->d_bv[0].ensure(nv * 8 * BCS));
+   GNOC_HIP(e, e->d_bv[1].ensure(nv * 8 * BCS));
    GNOC_HIP(e, e->d_bfin.ensure(nv * 8));
    GNOC_HIP(e, e->d_bzl.ensure(nv * 8));
    GNOC_HIP(e, e->d_bct.ensure(nv * 8));
@@ -895,10 +892,8 @@ static int upload_broadcasts(gnoc_engine* e)
    GNOC_HIP(e, hipMemcpy(e->d_bidx.p, bidx.data(), e->n * 4, hipMemcpyHostToDevice));
    GNOC_HIP(e, hipMemcpy(e->d_bid.p, e->h_bid.data(), (size_t) e->nb * 4, hipMemcpyHostToDevice));
    e->dc.bc_idx = e->d_bidx.as<uint32_t>();
-   e->dc.bc_mprev = e->d_bm0.as<uint64_t>();
-   e->dc.bc_mcur = e->d_bm1.as<uint64_t>();
-   e->dc.bc_u = e->d_bu.as<uint64_t>();
-   e->dc.bc_nv = nv;
+   e->dc.bc_prev = e->d_bv[0].as<uint64_t>();
+   e->dc.bc_cur = e->d_bv[1].as<uint64_t>();
    e->dc.bc_fin = e->d_bfin.as<uint64_t>();
    return GNOC_OK;
 }
@@ -1924,16 +1919,16 @@ int gnoc_run(gnoc_engine* e)
    if (e->nb && e->submitted)
    {
       GNOC_HIP(e, hipSetDevice(e->cfg.device));
-      GNOC_HIP(e, hipMemsetAsync(e->d_bm0.p, 0, nv * 40, e->stream));
+      GNOC_HIP(e, hipMemsetAsync(e->d_bv[0].p, 0, nv * 8 * BCS, e->stream));
+      e->dc.bc_prev = e->d_bv[0].as<uint64_t>();
+      e->dc.bc_cur = e->d_bv[1].as<uint64_t>();
    }
    double ms = 0.0;
    for (;;)
    {
       if (e->nb && e->submitted)
       {
-         GNOC_HIP(e, hipMemsetAsync(e->d_bm1.p, 0, nv * 8, e->stream));
-         GNOC_HIP(e, hipMemsetAsync(e->d_bu.p, 0xFF, nv * 8, e->stream));
-         GNOC_HIP(e, hipMemsetAsync(e->d_bu.as<uint64_t>() + nv, 0, nv * 48, e->stream));
+         GNOC_HIP(e, hipMemsetAsync(e->dc.bc_cur, 0, nv * 8 * BCS, e->stream));
       }
       e->force_v1 = forced;
       e->force_levels = 0;
@@ -1983,8 +1978,7 @@ int gnoc_run(gnoc_engine* e)
       GNOC_HIP(e, hipMemsetAsync(e->d_bflag.p, 0, 8, e->stream));
       GNOC_HIP(e, hipMemsetAsync(e->d_bflag.as<char>() + 8, 0xFF, 8, e->stream));
       hipLaunchKernelGGL(k_bcast_agree, dim3((uint32_t) std::min<size_t>((nv + 255) / 256, 4096)), dim3(256), 0,
-                         e->stream, (uint64_t) nv, e->d_bm0.as<uint64_t>(), (const uint64_t*) e->d_bm1.as<uint64_t>(),
-                         (const uint64_t*) e->d_bu.as<uint64_t>(),
+                         e->stream, (uint64_t) nv, (const uint64_t*) e->dc.bc_cur,
                          e->d_bflag.as<unsigned>());
       GNOC_HIP(e, hipGetLastError());
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 6, e->d_bflag.p, 4, hipMemcpyDeviceToHost, e->stream));
@@ -1995,14 +1989,36 @@ int gnoc_run(gnoc_engine* e)
          GNOC_HIP(e, hipMemcpy(hb, e->d_bflag.p, 16, hipMemcpyDeviceToHost));
          std::fprintf(stderr, "bcast pass %u: %.3f ms changed %u min_cycle %llu\n", e->bc_passes, e->last_ms, hb[1],
                       (unsigned long long) (hb[2] | (uint64_t) hb[3] << 32));
+         if (const char* dp = std::getenv("GNOC_BCAST_DUMP"))
+         {
+            // wrong visits of this pass: b, tile, final max, min u, max u, Xb by direction
+            std::vector<uint64_t> hu(nv * BCS);
+            GNOC_HIP(e, hipMemcpy(hu.data(), e->dc.bc_cur, nv * 8 * BCS, hipMemcpyDeviceToHost));
+            FILE* f = std::fopen(dp, e->bc_passes == 1 ? "w" : "a");
+            for (size_t k = 0; f && k < nv; k++)
+            {
+               const uint64_t* r = &hu[k * BCS];
+               const uint64_t m = r[BC_M], lo = ~r[BC_UMIN], hi = r[BC_UMAX];
+               if (!((m || hi) && (lo != m || hi != m))) continue;
+               std::fprintf(f, "%u %zu %zu %llu %llu %llu", e->bc_passes, k / e->dc.N, k % e->dc.N, (unsigned long long) m,
+                            (unsigned long long) lo, (unsigned long long) hi);
+               for (int d = 0; d < 5; d++) std::fprintf(f, " %llu", (unsigned long long) r[BC_WIN + d * BCW + BCW_B]);
+               std::fprintf(f, "\n");
+            }
+            if (f) std::fclose(f);
+         }
       }
       if (!*(unsigned*) (e->h_pinned + 6)) break;
       if (e->bc_passes >= max_passes)
       {
          e->ran = false;
-         return fail(e, GNOC_EUNSUPPORTED, "broadcast passes did not agree within " + std::to_string(max_passes) +
+         return fail(e, GNOC_EUNSUPPORTED, "broadcast passes did not converge within " + std::to_string(max_passes) +
                                                " (GNOC_BCAST_PASSES)");
       }
+      // this pass's visit records predict the next pass
+      uint64_t* const was = const_cast<uint64_t*>(e->dc.bc_prev);
+      e->dc.bc_prev = e->dc.bc_cur;
+      e->dc.bc_cur = was;
    }
    e->last_ms = ms;
    return GNOC_OK;

@@ -202,7 +202,7 @@ __device__ void fixup_slot(FixSmem& fx, Rec* __restrict__ r, uint32_t n)
 // tail]; the tail holds slot_cnt - bcnt.. slot_cnt, filled through btail in
 // any order.  Broadcast children are charged the max departure over their
 // router visit's ports (router_model.cc:86-101): this pass's value so far
-// (bc_mcur, atomicMax) or the previous pass's (bc_mprev), whichever is later.
+// so far this pass or predicted from the previous pass (bc_visit).
 template <bool F1, bool BC>
 __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32_t* __restrict__ ports,
                                                           const uint32_t* __restrict__ slot_cnt,
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
             {
                v = (uint64_t) c.bc_idx[id] * c.N + tile;
                const uint64_t tc = cyc_of<F1>(t, c.f);
-               ch = bc_visit(c, v, dir, tc, cc);
+               ch = bc_visit(c, v, dir, 0x1Fu, tc, cc, bc_win_wait(tc, cc));
             }
             st_sum += ch;
             st_cnt++;
@@ -725,11 +725,9 @@ __global__ __launch_bounds__(256) void k_bcast_final(DevCfg c, const uint32_t* _
 }
 
 // Pass check: a visit whose children were not all charged its final max
-// departure (min u or max u != mcur) sets *changed; the busy-until times of
-// its ports this pass become the next pass's input (mprev).  Visits no port
-// reached (u untouched, mcur 0) are skipped.
-__global__ __launch_bounds__(256) void k_bcast_agree(uint64_t nv, uint64_t* __restrict__ mprev,
-                                                     const uint64_t* __restrict__ mcur, const uint64_t* __restrict__ u,
+// departure (min u or max u != max) sets *changed.  Visits no port reached
+// (record untouched) are skipped.
+__global__ __launch_bounds__(256) void k_bcast_agree(uint64_t nv, const uint64_t* __restrict__ cur,
                                                      unsigned* __restrict__ changed)
 {
    bool ch = false;
@@ -737,8 +735,8 @@ __global__ __launch_bounds__(256) void k_bcast_agree(uint64_t nv, uint64_t* __re
    uint64_t tmin = ~0ull;
    for (uint64_t k = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; k < nv; k += (uint64_t) gridDim.x * blockDim.x)
    {
-      const uint64_t m = mcur[k], lo = u[k], hi = u[nv + k];
-      for (uint32_t d = 0; d < 5; d++) mprev[d * nv + k] = u[(2 + d) * nv + k];
+      const uint64_t* r = cur + k * BCS;
+      const uint64_t m = r[BC_M], lo = ~r[BC_UMIN], hi = r[BC_UMAX];
       if ((m || hi) && (lo != m || hi != m))
       {
          ch = true;

@@ -669,7 +669,7 @@ __device__ Scan3 lv_scan(LvSmem& sm, const Seg& sg)
 // cycle): the delay its router visit charges -- the max over the visit's ports (bc_visit) -- then its receipt (SELF) or one record into the exception tail of
 // each tree port at the next router (bc_mask).  Returns the charged delay.
 __device__ uint64_t lv_bcast(const LvSmem& sm, const DevCfg& c, uint64_t t, uint32_t id, uint32_t ax, uint64_t cc,
-                             uint64_t rl, Rec* __restrict__ recs, uint32_t* __restrict__ nexc,
+                             const BcWin& w, uint64_t rl, Rec* __restrict__ recs, uint32_t* __restrict__ nexc,
                              unsigned* __restrict__ errflag)
 {
    const uint32_t dir = sm.io.dir;
@@ -677,8 +677,10 @@ __device__ uint64_t lv_bcast(const LvSmem& sm, const DevCfg& c, uint64_t t, uint
    uint64_t v = 0;
    if (dir != P_INJ)
    {
+      // all later directions (a port the visit did not select has an empty record;
+      // computing this router's tree ports here measured slower)
       v = (uint64_t) c.bc_idx[id] * c.N + sm.io.port / PORTS;
-      ch = bc_visit(c, v, dir, LV_CYC(t), cc);
+      ch = bc_visit(c, v, dir, 0x1Fu, LV_CYC(t), cc, w);
    }
    const uint64_t tn = t + LV_PS(ch) + rl;
    if (dir == P_SELF)
@@ -695,6 +697,34 @@ __device__ uint64_t lv_bcast(const LvSmem& sm, const DevCfg& c, uint64_t t, uint
       lv_store_rec(recs + sm.io.obase[nd] + sm.io.ocnt[nd] - 1 - x, tn, id, ax);
    }
    return ch;
+}
+
+// The queue neighbourhood (BcWin) of the broadcast record at merged position j
+// (arrival tc, busy-until xb ahead of it), from the chunk's merged records in
+// LDS.  Ahead of the previous record the queue was busy until xb - F_prev when
+// that exceeds its arrival; otherwise it was idle there (0).
+__device__ __noinline__ BcWin lv_bcwin(const LvSmem& sm, uint32_t j, uint64_t tc, uint64_t xb)
+{
+   BcWin w;
+   w.ap = tc;
+   w.bp = 0;
+   w.b = xb;
+   w.an = ~0ull;
+   w.bn = xb;
+   if (j > 0)
+   {
+      const uint32_t kp = sm.perm[j - 1];
+      const uint64_t ap = LV_CYC(sm.kt[kp]), fp = aux_F(sm.ka[kp]);
+      w.ap = ap;
+      w.bp = xb > ap + fp ? xb - fp : 0;
+   }
+   if (j + 1 < sm.E)
+   {
+      const uint32_t kn = sm.perm[j + 1];
+      w.an = LV_CYC(sm.kt[kn]);
+      w.bn = (xb > w.an ? xb : w.an) + aux_F(sm.ka[kn]);
+   }
+   return w;
 }
 
 // Serial prefix while the queue has never idled (history tree + M/G/1), one
@@ -727,7 +757,7 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
          slast = slast > dep ? slast : dep;
          if (BC && (ax & AUX_BC))
          {
-            ssum += lv_bcast(sm, c, t, id, ax, cc, rl, recs, nexc, errflag);
+            ssum += lv_bcast(sm, c, t, id, ax, cc, bc_win_wait(LV_CYC(t), cc), rl, recs, nexc, errflag);
             continue;
          }
          ssum += cc;
@@ -796,10 +826,11 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
          const uint32_t ax = sm.ka[k];
          const uint64_t tc = LV_CYC(t);
          const uint64_t cc = X > tc ? X - tc : 0;
+         const uint64_t xb = X;
          X = (X > tc ? X : tc) + aux_F(ax);
          if (BC && (ax & AUX_BC))
          {
-            ssum += lv_bcast(sm, c, t, id, ax, cc, rl, recs, nexc, errflag);
+            ssum += lv_bcast(sm, c, t, id, ax, cc, lv_bcwin(sm, sg.a + i, tc, xb), rl, recs, nexc, errflag);
             continue;
          }
          ssum += cc;
