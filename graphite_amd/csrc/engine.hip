@@ -38,7 +38,16 @@ namespace gnoc {
 // N-entry source histogram (hist = 4 B per packet at most), and more, smaller
 // chunks keep enough waves in flight for the per-packet latency chains of the
 // scatter (16,384-tile sweeps: 65,536 -> 16,384 packets per chunk).
-static inline uint32_t prep_chunk(uint32_t N) { return std::max<uint32_t>(16384u, (N + 63u) & ~63u); }
+// Trace packets per prep workgroup (k_classify histograms, k_scatter4 ranks).
+// configs[1] (GNOC_PREP_CHUNK): 16384 -> 4.025 ms per step, 8192 -> 3.965
+// (k_scatter4 0.26 -> 0.23 ms), 4096 -> 3.977 (k_classify's per-chunk
+// histograms grow), 2048 -> 4.002.
+static inline uint32_t prep_chunk(uint32_t N)
+{
+   const char* v = std::getenv("GNOC_PREP_CHUNK");
+   const uint32_t base = v && std::atoi(v) >= 1024 ? (uint32_t) std::atoi(v) : 8192u;
+   return std::max<uint32_t>(base, (N + 63u) & ~63u);
+}
 }  // namespace gnoc
 
 using namespace gnoc;
