@@ -1056,17 +1056,31 @@ __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict_
       else if ((q + 1) * D <= t) q++;
       return q < wl ? q : wl;
    };
-   for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x)
+   // BW_U rounds of the workgroup per step: their loads are in flight together
+   constexpr uint32_t BW_U = 4;
+   for (uint32_t i0 = 0; i0 < n; i0 += BW_U * blockDim.x)
    {
-      const uint32_t i = i0 + threadIdx.x;
-      const uint64_t wi = i < n ? win(recs[base + i].t) : wl;
-      uint64_t wprev = (uint64_t) __shfl_up((long long) wi, 1);
-      if ((threadIdx.x & 63) == 0) wprev = i ? win(recs[base + i - 1].t) : 0;
-      if (i >= n) continue;
-      const int64_t wp = i ? (int64_t) wprev : -1;
-      for (int64_t v = wp + 1; v <= (int64_t) wi; v++) b[v] = i;
-      if (i == n - 1)
-         for (uint64_t v = wi + 1; v <= nW; v++) b[v] = n;
+      uint64_t tt[BW_U], tp[BW_U];
+#pragma unroll
+      for (uint32_t q = 0; q < BW_U; q++)
+      {
+         const uint32_t i = i0 + q * blockDim.x + threadIdx.x;
+         tt[q] = i < n ? recs[base + i].t : 0;
+         tp[q] = (threadIdx.x & 63) == 0 && i && i < n ? recs[base + i - 1].t : 0;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < BW_U; q++)
+      {
+         const uint32_t i = i0 + q * blockDim.x + threadIdx.x;
+         const uint64_t wi = i < n ? win(tt[q]) : wl;
+         uint64_t wprev = (uint64_t) __shfl_up((long long) wi, 1);
+         if ((threadIdx.x & 63) == 0) wprev = i ? win(tp[q]) : 0;
+         if (i >= n) continue;
+         const int64_t wp = i ? (int64_t) wprev : -1;
+         for (int64_t v = wp + 1; v <= (int64_t) wi; v++) b[v] = i;
+         if (i == n - 1)
+            for (uint64_t v = wi + 1; v <= nW; v++) b[v] = n;
+      }
    }
 }
 
