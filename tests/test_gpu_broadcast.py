@@ -119,3 +119,20 @@ def test_engine_paths_agree(monkeypatch, env):
     got, ref, _ = run_both(cfg, tr)
     assert_bcast_same(got, ref, tr)
     assert got.summary["engine_path"] == (0 if "GNOC_ENGINE" in env else 1)
+
+
+def test_synthetic_32x32_broadcast_mix():
+    """configs[1]'s traffic at 150 packets per tile with ~0.2% broadcasts (325,
+    one every ~90 cycles, so their trees overlap), bit-exact on a 1024-tile
+    mesh.  The pass count (31 when written) is bounded as a
+    regression guard."""
+    base = gnoc.synthetic_trace(32, 32, 0.005, 150, seed=3)
+    tr = gnoc.Trace(base.inject_ps, base.src, base.dst, base.bits, base.flags.copy())
+    rng = np.random.default_rng(17)
+    tr.flags[rng.random(len(tr)) < 2e-3] |= gnoc.PKT_BROADCAST
+    cfg = gnoc.EngineConfig(num_tiles=1024)
+    got, ref, (nb, passes) = run_both(cfg, tr)
+    print(f"broadcasts {nb}, passes {passes}")
+    assert nb > 100
+    assert_bcast_same(got, ref, tr)
+    assert passes <= 40
