@@ -79,3 +79,14 @@ def test_adapted_windows_repeat_exactly():
 def oracle_run(cfg, tr):
     from oracle import oracle
     return oracle.run(cfg, tr)
+
+
+@pytest.mark.parametrize("pch", [1024, 4096, 16384])
+def test_prep_chunk_sizes(monkeypatch, pch):
+    """The prep workgroups' trace chunk (GNOC_PREP_CHUNK, default 8192) only
+    changes how k_classify / k_scatter4 split the trace: same bytes."""
+    monkeypatch.setenv("GNOC_PREP_CHUNK", str(pch))
+    cfg = gnoc.EngineConfig(num_tiles=1024)
+    tr = gnoc.synthetic_trace(32, 32, 0.004, 60, seed=23, hotspot_fraction=0.1)
+    got, ref = run_both(cfg, tr)
+    assert_same(got, ref)
