@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-sample-ppt", type=int, default=1000)
     ap.add_argument("--verify", type=int, default=0, help="also check the GPU result vs the oracle (slow)")
+    ap.add_argument("--hotspot", type=int, default=1, help="also time the hotspot half of configs[1] (N=1 mesh)")
     ap.add_argument("--workload", choices=("auto", "mesh", "sharded", "replicas", "sweep"), default="auto",
                     help="auto: one 32x32 mesh at N=1, one 64x64 mesh sharded over N ranks at N>1")
     return ap.parse_args()
@@ -103,22 +104,8 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(a.warmup):
-        eng.run()
-
-    barrier_sync()
-    t_start = time.perf_counter()
-    for _ in range(a.steps):
-        eng.run()
-    barrier_sync()
-    elapsed = time.perf_counter() - t_start
-    summ = eng.summary()   # the last timed run (windows, reruns)
-
-    # kernel-level timing on the engine's own stream (HIP events), separate pass
-    eng.set_profiling(True)
-    eng.run()
-    kst = eng.kernel_stats()
-    eng.set_profiling(False)
+    m = measure(eng, a, barrier_sync, settle_fixed=sharded)
+    elapsed, summ, kst, reruns = m["elapsed"], m["summary"], m["kst"], m["reruns"]
 
     # end to end (SURVEY.md 8(d) "trace resident in host memory -> results in host
     # memory"): submit from pinned host arrays (host-side trace validation + H2D),
@@ -138,7 +125,7 @@ def main():
     # this rank's share: mesh hops through the ports it owns, packets it delivers
     res = eng.results()
     pc = res.port_count.reshape(-1, 6)
-    my_hops, my_pkts = int(pc[:, :5].sum()), int(pc[:, 0].sum())
+    my_pkts = int(pc[:, 0].sum())
     hops = int(summ["mesh_hops"])
     pkts = int(summ["routed_packets"])
     t = torch.tensor([elapsed, float(hops), float(pkts)], dtype=torch.float64, device="cuda")
@@ -157,26 +144,32 @@ def main():
             ref = oracle.run(cfg, tr)
             assert np.array_equal(got.final_ps, ref.final_ps), "GPU result differs from oracle"
 
+    # the other half of BASELINE configs[1] ("uniform-random + hotspot"): the same
+    # mesh and load with 20 % of the packets sent to 16 hotspot tiles, one GPU
+    hot_line = None
+    if wl == "mesh" and world == 1 and a.mix == "uniform" and a.hotspot:
+        eng.close()
+        trh = gnoc.synthetic_trace(W, H, load, a.ppt, seed=seed, hotspot_fraction=0.2, num_hotspots=16)
+        eng = gnoc.Engine(cfg)
+        eng.submit(trh)
+        mh = measure(eng, a, barrier_sync)
+        rh = eng.results()
+        pch = rh.port_count.reshape(-1, 6)
+        hh = int(mh["summary"]["mesh_hops"])
+        rfh = roofline(mh["kst"], pch, mh["summary"], int(pch[:, 0].sum()))
+        hot_line = {"workload": f"emesh_hop_by_hop {W}x{H} hotspot(0.2, 16 tiles) load={load} pkts/tile={a.ppt}",
+                    "value": hh * a.steps / mh["elapsed"], "ms_per_step": mh["elapsed"] / a.steps * 1e3,
+                    "mesh_hops": hh, "engine_path": int(mh["summary"].get("engine_path", -1)),
+                    "reruns": mh["reruns"], "roofline_frac": rfh["frac"], "kernel": rfh["kernel"],
+                    "kernel_avg_us": rfh["kernel_avg_us"], "kernel_ms": {k: round(v[0], 4) for k, v in mh["kst"].items()}}
+
     if rank == 0:
         value = hops_all * a.steps / elapsed_max
         ms_step = elapsed_max / a.steps * 1e3
-        # dominant kernel (most device time on this rank): k_chain (v4: the X and Y port
-        # chains), k_level (the chunked levels; on v4 the injection and SELF levels only) or
-        # k_port_stream (v1).  Algorithmic bytes of ITS launches: 32 B per
-        # hop record it moves -- k_chain: the mesh hops at RIGHT/LEFT/UP/DOWN ports; the
-        # level kernels: every hop record + 24 B per delivered packet.
-        dom = max(("k_chain", "k_level", "k_port_stream"), key=lambda k: kst.get(k, (0.0, 0))[0])
-        port_ms, port_launches = kst.get(dom, (0.0, 0))
-        xy_hops = int(pc[:, 1:5].sum())
-        if dom == "k_chain":
-            alg_bytes = xy_hops * BYTES_PER_HOP
-        elif int(summ.get("engine_path", 0)) == 4:   # v4 but k_level dominant: injection + SELF levels
-            alg_bytes = (int(pc[:, 0].sum()) + int(pc[:, 5].sum())) * BYTES_PER_HOP + my_pkts * BYTES_PER_PKT
-        else:
-            alg_bytes = my_hops * BYTES_PER_HOP + my_pkts * BYTES_PER_PKT
-        achieved = alg_bytes / (port_ms * 1e-3) / 1e9 if port_ms > 0 else 0.0
+        rf = roofline(kst, pc, summ, my_pkts)
         whole_job_gbs = value * (BYTES_PER_HOP + BYTES_PER_PKT * pkts / max(hops, 1)) / 1e9 / world
         workload = f"emesh_hop_by_hop {W}x{H} {a.mix} load={load} pkts/tile={a.ppt}"
+        bid = build_id()
         line = {
             "metric": "packet-hops simulated/sec (node) + % HBM roofline, 1024-tile emesh",
             "value": value,
@@ -200,40 +193,113 @@ def main():
                 "windows": [int(summ.get("windows", 0)), int(summ.get("windows_y", 0))],
                 "window_ps": [int(summ.get("window_ps_x", 0)), int(summ.get("window_ps_y", 0))],
             },
-            # every rerun is exact but slow: reported, and the bench refuses to report a
-            # configs[1] number that needed one
-            "reruns": {"retries": int(summ.get("retries", 0)), "fallbacks": int(summ.get("fallbacks", 0))},
+            # every rerun is exact but slow: counted over the timed steps (gnoc_summary's
+            # totals since submit), and the bench refuses a configs[1] number that needed one
+            "reruns": reruns,
+            "settle_runs": m["settle_runs"],
+            "build_id": bid,
             "e2e_ms_per_step": e2e_ms,
             "e2e_note": "submit from pinned host memory (H2D + device-side trace checks) + run + final_ps D2H",
             "roofline": {
                 "bound": "hbm",
-                "achieved": achieved,
+                "achieved": rf["achieved"],
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": pmc_traffic(workload, dom) if world == 1 else None,
-                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/" + PMC_FILE + ")",
-                "algorithmic_bytes_per_launch": alg_bytes / max(port_launches, 1),
-                "kernel": dom,
-                "kernel_launches": port_launches,
-                "kernel_avg_us": port_ms * 1e3 / max(port_launches, 1),
+                "frac": rf["frac"],
+                "traffic": pmc_traffic(workload, rf["kernel"], bid) if world == 1 else None,
+                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/" + PMC_FILE +
+                                ", same build_id only)",
+                "algorithmic_bytes_per_launch": rf["alg_bytes_per_launch"],
+                "kernel": rf["kernel"],
+                "kernel_launches": rf["launches"],
+                "kernel_avg_us": rf["kernel_avg_us"],
                 "whole_job_frac_per_gpu": whole_job_gbs / HBM_PEAK_GBS,
                 "scope": "rank 0's launches and its share of the hops",
             },
             "kernel_ms": {k: round(v[0], 4) for k, v in kst.items()},
             "trace_gen_s": round(gen_s, 2),
         }
+        if hot_line is not None:
+            line["hotspot"] = hot_line
         if a.cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(a, W, H, load, hot)
         print(json.dumps(line), flush=True)
-        if wl == "mesh" and (summ.get("fallbacks") or summ.get("retries") or int(summ.get("engine_path", -1)) != 4):
-            print(f"bench: the batch needed reruns {line['reruns']} or left the chain engine "
-                  f"(engine_path {summ.get('engine_path')})", file=sys.stderr)
+        bad = [ln for ln in [line] + ([hot_line] if hot_line else [])
+               if ln["reruns"]["retries"] or ln["reruns"]["fallbacks"] or
+               int(ln.get("engine_path", ln.get("config", {}).get("engine_path", -1))) != 4]
+        if wl == "mesh" and bad:
+            print(f"bench: a timed step needed reruns {[b['reruns'] for b in bad]} or left the chain engine", file=sys.stderr)
             sys.exit(3)
 
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def measure(eng, a, barrier_sync, settle_fixed=False):
+    """Settle the chain windows, W warmup runs, then EXACTLY K timed runs between
+    barrier + synchronize; then one profiled run for per-kernel device times (HIP
+    events on the engine's stream).  Reruns are counted over the timed runs from
+    gnoc_summary's totals since submit."""
+    settle = 0
+    # window adaptation (engine.hip adapt_windows): the first runs of a batch size the
+    # chain windows from the fill they measure; runs until one needed no rerun and used
+    # the windows of the run before (a sharded engine runs a fixed count: every rank
+    # must call the same collectives)
+    prev = None
+    for settle in range(1, 9):
+        eng.run()
+        sm = eng.summary()
+        cur = (sm["windows"], sm["windows_y"], sm["window_ps_x"], sm["window_ps_y"])
+        if settle_fixed and settle >= 3:
+            break
+        if not settle_fixed and sm["retries"] == 0 and sm["fallbacks"] == 0 and cur == prev:
+            break
+        prev = cur
+    for _ in range(a.warmup):
+        eng.run()
+    s0 = eng.summary()
+    barrier_sync()
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        eng.run()
+    barrier_sync()
+    elapsed = time.perf_counter() - t_start
+    s1 = eng.summary()
+    reruns = {"retries": int(s1["retries_total"] - s0["retries_total"]),
+              "fallbacks": int(s1["fallbacks_total"] - s0["fallbacks_total"]),
+              "timed_runs": int(s1["runs"] - s0["runs"])}
+    eng.set_profiling(True)
+    eng.run()
+    kst = eng.kernel_stats()
+    eng.set_profiling(False)
+    return {"elapsed": elapsed, "summary": s1, "kst": kst, "reruns": reruns, "settle_runs": settle}
+
+
+def roofline(kst, pc, summ, my_pkts):
+    """Dominant kernel (most device time on this rank): k_chain (v4: the X and Y port
+    chains), k_level (the chunked levels; on v4 the injection and SELF levels only) or
+    k_port_stream (v1).  Algorithmic bytes of ITS launches: 32 B per
+    hop record it moves -- k_chain: the mesh hops at RIGHT/LEFT/UP/DOWN ports; the
+    level kernels: every hop record + 24 B per delivered packet."""
+    dom = max(("k_chain", "k_level", "k_port_stream"), key=lambda k: kst.get(k, (0.0, 0))[0])
+    port_ms, launches = kst.get(dom, (0.0, 0))
+    my_hops = int(pc[:, :5].sum())
+    if dom == "k_chain":
+        alg = int(pc[:, 1:5].sum()) * BYTES_PER_HOP
+    elif int(summ.get("engine_path", 0)) == 4:   # v4 but k_level dominant: injection + SELF levels
+        alg = (int(pc[:, 0].sum()) + int(pc[:, 5].sum())) * BYTES_PER_HOP + my_pkts * BYTES_PER_PKT
+    else:
+        alg = my_hops * BYTES_PER_HOP + my_pkts * BYTES_PER_PKT
+    achieved = alg / (port_ms * 1e-3) / 1e9 if port_ms > 0 else 0.0
+    return {"kernel": dom, "achieved": achieved, "frac": achieved / HBM_PEAK_GBS, "launches": launches,
+            "kernel_avg_us": port_ms * 1e3 / max(launches, 1), "alg_bytes_per_launch": alg / max(launches, 1)}
+
+
+def build_id():
+    from graphite_amd import gnoc
+    lib = gnoc.load()
+    return lib.gnoc_build_id().decode() if hasattr(lib, "gnoc_build_id") else None
 
 
 def sweep_points():
@@ -363,20 +429,20 @@ def pinned_trace(tr):
                       pin(tr.flags if tr.flags is not None else np.zeros(len(tr), np.uint32)))
 
 
-PMC_FILE = "r2_pmc.json"
+PMC_FILE = "r3_pmc.json"
 
 
-def pmc_traffic(workload, kernel):
+def pmc_traffic(workload, kernel, bid):
     """HBM bytes per launch of the dominant kernel, from the committed PMC passes
-    (tools/gpu_round.sh -> tools/prof_summary.py) of this same workload; None if
-    no profile of this workload and kernel is committed."""
+    (tools/gpu_round.sh -> tools/prof_summary.py) of this same workload AND this same
+    build (gnoc_build_id); None if no such profile is committed."""
     p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", PMC_FILE)
     try:
         with open(p) as fh:
             d = json.load(fh)
     except (OSError, ValueError):
         return None
-    if d.get("workload") != workload or d.get("kernel") != kernel:
+    if d.get("workload") != workload or d.get("kernel") != kernel or not bid or d.get("build_id") != bid:
         return None
     return d.get("traffic_bytes_per_launch")
 

@@ -9,10 +9,11 @@
 // a few "insert" slots written by earlier phases (IN_LOCAL for X ports; IN_LOCAL,
 // IN_W, IN_E for Y ports).
 //
-// Time is cut into windows [w D, (w+1) D), the last one unbounded; D per phase,
+// Time is cut into windows [w D, (w+1) D), the last one unbounded; D per chain,
 // sized from the batch's busiest port and then from the fill the previous run
-// measured (engine.hip choose_windows / adapt_windows).  One workgroup task = (chain, window): it walks the chain's ports
-// in order, keeping the window's arrival stream in LDS:
+// measured (engine.hip choose_windows / adapt_windows).  One task = (chain,
+// window) = one wave: it walks the chain's ports in order, keeping the window's
+// arrival stream in LDS:
 //   port i:  stream (sorted)  --FIFO max-plus scan-->  departures
 //            continuing departures with t' < window end stay in LDS and are
 //            merged with port i+1's inserts of this window; the rest turn
@@ -24,6 +25,15 @@
 // (8-byte epoch-tagged granules, sc1 stores and loads, MI355X_MICROARCH.md
 // "Valid forms").  Tasks are handed out window-major, strictly in order to
 // running workgroups, so a task's predecessor is always running or done.
+//
+// A step (one port of one task) works on ROWS: the merged stream in 64-record
+// rows, record 64 r + lane in lane `lane` of row r.  The merge of the kept list
+// and the inserts is a bitmap over merged positions (each insert's position =
+// its rank in the kept list + its index), so every lane finds its record with
+// one mbcnt and every row loads with independent LDS reads; a row is scanned
+// with DPP (max-plus), route ranks come from ballots + mbcnt, so one row's
+// turning records of one direction land on consecutive HBM addresses and the
+// kept records on consecutive LDS entries.
 //
 // The history tree's serial state (queue_model_history_tree.cc:58-64) only
 // matters while a queue has never idled; without the M/G/1 branch it is the
@@ -40,18 +50,17 @@ namespace ch {
 // registers, and LDS needs no barriers (a wave's LDS operations execute in
 // program order).
 constexpr int T = 64;
-#ifndef CH_PER_V
-#define CH_PER_V 11
+#ifndef CH_ROWS_V
+#define CH_ROWS_V 11
 #endif
-constexpr int PER = CH_PER_V;             // stream records per lane
-constexpr int CAP = PER * T;              // stream records per (port, window)
-#ifndef CH_IPER_V
-#define CH_IPER_V 2
-#endif
-constexpr int IPER = CH_IPER_V;
-constexpr int ICAP = IPER * T;            // inserts per (port, window), + spill-ins of the slow path
+constexpr int ROWS = CH_ROWS_V;           // stream rows per (port, window)
+constexpr int CAP = ROWS * T;             // stream records per (port, window)
+constexpr int IROWS = 2;
+constexpr int ICAP = IROWS * T;           // inserts per (port, window); spill-ins of the slow path
+constexpr int SBN = CAP + ICAP;           // stream buffer: kept [0, CAP), inserts [CAP, CAP + ICAP)
+constexpr int BMW = CAP / 32;             // insert bitmap words over merged positions
 #ifndef CH_MINW
-#define CH_MINW 3                         // waves per SIMD the registers must leave room for
+#define CH_MINW 4                         // waves per SIMD the registers must leave room for
 #endif
 constexpr int NLMAX = 3;                  // local insert lists (Y ports: LOCAL, W, E)
 constexpr int SW = 8;                     // state words per (chain port, window)
@@ -60,16 +69,14 @@ constexpr uint32_t F_FALLBACK = 2u;       // M/G/1 would fire, exception tails, 
 constexpr uint32_t F_ROUTE = 4u;          // route-count invariant broken (internal error)
 constexpr uint32_t F_TIMEOUT = 8u;        // a hand-off wait timed out
 constexpr uint32_t F_ANY = F_RETRY | F_FALLBACK | F_ROUTE | F_TIMEOUT;
+// why a chain run declined (bits above F_ANY; reported with GNOC_CHAIN_DEBUG=1)
+enum : uint32_t { R_OFFSET = 1u << 8, R_TAIL = 1u << 9, R_SPILLIN = 1u << 10, R_LASTSPILL = 1u << 11, R_MG1 = 1u << 12,
+                  R_EXC = 1u << 13, R_OVF_INS = 1u << 14, R_OVF_STREAM = 1u << 15 };
 constexpr uint64_t SPIN_CYCLES = 1ull << 31;
 constexpr uint64_t M48 = (1ull << 48) - 1;
 constexpr uint64_t OFF_LIM = (1ull << 32) - 4096;   // time offsets within a window (32-bit cycle math)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-
-// LDS index padding of the kept list: one u64 per 32 entries, so the lanes'
-// segments (stride about PER) hit distinct banks.
-__host__ __device__ constexpr uint32_t pad(uint32_t r) { return r + (r >> 5); }
-constexpr int CAPP = CAP + CAP / 32 + 1;   // + the ~0 behind a full list
-
+static_assert(BMW <= T && CAP % 64 == 0, "bitmap words: one per lane");
 
 // Route-count fields of a chain port's outputs: SELF, the chain direction, UP,
 // DOWN (an X port never sends the opposite X way; a Y port only SELF or on).
@@ -91,16 +98,21 @@ __device__ __forceinline__ uint32_t route_field(uint32_t nx, uint32_t ny, uint32
 }  // namespace ch
 
 // One port of a chain (k_chain_plan): output slots of the next tile per route
-// field, insert slots of this port.  128 bytes: one wave copies it.
+// field, insert slots of this port, as record indices (the chain engine runs only
+// while the record buffer has fewer than 2^32 records).  128 bytes: a wave loads
+// it as one dword per lane (lanes 0-31; lanes 32-37 load the insert bounds of the
+// window, ch::load_pd).
 struct __attribute__((aligned(16))) ChainPort
 {
-   uint64_t obase[4];    // output slot base per field (SELF, cont, UP, DOWN)
-   uint64_t ibase[3];    // insert slot bases (IN_LOCAL, IN_W, IN_E)
-   uint32_t ocap[4];     // output slot capacities
-   uint32_t icnt[3];     // insert slot record counts
-   uint32_t port, tile, dir, cont;   // cont: the chain direction
-   uint32_t nx, ny, rl, nl;          // next tile, R + Lk (ps), local insert lists
-   uint32_t pad0[3];
+   uint32_t obase[4];    // [0-3]   output slot first record per field (SELF, cont, UP, DOWN)
+   uint32_t ocap[4];     // [4-7]   output slot capacities
+   uint32_t ibase[3];    // [8-10]  insert slots (IN_LOCAL, IN_W, IN_E): first record
+   uint32_t icnt[3];     // [11-13] insert slot record counts
+   uint32_t port;        // [14]    tile * PORTS + dir (counters)
+   uint32_t nx, ny;      // [15-16] next tile
+   uint32_t rl;          // [17]    R + Lk (ps)
+   uint32_t tile, dir, cont, nl;   // [18-21] (k_win_bounds, debugging)
+   uint32_t pad0[10];
 };
 static_assert(sizeof(ChainPort) == 128, "ChainPort is one 128-B line");
 
@@ -146,21 +158,14 @@ struct ChainArgs
 
 namespace ch {
 
+// The stream buffer of one wave: the kept list (records continuing from the
+// previous port, sorted, rewritten in place by this port) at [0, CAP), this
+// port's inserts at [CAP, CAP + ICAP); keys (t - wbase) << 32 | id.
 struct Smem
 {
-   // Port i's stream is the (t, id)-merge of two sorted lists, never materialised:
-   // the records kept from port i-1 (rewritten in place by port i: every read of
-   // the list precedes every write) and port i's inserts (double buffered by port
-   // parity: port i+1's land while port i runs).  ~0 sits behind each list's end.
-   uint64_t kkey[CAPP];           // kept: (t - wbase) << 32 | id
-   uint32_t kaux[CAPP];           // dx | dy << 10 | F << 20
-   uint64_t ikey[2][ICAP + 1];    // inserts
-   uint32_t iaux[2][ICAP + 1];
-   uint64_t rkey[ICAP + 1];       // Y ports' three fetched slot ranges (premerge -> ikey); the slow
-   uint32_t raux[ICAP + 1];       // path's inserts + spill-ins
-   ChainPort cp[3];               // ports i, i+1, i+2 (ring)
-   uint32_t blo[2][NLMAX], bhi[2][NLMAX];   // window bounds of ports i+1, i+2 (ring)
-   uint32_t ioffs[2][NLMAX + 1];  // offsets of a port's local insert lists (by port parity)
+   uint64_t key[SBN];
+   uint32_t aux[SBN];             // dx | dy << 10 | F << 20
+   uint32_t bm[BMW];              // merged positions of the inserts (bitmap)
 };
 
 __device__ __forceinline__ uint64_t ld1(const uint64_t* p)
@@ -173,25 +178,7 @@ __device__ __forceinline__ void st1(uint64_t* p, uint64_t v)
 }
 // Compiler-only ordering point between LDS phases of the one wave.
 __device__ __forceinline__ void wsync() { asm volatile("" ::: "memory"); }
-__device__ __forceinline__ uint32_t cf(uint64_t c, uint32_t f) { return (uint32_t) ((c >> (16 * f)) & 0xFFFFu); }
 
-// Max-plus aggregate of a run of requests: X -> max(X + A, B); C = route counts
-// (4 x 16-bit fields).  (A, B) of one request: (F, tc + F), cycles relative to
-// the window's base cycle (32-bit).
-struct Agg
-{
-   uint32_t A, B;
-   uint64_t C;
-};
-__device__ __forceinline__ Agg agg_op(const Agg& x, const Agg& y)   // x, then y
-{
-   Agg r;
-   r.A = x.A + y.A;
-   const uint32_t nb = x.B + y.A;
-   r.B = nb > y.B ? nb : y.B;
-   r.C = x.C + y.C;
-   return r;
-}
 template <int CTRL, int RM, int BM>
 __device__ __forceinline__ uint32_t dpp32(uint32_t v)
 {
@@ -203,28 +190,27 @@ __device__ __forceinline__ uint64_t dpp64(uint64_t v)
    const uint32_t lo = dpp32<CTRL, RM, BM>((uint32_t) v), hi = dpp32<CTRL, RM, BM>((uint32_t) (v >> 32));
    return (uint64_t) lo | ((uint64_t) hi << 32);
 }
-// The identity (0, 0, 0) is what DPP leaves in lanes without a source (B >= 0).
-template <int CTRL, int RM, int BM>
-__device__ __forceinline__ Agg dpp_agg(const Agg& v)
+// One level of the inclusive max-plus scan of (A, B) pairs, X -> max(X + A, B)
+// (cycles relative to the window's base cycle); the identity (0, 0) is what DPP
+// leaves in lanes without a source (B >= A >= 0 for every aggregate).
+template <int CTRL, int RM>
+__device__ __forceinline__ void scan_lvl(uint32_t& A, uint32_t& B)
 {
-   Agg r;
-   r.A = dpp32<CTRL, RM, BM>(v.A);
-   r.B = dpp32<CTRL, RM, BM>(v.B);
-   r.C = dpp64<CTRL, RM, BM>(v.C);
-   return r;
+   const uint32_t pa = dpp32<CTRL, RM, 0xF>(A), pb = dpp32<CTRL, RM, 0xF>(B);
+   const uint32_t nb = pb + A;
+   B = nb > B ? nb : B;
+   A += pa;
 }
 // Inclusive wave scan (GFX9 DPP: row_shr 1, 2, 4, 8; row_bcast 15, 31).
-__device__ __forceinline__ Agg wave_scan(Agg v)
+__device__ __forceinline__ void wave_scan(uint32_t& A, uint32_t& B)
 {
-   v = agg_op(dpp_agg<0x111, 0xF, 0xF>(v), v);
-   v = agg_op(dpp_agg<0x112, 0xF, 0xF>(v), v);
-   v = agg_op(dpp_agg<0x114, 0xF, 0xF>(v), v);
-   v = agg_op(dpp_agg<0x118, 0xF, 0xF>(v), v);
-   v = agg_op(dpp_agg<0x142, 0xA, 0xF>(v), v);
-   v = agg_op(dpp_agg<0x143, 0xC, 0xF>(v), v);
-   return v;
+   scan_lvl<0x111, 0xF>(A, B);
+   scan_lvl<0x112, 0xF>(A, B);
+   scan_lvl<0x114, 0xF>(A, B);
+   scan_lvl<0x118, 0xF>(A, B);
+   scan_lvl<0x142, 0xA>(A, B);
+   scan_lvl<0x143, 0xC>(A, B);
 }
-// Wave sums (same DPP pattern); the total is in lane 63.
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v)
 {
    v += dpp32<0x111, 0xF, 0xF>(v);
@@ -245,15 +231,15 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
    v += dpp64<0x143, 0xC, 0xF>(v);
    return v;
 }
-__device__ __forceinline__ uint32_t sgpr(uint32_t v) { return (uint32_t) __builtin_amdgcn_readfirstlane((int) v); }
-__device__ __forceinline__ uint64_t sgpr64(uint64_t v)
-{
-   return (uint64_t) sgpr((uint32_t) v) | ((uint64_t) sgpr((uint32_t) (v >> 32)) << 32);
-}
 __device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return (uint32_t) __builtin_amdgcn_readlane((int) v, l); }
 __device__ __forceinline__ uint64_t rdl64(uint64_t v, int l)
 {
    return (uint64_t) rdl((uint32_t) v, l) | ((uint64_t) rdl((uint32_t) (v >> 32), l) << 32);
+}
+// Lanes below this one with their bit set in m.
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m)
+{
+   return __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
 }
 
 // Lower bound (number of entries < k) in the sorted u64 array a[0, n), by
@@ -283,30 +269,20 @@ __device__ __forceinline__ bool flagged(const ChainArgs& a)
    return (__hip_atomic_load(a.errflag + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & F_ANY) != 0;
 }
 
-// A 128-B port descriptor: 32 lanes, one dword each.  The prefetch splits into
-// the load a step ahead (register) and the LDS store at the next step.
-__device__ __forceinline__ void load_cp(ChainPort* dst, const ChainPort* src, uint32_t l)
+// Port descriptor fields (lanes 0-31 of a "pd" register) and the port's insert
+// bounds of window w (lanes 32 + j: first record of list j, 32 + nl + j: end).
+enum : int { PD_OBASE = 0, PD_OCAP = 4, PD_IBASE = 8, PD_ICNT = 11, PD_PORT = 14, PD_NX = 15, PD_NY = 16, PD_RL = 17,
+             PD_LO = 32 };
+template <int NL>
+__device__ __forceinline__ uint32_t load_pd(const ChainArgs& a, uint32_t cpi, uint64_t bt_off, uint32_t nW, uint32_t i,
+                                            uint32_t w)
 {
-   reinterpret_cast<uint32_t*>(dst)[l] = reinterpret_cast<const uint32_t*>(src)[l];
-}
-__device__ __forceinline__ uint32_t fetch_cp(const ChainPort* src, uint32_t l)
-{
-   return reinterpret_cast<const uint32_t*>(src)[l];
-}
-__device__ __forceinline__ void put_cp(ChainPort* dst, uint32_t v, uint32_t l) { reinterpret_cast<uint32_t*>(dst)[l] = v; }
-// Window bounds [lo, hi) of the insert slots of port i of a chain whose bounds
-// block starts at bt_off (l < 2 nl).
-__device__ __forceinline__ uint32_t fetch_bounds(const ChainArgs& a, uint64_t bt_off, uint32_t nW, uint32_t i, uint32_t nl,
-                                                 uint32_t w, uint32_t l)
-{
-   if (l >= 2 * nl) return 0u;
-   const uint32_t j = l < nl ? l : l - nl;
-   return a.bt[bt_off + ((uint64_t) i * nl + j) * (nW + 1) + w + (l < nl ? 0u : 1u)];
-}
-__device__ __forceinline__ void put_bounds(Smem& sm, uint32_t slot, uint32_t v, uint32_t nl, uint32_t l)
-{
-   if (l < nl) sm.blo[slot][l] = v;
-   else if (l < 2 * nl) sm.bhi[slot][l - nl] = v;
+   const uint32_t lane = threadIdx.x;
+   if (lane < 32) return reinterpret_cast<const uint32_t*>(a.cp + cpi)[lane];
+   const uint32_t l = lane - 32;
+   if (l >= 2u * NL) return 0u;
+   const uint32_t j = l < (uint32_t) NL ? l : l - NL;
+   return a.bt[bt_off + ((uint64_t) i * NL + j) * (nW + 1) + w + (l < (uint32_t) NL ? 0u : 1u)];
 }
 
 // Poll the state words [0, nw) of block s until all carry the epoch tag (lane
@@ -330,32 +306,39 @@ __device__ bool poll_words(const ChainArgs& a, const uint64_t* s, uint32_t nw, u
    }
 }
 
-// Issue the loads of a port's local inserts of this window (registers); off =
-// the lists' offsets in the port's insert list (uniform).
+// A port's insert lists of this window: [lo_j, hi_j) of list j, clamped to the
+// slot (bounds come from sorted slots; nothing can load out of range).
 template <int NL>
-__device__ __forceinline__ uint32_t fetch_inserts(Smem& sm, const ChainArgs& a, uint32_t ring, uint32_t br,
-                                                  Rec (&iv)[IPER], uint32_t parity)
+struct Ins
 {
-   const uint32_t lane = threadIdx.x;
-   const ChainPort& P = sm.cp[ring];
-   uint32_t lo[NL], off[NL + 1];
-   uint64_t base[NL];
-   off[0] = 0;
+   uint32_t off[NL + 1];
+   uint32_t base[NL];
+};
+template <int NL>
+__device__ __forceinline__ Ins<NL> ins_lists(uint32_t pd)
+{
+   Ins<NL> L;
+   L.off[0] = 0;
 #pragma unroll
    for (int j = 0; j < NL; j++)
    {
-      // bounds come from sorted slots; clamped so that nothing can load out of range
-      const uint32_t cnt = sgpr(P.icnt[j]);
-      lo[j] = min(sgpr(sm.blo[br][j]), cnt);
-      const uint32_t hi = min(max(sgpr(sm.bhi[br][j]), lo[j]), cnt);
-      off[j + 1] = off[j] + (hi - lo[j]);
-      base[j] = sgpr64(P.ibase[j]) + lo[j];
+      const uint32_t cnt = rdl(pd, PD_ICNT + j);
+      const uint32_t lo = min(rdl(pd, PD_LO + j), cnt);
+      const uint32_t hi = min(max(rdl(pd, PD_LO + NL + j), lo), cnt);
+      L.off[j + 1] = L.off[j] + (hi - lo);
+      L.base[j] = rdl(pd, PD_IBASE + j) + lo;
    }
-   const uint32_t itot = off[NL];
-   // the lists' offsets, for premerge (LDS: no scalar registers held across the step)
-   if (NL > 1 && lane <= (uint32_t) NL) sm.ioffs[parity][lane] = off[lane < (uint32_t) NL ? lane : NL];
+   return L;
+}
+// Issue the loads of a port's inserts of this window (registers); returns their count.
+template <int NL>
+__device__ __forceinline__ uint32_t fetch_inserts(const ChainArgs& a, uint32_t pd, Rec (&iv)[IROWS])
+{
+   const uint32_t lane = threadIdx.x;
+   const Ins<NL> L = ins_lists<NL>(pd);
+   const uint32_t itot = L.off[NL];
 #pragma unroll
-   for (int q = 0; q < IPER; q++)
+   for (int q = 0; q < IROWS; q++)
    {
       const uint32_t g = lane + (uint32_t) q * T;
       iv[q].t = 0;
@@ -366,68 +349,70 @@ __device__ __forceinline__ uint32_t fetch_inserts(Smem& sm, const ChainArgs& a, 
          uint32_t j = 0;
 #pragma unroll
          for (int l = 1; l < NL; l++)
-            if (g >= off[l]) j = (uint32_t) l;
-         iv[q] = a.recs[base[j] + (g - off[j])];
+            if (g >= L.off[l]) j = (uint32_t) l;
+         iv[q] = a.recs[(uint64_t) L.base[j] + (g - L.off[j])];
       }
    }
    return itot;
 }
 
-// Fetched inserts into LDS as keys relative to wbase: X ports (one slot)
-// straight into insert list `buf`, Y ports into the staging lists (premerge).
+// Fetched inserts (itot <= ICAP) into the insert region as keys relative to
+// wbase.  Y ports' three lists land concatenated and are then merged in place
+// (own index + lower bounds in the other two lists).  True if a time offset
+// leaves the window's 32-bit range.
 template <int NL>
-__device__ __forceinline__ bool store_inserts(Smem& sm, const Rec (&iv)[IPER], uint32_t itot, uint64_t wbase, uint32_t buf)
+__device__ __forceinline__ bool land_inserts(Smem& sm, const Rec (&iv)[IROWS], uint32_t itot, uint64_t wbase, uint32_t pd)
 {
    const uint32_t lane = threadIdx.x;
    bool bad = false;
-   uint64_t* K = NL > 1 ? sm.rkey : sm.ikey[buf];
-   uint32_t* X = NL > 1 ? sm.raux : sm.iaux[buf];
+   uint64_t k[IROWS];
 #pragma unroll
-   for (int q = 0; q < IPER; q++)
+   for (int q = 0; q < IROWS; q++)
    {
       const uint32_t g = lane + (uint32_t) q * T;
-      if (g < itot && g < (uint32_t) ICAP)
+      const uint64_t dt = iv[q].t - wbase;
+      k[q] = (dt << 32) | iv[q].id;
+      if (g < itot)
       {
-         const uint64_t dt = iv[q].t - wbase;
          bad |= dt >= OFF_LIM;
-         K[g] = (dt << 32) | iv[q].id;
-         X[g] = iv[q].aux;
+         sm.key[CAP + g] = k[q];
+         if (NL == 1) sm.aux[CAP + g] = iv[q].aux;
       }
    }
-   if (NL == 1 && lane == 0 && itot <= (uint32_t) ICAP) K[itot] = ~0ull;
-   return __any(bad);
-}
-
-// Y ports: the staged slot ranges (each sorted) merged into insert list `buf`:
-// own index + lower bounds in the other two ranges.
-template <int NL>
-__device__ __forceinline__ void premerge(Smem& sm, uint32_t itot, uint32_t buf, uint32_t parity)
-{
-   if (NL == 1) return;
-   const uint32_t lane = threadIdx.x;
-   wsync();
-   uint32_t o[NL + 1];
-#pragma unroll
-   for (int l = 0; l <= NL; l++) o[l] = sm.ioffs[parity][l];
-#pragma unroll
-   for (int q = 0; q < IPER; q++)
+   if (NL > 1)
    {
-      const uint32_t g = lane + (uint32_t) q * T;
-      if (g >= itot || g >= (uint32_t) ICAP) continue;
-      const uint64_t k = sm.rkey[g];
-      uint32_t own = 0;
+      const Ins<NL> L = ins_lists<NL>(pd);
+      wsync();
+      uint32_t pos[IROWS];
 #pragma unroll
-      for (int l = 1; l < NL; l++)
-         if (g >= o[l]) own = (uint32_t) l;
-      uint32_t pos = g - o[own];
+      for (int q = 0; q < IROWS; q++)
+      {
+         const uint32_t g = lane + (uint32_t) q * T;
+         uint32_t own = 0;
 #pragma unroll
-      for (int l = 0; l < NL; l++)
-         if ((uint32_t) l != own) pos += lb(sm.rkey + o[l], o[l + 1] - o[l], k);
-      sm.ikey[buf][pos] = k;
-      sm.iaux[buf][pos] = sm.raux[g];
+         for (int l = 1; l < NL; l++)
+            if (g >= L.off[l]) own = (uint32_t) l;
+         uint32_t p = g - L.off[own];
+#pragma unroll
+         for (int l = 0; l < NL; l++)
+            if ((uint32_t) l != own) p += lb(sm.key + CAP + L.off[l], L.off[l + 1] - L.off[l], k[q]);
+         pos[q] = p;
+      }
+      // every lane's searches precede every write (one wave: LDS in program order)
+      wsync();
+#pragma unroll
+      for (int q = 0; q < IROWS; q++)
+      {
+         const uint32_t g = lane + (uint32_t) q * T;
+         if (g < itot)
+         {
+            sm.key[CAP + pos[q]] = k[q];
+            sm.aux[CAP + pos[q]] = iv[q].aux;
+         }
+      }
    }
-   if (lane == 0 && itot <= (uint32_t) ICAP) sm.ikey[buf][itot] = ~0ull;
    wsync();
+   return __any(bad);
 }
 
 // Cycles of a stream record relative to the window base cycle wb = max(wq - 1, 0):
@@ -438,146 +423,82 @@ __device__ __forceinline__ uint32_t rcyc(uint32_t off, uint32_t wr, uint32_t d0)
    return (wr + off + 999u) / 1000u + d0;
 }
 
-// Merge path: how many inserts are among the first d records of the merged
-// (kept K[0, nK), inserts I[0, nI)) stream.  Binary lifting over the insert
-// list (the short one), no divergence; keys are unique (one record per packet
-// per port).
-__device__ __forceinline__ uint32_t mp_split(const uint64_t* K, uint32_t nK, const uint64_t* I, uint32_t nI, uint32_t d)
-{
-   const uint32_t lo = d > nK ? d - nK : 0u, hi = d < nI ? d : nI;
-   uint32_t pos = lo;
-   for (uint32_t step = nI ? 1u << (31 - __builtin_clz(nI)) : 0u; step; step >>= 1)
-   {
-      const uint32_t q = pos + step;
-      const bool in = q <= hi;
-      // insert q-1 precedes kept record d-q: it is among the first d
-      const uint64_t vi = I[in ? q - 1 : 0u], vk = K[pad(in ? d - q : 0u)];
-      pos = (in && vi < vk) ? q : pos;
-   }
-   return pos;
-}
-
-// This lane's records of the merged stream (kept from x, inserts from y; cnt
-// of them) into registers, and their aggregate.
-template <bool XC>
-__device__ __forceinline__ Agg walk(const uint64_t* K, const uint32_t* KA, const uint64_t* I, const uint32_t* IA,
-                                   uint32_t x, uint32_t y, uint32_t cnt, uint32_t wr, uint32_t d0, uint32_t nx,
-                                   uint32_t ny, uint32_t cont, uint64_t (&rk)[PER], uint32_t (&ra)[PER], uint32_t& yend)
-{
-   Agg g;
-   g.A = 0;
-   g.B = 0;
-   g.C = 0;
-   uint64_t kx = K[pad(x)], ky = I[y];   // the heads (~0 behind each list's end)
-#pragma unroll
-   for (int j = 0; j < PER; j++)
-   {
-      rk[j] = 0;
-      ra[j] = 0;
-      if ((uint32_t) j < cnt)
-      {
-         const bool tk = kx < ky;
-         rk[j] = tk ? kx : ky;
-         ra[j] = *(tk ? KA + pad(x) : IA + y);
-         x += tk ? 1u : 0u;
-         y += tk ? 0u : 1u;
-         const uint64_t h = *(tk ? K + pad(x) : I + y);
-         kx = tk ? h : kx;
-         ky = tk ? ky : h;
-         const uint32_t p = aux_F(ra[j]);
-         const uint32_t nb = g.B + p, b2 = rcyc((uint32_t) (rk[j] >> 32), wr, d0) + p;
-         g.B = nb > b2 ? nb : b2;
-         g.A += p;
-         g.C += 1ull << (16 * route_field<XC>(nx, ny, ra[j]));
-      }
-   }
-   yend = y;
-   return g;
-}
-
-// Spill-ins of this port (slow path): [Kpp, Pep) of its chain slot, written by
-// earlier windows at the previous port (sorted: FIFO departure order).  Those
-// with t in this window join the port's insert list: (I, nI) and they merge into
-// the staging list.  Returns the records taken; skip = those consumed by
-// earlier windows.
-__device__ uint32_t spill_in(Smem& sm, const ChainArgs& a, uint64_t sbase, uint32_t spn, const uint64_t* I,
-                             const uint32_t* IA, uint32_t nI, uint32_t nK, uint64_t wbase, uint64_t wlen, uint32_t& skip)
+// The merged stream in rows: kept [0, nK), inserts [IB, IB + nI) (both sorted).
+// Each insert's merged position is its rank among the kept records + its index;
+// those positions form a bitmap, and the record of merged position 64 r + lane
+// is insert (inserts before it) or kept record (position - inserts before it).
+template <int RW>
+__device__ __forceinline__ void load_rows(Smem& sm, uint32_t nK, uint32_t IB, uint32_t nI, uint64_t (&rk)[RW],
+                                          uint32_t (&ra)[RW])
 {
    const uint32_t lane = threadIdx.x;
-   Rec sv[IPER];
-   uint32_t nb = 0, nt = 0;
-#pragma unroll
-   for (int q = 0; q < IPER; q++)
+   const uint32_t n = nK + nI;
+   uint32_t bmv = 0;
+   if (nI)
    {
-      const uint32_t g = lane + (uint32_t) q * T;
-      sv[q].t = 0;
-      sv[q].id = 0;
-      sv[q].aux = 0;
-      if (g < spn)
+      if (lane < (uint32_t) BMW) sm.bm[lane] = 0u;
+      // (at most ICAP inserts, or up to CAP spill-ins on the slow path)
+      for (uint32_t m0 = 0; m0 < nI; m0 += T)
       {
-         const uint64_t* r = reinterpret_cast<const uint64_t*>(a.recs + sbase + g);
-         sv[q].t = ld1(r);
-         const uint64_t ia = ld1(r + 1);
-         sv[q].id = (uint32_t) ia;
-         sv[q].aux = (uint32_t) (ia >> 32);
-         nb += sv[q].t < wbase ? 1u : 0u;
-         nt += (sv[q].t >= wbase && sv[q].t - wbase < wlen) ? 1u : 0u;
+         const uint32_t m = m0 + lane;
+         if (m < nI)
+         {
+            const uint32_t P = lb(sm.key, nK, sm.key[IB + m]) + m;
+            atomicOr(&sm.bm[P >> 5], 1u << (P & 31));
+         }
       }
+      wsync();
+      if (lane < (uint32_t) BMW) bmv = sm.bm[lane];
    }
-   skip = rdl(wave_sum32(nb), 63);
-   const uint32_t take = rdl(wave_sum32(nt), 63);
-   if (!take) return 0;
-   // staged right behind the kept list's end (the caller checked the room)
-   uint64_t* const sk = sm.kkey + pad(nK) + 1;
-   uint32_t* const sa = sm.kaux + pad(nK) + 1;
+   uint32_t ib = 0;
 #pragma unroll
-   for (int q = 0; q < IPER; q++)
+   for (int r = 0; r < RW; r++)
    {
-      const uint32_t g = lane + (uint32_t) q * T;
-      if (g < spn && sv[q].t >= wbase && sv[q].t - wbase < wlen)
-      {
-         sk[g - skip] = ((sv[q].t - wbase) << 32) | sv[q].id;
-         sa[g - skip] = sv[q].aux;
-      }
+      if ((uint32_t) r * T >= n) break;
+      const uint64_t M = (uint64_t) rdl(bmv, 2 * r) | ((uint64_t) rdl(bmv, 2 * r + 1) << 32);
+      const uint32_t p = (uint32_t) r * T + lane;
+      const uint32_t before = ib + mbcnt(M);
+      const bool isI = (M >> lane) & 1u;
+      uint32_t idx = isI ? IB + before : p - before;
+      idx = p < n ? idx : 0u;
+      rk[r] = sm.key[idx];
+      ra[r] = sm.aux[idx];
+      ib += (uint32_t) __popcll(M);
    }
-   wsync();
-#pragma unroll
-   for (int q = 0; q < IPER; q++)
-   {
-      const uint32_t g = lane + (uint32_t) q * T;
-      if (g < take)
-      {
-         const uint64_t k = sk[g];
-         const uint32_t p = g + lb(I, nI, k);
-         sm.rkey[p] = k;
-         sm.raux[p] = sa[g];
-      }
-      if (g < nI)
-      {
-         const uint64_t k = I[g];
-         const uint32_t p = g + lb(sk, take, k);
-         sm.rkey[p] = k;
-         sm.raux[p] = IA[g];
-      }
-   }
-   if (lane == 0) sm.rkey[nI + take] = ~0ull;
-   wsync();
-   return take;
 }
 
-// State word `lane` (< SW) of a port after a window: tail X, route counts, "no
-// gap yet", the port's unconsumed spill range.
-__device__ __forceinline__ uint64_t state_word(uint32_t lane, uint64_t Xo, const uint32_t (&cin)[4], uint64_t C,
-                                               uint32_t nogap, uint32_t Kout, uint32_t Pend)
+// Per-field tables: lane 1 + q holds route field q (SELF, cont, UP, DOWN), the
+// lanes of the state words that carry the route counts.
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t l)
+{
+   return (uint32_t) __builtin_amdgcn_ds_bpermute((int) (l << 2), (int) v);
+}
+// Lane 1 + q of a row's packed field counts (8 bits per field).
+__device__ __forceinline__ uint32_t field_cnt(uint32_t R, uint32_t lane)
+{
+   return lane - 1u < 4u ? (R >> (8u * (lane - 1u))) & 0xFFu : 0u;
+}
+// State word `lane` (< SW) of a port after a window: tail X, route counts (the
+// field tables), "no gap yet", the port's unconsumed spill range.
+__device__ __forceinline__ uint64_t state_word(uint32_t lane, uint64_t Xo, uint32_t cnt_t, uint32_t nogap, uint32_t Kout,
+                                               uint32_t Pend)
 {
    uint64_t v = Xo;
-#pragma unroll
-   for (int f = 0; f < 4; f++)
-      if (lane == 1u + f) v = cin[f] + cf(C, f);
+   if (lane - 1u < 4u) v = cnt_t;
    if (lane == 5) v = nogap;
    if (lane == 6) v = Kout;
    if (lane == 7) v = Pend;
    return v;
+}
+// Keep a kernel-argument pointer in its own scalar pair (not reloaded as part of
+// a wide argument tuple), as a global-memory pointer.
+template <typename P>
+using gptr = __attribute__((address_space(1))) P*;
+template <typename P>
+__device__ __forceinline__ gptr<P> sptr(P* p)
+{
+   asm volatile("" : "+s"(p));
+   return (gptr<P>) p;
 }
 
 // ---------------------------------------------------------------------------
@@ -600,11 +521,13 @@ __device__ __forceinline__ uint64_t state_word(uint32_t lane, uint64_t Xo, const
 template <int NL>
 __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
 {
+   constexpr bool XC = NL == 1;
    const uint32_t lane = threadIdx.x;
    const uint64_t D = a.cw[c].D, st_off = a.cw[c].st_off, bt_off = a.cw[c].bt_off;
    const uint32_t nW = a.cw[c].nW;
    const uint64_t wbase = (uint64_t) w * D;
-   const uint64_t wlen = (w + 1 < nW) ? D : OFF_LIM;   // kept offsets: t' - wbase < wlen
+   const uint32_t wlen = (w + 1 < nW) ? (uint32_t) D : (uint32_t) OFF_LIM;   // kept offsets: t' - wbase < wlen
+   const bool lastw = w + 1 >= nW;
    const uint64_t wq = wbase / 1000ull;
    const uint32_t wr = (uint32_t) (wbase - wq * 1000ull);
    const uint64_t wb = wq ? wq - 1 : 0;          // base cycle: every request of the window has tc > wb (w > 0)
@@ -612,105 +535,86 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
    const uint32_t len = a.len;
    const uint32_t cpb = c * len;
    const uint32_t mode0 = a.c.analytical ? 1u : 0u;
+   const gptr<Rec> recs = sptr(a.recs);
 
-   // ---- prologue: descriptors and insert bounds of ports 0 and 1, port 0's inserts;
-   // then the pipeline's first prefetches (port 1's inserts, port 2's descriptor and bounds)
-   if (lane < 32) load_cp(&sm.cp[0], a.cp + cpb, lane);
-   else if (len > 1) load_cp(&sm.cp[1], a.cp + cpb + 1, lane - 32);
-   if (lane < 2 * NL) put_bounds(sm, 0, fetch_bounds(a, bt_off, nW, 0, NL, w, lane), NL, lane);
-   else if (lane < 4 * NL && len > 1) put_bounds(sm, 1, fetch_bounds(a, bt_off, nW, 1, NL, w, lane - 2 * NL), NL, lane - 2 * NL);
-   if (lane == 0) sm.kkey[0] = ~0ull;
-   wsync();
-   uint64_t rk[PER];
-   uint32_t ra[PER];
-   Rec iv[IPER];                 // the next port's inserts in flight
-   uint32_t itot_f = 0;          // their count
-   uint32_t cpv = 0, bv = 0;     // descriptor / bounds of the port after next, in flight
-   uint32_t nK = 0, nI = 0;      // this port's kept records and inserts
-   uint32_t P0cur = 0, nin_prev = 0, ncont_prev = 0;   // this port's chain input: records before / kept / all of this window
-   uint32_t nmax = 0, imax = 0;  // the fullest stream / insert list of this task (window sizing)
+   // ---- prologue: descriptors of ports 0..2 (with their insert bounds), port 0's
+   // inserts landed, port 1's in flight
+   uint32_t pd0 = load_pd<NL>(a, cpb, bt_off, nW, 0, w);
+   uint32_t pd1 = len > 1 ? load_pd<NL>(a, cpb + 1, bt_off, nW, 1, w) : 0u;
+   uint32_t pd2 = len > 2 ? load_pd<NL>(a, cpb + 2, bt_off, nW, 2, w) : 0u;
+   Rec iv[IROWS];
+   uint32_t nI = fetch_inserts<NL>(a, pd0, iv);
+   if (nI > (uint32_t) ICAP)
    {
-      nI = fetch_inserts<NL>(sm, a, 0, 0, iv, 0);
-      if (nI > (uint32_t) ICAP)
-      {
-         if (lane == 0) flag_overflow(a, c);
-         return;
-      }
-      if (store_inserts<NL>(sm, iv, nI, wbase, 0) && lane == 0) flag(a, F_FALLBACK);
-      premerge<NL>(sm, nI, 0, 0);
-      if (len > 1) itot_f = fetch_inserts<NL>(sm, a, 1, 1, iv, 1);
-      if (len > 2)
-      {
-         if (lane < 32) cpv = fetch_cp(a.cp + cpb + 2, lane);
-         else bv = fetch_bounds(a, bt_off, nW, 2, NL, w, lane - 32);
-      }
+      if (lane == 0) flag_overflow(a, c);
+      return;
    }
+   if (land_inserts<NL>(sm, iv, nI, wbase, pd0) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
+   uint32_t itot_f = len > 1 ? fetch_inserts<NL>(a, pd1, iv) : 0u;   // port 1's inserts, landed in step 0
+
+   uint64_t rk[ROWS];
+   uint32_t ra[ROWS];
+   uint32_t nK = 0;              // this port's kept records
+   uint32_t P0cur = 0, nin_prev = 0, ncont_prev = 0;   // this port's chain input: records before / kept / all of this window
+   uint32_t ob1p = 0, oc1p = 0;  // the previous port's chain output slot (spill-ins)
+   uint32_t nmax = 0, imax = 0;  // the fullest stream / insert list of this task (window sizing)
 
    for (uint32_t i = 0; i < len; i++)
    {
-      const uint32_t cpi = cpb + i;
-      const uint32_t b = i & 1u, bn = b ^ 1u;
-      const ChainPort& P = sm.cp[i % 3];
       const bool has_next = i + 1 < len;
       uint64_t* const stw = a.st + st_off + ((uint64_t) i * nW + w) * SW;          // this window's state
       const uint64_t* const stp = w ? stw - SW : nullptr;                           // predecessor's
-
-      // ---- [A] land last step's prefetches: port i+1's inserts, port i+2's descriptor and
-      // bounds; load the predecessor's state of this port
       CH_STAMP(0);
-      const uint32_t itot = itot_f;
-      bool ibad = false;
-      if (has_next) ibad = store_inserts<NL>(sm, iv, itot, wbase, bn);
-      if (i + 2 < len)
-      {
-         if (lane < 32) put_cp(&sm.cp[(i + 2) % 3], cpv, lane);
-         else put_bounds(sm, (i + 2) & 1, bv, NL, lane - 32);
-      }
       uint64_t pv = 0;
       if (w && lane < (uint32_t) SW) pv = ld1(stp + lane);
-      const uint32_t nx = sgpr(P.nx), ny = sgpr(P.ny), cont = sgpr(P.cont), rl = sgpr(P.rl), port = sgpr(P.port);
-      wsync();
-      CH_STAMP(7);
+      const uint32_t nx = rdl(pd0, PD_NX), ny = rdl(pd0, PD_NY);
 
-      const uint64_t* Ic = sm.ikey[b];
-      const uint32_t* IAc = sm.iaux[b];
-      uint32_t n = nK + nI, a0 = 0, cnt = 0;
-      Agg ex, tot;
+      // ---- [B] the merged stream in rows; per-row max-plus scans, route-field totals
+      uint32_t n = nK + nI, IB = CAP;
+      uint32_t fpack = 0, tc_t = 0;
+      uint32_t totA = 0, totB = 0;
       bool first = true, published = false;
       uint32_t Xr = 0, mode = mode0, Kpp = 0, Pep = 0, Kout = 0, Pend = 0;
-      uint32_t cin[4] = { 0, 0, 0, 0 };
+      uint32_t cin_t = 0;
+      const uint32_t itot = itot_f;
       for (;;)
       {
-         // ---- [B][C] this lane's segment of the merged stream, wave scan (first pass: no
-         // spill-ins yet)
+         load_rows<ROWS>(sm, nK, IB, nI, rk, ra);
+         if (first) CH_STAMP(1);
+         totA = totB = 0;
+         fpack = 0;
+         tc_t = 0;
+#pragma unroll
+         for (int r = 0; r < ROWS; r++)
          {
-            const uint32_t k = (n + T - 1) / T;
-            a0 = min(lane * k, n);
-            cnt = min(k, n - a0);
-            const uint32_t y = mp_split(sm.kkey, nK, Ic, nI, a0);
-            uint32_t yend = 0;
-            const Agg g0 = walk<NL == 1>(sm.kkey, sm.kaux, Ic, IAc, a0 - y, y, cnt, wr, d0, nx, ny, cont, rk, ra, yend);
-#ifdef CH_DEBUG
-            // the next lane's split must be where this one's walk ended
-            const uint32_t ynext = (uint32_t) __shfl_down((int) y, 1);
-            if ((lane < 63 && cnt && a0 + cnt < n && ynext != yend) || yend > nI || a0 + cnt - yend > nK)
-               flag(a, F_ROUTE | 64u);
-#endif
-            if (first) CH_STAMP(8);
-            const Agg inc = wave_scan(g0);
-            ex.A = dpp32<0x138, 0xF, 0xF>(inc.A);   // exclusive: wave_shr 1
-            ex.B = dpp32<0x138, 0xF, 0xF>(inc.B);
-            ex.C = dpp64<0x138, 0xF, 0xF>(inc.C);
-            tot.A = rdl(inc.A, 63);
-            tot.B = rdl(inc.B, 63);
-            tot.C = rdl64(inc.C, 63);
+            if ((uint32_t) r * T >= n) break;
+            const bool valid = (uint32_t) r * T + lane < n;
+            const uint32_t p = aux_F(ra[r]);
+            uint32_t A = valid ? p : 0u;
+            uint32_t B = valid ? rcyc((uint32_t) (rk[r] >> 32), wr, d0) + p : 0u;
+            wave_scan(A, B);
+            const uint32_t rA = rdl(A, 63), rB = rdl(B, 63);
+            const uint32_t nb = totB + rA;
+            totB = nb > rB ? nb : rB;
+            totA += rA;
+            const uint32_t f = route_field<XC>(nx, ny, ra[r]);
+            fpack |= (valid ? f : 0u) << (2 * r);
+            tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
          }
          if (!first) break;
-         CH_STAMP(1);
+         CH_STAMP(2);
          first = false;
-         if (ibad && lane == 0) flag(a, F_FALLBACK);
-         // Y ports: the three insert ranges into one sorted list (read at the next step)
-         if (has_next) premerge<NL>(sm, itot, bn, (i + 1) & 1);
+         // the stream is in registers: the insert region takes the next port's inserts
+         if (has_next)
+         {
+            if (itot > (uint32_t) ICAP)
+            {
+               if (lane == 0) flag_overflow(a, c);
+               return;
+            }
+            if (land_inserts<NL>(sm, iv, itot, wbase, pd1) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
+         }
+         CH_STAMP(3);
 
          // ---- [D] predecessor's state
          bool ok = true;
@@ -719,19 +623,18 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          {
             ok = poll_words(a, stp, SW, lane, pv);
             X_in = rdl64(pv, 0) & M48;
-#pragma unroll
-            for (int f = 0; f < 4; f++) cin[f] = (uint32_t) (rdl64(pv, 1 + f) & M48);
+            cin_t = lane - 1u < 4u ? (uint32_t) (pv & M48) : 0u;
             mode = (uint32_t) (rdl64(pv, 5) & 1u);
             Kpp = (uint32_t) (rdl64(pv, 6) & M48);
             Pep = (uint32_t) (rdl64(pv, 7) & M48);
          }
-         CH_STAMP(2);
+         CH_STAMP(4);
          if (!ok) return;
          // window-relative tail: an earlier tail behaves like the base cycle (every tc > wb)
          const uint64_t xr = X_in > wb ? X_in - wb : 0;
          if (xr >= (1ull << 31))
          {
-            if (lane == 0) flag(a, F_FALLBACK);
+            if (lane == 0) flag(a, F_FALLBACK | R_TAIL);
             return;
          }
          Xr = (uint32_t) xr;
@@ -742,191 +645,221 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          published = !mode && Pep == Kpp;
          if (published && lane < (uint32_t) SW)
          {
-            const uint32_t nx0 = Xr + tot.A;
-            st1(stw + lane, a.etag | state_word(lane, wb + (nx0 > tot.B ? nx0 : tot.B), cin, tot.C, 0u, Kout, Pend));
-         }
-         CH_STAMP(3);
-         // next prefetches (they land at the next step's [A]): port i+2's inserts (its
-         // descriptor and bounds landed at this step's [A]), port i+3's descriptor and bounds
-         if (i + 2 < len) itot_f = fetch_inserts<NL>(sm, a, (i + 2) % 3, (i + 2) & 1, iv, (i + 2) & 1);
-         if (i + 3 < len)
-         {
-            if (lane < 32) cpv = fetch_cp(a.cp + cpi + 3, lane);
-            else bv = fetch_bounds(a, bt_off, nW, i + 3, NL, w, lane - 32);
+            const uint32_t x0 = Xr + totA;
+            st1(stw + lane, a.etag | state_word(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u, Kout, Pend));
          }
          if (Pep == Kpp) break;
-         // ---- slow path: spill-ins join the insert list, then rescan
+         // ---- slow path: spill-ins (records the previous port spilled in earlier windows,
+         // sorted: FIFO departures) with t in this window join the stream as inserts
+         // behind the merged stream, then the rows are rebuilt
          const uint32_t spn = Pep - Kpp;
-         const bool sok = i > 0 && spn + nI <= (uint32_t) ICAP && (uint64_t) Kpp + spn <= a.cp[cpi - 1].ocap[1] &&
-                          pad(nK) + 1 + spn <= (uint32_t) CAPP;   // room to stage the spills behind the kept list
-         if (!sok)
+         if (!(i > 0 && (uint64_t) Kpp + spn <= oc1p))
          {
-            if (lane == 0) flag(a, F_FALLBACK);
+            if (lane == 0) flag(a, F_FALLBACK | R_SPILLIN);
             return;
          }
-         uint32_t skip = 0;
-         const uint32_t take = spill_in(sm, a, a.cp[cpi - 1].obase[1] + Kpp, spn, Ic, IAc, nI, nK, wbase, wlen, skip);
+#pragma unroll
+         for (int r = 0; r < ROWS; r++)
+         {
+            const uint32_t p = (uint32_t) r * T + lane;
+            if ((uint32_t) r * T >= n) break;
+            if (p < n)
+            {
+               sm.key[p] = rk[r];
+               sm.aux[p] = ra[r];
+            }
+         }
+         uint32_t skip = 0, take = 0;
+         for (uint32_t g0 = 0; g0 < spn; g0 += T)
+         {
+            const uint32_t g = g0 + lane;
+            uint64_t t = 0, ia = 0;
+            if (g < spn)
+            {
+               const uint64_t* r = reinterpret_cast<const uint64_t*>(a.recs + (uint64_t) ob1p + Kpp + g);
+               t = ld1(r);
+               ia = ld1(r + 1);
+            }
+            const bool early = g < spn && t < wbase;
+            const bool in = g < spn && t >= wbase && t - wbase < wlen;
+            const uint64_t mt = __ballot(in);
+            const uint32_t dst = n + take + mbcnt(mt);
+            if (in && dst < (uint32_t) CAP)
+            {
+               sm.key[dst] = ((t - wbase) << 32) | (uint32_t) ia;
+               sm.aux[dst] = (uint32_t) (ia >> 32);
+            }
+            skip += (uint32_t) __popcll(__ballot(early));
+            take += (uint32_t) __popcll(mt);
+            if (__ballot(g < spn && !early && !in)) break;   // the rest leave after this window
+         }
+         wsync();
+         if (!nin_prev) Kout = Kpp + skip + take;   // the consumed prefix of the old spills
+         if (!take) break;                          // nothing merged: the scan stands
          if (n + take > (uint32_t) CAP)
          {
             if (lane == 0) flag_overflow(a, c);
             return;
          }
-         if (!nin_prev) Kout = Kpp + skip + take;   // the consumed prefix of the old spills
-         if (!take) break;   // nothing merged: the scan stands
-         Ic = sm.rkey;
-         IAc = sm.raux;
-         nI += take;
+         nK = n;
+         IB = n;
+         nI = take;
          n += take;          // rescan (the stream changed)
       }
+      CH_STAMP(5);
       // publish now (unless the history tree still has no gap: after the outputs)
       if (!published && !mode && lane < (uint32_t) SW)
       {
-         const uint32_t nx0 = Xr + tot.A;
-         st1(stw + lane, a.etag | state_word(lane, wb + (nx0 > tot.B ? nx0 : tot.B), cin, tot.C, 0u, Kout, Pend));
+         const uint32_t x0 = Xr + totA;
+         st1(stw + lane, a.etag | state_word(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u, Kout, Pend));
       }
 
-      // ---- [E] recurrence, outputs: kept records in place into the kept list
-      uint32_t X = Xr + ex.A;
-      X = X > ex.B ? X : ex.B;
-      uint32_t run[4];
-#pragma unroll
-      for (int f = 0; f < 4; f++) run[f] = cin[f] + cf(ex.C, f);
-      const uint32_t P0n = cin[1];   // chain-direction records before this window
+      // ---- [E] recurrence and outputs, row by row: kept records in place into the kept list
+      const uint32_t rl = rdl(pd0, PD_RL);
+      // field tables (lane 1 + q): output slot base, capacity, records routed so far
+      const uint32_t obf_t = bperm(pd0, lane - 1u), ocf_t = bperm(pd0, lane + 3u);
+      uint32_t run_t = cin_t;
+      const uint32_t P0n = rdl(cin_t, 2);   // chain-direction records before this window
+      const gptr<uint64_t> samp_t = sptr(a.samp_t);
+      const gptr<uint32_t> samp_id = sptr(a.samp_id);
       uint64_t ssum = 0;
-      uint32_t nkeep = 0, fgap = NONE, ffire = NONE;
+      uint32_t Xc = Xr, nkeep = 0, fgap = NONE, ffire = NONE;
       bool spilled = false, bad = false, route = false;
-      CH_STAMP(12);
 #pragma unroll
-      for (int j = 0; j < PER; j++)
+      for (int r = 0; r < ROWS; r++)
       {
-         if ((uint32_t) j >= cnt) continue;
-         const uint32_t off = (uint32_t) (rk[j] >> 32);
-         const uint32_t id = (uint32_t) rk[j];
-         const uint32_t ax = ra[j];
+         if ((uint32_t) r * T >= n) break;
+         const uint32_t p0 = (uint32_t) r * T;
+         const bool valid = p0 + lane < n;
+         const uint32_t off = (uint32_t) (rk[r] >> 32);
+         const uint32_t id = (uint32_t) rk[r];
+         const uint32_t ax = ra[r];
          const uint32_t tc = rcyc(off, wr, d0);
          const uint32_t p = aux_F(ax);
-         const uint32_t Xb = X;
-         const uint32_t cc = Xb > tc ? Xb - tc : 0;
-         X = (Xb > tc ? Xb : tc) + p;
+         // the row's exclusive prefix (rescanned: registers for 11 rows of prefixes cost
+         // more than the scan)
+         uint32_t A = valid ? p : 0u, B = valid ? tc + p : 0u;
+         wave_scan(A, B);
+         const uint32_t exA = dpp32<0x138, 0xF, 0xF>(A), exB = dpp32<0x138, 0xF, 0xF>(B);   // wave_shr 1
+         const uint32_t xa = Xc + exA;
+         const uint32_t Xb = xa > exB ? xa : exB;
+         const uint32_t cc = valid && Xb > tc ? Xb - tc : 0u;
+         const uint32_t Xa = (Xb > tc ? Xb : tc) + p;
          if (mode)
          {
             // history tree with no gap yet: an idle period makes one (:79-86); the M/G/1
             // branch fires while there is none and the tail lies beyond t + p (:58-64)
-            if (tc > Xb && fgap == NONE) fgap = a0 + j;
-            if (Xb > tc + p && ffire == NONE) ffire = a0 + j;
+            const uint64_t gm = __ballot(valid && tc > Xb), fm = __ballot(valid && Xb > tc + p);
+            if (fgap == NONE && gm) fgap = p0 + (uint32_t) __builtin_ctzll(gm);
+            if (ffire == NONE && fm) ffire = p0 + (uint32_t) __builtin_ctzll(fm);
          }
+         Xc = rdl(Xa, (int) min(63u, n - 1 - p0));
          ssum += cc;
          const uint64_t dn = (uint64_t) off + (uint64_t) cc * 1000ull + rl;   // t' - wbase
-         const uint32_t f = route_field<NL == 1>(nx, ny, ax);
-         uint32_t pos = 0;
-#pragma unroll
-         for (int q = 0; q < 4; q++)
-            if (f == (uint32_t) q) pos = run[q]++;
-         if (f == 1)
+         // route ranks: a packed (8 bits per field) prefix count over the row
+         const uint32_t f = (fpack >> (2 * r)) & 3u;
+         const uint32_t one = valid ? 1u << (8 * f) : 0u;
+         const uint32_t inc = wave_sum32(one);
+         const uint32_t rank = ((inc - one) >> (8 * f)) & 0xFFu;
+         const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
+         const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
+         const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
+         run_t += field_cnt(rdl(inc, 63), lane);
+         // continuing: kept (a prefix of the window's continuing records) or spilled
+         const bool keep = valid && f == 1 && dn < wlen;
+         nkeep += (uint32_t) __popcll(__ballot(keep));
+         if (keep)
          {
-            // continuing: kept (a prefix of the window's continuing records) or spilled;
-            // a spill marks the kept list's end (~0 at its index, the first one counts)
-            const uint32_t ci = pos - P0n;
-            const bool keep = dn < wlen;
-            sm.kkey[pad(ci)] = keep ? ((dn << 32) | id) : ~0ull;
-            if (keep)
+            sm.key[kb + rank] = (dn << 32) | id;
+            sm.aux[kb + rank] = ax;
+         }
+         else if (valid)
+         {
+            const uint64_t gp = (uint64_t) gb + rank;
+            const uint64_t tn = wbase + dn;
+            if (rank >= room) route = true;
+            else if (f == 1)
             {
-               sm.kaux[pad(ci)] = ax;
-               nkeep++;
-               continue;
+               // spill: taken by task (chain, w+1) at the next port (sc1: read in-launch)
+               bad |= lastw;   // the last window keeps everything (or its offsets overflowed)
+               uint64_t* q = reinterpret_cast<uint64_t*>(a.recs + gp);
+               st1(q, tn);
+               st1(q + 1, (uint64_t) id | ((uint64_t) ax << 32));
+               spilled = true;
             }
-         }
-         // the output slot of field f: read per record from the descriptor (no scalar
-         // registers held across the step; the next prefetch lands in another slot)
-         if (pos >= P.ocap[f]) { route = true; continue; }
-         const uint64_t gp = P.obase[f] + pos;
-         const uint64_t tn = wbase + dn;
-         if (f == 1)
-         {
-            // spill: taken by task (chain, w+1) at the next port (sc1: read in-launch)
-            bad |= w + 1 >= nW;   // the last window keeps everything (or its offsets overflowed)
-            uint64_t* r = reinterpret_cast<uint64_t*>(a.recs + gp);
-            st1(r, tn);
-            st1(r + 1, (uint64_t) id | ((uint64_t) ax << 32));
-            spilled = true;
-         }
-         else
-         {
-            Rec o;
-            o.t = tn;
-            o.id = id;
-            o.aux = ax;
-            a.recs[gp] = o;
-            if ((gp & 63) == 0)
+            else
             {
-               a.samp_t[gp >> 6] = tn;
-               a.samp_id[gp >> 6] = id;
+               typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+               v4u o;
+               o.x = (uint32_t) tn;
+               o.y = (uint32_t) (tn >> 32);
+               o.z = id;
+               o.w = ax;
+               *(gptr<v4u>) (recs + gp) = o;
+               if ((gp & 63) == 0)
+               {
+                  samp_t[gp >> 6] = tn;
+                  samp_id[gp >> 6] = id;
+               }
             }
          }
       }
-      CH_STAMP(13);
-      // the kept list's end when nothing spilled
-      if (lane == 0) sm.kkey[pad(cf(tot.C, 1))] = ~0ull;
+      CH_STAMP(6);
       if (__any(route) && lane == 0) flag(a, F_ROUTE);
-      if (__any(bad) && lane == 0) flag(a, F_FALLBACK);
-      // wave reductions: queue delay sum, kept records, first gap / M/G/1 condition
+      if (__any(bad) && lane == 0) flag(a, F_FALLBACK | R_LASTSPILL);
       const uint64_t ssw = rdl64(wave_sum64(ssum), 63);
-      const uint32_t nin = rdl(wave_sum32(nkeep), 63);
       if (__any(spilled)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drained before the next publish
       wsync();
-      CH_STAMP(4);
 
       // ---- [F] late publish (no gap yet), port counters, route check
-      const uint32_t nx0 = Xr + tot.A;
-      const uint64_t Xo = wb + (nx0 > tot.B ? nx0 : tot.B);
+      const uint32_t x0 = Xr + totA;
+      const uint64_t Xo = wb + (x0 > totB ? x0 : totB);
       if (!published && mode)
       {
-         // the records are in lane order: the first lane with a gap / firing holds the first
-         const uint64_t mg = __ballot(fgap != NONE), mf = __ballot(ffire != NONE);
-         const uint32_t fg = mg ? rdl(fgap, __builtin_ctzll(mg)) : NONE;
-         const uint32_t ff = mf ? rdl(ffire, __builtin_ctzll(mf)) : NONE;
          // the M/G/1 branch would serve a request that arrives before the first gap
-         if (lane == 0 && ff != NONE && (fg == NONE || ff < fg)) flag(a, F_FALLBACK);
-         if (lane < (uint32_t) SW)
-            st1(stw + lane, a.etag | state_word(lane, Xo, cin, tot.C, fg == NONE ? 1u : 0u, Kout, Pend));
+         if (lane == 0 && ffire != NONE && (fgap == NONE || ffire < fgap)) flag(a, F_FALLBACK | R_MG1);
+         if (lane < (uint32_t) SW) st1(stw + lane, a.etag | state_word(lane, Xo, run_t, fgap == NONE ? 1u : 0u, Kout, Pend));
       }
-      if (lane == 0)
+      // every record of the port has passed at the last window: the route counts fill
+      // every output slot
+      if (lastw && __any(lane - 1u < 4u && run_t != ocf_t) && lane == 0) flag(a, F_ROUTE);
+      if (lane == 0 && n)
       {
-         if (w + 1 == nW)
-         {
-            // every record of the port has passed: the route counts fill every output slot
-            bool full = true;
-            for (uint32_t f = 0; f < 4; f++) full &= cin[f] + cf(tot.C, f) == P.ocap[f];
-            if (!full) flag(a, F_ROUTE);
-         }
-         if (n)
-         {
-            atomicAdd(&a.port_sum[port], (unsigned long long) ssw);
-            atomicAdd(&a.port_cnt[port], (unsigned long long) n);
-            atomicAdd(&a.port_flit[port], (unsigned long long) tot.A);
-            atomicMax(&a.port_last[port], (unsigned long long) Xo);
-         }
+         const uint32_t port = rdl(pd0, PD_PORT);
+         atomicAdd(&a.port_sum[port], (unsigned long long) ssw);
+         atomicAdd(&a.port_cnt[port], (unsigned long long) n);
+         atomicAdd(&a.port_flit[port], (unsigned long long) totA);
+         atomicMax(&a.port_last[port], (unsigned long long) Xo);
       }
       nmax = n > nmax ? n : nmax;
-      imax = itot > imax ? itot : imax;   // the next port's inserts (checked against ICAP below)
+      imax = itot > imax ? itot : imax;   // the next port's inserts (checked against ICAP at landing)
       // the next port's chain input: records before this window, kept, all of this window
-      P0cur = cin[1];
-      nin_prev = nin;
-      ncont_prev = cf(tot.C, 1);
-      CH_STAMP(9);
+      P0cur = P0n;
+      nin_prev = nkeep;
+      ncont_prev = rdl(tc_t, 2);
+      ob1p = rdl(pd0, PD_OBASE + 1);
+      oc1p = rdl(pd0, PD_OCAP + 1);
+      CH_STAMP(7);
 #ifdef CH_STAMPS
       if (a.stamps && lane == 0)
-         a.stamps[((uint64_t) tk * len + i) * 16 + 6] = (uint64_t) n | ((uint64_t) itot << 16) |
-                                                     ((uint64_t) nin << 32) | ((uint64_t) (Pep != Kpp) << 63);
+         a.stamps[((uint64_t) tk * len + i) * 16 + 8] = (uint64_t) n | ((uint64_t) itot << 16) |
+                                                     ((uint64_t) nkeep << 32) | ((uint64_t) (Pep != Kpp) << 63);
 #endif
       if (!has_next) break;
-      if (itot > (uint32_t) ICAP || nin + itot > (uint32_t) CAP)
+      if (nkeep + itot > (uint32_t) CAP)
       {
          if (lane == 0) flag_overflow(a, c);
          return;
       }
-      nK = nin;
+      nK = nkeep;
       nI = itot;
+      // ---- next prefetches: port i+2's inserts (its descriptor landed a step ago), port
+      // i+3's descriptor and bounds; the ring moves on
+      if (i + 2 < len) itot_f = fetch_inserts<NL>(a, pd2, iv);
+      const uint32_t pdn = i + 3 < len ? load_pd<NL>(a, cpb + i + 3, bt_off, nW, i + 3, w) : 0u;
+      pd0 = pd1;
+      pd1 = pd2;
+      pd2 = pdn;
    }
    if (lane == 0)
    {
@@ -944,7 +877,7 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
    // inputs are not in FIFO order -> the level engine reruns the batch
    if (a.errflag[2] != 0)
    {
-      if (threadIdx.x == 0 && blockIdx.x == 0) flag(a, F_FALLBACK);
+      if (threadIdx.x == 0 && blockIdx.x == 0) flag(a, F_FALLBACK | R_EXC);
       return;
    }
    for (;;)
@@ -1005,15 +938,15 @@ __global__ __launch_bounds__(256) void k_chain_plan(DevCfg c, uint32_t ncpx, uin
       // a Y port's UP / DOWN fields other than its own direction carry nothing
       const bool used = f < 2 || dir == P_LEFT || dir == P_RIGHT;
       const uint32_t os = slot_of(ntile, fdir[f], slot_side(fdir[f], nside));
-      p.obase[f] = used ? slot_base[os] : 0;
-      p.ocap[f] = used ? slot_cnt[os] : 0;
+      p.obase[f] = used ? (uint32_t) slot_base[os] : 0u;
+      p.ocap[f] = used ? slot_cnt[os] : 0u;
    }
    const uint32_t sides[3] = { IN_LOCAL, IN_W, IN_E };
    for (uint32_t j = 0; j < 3; j++)
    {
       const uint32_t s = slot_of(tile, dir, sides[j]);
-      p.ibase[j] = j < nl ? slot_base[s] : 0;
-      p.icnt[j] = j < nl ? slot_cnt[s] : 0;
+      p.ibase[j] = j < nl ? (uint32_t) slot_base[s] : 0u;
+      p.icnt[j] = j < nl ? slot_cnt[s] : 0u;
    }
    p.port = tile * PORTS + dir;
    p.tile = tile;
@@ -1023,7 +956,7 @@ __global__ __launch_bounds__(256) void k_chain_plan(DevCfg c, uint32_t ncpx, uin
    p.ny = ntile / W;
    p.rl = (uint32_t) rl_of(c, tile);
    p.nl = nl;
-   p.pad0[0] = p.pad0[1] = p.pad0[2] = 0;
+   for (int q = 0; q < 10; q++) p.pad0[q] = 0;
    out[k] = p;
 }
 

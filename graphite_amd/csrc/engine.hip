@@ -106,6 +106,7 @@ struct gnoc_engine
    // trace
    size_t n = 0;
    uint64_t rec_bound = 0;    // records incl. slot padding (from the trace at submit)
+   uint32_t runs = 0, tot_retry = 0, tot_fallback = 0;   // since the last submit (gnoc_summary)
    bool submitted = false, ran = false;
    const uint64_t* d_inj = nullptr;
    const uint32_t *d_src = nullptr, *d_dst = nullptr, *d_bits = nullptr, *d_flags = nullptr;
@@ -333,6 +334,10 @@ static hipError_t upload_levels(gnoc_engine* e)
 extern "C" {
 
 int gnoc_abi_version(void) { return GNOC_ABI_VERSION; }
+#ifndef GNOC_BUILD_ID
+#define GNOC_BUILD_ID "unknown"
+#endif
+const char* gnoc_build_id(void) { return GNOC_BUILD_ID; }
 
 void gnoc_config_default(gnoc_config* cfg, int32_t num_tiles)
 {
@@ -587,6 +592,7 @@ static uint64_t record_bound(const gnoc_engine* e, uint64_t records)
 // each run adapt_windows resizes D from the fullest step the run measured.
 static constexpr double CH_FILL = 0.45;     // first run: the steady-rate estimate (bursts reach ~1.7x on the Y phase)
 static constexpr double CH_TARGET = 0.95;    // adapted windows: the fullest step at 0.95 of capacity (0.9: 3.94 ms, 0.95: 3.81, 0.98: 3.89 on configs[1]; 1.0 declines the chains)
+static constexpr double CH_GROW = 1.6;       // most a chain's window grows per run
 static constexpr uint32_t CH_NW_MAX = 4096;
 static constexpr uint64_t CH_D_MIN = 1024, CH_D_MAX = 1ull << 31;   // 32-bit time offsets in a window
 static uint32_t windows_of(uint64_t D, uint64_t t_last) { return (uint32_t) (t_last / D + 1); }
@@ -656,6 +662,7 @@ static void adapt_windows(gnoc_engine* e)
          double r = CH_TARGET * ch::CAP / (double) n;
          if (ni) r = std::min(r, 0.95 * ch::ICAP / (double) ni);   // inserts are few: only keep them in the buffer
          if (r > 0.92 && r < 1.08) continue;                        // close enough: no churn
+         r = std::min(r, CH_GROW);                                   // bursts the last run did not see: grow in steps
          double d = (double) e->chD[p][c] * r;
          if (e->chCap[p][c]) d = std::min(d, 0.95 * (double) e->chCap[p][c]);   // stay below a size that overflowed
          const uint64_t D = clamp_window(e, d);
@@ -932,6 +939,16 @@ static int partition_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n, gno
       if (s >= N || d >= N) return fail(e, GNOC_ETRACE, "tile id out of range at packet " + std::to_string(i));
       if (i && pk->inject_ps[i] < pk->inject_ps[i - 1])
          return fail(e, GNOC_ETRACE, "trace not ordered by inject_ps at packet " + std::to_string(i));
+      // the rest of k_validate's per-packet contract, in its order: every rank checks
+      // the whole trace, so a bad packet fails gnoc_submit on every rank alike (a rank
+      // would otherwise see only the packets it keeps)
+      const uint32_t fw = e->dc.flit_width, b = pk->bits[i];
+      const uint32_t F = (b % fw) ? b / fw + 1 : b / fw;
+      const bool bypass = s == d || (fl & GNOC_PKT_UNMODELED);
+      if (F == 0 && !bypass) return fail(e, GNOC_ETRACE, "zero-flit packet " + std::to_string(i));
+      if (F > AUX_F_MAX) return fail(e, GNOC_EUNSUPPORTED, "packet longer than 2047 flits (packet " + std::to_string(i) + ")");
+      if (pk->inject_ps[i] >= (1ull << 50))
+         return fail(e, GNOC_EUNSUPPORTED, "inject time beyond 2^50 ps at packet " + std::to_string(i));
       const uint32_t sx = s % W, sy = s / W, dx = d % W, dy = d / W;
       if (s != d && !(fl & GNOC_PKT_UNMODELED))
       {
@@ -1036,6 +1053,7 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk_in, size_t n)
    if (rc) return rc;
    rc = build_exchange(e);
    if (rc) return rc;
+   e->runs = e->tot_retry = e->tot_fallback = 0;
    e->submitted = true;
    e->ran = false;
    e->begun = false;
@@ -1073,6 +1091,7 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    e->h_bid.clear();
    rc = upload_broadcasts(e);
    if (rc) return rc;
+   e->runs = e->tot_retry = e->tot_fallback = 0;
    e->submitted = true;
    e->ran = false;
    e->begun = false;
@@ -1270,7 +1289,7 @@ static bool chain_usable(const gnoc_engine* e)
    const char* env = std::getenv("GNOC_ENGINE");
    if (env && (std::strcmp(env, "levels") == 0 || std::strcmp(env, "v1") == 0)) return false;
    return e->ch_on && e->f1 && !e->nb && !e->force_levels && !e->ch_declined && !e->force_v1 && !e->dc.hop_counter &&
-          e->dc.max_list >= 3 && (e->dc.W > 1 || e->dc.H > 1);
+          e->dc.max_list >= 3 && (e->dc.W > 1 || e->dc.H > 1) && e->rec_bound < (1ull << 32);   // u32 record indices
 }
 
 // Chain descriptors, state buffers, epoch.  After run_plan_v3 (slot layout known).
@@ -1632,6 +1651,7 @@ static int run_post(gnoc_engine* e, bool closed_form)
    const unsigned errf = ef[0];
    if (e->used_chain && (ef[4] & ch::F_ANY))
    {
+      if (std::getenv("GNOC_CHAIN_DEBUG")) std::fprintf(stderr, "gnoc: chain engine declined, flags 0x%x\n", ef[4]);
       if (ef[4] & ch::F_ROUTE)
       {
          char m[96];
@@ -1908,9 +1928,19 @@ int gnoc_set_basic_moving_average(gnoc_engine* e, int32_t type, uint32_t window_
    return GNOC_OK;
 }
 
+static int run_impl(gnoc_engine* e);
 int gnoc_run(gnoc_engine* e)
 {
    if (!e) return GNOC_EINVAL;
+   e->n_retry = e->n_fallback = 0;
+   const int rc = run_impl(e);
+   e->runs++;
+   e->tot_retry += e->n_retry;
+   e->tot_fallback += e->n_fallback;
+   return rc;
+}
+static int run_impl(gnoc_engine* e)
+{
    if (e->ma_type && e->dc.contention) return run_ma(e);
    if (e->nranks > 1) return fail(e, GNOC_ESTATE, "sharded engine: use gnoc_run_begin / exchange / gnoc_run_finish");
    const char* env = std::getenv("GNOC_ENGINE");
@@ -1943,7 +1973,6 @@ int gnoc_run(gnoc_engine* e)
       e->force_levels = 0;
       e->chD_run[0] = e->chD[0];
       e->chD_run[1] = e->chD[1];
-      if (e->bc_passes == 0) { e->n_retry = 0; e->n_fallback = 0; }
       int rc = run_once(e);
       // chain engine: a window that overflowed LDS reruns with windows half as long
       // (twice as many), up to 3 times; anything else it cannot take reruns on levels
@@ -2103,16 +2132,18 @@ static int rccl_exchange(gnoc_engine* e, const void* send, const uint64_t* su, v
    // grouped point-to-point: every peer pair is one xGMI transfer (no ring relay)
    if (ncclGroupStart() != ncclSuccess) return fail(e, GNOC_EHIP, "ncclGroupStart");
    uint64_t so = 0, ro = 0;
-   for (int q = 0; q < nr; q++)
+   const char* bad = nullptr;   // the group is always closed, so the status all-reduce after it runs
+   for (int q = 0; q < nr && !bad; q++)
    {
       if (su[q] && ncclSend(static_cast<const char*>(send) + so * 16, su[q] * 16, ncclChar, q, comm, e->stream) != ncclSuccess)
-         return fail(e, GNOC_EHIP, "ncclSend");
-      if (ru[q] && ncclRecv(static_cast<char*>(recv) + ro * 16, ru[q] * 16, ncclChar, q, comm, e->stream) != ncclSuccess)
-         return fail(e, GNOC_EHIP, "ncclRecv");
+         bad = "ncclSend";
+      else if (ru[q] && ncclRecv(static_cast<char*>(recv) + ro * 16, ru[q] * 16, ncclChar, q, comm, e->stream) != ncclSuccess)
+         bad = "ncclRecv";
       so += su[q];
       ro += ru[q];
    }
-   if (ncclGroupEnd() != ncclSuccess) return fail(e, GNOC_EHIP, "ncclGroupEnd");
+   if (ncclGroupEnd() != ncclSuccess && !bad) bad = "ncclGroupEnd";
+   if (bad) return fail(e, GNOC_EHIP, bad);
    GNOC_HIP(e, hipStreamSynchronize(e->stream));
    return GNOC_OK;
 }
@@ -2174,13 +2205,18 @@ int gnoc_run_sharded(gnoc_engine* e)
    if (!e) return GNOC_EINVAL;
    if (e->nranks <= 1) return gnoc_run(e);
    if (!e->nccl && !e->tp.exchange) return fail(e, GNOC_ESTATE, "gnoc_run_sharded needs gnoc_shard_set_comm or a transport");
-   if (!e->submitted) return fail(e, GNOC_ESTATE, "gnoc_run_sharded before gnoc_submit");
+   // from here every failure goes through the status agreement, so no peer waits
+   // in a collective this rank never joins
+   if (!e->submitted)
+      return shard_agree(e, fail(e, GNOC_ESTATE, "gnoc_run_sharded before gnoc_submit"), "gnoc_run_begin");
    uint64_t ns = 0, nrv = 0;
    for (uint64_t u : e->xs_units) ns += u;
    for (uint64_t u : e->xr_units) nrv += u;
-   GNOC_HIP(e, hipSetDevice(e->cfg.device));
-   GNOC_HIP(e, e->xsend.ensure(std::max<uint64_t>(ns, 1) * 16));
-   GNOC_HIP(e, e->xrecv.ensure(std::max<uint64_t>(nrv, 1) * 16));
+   hipError_t he = hipSetDevice(e->cfg.device);
+   if (he == hipSuccess) he = e->xsend.ensure(std::max<uint64_t>(ns, 1) * 16);
+   if (he == hipSuccess) he = e->xrecv.ensure(std::max<uint64_t>(nrv, 1) * 16);
+   if (he != hipSuccess)
+      return shard_agree(e, fail(e, GNOC_EHIP, std::string("exchange buffers: ") + hipGetErrorString(he)), "gnoc_run_begin");
    std::vector<uint64_t> su((size_t) e->nranks, 0), ru((size_t) e->nranks, 0);
    for (size_t q = 0; q < su.size(); q++)
    {
@@ -2283,9 +2319,18 @@ int gnoc_run_begin(gnoc_engine* e, void* send_buf)
    return GNOC_OK;
 }
 
+static int run_finish_impl(gnoc_engine* e, const void* recv_buf);
 int gnoc_run_finish(gnoc_engine* e, const void* recv_buf)
 {
    if (!e) return GNOC_EINVAL;
+   const int rc = run_finish_impl(e, recv_buf);
+   e->runs++;
+   e->tot_retry += e->n_retry;
+   e->tot_fallback += e->n_fallback;
+   return rc;
+}
+static int run_finish_impl(gnoc_engine* e, const void* recv_buf)
+{
    if (!e->begun) return fail(e, GNOC_ESTATE, "gnoc_run_finish without gnoc_run_begin");
    e->begun = false;
    if (!e->dc.contention) return GNOC_OK;   // closed form finished in gnoc_run_begin
@@ -2445,6 +2490,10 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
    out->abi_pad = 0;
    out->window_ps_x = dm[0];
    out->window_ps_y = dm[1];
+   out->runs = e->runs;
+   out->retries_total = e->tot_retry;
+   out->fallbacks_total = e->tot_fallback;
+   out->abi_pad2 = 0;
    if (e->ran && e->dc.contention)
    {
       std::vector<uint64_t> m((size_t) e->dc.N * PORTS);

@@ -15,6 +15,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNOC_LIB", os.path.join(_HERE, "_build", "libgnoc.so"))
+ABI_VERSION = 3   # include/gnoc.h GNOC_ABI_VERSION
 
 GNOC_OK = 0
 GNOC_EINVAL = -1
@@ -43,6 +44,7 @@ EXPORTED = (
     "gnoc_shard", "gnoc_exchange_counts", "gnoc_run_begin", "gnoc_run_finish",
     "gnoc_create_sweep", "gnoc_sweep_layout", "gnoc_get_port_utilization", "gnoc_create_hop_counter",
     "gnoc_get_broadcast_results", "gnoc_get_broadcast_info", "gnoc_set_basic_moving_average",
+    "gnoc_build_id",
 )
 
 
@@ -106,6 +108,10 @@ class GnocSummary(ctypes.Structure):
         ("abi_pad", ctypes.c_uint32),
         ("window_ps_x", ctypes.c_uint64),
         ("window_ps_y", ctypes.c_uint64),
+        ("runs", ctypes.c_uint32),
+        ("retries_total", ctypes.c_uint32),
+        ("fallbacks_total", ctypes.c_uint32),
+        ("abi_pad2", ctypes.c_uint32),
     ]
 
 
@@ -147,6 +153,13 @@ def load() -> ctypes.CDLL:
         ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_uint64, ctypes.c_double, ctypes.c_int32, vp, vp, vp, vp, sz, ctypes.POINTER(sz)]
     lib.gnoc_abi_version.argtypes = []
+    # an older library (A/B timing against an earlier build) fills a prefix of the
+    # summary and has no build id
+    if not 2 <= lib.gnoc_abi_version() <= ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: ABI {lib.gnoc_abi_version()}, this module speaks {ABI_VERSION}")
+    if hasattr(lib, "gnoc_build_id"):
+        lib.gnoc_build_id.argtypes = []
+        lib.gnoc_build_id.restype = ctypes.c_char_p
     lib.gnoc_trace_file_write.argtypes = [ctypes.c_char_p, ctypes.POINTER(GnocConfig), ctypes.POINTER(GnocPackets), sz]
     lib.gnoc_trace_file_write_q.argtypes = [ctypes.c_char_p, ctypes.POINTER(GnocConfig), ctypes.POINTER(GnocTraceQueue),
                                             ctypes.POINTER(GnocPackets), sz]

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GNOC_ABI_VERSION 2
+#define GNOC_ABI_VERSION 3
 
 /* error codes */
 #define GNOC_OK             0
@@ -139,8 +139,8 @@ typedef struct gnoc_summary
    uint32_t engine_path;        /* 0 whole-port streams, 1 chunked look-back, 2 closed form,
                                    3 serial moving-average queues, 4 port chains in time windows */
    double   last_run_ms;        /* device time of the last gnoc_run (HIP events)        */
-   /* ABI 2: how the last gnoc_run got there.  Every rerun is exact; these count
-      the cost.  retries: chain-engine reruns with windows half as long (a window
+   /* How the last gnoc_run got there.  Every rerun is exact; these count the
+      cost.  retries: chain-engine reruns with windows half as long (a window
       overflowed LDS); fallbacks: reruns on a slower path (chain -> chunked
       levels when a request would take the M/G/1 branch or an earlier level
       wrote exception tails; chunked -> whole-port streams on a look-back
@@ -149,12 +149,17 @@ typedef struct gnoc_summary
    uint32_t fallbacks;
    uint32_t windows;            /* chain-engine time windows of the last attempt, X phase (0 = not used) */
    uint32_t window_shift;       /* floor(log2) of the X phase's window length in ps     */
-   /* ABI 3: windows per phase, any length (sized from each run's measured fill) */
    uint32_t windows_y;          /* Y phase's windows                                     */
    uint32_t abi_pad;
    uint64_t window_ps_x;        /* window length (ps) of the X phase                     */
    uint64_t window_ps_y;        /* ... of the Y phase                                    */
-} gnoc_summary;
+   /* since the last gnoc_submit: runs, and the retries / fallbacks of all of them
+      (a caller timing several runs checks these, not the last run's) */
+   uint32_t runs;
+   uint32_t retries_total;
+   uint32_t fallbacks_total;
+   uint32_t abi_pad2;
+} gnoc_summary;   /* ABI 3 layout: a client checks gnoc_abi_version() == GNOC_ABI_VERSION first */
 
 /* Replaces NetworkModel::createModel(..., NETWORK_EMESH_HOP_BY_HOP)
  * (network_model.cc:50-71) + the RouterModel/QueueModel::create calls of
@@ -162,6 +167,11 @@ typedef struct gnoc_summary
  * Validates what the reference asserts: N == W*H (:56-58, :309-320), the link
  * delay identity (:126), queue type (queue_model.cc:33-36). */
 int gnoc_create(const gnoc_config *cfg, gnoc_engine **out);
+
+/* The library's build identity: a SHA-256 prefix of the device sources and the
+ * compile flags it was built from (profiles record it; the bench reports a
+ * profile's HBM traffic only for the build that was profiled). */
+const char *gnoc_build_id(void);
 
 /* Replaces the moving-average part of QueueModelBasic's constructor
  * (queue_model_basic.cc:7-30: queue_model/basic/moving_avg_enabled, _type,

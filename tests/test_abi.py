@@ -28,12 +28,25 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_defaults():
     lib = gnoc.load()
-    assert lib.gnoc_abi_version() == 2
+    assert lib.gnoc_abi_version() == 3 == gnoc.ABI_VERSION
+    # the summary layout of ABI 3 (include/gnoc.h): 112 bytes, the cumulative counters last
+    assert ctypes.sizeof(gnoc.GnocSummary) == 112
+    assert gnoc.GnocSummary.runs.offset == 96 and gnoc.GnocSummary.abi_pad2.offset == 108
     c = gnoc.GnocConfig()
     lib.gnoc_config_default(ctypes.byref(c), 1024)
     assert (c.num_tiles, c.flit_width, c.router_delay, c.link_delay) == (1024, 64, 1, 1)
     assert (c.contention_enabled, c.analytical_enabled, c.max_list_size) == (1, 1, 100)
     assert c.frequency_ghz == 1.0 and c.tile_width_mm == 1.0
+
+
+def test_build_id_names_the_sources():
+    """gnoc_build_id is the SHA-256 prefix build() computed over the device sources
+    and flags (profiles/ record it; bench.py pairs a PMC profile with the build)."""
+    import __graft_entry__ as ge
+    lib = gnoc.load()
+    bid = lib.gnoc_build_id().decode()
+    assert re.fullmatch(r"[0-9a-f]{16}", bid), bid
+    assert bid == ge.build_id(), "libgnoc.so is stale: rebuild (__graft_entry__.build())"
 
 
 def test_create_rejects_invalid_config_without_gpu():

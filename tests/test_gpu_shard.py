@@ -104,3 +104,33 @@ def test_local_shards_vs_unsharded(W, n, hot):
     ref = e.results()
     e.close()
     _local_vs(cfg, tr, n, ref)
+
+
+@pytest.mark.parametrize("bad", ["zero_flit", "too_long", "late"])
+def test_bad_packet_on_one_rank_fails_every_rank(bad):
+    """A packet that breaks the submit contract and that only rank 1 keeps (source
+    in its row band, destination in its column band): every rank's gnoc_submit
+    fails alike, since each checks the whole trace (a rank that succeeded alone
+    would wait on its peers in the first exchange)."""
+    import numpy as np
+    from graphite_amd import gnoc
+    from tests.traces import random_trace
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = random_trace(2000, 8, 8, seed=11, max_cycle=3000)
+    k = len(tr) // 2
+    tr.src[k], tr.dst[k], tr.flags[k] = 5 * 8 + 5, 6 * 8 + 6, 0   # rank 1 of 2: rows 4-7, columns 4-7
+    if bad == "zero_flit":
+        tr.bits[k] = 0
+    elif bad == "too_long":
+        tr.bits[k] = 64 * 3000
+    else:
+        tr.inject_ps[k:] = np.uint64(1 << 50)
+    msgs = []
+    for r in range(2):
+        e = gnoc.Engine(cfg)
+        e._check(e.lib.gnoc_shard(e._h, r, 2))
+        with pytest.raises(gnoc.GnocError) as ei:
+            e.submit(tr)
+        msgs.append(str(ei.value))
+        e.close()
+    assert msgs[0] == msgs[1] and str(k) in msgs[0], msgs
