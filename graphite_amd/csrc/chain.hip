@@ -518,7 +518,7 @@ __device__ __forceinline__ gptr<P> sptr(P* p)
    } while (0)
 #endif
 
-template <int NL>
+template <int NL, bool F1>
 __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
 {
    constexpr bool XC = NL == 1;
@@ -528,10 +528,20 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
    const uint64_t wbase = (uint64_t) w * D;
    const uint32_t wlen = (w + 1 < nW) ? (uint32_t) D : (uint32_t) OFF_LIM;   // kept offsets: t' - wbase < wlen
    const bool lastw = w + 1 >= nW;
-   const uint64_t wq = wbase / 1000ull;
-   const uint32_t wr = (uint32_t) (wbase - wq * 1000ull);
-   const uint64_t wb = wq ? wq - 1 : 0;          // base cycle: every request of the window has tc > wb (w > 0)
+   const double fq = a.c.f;
+   // base cycle wb: every request of the window has tc >= wb (1 GHz: ceil(t / 1000) > wq - 1;
+   // any other frequency: Time::toCycles is monotone in t, so tc >= toCycles(wbase) > wb)
+   const uint64_t wq = F1 ? wbase / 1000ull : cyc_of<false>(wbase, fq);
+   const uint32_t wr = F1 ? (uint32_t) (wbase - wq * 1000ull) : 0u;
+   const uint64_t wb = wq ? wq - 1 : 0;
    const uint32_t d0 = (uint32_t) (wq - wb);
+   // window-relative cycles of a stream offset (time_types.h:104-109) and the ps of a
+   // contention delay (:81-86): integer at 1 GHz, the reference's double expressions otherwise
+   auto cyc = [&](uint32_t off) -> uint32_t {
+      if (F1) return rcyc(off, wr, d0);
+      return (uint32_t) (cyc_of<false>(wbase + off, fq) - wb);
+   };
+   auto cps = [&](uint32_t cc) -> uint64_t { return F1 ? (uint64_t) cc * 1000ull : ps_of<false>(cc, fq); };
    const uint32_t len = a.len;
    const uint32_t cpb = c * len;
    const uint32_t mode0 = a.c.analytical ? 1u : 0u;
@@ -591,7 +601,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
             const bool valid = (uint32_t) r * T + lane < n;
             const uint32_t p = aux_F(ra[r]);
             uint32_t A = valid ? p : 0u;
-            uint32_t B = valid ? rcyc((uint32_t) (rk[r] >> 32), wr, d0) + p : 0u;
+            uint32_t B = valid ? cyc((uint32_t) (rk[r] >> 32)) + p : 0u;
             wave_scan(A, B);
             const uint32_t rA = rdl(A, 63), rB = rdl(B, 63);
             const uint32_t nb = totB + rA;
@@ -734,7 +744,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          const uint32_t off = (uint32_t) (rk[r] >> 32);
          const uint32_t id = (uint32_t) rk[r];
          const uint32_t ax = ra[r];
-         const uint32_t tc = rcyc(off, wr, d0);
+         const uint32_t tc = cyc(off);
          const uint32_t p = aux_F(ax);
          // the row's exclusive prefix (rescanned: registers for 11 rows of prefixes cost
          // more than the scan)
@@ -755,7 +765,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          }
          Xc = rdl(Xa, (int) min(63u, n - 1 - p0));
          ssum += cc;
-         const uint64_t dn = (uint64_t) off + (uint64_t) cc * 1000ull + rl;   // t' - wbase
+         const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
          // route ranks: a packed (8 bits per field) prefix count over the row
          const uint32_t f = (fpack >> (2 * r)) & 3u;
          const uint32_t one = valid ? 1u << (8 * f) : 0u;
@@ -868,7 +878,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
    }
 }
 
-template <int NL>
+template <int NL, bool F1>
 __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
 {
    __shared__ Smem sm;
@@ -889,7 +899,7 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
       tk = rdl(tk, 0);
       if (tk >= ntasks || flagged(a)) return;
       const uint32_t cw = a.tasks[tk];
-      task<NL>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
+      task<NL, F1>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
       wsync();
    }
 }

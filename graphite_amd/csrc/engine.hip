@@ -442,8 +442,8 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
       e->level_grid = std::max(1, per_cu) * std::max(1, cus);
       // the chain kernels' residency (a grid beyond it only queues: tasks are handed out in order)
       int c1 = 0, c3 = 0;
-      if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c1, ch::k_chain<1>, ch::T, 0);
-      if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c3, ch::k_chain<3>, ch::T, 0);
+      if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c1, ch::k_chain<1, true>, ch::T, 0);
+      if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c3, ch::k_chain<3, true>, ch::T, 0);
       e->ch_grid = std::max(1, std::min(c1, c3)) * std::max(1, cus);
    }
    if (he != hipSuccess)
@@ -1288,7 +1288,7 @@ static bool chain_usable(const gnoc_engine* e)
 {
    const char* env = std::getenv("GNOC_ENGINE");
    if (env && (std::strcmp(env, "levels") == 0 || std::strcmp(env, "v1") == 0)) return false;
-   return e->ch_on && e->f1 && !e->nb && !e->force_levels && !e->ch_declined && !e->force_v1 && !e->dc.hop_counter &&
+   return e->ch_on && !e->nb && !e->force_levels && !e->ch_declined && !e->force_v1 && !e->dc.hop_counter &&
           e->dc.max_list >= 3 && (e->dc.W > 1 || e->dc.H > 1) && e->rec_bound < (1ull << 32);   // u32 record indices
 }
 
@@ -1381,8 +1381,11 @@ static int chain_phase(gnoc_engine* e, int phase)
       a.stamps = sb.as<uint64_t>();
    }
    const uint32_t grid = (uint32_t) std::min<uint64_t>((uint64_t) e->ch_grid, (uint64_t) a.ntasks);
-   if (phase) GNOC_LAUNCH(e, KC_CHAIN, ch::k_chain<3>, dim3(grid), dim3(ch::T), 0, s, a);
-   else GNOC_LAUNCH(e, KC_CHAIN, ch::k_chain<1>, dim3(grid), dim3(ch::T), 0, s, a);
+   // f != 1 GHz: the copy with the reference's double ps <-> cycle conversions
+   if (phase && e->f1) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<3, true>), dim3(grid), dim3(ch::T), 0, s, a);
+   else if (phase) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<3, false>), dim3(grid), dim3(ch::T), 0, s, a);
+   else if (e->f1) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<1, true>), dim3(grid), dim3(ch::T), 0, s, a);
+   else GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<1, false>), dim3(grid), dim3(ch::T), 0, s, a);
    return GNOC_OK;
 }
 

@@ -122,9 +122,23 @@ def test_non_unit_frequency(freq):
     eng.submit(tr)
     eng.run()
     got = eng.results()
-    assert eng.summary()["engine_path"] == 1      # the chunked kernel with the double ps <-> cycle conversions
+    assert eng.summary()["engine_path"] in (1, 4)   # chunked or chain kernels with the double ps <-> cycle conversions
     eng.close()
     assert_same(got, oracle.run(cfg, tr))
+
+
+@pytest.mark.parametrize("freq", [0.9, 1.25, 0.7, 1.5])
+def test_non_unit_frequency_chain_engine(freq):
+    """f != 1 GHz on the chain engine (Time::toCycles / Latency::toPicosec, time_types.h:81-109,
+    as the reference's double expressions): a 16x16 synthetic batch stays on engine path 4
+    and is bit-exact, ports included."""
+    cfg = gnoc.EngineConfig(num_tiles=256, frequency_ghz=freq)
+    tr = gnoc.synthetic_trace(16, 16, 0.01, 300, seed=int(freq * 100), frequency_ghz=freq)
+    got, ref = run_both(cfg, tr)
+    assert got.summary["engine_path"] == 4 and got.summary["fallbacks"] == 0
+    assert_same(got, ref)
+    for k in ("port_flit", "port_last"):
+        assert np.array_equal(getattr(got, k), getattr(ref, k)), k
 
 
 @pytest.mark.parametrize("freq", [0.9, 1.25])
