@@ -600,8 +600,9 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
             if ((uint32_t) r * T >= n) break;
             const bool valid = (uint32_t) r * T + lane < n;
             const uint32_t p = aux_F(ra[r]);
+            const uint32_t tcv = cyc((uint32_t) (rk[r] >> 32)) + p;   // (every lane: no exec branch)
             uint32_t A = valid ? p : 0u;
-            uint32_t B = valid ? cyc((uint32_t) (rk[r] >> 32)) + p : 0u;
+            uint32_t B = valid ? tcv : 0u;
             wave_scan(A, B);
             const uint32_t rA = rdl(A, 63), rB = rdl(B, 63);
             const uint32_t nb = totB + rA;
@@ -622,6 +623,11 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
                if (lane == 0) flag_overflow(a, c);
                return;
             }
+            // the prefetched inserts are consumed only here: tie them to the scan's result so
+            // the compiler cannot hoist their use (and the wait for their loads, which also
+            // waits for the previous step's stores) to the top of the step
+#pragma unroll
+            for (int q = 0; q < IROWS; q++) asm volatile("" : "+v"(iv[q].t), "+v"(iv[q].id), "+v"(iv[q].aux) : "s"(totB));
             if (land_inserts<NL>(sm, iv, itot, wbase, pd1) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
          }
          CH_STAMP(3);
@@ -703,6 +709,9 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
             take += (uint32_t) __popcll(mt);
             if (__ballot(g < spn && !early && !in)) break;   // the rest leave after this window
          }
+         // the spill-in loads have all landed (a wait the compiler sees: no load stays
+         // pending into the output rows, where a vmcnt(0) would also wait for the stores)
+         __builtin_amdgcn_s_waitcnt(0x0F70);
          wsync();
          if (!nin_prev) Kout = Kpp + skip + take;   // the consumed prefix of the old spills
          if (!take) break;                          // nothing merged: the scan stands
@@ -734,7 +743,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       const gptr<uint32_t> samp_id = sptr(a.samp_id);
       uint64_t ssum = 0;
       uint32_t Xc = Xr, nkeep = 0, fgap = NONE, ffire = NONE;
-      bool spilled = false, bad = false, route = false;
+      uint64_t rte = 0, spm = 0;   // lanes (over all rows) that overflowed an output slot / spilled
 #pragma unroll
       for (int r = 0; r < ROWS; r++)
       {
@@ -753,8 +762,9 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          const uint32_t exA = dpp32<0x138, 0xF, 0xF>(A), exB = dpp32<0x138, 0xF, 0xF>(B);   // wave_shr 1
          const uint32_t xa = Xc + exA;
          const uint32_t Xb = xa > exB ? xa : exB;
-         const uint32_t cc = valid && Xb > tc ? Xb - tc : 0u;
-         const uint32_t Xa = (Xb > tc ? Xb : tc) + p;
+         const uint32_t Xm = Xb > tc ? Xb : tc;
+         const uint32_t cc = valid ? Xm - tc : 0u;
+         const uint32_t Xa = Xm + p;
          if (mode)
          {
             // history tree with no gap yet: an idle period makes one (:79-86); the M/G/1
@@ -775,50 +785,41 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
          const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
          run_t += field_cnt(rdl(inc, 63), lane);
-         // continuing: kept (a prefix of the window's continuing records) or spilled
+         // continuing: kept (a prefix of the window's continuing records) or spilled;
+         // everything else leaves through one 16-B write-through store (turns and spills
+         // alike: a spill is read in-launch by task (chain, w+1), MI355X_MICROARCH.md
+         // "Valid forms"; a turn by the next launch)
          const bool keep = valid && f == 1 && dn < wlen;
+         const bool out = valid && !keep;
+         const bool st = out && rank < room;
          nkeep += (uint32_t) __popcll(__ballot(keep));
+         rte |= __ballot(out && rank >= room);
+         spm |= __ballot(st && f == 1);
          if (keep)
          {
             sm.key[kb + rank] = (dn << 32) | id;
             sm.aux[kb + rank] = ax;
          }
-         else if (valid)
+         if (st)
          {
             const uint64_t gp = (uint64_t) gb + rank;
             const uint64_t tn = wbase + dn;
-            if (rank >= room) route = true;
-            else if (f == 1)
+            const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
+            __hip_atomic_store(q, tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(q + 1, (uint64_t) id | ((uint64_t) ax << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((gp & 63) == 0)
             {
-               // spill: taken by task (chain, w+1) at the next port (sc1: read in-launch)
-               bad |= lastw;   // the last window keeps everything (or its offsets overflowed)
-               uint64_t* q = reinterpret_cast<uint64_t*>(a.recs + gp);
-               st1(q, tn);
-               st1(q + 1, (uint64_t) id | ((uint64_t) ax << 32));
-               spilled = true;
-            }
-            else
-            {
-               typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-               v4u o;
-               o.x = (uint32_t) tn;
-               o.y = (uint32_t) (tn >> 32);
-               o.z = id;
-               o.w = ax;
-               *(gptr<v4u>) (recs + gp) = o;
-               if ((gp & 63) == 0)
-               {
-                  samp_t[gp >> 6] = tn;
-                  samp_id[gp >> 6] = id;
-               }
+               samp_t[gp >> 6] = tn;
+               samp_id[gp >> 6] = id;
             }
          }
       }
       CH_STAMP(6);
-      if (__any(route) && lane == 0) flag(a, F_ROUTE);
-      if (__any(bad) && lane == 0) flag(a, F_FALLBACK | R_LASTSPILL);
+      const bool spilled = spm != 0;
+      if (rte && lane == 0) flag(a, F_ROUTE);
+      if (spilled && lastw && lane == 0) flag(a, F_FALLBACK | R_LASTSPILL);   // the last window keeps everything
       const uint64_t ssw = rdl64(wave_sum64(ssum), 63);
-      if (__any(spilled)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drained before the next publish
+      if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drained before the next publish
       wsync();
 
       // ---- [F] late publish (no gap yet), port counters, route check
