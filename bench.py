@@ -95,7 +95,15 @@ def main():
     tr = gnoc.synthetic_trace(W, H, load, a.ppt, seed=seed, hotspot_fraction=hot, num_hotspots=16)
     gen_s = time.time() - t0
     cfg = gnoc.EngineConfig(num_tiles=W * H, device=local)
-    eng = gnoc.ShardedEngine(cfg, rank, world) if sharded else gnoc.Engine(cfg)
+    # N > 1 over RCCL: the exchange inside libgnoc (gnoc_run_sharded on an RCCL
+    # communicator of libgnoc's own, grouped ncclSend / ncclRecv on the engine's
+    # stream); GNOC_BENCH_NATIVE=0 (or the gloo rehearsal) drives it from torch instead
+    native = sharded and backend == "nccl" and os.environ.get("GNOC_BENCH_NATIVE", "1") != "0"
+    comm = gnoc.RcclComm(world, rank, local) if native else None
+    if native:
+        eng = gnoc.NativeShardedEngine(cfg, rank, world, comm)
+    else:
+        eng = gnoc.ShardedEngine(cfg, rank, world) if sharded else gnoc.Engine(cfg)
     eng.submit(tr)          # trace now resident in HBM; steps start from there
 
     def barrier_sync():
@@ -110,17 +118,35 @@ def main():
     # end to end (SURVEY.md 8(d) "trace resident in host memory -> results in host
     # memory"): submit from pinned host arrays (host-side trace validation + H2D),
     # run, final_ps back into a pinned host array; reported beside the HBM-resident value
-    e2e_ms = None
+    e2e_ms = e2e_serial_ms = None
     if not sharded:
         ptr = pinned_trace(tr)
-        fin = torch.empty(len(tr), dtype=torch.int64, pin_memory=True).numpy()
+        fins = [torch.empty(len(tr), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64) for _ in range(2)]
+        K = max(2, a.steps // 2)
+        # one batch at a time: submit (H2D + device checks), run, final_ps read-back
         barrier_sync()
         t_e = time.perf_counter()
-        for _ in range(max(1, a.steps // 2)):
+        for _ in range(K):
             eng.submit(ptr)
             eng.run()
-            eng.final_ps_into(fin)
-        e2e_ms = (time.perf_counter() - t_e) / max(1, a.steps // 2) * 1e3
+            eng.final_ps_into(fins[0])
+        e2e_serial_ms = (time.perf_counter() - t_e) / K * 1e3
+        # pipelined (gnoc_submit_async / gnoc_fetch_final_ps): batch k+1's upload and
+        # batch k's read-back run on copy streams beside the runs
+        barrier_sync()
+        t_e = time.perf_counter()
+        eng.submit(ptr)
+        for k in range(K):
+            if k + 1 < K:
+                eng.submit_async(ptr)
+            eng.run()
+            eng.fetch_final_ps(fins[k % 2])
+            if k + 1 < K:
+                eng.submit_commit()
+        eng.fetch_wait()
+        e2e_ms = (time.perf_counter() - t_e) / K * 1e3
+        want = eng.results().final_ps
+        assert all(np.array_equal(f, want) for f in fins), "pipelined read-back differs from the run's final_ps"
 
     # this rank's share: mesh hops through the ports it owns, packets it delivers
     res = eng.results()
@@ -187,7 +213,8 @@ def main():
                 "workload": workload,
                 "tiles": W * H, "packets": len(tr) * (world if wl == "replicas" else 1), "mesh_hops": int(hops_all),
                 "flit_width": 64, "router_delay": 1, "link_delay": 1, "queue": "history_tree+mg1",
-                "parallelism": (f"rowband/colband{world} + RCCL all-to-all" if sharded and world > 1 else
+                "parallelism": (f"rowband/colband{world} + RCCL grouped send/recv in libgnoc" if native else
+                                f"rowband/colband{world} + torch all-to-all ({backend})" if sharded and world > 1 else
                                 f"replicas{world}" if world > 1 else "single"),
                 "engine_path": int(summ.get("engine_path", -1)),
                 "windows": [int(summ.get("windows", 0)), int(summ.get("windows_y", 0))],
@@ -199,7 +226,10 @@ def main():
             "settle_runs": m["settle_runs"],
             "build_id": bid,
             "e2e_ms_per_step": e2e_ms,
-            "e2e_note": "submit from pinned host memory (H2D + device-side trace checks) + run + final_ps D2H",
+            "e2e_serial_ms_per_step": e2e_serial_ms,
+            "e2e_note": "host trace (pinned) -> host final_ps per batch: submit (H2D + device-side trace checks) + run + "
+                        "final_ps D2H; e2e_ms_per_step pipelined (batch k+1's upload and batch k's read-back on copy "
+                        "streams beside the runs), e2e_serial_ms_per_step one batch at a time",
             "roofline": {
                 "bound": "hbm",
                 "achieved": rf["achieved"],
@@ -232,6 +262,8 @@ def main():
             sys.exit(3)
 
     eng.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -53,6 +53,9 @@ constexpr int T = 64;
 #ifndef CH_ROWS_V
 #define CH_ROWS_V 11
 #endif
+#ifndef CH_KEEPSCAN
+#define CH_KEEPSCAN 0                     // 1: [E] reuses [B]'s row scans (registers; spills at 4 waves per SIMD, measured slower at 3)
+#endif
 constexpr int ROWS = CH_ROWS_V;           // stream rows per (port, window)
 constexpr int CAP = ROWS * T;             // stream records per (port, window)
 constexpr int IROWS = 2;
@@ -511,6 +514,8 @@ __device__ __forceinline__ gptr<P> sptr(P* p)
    {                                                                                                       \
       if (a.stamps && lane == 0) a.stamps[((uint64_t) tk * len + i) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
    } while (0)
+#elif defined(CH_MARKS)
+#define CH_STAMP(k) asm volatile(";;MARK " #k ::: "memory")   // static instruction counts per phase (asm listing)
 #else
 #define CH_STAMP(k) \
    do             \
@@ -564,6 +569,11 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
 
    uint64_t rk[ROWS];
    uint32_t ra[ROWS];
+#if CH_KEEPSCAN
+   // [B]'s inclusive row scans reused by [E]: B, (exclusive field rank << 17 | A), and the
+   // row's field totals in lane r of rcnt
+   uint32_t sB[ROWS], sAR[ROWS], rcnt = 0;
+#endif
    uint32_t nK = 0;              // this port's kept records
    uint32_t P0cur = 0, nin_prev = 0, ncont_prev = 0;   // this port's chain input: records before / kept / all of this window
    uint32_t ob1p = 0, oc1p = 0;  // the previous port's chain output slot (spill-ins)
@@ -610,7 +620,16 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
             totA += rA;
             const uint32_t f = route_field<XC>(nx, ny, ra[r]);
             fpack |= (valid ? f : 0u) << (2 * r);
-            tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
+            const uint32_t inc = wave_sum32(valid ? 1u << (8 * f) : 0u);
+            tc_t += field_cnt(rdl(inc, 63), lane);
+#if CH_KEEPSCAN
+            {
+               const uint32_t one = valid ? 1u << (8 * f) : 0u;
+               sB[r] = B;
+               sAR[r] = A | ((((inc - one) >> (8 * f)) & 0xFFu) << 17);   // A < 64 * 2048
+               rcnt = lane == (uint32_t) r ? rdl(inc, 63) : rcnt;
+            }
+#endif
          }
          if (!first) break;
          CH_STAMP(2);
@@ -635,7 +654,13 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          // ---- [D] predecessor's state
          bool ok = true;
          uint64_t X_in = 0;
+#ifdef CH_NOWAIT
+         // timing experiment only (results invalid): no hand-off wait, a neutral predecessor
+         pv = 0;
+         if (false)
+#else
          if (w)
+#endif
          {
             ok = poll_words(a, stp, SW, lane, pv);
             X_in = rdl64(pv, 0) & M48;
@@ -757,8 +782,12 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          const uint32_t p = aux_F(ax);
          // the row's exclusive prefix (rescanned: registers for 11 rows of prefixes cost
          // more than the scan)
+#if CH_KEEPSCAN
+         const uint32_t A = sAR[r] & 0x1FFFFu, B = sB[r];
+#else
          uint32_t A = valid ? p : 0u, B = valid ? tc + p : 0u;
          wave_scan(A, B);
+#endif
          const uint32_t exA = dpp32<0x138, 0xF, 0xF>(A), exB = dpp32<0x138, 0xF, 0xF>(B);   // wave_shr 1
          const uint32_t xa = Xc + exA;
          const uint32_t Xb = xa > exB ? xa : exB;
@@ -778,13 +807,19 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
          // route ranks: a packed (8 bits per field) prefix count over the row
          const uint32_t f = (fpack >> (2 * r)) & 3u;
+#if CH_KEEPSCAN
+         const uint32_t rank = sAR[r] >> 17;
+         const uint32_t rtot = rdl(rcnt, r);
+#else
          const uint32_t one = valid ? 1u << (8 * f) : 0u;
          const uint32_t inc = wave_sum32(one);
          const uint32_t rank = ((inc - one) >> (8 * f)) & 0xFFu;
+         const uint32_t rtot = rdl(inc, 63);
+#endif
          const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
          const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
          const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
-         run_t += field_cnt(rdl(inc, 63), lane);
+         run_t += field_cnt(rtot, lane);
          // continuing: kept (a prefix of the window's continuing records) or spilled;
          // everything else leaves through one 16-B write-through store (turns and spills
          // alike: a spill is read in-launch by task (chain, w+1), MI355X_MICROARCH.md

@@ -75,6 +75,11 @@ struct DevBuf
       return e;
    }
    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+   void swap(DevBuf& o)
+   {
+      std::swap(p, o.p);
+      std::swap(bytes, o.bytes);
+   }
 };
 
 }  // namespace
@@ -112,6 +117,17 @@ struct gnoc_engine
    const uint32_t *d_src = nullptr, *d_dst = nullptr, *d_bits = nullptr, *d_flags = nullptr;
    DevBuf t_inj, t_src, t_dst, t_bits, t_flags;
    DevBuf vbuf;                             // submit-time checks and statistics (k_validate)
+   // pipelined batches (gnoc_submit_async / gnoc_submit_commit / gnoc_fetch_final_ps):
+   // the next batch's trace lands in a second buffer set on a copy stream while a
+   // run computes; a run's final_ps is read back on another copy stream while the
+   // next run writes a second final_ps buffer (ev_fin / ev_alt: the last read-back
+   // of each buffer)
+   hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+   hipEvent_t ev_h2d = nullptr, ev_done = nullptr, ev_fin = nullptr, ev_alt = nullptr;
+   DevBuf t2_inj, t2_src, t2_dst, t2_bits, t2_flags, final_alt;
+   bool staged = false, fetched = false;
+   gnoc_packets staged_pk{};
+   size_t staged_n = 0;
    // gnoc_run_sharded: the engine's own exchange buffers and transport
    DevBuf xsend, xrecv, xflag;
    gnoc_transport tp{};
@@ -571,6 +587,14 @@ void gnoc_destroy(gnoc_engine* e)
    if (e->h_pinned) (void) hipHostFree(e->h_pinned);
    if (e->h_nmax) (void) hipHostFree(e->h_nmax);
    for (hipEvent_t ev : e->evpool) (void) hipEventDestroy(ev);
+   for (hipStream_t q : { e->s_h2d, e->s_d2h })
+      if (q)
+      {
+         (void) hipStreamSynchronize(q);
+         (void) hipStreamDestroy(q);
+      }
+   for (hipEvent_t ev : { e->ev_h2d, e->ev_done, e->ev_fin, e->ev_alt })
+      if (ev) (void) hipEventDestroy(ev);
    if (e->stream) (void) hipStreamDestroy(e->stream);
    delete e;
 }
@@ -982,6 +1006,8 @@ static int partition_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n, gno
    return GNOC_OK;
 }
 
+static int submit_tail(gnoc_engine* e, const gnoc_packets* pk, size_t n);
+
 int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk_in, size_t n)
 {
    if (!e || !pk_in) return GNOC_EINVAL;
@@ -1040,6 +1066,14 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk_in, size_t n)
       }
       e->dc.g2l = e->d_g2l.as<uint32_t>();
    }
+   return submit_tail(e, pk, n);
+}
+
+// The rest of a host-trace submit, once the trace is in the engine's buffers
+// (d_inj .. d_flags, n): the device-side contract checks and statistics, the
+// record bound, broadcast tables (from the host flags), the exchange layout.
+static int submit_tail(gnoc_engine* e, const gnoc_packets* pk, size_t n)
+{
    uint64_t records = 0, nbc = 0;
    int rc = device_validate(e, n, &records, &nbc);   // (its sync also ends the copies)
    if (rc) return rc;
@@ -1057,6 +1091,103 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk_in, size_t n)
    e->submitted = true;
    e->ran = false;
    e->begun = false;
+   return GNOC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// pipelined batches: upload of batch k+1 and read-back of batch k-1 beside run k
+// ---------------------------------------------------------------------------
+static hipError_t pipe_streams(gnoc_engine* e)
+{
+   hipError_t he = hipSuccess;
+   if (!e->s_h2d) he = hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking);
+   if (he == hipSuccess && !e->s_d2h) he = hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking);
+   for (hipEvent_t* ev : { &e->ev_h2d, &e->ev_done, &e->ev_fin, &e->ev_alt })
+      if (he == hipSuccess && !*ev) he = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+   return he;
+}
+
+int gnoc_submit_async(gnoc_engine* e, const gnoc_packets* pk, size_t n)
+{
+   if (!e || !pk) return GNOC_EINVAL;
+   if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return fail(e, GNOC_EINVAL, "null trace array");
+   if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
+   if (e->nranks > 1) return fail(e, GNOC_EUNSUPPORTED, "a sharded engine takes gnoc_submit");
+   if (e->staged) return fail(e, GNOC_ESTATE, "a staged batch is waiting for gnoc_submit_commit");
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   GNOC_HIP(e, pipe_streams(e));
+   GNOC_HIP(e, e->t2_inj.ensure(n * 8));
+   GNOC_HIP(e, e->t2_src.ensure(n * 4));
+   GNOC_HIP(e, e->t2_dst.ensure(n * 4));
+   GNOC_HIP(e, e->t2_bits.ensure(n * 4));
+   GNOC_HIP(e, e->t2_flags.ensure(n * 4));
+   if (n)
+   {
+      hipStream_t q = e->s_h2d;
+      GNOC_HIP(e, hipMemcpyAsync(e->t2_inj.p, pk->inject_ps, n * 8, hipMemcpyHostToDevice, q));
+      GNOC_HIP(e, hipMemcpyAsync(e->t2_src.p, pk->src, n * 4, hipMemcpyHostToDevice, q));
+      GNOC_HIP(e, hipMemcpyAsync(e->t2_dst.p, pk->dst, n * 4, hipMemcpyHostToDevice, q));
+      GNOC_HIP(e, hipMemcpyAsync(e->t2_bits.p, pk->bits, n * 4, hipMemcpyHostToDevice, q));
+      if (pk->flags) GNOC_HIP(e, hipMemcpyAsync(e->t2_flags.p, pk->flags, n * 4, hipMemcpyHostToDevice, q));
+      else GNOC_HIP(e, hipMemsetAsync(e->t2_flags.p, 0, n * 4, q));
+   }
+   GNOC_HIP(e, hipEventRecord(e->ev_h2d, e->s_h2d));
+   e->staged = true;
+   e->staged_pk = *pk;
+   e->staged_n = n;
+   return GNOC_OK;
+}
+
+int gnoc_submit_commit(gnoc_engine* e)
+{
+   if (!e) return GNOC_EINVAL;
+   if (!e->staged) return fail(e, GNOC_ESTATE, "gnoc_submit_commit without gnoc_submit_async");
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   e->staged = false;
+   e->submitted = false;
+   // the compute stream takes the staged buffers once their upload is done
+   GNOC_HIP(e, hipStreamWaitEvent(e->stream, e->ev_h2d, 0));
+   e->t_inj.swap(e->t2_inj);
+   e->t_src.swap(e->t2_src);
+   e->t_dst.swap(e->t2_dst);
+   e->t_bits.swap(e->t2_bits);
+   e->t_flags.swap(e->t2_flags);
+   const size_t n = e->staged_n;
+   e->part = false;
+   e->n_glob = n;
+   e->dc.g2l = nullptr;
+   e->d_inj = e->t_inj.as<uint64_t>();
+   e->d_src = e->t_src.as<uint32_t>();
+   e->d_dst = e->t_dst.as<uint32_t>();
+   e->d_bits = e->t_bits.as<uint32_t>();
+   e->d_flags = e->t_flags.as<uint32_t>();
+   e->n = n;
+   e->dc.npk = n;
+   gnoc_packets pk = e->staged_pk;
+   return submit_tail(e, &pk, n);
+}
+
+int gnoc_fetch_final_ps(gnoc_engine* e, uint64_t* host_out, size_t n)
+{
+   if (!e || !host_out) return GNOC_EINVAL;
+   if (!e->ran) return fail(e, GNOC_ESTATE, "no results: call gnoc_run first");
+   if (e->part || e->nranks > 1) return fail(e, GNOC_EUNSUPPORTED, "a sharded rank's results: gnoc_get_packet_results");
+   if (n != e->n) return fail(e, GNOC_EINVAL, "n differs from the submitted batch");
+   if (e->nb) return fail(e, GNOC_EUNSUPPORTED, "broadcast batches: gnoc_get_packet_results");
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   GNOC_HIP(e, pipe_streams(e));
+   GNOC_HIP(e, hipEventRecord(e->ev_done, e->stream));
+   GNOC_HIP(e, hipStreamWaitEvent(e->s_d2h, e->ev_done, 0));
+   if (n) GNOC_HIP(e, hipMemcpyAsync(host_out, e->final_ps.p, n * 8, hipMemcpyDeviceToHost, e->s_d2h));
+   GNOC_HIP(e, hipEventRecord(e->ev_fin, e->s_d2h));
+   e->fetched = true;   // the next run writes the other buffer
+   return GNOC_OK;
+}
+
+int gnoc_fetch_wait(gnoc_engine* e)
+{
+   if (!e) return GNOC_EINVAL;
+   if (e->s_d2h) GNOC_HIP(e, hipStreamSynchronize(e->s_d2h));
    return GNOC_OK;
 }
 
@@ -1944,6 +2075,16 @@ int gnoc_run(gnoc_engine* e)
 }
 static int run_impl(gnoc_engine* e)
 {
+   if (e->fetched)
+   {
+      // gnoc_fetch_final_ps is reading the last run's final_ps: this run writes the
+      // other buffer, once that buffer's own read-back (two runs ago) has ended
+      GNOC_HIP(e, hipSetDevice(e->cfg.device));
+      e->final_ps.swap(e->final_alt);
+      std::swap(e->ev_fin, e->ev_alt);
+      GNOC_HIP(e, hipStreamWaitEvent(e->stream, e->ev_fin, 0));
+      e->fetched = false;
+   }
    if (e->ma_type && e->dc.contention) return run_ma(e);
    if (e->nranks > 1) return fail(e, GNOC_ESTATE, "sharded engine: use gnoc_run_begin / exchange / gnoc_run_finish");
    const char* env = std::getenv("GNOC_ENGINE");
@@ -2166,6 +2307,38 @@ static int rccl_agree(gnoc_engine* e, int32_t status, int32_t* out)
    return GNOC_OK;
 }
 
+// An RCCL communicator for gnoc_shard_set_comm from the library libgnoc itself
+// links (so the ncclComm_t handed back is one its ncclSend / ncclRecv accept):
+// rank 0 makes the 128-byte unique id, the caller broadcasts it (any channel),
+// every rank joins on its device.
+int gnoc_rccl_unique_id(void* id128)
+{
+   if (!id128) return GNOC_EINVAL;
+   ncclUniqueId id;
+   static_assert(sizeof(ncclUniqueId) == GNOC_RCCL_ID_BYTES, "ncclUniqueId size");
+   if (ncclGetUniqueId(&id) != ncclSuccess) return GNOC_EHIP;
+   std::memcpy(id128, &id, sizeof id);
+   return GNOC_OK;
+}
+
+int gnoc_rccl_comm_init(int32_t nranks, int32_t rank, int32_t device, const void* id128, void** comm)
+{
+   if (!id128 || !comm || nranks < 1 || rank < 0 || rank >= nranks) return GNOC_EINVAL;
+   if (hipSetDevice(device) != hipSuccess) return GNOC_EHIP;
+   ncclUniqueId id;
+   std::memcpy(&id, id128, sizeof id);
+   ncclComm_t c = nullptr;
+   if (ncclCommInitRank(&c, nranks, id, rank) != ncclSuccess) return GNOC_EHIP;
+   *comm = c;
+   return GNOC_OK;
+}
+
+int gnoc_rccl_comm_destroy(void* comm)
+{
+   if (!comm) return GNOC_EINVAL;
+   return ncclCommDestroy(static_cast<ncclComm_t>(comm)) == ncclSuccess ? GNOC_OK : GNOC_EHIP;
+}
+
 int gnoc_shard_set_comm(gnoc_engine* e, void* nccl_comm)
 {
    if (!e) return GNOC_EINVAL;
@@ -2206,7 +2379,10 @@ static int shard_agree(gnoc_engine* e, int rc, const char* what)
 int gnoc_run_sharded(gnoc_engine* e)
 {
    if (!e) return GNOC_EINVAL;
-   if (e->nranks <= 1) return gnoc_run(e);
+   // one rank without a communicator: the plain run; with one, the full protocol
+   // (an empty grouped exchange and the status all-reduces), as every rank of a
+   // larger communicator runs it
+   if (e->nranks <= 1 && !e->nccl && !e->tp.exchange) return gnoc_run(e);
    if (!e->nccl && !e->tp.exchange) return fail(e, GNOC_ESTATE, "gnoc_run_sharded needs gnoc_shard_set_comm or a transport");
    // from here every failure goes through the status agreement, so no peer waits
    // in a collective this rank never joins

@@ -19,6 +19,20 @@
 //     tools/gen_pow_tables.py).
 // tests/cpp/test_pow.cc checks pow() against glibc's on the host over random and
 // special operands, and to_u64_x86 against gcc's cast.
+//
+// Upstream notice.  This header restates the algorithm, constants and operation
+// order of glibc 2.35 sysdeps/ieee754/dbl-64/e_pow.c and e_exp_data.c /
+// e_pow_log_data.c: "Copyright (C) 2018-2022 Free Software Foundation, Inc.
+// This file is part of the GNU C Library", distributed under the GNU Lesser
+// General Public License, version 2.1 or (at your option) any later version.
+// glibc took the algorithm from Arm's optimized-routines (Copyright (c) 2018,
+// Arm Limited; MIT OR Apache-2.0 WITH LLVM-exception).  Those terms apply to
+// this restatement and to pow_tables.h.
+//
+// Exactness holds against THAT pow: the reference's std::pow on an x86-64 host
+// whose glibc 2.35 ifunc picks __pow_fma (FMA + AVX2).  A host without FMA, or
+// another libm, runs another last-bit-inexact routine; geometric-mean results
+// computed there are not pinned by this header.
 #pragma once
 
 #include <cstdint>

@@ -44,7 +44,8 @@ EXPORTED = (
     "gnoc_shard", "gnoc_exchange_counts", "gnoc_run_begin", "gnoc_run_finish",
     "gnoc_create_sweep", "gnoc_sweep_layout", "gnoc_get_port_utilization", "gnoc_create_hop_counter",
     "gnoc_get_broadcast_results", "gnoc_get_broadcast_info", "gnoc_set_basic_moving_average",
-    "gnoc_build_id",
+    "gnoc_build_id", "gnoc_rccl_unique_id", "gnoc_rccl_comm_init", "gnoc_rccl_comm_destroy",
+    "gnoc_submit_async", "gnoc_submit_commit", "gnoc_fetch_final_ps", "gnoc_fetch_wait",
 )
 
 
@@ -181,6 +182,17 @@ def load() -> ctypes.CDLL:
     lib.gnoc_run_begin.argtypes = [vp, vp]
     lib.gnoc_run_finish.argtypes = [vp, vp]
     lib.gnoc_set_basic_moving_average.argtypes = [vp, ctypes.c_int32, ctypes.c_uint32]
+    if hasattr(lib, "gnoc_submit_async"):
+        lib.gnoc_submit_async.argtypes = [vp, ctypes.POINTER(GnocPackets), sz]
+        lib.gnoc_submit_commit.argtypes = [vp]
+        lib.gnoc_fetch_final_ps.argtypes = [vp, vp, sz]
+        lib.gnoc_fetch_wait.argtypes = [vp]
+    lib.gnoc_shard_set_comm.argtypes = [vp, vp]
+    lib.gnoc_run_sharded.argtypes = [vp]
+    if hasattr(lib, "gnoc_rccl_unique_id"):
+        lib.gnoc_rccl_unique_id.argtypes = [vp]
+        lib.gnoc_rccl_comm_init.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, ctypes.POINTER(vp)]
+        lib.gnoc_rccl_comm_destroy.argtypes = [vp]
     _lib = lib
     return lib
 
@@ -407,6 +419,30 @@ class Engine:
     def run(self) -> None:
         self._check(self.lib.gnoc_run(self._h))
 
+    # pipelined batches (gnoc_submit_async / _commit, gnoc_fetch_final_ps / _wait)
+    def submit_async(self, tr: "Trace") -> None:
+        """Start uploading the next batch (page-locked arrays overlap with the run
+        in flight); it becomes current at submit_commit()."""
+        tr = tr.normalized()
+        pk = GnocPackets(tr.inject_ps.ctypes.data, tr.src.ctypes.data, tr.dst.ctypes.data, tr.bits.ctypes.data,
+                         tr.flags.ctypes.data)
+        self._check(self.lib.gnoc_submit_async(self._h, ctypes.byref(pk), len(tr)))
+        self._staged = (tr, len(tr))
+
+    def submit_commit(self) -> None:
+        self._check(self.lib.gnoc_submit_commit(self._h))
+        self._n = self._staged[1]
+        self._staged = None
+
+    def fetch_final_ps(self, out: np.ndarray) -> None:
+        """Start copying the last run's final_ps into `out` (page-locked uint64 of
+        the batch size); complete after fetch_wait()."""
+        assert out.dtype.itemsize == 8 and out.shape[0] == self._n and out.flags["C_CONTIGUOUS"]
+        self._check(self.lib.gnoc_fetch_final_ps(self._h, out.ctypes.data, self._n))
+
+    def fetch_wait(self) -> None:
+        self._check(self.lib.gnoc_fetch_wait(self._h))
+
     def summary(self) -> dict:
         s = GnocSummary()
         self._check(self.lib.gnoc_get_summary(self._h, ctypes.byref(s)))
@@ -571,6 +607,67 @@ class ShardedEngine(Engine):
         o = [0, n, 2 * n, 3 * n, 3 * n + npt, 3 * n + 2 * npt, 3 * n + 3 * npt, 3 * n + 4 * npt, 3 * n + 5 * npt]
         a = [out[o[k]:o[k + 1]].copy() for k in range(8)]
         return Results(*a[:6], summary=r.summary, port_flit=a[6], port_last=a[7])
+
+
+RCCL_ID_BYTES = 128   # GNOC_RCCL_ID_BYTES
+
+
+class RcclComm:
+    """An RCCL communicator made by libgnoc's own RCCL (gnoc_rccl_comm_init), for
+    gnoc_shard_set_comm.  The 128-byte unique id goes from rank 0 to every rank
+    over `broadcast(buf: bytearray)` -- by default torch.distributed's default
+    process group (any backend)."""
+
+    def __init__(self, nranks: int, rank: int, device: int, broadcast=None):
+        self.lib = load()
+        idb = (ctypes.c_ubyte * RCCL_ID_BYTES)()
+        if rank == 0:
+            rc = self.lib.gnoc_rccl_unique_id(ctypes.cast(idb, ctypes.c_void_p))
+            if rc:
+                raise GnocError(rc, "ncclGetUniqueId failed")
+        if nranks > 1:
+            buf = bytearray(bytes(idb))
+            (broadcast or _torch_broadcast_bytes)(buf)
+            ctypes.memmove(idb, bytes(buf), RCCL_ID_BYTES)
+        self.comm = ctypes.c_void_p()
+        rc = self.lib.gnoc_rccl_comm_init(nranks, rank, device, ctypes.cast(idb, ctypes.c_void_p), ctypes.byref(self.comm))
+        if rc:
+            raise GnocError(rc, "ncclCommInitRank failed")
+
+    def close(self) -> None:
+        if self.comm:
+            self.lib.gnoc_rccl_comm_destroy(self.comm)
+            self.comm = ctypes.c_void_p()
+
+
+def _torch_broadcast_bytes(buf: bytearray) -> None:
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(list(buf), dtype=torch.uint8)
+    if dist.get_backend() == "nccl":
+        t = t.cuda()
+    dist.broadcast(t, 0)
+    buf[:] = bytes(t.cpu().tolist())
+
+
+class NativeShardedEngine(Engine):
+    """One rank's share of a sharded mesh with the exchange inside libgnoc:
+    gnoc_shard + gnoc_shard_set_comm(an RcclComm) + gnoc_run_sharded (prep and X
+    phase, grouped ncclSend / ncclRecv of the turn records over xGMI on the
+    engine's stream, Y phase; every rank's status max-reduced around the
+    exchange).  No torch collective and no Python on the data path."""
+
+    def __init__(self, cfg: EngineConfig, rank: int, nranks: int, comm: RcclComm):
+        super().__init__(cfg)
+        self.rank, self.nranks, self.comm_obj = rank, nranks, comm
+        self._check(self.lib.gnoc_shard(self._h, rank, nranks))
+        self._check(self.lib.gnoc_shard_set_comm(self._h, comm.comm))
+
+    def run(self) -> None:
+        self._check(self.lib.gnoc_run_sharded(self._h))
+
+    group = None
+    gathered_results = ShardedEngine.gathered_results
 
 
 class LocalShardSet:

@@ -179,7 +179,9 @@ const char *gnoc_build_id(void);
  * time as MovingAverage::compute(packet time) (queue_model_basic.cc:38-46).
  * Requires queue_type GNOC_QUEUE_BASIC; window_size in [1, 65536] (the
  * reference divides by zero at 0).  All three averages are bit-exact; the
- * geometric mean runs glibc's own pow (graphite_amd/csrc/glibc_pow.h).  Single unsharded mesh engines only
+ * geometric mean runs glibc's own pow (graphite_amd/csrc/glibc_pow.h), so its
+ * exactness holds against a reference built on x86-64 glibc 2.35 whose ifunc
+ * picks __pow_fma (FMA + AVX2); another libm's pow may differ in the last bit.  Single unsharded mesh engines only
  * (GNOC_EUNSUPPORTED for sharded, sweep and hop-counter engines and, at
  * gnoc_run, for broadcast packets).  Takes effect at the next gnoc_run. */
 int gnoc_set_basic_moving_average(gnoc_engine *eng, int32_t type, uint32_t window_size);
@@ -298,8 +300,8 @@ int gnoc_sweep_layout(const gnoc_engine *eng, int32_t *blocks_x, int32_t *blocks
  * Results are bit-identical to an unsharded run.  A rank reports the packets it
  * delivers (destination column in its band) and the ports it owns; every other
  * entry reads 0, so an element-wise sum over ranks is the whole mesh's result.
- * gnoc_run is refused on an engine with n > 1.  Needs f = 1 GHz and
- * max_list_size >= 3 when contention is enabled. */
+ * gnoc_run is refused on an engine with n > 1.  Needs max_list_size >= 3
+ * when contention is enabled. */
 int gnoc_shard(gnoc_engine *eng, int32_t rank, int32_t nranks);
 int gnoc_exchange_counts(gnoc_engine *eng, uint64_t *send_units, uint64_t *recv_units, size_t nranks);
 int gnoc_run_begin(gnoc_engine *eng, void *send_dev);
@@ -328,6 +330,35 @@ typedef struct gnoc_transport
 int gnoc_shard_set_comm(gnoc_engine *eng, void *nccl_comm);
 int gnoc_shard_set_transport(gnoc_engine *eng, const gnoc_transport *tp);
 int gnoc_run_sharded(gnoc_engine *eng);
+/* An ncclComm_t for gnoc_shard_set_comm, made by the RCCL library libgnoc links
+ * (callers without their own RCCL binding, e.g. Python over ctypes): rank 0
+ * calls gnoc_rccl_unique_id, the caller broadcasts the GNOC_RCCL_ID_BYTES bytes
+ * to every rank by any channel, and each rank calls gnoc_rccl_comm_init on its
+ * engine's device (collective: every rank must call it).  gnoc_run_sharded with
+ * a communicator set runs the whole protocol even at one rank. */
+#define GNOC_RCCL_ID_BYTES 128
+int gnoc_rccl_unique_id(void *id_out);
+int gnoc_rccl_comm_init(int32_t nranks, int32_t rank, int32_t device, const void *id, void **comm_out);
+int gnoc_rccl_comm_destroy(void *comm);
+
+/* Pipelined batches (host trace -> host results, SURVEY.md 8d end to end): the
+ * upload of batch k+1 and the read-back of batch k overlap the runs beside them.
+ *   gnoc_submit_async(eng, pk, n)   starts copying a host trace (page-locked for
+ *                                   the copy to overlap) into the engine's second
+ *                                   trace buffer on its own stream and returns; the
+ *                                   arrays stay valid until gnoc_submit_commit
+ *   gnoc_submit_commit(eng)         waits for that copy, checks the batch as
+ *                                   gnoc_submit does and makes it the current one
+ *   gnoc_fetch_final_ps(eng, out, n) starts copying the last run's final_ps into
+ *                                   `out` (page-locked) on a third stream; the next
+ *                                   gnoc_run writes a second buffer meanwhile
+ *   gnoc_fetch_wait(eng)            waits for the started read-backs
+ * e.g. submit(0); loop k: submit_async(k+1); run(k); fetch_final_ps(k);
+ * submit_commit(k+1).  Unsharded engines, unicast batches. */
+int gnoc_submit_async(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
+int gnoc_submit_commit(gnoc_engine *eng);
+int gnoc_fetch_final_ps(gnoc_engine *eng, uint64_t *final_ps_out, size_t n);
+int gnoc_fetch_wait(gnoc_engine *eng);
 
 const char *gnoc_last_error(const gnoc_engine *eng);
 void gnoc_destroy(gnoc_engine *eng);

@@ -134,3 +134,35 @@ def test_bad_packet_on_one_rank_fails_every_rank(bad):
         msgs.append(str(ei.value))
         e.close()
     assert msgs[0] == msgs[1] and str(k) in msgs[0], msgs
+
+
+@pytest.mark.parametrize("W,load,ppt", [(8, 0.05, 300), (32, 0.005, 1000)])
+def test_rccl_one_rank_run_sharded(W, load, ppt):
+    """gnoc_run_sharded over a real RCCL communicator (libgnoc's own RCCL,
+    gnoc_rccl_comm_init) at one rank: the grouped send / receive of the turn
+    exchange and the status all-reduces run on the engine's stream, and the
+    results equal the unsharded run's and the oracle's."""
+    import numpy as np
+    from graphite_amd import gnoc
+    from oracle import oracle
+    cfg = gnoc.EngineConfig(num_tiles=W * W)
+    tr = gnoc.synthetic_trace(W, W, load, ppt, seed=11)
+    comm = gnoc.RcclComm(1, 0, 0)
+    eng = gnoc.NativeShardedEngine(cfg, 0, 1, comm)
+    eng.submit(tr)
+    for _ in range(2):
+        eng.run()
+    got = eng.results()
+    eng.close()
+    comm.close()
+    ref = gnoc.Engine(cfg)
+    ref.submit(tr)
+    ref.run()
+    want = ref.results()
+    ref.close()
+    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1", "port_flit",
+              "port_last"):
+        assert np.array_equal(getattr(got, k), getattr(want, k)), k
+    if W <= 8:
+        orc = oracle.run(cfg, tr)
+        assert np.array_equal(got.final_ps, orc.final_ps)
