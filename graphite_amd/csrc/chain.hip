@@ -53,9 +53,6 @@ constexpr int T = 64;
 #ifndef CH_ROWS_V
 #define CH_ROWS_V 11
 #endif
-#ifndef CH_KEEPSCAN
-#define CH_KEEPSCAN 0                     // 1: [E] reuses [B]'s row scans (registers; spills at 4 waves per SIMD, measured slower at 3)
-#endif
 constexpr int ROWS = CH_ROWS_V;           // stream rows per (port, window)
 constexpr int CAP = ROWS * T;             // stream records per (port, window)
 constexpr int IROWS = 2;
@@ -66,7 +63,19 @@ constexpr int BMW = CAP / 32;             // insert bitmap words over merged pos
 #define CH_MINW 4                         // waves per SIMD the registers must leave room for
 #endif
 constexpr int NLMAX = 3;                  // local insert lists (Y ports: LOCAL, W, E)
-constexpr int SW = 8;                     // state words per (chain port, window)
+// State granules per (chain port, window), each an epoch-tagged u64 written by one
+// sc1 store:
+//   INC  (inclusive, after the look-back): tail X, the 4 cumulative route counts, "no gap yet"
+//   AGG  (own aggregate, before the look-back): B (absolute cycles), A, the 4 window counts
+//   KO   the port's consumed spill prefix after this window
+//   POST (after the outputs, its spill stores drained): the chain outputs before this
+//        window (low 32 bits) and its kept count (bits 32..47)
+constexpr int SW = 12;
+enum : int { G_X = 0, G_CNT = 1, G_MODE = 5, G_AB = 6, G_AA = 7, G_AC = 8, G_KO = 9, G_POST = 10 };
+constexpr uint64_t INC_MASK = 0x3Full, AGG_MASK = 0x1C0ull;
+constexpr int SW_SER = 8;                 // the serial protocol's state: X, 4 counts, "no gap yet", KO, spill end
+constexpr int LB_POST = 2 * SW;           // the look-back prefetch's lane for POST of (w-1, i-1)
+static_assert(LB_POST < 64, "look-back prefetch fits one wave");
 constexpr uint32_t F_RETRY = 1u;          // a window overflowed LDS: rerun with smaller windows
 constexpr uint32_t F_FALLBACK = 2u;       // M/G/1 would fire, exception tails, ...: rerun on the level engine
 constexpr uint32_t F_ROUTE = 4u;          // route-count invariant broken (internal error)
@@ -154,7 +163,7 @@ struct ChainArgs
    uint64_t etag;                 // epoch << 48
    unsigned* nmax;                // [2 c] the most stream records, [2 c + 1] the most inserts of chain c's steps
    uint64_t* stamps;              // debug (GNOC_STAMPS=1): [(task * len + i) * 16 + k] phase stamps, else null
-   uint32_t exp;                  // unused
+   uint32_t lookback;             // 1: look-back over earlier windows' AGG / INC; 0: wait for window w-1's INC
    uint32_t pad1;
 };
 
@@ -286,27 +295,6 @@ __device__ __forceinline__ uint32_t load_pd(const ChainArgs& a, uint32_t cpi, ui
    if (l >= 2u * NL) return 0u;
    const uint32_t j = l < (uint32_t) NL ? l : l - NL;
    return a.bt[bt_off + ((uint64_t) i * NL + j) * (nW + 1) + w + (l < (uint32_t) NL ? 0u : 1u)];
-}
-
-// Poll the state words [0, nw) of block s until all carry the epoch tag (lane
-// q < nw holds word q).  Wave-wide; false on abort.
-__device__ bool poll_words(const ChainArgs& a, const uint64_t* s, uint32_t nw, uint32_t lane, uint64_t& v)
-{
-   const uint64_t t0 = __builtin_amdgcn_s_memtime();
-   for (;;)
-   {
-      bool ok = true;
-      if (lane < nw) ok = (v & ~M48) == a.etag;
-      if (__all(ok)) return true;
-      if (__builtin_amdgcn_s_memtime() - t0 > SPIN_CYCLES)
-      {
-         if (lane == 0) flag(a, F_TIMEOUT);
-         return false;
-      }
-      if (flagged(a)) return false;
-      __builtin_amdgcn_s_sleep(1);
-      if (lane < nw) v = ld1(s + lane);
-   }
 }
 
 // A port's insert lists of this window: [lo_j, hi_j) of list j, clamped to the
@@ -481,17 +469,19 @@ __device__ __forceinline__ uint32_t field_cnt(uint32_t R, uint32_t lane)
 {
    return lane - 1u < 4u ? (R >> (8u * (lane - 1u))) & 0xFFu : 0u;
 }
-// State word `lane` (< SW) of a port after a window: tail X, route counts (the
-// field tables), "no gap yet", the port's unconsumed spill range.
-__device__ __forceinline__ uint64_t state_word(uint32_t lane, uint64_t Xo, uint32_t cnt_t, uint32_t nogap, uint32_t Kout,
-                                               uint32_t Pend)
+// INC granule `lane` (< G_AB) of a port after a window: tail X, the cumulative route
+// counts (the field tables, lanes 1..4), "no gap yet".
+__device__ __forceinline__ uint64_t inc_word(uint32_t lane, uint64_t Xo, uint32_t cnt_t, uint32_t nogap)
 {
    uint64_t v = Xo;
    if (lane - 1u < 4u) v = cnt_t;
-   if (lane == 5) v = nogap;
-   if (lane == 6) v = Kout;
-   if (lane == 7) v = Pend;
+   if (lane == G_MODE) v = nogap;
    return v;
+}
+// Lane l's value of a 64-bit register (ds_bpermute, any lane pattern).
+__device__ __forceinline__ uint64_t sh64(uint64_t v, uint32_t l)
+{
+   return (uint64_t) bperm((uint32_t) v, l & 63u) | ((uint64_t) bperm((uint32_t) (v >> 32), l & 63u) << 32);
 }
 // Keep a kernel-argument pointer in its own scalar pair (not reloaded as part of
 // a wide argument tuple), as a global-memory pointer.
@@ -503,6 +493,8 @@ __device__ __forceinline__ gptr<P> sptr(P* p)
    asm volatile("" : "+s"(p));
    return (gptr<P>) p;
 }
+
+
 
 // ---------------------------------------------------------------------------
 // one task: chain c, window w (one wave)
@@ -523,8 +515,45 @@ __device__ __forceinline__ gptr<P> sptr(P* p)
    } while (0)
 #endif
 
+// ---------------------------------------------------------------------------
+// one task, serial protocol: every window waits for window w-1's state of the
+// port (published as early as possible); the state block holds SW_SER granules
+// ---------------------------------------------------------------------------
+// Poll the state words [0, nw) of block s until all carry the epoch tag (lane
+// q < nw holds word q).  Wave-wide; false on abort.
+__device__ bool poll_words(const ChainArgs& a, const uint64_t* s, uint32_t nw, uint32_t lane, uint64_t& v)
+{
+   const uint64_t t0 = __builtin_amdgcn_s_memtime();
+   for (;;)
+   {
+      bool ok = true;
+      if (lane < nw) ok = (v & ~M48) == a.etag;
+      if (__all(ok)) return true;
+      if (__builtin_amdgcn_s_memtime() - t0 > SPIN_CYCLES)
+      {
+         if (lane == 0) flag(a, F_TIMEOUT);
+         return false;
+      }
+      if (flagged(a)) return false;
+      __builtin_amdgcn_s_sleep(1);
+      if (lane < nw) v = ld1(s + lane);
+   }
+}
+
+// State word `lane` (< SW_SER) of a port after a window: tail X, route counts (the
+// field tables), "no gap yet", the port's unconsumed spill range.
+__device__ __forceinline__ uint64_t state_word_ser(uint32_t lane, uint64_t Xo, uint32_t cnt_t, uint32_t nogap, uint32_t Kout,
+                                               uint32_t Pend)
+{
+   uint64_t v = Xo;
+   if (lane - 1u < 4u) v = cnt_t;
+   if (lane == 5) v = nogap;
+   if (lane == 6) v = Kout;
+   if (lane == 7) v = Pend;
+   return v;
+}
 template <int NL, bool F1>
-__device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
+__device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
 {
    constexpr bool XC = NL == 1;
    const uint32_t lane = threadIdx.x;
@@ -569,11 +598,6 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
 
    uint64_t rk[ROWS];
    uint32_t ra[ROWS];
-#if CH_KEEPSCAN
-   // [B]'s inclusive row scans reused by [E]: B, (exclusive field rank << 17 | A), and the
-   // row's field totals in lane r of rcnt
-   uint32_t sB[ROWS], sAR[ROWS], rcnt = 0;
-#endif
    uint32_t nK = 0;              // this port's kept records
    uint32_t P0cur = 0, nin_prev = 0, ncont_prev = 0;   // this port's chain input: records before / kept / all of this window
    uint32_t ob1p = 0, oc1p = 0;  // the previous port's chain output slot (spill-ins)
@@ -586,7 +610,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       const uint64_t* const stp = w ? stw - SW : nullptr;                           // predecessor's
       CH_STAMP(0);
       uint64_t pv = 0;
-      if (w && lane < (uint32_t) SW) pv = ld1(stp + lane);
+      if (w && lane < (uint32_t) SW_SER) pv = ld1(stp + lane);
       const uint32_t nx = rdl(pd0, PD_NX), ny = rdl(pd0, PD_NY);
 
       // ---- [B] the merged stream in rows; per-row max-plus scans, route-field totals
@@ -622,14 +646,6 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
             fpack |= (valid ? f : 0u) << (2 * r);
             const uint32_t inc = wave_sum32(valid ? 1u << (8 * f) : 0u);
             tc_t += field_cnt(rdl(inc, 63), lane);
-#if CH_KEEPSCAN
-            {
-               const uint32_t one = valid ? 1u << (8 * f) : 0u;
-               sB[r] = B;
-               sAR[r] = A | ((((inc - one) >> (8 * f)) & 0xFFu) << 17);   // A < 64 * 2048
-               rcnt = lane == (uint32_t) r ? rdl(inc, 63) : rcnt;
-            }
-#endif
          }
          if (!first) break;
          CH_STAMP(2);
@@ -654,15 +670,9 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          // ---- [D] predecessor's state
          bool ok = true;
          uint64_t X_in = 0;
-#ifdef CH_NOWAIT
-         // timing experiment only (results invalid): no hand-off wait, a neutral predecessor
-         pv = 0;
-         if (false)
-#else
          if (w)
-#endif
          {
-            ok = poll_words(a, stp, SW, lane, pv);
+            ok = poll_words(a, stp, SW_SER, lane, pv);
             X_in = rdl64(pv, 0) & M48;
             cin_t = lane - 1u < 4u ? (uint32_t) (pv & M48) : 0u;
             mode = (uint32_t) (rdl64(pv, 5) & 1u);
@@ -684,10 +694,10 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          // publish before the outputs unless spill-ins change the stream or the history
          // tree has had no gap yet (then the outputs decide)
          published = !mode && Pep == Kpp;
-         if (published && lane < (uint32_t) SW)
+         if (published && lane < (uint32_t) SW_SER)
          {
             const uint32_t x0 = Xr + totA;
-            st1(stw + lane, a.etag | state_word(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u, Kout, Pend));
+            st1(stw + lane, a.etag | state_word_ser(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u, Kout, Pend));
          }
          if (Pep == Kpp) break;
          // ---- slow path: spill-ins (records the previous port spilled in earlier windows,
@@ -752,10 +762,10 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       }
       CH_STAMP(5);
       // publish now (unless the history tree still has no gap: after the outputs)
-      if (!published && !mode && lane < (uint32_t) SW)
+      if (!published && !mode && lane < (uint32_t) SW_SER)
       {
          const uint32_t x0 = Xr + totA;
-         st1(stw + lane, a.etag | state_word(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u, Kout, Pend));
+         st1(stw + lane, a.etag | state_word_ser(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u, Kout, Pend));
       }
 
       // ---- [E] recurrence and outputs, row by row: kept records in place into the kept list
@@ -782,12 +792,8 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          const uint32_t p = aux_F(ax);
          // the row's exclusive prefix (rescanned: registers for 11 rows of prefixes cost
          // more than the scan)
-#if CH_KEEPSCAN
-         const uint32_t A = sAR[r] & 0x1FFFFu, B = sB[r];
-#else
          uint32_t A = valid ? p : 0u, B = valid ? tc + p : 0u;
          wave_scan(A, B);
-#endif
          const uint32_t exA = dpp32<0x138, 0xF, 0xF>(A), exB = dpp32<0x138, 0xF, 0xF>(B);   // wave_shr 1
          const uint32_t xa = Xc + exA;
          const uint32_t Xb = xa > exB ? xa : exB;
@@ -807,15 +813,10 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
          const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
          // route ranks: a packed (8 bits per field) prefix count over the row
          const uint32_t f = (fpack >> (2 * r)) & 3u;
-#if CH_KEEPSCAN
-         const uint32_t rank = sAR[r] >> 17;
-         const uint32_t rtot = rdl(rcnt, r);
-#else
          const uint32_t one = valid ? 1u << (8 * f) : 0u;
          const uint32_t inc = wave_sum32(one);
          const uint32_t rank = ((inc - one) >> (8 * f)) & 0xFFu;
          const uint32_t rtot = rdl(inc, 63);
-#endif
          const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
          const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
          const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
@@ -864,7 +865,7 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
       {
          // the M/G/1 branch would serve a request that arrives before the first gap
          if (lane == 0 && ffire != NONE && (fgap == NONE || ffire < fgap)) flag(a, F_FALLBACK | R_MG1);
-         if (lane < (uint32_t) SW) st1(stw + lane, a.etag | state_word(lane, Xo, run_t, fgap == NONE ? 1u : 0u, Kout, Pend));
+         if (lane < (uint32_t) SW_SER) st1(stw + lane, a.etag | state_word_ser(lane, Xo, run_t, fgap == NONE ? 1u : 0u, Kout, Pend));
       }
       // every record of the port has passed at the last window: the route counts fill
       // every output slot
@@ -914,7 +915,517 @@ __device__ void task(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint3
    }
 }
 
+
+// ---------------------------------------------------------------------------
+// one task, look-back protocol (AGG / INC / KO / POST granules)
+// ---------------------------------------------------------------------------
 template <int NL, bool F1>
+__device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
+{
+   constexpr bool XC = NL == 1;
+   const uint32_t lane = threadIdx.x;
+   const uint64_t D = a.cw[c].D, st_off = a.cw[c].st_off, bt_off = a.cw[c].bt_off;
+   const uint32_t nW = a.cw[c].nW;
+   const uint64_t wbase = (uint64_t) w * D;
+   const uint32_t wlen = (w + 1 < nW) ? (uint32_t) D : (uint32_t) OFF_LIM;   // kept offsets: t' - wbase < wlen
+   const bool lastw = w + 1 >= nW;
+   const double fq = a.c.f;
+   // base cycle wb: every request of the window has tc >= wb (1 GHz: ceil(t / 1000) > wq - 1;
+   // any other frequency: Time::toCycles is monotone in t, so tc >= toCycles(wbase) > wb)
+   const uint64_t wq = F1 ? wbase / 1000ull : cyc_of<false>(wbase, fq);
+   const uint32_t wr = F1 ? (uint32_t) (wbase - wq * 1000ull) : 0u;
+   const uint64_t wb = wq ? wq - 1 : 0;
+   const uint32_t d0 = (uint32_t) (wq - wb);
+   // window-relative cycles of a stream offset (time_types.h:104-109) and the ps of a
+   // contention delay (:81-86): integer at 1 GHz, the reference's double expressions otherwise
+   auto cyc = [&](uint32_t off) -> uint32_t {
+      if (F1) return rcyc(off, wr, d0);
+      return (uint32_t) (cyc_of<false>(wbase + off, fq) - wb);
+   };
+   auto cps = [&](uint32_t cc) -> uint64_t { return F1 ? (uint64_t) cc * 1000ull : ps_of<false>(cc, fq); };
+   const uint32_t len = a.len;
+   const uint32_t cpb = c * len;
+   const uint32_t mode0 = a.c.analytical ? 1u : 0u;
+   const gptr<Rec> recs = sptr(a.recs);
+
+   // ---- prologue: descriptors of ports 0..2 (with their insert bounds), port 0's
+   // inserts landed, port 1's in flight
+   uint32_t pd0 = load_pd<NL>(a, cpb, bt_off, nW, 0, w);
+   uint32_t pd1 = len > 1 ? load_pd<NL>(a, cpb + 1, bt_off, nW, 1, w) : 0u;
+   uint32_t pd2 = len > 2 ? load_pd<NL>(a, cpb + 2, bt_off, nW, 2, w) : 0u;
+   Rec iv[IROWS];
+   uint32_t nI = fetch_inserts<NL>(a, pd0, iv);
+   if (nI > (uint32_t) ICAP)
+   {
+      if (lane == 0) flag_overflow(a, c);
+      return;
+   }
+   if (land_inserts<NL>(sm, iv, nI, wbase, pd0) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
+   uint32_t itot_f = len > 1 ? fetch_inserts<NL>(a, pd1, iv) : 0u;   // port 1's inserts, landed in step 0
+
+   uint64_t rk[ROWS];
+   uint32_t ra[ROWS];
+   uint32_t nK = 0;              // this port's kept records
+   uint32_t P0cur = 0, nin_prev = 0;   // the previous port's chain outputs before this window / kept of this window
+   uint32_t ob1p = 0, oc1p = 0;  // the previous port's chain output slot (spill-ins)
+   uint32_t nmax = 0, imax = 0;  // the fullest stream / insert list of this task (window sizing)
+
+   for (uint32_t i = 0; i < len; i++)
+   {
+      const bool has_next = i + 1 < len;
+      uint64_t* const stw = a.st + st_off + ((uint64_t) i * nW + w) * SW;          // this window's state
+      CH_STAMP(0);
+      // prefetch for the look-back: lanes [0, SW) the state of (w-1, i), [SW, 2 SW) of (w-2, i),
+      // lane LB_POST the POST granule of (w-1, i-1) (the kept count that gives this port's spill range)
+      uint64_t pv = 0;
+      if (lane < 2u * SW && w > lane / SW) pv = ld1(stw - (lane / SW + 1) * SW + lane % SW);
+      else if (lane == LB_POST && w && i) pv = ld1(stw - (uint64_t) nW * SW - SW + G_POST);
+      const uint32_t nx = rdl(pd0, PD_NX), ny = rdl(pd0, PD_NY);
+
+      // ---- [B] the merged stream in rows; per-row max-plus scans, route-field totals
+      uint32_t n = nK + nI, IB = CAP;
+      const uint32_t itot = itot_f;
+      uint32_t fpack = 0, tc_t = 0, totA = 0, totB = 0;
+      bool first = true;
+      // spill-ins: records port i-1 spilled in earlier windows (departures after their
+      // window's end) that arrive here in this window.  Pending range [Kpp, Pep): Pep = port
+      // i-1's chain outputs before this window (this task's own look-back there), Kpp = the
+      // prefix consumed after window w-1 (KO of (w-1, i), or from (w-1, i-1)'s POST when it
+      // kept any records: kept records follow every earlier record in FIFO order)
+      const uint32_t Pep = P0cur;
+      uint32_t Kpp = Pep, skip = 0, take = 0;
+      for (;;)
+      {
+         load_rows<ROWS>(sm, nK, IB, nI, rk, ra);
+         if (first) CH_STAMP(1);
+         fpack = tc_t = totA = totB = 0;
+#pragma unroll
+         for (int r = 0; r < ROWS; r++)
+         {
+            if ((uint32_t) r * T >= n) break;
+            const bool valid = (uint32_t) r * T + lane < n;
+            const uint32_t p = aux_F(ra[r]);
+            const uint32_t tcv = cyc((uint32_t) (rk[r] >> 32)) + p;   // (every lane: no exec branch)
+            uint32_t A = valid ? p : 0u;
+            uint32_t B = valid ? tcv : 0u;
+            wave_scan(A, B);
+            const uint32_t rA = rdl(A, 63), rB = rdl(B, 63);
+            const uint32_t nb = totB + rA;
+            totB = nb > rB ? nb : rB;
+            totA += rA;
+            const uint32_t f = route_field<XC>(nx, ny, ra[r]);
+            fpack |= (valid ? f : 0u) << (2 * r);
+            tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
+         }
+         if (!first) break;
+         first = false;
+         CH_STAMP(2);
+         // the stream is in registers: the insert region takes the next port's inserts
+         if (has_next)
+         {
+            if (itot > (uint32_t) ICAP)
+            {
+               if (lane == 0) flag_overflow(a, c);
+               return;
+            }
+            // the prefetched inserts are consumed only here: tie them to the scan's result so
+            // the compiler cannot hoist their use (and the wait for their loads, which also
+            // waits for the previous step's stores) to the top of the step
+#pragma unroll
+            for (int q = 0; q < IROWS; q++) asm volatile("" : "+v"(iv[q].t), "+v"(iv[q].id), "+v"(iv[q].aux) : "s"(totB));
+            if (land_inserts<NL>(sm, iv, itot, wbase, pd1) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
+         }
+         // ---- [D1] the predecessor window's state: its KO (or POST) for the spill range,
+         // and, with the serial protocol, its INC; one poll reloads every prefetched lane
+         if (w)
+         {
+            const bool need_k = i && Pep;
+            const uint64_t t0 = __builtin_amdgcn_s_memtime();
+            for (;;)
+            {
+               const uint64_t mt = __ballot((pv & ~M48) == a.etag);
+               bool ok = a.lookback || (mt & INC_MASK) == INC_MASK;
+               if (need_k)
+               {
+                  const uint64_t ko = rdl64(pv, G_KO), po = rdl64(pv, LB_POST);
+                  if ((ko & ~M48) == a.etag) Kpp = (uint32_t) (ko & M48);
+                  else if ((po & ~M48) == a.etag && (po >> 32 & 0xFFFFu))
+                     Kpp = (uint32_t) po + (uint32_t) (po >> 32 & 0xFFFFu);   // P0 + kept of (w-1, i-1)
+                  else ok = false;
+               }
+               if (ok) break;
+               if (__builtin_amdgcn_s_memtime() - t0 > SPIN_CYCLES)
+               {
+                  if (lane == 0) flag(a, F_TIMEOUT);
+                  return;
+               }
+               if (flagged(a)) return;
+               __builtin_amdgcn_s_sleep(1);
+               if (lane < 2u * SW && w > lane / SW) pv = ld1(stw - (lane / SW + 1) * SW + lane % SW);
+               else if (lane == LB_POST && i) pv = ld1(stw - (uint64_t) nW * SW - SW + G_POST);
+            }
+         }
+         if (Kpp >= Pep) break;
+         // ---- slow path: the pending spills were written by the windows back to the one
+         // whose outputs start at or before Kpp: wait for each one's POST (published once its
+         // stores drained); those in this window join the stream as inserts behind the merged
+         // stream, and the rows are rebuilt
+         const uint32_t spn = Pep - Kpp;
+         if (!((uint64_t) Kpp + spn <= oc1p))
+         {
+            if (lane == 0) flag(a, F_FALLBACK | R_SPILLIN);
+            return;
+         }
+         if (a.lookback)   // (the serial protocol's INC of w-1 implies every earlier window's drain)
+         {
+            const uint64_t t0 = __builtin_amdgcn_s_memtime();
+            for (uint32_t q = w; q-- > 0;)
+            {
+               uint64_t po = 0;
+               for (;;)
+               {
+                  if (lane == 0) po = ld1(a.st + st_off + ((uint64_t) (i - 1) * nW + q) * SW + G_POST);
+                  po = rdl64(po, 0);
+                  if ((po & ~M48) == a.etag) break;
+                  if (__builtin_amdgcn_s_memtime() - t0 > SPIN_CYCLES)
+                  {
+                     if (lane == 0) flag(a, F_TIMEOUT);
+                     return;
+                  }
+                  if (flagged(a)) return;
+                  __builtin_amdgcn_s_sleep(1);
+               }
+               if ((uint32_t) po <= Kpp) break;
+            }
+         }
+#pragma unroll
+         for (int r = 0; r < ROWS; r++)
+         {
+            const uint32_t p = (uint32_t) r * T + lane;
+            if ((uint32_t) r * T >= n) break;
+            if (p < n)
+            {
+               sm.key[p] = rk[r];
+               sm.aux[p] = ra[r];
+            }
+         }
+         for (uint32_t g0 = 0; g0 < spn; g0 += T)
+         {
+            const uint32_t g = g0 + lane;
+            uint64_t t = 0, ia = 0;
+            if (g < spn)
+            {
+               const uint64_t* r = reinterpret_cast<const uint64_t*>(a.recs + (uint64_t) ob1p + Kpp + g);
+               t = ld1(r);
+               ia = ld1(r + 1);
+            }
+            const bool early = g < spn && t < wbase;
+            const bool in = g < spn && t >= wbase && t - wbase < wlen;
+            const uint64_t mt = __ballot(in);
+            const uint32_t dst = n + take + mbcnt(mt);
+            if (in && dst < (uint32_t) CAP)
+            {
+               sm.key[dst] = ((t - wbase) << 32) | (uint32_t) ia;
+               sm.aux[dst] = (uint32_t) (ia >> 32);
+            }
+            skip += (uint32_t) __popcll(__ballot(early));
+            take += (uint32_t) __popcll(mt);
+            if (__ballot(g < spn && !early && !in)) break;   // the rest arrive after this window
+         }
+         // the spill-in loads have all landed (a wait the compiler sees: no load stays
+         // pending into the output rows, where a vmcnt(0) would also wait for the stores)
+         __builtin_amdgcn_s_waitcnt(0x0F70);
+         wsync();
+         if (!take) break;                          // nothing merged: the scan stands
+         if (n + take > (uint32_t) CAP)
+         {
+            if (lane == 0) flag_overflow(a, c);
+            return;
+         }
+         nK = n;
+         IB = n;
+         nI = take;
+         n += take;          // rescan (the stream changed)
+      }
+      // this port's consumed spill prefix after this window (KO) and its own aggregate
+      // (AGG: B in absolute cycles, A, the window's route counts): what the successors'
+      // look-back composes without waiting for this task's predecessor
+      const uint32_t Kout = nin_prev ? P0cur + nin_prev : Kpp + skip + take;
+      if (lane - (uint32_t) G_AB < 4u && (a.lookback || lane == G_KO))
+      {
+         uint64_t v = wb + totB;
+         if (lane == G_AA) v = totA;
+         if (lane == G_AC)
+            v = (uint64_t) rdl(tc_t, 1) | (uint64_t) rdl(tc_t, 2) << 12 | (uint64_t) rdl(tc_t, 3) << 24 |
+                (uint64_t) rdl(tc_t, 4) << 36;
+         if (lane == G_KO) v = Kout;
+         st1(stw + lane, a.etag | v);
+      }
+      CH_STAMP(3);
+
+      // ---- [D] look-back over the earlier windows of this port: the nearest INC (inclusive
+      // state), composed with the AGGs of the windows after it.  While the history tree may
+      // still have had no gap (an INC with the flag set, or window -1 with the analytical
+      // model on) the exact state of window w-1 is needed: wait for its INC.
+      uint64_t X_in = 0;
+      uint32_t cin_t = 0, mode = mode0;
+      if (w)
+      {
+         // lanes [0, SW) hold window w - d, [SW, 2 SW) window w - d - 1; (cA, cB, ccnt_t) is the
+         // composition of windows w - d + 1 .. w - 1 (AGG form: X -> max(X + cA, cB))
+         bool serial = !a.lookback;
+         uint32_t d = 1;
+         uint32_t cA = 0, ccnt_t = 0;
+         uint64_t cB = 0;
+         // prepend window AGG block b (0 or SW) to the composition
+         auto prepend = [&](uint32_t b) {
+            const uint64_t Bq = rdl64(pv, b + G_AB) & M48;
+            const uint32_t Aq = (uint32_t) rdl64(pv, b + G_AA);
+            const uint64_t Cq = rdl64(pv, b + G_AC) & M48;
+            cB = Bq + cA > cB ? Bq + cA : cB;
+            cA += Aq;
+            ccnt_t += lane - 1u < 4u ? (uint32_t) ((Cq >> (12 * (lane - 1u))) & 0xFFFu) : 0u;
+         };
+         const uint64_t t0 = __builtin_amdgcn_s_memtime();
+         for (;;)
+         {
+            const uint64_t mt = __ballot((pv & ~M48) == a.etag);
+            const bool inc1 = (mt & INC_MASK) == INC_MASK, agg1 = (mt & AGG_MASK) == AGG_MASK;
+            const bool has2 = w >= d + 1;   // window w - d - 1 exists
+            const bool inc2 = has2 && ((mt >> SW) & INC_MASK) == INC_MASK;
+            const bool agg2 = has2 && ((mt >> SW) & AGG_MASK) == AGG_MASK;
+            // the look-back ends at an INC (block src) or at window -1 (src = 2: tail 0, no
+            // records, "no gap yet" iff analytical); an exact "no gap yet" state is needed
+            // unless the INC found is window w-1's own
+            uint32_t src = NONE;
+            bool more = false;          // composed further without reaching an end: reload now
+            if (inc1 && (d == 1 || !(rdl64(pv, G_MODE) & 1u))) src = 0;
+            else if (inc1 || (serial && d == 1)) serial = true;   // exact: window w-1's INC only
+            else if (!serial && agg1)
+            {
+               prepend(0);
+               if (w == d) src = 2;                       // window w-d was window 0
+               else if (inc2 && !(rdl64(pv, SW + G_MODE) & 1u)) src = SW;
+               else if (inc2) serial = true;
+               else if (agg2)
+               {
+                  prepend(SW);
+                  if (w == d + 1) src = 2;                // window w-d-1 was window 0
+                  else more = true;
+                  d += 2;
+               }
+               else d += 1;   // window w-d-1 not there yet: it moves to lanes [0, SW)
+            }
+            if (src == 2 && mode0) serial = true;         // the first window may still have no gap
+            if (serial && src != 0) src = NONE;
+            if (src != NONE)
+            {
+               uint64_t Xp = 0;
+               uint32_t cp_t = 0, mp = 0;
+               if (src != 2)
+               {
+                  Xp = rdl64(pv, src + G_X) & M48;
+                  const uint64_t cw_ = sh64(pv, src + lane);   // lanes 1..4: the cumulative counts
+                  cp_t = lane - 1u < 4u ? (uint32_t) (cw_ & M48) : 0u;
+                  mp = (uint32_t) (rdl64(pv, src + G_MODE) & 1u);
+               }
+               const uint64_t xa = Xp + cA;
+               X_in = xa > cB ? xa : cB;
+               cin_t = cp_t + ccnt_t;
+               mode = d == 1 && src == 0 ? mp : 0u;
+               break;
+            }
+            if (serial)
+            {
+               // exact: wait for window w-1's INC, nothing composed
+               d = 1;
+               cA = 0;
+               cB = 0;
+               ccnt_t = 0;
+               more = false;
+            }
+            if (!more)
+            {
+               if (__builtin_amdgcn_s_memtime() - t0 > SPIN_CYCLES)
+               {
+                  if (lane == 0) flag(a, F_TIMEOUT);
+                  return;
+               }
+               if (flagged(a)) return;
+               __builtin_amdgcn_s_sleep(1);
+            }
+            pv = 0;
+            if (lane < 2u * SW && w >= d + lane / SW) pv = ld1(stw - (lane / SW + d) * SW + lane % SW);
+         }
+      }
+      CH_STAMP(4);
+      // window-relative tail: an earlier tail behaves like the base cycle (every tc > wb)
+      const uint64_t xr = X_in > wb ? X_in - wb : 0;
+      if (xr >= (1ull << 31))
+      {
+         if (lane == 0) flag(a, F_FALLBACK | R_TAIL);
+         return;
+      }
+      const uint32_t Xr = (uint32_t) xr;
+      // INC: publish before the outputs unless the history tree has had no gap yet (then
+      // the outputs decide)
+      if (!mode && lane < (uint32_t) G_AB)
+      {
+         const uint32_t x0 = Xr + totA;
+         st1(stw + lane, a.etag | inc_word(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u));
+      }
+      CH_STAMP(5);
+
+      // ---- [E] recurrence and outputs, row by row: kept records in place into the kept list
+      const uint32_t rl = rdl(pd0, PD_RL);
+      // field tables (lane 1 + q): output slot base, capacity, records routed so far
+      const uint32_t obf_t = bperm(pd0, lane - 1u), ocf_t = bperm(pd0, lane + 3u);
+      uint32_t run_t = cin_t;
+      const uint32_t P0n = rdl(cin_t, 2);   // chain-direction records before this window
+      const gptr<uint64_t> samp_t = sptr(a.samp_t);
+      const gptr<uint32_t> samp_id = sptr(a.samp_id);
+      uint64_t ssum = 0;
+      uint32_t Xc = Xr, nkeep = 0, fgap = NONE, ffire = NONE;
+      uint64_t rte = 0, spm = 0;   // lanes (over all rows) that overflowed an output slot / spilled
+#pragma unroll
+      for (int r = 0; r < ROWS; r++)
+      {
+         if ((uint32_t) r * T >= n) break;
+         const uint32_t p0 = (uint32_t) r * T;
+         const bool valid = p0 + lane < n;
+         const uint32_t off = (uint32_t) (rk[r] >> 32);
+         const uint32_t id = (uint32_t) rk[r];
+         const uint32_t ax = ra[r];
+         const uint32_t tc = cyc(off);
+         const uint32_t p = aux_F(ax);
+         // the row's exclusive prefix (rescanned: registers for 11 rows of prefixes cost
+         // more than the scan)
+         uint32_t A = valid ? p : 0u, B = valid ? tc + p : 0u;
+         wave_scan(A, B);
+         const uint32_t exA = dpp32<0x138, 0xF, 0xF>(A), exB = dpp32<0x138, 0xF, 0xF>(B);   // wave_shr 1
+         const uint32_t xa = Xc + exA;
+         const uint32_t Xb = xa > exB ? xa : exB;
+         const uint32_t Xm = Xb > tc ? Xb : tc;
+         const uint32_t cc = valid ? Xm - tc : 0u;
+         const uint32_t Xa = Xm + p;
+         if (mode)
+         {
+            // history tree with no gap yet: an idle period makes one (:79-86); the M/G/1
+            // branch fires while there is none and the tail lies beyond t + p (:58-64)
+            const uint64_t gm = __ballot(valid && tc > Xb), fm = __ballot(valid && Xb > tc + p);
+            if (fgap == NONE && gm) fgap = p0 + (uint32_t) __builtin_ctzll(gm);
+            if (ffire == NONE && fm) ffire = p0 + (uint32_t) __builtin_ctzll(fm);
+         }
+         Xc = rdl(Xa, (int) min(63u, n - 1 - p0));
+         ssum += cc;
+         const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
+         // route ranks: a packed (8 bits per field) prefix count over the row
+         const uint32_t f = (fpack >> (2 * r)) & 3u;
+         const uint32_t one = valid ? 1u << (8 * f) : 0u;
+         const uint32_t inc = wave_sum32(one);
+         const uint32_t rank = ((inc - one) >> (8 * f)) & 0xFFu;
+         const uint32_t rtot = rdl(inc, 63);
+         const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
+         const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
+         const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
+         run_t += field_cnt(rtot, lane);
+         // continuing: kept (a prefix of the window's continuing records) or spilled
+         const bool keep = valid && f == 1 && dn < wlen;
+         const bool out = valid && !keep;
+         const bool st = out && rank < room;
+         nkeep += (uint32_t) __popcll(__ballot(keep));
+         rte |= __ballot(out && rank >= room);
+         spm |= __ballot(st && f == 1);
+         if (keep)
+         {
+            sm.key[kb + rank] = (dn << 32) | id;
+            sm.aux[kb + rank] = ax;
+         }
+         if (st)
+         {
+            // a turn is read by the next launch, a spill by a later window's task in this one
+            // (after that window saw the producer's POST, written once these are drained):
+            // write-through 8-B stores either way (MI355X_MICROARCH.md "Valid forms")
+            const uint64_t gp = (uint64_t) gb + rank;
+            const uint64_t tn = wbase + dn;
+            const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
+            __hip_atomic_store(q, tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(q + 1, (uint64_t) id | ((uint64_t) ax << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((gp & 63) == 0)
+            {
+               samp_t[gp >> 6] = tn;
+               samp_id[gp >> 6] = id;
+            }
+         }
+      }
+      CH_STAMP(6);
+      const bool spilled = spm != 0;
+      if (rte && lane == 0) flag(a, F_ROUTE);
+      if (spilled && lastw && lane == 0) flag(a, F_FALLBACK | R_LASTSPILL);   // the last window keeps everything
+      const uint64_t ssw = rdl64(wave_sum64(ssum), 63);
+      if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drained before the next publish
+      wsync();
+
+      // ---- [F] late INC (no gap yet), POST, port counters, route check
+      const uint32_t x0 = Xr + totA;
+      const uint64_t Xo = wb + (x0 > totB ? x0 : totB);
+      if (mode)
+      {
+         // the M/G/1 branch would serve a request that arrives before the first gap
+         if (lane == 0 && ffire != NONE && (fgap == NONE || ffire < fgap)) flag(a, F_FALLBACK | R_MG1);
+         if (lane < (uint32_t) G_AB) st1(stw + lane, a.etag | inc_word(lane, Xo, run_t, fgap == NONE ? 1u : 0u));
+      }
+      // POST: the chain outputs before this window and whether it kept any (the next
+      // window's spill range at the next port, without waiting for its KO)
+      if (lane == G_POST) st1(stw + G_POST, a.etag | (uint64_t) P0n | (uint64_t) nkeep << 32);
+      // every record of the port has passed at the last window: the route counts fill
+      // every output slot
+      if (lastw && __any(lane - 1u < 4u && run_t != ocf_t) && lane == 0) flag(a, F_ROUTE);
+      if (lane == 0 && n)
+      {
+         const uint32_t port = rdl(pd0, PD_PORT);
+         atomicAdd(&a.port_sum[port], (unsigned long long) ssw);
+         atomicAdd(&a.port_cnt[port], (unsigned long long) n);
+         atomicAdd(&a.port_flit[port], (unsigned long long) totA);
+         atomicMax(&a.port_last[port], (unsigned long long) Xo);
+      }
+      nmax = n > nmax ? n : nmax;
+      imax = itot > imax ? itot : imax;   // the next port's inserts (checked against ICAP at landing)
+      // the next port's chain input: records before this window, kept of this window
+      P0cur = P0n;
+      nin_prev = nkeep;
+      ob1p = rdl(pd0, PD_OBASE + 1);
+      oc1p = rdl(pd0, PD_OCAP + 1);
+      CH_STAMP(7);
+#ifdef CH_STAMPS
+      if (a.stamps && lane == 0)
+         a.stamps[((uint64_t) tk * len + i) * 16 + 8] = (uint64_t) n | ((uint64_t) itot << 16) |
+                                                     ((uint64_t) nkeep << 32) | ((uint64_t) (take != 0) << 63);
+#endif
+      if (!has_next) break;
+      if (nkeep + itot > (uint32_t) CAP)
+      {
+         if (lane == 0) flag_overflow(a, c);
+         return;
+      }
+      nK = nkeep;
+      nI = itot;
+      // ---- next prefetches: port i+2's inserts (its descriptor landed a step ago), port
+      // i+3's descriptor and bounds; the ring moves on
+      if (i + 2 < len) itot_f = fetch_inserts<NL>(a, pd2, iv);
+      const uint32_t pdn = i + 3 < len ? load_pd<NL>(a, cpb + i + 3, bt_off, nW, i + 3, w) : 0u;
+      pd0 = pd1;
+      pd1 = pd2;
+      pd2 = pdn;
+   }
+   if (lane == 0)
+   {
+      atomicMax(a.nmax + 2 * c, nmax);
+      atomicMax(a.nmax + 2 * c + 1, imax);
+   }
+}
+
+template <int NL, bool F1, bool LB>
 __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
 {
    __shared__ Smem sm;
@@ -935,7 +1446,8 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
       tk = rdl(tk, 0);
       if (tk >= ntasks || flagged(a)) return;
       const uint32_t cw = a.tasks[tk];
-      task<NL, F1>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
+      if (LB) task_lb<NL, F1>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
+      else task_ser<NL, F1>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
       wsync();
    }
 }

@@ -211,6 +211,13 @@ struct gnoc_engine
    uint32_t ncpx = 0, ncpy = 0;
    DevBuf ch_cp, ch_bt, ch_st, ch_ctr, ch_stamps0, ch_stamps1;
    uint32_t n_retry = 0, n_fallback = 0;    // reruns of the last gnoc_run (chain -> smaller windows / levels, v3 -> v1)
+   // per phase, the hand-off protocol of k_chain (0: each window waits for window w-1's
+   // inclusive state; 1: look-back over earlier windows' aggregates): both are exact, and
+   // each is timed once on the settled windows, then the faster one runs
+   uint32_t ch_lb_run[2] = { 0, 0 };
+   float ch_lb_ms[2][2] = { { -1.f, -1.f }, { -1.f, -1.f } };
+   std::vector<uint64_t> ch_lb_D[2];        // the windows those times belong to
+   hipEvent_t ch_ev[2][2] = { { nullptr, nullptr }, { nullptr, nullptr } };
 
    // kernel profiling (gnoc_set_profiling)
    bool prof = false;
@@ -458,8 +465,8 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
       e->level_grid = std::max(1, per_cu) * std::max(1, cus);
       // the chain kernels' residency (a grid beyond it only queues: tasks are handed out in order)
       int c1 = 0, c3 = 0;
-      if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c1, ch::k_chain<1, true>, ch::T, 0);
-      if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c3, ch::k_chain<3, true>, ch::T, 0);
+      if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c1, ch::k_chain<1, true, false>, ch::T, 0);
+      if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c3, ch::k_chain<3, true, true>, ch::T, 0);
       e->ch_grid = std::max(1, std::min(c1, c3)) * std::max(1, cus);
    }
    if (he != hipSuccess)
@@ -593,7 +600,8 @@ void gnoc_destroy(gnoc_engine* e)
          (void) hipStreamSynchronize(q);
          (void) hipStreamDestroy(q);
       }
-   for (hipEvent_t ev : { e->ev_h2d, e->ev_done, e->ev_fin, e->ev_alt })
+   for (hipEvent_t ev : { e->ev_h2d, e->ev_done, e->ev_fin, e->ev_alt, e->ch_ev[0][0], e->ch_ev[0][1], e->ch_ev[1][0],
+                          e->ch_ev[1][1] })
       if (ev) (void) hipEventDestroy(ev);
    if (e->stream) (void) hipStreamDestroy(e->stream);
    delete e;
@@ -1455,6 +1463,22 @@ static int chain_setup(gnoc_engine* e)
       if (e->ch_epoch == 0) e->ch_epoch = 1;
    }
    GNOC_HIP(e, hipMemsetAsync(e->ch_ctr.p, 0, 256, s));
+   // the hand-off protocol per phase: GNOC_CHAIN_LOOKBACK=0/1 forces one; otherwise each is
+   // timed once on the current windows and the faster one is kept
+   const char* lbv = std::getenv("GNOC_CHAIN_LOOKBACK");
+   for (int p = 0; p < 2; p++)
+   {
+      if (!e->ch_ev[p][0]) GNOC_HIP(e, hipEventCreate(&e->ch_ev[p][0]));
+      if (!e->ch_ev[p][1]) GNOC_HIP(e, hipEventCreate(&e->ch_ev[p][1]));
+      if (e->ch_lb_D[p] != e->chD_run[p])
+      {
+         e->ch_lb_D[p] = e->chD_run[p];
+         e->ch_lb_ms[p][0] = e->ch_lb_ms[p][1] = -1.f;
+      }
+      const float* m = e->ch_lb_ms[p];
+      e->ch_lb_run[p] = lbv && *lbv ? (uint32_t) (std::atoi(lbv) != 0)
+                                    : m[0] < 0 ? 0u : m[1] < 0 ? 1u : (m[1] < m[0] ? 1u : 0u);
+   }
    if (ncp)
       GNOC_LAUNCH(e, KC_PLAN, ch::k_chain_plan, dim3((ncp + 255) / 256), dim3(256), 0, s, c, e->ncpx, e->ncpy, e->ry0,
                   e->cx0, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->ch_cp.as<ChainPort>());
@@ -1499,8 +1523,7 @@ static int chain_phase(gnoc_engine* e, int phase)
    a.pad0 = 0;
    a.etag = (uint64_t) e->ch_epoch << 48;
    a.stamps = nullptr;
-   const char* xv = std::getenv("GNOC_CHAIN_EXPERIMENT");
-   a.exp = xv ? (uint32_t) std::atoi(xv) : 0u;
+   a.lookback = e->ch_lb_run[phase];
    a.pad1 = 0;
    const char* stv = std::getenv("GNOC_STAMPS");
    if (stv && *stv == '1')
@@ -1512,11 +1535,20 @@ static int chain_phase(gnoc_engine* e, int phase)
       a.stamps = sb.as<uint64_t>();
    }
    const uint32_t grid = (uint32_t) std::min<uint64_t>((uint64_t) e->ch_grid, (uint64_t) a.ntasks);
+   GNOC_HIP(e, hipEventRecord(e->ch_ev[phase][0], s));
    // f != 1 GHz: the copy with the reference's double ps <-> cycle conversions
-   if (phase && e->f1) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<3, true>), dim3(grid), dim3(ch::T), 0, s, a);
-   else if (phase) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<3, false>), dim3(grid), dim3(ch::T), 0, s, a);
-   else if (e->f1) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<1, true>), dim3(grid), dim3(ch::T), 0, s, a);
-   else GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<1, false>), dim3(grid), dim3(ch::T), 0, s, a);
+#define GNOC_CHAIN(NLV, F1V)                                                                                  \
+   do                                                                                                          \
+   {                                                                                                           \
+      if (a.lookback) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<NLV, F1V, true>), dim3(grid), dim3(ch::T), 0, s, a); \
+      else GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<NLV, F1V, false>), dim3(grid), dim3(ch::T), 0, s, a);         \
+   } while (0)
+   if (phase && e->f1) GNOC_CHAIN(3, true);
+   else if (phase) GNOC_CHAIN(3, false);
+   else if (e->f1) GNOC_CHAIN(1, true);
+   else GNOC_CHAIN(1, false);
+#undef GNOC_CHAIN
+   GNOC_HIP(e, hipEventRecord(e->ch_ev[phase][1], s));
    return GNOC_OK;
 }
 
@@ -1783,6 +1815,19 @@ static int run_post(gnoc_engine* e, bool closed_form)
    if (e->h_pinned[3] > e->rec_bound) return fail(e, GNOC_EHIP, "internal: slot layout exceeds the record bound");
    const unsigned* ef = (const unsigned*) (e->h_pinned + 8);
    const unsigned errf = ef[0];
+   if (e->used_chain && !(ef[4] & ch::F_ANY))
+   {
+      // this run's time of each phase's protocol (chain_setup keeps the faster one)
+      for (int p = 0; p < 2; p++)
+      {
+         float ms = 0;
+         if ((p ? e->ncpy : e->ncpx) && hipEventElapsedTime(&ms, e->ch_ev[p][0], e->ch_ev[p][1]) == hipSuccess)
+            e->ch_lb_ms[p][e->ch_lb_run[p]] = ms;
+      }
+      if (std::getenv("GNOC_CHAIN_DEBUG"))
+         std::fprintf(stderr, "gnoc: chain protocol X %u (%.3f / %.3f ms)  Y %u (%.3f / %.3f ms)\n", e->ch_lb_run[0],
+                      e->ch_lb_ms[0][0], e->ch_lb_ms[0][1], e->ch_lb_run[1], e->ch_lb_ms[1][0], e->ch_lb_ms[1][1]);
+   }
    if (e->used_chain && (ef[4] & ch::F_ANY))
    {
       if (std::getenv("GNOC_CHAIN_DEBUG")) std::fprintf(stderr, "gnoc: chain engine declined, flags 0x%x\n", ef[4]);
