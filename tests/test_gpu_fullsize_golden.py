@@ -42,18 +42,23 @@ def _trace(name):
     return tr
 
 
+@pytest.mark.parametrize("lookback", ["0", "1"])
 @pytest.mark.parametrize("name", ["32x32_uniform_l0.005_ppt10000", "32x32_hotspot_l0.005_ppt10000"])
-def test_configs1_full_size_matches_oracle(name):
+def test_configs1_full_size_matches_oracle(name, lookback, monkeypatch):
+    """Both chain hand-off protocols (GNOC_CHAIN_LOOKBACK: 0 serial, 1 look-back), over
+    several runs so the adapted windows (and their spill patterns) are covered too."""
+    monkeypatch.setenv("GNOC_CHAIN_LOOKBACK", lookback)
     tr = _trace(name)
     cfg = gnoc.EngineConfig(num_tiles=1024)
     eng = gnoc.Engine(cfg)
     eng.submit(tr)
-    eng.run()
-    s = eng.summary()
-    res = eng.results()
+    for k in range(3):
+        eng.run()
+        s = eng.summary()
+        assert s["engine_path"] == 4 and s["fallbacks"] == 0
+        assert s["mesh_hops"] == GOLD[name]["mesh_hops"]
+        _check(name, eng.results())
     eng.close()
-    assert s["mesh_hops"] == GOLD[name]["mesh_hops"]
-    _check(name, res)
 
 
 def test_configs1_full_size_level_engine_matches_oracle(monkeypatch):
@@ -70,7 +75,9 @@ def test_configs1_full_size_level_engine_matches_oracle(monkeypatch):
     _check(name, res)
 
 
-def test_configs2_full_size_matches_oracle_single_and_8_ranks():
+@pytest.mark.parametrize("lookback", ["0", "1"])
+def test_configs2_full_size_matches_oracle_single_and_8_ranks(lookback, monkeypatch):
+    monkeypatch.setenv("GNOC_CHAIN_LOOKBACK", lookback)
     name = "64x64_uniform_l0.002_ppt10000"
     tr = _trace(name)
     cfg = gnoc.EngineConfig(num_tiles=4096)
