@@ -118,35 +118,54 @@ def main():
     # end to end (SURVEY.md 8(d) "trace resident in host memory -> results in host
     # memory"): submit from pinned host arrays (host-side trace validation + H2D),
     # run, final_ps back into a pinned host array; reported beside the HBM-resident value
-    e2e_ms = e2e_serial_ms = None
+    e2e_ms = e2e_serial_ms = e2e_wide_ms = None
+    wire = None
     if not sharded:
         ptr = pinned_trace(tr)
         fins = [torch.empty(len(tr), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64) for _ in range(2)]
         K = max(2, a.steps // 2)
+        # the narrow wire format (gnoc_packets_narrow: u16 tile ids / lengths, u8 flags,
+        # 15 B per packet) where the batch fits it, else the 24-B one
+        try:
+            ntr = gnoc.NarrowTrace.of(tr, alloc=lambda shape, dt: pinned_array(shape[0], dt))
+            sub, sub_async, wire = eng.submit_narrow, eng.submit_async_narrow, 15
+        except ValueError:
+            ntr, sub, sub_async, wire = ptr, eng.submit, eng.submit_async, 24
+
+        def pipelined(submit, submit_async, x):
+            # batch k+1's upload and batch k's read-back run on copy streams beside run k
+            barrier_sync()
+            t_e = time.perf_counter()
+            submit(x)
+            for k in range(K):
+                if k + 1 < K:
+                    submit_async(x)
+                eng.run()
+                eng.fetch_final_ps(fins[k % 2])
+                if k + 1 < K:
+                    eng.submit_commit()
+            eng.fetch_wait()
+            ms = (time.perf_counter() - t_e) / K * 1e3
+            want = eng.results().final_ps
+            assert all(np.array_equal(f, want) for f in fins), "pipelined read-back differs from the run's final_ps"
+            return ms
+        # untimed: the second trace buffers, copy streams and staging areas get allocated
+        for sa, x in ((sub_async, ntr), (eng.submit_async, ptr)):
+            sa(x)
+            eng.submit_commit()
+            eng.run()
+            eng.fetch_final_ps(fins[0])
+            eng.fetch_wait()
         # one batch at a time: submit (H2D + device checks), run, final_ps read-back
         barrier_sync()
         t_e = time.perf_counter()
         for _ in range(K):
-            eng.submit(ptr)
+            sub(ntr)
             eng.run()
             eng.final_ps_into(fins[0])
         e2e_serial_ms = (time.perf_counter() - t_e) / K * 1e3
-        # pipelined (gnoc_submit_async / gnoc_fetch_final_ps): batch k+1's upload and
-        # batch k's read-back run on copy streams beside the runs
-        barrier_sync()
-        t_e = time.perf_counter()
-        eng.submit(ptr)
-        for k in range(K):
-            if k + 1 < K:
-                eng.submit_async(ptr)
-            eng.run()
-            eng.fetch_final_ps(fins[k % 2])
-            if k + 1 < K:
-                eng.submit_commit()
-        eng.fetch_wait()
-        e2e_ms = (time.perf_counter() - t_e) / K * 1e3
-        want = eng.results().final_ps
-        assert all(np.array_equal(f, want) for f in fins), "pipelined read-back differs from the run's final_ps"
+        e2e_ms = pipelined(sub, sub_async, ntr)
+        e2e_wide_ms = pipelined(eng.submit, eng.submit_async, ptr) if wire == 15 else e2e_ms
 
     # this rank's share: mesh hops through the ports it owns, packets it delivers
     res = eng.results()
@@ -227,9 +246,12 @@ def main():
             "build_id": bid,
             "e2e_ms_per_step": e2e_ms,
             "e2e_serial_ms_per_step": e2e_serial_ms,
+            "e2e_24B_ms_per_step": e2e_wide_ms,
+            "e2e_wire_bytes_per_packet": wire,
             "e2e_note": "host trace (pinned) -> host final_ps per batch: submit (H2D + device-side trace checks) + run + "
                         "final_ps D2H; e2e_ms_per_step pipelined (batch k+1's upload and batch k's read-back on copy "
-                        "streams beside the runs), e2e_serial_ms_per_step one batch at a time",
+                        "streams beside the runs) in the narrow wire format, e2e_serial_ms_per_step one batch at a "
+                        "time (same format), e2e_24B_ms_per_step pipelined with the 24-B format",
             "roofline": {
                 "bound": "hbm",
                 "achieved": rf["achieved"],
@@ -446,6 +468,13 @@ def sweep_cpu_baseline(a, pts, ppt, npts=64, workers=None):
             "nproc": os.cpu_count(), "affinity_cpus": avail,
             "sample": f"{npts} of the {len(pts)} sweep points, pkts/tile={ppt}: {hops} mesh hops, "
                       f"{busy:.2f} s of oracle time per worker ({workers} single-threaded oracle processes)"}
+
+
+def pinned_array(n, dt):
+    """A page-locked numpy array (a view of a pinned torch tensor's bytes)."""
+    nbytes = int(n) * np.dtype(dt).itemsize
+    t = torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=True)
+    return t.numpy()[:nbytes].view(dt)
 
 
 def pinned_trace(tr):

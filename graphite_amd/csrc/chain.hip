@@ -493,6 +493,39 @@ __device__ __forceinline__ gptr<P> sptr(P* p)
    asm volatile("" : "+s"(p));
    return (gptr<P>) p;
 }
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+#ifndef CH_TURN16
+#define CH_TURN16 0   // 1: turns as one plain 16-B store (measured: see DESIGN.md 7)
+#endif
+// A record that leaves the chain at slot position gp.  A turn is read by the next
+// launch: one plain 16-B store.  A spill is read in this launch by a later window's
+// task once the producer published a state after draining its stores: write-through
+// 8-B stores (MI355X_MICROARCH.md "Valid forms").  Every 64th position also writes
+// the slot's key sample.
+__device__ __forceinline__ void out_record(gptr<Rec> recs, gptr<uint64_t> samp_t, gptr<uint32_t> samp_id, uint64_t gp,
+                                           uint64_t tn, uint32_t id, uint32_t ax, bool spill)
+{
+   if (!CH_TURN16 || spill)
+   {
+      const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
+      __hip_atomic_store(q, tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(q + 1, (uint64_t) id | ((uint64_t) ax << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+   }
+   else
+   {
+      v4u o;
+      o.x = (uint32_t) tn;
+      o.y = (uint32_t) (tn >> 32);
+      o.z = id;
+      o.w = ax;
+      *(gptr<v4u>) (recs + gp) = o;
+   }
+   if ((gp & 63) == 0)
+   {
+      samp_t[gp >> 6] = tn;
+      samp_id[gp >> 6] = id;
+   }
+}
 
 
 
@@ -836,19 +869,7 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
             sm.key[kb + rank] = (dn << 32) | id;
             sm.aux[kb + rank] = ax;
          }
-         if (st)
-         {
-            const uint64_t gp = (uint64_t) gb + rank;
-            const uint64_t tn = wbase + dn;
-            const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
-            __hip_atomic_store(q, tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(q + 1, (uint64_t) id | ((uint64_t) ax << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((gp & 63) == 0)
-            {
-               samp_t[gp >> 6] = tn;
-               samp_id[gp >> 6] = id;
-            }
-         }
+         if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
       }
       CH_STAMP(6);
       const bool spilled = spm != 0;
@@ -1341,22 +1362,7 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
             sm.key[kb + rank] = (dn << 32) | id;
             sm.aux[kb + rank] = ax;
          }
-         if (st)
-         {
-            // a turn is read by the next launch, a spill by a later window's task in this one
-            // (after that window saw the producer's POST, written once these are drained):
-            // write-through 8-B stores either way (MI355X_MICROARCH.md "Valid forms")
-            const uint64_t gp = (uint64_t) gb + rank;
-            const uint64_t tn = wbase + dn;
-            const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
-            __hip_atomic_store(q, tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(q + 1, (uint64_t) id | ((uint64_t) ax << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((gp & 63) == 0)
-            {
-               samp_t[gp >> 6] = tn;
-               samp_id[gp >> 6] = id;
-            }
-         }
+         if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
       }
       CH_STAMP(6);
       const bool spilled = spm != 0;

@@ -125,6 +125,8 @@ struct gnoc_engine
    hipStream_t s_h2d = nullptr, s_d2h = nullptr;
    hipEvent_t ev_h2d = nullptr, ev_done = nullptr, ev_fin = nullptr, ev_alt = nullptr;
    DevBuf t2_inj, t2_src, t2_dst, t2_bits, t2_flags, final_alt;
+   DevBuf nw_stage, nw_stage2;               // narrow wire format (gnoc_packets_narrow) before widening
+   bool staged_narrow = false;
    bool staged = false, fetched = false;
    gnoc_packets staged_pk{};
    size_t staged_n = 0;
@@ -1016,6 +1018,72 @@ static int partition_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n, gno
 
 static int submit_tail(gnoc_engine* e, const gnoc_packets* pk, size_t n);
 
+// Narrow wire format -> the engine's u32 trace arrays (one pass, coalesced).
+__global__ __launch_bounds__(256) void k_widen(uint64_t n, const uint16_t* __restrict__ src, const uint16_t* __restrict__ dst,
+                                               const uint16_t* __restrict__ bits, const uint8_t* __restrict__ flags,
+                                               uint32_t* __restrict__ osrc, uint32_t* __restrict__ odst,
+                                               uint32_t* __restrict__ obits, uint32_t* __restrict__ oflags)
+{
+   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+   {
+      osrc[i] = src[i];
+      odst[i] = dst[i];
+      obits[i] = bits[i];
+      oflags[i] = flags ? flags[i] : 0u;
+   }
+}
+
+// Copy a narrow trace (host) into the stage buffer and widen it into (inj, src, dst,
+// bits, flags) on stream q.
+static int stage_narrow(gnoc_engine* e, const gnoc_packets_narrow* pk, size_t n, DevBuf& stage, DevBuf& inj, DevBuf& src,
+                        DevBuf& dst, DevBuf& bits, DevBuf& flags, hipStream_t q)
+{
+   if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return fail(e, GNOC_EINVAL, "null trace array");
+   if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
+   if (e->nranks > 1) return fail(e, GNOC_EUNSUPPORTED, "a sharded engine takes gnoc_submit");
+   if (e->dc.N > 65536) return fail(e, GNOC_EUNSUPPORTED, "the narrow wire format needs at most 65,536 tiles");
+   GNOC_HIP(e, inj.ensure(n * 8));
+   GNOC_HIP(e, src.ensure(n * 4));
+   GNOC_HIP(e, dst.ensure(n * 4));
+   GNOC_HIP(e, bits.ensure(n * 4));
+   GNOC_HIP(e, flags.ensure(n * 4));
+   GNOC_HIP(e, stage.ensure(n * 7 + 16));
+   if (!n) return GNOC_OK;
+   uint16_t* s16 = stage.as<uint16_t>();
+   uint8_t* f8 = reinterpret_cast<uint8_t*>(s16 + 3 * n);
+   GNOC_HIP(e, hipMemcpyAsync(inj.p, pk->inject_ps, n * 8, hipMemcpyHostToDevice, q));
+   GNOC_HIP(e, hipMemcpyAsync(s16, pk->src, n * 2, hipMemcpyHostToDevice, q));
+   GNOC_HIP(e, hipMemcpyAsync(s16 + n, pk->dst, n * 2, hipMemcpyHostToDevice, q));
+   GNOC_HIP(e, hipMemcpyAsync(s16 + 2 * n, pk->bits, n * 2, hipMemcpyHostToDevice, q));
+   if (pk->flags) GNOC_HIP(e, hipMemcpyAsync(f8, pk->flags, n, hipMemcpyHostToDevice, q));
+   const uint32_t grid = (uint32_t) std::min<size_t>((n + 255) / 256, 4096);
+   hipLaunchKernelGGL(k_widen, dim3(grid), dim3(256), 0, q, (uint64_t) n, (const uint16_t*) s16, (const uint16_t*) (s16 + n),
+                      (const uint16_t*) (s16 + 2 * n), pk->flags ? (const uint8_t*) f8 : nullptr, src.as<uint32_t>(),
+                      dst.as<uint32_t>(), bits.as<uint32_t>(), flags.as<uint32_t>());
+   GNOC_HIP(e, hipGetLastError());
+   return GNOC_OK;
+}
+
+int gnoc_submit_narrow(gnoc_engine* e, const gnoc_packets_narrow* pk, size_t n)
+{
+   if (!e || !pk) return GNOC_EINVAL;
+   e->submitted = false;
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   int rc = stage_narrow(e, pk, n, e->nw_stage, e->t_inj, e->t_src, e->t_dst, e->t_bits, e->t_flags, e->stream);
+   if (rc) return rc;
+   e->part = false;
+   e->n_glob = n;
+   e->dc.g2l = nullptr;
+   e->d_inj = e->t_inj.as<uint64_t>();
+   e->d_src = e->t_src.as<uint32_t>();
+   e->d_dst = e->t_dst.as<uint32_t>();
+   e->d_bits = e->t_bits.as<uint32_t>();
+   e->d_flags = e->t_flags.as<uint32_t>();
+   e->n = n;
+   e->dc.npk = n;
+   return submit_tail(e, nullptr, n);
+}
+
 int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk_in, size_t n)
 {
    if (!e || !pk_in) return GNOC_EINVAL;
@@ -1088,6 +1156,7 @@ static int submit_tail(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    if (record_bound(e, records) >= (1ull << 31)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^31 hop records");
    e->rec_bound = record_bound(e, records);
    e->h_bid.clear();
+   if (nbc && !pk) return fail(e, GNOC_EUNSUPPORTED, "broadcast packets need gnoc_submit");
    if (nbc)
       for (size_t i = 0; i < n; i++)
          if (pk->flags[i] & GNOC_PKT_BROADCAST) e->h_bid.push_back((uint32_t) i);
@@ -1141,7 +1210,24 @@ int gnoc_submit_async(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    }
    GNOC_HIP(e, hipEventRecord(e->ev_h2d, e->s_h2d));
    e->staged = true;
+   e->staged_narrow = false;
    e->staged_pk = *pk;
+   e->staged_n = n;
+   return GNOC_OK;
+}
+
+int gnoc_submit_async_narrow(gnoc_engine* e, const gnoc_packets_narrow* pk, size_t n)
+{
+   if (!e || !pk) return GNOC_EINVAL;
+   if (e->staged) return fail(e, GNOC_ESTATE, "a staged batch is waiting for gnoc_submit_commit");
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   GNOC_HIP(e, pipe_streams(e));
+   int rc = stage_narrow(e, pk, n, e->nw_stage2, e->t2_inj, e->t2_src, e->t2_dst, e->t2_bits, e->t2_flags, e->s_h2d);
+   if (rc) return rc;
+   GNOC_HIP(e, hipEventRecord(e->ev_h2d, e->s_h2d));
+   e->staged = true;
+   e->staged_narrow = true;
+   e->staged_pk = gnoc_packets{};
    e->staged_n = n;
    return GNOC_OK;
 }
@@ -1172,7 +1258,9 @@ int gnoc_submit_commit(gnoc_engine* e)
    e->n = n;
    e->dc.npk = n;
    gnoc_packets pk = e->staged_pk;
-   return submit_tail(e, &pk, n);
+   const bool narrow = e->staged_narrow;
+   e->staged_narrow = false;
+   return submit_tail(e, narrow ? nullptr : &pk, n);
 }
 
 int gnoc_fetch_final_ps(gnoc_engine* e, uint64_t* host_out, size_t n)

@@ -46,6 +46,7 @@ EXPORTED = (
     "gnoc_get_broadcast_results", "gnoc_get_broadcast_info", "gnoc_set_basic_moving_average",
     "gnoc_build_id", "gnoc_rccl_unique_id", "gnoc_rccl_comm_init", "gnoc_rccl_comm_destroy",
     "gnoc_submit_async", "gnoc_submit_commit", "gnoc_fetch_final_ps", "gnoc_fetch_wait",
+    "gnoc_submit_narrow", "gnoc_submit_async_narrow",
 )
 
 
@@ -78,6 +79,16 @@ class GnocPoint(ctypes.Structure):
 
 
 class GnocPackets(ctypes.Structure):
+    _fields_ = [
+        ("inject_ps", ctypes.c_void_p),
+        ("src", ctypes.c_void_p),
+        ("dst", ctypes.c_void_p),
+        ("bits", ctypes.c_void_p),
+        ("flags", ctypes.c_void_p),
+    ]
+
+
+class GnocPacketsNarrow(ctypes.Structure):
     _fields_ = [
         ("inject_ps", ctypes.c_void_p),
         ("src", ctypes.c_void_p),
@@ -182,6 +193,9 @@ def load() -> ctypes.CDLL:
     lib.gnoc_run_begin.argtypes = [vp, vp]
     lib.gnoc_run_finish.argtypes = [vp, vp]
     lib.gnoc_set_basic_moving_average.argtypes = [vp, ctypes.c_int32, ctypes.c_uint32]
+    if hasattr(lib, "gnoc_submit_narrow"):
+        lib.gnoc_submit_narrow.argtypes = [vp, ctypes.POINTER(GnocPacketsNarrow), sz]
+        lib.gnoc_submit_async_narrow.argtypes = [vp, ctypes.POINTER(GnocPacketsNarrow), sz]
     if hasattr(lib, "gnoc_submit_async"):
         lib.gnoc_submit_async.argtypes = [vp, ctypes.POINTER(GnocPackets), sz]
         lib.gnoc_submit_commit.argtypes = [vp]
@@ -263,6 +277,42 @@ class Trace:
         return Trace(np.ascontiguousarray(self.inject_ps, np.uint64), np.ascontiguousarray(self.src, np.uint32),
                      np.ascontiguousarray(self.dst, np.uint32), np.ascontiguousarray(self.bits, np.uint32),
                      np.ascontiguousarray(f, np.uint32))
+
+
+@dataclass
+class NarrowTrace:
+    """A trace in the narrow wire format (gnoc_packets_narrow): u16 tile ids and
+    modeled lengths, u8 flags -- 15 bytes per packet over PCIe instead of 24."""
+    inject_ps: np.ndarray
+    src: np.ndarray
+    dst: np.ndarray
+    bits: np.ndarray
+    flags: np.ndarray
+
+    def __len__(self) -> int:
+        return int(self.inject_ps.shape[0])
+
+    @staticmethod
+    def of(tr: "Trace", alloc=np.empty) -> "NarrowTrace":
+        """Narrow a trace (ValueError if a tile id, length or flag does not fit);
+        alloc(shape, dtype) places the arrays (e.g. in page-locked memory)."""
+        tr = tr.normalized()
+        n = len(tr)
+        for name, a, lim in (("src", tr.src, 1 << 16), ("dst", tr.dst, 1 << 16), ("bits", tr.bits, 1 << 16),
+                             ("flags", tr.flags, 1 << 8)):
+            if n and int(a.max()) >= lim:
+                raise ValueError(f"{name} does not fit the narrow wire format")
+        out = []
+        for a, dt in ((tr.inject_ps, np.uint64), (tr.src, np.uint16), (tr.dst, np.uint16), (tr.bits, np.uint16),
+                      (tr.flags, np.uint8)):
+            b = alloc((n,), dt)
+            b[:] = a
+            out.append(b)
+        return NarrowTrace(*out)
+
+    def packets(self) -> GnocPacketsNarrow:
+        return GnocPacketsNarrow(self.inject_ps.ctypes.data, self.src.ctypes.data, self.dst.ctypes.data,
+                                 self.bits.ctypes.data, self.flags.ctypes.data)
 
 
 # synthetic_network.cc NetworkTrafficType (:16-24), include/gnoc.h GNOC_TRAFFIC_*
@@ -428,6 +478,15 @@ class Engine:
                          tr.flags.ctypes.data)
         self._check(self.lib.gnoc_submit_async(self._h, ctypes.byref(pk), len(tr)))
         self._staged = (tr, len(tr))
+
+    def submit_narrow(self, nt: "NarrowTrace") -> None:
+        """gnoc_submit_narrow: the 15-byte-per-packet wire format (widened on the device)."""
+        self._check(self.lib.gnoc_submit_narrow(self._h, ctypes.byref(nt.packets()), len(nt)))
+        self._n = len(nt)
+
+    def submit_async_narrow(self, nt: "NarrowTrace") -> None:
+        self._check(self.lib.gnoc_submit_async_narrow(self._h, ctypes.byref(nt.packets()), len(nt)))
+        self._staged = (nt, len(nt))
 
     def submit_commit(self) -> None:
         self._check(self.lib.gnoc_submit_commit(self._h))

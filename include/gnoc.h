@@ -125,6 +125,20 @@ typedef struct gnoc_packets
    const uint32_t *flags;       /* GNOC_PKT_* (may be NULL = all zero)                  */
 } gnoc_packets;
 
+/* The same trace in a narrow wire format, 15 bytes per packet instead of 24: for
+ * meshes of at most 65,536 tiles and modeled lengths below 65,536 bits (checked).
+ * gnoc_submit_narrow / gnoc_submit_async_narrow copy these over PCIe and widen
+ * them on the device (SURVEY.md 8d end-to-end: the host link, not the engine,
+ * bounds a host-to-host batch). */
+typedef struct gnoc_packets_narrow
+{
+   const uint64_t *inject_ps;
+   const uint16_t *src;
+   const uint16_t *dst;
+   const uint16_t *bits;
+   const uint8_t *flags;        /* may be NULL = all zero */
+} gnoc_packets_narrow;
+
 typedef struct gnoc_engine gnoc_engine;
 
 typedef struct gnoc_summary
@@ -193,6 +207,7 @@ int gnoc_submit(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
 /* Same, but the arrays already live in device memory (HBM) on cfg->device;
  * they must stay valid until gnoc_run returns. */
 int gnoc_submit_device(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
+int gnoc_submit_narrow(gnoc_engine *eng, const gnoc_packets_narrow *pk, size_t n);
 
 /* Runs the whole batch (all hops of all packets) on the GPU.  Blocking. */
 int gnoc_run(gnoc_engine *eng);
@@ -356,6 +371,7 @@ int gnoc_rccl_comm_destroy(void *comm);
  * e.g. submit(0); loop k: submit_async(k+1); run(k); fetch_final_ps(k);
  * submit_commit(k+1).  Unsharded engines, unicast batches. */
 int gnoc_submit_async(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
+int gnoc_submit_async_narrow(gnoc_engine *eng, const gnoc_packets_narrow *pk, size_t n);
 int gnoc_submit_commit(gnoc_engine *eng);
 int gnoc_fetch_final_ps(gnoc_engine *eng, uint64_t *final_ps_out, size_t n);
 int gnoc_fetch_wait(gnoc_engine *eng);

@@ -71,3 +71,32 @@ def test_pipeline_state_errors():
     eng.fetch_wait()
     assert np.array_equal(out, eng.results().final_ps)
     eng.close()
+
+
+def test_narrow_wire_format_matches_wide():
+    """gnoc_submit_narrow / gnoc_submit_async_narrow (u16 ids and lengths, u8 flags,
+    widened on the device) give the same results as the 24-B format, self-sends and
+    unmodeled packets included; traces that do not fit are refused on the host."""
+    from tests.traces import random_trace
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = random_trace(5000, 8, 8, seed=17, max_cycle=3000, burst0=5, self_frac=0.05)
+    tr.flags[::37] |= gnoc.PKT_UNMODELED
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    want = eng.results()
+    nt = gnoc.NarrowTrace.of(tr)
+    eng.submit_narrow(nt)
+    eng.run()
+    got = eng.results()
+    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_flit"):
+        assert np.array_equal(getattr(got, k), getattr(want, k)), k
+    eng.submit_async_narrow(nt)
+    eng.submit_commit()
+    eng.run()
+    assert np.array_equal(eng.results().final_ps, want.final_ps)
+    eng.close()
+    big = gnoc.Trace(tr.inject_ps, tr.src, tr.dst, tr.bits.copy(), tr.flags)
+    big.bits[0] = 1 << 16
+    with pytest.raises(ValueError):
+        gnoc.NarrowTrace.of(big)
