@@ -159,7 +159,7 @@ struct ChainArgs
    const ChainWin* cw;            // [nch] windows per chain: window w = [w D, (w + 1) D), the last one unbounded
    const uint32_t* tasks;         // [ntasks] c << 16 | w, ordered by the window's start time w D
    uint32_t cp0;                  // unused (0)
-   uint32_t pad0;
+   uint32_t excfix;               // 1: k_exc_merge put the injection level's exception tails in order
    uint64_t etag;                 // epoch << 48
    unsigned* nmax;                // [2 c] the most stream records, [2 c + 1] the most inserts of chain c's steps
    uint64_t* stamps;              // debug (GNOC_STAMPS=1): [(task * len + i) * 16 + k] phase stamps, else null
@@ -280,6 +280,14 @@ __device__ __forceinline__ bool flagged(const ChainArgs& a)
 {
    return (__hip_atomic_load(a.errflag + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & F_ANY) != 0;
 }
+// The polls' abort check rides along in lane FL (no state word uses it): the flag load
+// is issued beside the state reloads, so a poll round costs one memory round trip.
+constexpr uint32_t FL = 63;
+__device__ __forceinline__ void ld_flag(const ChainArgs& a, uint32_t lane, uint32_t& ef)
+{
+   if (lane == FL) ef = __hip_atomic_load(a.errflag + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool aborted(uint32_t ef) { return (rdl(ef, (int) FL) & F_ANY) != 0; }
 
 // Port descriptor fields (lanes 0-31 of a "pd" register) and the port's insert
 // bounds of window w (lanes 32 + j: first record of list j, 32 + nl + j: end).
@@ -557,19 +565,20 @@ __device__ __forceinline__ void out_record(gptr<Rec> recs, gptr<uint64_t> samp_t
 __device__ bool poll_words(const ChainArgs& a, const uint64_t* s, uint32_t nw, uint32_t lane, uint64_t& v)
 {
    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+   uint32_t ef = 0;
    for (;;)
    {
       bool ok = true;
       if (lane < nw) ok = (v & ~M48) == a.etag;
       if (__all(ok)) return true;
+      if (aborted(ef)) return false;
       if (__builtin_amdgcn_s_memtime() - t0 > SPIN_CYCLES)
       {
          if (lane == 0) flag(a, F_TIMEOUT);
          return false;
       }
-      if (flagged(a)) return false;
-      __builtin_amdgcn_s_sleep(1);
       if (lane < nw) v = ld1(s + lane);
+      ld_flag(a, lane, ef);
    }
 }
 
@@ -910,6 +919,7 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
       CH_STAMP(7);
 #ifdef CH_STAMPS
       if (a.stamps && lane == 0)
+         a.stamps[((uint64_t) tk * len + i) * 16 + 9] = __builtin_amdgcn_s_memrealtime(),   // 100 MHz, one clock for all XCDs
          a.stamps[((uint64_t) tk * len + i) * 16 + 8] = (uint64_t) n | ((uint64_t) itot << 16) |
                                                      ((uint64_t) nkeep << 32) | ((uint64_t) (Pep != Kpp) << 63);
 #endif
@@ -1062,6 +1072,7 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
          {
             const bool need_k = i && Pep;
             const uint64_t t0 = __builtin_amdgcn_s_memtime();
+            uint32_t ef = 0;
             for (;;)
             {
                const uint64_t mt = __ballot((pv & ~M48) == a.etag);
@@ -1075,15 +1086,15 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
                   else ok = false;
                }
                if (ok) break;
+               if (aborted(ef)) return;
                if (__builtin_amdgcn_s_memtime() - t0 > SPIN_CYCLES)
                {
                   if (lane == 0) flag(a, F_TIMEOUT);
                   return;
                }
-               if (flagged(a)) return;
-               __builtin_amdgcn_s_sleep(1);
                if (lane < 2u * SW && w > lane / SW) pv = ld1(stw - (lane / SW + 1) * SW + lane % SW);
                else if (lane == LB_POST && i) pv = ld1(stw - (uint64_t) nW * SW - SW + G_POST);
+               ld_flag(a, lane, ef);
             }
          }
          if (Kpp >= Pep) break;
@@ -1100,21 +1111,22 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
          if (a.lookback)   // (the serial protocol's INC of w-1 implies every earlier window's drain)
          {
             const uint64_t t0 = __builtin_amdgcn_s_memtime();
+            uint32_t ef = 0;
             for (uint32_t q = w; q-- > 0;)
             {
                uint64_t po = 0;
                for (;;)
                {
                   if (lane == 0) po = ld1(a.st + st_off + ((uint64_t) (i - 1) * nW + q) * SW + G_POST);
+                  ld_flag(a, lane, ef);
                   po = rdl64(po, 0);
                   if ((po & ~M48) == a.etag) break;
+                  if (aborted(ef)) return;
                   if (__builtin_amdgcn_s_memtime() - t0 > SPIN_CYCLES)
                   {
                      if (lane == 0) flag(a, F_TIMEOUT);
                      return;
                   }
-                  if (flagged(a)) return;
-                  __builtin_amdgcn_s_sleep(1);
                }
                if ((uint32_t) po <= Kpp) break;
             }
@@ -1208,6 +1220,7 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
             ccnt_t += lane - 1u < 4u ? (uint32_t) ((Cq >> (12 * (lane - 1u))) & 0xFFFu) : 0u;
          };
          const uint64_t t0 = __builtin_amdgcn_s_memtime();
+         uint32_t ef = 0;
          for (;;)
          {
             const uint64_t mt = __ballot((pv & ~M48) == a.etag);
@@ -1267,16 +1280,16 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
             }
             if (!more)
             {
+               if (aborted(ef)) return;
                if (__builtin_amdgcn_s_memtime() - t0 > SPIN_CYCLES)
                {
                   if (lane == 0) flag(a, F_TIMEOUT);
                   return;
                }
-               if (flagged(a)) return;
-               __builtin_amdgcn_s_sleep(1);
             }
             pv = 0;
             if (lane < 2u * SW && w >= d + lane / SW) pv = ld1(stw - (lane / SW + d) * SW + lane % SW);
+            ld_flag(a, lane, ef);
          }
       }
       CH_STAMP(4);
@@ -1405,6 +1418,7 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
       CH_STAMP(7);
 #ifdef CH_STAMPS
       if (a.stamps && lane == 0)
+         a.stamps[((uint64_t) tk * len + i) * 16 + 9] = __builtin_amdgcn_s_memrealtime(),   // 100 MHz, one clock for all XCDs
          a.stamps[((uint64_t) tk * len + i) * 16 + 8] = (uint64_t) n | ((uint64_t) itot << 16) |
                                                      ((uint64_t) nkeep << 32) | ((uint64_t) (take != 0) << 63);
 #endif
@@ -1438,7 +1452,7 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
    const uint32_t ntasks = a.ntasks;
    // an earlier level served a request by M/G/1 (exception tails): the chain's
    // inputs are not in FIFO order -> the level engine reruns the batch
-   if (a.errflag[2] != 0)
+   if (a.errflag[2] != 0 && (!a.excfix || (a.errflag[2] & 2u)))
    {
       if (threadIdx.x == 0 && blockIdx.x == 0) flag(a, F_FALLBACK | R_EXC);
       return;
@@ -1455,6 +1469,166 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
       if (LB) task_lb<NL, F1>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
       else task_ser<NL, F1>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
       wsync();
+   }
+}
+
+// ---------------------------------------------------------------------------
+// exception tails into order (before the chains)
+// ---------------------------------------------------------------------------
+// A request the injection level served by M/G/1 may leave its queue out of FIFO
+// order; k_level stores such records at the end of their slot (nexc counts them,
+// errflag[2] says some slot has them).  The chains need every insert slot sorted by
+// (t, id), the arrival order at the next port: one workgroup per such slot sorts its
+// exceptions in LDS and merges them into the FIFO part in place (the FIFO records
+// behind the first exception move up, chunk by chunk from the top), rewriting the
+// key samples of every position it writes.  A slot with more than XM exceptions
+// raises errflag[2] bit 1 and the chains decline the batch as before.
+constexpr int XM = 2048;
+constexpr int XT = 256;
+__device__ __forceinline__ bool key_lt(uint64_t ta, uint32_t ia, uint64_t tb, uint32_t ib)
+{
+   return ta < tb || (ta == tb && ia < ib);
+}
+__global__ __launch_bounds__(XT) void k_exc_merge(uint32_t nslots, const uint32_t* __restrict__ cnt,
+                                                  const uint64_t* __restrict__ base, uint32_t* __restrict__ nexc,
+                                                  Rec* __restrict__ recs, uint64_t* __restrict__ samp_t,
+                                                  uint32_t* __restrict__ samp_id, unsigned* __restrict__ errflag)
+{
+   __shared__ uint64_t et[XM];
+   __shared__ uint32_t eid[XM], eax[XM], edst[XM];
+   __shared__ uint32_t s_list[XT], s_n;
+   if (errflag[2] == 0) return;   // no exception anywhere
+   const uint32_t tid = threadIdx.x;
+   for (uint32_t s0 = blockIdx.x * XT; s0 < nslots; s0 += gridDim.x * XT)
+   {
+      if (tid == 0) s_n = 0;
+      __syncthreads();
+      const uint32_t sl = s0 + tid;
+      if (sl < nslots && nexc[sl]) s_list[atomicAdd(&s_n, 1u)] = sl;
+      __syncthreads();
+      const uint32_t nl = s_n;
+      for (uint32_t q = 0; q < nl; q++)
+      {
+         const uint32_t slot = s_list[q];
+         const uint32_t c = cnt[slot], x = nexc[slot];
+         const uint64_t b = base[slot];
+         if (x > (uint32_t) XM || x > c)
+         {
+            if (tid == 0) atomicOr(errflag + 2, 2u);
+            continue;
+         }
+         const uint32_t m = c - x;   // FIFO part [0, m), exception k at c - 1 - k
+         uint32_t P = 1;
+         while (P < x) P <<= 1;
+         for (uint32_t k = tid; k < P; k += XT)
+         {
+            if (k < x)
+            {
+               const Rec r = recs[b + c - 1 - k];
+               et[k] = r.t;
+               eid[k] = r.id;
+               eax[k] = r.aux;
+            }
+            else
+            {
+               et[k] = ~0ull;
+               eid[k] = ~0u;
+            }
+         }
+         __syncthreads();
+         // bitonic sort of the exceptions by (t, id)
+         for (uint32_t kk = 2; kk <= P; kk <<= 1)
+            for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1)
+            {
+               for (uint32_t i = tid; i < P; i += XT)
+               {
+                  const uint32_t l = i ^ jj;
+                  if (l > i)
+                  {
+                     const bool up = (i & kk) == 0;
+                     const bool gt = key_lt(et[l], eid[l], et[i], eid[i]);
+                     if (gt == up)
+                     {
+                        const uint64_t t0 = et[i];
+                        et[i] = et[l];
+                        et[l] = t0;
+                        const uint32_t i0 = eid[i];
+                        eid[i] = eid[l];
+                        eid[l] = i0;
+                        const uint32_t a0 = eax[i];
+                        eax[i] = eax[l];
+                        eax[l] = a0;
+                     }
+                  }
+               }
+               __syncthreads();
+            }
+         // each exception's merged position: its rank + the FIFO records before it
+         for (uint32_t k = tid; k < x; k += XT)
+         {
+            uint32_t lo = 0, hi = m;
+            while (lo < hi)
+            {
+               const uint32_t mid = (lo + hi) >> 1;
+               const Rec r = recs[b + mid];
+               if (key_lt(r.t, r.id, et[k], eid[k])) lo = mid + 1;
+               else hi = mid;
+            }
+            edst[k] = k + lo;
+         }
+         __syncthreads();
+         // FIFO records from the first exception's position up move by the exceptions
+         // before them: top chunk first, each chunk read completely before it is written
+         const uint32_t i0 = x ? edst[0] : m;
+         for (uint32_t top = m; top > i0;)
+         {
+            const uint32_t a0 = top > i0 + XT ? top - XT : i0;
+            const uint32_t i = a0 + tid;
+            Rec r;
+            uint32_t d = 0;
+            if (i < top)
+            {
+               r = recs[b + i];
+               uint32_t lo = 0, hi = x;
+               while (lo < hi)
+               {
+                  const uint32_t mid = (lo + hi) >> 1;
+                  if (key_lt(et[mid], eid[mid], r.t, r.id)) lo = mid + 1;
+                  else hi = mid;
+               }
+               d = i + lo;
+            }
+            __syncthreads();
+            if (i < top)
+            {
+               const uint64_t g = b + d;
+               recs[g] = r;
+               if ((g & 63) == 0)
+               {
+                  samp_t[g >> 6] = r.t;
+                  samp_id[g >> 6] = r.id;
+               }
+            }
+            __syncthreads();
+            top = a0;
+         }
+         for (uint32_t k = tid; k < x; k += XT)
+         {
+            const uint64_t g = b + edst[k];
+            Rec r;
+            r.t = et[k];
+            r.id = eid[k];
+            r.aux = eax[k];
+            recs[g] = r;
+            if ((g & 63) == 0)
+            {
+               samp_t[g >> 6] = r.t;
+               samp_id[g >> 6] = r.id;
+            }
+         }
+         if (tid == 0) nexc[slot] = 0;
+         __syncthreads();
+      }
    }
 }
 

@@ -208,6 +208,8 @@ struct gnoc_engine
    int ch_grid = 0;
    int force_levels = 0;
    int ch_declined = 0;                     // this batch fell back from the chain engine: later runs skip it
+   int exc_fix = 0;                         // this batch's injection level leaves exception tails: k_exc_merge
+   std::vector<std::pair<void*, uint64_t>> zq;   // buffers to zero before the first level launch (one k_zero_segs)
    int ch_resized = 0;                      // the windows were already changed during this (sharded) run
    int used_chain = 0;
    uint32_t ncpx = 0, ncpy = 0;
@@ -654,6 +656,7 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
                      !std::getenv("GNOC_WINDOW_PS") && !std::getenv("GNOC_WINDOW_PS_X") && !std::getenv("GNOC_WINDOW_PS_Y");
    std::copy(key, key + 4, e->ch_key);
    e->ch_declined = 0;
+   e->exc_fix = 0;
    if (same) return;
    const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size (2^shift ps)
    const char* pv = std::getenv("GNOC_WINDOW_PS");      // test knob: force the window size (ps)
@@ -946,6 +949,24 @@ static int upload_broadcasts(gnoc_engine* e)
    e->dc.bc_cur = e->d_bv[1].as<uint64_t>();
    e->dc.bc_fin = e->d_bfin.as<uint64_t>();
    return GNOC_OK;
+}
+
+// The per-run zeroing of counters, slot counts, exception counts and port counters
+// in one launch (segment = blockIdx.y) instead of one fill per buffer.  Segment 0
+// is the counter block: with broadcasts its word 10 (errflag[2], "slots have
+// tails") starts at 1.
+constexpr int ZSEG = 10;
+struct ZeroSegs
+{
+   uint32_t* p[ZSEG];
+   uint64_t nw[ZSEG];
+};
+__global__ __launch_bounds__(256) void k_zero_segs(ZeroSegs z, uint32_t w10)
+{
+   uint32_t* const p = z.p[blockIdx.y];
+   const uint64_t n = z.nw[blockIdx.y];
+   for (uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
+      p[i] = (blockIdx.y == 0 && i == 10) ? w10 : 0u;
 }
 
 __global__ void k_g2l(uint64_t n, const uint32_t* __restrict__ gid, uint32_t* __restrict__ g2l)
@@ -1404,6 +1425,7 @@ static uint64_t chunk_bound_of(const gnoc_engine* e, uint32_t P)
    return e->rec_bound / cmin + P + 1;
 }
 
+static int zq_flush(gnoc_engine* e, hipStream_t s);
 static int run_plan_v3(gnoc_engine* e)
 {
    const DevCfg& c = e->dc;
@@ -1420,7 +1442,7 @@ static int run_plan_v3(gnoc_engine* e)
    GNOC_HIP(e, e->st.ensure(chunk_bound * LV_STATE_WORDS * 8));
    GNOC_HIP(e, e->lvl_ctr.ensure((size_t) L * LV_QUEUES * 4));
    GNOC_HIP(e, e->lvl_qb.ensure((size_t) L * LV_QB * 4));
-   GNOC_HIP(e, hipMemsetAsync(e->lvl_ctr.p, 0, (size_t) L * LV_QUEUES * 4, s));
+   e->zq.push_back({ e->lvl_ctr.p, (uint64_t) L * LV_QUEUES * 4 });   // zeroed before the first level (zq_flush)
    const uint32_t pg = (P + 255) / 256;
    GNOC_LAUNCH(e, KC_PLAN, k_plan_ports, dim3(pg), dim3(256), 0, s, c, P, e->d_lvl_ports.as<uint32_t>(),
                e->d_port_k.as<uint32_t>(), e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
@@ -1459,7 +1481,11 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
    if (l0 == 0)
    {
       GNOC_HIP(e, e->done.ensure((size_t) std::max<uint32_t>(P, 1) * 4));
-      GNOC_HIP(e, hipMemsetAsync(e->done.p, 0, (size_t) std::max<uint32_t>(P, 1) * 4, s));
+      e->zq.push_back({ e->done.p, (uint64_t) std::max<uint32_t>(P, 1) * 4 });
+   }
+   {
+      const int zr = zq_flush(e, s);
+      if (zr) return zr;
    }
    // default: one launch per level (the launch boundary is the level barrier).
    // GNOC_XLEVEL=1: one persistent launch over every level with port-level
@@ -1507,6 +1533,7 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
 constexpr int GNOC_V3_RETRY = 1000;
 constexpr int GNOC_CH_RETRY = 1001;      // a chain window overflowed LDS: smaller windows
 constexpr int GNOC_CH_FALLBACK = 1002;   // the chain engine cannot take this batch: level engine
+constexpr int GNOC_CH_EXC = 1003;        // only the injection level's exception tails: merge them, rerun
 
 // ---------------------------------------------------------------------------
 // v4: chain engine for the X and Y phases (chain.hip); INJ and SELF levels on k_level
@@ -1538,7 +1565,7 @@ static int chain_setup(gnoc_engine* e)
    // atomics next to it slowed the polls by half)
    const size_t nmx = 2 * (e->h_cw[0].size() + e->h_cw[1].size());
    GNOC_HIP(e, e->ch_nmax.ensure(std::max<size_t>(nmx, 1) * 4));
-   GNOC_HIP(e, hipMemsetAsync(e->ch_nmax.p, 0, std::max<size_t>(nmx, 1) * 4, s));
+   e->zq.push_back({ e->ch_nmax.p, (uint64_t) std::max<size_t>(nmx, 1) * 4 });   // (zq_flush: before the INJ level)
    const size_t stb = (e->ch_st_words[0] + e->ch_st_words[1] + ch::SW) * 8;
    const bool fresh = e->ch_st.bytes < stb;
    GNOC_HIP(e, e->ch_st.ensure(stb));
@@ -1550,7 +1577,7 @@ static int chain_setup(gnoc_engine* e)
       GNOC_HIP(e, hipMemsetAsync(e->ch_st.p, 0, e->ch_st.bytes, s));
       if (e->ch_epoch == 0) e->ch_epoch = 1;
    }
-   GNOC_HIP(e, hipMemsetAsync(e->ch_ctr.p, 0, 256, s));
+   e->zq.push_back({ e->ch_ctr.p, 256 });
    // the hand-off protocol per phase: GNOC_CHAIN_LOOKBACK=0/1 forces one; otherwise each is
    // timed once on the current windows and the faster one is kept
    const char* lbv = std::getenv("GNOC_CHAIN_LOOKBACK");
@@ -1576,6 +1603,10 @@ static int chain_setup(gnoc_engine* e)
 // One phase: 0 = X (rows of this rank), 1 = Y (columns of this rank).
 static int chain_phase(gnoc_engine* e, int phase)
 {
+   {
+      const int zr = zq_flush(e, e->stream);
+      if (zr) return zr;
+   }
    const DevCfg& c = e->dc;
    hipStream_t s = e->stream;
    const uint32_t ncp = phase ? e->ncpy : e->ncpx;
@@ -1608,7 +1639,7 @@ static int chain_phase(gnoc_engine* e, int phase)
    a.tasks = e->ch_tasks.as<uint32_t>() + (phase ? e->h_tasks[0].size() : 0);
    a.cp0 = 0;
    a.nmax = e->ch_nmax.as<unsigned>() + (phase ? 2 * e->h_cw[0].size() : 0);
-   a.pad0 = 0;
+   a.excfix = (uint32_t) e->exc_fix;
    a.etag = (uint64_t) e->ch_epoch << 48;
    a.stamps = nullptr;
    a.lookback = e->ch_lb_run[phase];
@@ -1641,6 +1672,39 @@ static int chain_phase(gnoc_engine* e, int phase)
 }
 
 static int run_post(gnoc_engine* e, bool closed_form);
+
+// Zero the queued buffers (e->zq) in one launch.
+static int zq_flush(gnoc_engine* e, hipStream_t s)
+{
+   while (!e->zq.empty())
+   {
+      ZeroSegs z{};
+      uint32_t ns = 0;
+      uint64_t mx = 0;
+      while (!e->zq.empty() && ns < (uint32_t) ZSEG)
+      {
+         z.p[ns] = (uint32_t*) e->zq.back().first;
+         z.nw[ns] = e->zq.back().second / 4;
+         mx = std::max(mx, z.nw[ns]);
+         ns++;
+         e->zq.pop_back();
+      }
+      const uint32_t gx = (uint32_t) std::max<uint64_t>(1, std::min<uint64_t>((mx + 255) / 256, 512));
+      GNOC_LAUNCH(e, KC_PLAN, k_zero_segs, dim3(gx, ns), dim3(256), 0, s, z, 0u);
+   }
+   return GNOC_OK;
+}
+
+// The injection level's exception tails into (t, id) order (chain.hip k_exc_merge)
+static int exc_merge(gnoc_engine* e)
+{
+   const uint32_t nslots = e->dc.N * PORTS * INS;
+   const uint32_t wins = (nslots + ch::XT - 1) / ch::XT;
+   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_exc_merge, dim3(std::max(1u, std::min(wins, 2048u))), dim3(ch::XT), 0, e->stream, nslots,
+               e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->nexc.as<uint32_t>(), e->recs.as<Rec>(),
+               e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->counters.as<unsigned>() + 8);
+   return GNOC_OK;
+}
 
 // Phase 1 of a run: per-run buffers, classification, injection-slot layout,
 // stable scatter, closed-form slot counts and bases.  Queue models disabled
@@ -1699,20 +1763,35 @@ static int run_prep(gnoc_engine* e, bool* done)
 
    e->evused = 0;
    e->evkid.clear();
+   e->zq.clear();
    GNOC_HIP(e, hipEventRecord(e->ev0, s));
-   GNOC_HIP(e, hipMemsetAsync(e->counters.p, 0, 64, s));
-   // broadcast children live in the exception tails of their slots (level.hip
-   // lv_bcast): every level reads the tail counts (errflag word 2)
-   if (e->nb) GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned>() + 8 + 2, 1, 1, s));
-   GNOC_HIP(e, hipMemsetAsync(e->slot_cnt.p, 0, (size_t) nslots * 4, s));
-   GNOC_HIP(e, hipMemsetAsync(e->nexc.p, 0, (size_t) nslots * 4, s));
-   GNOC_HIP(e, hipMemsetAsync(e->port_sum.p, 0, nports * 8, s));
-   GNOC_HIP(e, hipMemsetAsync(e->port_cnt.p, 0, nports * 8, s));
-   GNOC_HIP(e, hipMemsetAsync(e->port_mg1.p, 0, nports * 8, s));
-   GNOC_HIP(e, hipMemsetAsync(e->port_flit.p, 0, nports * 8, s));
-   GNOC_HIP(e, hipMemsetAsync(e->port_last.p, 0, nports * 8, s));
-   if (!pp_lds) GNOC_HIP(e, hipMemsetAsync(e->Pp.p, 0, (size_t) H * G * N * 4, s));
-   if (band_prep) GNOC_HIP(e, hipMemsetAsync(e->pcol.p, 0, (size_t) nC * H * H * 3 * 4, s));
+   {
+      // counters; slot and exception counts; port counters (and the prefix tables the
+      // prep kernels accumulate into): one launch.  Broadcast children live in the
+      // exception tails of their slots (level.hip lv_bcast): with broadcasts every
+      // level reads the tail counts (errflag word 2 = counter word 10 starts at 1)
+      ZeroSegs z{};
+      uint32_t ns = 0;
+      uint64_t mx = 0;
+      auto seg = [&](void* p, uint64_t bytes) {
+         z.p[ns] = (uint32_t*) p;
+         z.nw[ns] = bytes / 4;
+         mx = std::max(mx, bytes / 4);
+         ns++;
+      };
+      seg(e->counters.p, 64);
+      seg(e->slot_cnt.p, (uint64_t) nslots * 4);
+      seg(e->nexc.p, (uint64_t) nslots * 4);
+      seg(e->port_sum.p, nports * 8);
+      seg(e->port_cnt.p, nports * 8);
+      seg(e->port_mg1.p, nports * 8);
+      seg(e->port_flit.p, nports * 8);
+      seg(e->port_last.p, nports * 8);
+      if (!pp_lds) seg(e->Pp.p, (uint64_t) H * G * N * 4);
+      if (band_prep) seg(e->pcol.p, (uint64_t) nC * H * H * 3 * 4);
+      const uint32_t gx = (uint32_t) std::max<uint64_t>(1, std::min<uint64_t>((mx + 255) / 256, 512));
+      GNOC_LAUNCH(e, KC_CLASSIFY, k_zero_segs, dim3(gx, ns), dim3(256), 0, s, z, e->nb ? 1u : 0u);
+   }
 
    // always launched: for an empty batch it writes the all-zero source histogram
    GNOC_LAUNCH(e, KC_CLASSIFY, k_classify, dim3(nch), dim3(256), N * 4, s, c, (uint64_t) n, pch, e->d_inj, e->d_src,
@@ -1925,6 +2004,8 @@ static int run_post(gnoc_engine* e, bool closed_form)
          std::snprintf(m, sizeof m, "internal: chain route-count invariant violated (flags 0x%x)", ef[4]);
          return fail(e, GNOC_EHIP, m);
       }
+      // declined only because the injection level left exception tails: rerun with them merged
+      if (!e->exc_fix && ef[4] == (ch::F_FALLBACK | ch::R_EXC) && !(ef[2] & 2u)) return GNOC_CH_EXC;
       return (ef[4] & (ch::F_FALLBACK | ch::F_TIMEOUT)) ? GNOC_CH_FALLBACK : GNOC_CH_RETRY;
    }
    // a leaf the splitter could not cut (or a look-back timeout) leaves garbage
@@ -1957,6 +2038,7 @@ static int run_once(gnoc_engine* e)
       rc = run_plan_v3(e);
       if (!rc) rc = chain_setup(e);
       if (!rc) rc = run_levels_v3(e, 0, 1);
+      if (!rc && e->exc_fix) rc = exc_merge(e);
       if (!rc) rc = chain_phase(e, 0);
       if (!rc) rc = chain_phase(e, 1);
       const char* xv = std::getenv("GNOC_CHAIN_EXPERIMENT");
@@ -2251,6 +2333,13 @@ static int run_impl(gnoc_engine* e)
       e->chD_run[0] = e->chD[0];
       e->chD_run[1] = e->chD[1];
       int rc = run_once(e);
+      if (rc == GNOC_CH_EXC)
+      {
+         e->exc_fix = 1;   // later runs of this batch merge the tails up front
+         e->n_retry++;
+         rc = run_once(e);
+      }
+      if (rc == GNOC_CH_EXC) rc = GNOC_CH_FALLBACK;
       // chain engine: a window that overflowed LDS reruns with windows half as long
       // (twice as many), up to 3 times; anything else it cannot take reruns on levels
       while (rc == GNOC_CH_RETRY && e->n_retry < 3)

@@ -1,0 +1,64 @@
+"""Exception tails of the injection level merged into order before the chains
+(chain.hip k_exc_merge): a batch whose injection queues serve cycle-0 bursts by
+M/G/1 (the history tree's analytical branch, queue_model_history_tree.cc:58-64)
+stays on the chain engine, bit-exact against the oracle."""
+import numpy as np
+import pytest
+
+from graphite_amd import gnoc
+from oracle import oracle
+from tests.traces import random_trace
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1", "port_flit")
+
+
+def same(got, ref):
+    for k in FIELDS:
+        a, b = getattr(got, k), getattr(ref, k)
+        if not np.array_equal(a, b):
+            bad = np.nonzero(a != b)[0]
+            raise AssertionError(f"{k}: {bad.size} differ, first {bad[0]}: {a[bad[0]]} vs {b[bad[0]]}")
+
+
+def burst_trace(W, H, per_tile, tail, seed, max_cycle=4000):
+    """Every tile injects `per_tile` packets at cycle 0, then a light random tail."""
+    rng = np.random.default_rng(seed)
+    N = W * H
+    src0 = np.repeat(np.arange(N, dtype=np.uint32), per_tile)
+    t1 = np.sort(rng.integers(1, max_cycle, tail)).astype(np.uint64) * np.uint64(1000)
+    src = np.concatenate([src0, rng.integers(0, N, tail).astype(np.uint32)])
+    t = np.concatenate([np.zeros(src0.size, np.uint64), t1])
+    dst = rng.integers(0, N, src.size).astype(np.uint32)
+    return gnoc.Trace(t, src, dst, np.full(src.size, 576, np.uint32), np.zeros(src.size, np.uint32))
+
+
+@pytest.mark.parametrize("W,H,per_tile,seed", [(8, 8, 6, 1), (8, 8, 20, 2), (5, 3, 12, 3), (16, 16, 4, 4)])
+def test_injection_mg1_stays_on_chain(W, H, per_tile, seed):
+    cfg = gnoc.EngineConfig(num_tiles=W * H, mesh_width=W, mesh_height=H)
+    tr = burst_trace(W, H, per_tile, 4000, seed)
+    ref = oracle.run(cfg, tr)
+    assert ref.port_mg1.sum() > 0
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    paths = []
+    for _ in range(3):
+        eng.run()
+        got = eng.results()
+        same(got, ref)
+        paths.append(got.summary["engine_path"])
+    eng.close()
+    print("engine paths", paths, "mg1 uses", int(ref.port_mg1.sum()))
+
+
+def test_saturated_mg1_matches_either_path():
+    """test_gpu_parity's saturated batch (M/G/1 also in mesh ports): still exact."""
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = random_trace(20000, 8, 8, seed=3, max_cycle=300, burst0=400)
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    got = eng.results()
+    eng.close()
+    same(got, oracle.run(cfg, tr))

@@ -81,10 +81,23 @@ def main():
             if m.sum() > 100:
                 print(f"    {r:2d} rows: {m.sum():7d} steps, mean step {tot[m].mean():7.0f}  emit {d['emit'][ok][m].mean():6.0f}"
                       f"  bscan {d['bscan'][ok][m].mean():6.0f}  rows {d['rows'][ok][m].mean():6.0f}")
-        good = t[:, 0, 0] > 0
+        good = (t[:, 0, 0] > 0) & (t[:, -1, 7] > 0)
         task_t = t[:, -1, 7] - t[:, 0, 0]
-        print(f"  task duration med {np.median(task_t[good]):.0f} cyc; span of phase "
-              f"{t[good][:, -1, 7].max() - t[good][:, 0, 0].min()} cyc")
+        print(f"  task duration med {np.median(task_t[good]):.0f} cyc")
+        # occupancy over the phase from s_memrealtime (100 MHz, shared by the XCDs; the
+        # s_memtime counters are per XCD): running tasks per 1/50 of the phase
+        rt = st[:, :, 9].astype(np.int64)
+        good &= (rt[:, 0] > 0) & (rt[:, -1] > 0)
+        t0, t1 = rt[good][:, 0].min(), rt[good][:, -1].max()
+        print(f"  span of phase {(t1 - t0) / 100:.1f} us (s_memrealtime, step end marks)")
+        st_, en_ = rt[good][:, 0] - t0, rt[good][:, -1] - t0
+        task_t = en_ - st_
+        nb = 50
+        edges = np.linspace(0, t1 - t0, nb + 1)
+        run = np.array([((st_ < edges[b + 1]) & (en_ > edges[b])).sum() for b in range(nb)])
+        busy = task_t[good].sum() / (run.max() * (t1 - t0))
+        print(f"  running tasks per 1/{nb} of the phase: " + " ".join(str(x) for x in run))
+        print(f"  task-slot utilisation (task time / (peak running x span)): {busy:.3f}")
 
 
 if __name__ == "__main__":
