@@ -52,6 +52,42 @@ def test_injection_mg1_stays_on_chain(W, H, per_tile, seed):
     print("engine paths", paths, "mg1 uses", int(ref.port_mg1.sum()))
 
 
+def star_trace(W, H, ax, ay, seed, tail=3000):
+    """Tile (ax, ay) injects 6 packets at cycle 0, one along each of 6 paths (no mesh
+    port gets more than 2 of them, so only its injection queue backs up beyond one
+    service time: packets 3-6 are served by M/G/1 there); random traffic from cycle 500."""
+    rng = np.random.default_rng(seed)
+    a = ay * W + ax
+    dst0 = [(ax + 2, ay), (ax - 2, ay), (ax, ay + 2), (ax, ay - 2), (ax + 1, ay + 1), (ax - 1, ay - 1)]
+    d0 = np.array([y * W + x for x, y in dst0], np.uint32)
+    t1 = np.sort(rng.integers(500, 5000, tail)).astype(np.uint64) * np.uint64(1000)
+    t = np.concatenate([np.zeros(6, np.uint64), t1])
+    src = np.concatenate([np.full(6, a, np.uint32), rng.integers(0, W * H, tail).astype(np.uint32)])
+    dst = np.concatenate([d0, rng.integers(0, W * H, tail).astype(np.uint32)])
+    return gnoc.Trace(t, src, dst, np.full(t.size, 576, np.uint32), np.zeros(t.size, np.uint32))
+
+
+@pytest.mark.parametrize("W,ax,ay", [(8, 4, 4), (16, 7, 9), (8, 2, 5)])
+def test_injection_only_mg1_runs_on_chain(W, ax, ay):
+    """M/G/1 only in one injection queue: the first run merges its exception tails and
+    reruns on the chains (one retry), later runs merge up front; bit-exact throughout."""
+    cfg = gnoc.EngineConfig(num_tiles=W * W)
+    tr = star_trace(W, W, ax, ay, seed=W + ax)
+    ref = oracle.run(cfg, tr)
+    assert ref.port_mg1.sum() > 0
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    for k in range(3):
+        eng.run()
+        got = eng.results()
+        same(got, ref)
+        s = got.summary
+        assert s["engine_path"] == 4, s
+        assert s["fallbacks"] == 0
+        assert s["retries"] == (1 if k == 0 else 0), s
+    eng.close()
+
+
 def test_saturated_mg1_matches_either_path():
     """test_gpu_parity's saturated batch (M/G/1 also in mesh ports): still exact."""
     cfg = gnoc.EngineConfig(num_tiles=64)
