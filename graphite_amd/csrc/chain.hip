@@ -25,6 +25,12 @@
 // (8-byte epoch-tagged granules, sc1 stores and loads, MI355X_MICROARCH.md
 // "Valid forms").  Tasks are handed out window-major, strictly in order to
 // running workgroups, so a task's predecessor is always running or done.
+// Two protocols (task_ser / task_lb), chosen per phase by the engine from their
+// measured times: the serial one waits for window w-1's state of each port; the
+// look-back one composes the nearest inclusive state with the aggregates the
+// windows after it publish right after their scans (a hot chain's windows then
+// stop queueing behind each other), waiting serially only where exactness needs
+// it (a queue that may still have had no gap; pending spills).
 //
 // A step (one port of one task) works on ROWS: the merged stream in 64-record
 // rows, record 64 r + lane in lane `lane` of row r.  The merge of the kept list
@@ -39,8 +45,9 @@
 // matters while a queue has never idled; without the M/G/1 branch it is the
 // FIFO recurrence, so the chain runs FIFO and checks, per record, the branch
 // condition X > t + p while the port has had no gap.  If it would fire (or an
-// earlier level wrote exception tails, or a window overflows LDS) the kernel
-// raises a flag and the host reruns the batch (smaller windows / level engine).
+// earlier level wrote exception tails the engine has not merged, k_exc_merge, or
+// a window overflows LDS) the kernel raises a flag and the host reruns the batch
+// (merged tails / smaller windows / level engine).
 #include "common.h"
 
 namespace gnoc {

@@ -2005,7 +2005,7 @@ static int run_post(gnoc_engine* e, bool closed_form)
          return fail(e, GNOC_EHIP, m);
       }
       // declined only because the injection level left exception tails: rerun with them merged
-      if (!e->exc_fix && ef[4] == (ch::F_FALLBACK | ch::R_EXC) && !(ef[2] & 2u)) return GNOC_CH_EXC;
+      if (!e->exc_fix && e->nranks <= 1 && ef[4] == (ch::F_FALLBACK | ch::R_EXC) && !(ef[2] & 2u)) return GNOC_CH_EXC;
       return (ef[4] & (ch::F_FALLBACK | ch::F_TIMEOUT)) ? GNOC_CH_FALLBACK : GNOC_CH_RETRY;
    }
    // a leaf the splitter could not cut (or a look-back timeout) leaves garbage
@@ -2757,6 +2757,7 @@ static int run_finish_impl(gnoc_engine* e, const void* recv_buf)
       rc = chain_phase(e, 1);
       if (!rc) rc = run_levels_v3(e, L - 1, L);
       if (!rc) rc = run_post(e, false);
+      if (rc == GNOC_CH_EXC) rc = GNOC_CH_FALLBACK;   // (no exception merge on the sharded path)
       // the windows of the next run: from this run's measured fill, or shorter
       // for the chains that overflowed (results never depend on them)
       if (!rc && !e->ch_resized) adapt_windows(e);
