@@ -99,10 +99,33 @@ def main():
     # communicator of libgnoc's own, grouped ncclSend / ncclRecv on the engine's
     # stream); GNOC_BENCH_NATIVE=0 (or the gloo rehearsal) drives it from torch instead
     native = sharded and backend == "nccl" and os.environ.get("GNOC_BENCH_NATIVE", "1") != "0"
-    comm = gnoc.RcclComm(world, rank, local) if native else None
+    comm = None
     if native:
-        eng = gnoc.NativeShardedEngine(cfg, rank, world, comm)
-    else:
+        # one trial step on the native path; if it raises on any rank (gnoc_run_sharded
+        # max-reduces its status, so a failing rank fails every rank instead of
+        # leaving one inside the exchange), every rank takes the torch-driven exchange
+        ok = 1
+        try:
+            comm = gnoc.RcclComm(world, rank, local)
+            eng = gnoc.NativeShardedEngine(cfg, rank, world, comm)
+            eng.submit(tr)
+            eng.run()
+        except Exception as ex:   # noqa: BLE001 -- reported, then the other path
+            print(f"bench: rank {rank}: native RCCL path failed ({ex}); using the torch exchange", file=sys.stderr)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device="cuda")
+        if world > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not int(flag.item()):
+            native = False
+            for x in (locals().get("eng"), comm):
+                try:
+                    if x is not None:
+                        x.close()
+                except Exception:   # noqa: BLE001
+                    pass
+            comm = None
+    if not native:
         eng = gnoc.ShardedEngine(cfg, rank, world) if sharded else gnoc.Engine(cfg)
     eng.submit(tr)          # trace now resident in HBM; steps start from there
 

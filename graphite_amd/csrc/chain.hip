@@ -171,7 +171,7 @@ struct ChainArgs
    unsigned* nmax;                // [2 c] the most stream records, [2 c + 1] the most inserts of chain c's steps
    uint64_t* stamps;              // debug (GNOC_STAMPS=1): [(task * len + i) * 16 + k] phase stamps, else null
    uint32_t lookback;             // 1: look-back over earlier windows' AGG / INC; 0: wait for window w-1's INC
-   uint32_t pad1;
+   uint32_t fw;                   // this phase's flag word: errflag[4] (X) or errflag[5] (Y)
 };
 
 
@@ -276,7 +276,7 @@ __device__ __forceinline__ uint32_t lb(const uint64_t* a, uint32_t n, uint64_t k
    return pos;
 }
 
-__device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f) { atomicOr(a.errflag + 4, f); }
+__device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f) { atomicOr(a.errflag + a.fw, f); }
 // A window of chain c overflowed LDS: the run retries, halving that chain's windows.
 __device__ __forceinline__ void flag_overflow(const ChainArgs& a, uint32_t c)
 {
@@ -285,14 +285,14 @@ __device__ __forceinline__ void flag_overflow(const ChainArgs& a, uint32_t c)
 }
 __device__ __forceinline__ bool flagged(const ChainArgs& a)
 {
-   return (__hip_atomic_load(a.errflag + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & F_ANY) != 0;
+   return (__hip_atomic_load(a.errflag + a.fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & F_ANY) != 0;
 }
 // The polls' abort check rides along in lane FL (no state word uses it): the flag load
 // is issued beside the state reloads, so a poll round costs one memory round trip.
 constexpr uint32_t FL = 63;
 __device__ __forceinline__ void ld_flag(const ChainArgs& a, uint32_t lane, uint32_t& ef)
 {
-   if (lane == FL) ef = __hip_atomic_load(a.errflag + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+   if (lane == FL) ef = __hip_atomic_load(a.errflag + a.fw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ bool aborted(uint32_t ef) { return (rdl(ef, (int) FL) & F_ANY) != 0; }
 
@@ -1459,6 +1459,8 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
    const uint32_t ntasks = a.ntasks;
    // an earlier level served a request by M/G/1 (exception tails): the chain's
    // inputs are not in FIFO order -> the level engine reruns the batch
+   // the X phase declined: its outputs are incomplete and the batch reruns on levels
+   if (a.fw != 4 && (a.errflag[4] & F_ANY)) return;
    if (a.errflag[2] != 0 && (!a.excfix || (a.errflag[2] & 2u)))
    {
       if (threadIdx.x == 0 && blockIdx.x == 0) flag(a, F_FALLBACK | R_EXC);

@@ -208,6 +208,7 @@ struct gnoc_engine
    int ch_grid = 0;
    int force_levels = 0;
    int ch_declined = 0;                     // this batch fell back from the chain engine: later runs skip it
+   int ch_ydeclined = 0;                    // only its Y phase did: later runs take X chains + Y levels (path 5)
    int exc_fix = 0;                         // this batch's injection level leaves exception tails: k_exc_merge
    std::vector<std::pair<void*, uint64_t>> zq;   // buffers to zero before the first level launch (one k_zero_segs)
    int ch_resized = 0;                      // the windows were already changed during this (sharded) run
@@ -656,6 +657,7 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
                      !std::getenv("GNOC_WINDOW_PS") && !std::getenv("GNOC_WINDOW_PS_X") && !std::getenv("GNOC_WINDOW_PS_Y");
    std::copy(key, key + 4, e->ch_key);
    e->ch_declined = 0;
+   e->ch_ydeclined = 0;
    e->exc_fix = 0;
    if (same) return;
    const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size (2^shift ps)
@@ -1534,6 +1536,7 @@ constexpr int GNOC_V3_RETRY = 1000;
 constexpr int GNOC_CH_RETRY = 1001;      // a chain window overflowed LDS: smaller windows
 constexpr int GNOC_CH_FALLBACK = 1002;   // the chain engine cannot take this batch: level engine
 constexpr int GNOC_CH_EXC = 1003;        // only the injection level's exception tails: merge them, rerun
+constexpr int GNOC_CH_YFALL = 1004;      // only the Y chains declined: Y and SELF levels on k_level
 
 // ---------------------------------------------------------------------------
 // v4: chain engine for the X and Y phases (chain.hip); INJ and SELF levels on k_level
@@ -1643,7 +1646,7 @@ static int chain_phase(gnoc_engine* e, int phase)
    a.etag = (uint64_t) e->ch_epoch << 48;
    a.stamps = nullptr;
    a.lookback = e->ch_lb_run[phase];
-   a.pad1 = 0;
+   a.fw = phase ? 5u : 4u;
    const char* stv = std::getenv("GNOC_STAMPS");
    if (stv && *stv == '1')
    {
@@ -1982,31 +1985,39 @@ static int run_post(gnoc_engine* e, bool closed_form)
    if (e->h_pinned[3] > e->rec_bound) return fail(e, GNOC_EHIP, "internal: slot layout exceeds the record bound");
    const unsigned* ef = (const unsigned*) (e->h_pinned + 8);
    const unsigned errf = ef[0];
-   if (e->used_chain && !(ef[4] & ch::F_ANY))
+   const unsigned cf = ef[4] | ef[5];   // the X phase's and the Y phase's chain flags
+   if (e->used_chain && !(cf & ch::F_ANY))
    {
       // this run's time of each phase's protocol (chain_setup keeps the faster one)
       for (int p = 0; p < 2; p++)
       {
          float ms = 0;
-         if ((p ? e->ncpy : e->ncpx) && hipEventElapsedTime(&ms, e->ch_ev[p][0], e->ch_ev[p][1]) == hipSuccess)
+         if ((p ? e->ncpy && !e->ch_ydeclined : e->ncpx) &&
+             hipEventElapsedTime(&ms, e->ch_ev[p][0], e->ch_ev[p][1]) == hipSuccess)
             e->ch_lb_ms[p][e->ch_lb_run[p]] = ms;
       }
       if (std::getenv("GNOC_CHAIN_DEBUG"))
          std::fprintf(stderr, "gnoc: chain protocol X %u (%.3f / %.3f ms)  Y %u (%.3f / %.3f ms)\n", e->ch_lb_run[0],
                       e->ch_lb_ms[0][0], e->ch_lb_ms[0][1], e->ch_lb_run[1], e->ch_lb_ms[1][0], e->ch_lb_ms[1][1]);
    }
-   if (e->used_chain && (ef[4] & ch::F_ANY))
+   if (e->used_chain && (cf & ch::F_ANY))
    {
-      if (std::getenv("GNOC_CHAIN_DEBUG")) std::fprintf(stderr, "gnoc: chain engine declined, flags 0x%x\n", ef[4]);
-      if (ef[4] & ch::F_ROUTE)
+      if (std::getenv("GNOC_CHAIN_DEBUG"))
+         std::fprintf(stderr, "gnoc: chain engine declined, flags X 0x%x Y 0x%x\n", ef[4], ef[5]);
+      if (cf & ch::F_ROUTE)
       {
          char m[96];
-         std::snprintf(m, sizeof m, "internal: chain route-count invariant violated (flags 0x%x)", ef[4]);
+         std::snprintf(m, sizeof m, "internal: chain route-count invariant violated (flags 0x%x 0x%x)", ef[4], ef[5]);
          return fail(e, GNOC_EHIP, m);
       }
+      // only the Y chains declined, for a reason the level engine takes (the M/G/1
+      // branch, a spill range, a hand-off timeout): the X phase's outputs stand
+      if (!(ef[4] & ch::F_ANY) && (ef[5] & (ch::F_FALLBACK | ch::F_TIMEOUT)) && !(ef[5] & ch::F_RETRY) && e->nranks <= 1)
+         return GNOC_CH_YFALL;
       // declined only because the injection level left exception tails: rerun with them merged
-      if (!e->exc_fix && e->nranks <= 1 && ef[4] == (ch::F_FALLBACK | ch::R_EXC) && !(ef[2] & 2u)) return GNOC_CH_EXC;
-      return (ef[4] & (ch::F_FALLBACK | ch::F_TIMEOUT)) ? GNOC_CH_FALLBACK : GNOC_CH_RETRY;
+      if (!e->exc_fix && e->nranks <= 1 && ef[4] == (ch::F_FALLBACK | ch::R_EXC) && !(ef[5] & ch::F_ANY) && !(ef[2] & 2u))
+         return GNOC_CH_EXC;
+      return (cf & (ch::F_FALLBACK | ch::F_TIMEOUT)) ? GNOC_CH_FALLBACK : GNOC_CH_RETRY;
    }
    // a leaf the splitter could not cut (or a look-back timeout) leaves garbage
    // downstream, so it takes precedence: rerun exactly on the v1 path
@@ -2040,7 +2051,7 @@ static int run_once(gnoc_engine* e)
       if (!rc) rc = run_levels_v3(e, 0, 1);
       if (!rc && e->exc_fix) rc = exc_merge(e);
       if (!rc) rc = chain_phase(e, 0);
-      if (!rc) rc = chain_phase(e, 1);
+      if (!rc && !e->ch_ydeclined) rc = chain_phase(e, 1);
       const char* xv = std::getenv("GNOC_CHAIN_EXPERIMENT");
       if (!rc && xv && std::atoi(xv))
       {
@@ -2054,7 +2065,9 @@ static int run_once(gnoc_engine* e)
          e->ran = true;
          return GNOC_OK;
       }
-      if (!rc) rc = run_levels_v3(e, L - 1, L);
+      // Y phase on the chains, or (this batch's Y chains declined before) on levels
+      if (!rc) rc = run_levels_v3(e, e->ch_ydeclined ? e->lvl_y0 : L - 1, L);
+      if (e->ch_ydeclined) e->used_v3 = 5;
    }
    else if (v3)
    {
@@ -2065,6 +2078,26 @@ static int run_once(gnoc_engine* e)
       rc = run_levels_v1(e);
    if (rc) return rc;
    return run_post(e, false);
+}
+
+// After the Y chains declined (GNOC_CH_YFALL): the X phase's outputs and counters
+// stand; the Y phase's flags and its ports' counters are cleared, and the Y and
+// SELF levels run on k_level (their look-back state is untouched: k_level returned
+// at its first check while a chain flag was set).
+static int y_levels_rerun(gnoc_engine* e)
+{
+   hipStream_t s = e->stream;
+   GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 5, 0, 4, s));
+   const uint32_t np = e->dc.N * PORTS;
+   GNOC_LAUNCH(e, KC_CHAIN, ch::k_zero_ports, dim3((np + 255) / 256), dim3(256), 0, s, np,
+               (1u << P_UP) | (1u << P_DOWN) | (1u << P_SELF), e->port_sum.as<unsigned long long>(),
+               e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
+               e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>());
+   e->used_chain = 0;
+   e->used_v3 = 5;
+   int rc = run_levels_v3(e, e->lvl_y0, (uint32_t) e->lvl_off.size() - 1);
+   if (!rc) rc = run_post(e, false);
+   return rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -2340,6 +2373,14 @@ static int run_impl(gnoc_engine* e)
          rc = run_once(e);
       }
       if (rc == GNOC_CH_EXC) rc = GNOC_CH_FALLBACK;
+      if (rc == GNOC_CH_YFALL)
+      {
+         // the Y chains declined this batch (deterministic): its Y and SELF levels run on
+         // k_level now, and later runs go there straight after the X chains
+         e->n_fallback++;
+         e->ch_ydeclined = 1;
+         rc = y_levels_rerun(e);
+      }
       // chain engine: a window that overflowed LDS reruns with windows half as long
       // (twice as many), up to 3 times; anything else it cannot take reruns on levels
       while (rc == GNOC_CH_RETRY && e->n_retry < 3)
@@ -2680,7 +2721,7 @@ int gnoc_run_begin(gnoc_engine* e, void* send_buf)
             e->ch_resized = 1;
          }
          e->n_fallback++;
-         GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, 0, 4, s));
+         GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, 0, 8, s));
          const uint32_t np = e->dc.N * PORTS;
          hipLaunchKernelGGL(ch::k_zero_ports, dim3((np + 255) / 256), dim3(256), 0, s, np,
                             (1u << P_LEFT) | (1u << P_RIGHT), e->port_sum.as<unsigned long long>(),
@@ -2757,7 +2798,7 @@ static int run_finish_impl(gnoc_engine* e, const void* recv_buf)
       rc = chain_phase(e, 1);
       if (!rc) rc = run_levels_v3(e, L - 1, L);
       if (!rc) rc = run_post(e, false);
-      if (rc == GNOC_CH_EXC) rc = GNOC_CH_FALLBACK;   // (no exception merge on the sharded path)
+      if (rc == GNOC_CH_EXC || rc == GNOC_CH_YFALL) rc = GNOC_CH_FALLBACK;   // (the sharded path's own Y fallback below)
       // the windows of the next run: from this run's measured fill, or shorter
       // for the chains that overflowed (results never depend on them)
       if (!rc && !e->ch_resized) adapt_windows(e);
@@ -2767,7 +2808,7 @@ static int run_finish_impl(gnoc_engine* e, const void* recv_buf)
       // the Y chains declined: Y and SELF levels on k_level (fresh look-back state)
       e->n_fallback++;
       e->used_chain = 0;
-      GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, 0, 4, s));
+      GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, 0, 8, s));
       const uint32_t np = e->dc.N * PORTS;
       hipLaunchKernelGGL(ch::k_zero_ports, dim3((np + 255) / 256), dim3(256), 0, s, np,
                          (1u << P_UP) | (1u << P_DOWN) | (1u << P_SELF), e->port_sum.as<unsigned long long>(),

@@ -1281,7 +1281,7 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
    const bool anyexc = XL || errflag[2] != 0;
    // the chain engine (chain.hip) declined this batch: its outputs are incomplete,
    // the host reruns the batch on the level engine
-   if (errflag[4] != 0) return;
+   if (errflag[4] != 0 || errflag[5] != 0) return;
    if (tid == 0) { sm.nx.ready = 0; sm.qdone = 0; }
 #if LV_GEN
    if (tid == 0) sm.fq = c.f;

@@ -151,7 +151,9 @@ typedef struct gnoc_summary
    uint64_t mg1_uses;           /* requests served by the M/G/1 fallback                */
    uint32_t levels;             /* dependency levels executed                           */
    uint32_t engine_path;        /* 0 whole-port streams, 1 chunked look-back, 2 closed form,
-                                   3 serial moving-average queues, 4 port chains in time windows */
+                                   3 serial moving-average queues, 4 port chains in time windows,
+                                   5 port chains for the X phase, chunked look-back for the Y phase
+                                   (the batch's Y chains declined, e.g. an M/G/1 request there) */
    double   last_run_ms;        /* device time of the last gnoc_run (HIP events)        */
    /* How the last gnoc_run got there.  Every rerun is exact; these count the
       cost.  retries: chain-engine reruns with windows half as long (a window

@@ -1,7 +1,9 @@
 """Exception tails of the injection level merged into order before the chains
 (chain.hip k_exc_merge): a batch whose injection queues serve cycle-0 bursts by
 M/G/1 (the history tree's analytical branch, queue_model_history_tree.cc:58-64)
-stays on the chain engine, bit-exact against the oracle."""
+stays on the chain engine, bit-exact against the oracle.  A batch whose M/G/1
+requests reach only Y-direction ports keeps its X phase on the chains and runs
+the Y and SELF levels on k_level (engine path 5)."""
 import numpy as np
 import pytest
 
@@ -98,3 +100,38 @@ def test_saturated_mg1_matches_either_path():
     got = eng.results()
     eng.close()
     same(got, oracle.run(cfg, tr))
+
+
+def column_burst_trace(W, H, ax, ay, k, seed, tail=3000):
+    """Tile (ax, ay) injects k packets at cycle 0, all to tiles of its own column (they
+    turn UP / DOWN at the source router: the injection queue and the source's Y ports
+    back up, its X ports see nothing of the burst); random traffic from cycle 500."""
+    rng = np.random.default_rng(seed)
+    a = ay * W + ax
+    ys = [y for y in range(H) if y != ay]
+    d0 = np.array([rng.choice(ys) * W + ax for _ in range(k)], np.uint32)
+    t1 = np.sort(rng.integers(500, 5000, tail)).astype(np.uint64) * np.uint64(1000)
+    t = np.concatenate([np.zeros(k, np.uint64), t1])
+    src = np.concatenate([np.full(k, a, np.uint32), rng.integers(0, W * H, tail).astype(np.uint32)])
+    dst = np.concatenate([d0, rng.integers(0, W * H, tail).astype(np.uint32)])
+    return gnoc.Trace(t, src, dst, np.full(t.size, 576, np.uint32), np.zeros(t.size, np.uint32))
+
+
+@pytest.mark.parametrize("W,ax,ay,k", [(8, 3, 4, 14), (8, 6, 1, 20), (16, 9, 8, 24)])
+def test_y_only_mg1_keeps_x_on_chain(W, ax, ay, k):
+    cfg = gnoc.EngineConfig(num_tiles=W * W)
+    tr = column_burst_trace(W, W, ax, ay, k, seed=W * 7 + k)
+    ref = oracle.run(cfg, tr)
+    mg = ref.port_mg1.reshape(-1, 6)
+    assert mg[:, [3, 4]].sum() > 0                       # M/G/1 in DOWN / UP ports
+    assert mg[:, [1, 2]].sum() == 0                      # none in LEFT / RIGHT
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    for r in range(3):
+        eng.run()
+        got = eng.results()
+        same(got, ref)
+        s = got.summary
+        assert s["engine_path"] == 5, s
+        assert s["fallbacks"] == (1 if r == 0 else 0), s
+    eng.close()
