@@ -583,25 +583,33 @@ __global__ __launch_bounds__(512) void k_scatter4(uint64_t n, uint32_t pch, uint
       }
       return;
    }
-   // software pipeline: loads of the next 64 packets issued before placing these
-   uint64_t i = lo + lane;
-   bool nv = false;
-   uint32_t ns = 0, na = 0;
-   uint64_t nt = 0;
-   if (i < hi) { nv = (routed[i] & 2) != 0; ns = src[i] - s0; }
-   if (nv) { nt = inj[i]; na = aux[i]; }   // a sharded rank places only its row band's packets
-   for (uint64_t k = lo; k < hi; k += 64)
+   // software pipeline SC_D groups of 64 packets deep: group g + SC_D's loads are
+   // issued (all four fields, none waiting on another) before group g is placed,
+   // so a wave keeps several KB of loads in flight instead of waiting on each group
+   constexpr int SC_D = 4;
+   uint32_t pr[SC_D], ps[SC_D], pa[SC_D];
+   uint64_t pt[SC_D];
+#pragma unroll
+   for (int d = 0; d < SC_D; d++)
    {
-      const bool valid = nv;
-      const uint32_t sidx = ns;
-      const uint64_t t = nt;
-      const uint32_t a = na;
+      const uint64_t i = lo + (uint64_t) d * 64 + lane;
+      pr[d] = 0; ps[d] = 0; pa[d] = 0; pt[d] = 0;
+      if (i < hi) { pr[d] = routed[i]; ps[d] = src[i]; pt[d] = inj[i]; pa[d] = aux[i]; }
+   }
+   for (uint64_t k0 = lo; k0 < hi; k0 += 64 * SC_D)
+#pragma unroll
+   for (int d = 0; d < SC_D; d++)
+   {
+      const uint64_t k = k0 + (uint64_t) d * 64;
+      if (k >= hi) break;
+      const bool valid = (pr[d] & 2) != 0;   // a sharded rank places only its row band's packets
+      const uint32_t sidx = valid ? ps[d] - s0 : 0u;
+      const uint64_t t = pt[d];
+      const uint32_t a = pa[d];
       const uint64_t id = k + lane;
-      const uint64_t i2 = k + 64 + lane;
-      nv = false;
-      if (i2 < hi) { nv = (routed[i2] & 2) != 0; ns = src[i2] - s0; }
-      if (nv) { nt = inj[i2]; na = aux[i2]; }
-      if (!nv) ns = 0;
+      const uint64_t i2 = k + 64 * SC_D + lane;
+      pr[d] = 0; ps[d] = 0; pa[d] = 0; pt[d] = 0;
+      if (i2 < hi) { pr[d] = routed[i2]; ps[d] = src[i2]; pt[d] = inj[i2]; pa[d] = aux[i2]; }
       const uint64_t m = match_mask(sidx, valid, nbits);
       const uint32_t old = valid ? hw[sidx] : 0u;
       __builtin_amdgcn_wave_barrier();
