@@ -101,30 +101,16 @@ def main():
     native = sharded and backend == "nccl" and os.environ.get("GNOC_BENCH_NATIVE", "1") != "0"
     comm = None
     if native:
-        # one trial step on the native path; if it raises on any rank (gnoc_run_sharded
-        # max-reduces its status, so a failing rank fails every rank instead of
-        # leaving one inside the exchange), every rank takes the torch-driven exchange
-        ok = 1
+        # the native path or nothing: a failure on any rank (gnoc_run_sharded max-reduces
+        # its status, so a failing rank fails every rank instead of leaving one inside the
+        # exchange) ends the bench with exit code 4 -- no silent switch to another exchange
+        # (GNOC_BENCH_NATIVE=0 selects the torch-driven one explicitly)
         try:
             comm = gnoc.RcclComm(world, rank, local)
             eng = gnoc.NativeShardedEngine(cfg, rank, world, comm)
-            eng.submit(tr)
-            eng.run()
-        except Exception as ex:   # noqa: BLE001 -- reported, then the other path
-            print(f"bench: rank {rank}: native RCCL path failed ({ex}); using the torch exchange", file=sys.stderr)
-            ok = 0
-        flag = torch.tensor([ok], dtype=torch.int32, device="cuda")
-        if world > 1:
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if not int(flag.item()):
-            native = False
-            for x in (locals().get("eng"), comm):
-                try:
-                    if x is not None:
-                        x.close()
-                except Exception:   # noqa: BLE001
-                    pass
-            comm = None
+        except Exception as ex:   # noqa: BLE001 -- reported, then exit
+            print(f"bench: rank {rank}: native RCCL path failed: {ex}", file=sys.stderr, flush=True)
+            sys.exit(4)
     if not native:
         eng = gnoc.ShardedEngine(cfg, rank, world) if sharded else gnoc.Engine(cfg)
     eng.submit(tr)          # trace now resident in HBM; steps start from there
@@ -228,6 +214,7 @@ def main():
         hot_line = {"workload": f"emesh_hop_by_hop {W}x{H} hotspot(0.2, 16 tiles) load={load} pkts/tile={a.ppt}",
                     "value": hh * a.steps / mh["elapsed"], "ms_per_step": mh["elapsed"] / a.steps * 1e3,
                     "mesh_hops": hh, "engine_path": int(mh["summary"].get("engine_path", -1)),
+                    "chain_protocol": chain_protocol(mh["summary"]),
                     "reruns": mh["reruns"], "roofline_frac": rfh["frac"], "kernel": rfh["kernel"],
                     "kernel_avg_us": rfh["kernel_avg_us"], "kernel_ms": {k: round(v[0], 4) for k, v in mh["kst"].items()}}
 
@@ -261,6 +248,7 @@ def main():
                 "engine_path": int(summ.get("engine_path", -1)),
                 "windows": [int(summ.get("windows", 0)), int(summ.get("windows_y", 0))],
                 "window_ps": [int(summ.get("window_ps_x", 0)), int(summ.get("window_ps_y", 0))],
+                "chain_protocol": chain_protocol(summ),
             },
             # every rerun is exact but slow: counted over the timed steps (gnoc_summary's
             # totals since submit), and the bench refuses a configs[1] number that needed one
@@ -351,6 +339,16 @@ def measure(eng, a, barrier_sync, settle_fixed=False):
     kst = eng.kernel_stats()
     eng.set_profiling(False)
     return {"elapsed": elapsed, "summary": s1, "kst": kst, "reruns": reruns, "settle_runs": settle}
+
+
+def chain_protocol(summ):
+    """The hand-off protocol each chain phase ran (gnoc_summary.chain_protocol): the
+    engine keeps the serial one unless look-back measured > 5 % faster."""
+    v = int(summ.get("chain_protocol", 0))
+    if not v & 0x100:
+        return None
+    return {"x": "lookback" if v & 1 else "serial", "y": "lookback" if v & 2 else "serial",
+            "launch": "fused x+y" if v & 0x200 else "x, y"}
 
 
 def roofline(kst, pc, summ, my_pkts):

@@ -90,7 +90,7 @@ constexpr uint32_t F_TIMEOUT = 8u;        // a hand-off wait timed out
 constexpr uint32_t F_ANY = F_RETRY | F_FALLBACK | F_ROUTE | F_TIMEOUT;
 // why a chain run declined (bits above F_ANY; reported with GNOC_CHAIN_DEBUG=1)
 enum : uint32_t { R_OFFSET = 1u << 8, R_TAIL = 1u << 9, R_SPILLIN = 1u << 10, R_LASTSPILL = 1u << 11, R_MG1 = 1u << 12,
-                  R_EXC = 1u << 13, R_OVF_INS = 1u << 14, R_OVF_STREAM = 1u << 15 };
+                  R_EXC = 1u << 13, R_OVF_INS = 1u << 14, R_OVF_STREAM = 1u << 15, R_XDONE = 1u << 17 };
 constexpr uint64_t SPIN_CYCLES = 1ull << 31;
 constexpr uint64_t M48 = (1ull << 48) - 1;
 constexpr uint64_t OFF_LIM = (1ull << 32) - 4096;   // time offsets within a window (32-bit cycle math)
@@ -172,6 +172,13 @@ struct ChainArgs
    uint64_t* stamps;              // debug (GNOC_STAMPS=1): [(task * len + i) * 16 + k] phase stamps, else null
    uint32_t lookback;             // 1: look-back over earlier windows' AGG / INC; 0: wait for window w-1's INC
    uint32_t fw;                   // this phase's flag word: errflag[4] (X) or errflag[5] (Y)
+   // the fused launch (k_chain_xy: X and Y tasks in one persistent grid)
+   uint32_t fw2;                  // flags are mirrored here too (X: Y's word, so Y tasks see an X decline)
+   uint32_t nx_tasks;             // X tasks of the launch
+   uint64_t* xdone;               // [nx_tasks] epoch tag once X task (in key order) has drained its outputs
+   unsigned* xprefix;             // leading X tasks known done (advanced by the Y tasks that wait on it)
+   const ChainWin* xcw;           // Y tasks: the X phase's windows ...
+   const uint64_t* xst;           // ... and hand-off state (the producer ports' cumulative route counts)
 };
 
 
@@ -276,7 +283,11 @@ __device__ __forceinline__ uint32_t lb(const uint64_t* a, uint32_t n, uint64_t k
    return pos;
 }
 
-__device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f) { atomicOr(a.errflag + a.fw, f); }
+__device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f)
+{
+   atomicOr(a.errflag + a.fw, f);
+   if (a.fw2 != a.fw) atomicOr(a.errflag + a.fw2, f);
+}
 // A window of chain c overflowed LDS: the run retries, halving that chain's windows.
 __device__ __forceinline__ void flag_overflow(const ChainArgs& a, uint32_t c)
 {
@@ -296,19 +307,38 @@ __device__ __forceinline__ void ld_flag(const ChainArgs& a, uint32_t lane, uint3
 }
 __device__ __forceinline__ bool aborted(uint32_t ef) { return (rdl(ef, (int) FL) & F_ANY) != 0; }
 
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t l)
+{
+   return (uint32_t) __builtin_amdgcn_ds_bpermute((int) (l << 2), (int) v);
+}
+
 // Port descriptor fields (lanes 0-31 of a "pd" register) and the port's insert
 // bounds of window w (lanes 32 + j: first record of list j, 32 + nl + j: end).
+// A Y task of the fused launch (FU) takes its IN_W / IN_E bounds from the search
+// it ran at its start (y_bounds: list 2 i + j - 1 packed lo | (hi - lo) << 24 in
+// lane L % 64 of bnd[L / 64]), the IN_LOCAL bounds from k_win_bounds.
 enum : int { PD_OBASE = 0, PD_OCAP = 4, PD_IBASE = 8, PD_ICNT = 11, PD_PORT = 14, PD_NX = 15, PD_NY = 16, PD_RL = 17,
              PD_LO = 32 };
-template <int NL>
+template <int NL, bool FU>
 __device__ __forceinline__ uint32_t load_pd(const ChainArgs& a, uint32_t cpi, uint64_t bt_off, uint32_t nW, uint32_t i,
-                                            uint32_t w)
+                                            uint32_t w, uint32_t bnd0 = 0u, uint32_t bnd1 = 0u)
 {
    const uint32_t lane = threadIdx.x;
+   uint32_t fb = 0;
+   if (FU && NL == 3)
+   {
+      // (every lane takes part in the permutes)
+      const uint32_t l = lane - 32u, j = l < 3u ? l : l - 3u;
+      const uint32_t L = 2u * i + (j ? j - 1u : 0u);
+      const uint32_t v0 = bperm(bnd0, L & 63u), v1 = bperm(bnd1, L & 63u);
+      const uint32_t v = L < 64u ? v0 : v1;
+      fb = (v & 0xFFFFFFu) + (l < 3u ? 0u : v >> 24);
+   }
    if (lane < 32) return reinterpret_cast<const uint32_t*>(a.cp + cpi)[lane];
    const uint32_t l = lane - 32;
    if (l >= 2u * NL) return 0u;
    const uint32_t j = l < (uint32_t) NL ? l : l - NL;
+   if (FU && NL == 3 && j) return fb;
    return a.bt[bt_off + ((uint64_t) i * NL + j) * (nW + 1) + w + (l < (uint32_t) NL ? 0u : 1u)];
 }
 
@@ -337,7 +367,9 @@ __device__ __forceinline__ Ins<NL> ins_lists(uint32_t pd)
    return L;
 }
 // Issue the loads of a port's inserts of this window (registers); returns their count.
-template <int NL>
+// A fused launch's Y task reads the IN_W / IN_E lists, written in this launch by X
+// tasks with write-through stores, with sc1 loads (MI355X_MICROARCH.md "Valid forms").
+template <int NL, bool FU>
 __device__ __forceinline__ uint32_t fetch_inserts(const ChainArgs& a, uint32_t pd, Rec (&iv)[IROWS])
 {
    const uint32_t lane = threadIdx.x;
@@ -356,16 +388,31 @@ __device__ __forceinline__ uint32_t fetch_inserts(const ChainArgs& a, uint32_t p
 #pragma unroll
          for (int l = 1; l < NL; l++)
             if (g >= L.off[l]) j = (uint32_t) l;
-         iv[q] = a.recs[(uint64_t) L.base[j] + (g - L.off[j])];
+         const uint64_t ri = (uint64_t) L.base[j] + (g - L.off[j]);
+         if (FU && NL == 3 && j)
+         {
+            const uint64_t* r = reinterpret_cast<const uint64_t*>(a.recs + ri);
+            const uint64_t t = ld1(r), ia = ld1(r + 1);
+            iv[q].t = t;
+            iv[q].id = (uint32_t) ia;
+            iv[q].aux = (uint32_t) (ia >> 32);
+         }
+         else
+            iv[q] = a.recs[ri];
       }
    }
    return itot;
 }
 
 // Fetched inserts (itot <= ICAP) into the insert region as keys relative to
-// wbase.  Y ports' three lists land concatenated and are then merged in place
-// (own index + lower bounds in the other two lists).  True if a time offset
-// leaves the window's 32-bit range.
+// wbase.  Y ports' three lists land concatenated and are then merged in place:
+// an insert's merged position is the number of inserts whose key is below its own
+// (keys (t, id) are unique at a port).  The region is small (~30 keys a step), and
+// every lane reads the same key in each iteration of the count (an LDS broadcast),
+// so the reads pipeline -- a binary search into each other list was a chain of
+// dependent LDS reads (6.4 K cycles a Y step against 1.3 K for an X step's landing,
+// profiles/r3_chain_stamps_occupancy.txt).  True if a time offset leaves the
+// window's 32-bit range.
 template <int NL>
 __device__ __forceinline__ bool land_inserts(Smem& sm, const Rec (&iv)[IROWS], uint32_t itot, uint64_t wbase, uint32_t pd)
 {
@@ -387,22 +434,24 @@ __device__ __forceinline__ bool land_inserts(Smem& sm, const Rec (&iv)[IROWS], u
    }
    if (NL > 1)
    {
-      const Ins<NL> L = ins_lists<NL>(pd);
+      (void) pd;
       wsync();
-      uint32_t pos[IROWS];
-#pragma unroll
-      for (int q = 0; q < IROWS; q++)
+      uint32_t pos[IROWS] = {};
+      static_assert(IROWS == 2, "the count below handles two rows");
+      if (itot <= (uint32_t) T)
       {
-         const uint32_t g = lane + (uint32_t) q * T;
-         uint32_t own = 0;
-#pragma unroll
-         for (int l = 1; l < NL; l++)
-            if (g >= L.off[l]) own = (uint32_t) l;
-         uint32_t p = g - L.off[own];
-#pragma unroll
-         for (int l = 0; l < NL; l++)
-            if ((uint32_t) l != own) p += lb(sm.key + CAP + L.off[l], L.off[l + 1] - L.off[l], k[q]);
-         pos[q] = p;
+#pragma unroll 4
+         for (uint32_t m = 0; m < itot; m++) pos[0] += sm.key[CAP + m] < k[0] ? 1u : 0u;
+      }
+      else
+      {
+#pragma unroll 4
+         for (uint32_t m = 0; m < itot; m++)
+         {
+            const uint64_t x = sm.key[CAP + m];
+            pos[0] += x < k[0] ? 1u : 0u;
+            pos[1] += x < k[1] ? 1u : 0u;
+         }
       }
       // every lane's searches precede every write (one wave: LDS in program order)
       wsync();
@@ -475,10 +524,6 @@ __device__ __forceinline__ void load_rows(Smem& sm, uint32_t nK, uint32_t IB, ui
 
 // Per-field tables: lane 1 + q holds route field q (SELF, cont, UP, DOWN), the
 // lanes of the state words that carry the route counts.
-__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t l)
-{
-   return (uint32_t) __builtin_amdgcn_ds_bpermute((int) (l << 2), (int) v);
-}
 // Lane 1 + q of a row's packed field counts (8 bits per field).
 __device__ __forceinline__ uint32_t field_cnt(uint32_t R, uint32_t lane)
 {
@@ -544,6 +589,120 @@ __device__ __forceinline__ void out_record(gptr<Rec> recs, gptr<uint64_t> samp_t
 
 
 
+
+// ---------------------------------------------------------------------------
+// the fused launch (k_chain_xy): a Y task's dependence on the launch's X tasks
+// ---------------------------------------------------------------------------
+// Wait until the first `need` X tasks in key order (every X task whose window starts
+// before this Y window ends: only those can emit a turn record with t below its
+// end) have drained their outputs.  The waiting tasks advance the shared prefix over
+// the per-task done granules, 64 at a time.  False on abort.
+__device__ bool wait_x_prefix(const ChainArgs& a, uint32_t need, uint32_t lane)
+{
+   const uint64_t t0 = __builtin_amdgcn_s_memtime();
+   uint32_t ef = 0;
+   for (;;)
+   {
+      uint32_t P = 0;
+      if (lane == 0) P = __hip_atomic_load(a.xprefix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      P = rdl(P, 0);
+      if (P >= need) return true;
+      uint64_t d = 0;
+      if (P + lane < a.nx_tasks) d = ld1(a.xdone + P + lane);
+      ld_flag(a, lane, ef);
+      const uint64_t m = __ballot(P + lane < a.nx_tasks && d == a.etag);
+      const uint32_t run = m == ~0ull ? 64u : (uint32_t) __builtin_ctzll(~m);
+      if (run)
+      {
+         if (lane == 0) atomicMax(a.xprefix, P + run);
+         continue;
+      }
+      if (aborted(ef)) return false;
+      if (__builtin_amdgcn_s_memtime() - t0 > SPIN_CYCLES)
+      {
+         if (lane == 0) flag(a, F_TIMEOUT);
+         return false;
+      }
+      __builtin_amdgcn_s_sleep(2);
+   }
+}
+
+// The IN_W / IN_E insert bounds of every port of Y chain c in window w ([w D, (w+1) D),
+// the last one unbounded), once wait_x_prefix has returned: list L = 2 p + j - 1 (port
+// p, side IN_W / IN_E) in lane L % 64 of bnd[L / 64], packed lo | (hi - lo) << 24.  The
+// slot's producer is an X port (RIGHT of (x-1, y) / LEFT of (x+1, y)); its cumulative
+// count K of this field after its window that holds (w+1) D - 1 is an INC granule, and
+// the slot's first K records (FIFO departures: sorted by t) are every record with
+// t < (w+1) D plus a few later ones.  lo / hi = K minus the records at the end of
+// [0, K) with t >= w D / t >= (w+1) D, counted backwards 8 loads at a time.  False
+// when a granule is missing or a bound leaves the packed range.
+__device__ bool y_bounds(const ChainArgs& a, uint32_t c, uint32_t w, uint64_t D, uint32_t nW, uint32_t& bnd0,
+                         uint32_t& bnd1)
+{
+   const uint32_t lane = threadIdx.x, len = a.len, W = a.c.W, H = a.c.H;
+   const uint32_t x = c / 2u;                  // (fused launches are unsharded: column band = all)
+   const bool up = (c & 1u) == 0u;
+   const bool lastw = w + 1 >= nW;
+   const uint64_t Tlo = (uint64_t) w * D, Thi = lastw ? ~0ull : (uint64_t) (w + 1) * D;
+   const uint64_t Tstop = w ? Tlo : Thi;       // window 0: lo = 0, the scan looks for hi only
+   const uint32_t field = up ? 2u : 3u;
+   bool bad = false;
+   uint32_t out[2] = { 0u, 0u };
+#pragma unroll
+   for (int r = 0; r < 2; r++)
+   {
+      if (64u * (uint32_t) r >= 2u * len) break;
+      const uint32_t L = lane + 64u * (uint32_t) r;
+      const uint32_t p = L >> 1, j = 1u + (L & 1u);
+      const bool act = p < len && (j == 1u ? x > 0u : x + 1u < W);
+      uint32_t K = 0, base = 0;
+      if (act)
+      {
+         const uint32_t y = up ? p : H - 1u - p;
+         const uint32_t xc = 2u * y + (j == 2u ? 1u : 0u);
+         const uint32_t xp = j == 1u ? x - 1u : W - 2u - x;
+         const ChainWin cw = a.xcw[xc];
+         uint32_t wr = cw.nW - 1u;
+         if (!lastw)
+         {
+            const uint64_t q = (Thi - 1) / cw.D;
+            if (q < wr) wr = (uint32_t) q;
+         }
+         const uint64_t g = ld1(a.xst + cw.st_off + ((uint64_t) xp * cw.nW + wr) * SW + G_CNT + field);
+         bad |= (g & ~M48) != a.etag || (g & M48) >= (1ull << 24);
+         K = (uint32_t) (g & M48);
+         base = a.cp[c * len + p].ibase[j];
+      }
+      uint32_t clo = 0, chi = 0, pos = K;
+      bool scan = act && !(w == 0 && lastw);
+      while (__any(scan))
+      {
+         uint64_t tq[8];
+#pragma unroll
+         for (int q = 0; q < 8; q++)
+            tq[q] = scan && pos > (uint32_t) q ? ld1(reinterpret_cast<const uint64_t*>(a.recs + base + pos - 1 - q)) : 0ull;
+#pragma unroll
+         for (int q = 0; q < 8; q++)
+         {
+            if (scan && pos > (uint32_t) q && tq[q] >= Tstop)
+            {
+               clo += tq[q] >= Tlo ? 1u : 0u;
+               chi += tq[q] >= Thi ? 1u : 0u;
+            }
+            else
+               scan = false;
+         }
+         pos = pos >= 8u ? pos - 8u : 0u;
+      }
+      const uint32_t lo = w ? K - clo : 0u, hi = K - chi;
+      bad |= act && lo >= (1u << 24);
+      out[r] = lo | (min(hi - lo, 255u) << 24);
+   }
+   bnd0 = out[0];
+   bnd1 = out[1];
+   return !__any(bad);
+}
+
 // ---------------------------------------------------------------------------
 // one task: chain c, window w (one wave)
 // ---------------------------------------------------------------------------
@@ -601,8 +760,8 @@ __device__ __forceinline__ uint64_t state_word_ser(uint32_t lane, uint64_t Xo, u
    if (lane == 7) v = Pend;
    return v;
 }
-template <int NL, bool F1>
-__device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
+template <int NL, bool F1, bool FU>
+__device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk, uint32_t aux)
 {
    constexpr bool XC = NL == 1;
    const uint32_t lane = threadIdx.x;
@@ -629,21 +788,38 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
    const uint32_t cpb = c * len;
    const uint32_t mode0 = a.c.analytical ? 1u : 0u;
    const gptr<Rec> recs = sptr(a.recs);
+   // fused launch, Y task: the X tasks it depends on are done; its IN_W / IN_E bounds
+   uint32_t bnd0 = 0, bnd1 = 0;
+#ifdef CH_STAMPS
+   if (a.stamps && lane == 0) a.stamps[(uint64_t) tk * len * 16 + 10] = __builtin_amdgcn_s_memrealtime();
+#endif
+   if (FU && NL == 3)
+   {
+      if (!wait_x_prefix(a, aux, lane)) return;
+#ifdef CH_STAMPS
+      if (a.stamps && lane == 0) a.stamps[(uint64_t) tk * len * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+#endif
+      if (!y_bounds(a, c, w, D, nW, bnd0, bnd1))
+      {
+         if (lane == 0) flag(a, F_FALLBACK | R_XDONE);
+         return;
+      }
+   }
 
    // ---- prologue: descriptors of ports 0..2 (with their insert bounds), port 0's
    // inserts landed, port 1's in flight
-   uint32_t pd0 = load_pd<NL>(a, cpb, bt_off, nW, 0, w);
-   uint32_t pd1 = len > 1 ? load_pd<NL>(a, cpb + 1, bt_off, nW, 1, w) : 0u;
-   uint32_t pd2 = len > 2 ? load_pd<NL>(a, cpb + 2, bt_off, nW, 2, w) : 0u;
+   uint32_t pd0 = load_pd<NL, FU>(a, cpb, bt_off, nW, 0, w, bnd0, bnd1);
+   uint32_t pd1 = len > 1 ? load_pd<NL, FU>(a, cpb + 1, bt_off, nW, 1, w, bnd0, bnd1) : 0u;
+   uint32_t pd2 = len > 2 ? load_pd<NL, FU>(a, cpb + 2, bt_off, nW, 2, w, bnd0, bnd1) : 0u;
    Rec iv[IROWS];
-   uint32_t nI = fetch_inserts<NL>(a, pd0, iv);
+   uint32_t nI = fetch_inserts<NL, FU>(a, pd0, iv);
    if (nI > (uint32_t) ICAP)
    {
       if (lane == 0) flag_overflow(a, c);
       return;
    }
    if (land_inserts<NL>(sm, iv, nI, wbase, pd0) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
-   uint32_t itot_f = len > 1 ? fetch_inserts<NL>(a, pd1, iv) : 0u;   // port 1's inserts, landed in step 0
+   uint32_t itot_f = len > 1 ? fetch_inserts<NL, FU>(a, pd1, iv) : 0u;   // port 1's inserts, landed in step 0
 
    uint64_t rk[ROWS];
    uint32_t ra[ROWS];
@@ -940,8 +1116,8 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
       nI = itot;
       // ---- next prefetches: port i+2's inserts (its descriptor landed a step ago), port
       // i+3's descriptor and bounds; the ring moves on
-      if (i + 2 < len) itot_f = fetch_inserts<NL>(a, pd2, iv);
-      const uint32_t pdn = i + 3 < len ? load_pd<NL>(a, cpb + i + 3, bt_off, nW, i + 3, w) : 0u;
+      if (i + 2 < len) itot_f = fetch_inserts<NL, FU>(a, pd2, iv);
+      const uint32_t pdn = i + 3 < len ? load_pd<NL, FU>(a, cpb + i + 3, bt_off, nW, i + 3, w, bnd0, bnd1) : 0u;
       pd0 = pd1;
       pd1 = pd2;
       pd2 = pdn;
@@ -951,14 +1127,21 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
       atomicMax(a.nmax + 2 * c, nmax);
       atomicMax(a.nmax + 2 * c + 1, imax);
    }
+   if (FU && NL == 1)
+   {
+      // fused launch: every output of this X task has landed (write-through stores);
+      // its done granule lets the Y tasks that wait on it read them (sc1 loads)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) st1(a.xdone + aux, a.etag);
+   }
 }
 
 
 // ---------------------------------------------------------------------------
 // one task, look-back protocol (AGG / INC / KO / POST granules)
 // ---------------------------------------------------------------------------
-template <int NL, bool F1>
-__device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
+template <int NL, bool F1, bool FU>
+__device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk, uint32_t aux)
 {
    constexpr bool XC = NL == 1;
    const uint32_t lane = threadIdx.x;
@@ -985,21 +1168,38 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
    const uint32_t cpb = c * len;
    const uint32_t mode0 = a.c.analytical ? 1u : 0u;
    const gptr<Rec> recs = sptr(a.recs);
+   // fused launch, Y task: the X tasks it depends on are done; its IN_W / IN_E bounds
+   uint32_t bnd0 = 0, bnd1 = 0;
+#ifdef CH_STAMPS
+   if (a.stamps && lane == 0) a.stamps[(uint64_t) tk * len * 16 + 10] = __builtin_amdgcn_s_memrealtime();
+#endif
+   if (FU && NL == 3)
+   {
+      if (!wait_x_prefix(a, aux, lane)) return;
+#ifdef CH_STAMPS
+      if (a.stamps && lane == 0) a.stamps[(uint64_t) tk * len * 16 + 11] = __builtin_amdgcn_s_memrealtime();
+#endif
+      if (!y_bounds(a, c, w, D, nW, bnd0, bnd1))
+      {
+         if (lane == 0) flag(a, F_FALLBACK | R_XDONE);
+         return;
+      }
+   }
 
    // ---- prologue: descriptors of ports 0..2 (with their insert bounds), port 0's
    // inserts landed, port 1's in flight
-   uint32_t pd0 = load_pd<NL>(a, cpb, bt_off, nW, 0, w);
-   uint32_t pd1 = len > 1 ? load_pd<NL>(a, cpb + 1, bt_off, nW, 1, w) : 0u;
-   uint32_t pd2 = len > 2 ? load_pd<NL>(a, cpb + 2, bt_off, nW, 2, w) : 0u;
+   uint32_t pd0 = load_pd<NL, FU>(a, cpb, bt_off, nW, 0, w, bnd0, bnd1);
+   uint32_t pd1 = len > 1 ? load_pd<NL, FU>(a, cpb + 1, bt_off, nW, 1, w, bnd0, bnd1) : 0u;
+   uint32_t pd2 = len > 2 ? load_pd<NL, FU>(a, cpb + 2, bt_off, nW, 2, w, bnd0, bnd1) : 0u;
    Rec iv[IROWS];
-   uint32_t nI = fetch_inserts<NL>(a, pd0, iv);
+   uint32_t nI = fetch_inserts<NL, FU>(a, pd0, iv);
    if (nI > (uint32_t) ICAP)
    {
       if (lane == 0) flag_overflow(a, c);
       return;
    }
    if (land_inserts<NL>(sm, iv, nI, wbase, pd0) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
-   uint32_t itot_f = len > 1 ? fetch_inserts<NL>(a, pd1, iv) : 0u;   // port 1's inserts, landed in step 0
+   uint32_t itot_f = len > 1 ? fetch_inserts<NL, FU>(a, pd1, iv) : 0u;   // port 1's inserts, landed in step 0
 
    uint64_t rk[ROWS];
    uint32_t ra[ROWS];
@@ -1439,8 +1639,8 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
       nI = itot;
       // ---- next prefetches: port i+2's inserts (its descriptor landed a step ago), port
       // i+3's descriptor and bounds; the ring moves on
-      if (i + 2 < len) itot_f = fetch_inserts<NL>(a, pd2, iv);
-      const uint32_t pdn = i + 3 < len ? load_pd<NL>(a, cpb + i + 3, bt_off, nW, i + 3, w) : 0u;
+      if (i + 2 < len) itot_f = fetch_inserts<NL, FU>(a, pd2, iv);
+      const uint32_t pdn = i + 3 < len ? load_pd<NL, FU>(a, cpb + i + 3, bt_off, nW, i + 3, w, bnd0, bnd1) : 0u;
       pd0 = pd1;
       pd1 = pd2;
       pd2 = pdn;
@@ -1449,6 +1649,13 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
    {
       atomicMax(a.nmax + 2 * c, nmax);
       atomicMax(a.nmax + 2 * c + 1, imax);
+   }
+   if (FU && NL == 1)
+   {
+      // fused launch: every output of this X task has landed (write-through stores);
+      // its done granule lets the Y tasks that wait on it read them (sc1 loads)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) st1(a.xdone + aux, a.etag);
    }
 }
 
@@ -1475,8 +1682,58 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
       tk = rdl(tk, 0);
       if (tk >= ntasks || flagged(a)) return;
       const uint32_t cw = a.tasks[tk];
-      if (LB) task_lb<NL, F1>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
-      else task_ser<NL, F1>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
+      if (LB) task_lb<NL, F1, false>(sm, a, cw >> 16, cw & 0xFFFFu, tk, 0u);
+      else task_ser<NL, F1, false>(sm, a, cw >> 16, cw & 0xFFFFu, tk, 0u);
+      wsync();
+   }
+}
+
+// The X and Y phases in ONE persistent launch: the Y tasks fill the slots the X
+// phase's drain leaves empty.  One table in key order: X task (c, w) at its window's
+// start w D_c, Y task (c, w) at its window's end (w+1) D_c plus a lag (GNOC_XY_LAG),
+// so every X task a Y task waits for (wait_x_prefix) and its predecessor window are
+// handed out before it (no deadlock).  taux: an X task's rank in the X tasks' key
+// order (its done granule), a Y task's count of X tasks that must be done first.  An
+// X decline (mirrored into the Y flag word) stops every task; a Y decline only the
+// Y tasks (the X outputs stand: the host reruns the Y and SELF levels, path 5).
+struct XYArgs
+{
+   ChainArgs x, y;
+   const uint32_t* tasks;         // bit 31: Y task; bits 16-30 chain; bits 0-15 window
+   const uint32_t* taux;
+   uint32_t ntasks;
+};
+template <bool F1, bool XLB, bool YLB>
+__global__ __launch_bounds__(T, CH_MINW) void k_chain_xy(XYArgs xa)
+{
+   __shared__ Smem sm;
+   const ChainArgs& ax = xa.x;
+   const ChainArgs& ay = xa.y;
+   if (ax.errflag[2] != 0 && (!ax.excfix || (ax.errflag[2] & 2u)))
+   {
+      if (threadIdx.x == 0 && blockIdx.x == 0) flag(ax, F_FALLBACK | R_EXC);
+      return;
+   }
+   for (;;)
+   {
+      uint32_t tk = 0;
+      if (threadIdx.x == 0) tk = atomicAdd(ax.ctr, 1u);
+      tk = rdl(tk, 0);
+      if (tk >= xa.ntasks) return;
+      const uint32_t e = xa.tasks[tk], aux = xa.taux[tk];
+      const uint32_t c = (e >> 16) & 0x7FFFu, w = e & 0xFFFFu;
+      if (e >> 31)
+      {
+         if (flagged(ay)) continue;   // (X flags are mirrored into Y's word)
+         if (YLB) task_lb<3, F1, true>(sm, ay, c, w, tk, aux);
+         else task_ser<3, F1, true>(sm, ay, c, w, tk, aux);
+      }
+      else
+      {
+         if (flagged(ax)) return;
+         if (XLB) task_lb<1, F1, true>(sm, ax, c, w, tk, aux);
+         else task_ser<1, F1, true>(sm, ax, c, w, tk, aux);
+      }
       wsync();
    }
 }
@@ -1707,14 +1964,16 @@ __global__ __launch_bounds__(256) void k_chain_plan(DevCfg c, uint32_t ncpx, uin
    out[k] = p;
 }
 
-// One workgroup per (chain port, insert list): bt[w] = first record of the
-// slot with t >= w D (w < nW), bt[nW] = record count.  Window of t:
-// min(t / D, nW - 1) (the last window is unbounded).
+// One workgroup per (chain port, insert list j < nlrun): bt[w] = first record of
+// the slot with t >= w D (w < nW), bt[nW] = record count.  Window of t:
+// min(t / D, nW - 1) (the last window is unbounded).  The fused launch needs the
+// Y ports' IN_LOCAL lists only (nlrun = 1): their IN_W / IN_E slots are written in
+// that launch (y_bounds).
 __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict__ cp, uint32_t nl, uint32_t len,
                                                     const ChainWin* __restrict__ cw, const Rec* __restrict__ recs,
-                                                    uint32_t* __restrict__ bt)
+                                                    uint32_t* __restrict__ bt, uint32_t nlrun)
 {
-   const uint32_t k = blockIdx.x / nl, j = blockIdx.x % nl, c = k / len, i = k % len;
+   const uint32_t k = blockIdx.x / nlrun, j = blockIdx.x % nlrun, c = k / len, i = k % len;
    const uint64_t D = cw[c].D;
    const uint32_t nW = cw[c].nW;
    const uint64_t base = cp[k].ibase[j];

@@ -155,6 +155,9 @@ struct gnoc_engine
    // row band (sources) or column band (destinations), in trace order; gid maps
    // them to their global index, g2l back
    bool part = false;
+   int xself = 0;
+   int declined_once = 0;                   // test knob GNOC_DECLINE_ONCE_RANK: fired
+   bool fin_closed = false;                 // finish_enqueue: the closed form finished in run_begin                           // test knob GNOC_SHARD_SELF_EXCHANGE: own turn records through the transport
    size_t n_glob = 0;
    uint64_t h_glob_hops = 0, h_glob_routed = 0;
    std::vector<uint32_t> h_gid;
@@ -204,11 +207,17 @@ struct gnoc_engine
    uint64_t ch_st_words[2] = { 0, 0 }, ch_bt_words[2] = { 0, 0 };
    unsigned* h_nmax = nullptr;               // pinned: per chain fill maxima of the last run
    DevBuf ch_cw, ch_tasks, ch_nmax;
+   // the fused launch (k_chain_xy): one task table in key order (tasks, then their aux words)
+   std::vector<uint32_t> h_xy, h_xy_aux;
+   DevBuf ch_xy, ch_xdone;
+   int ch_fused = 0;                        // the last chain run was one fused launch
+   double xy_lag = -1.0;                    // Y task key lag, in units of the batch's last injection time
    uint32_t ch_epoch = 0;
    int ch_grid = 0;
    int force_levels = 0;
    int ch_declined = 0;                     // this batch fell back from the chain engine: later runs skip it
    int ch_ydeclined = 0;                    // only its Y phase did: later runs take X chains + Y levels (path 5)
+   unsigned ch_yflags = 0;                  // the Y phase's chain flags of the last run that declined
    int exc_fix = 0;                         // this batch's injection level leaves exception tails: k_exc_merge
    std::vector<std::pair<void*, uint64_t>> zq;   // buffers to zero before the first level launch (one k_zero_segs)
    int ch_resized = 0;                      // the windows were already changed during this (sharded) run
@@ -222,6 +231,9 @@ struct gnoc_engine
    uint32_t ch_lb_run[2] = { 0, 0 };
    float ch_lb_ms[2][2] = { { -1.f, -1.f }, { -1.f, -1.f } };
    std::vector<uint64_t> ch_lb_D[2];        // the windows those times belong to
+   std::vector<uint64_t> ch_prevD[2];       // the windows of the previous attempt
+   int ch_lb_dec[2] = { -1, -1 };           // the decision per phase (-1: none yet: serial)
+   int ch_trial = 0;                        // this run times a protocol (phases as separate launches)
    hipEvent_t ch_ev[2][2] = { { nullptr, nullptr }, { nullptr, nullptr } };
 
    // kernel profiling (gnoc_set_profiling)
@@ -457,7 +469,7 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    if (he == hipSuccess) he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
    if (he == hipSuccess) he = hipEventCreate(&e->ev0);
    if (he == hipSuccess) he = hipEventCreate(&e->ev1);
-   if (he == hipSuccess) he = hipHostMalloc((void**) &e->h_pinned, 128, hipHostMallocDefault);
+   if (he == hipSuccess) he = hipHostMalloc((void**) &e->h_pinned, 256, hipHostMallocDefault);
    // per chain fill maxima: 2 u32 for each of the <= 2 (W + H) chains
    if (he == hipSuccess)
       he = hipHostMalloc((void**) &e->h_nmax, 16 * ((size_t) e->dc.W + e->dc.H) + 64, hipHostMallocDefault);
@@ -631,6 +643,7 @@ static constexpr double CH_FILL = 0.45;     // first run: the steady-rate estima
 static constexpr double CH_TARGET = 0.95;    // adapted windows: the fullest step at 0.95 of capacity (0.9: 3.94 ms, 0.95: 3.81, 0.98: 3.89 on configs[1]; 1.0 declines the chains)
 static constexpr double CH_GROW = 1.6;       // most a chain's window grows per run
 static constexpr uint32_t CH_NW_MAX = 4096;
+static constexpr float CH_LB_MARGIN = 0.05f;  // look-back replaces the serial hand-off only when > 5% faster
 static constexpr uint64_t CH_D_MIN = 1024, CH_D_MAX = 1ull << 31;   // 32-bit time offsets in a window
 static uint32_t windows_of(uint64_t D, uint64_t t_last) { return (uint32_t) (t_last / D + 1); }
 static uint32_t chain_count(const gnoc_engine* e, int p)
@@ -656,6 +669,7 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
    const bool same = std::equal(key, key + 4, e->ch_key) && e->ch_on && !std::getenv("GNOC_WINDOW_SHIFT") &&
                      !std::getenv("GNOC_WINDOW_PS") && !std::getenv("GNOC_WINDOW_PS_X") && !std::getenv("GNOC_WINDOW_PS_Y");
    std::copy(key, key + 4, e->ch_key);
+   if (!same) e->ch_lb_dec[0] = e->ch_lb_dec[1] = -1;
    e->ch_declined = 0;
    e->ch_ydeclined = 0;
    e->exc_fix = 0;
@@ -773,6 +787,53 @@ static int chain_tables(gnoc_engine* e)
       e->ch_st_words[p] = st;
       e->ch_bt_words[p] = bt;
    }
+   {
+      // the fused table: X task (c, w) keyed by its window's start w D_c, Y task (c, w) by
+      // its window's end (w+1) D_c + lag; ties: X first.  aux: an X task's rank among the
+      // X tasks (its done granule), a Y task's count of X tasks keyed before its window's
+      // end (all must be done before it reads their turn records).
+      if (e->xy_lag < 0)
+      {
+         const char* lv = std::getenv("GNOC_XY_LAG");
+         e->xy_lag = lv && *lv ? std::atof(lv) : 0.1;
+      }
+      const uint64_t lag = (uint64_t) (e->xy_lag * (double) (e->h_tlast + 1));
+      std::vector<uint64_t> xkey;
+      xkey.reserve(e->h_tasks[0].size());
+      for (uint32_t t : e->h_tasks[0]) xkey.push_back((uint64_t) (t & 0xFFFFu) * e->h_cw[0][t >> 16].D);
+      std::vector<std::pair<uint64_t, uint32_t>> yk;
+      yk.reserve(e->h_tasks[1].size());
+      for (uint32_t t : e->h_tasks[1])
+      {
+         const ChainWin& w = e->h_cw[1][t >> 16];
+         const uint32_t wi = t & 0xFFFFu;
+         yk.push_back({ (uint64_t) (wi + 1) * w.D + lag, t });
+      }
+      std::stable_sort(yk.begin(), yk.end(), [](const std::pair<uint64_t, uint32_t>& x, const std::pair<uint64_t, uint32_t>& y) {
+         return x.first < y.first;
+      });
+      e->h_xy.clear();
+      e->h_xy_aux.clear();
+      size_t ix = 0;
+      for (size_t iy = 0; iy <= yk.size(); iy++)
+      {
+         const uint64_t ky = iy < yk.size() ? yk[iy].first : ~0ull;
+         for (; ix < xkey.size() && xkey[ix] <= ky; ix++)
+         {
+            e->h_xy.push_back(e->h_tasks[0][ix]);
+            e->h_xy_aux.push_back((uint32_t) ix);
+         }
+         if (iy == yk.size()) break;
+         const uint32_t t = yk[iy].second;
+         const ChainWin& w = e->h_cw[1][t >> 16];
+         const uint32_t wi = t & 0xFFFFu;
+         uint32_t need = (uint32_t) xkey.size();
+         if (wi + 1 < w.nW)
+            need = (uint32_t) (std::lower_bound(xkey.begin(), xkey.end(), (uint64_t) (wi + 1) * w.D) - xkey.begin());
+         e->h_xy.push_back(t | 0x80000000u);
+         e->h_xy_aux.push_back(need);
+      }
+   }
    const size_t ncw = e->h_cw[0].size() + e->h_cw[1].size(), nt = e->h_tasks[0].size() + e->h_tasks[1].size();
    GNOC_HIP(e, e->ch_cw.ensure(std::max<size_t>(ncw, 1) * sizeof(ChainWin)));
    GNOC_HIP(e, e->ch_tasks.ensure(std::max<size_t>(nt, 1) * 4));
@@ -781,6 +842,10 @@ static int chain_tables(gnoc_engine* e)
                          hipMemcpyHostToDevice));
    GNOC_HIP(e, hipMemcpy(e->ch_tasks.p, e->h_tasks[0].data(), e->h_tasks[0].size() * 4, hipMemcpyHostToDevice));
    GNOC_HIP(e, hipMemcpy(e->ch_tasks.as<uint32_t>() + e->h_tasks[0].size(), e->h_tasks[1].data(), e->h_tasks[1].size() * 4,
+                         hipMemcpyHostToDevice));
+   GNOC_HIP(e, e->ch_xy.ensure(std::max<size_t>(e->h_xy.size(), 1) * 8));
+   GNOC_HIP(e, hipMemcpy(e->ch_xy.p, e->h_xy.data(), e->h_xy.size() * 4, hipMemcpyHostToDevice));
+   GNOC_HIP(e, hipMemcpy(e->ch_xy.as<uint32_t>() + e->h_xy.size(), e->h_xy_aux.data(), e->h_xy_aux.size() * 4,
                          hipMemcpyHostToDevice));
    e->chD_up[0] = e->chD_run[0];
    e->chD_up[1] = e->chD_run[1];
@@ -830,7 +895,7 @@ static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t
             GNOC_HIP(e, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_validate<true>),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
          hipLaunchKernelGGL(k_validate<true>, dim3(nblk), dim3(256), lds, s, e->dc, (uint64_t) n, e->d_inj, e->d_src,
-                            e->d_dst, e->d_bits, e->d_flags, tree, sweep, nr, (uint32_t) e->rank, vo, dxr, ntab, part, xcnt);
+                            e->d_dst, e->d_bits, e->d_flags, tree, sweep, nr, (uint32_t) e->rank, (uint32_t) e->xself, vo, dxr, ntab, part, xcnt);
          GNOC_HIP(e, hipGetLastError());
          hipLaunchKernelGGL(k_validate_sum, dim3((ntab + 255) / 256), dim3(256), 0, s, ntab, nblk, part, dxr);
       }
@@ -838,7 +903,7 @@ static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t
       {
          const uint32_t grid = (uint32_t) std::min<uint64_t>((n + 255) / 256, 4096);
          hipLaunchKernelGGL(k_validate<false>, dim3(grid), dim3(256), 0, s, e->dc, (uint64_t) n, e->d_inj, e->d_src,
-                            e->d_dst, e->d_bits, e->d_flags, tree, sweep, nr, (uint32_t) e->rank, vo, dxr, ntab, part, xcnt);
+                            e->d_dst, e->d_bits, e->d_flags, tree, sweep, nr, (uint32_t) e->rank, (uint32_t) e->xself, vo, dxr, ntab, part, xcnt);
       }
       GNOC_HIP(e, hipGetLastError());
       hipLaunchKernelGGL(k_validate_max, dim3(1), dim3(1024), 0, s, W, H, dxr, dxl, dyu, dyd, insx, insy, vo);
@@ -846,7 +911,7 @@ static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t
    }
    GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, vo, sizeof(ValOut), hipMemcpyDeviceToHost, s));
    e->x_cnt.assign((size_t) nr * nr, 0);
-   if (nr > 1) GNOC_HIP(e, hipMemcpyAsync(e->x_cnt.data(), xcnt, (size_t) nr * nr * 8, hipMemcpyDeviceToHost, s));
+   if (nr > 1 || e->xself) GNOC_HIP(e, hipMemcpyAsync(e->x_cnt.data(), xcnt, (size_t) nr * nr * 8, hipMemcpyDeviceToHost, s));
    GNOC_HIP(e, hipStreamSynchronize(s));
    ValOut v;
    std::memcpy(&v, e->h_pinned, sizeof v);
@@ -888,11 +953,13 @@ static int build_exchange(gnoc_engine* e)
    e->xs_units.assign(nr, 0);
    e->xr_units.assign(nr, 0);
    e->xs_slots = e->xr_slots = 0;
-   if (nr <= 1 || !e->dc.contention) return GNOC_OK;
+   if ((nr <= 1 && !e->xself) || !e->dc.contention) return GNOC_OK;
    uint64_t su = 0, ru = 0;
    for (uint32_t q = 0; q < nr; q++)
    {
-      if (q == me) continue;
+      // a rank's own turn records stay in place, except under the self-exchange test
+      // knob, which sends them to itself (through the transport) and back into the slots
+      if (q == me && !e->xself) continue;
       for (int side = 0; side < 2; side++)
       {
          // side 0: my rows -> q's columns (send); side 1: q's rows -> my columns (receive)
@@ -904,7 +971,7 @@ static int build_exchange(gnoc_engine* e)
          p.ny = band_lo(rr + 1, nr, H) - p.y0;
          p.nslots = p.nx * p.ny * XS_PER_TILE;
          p.expect = e->x_cnt[(size_t) rr * nr + cc];
-         const uint64_t hdr = (p.nslots + 3) / 4;
+         const uint64_t hdr = 1 + (p.nslots + 3) / 4;   // status unit + exception counts (shard.hip)
          uint64_t& u = side ? ru : su;
          p.hdr_unit = u;
          p.rec_unit = u + hdr;
@@ -1570,20 +1637,32 @@ static int chain_setup(gnoc_engine* e)
    GNOC_HIP(e, e->ch_nmax.ensure(std::max<size_t>(nmx, 1) * 4));
    e->zq.push_back({ e->ch_nmax.p, (uint64_t) std::max<size_t>(nmx, 1) * 4 });   // (zq_flush: before the INJ level)
    const size_t stb = (e->ch_st_words[0] + e->ch_st_words[1] + ch::SW) * 8;
-   const bool fresh = e->ch_st.bytes < stb;
+   const size_t xdb = std::max<size_t>(e->h_tasks[0].size(), 1) * 8;
+   const bool fresh = e->ch_st.bytes < stb || e->ch_xdone.bytes < xdb;
    GNOC_HIP(e, e->ch_st.ensure(stb));
+   GNOC_HIP(e, e->ch_xdone.ensure(xdb));
    // hand-off granules carry a 16-bit epoch: a new epoch per attempt, the buffer
    // zeroed when it is new or the epoch wraps
    e->ch_epoch = (e->ch_epoch + 1) & 0xFFFFu;
    if (fresh || e->ch_epoch == 0)
    {
       GNOC_HIP(e, hipMemsetAsync(e->ch_st.p, 0, e->ch_st.bytes, s));
+      GNOC_HIP(e, hipMemsetAsync(e->ch_xdone.p, 0, e->ch_xdone.bytes, s));
       if (e->ch_epoch == 0) e->ch_epoch = 1;
    }
    e->zq.push_back({ e->ch_ctr.p, 256 });
-   // the hand-off protocol per phase: GNOC_CHAIN_LOOKBACK=0/1 forces one; otherwise each is
-   // timed once on the current windows and the faster one is kept
+   // The hand-off protocol per phase.  GNOC_CHAIN_LOOKBACK=0/1 forces one.  Otherwise,
+   // once the windows have settled (this attempt's windows are the previous attempt's),
+   // each protocol is timed once on them, the phases as separate launches (the trial
+   // runs), and the decision is kept for the batch until its windows change again:
+   // serial unless look-back is faster by more than CH_LB_MARGIN, so near-equal times
+   // (configs[1]'s uniform X phase) keep the serial protocol in every process.  Until a
+   // decision exists, serial.
    const char* lbv = std::getenv("GNOC_CHAIN_LOOKBACK");
+   const bool settled = e->chD_run[0] == e->ch_prevD[0] && e->chD_run[1] == e->ch_prevD[1];
+   e->ch_prevD[0] = e->chD_run[0];
+   e->ch_prevD[1] = e->chD_run[1];
+   e->ch_trial = 0;
    for (int p = 0; p < 2; p++)
    {
       if (!e->ch_ev[p][0]) GNOC_HIP(e, hipEventCreate(&e->ch_ev[p][0]));
@@ -1594,36 +1673,30 @@ static int chain_setup(gnoc_engine* e)
          e->ch_lb_ms[p][0] = e->ch_lb_ms[p][1] = -1.f;
       }
       const float* m = e->ch_lb_ms[p];
+      if (m[0] >= 0 && m[1] >= 0) e->ch_lb_dec[p] = m[1] < (1.f - CH_LB_MARGIN) * m[0] ? 1 : 0;
+      const bool trial = settled && (m[0] < 0 || m[1] < 0);
+      e->ch_trial |= trial;
       e->ch_lb_run[p] = lbv && *lbv ? (uint32_t) (std::atoi(lbv) != 0)
-                                    : m[0] < 0 ? 0u : m[1] < 0 ? 1u : (m[1] < m[0] ? 1u : 0u);
+                                    : trial ? (m[0] < 0 ? 0u : 1u) : (e->ch_lb_dec[p] > 0 ? 1u : 0u);
    }
+   if (lbv && *lbv) e->ch_trial = 0;
    if (ncp)
       GNOC_LAUNCH(e, KC_PLAN, ch::k_chain_plan, dim3((ncp + 255) / 256), dim3(256), 0, s, c, e->ncpx, e->ncpy, e->ry0,
                   e->cx0, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->ch_cp.as<ChainPort>());
    return GNOC_OK;
 }
 
-// One phase: 0 = X (rows of this rank), 1 = Y (columns of this rank).
-static int chain_phase(gnoc_engine* e, int phase)
+// The kernel arguments of one phase: 0 = X (rows of this rank), 1 = Y (columns of
+// this rank).
+static ChainArgs chain_args(gnoc_engine* e, int phase)
 {
-   {
-      const int zr = zq_flush(e, e->stream);
-      if (zr) return zr;
-   }
    const DevCfg& c = e->dc;
-   hipStream_t s = e->stream;
    const uint32_t ncp = phase ? e->ncpy : e->ncpx;
-   if (!ncp) return GNOC_OK;
    const uint32_t len = phase ? c.H - 1 : c.W - 1;
-   const uint32_t nl = phase ? 3u : 1u;
-   const ChainPort* cp = e->ch_cp.as<ChainPort>() + (phase ? e->ncpx : 0);
-   uint32_t* bt = e->ch_bt.as<uint32_t>() + (phase ? e->ch_bt_words[0] : 0);
-   const ChainWin* cw = e->ch_cw.as<ChainWin>() + (phase ? e->h_cw[0].size() : 0);
-   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, cp, nl, len, cw, e->recs.as<Rec>(), bt);
-   ChainArgs a;
+   ChainArgs a{};
    a.c = c;
-   a.cp = cp;
-   a.bt = bt;
+   a.cp = e->ch_cp.as<ChainPort>() + (phase ? e->ncpx : 0);
+   a.bt = e->ch_bt.as<uint32_t>() + (phase ? e->ch_bt_words[0] : 0);
    a.recs = e->recs.as<Rec>();
    a.samp_t = e->samp_t.as<uint64_t>();
    a.samp_id = e->samp_id.as<uint32_t>();
@@ -1634,11 +1707,11 @@ static int chain_phase(gnoc_engine* e, int phase)
    a.port_last = e->port_last.as<unsigned long long>();
    a.errflag = e->counters.as<unsigned>() + 8;
    a.ctr = e->ch_ctr.as<unsigned>() + phase;
-   a.nch = ncp / len;
+   a.nch = len ? ncp / len : 0;
    a.len = len;
    a.ntasks = (uint32_t) e->h_tasks[phase].size();
    a.pad2 = 0;
-   a.cw = cw;
+   a.cw = e->ch_cw.as<ChainWin>() + (phase ? e->h_cw[0].size() : 0);
    a.tasks = e->ch_tasks.as<uint32_t>() + (phase ? e->h_tasks[0].size() : 0);
    a.cp0 = 0;
    a.nmax = e->ch_nmax.as<unsigned>() + (phase ? 2 * e->h_cw[0].size() : 0);
@@ -1646,11 +1719,28 @@ static int chain_phase(gnoc_engine* e, int phase)
    a.etag = (uint64_t) e->ch_epoch << 48;
    a.stamps = nullptr;
    a.lookback = e->ch_lb_run[phase];
-   a.fw = phase ? 5u : 4u;
+   a.fw = a.fw2 = phase ? 5u : 4u;
+   return a;
+}
+
+// One phase as its own launch.
+static int chain_phase(gnoc_engine* e, int phase)
+{
+   {
+      const int zr = zq_flush(e, e->stream);
+      if (zr) return zr;
+   }
+   hipStream_t s = e->stream;
+   const uint32_t ncp = phase ? e->ncpy : e->ncpx;
+   if (!ncp) return GNOC_OK;
+   ChainArgs a = chain_args(e, phase);
+   const uint32_t nl = phase ? 3u : 1u;
+   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, a.cp, nl, a.len, a.cw, e->recs.as<Rec>(),
+               const_cast<uint32_t*>(a.bt), nl);
    const char* stv = std::getenv("GNOC_STAMPS");
    if (stv && *stv == '1')
    {
-      const size_t nst = (size_t) a.ntasks * len * 16;
+      const size_t nst = (size_t) a.ntasks * a.len * 16;
       DevBuf& sb = phase ? e->ch_stamps1 : e->ch_stamps0;
       GNOC_HIP(e, sb.ensure(nst * 8));
       GNOC_HIP(e, hipMemsetAsync(sb.p, 0, nst * 8, s));
@@ -1674,7 +1764,78 @@ static int chain_phase(gnoc_engine* e, int phase)
    return GNOC_OK;
 }
 
+// Both phases in one launch (chain.hip k_chain_xy, GNOC_XY=1): a single unsharded
+// mesh whose Y chains have at most 64 ports, outside the protocol trial runs (which
+// launch the phases separately).  Measured on configs[1] it is exact but not faster
+// than the two launches, so the two launches are the default.
+static bool chain_fusable(const gnoc_engine* e)
+{
+   const char* v = std::getenv("GNOC_XY");
+   if (!v || !*v || std::atoi(v) == 0) return false;
+   if (e->nranks > 1 || e->ch_ydeclined || !e->ncpx || !e->ncpy || e->dc.H - 1 > 64) return false;
+   return !e->ch_trial;
+}
+
+static int chain_fused(gnoc_engine* e)
+{
+   {
+      const int zr = zq_flush(e, e->stream);
+      if (zr) return zr;
+   }
+   hipStream_t s = e->stream;
+   ch::XYArgs xa;
+   xa.x = chain_args(e, 0);
+   xa.y = chain_args(e, 1);
+   // X inserts (injection outputs) and the Y ports' IN_LOCAL lists: complete before the launch
+   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpx), dim3(256), 0, s, xa.x.cp, 1u, xa.x.len, xa.x.cw,
+               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.x.bt), 1u);
+   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpy), dim3(256), 0, s, xa.y.cp, 3u, xa.y.len, xa.y.cw,
+               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.y.bt), 1u);
+   const uint32_t nx = (uint32_t) e->h_tasks[0].size();
+   xa.x.fw2 = 5u;                                  // an X decline stops the Y tasks too
+   xa.y.ctr = xa.x.ctr;                            // one dequeue head
+   for (ChainArgs* q : { &xa.x, &xa.y })
+   {
+      q->nx_tasks = nx;
+      q->xdone = e->ch_xdone.as<uint64_t>();
+      q->xprefix = e->ch_ctr.as<unsigned>() + 2;   // (zeroed with the dequeue heads)
+      q->xcw = xa.x.cw;
+      q->xst = xa.x.st;
+   }
+   xa.tasks = e->ch_xy.as<uint32_t>();
+   xa.taux = e->ch_xy.as<uint32_t>() + e->h_xy.size();
+   xa.ntasks = (uint32_t) e->h_xy.size();
+   const char* stv = std::getenv("GNOC_STAMPS");
+   if (stv && *stv == '1')
+   {
+      const size_t nst = (size_t) xa.ntasks * std::max(xa.x.len, xa.y.len) * 16;
+      GNOC_HIP(e, e->ch_stamps0.ensure(nst * 8));
+      GNOC_HIP(e, hipMemsetAsync(e->ch_stamps0.p, 0, nst * 8, s));
+      xa.x.stamps = xa.y.stamps = e->ch_stamps0.as<uint64_t>();
+   }
+   const uint32_t grid = (uint32_t) std::min<uint64_t>((uint64_t) e->ch_grid, (uint64_t) xa.ntasks);
+   GNOC_HIP(e, hipEventRecord(e->ch_ev[0][0], s));
+#define GNOC_XYL(F1V, XL, YL) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain_xy<F1V, XL, YL>), dim3(grid), dim3(ch::T), 0, s, xa)
+#define GNOC_XYF(F1V)                                  \
+   do                                                  \
+   {                                                   \
+      if (xa.x.lookback && xa.y.lookback) GNOC_XYL(F1V, true, true);        \
+      else if (xa.x.lookback) GNOC_XYL(F1V, true, false);                   \
+      else if (xa.y.lookback) GNOC_XYL(F1V, false, true);                   \
+      else GNOC_XYL(F1V, false, false);                                     \
+   } while (0)
+   if (e->f1) GNOC_XYF(true);
+   else GNOC_XYF(false);
+#undef GNOC_XYF
+#undef GNOC_XYL
+   GNOC_HIP(e, hipEventRecord(e->ch_ev[0][1], s));
+   e->ch_fused = 1;
+   return GNOC_OK;
+}
+
 static int run_post(gnoc_engine* e, bool closed_form);
+static int run_post_enqueue(gnoc_engine* e, bool closed_form);
+static int run_post_check(gnoc_engine* e, bool closed_form);
 
 // Zero the queued buffers (e->zq) in one launch.
 static int zq_flush(gnoc_engine* e, hipStream_t s)
@@ -1776,7 +1937,13 @@ static int run_prep(gnoc_engine* e, bool* done)
       ZeroSegs z{};
       uint32_t ns = 0;
       uint64_t mx = 0;
+      bool zover = false;   // ZeroSegs holds ZSEG segments: one more per-run buffer belongs in zq
       auto seg = [&](void* p, uint64_t bytes) {
+         if (ns >= (uint32_t) ZSEG)
+         {
+            zover = true;
+            return;
+         }
          z.p[ns] = (uint32_t*) p;
          z.nw[ns] = bytes / 4;
          mx = std::max(mx, bytes / 4);
@@ -1792,6 +1959,7 @@ static int run_prep(gnoc_engine* e, bool* done)
       seg(e->port_last.p, nports * 8);
       if (!pp_lds) seg(e->Pp.p, (uint64_t) H * G * N * 4);
       if (band_prep) seg(e->pcol.p, (uint64_t) nC * H * H * 3 * 4);
+      if (zover) return fail(e, GNOC_EHIP, "internal: more per-run zero segments than ZeroSegs holds");
       const uint32_t gx = (uint32_t) std::max<uint64_t>(1, std::min<uint64_t>((mx + 255) / 256, 512));
       GNOC_LAUNCH(e, KC_CLASSIFY, k_zero_segs, dim3(gx, ns), dim3(256), 0, s, z, e->nb ? 1u : 0u);
    }
@@ -1931,7 +2099,7 @@ static int run_prep(gnoc_engine* e, bool* done)
 
 // Last phase: per-packet zero-load / contention (packets this rank delivers:
 // destination in its column band), end event, counters and flags to the host.
-static int run_post(gnoc_engine* e, bool closed_form)
+static int run_post_enqueue(gnoc_engine* e, bool closed_form)
 {
    const DevCfg& c = e->dc;
    const size_t n = e->n;
@@ -1969,7 +2137,12 @@ static int run_post(gnoc_engine* e, bool closed_form)
          GNOC_HIP(e, hipMemcpyAsync(e->h_nmax, e->ch_nmax.p, 8 * (e->h_cw[0].size() + e->h_cw[1].size()),
                                     hipMemcpyDeviceToHost, s));
    }
-   GNOC_HIP(e, hipStreamSynchronize(s));
+   return GNOC_OK;
+}
+// The run's one host sync, then its counters and flags.
+static int run_post_check(gnoc_engine* e, bool closed_form)
+{
+   GNOC_HIP(e, hipStreamSynchronize(e->stream));
    e->h_counters[0] = e->h_pinned[0];
    e->h_counters[1] = e->h_pinned[1];
    float ms = 0;
@@ -1986,7 +2159,7 @@ static int run_post(gnoc_engine* e, bool closed_form)
    const unsigned* ef = (const unsigned*) (e->h_pinned + 8);
    const unsigned errf = ef[0];
    const unsigned cf = ef[4] | ef[5];   // the X phase's and the Y phase's chain flags
-   if (e->used_chain && !(cf & ch::F_ANY))
+   if (e->used_chain && !e->ch_fused && e->ch_trial && !(cf & ch::F_ANY))
    {
       // this run's time of each phase's protocol (chain_setup keeps the faster one)
       for (int p = 0; p < 2; p++)
@@ -2012,6 +2185,7 @@ static int run_post(gnoc_engine* e, bool closed_form)
       }
       // only the Y chains declined, for a reason the level engine takes (the M/G/1
       // branch, a spill range, a hand-off timeout): the X phase's outputs stand
+      e->ch_yflags = ef[5];
       if (!(ef[4] & ch::F_ANY) && (ef[5] & (ch::F_FALLBACK | ch::F_TIMEOUT)) && !(ef[5] & ch::F_RETRY) && e->nranks <= 1)
          return GNOC_CH_YFALL;
       // declined only because the injection level left exception tails: rerun with them merged
@@ -2029,6 +2203,11 @@ static int run_post(gnoc_engine* e, bool closed_form)
    if (errf & 1u) return fail(e, GNOC_EHIP, "internal: route-count invariant violated");
    e->ran = true;
    return GNOC_OK;
+}
+static int run_post(gnoc_engine* e, bool closed_form)
+{
+   const int rc = run_post_enqueue(e, closed_form);
+   return rc ? rc : run_post_check(e, closed_form);
 }
 
 static int run_once(gnoc_engine* e)
@@ -2050,8 +2229,13 @@ static int run_once(gnoc_engine* e)
       if (!rc) rc = chain_setup(e);
       if (!rc) rc = run_levels_v3(e, 0, 1);
       if (!rc && e->exc_fix) rc = exc_merge(e);
-      if (!rc) rc = chain_phase(e, 0);
-      if (!rc && !e->ch_ydeclined) rc = chain_phase(e, 1);
+      e->ch_fused = 0;
+      if (!rc && chain_fusable(e)) rc = chain_fused(e);
+      else
+      {
+         if (!rc) rc = chain_phase(e, 0);
+         if (!rc && !e->ch_ydeclined) rc = chain_phase(e, 1);
+      }
       const char* xv = std::getenv("GNOC_CHAIN_EXPERIMENT");
       if (!rc && xv && std::atoi(xv))
       {
@@ -2365,30 +2549,41 @@ static int run_impl(gnoc_engine* e)
       e->force_levels = 0;
       e->chD_run[0] = e->chD[0];
       e->chD_run[1] = e->chD[1];
-      int rc = run_once(e);
-      if (rc == GNOC_CH_EXC)
+      // chain engine: a run that declined only for the injection level's exception tails
+      // reruns once with them merged (later runs of the batch merge up front); a window
+      // that overflowed LDS reruns with windows half as long (twice as many), up to 3
+      // halvings.  Both count as reruns (gnoc_summary.retries); only halvings use up
+      // the halving budget.
+      int rc = GNOC_OK;
+      uint32_t halvings = 0;
+      for (;;)
       {
-         e->exc_fix = 1;   // later runs of this batch merge the tails up front
-         e->n_retry++;
          rc = run_once(e);
+         if (rc == GNOC_CH_EXC && !e->exc_fix)
+         {
+            e->exc_fix = 1;
+            e->n_retry++;
+            continue;
+         }
+         if (rc == GNOC_CH_EXC) rc = GNOC_CH_FALLBACK;
+         // halve the windows of the chains that overflowed (all, when none is marked)
+         if (rc == GNOC_CH_RETRY && halvings < 3 && halve_overflowed(e, e->chD_run))
+         {
+            halvings++;
+            e->n_retry++;
+            continue;
+         }
+         break;
       }
-      if (rc == GNOC_CH_EXC) rc = GNOC_CH_FALLBACK;
       if (rc == GNOC_CH_YFALL)
       {
-         // the Y chains declined this batch (deterministic): its Y and SELF levels run on
-         // k_level now, and later runs go there straight after the X chains
+         // only the Y chains declined: the batch's Y and SELF levels run on k_level now.
+         // For an M/G/1 request or a spill range (properties of the batch) later runs go
+         // there straight after the X chains; a hand-off timeout (a scheduling event)
+         // moves this run only.
          e->n_fallback++;
-         e->ch_ydeclined = 1;
+         if (e->ch_yflags & ch::F_FALLBACK) e->ch_ydeclined = 1;
          rc = y_levels_rerun(e);
-      }
-      // chain engine: a window that overflowed LDS reruns with windows half as long
-      // (twice as many), up to 3 times; anything else it cannot take reruns on levels
-      while (rc == GNOC_CH_RETRY && e->n_retry < 3)
-      {
-         // halve the windows of the chains that overflowed (all, when none is marked)
-         if (!halve_overflowed(e, e->chD_run)) break;
-         e->n_retry++;
-         rc = run_once(e);
       }
       if (rc == GNOC_CH_RETRY || rc == GNOC_CH_FALLBACK)
       {
@@ -2399,7 +2594,7 @@ static int run_impl(gnoc_engine* e)
          e->ch_declined = 1;
          rc = run_once(e);
       }
-      else if (!rc && e->used_chain && e->n_retry)
+      else if (!rc && e->used_chain && halvings)
       {
          // the window sizes that fit: later runs of this batch start with them
          e->chD[0] = e->chD_run[0];
@@ -2507,6 +2702,10 @@ int gnoc_shard(gnoc_engine* e, int32_t rank, int32_t nranks)
       return fail(e, GNOC_EUNSUPPORTED, "sharding needs the chunked path (max_list_size >= 3)");
    e->rank = rank;
    e->nranks = nranks;
+   {
+      const char* xv = std::getenv("GNOC_SHARD_SELF_EXCHANGE");
+      e->xself = xv && *xv && std::atoi(xv) != 0;
+   }
    build_static_levels(e);
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    GNOC_HIP(e, upload_levels(e));
@@ -2551,8 +2750,7 @@ static int rccl_exchange(gnoc_engine* e, const void* send, const uint64_t* su, v
    }
    if (ncclGroupEnd() != ncclSuccess && !bad) bad = "ncclGroupEnd";
    if (bad) return fail(e, GNOC_EHIP, bad);
-   GNOC_HIP(e, hipStreamSynchronize(e->stream));
-   return GNOC_OK;
+   return GNOC_OK;   // on the stream: the Y phase that reads the buffer follows in order
 }
 
 static int rccl_agree(gnoc_engine* e, int32_t status, int32_t* out)
@@ -2639,12 +2837,93 @@ static int shard_agree(gnoc_engine* e, int rc, const char* what)
    return GNOC_OK;
 }
 
+static int begin_x(gnoc_engine* e, void* send_buf, bool sync);
+static int finish_enqueue(gnoc_engine* e, const void* recv_buf);
+static int finish_check(gnoc_engine* e);
+
+// The synchronous protocol: every phase brackets its outcome with a status
+// agreement (a failed rank fails every rank; none waits in a collective a peer
+// never joins).  Used by the caller-transport path, and by the RCCL path to rerun a
+// step whose stream-path status said a rank's X phase did not complete.
+static int run_sharded_sync(gnoc_engine* e, const uint64_t* su, const uint64_t* ru)
+{
+   int rc = shard_agree(e, begin_x(e, e->xsend.p, true), "gnoc_run_begin");
+   if (rc) return rc;
+   if (e->nccl)
+   {
+      rc = rccl_exchange(e, e->xsend.p, su, e->xrecv.p, ru);
+      if (!rc) GNOC_HIP(e, hipStreamSynchronize(e->stream));
+   }
+   else if (e->tp.exchange(e->tp.ctx, e->xsend.p, su, e->xrecv.p, ru, e->stream))
+      rc = fail(e, GNOC_EHIP, "transport exchange failed");
+   rc = shard_agree(e, rc, "the turn exchange");
+   if (rc) return rc;
+   return shard_agree(e, gnoc_run_finish(e, e->xrecv.p), "gnoc_run_finish");
+}
+
+// The stream path over RCCL: X phase, pack, grouped send / receive, Y phase, the
+// status all-reduce and the read-back all go onto the engine's stream, then ONE
+// host sync.  Every rank issues the same two collectives whatever happens locally:
+// a rank that cannot complete its X phase marks its send buffer's pair status units
+// (its peers' Y phases then skip), and the reduced status sends every rank to the
+// synchronous protocol for this step.
+static int run_sharded_stream(gnoc_engine* e, const uint64_t* su, const uint64_t* ru, uint64_t ns, bool* accounted)
+{
+   hipStream_t s = e->stream;
+   ncclComm_t comm = static_cast<ncclComm_t>(e->nccl);
+   int lrc = begin_x(e, e->xsend.p, false);
+   if (lrc)
+   {
+      // the buffer may be unpacked: every pair's status unit reads "failed"
+      (void) hipMemsetAsync(e->xsend.p, 0xFF, std::max<uint64_t>(ns, 1) * 16, s);
+      e->begun = false;
+   }
+   const int xrc = rccl_exchange(e, e->xsend.p, su, e->xrecv.p, ru);
+   if (!lrc && xrc) lrc = xrc;
+   if (!lrc)
+   {
+      lrc = finish_enqueue(e, e->xrecv.p);
+      if (lrc) e->begun = false;
+   }
+   hipError_t he = e->xflag.ensure(16);
+   int32_t* hst = reinterpret_cast<int32_t*>(e->h_pinned + 16);
+   if (he == hipSuccess)
+   {
+      hipLaunchKernelGGL(k_shard_status, dim3(1), dim3(64), 0, s, e->counters.as<unsigned>() + 8, lrc ? 1 : 0,
+                         e->xflag.as<int>());
+      he = hipGetLastError();
+   }
+   const bool red = he == hipSuccess && ncclAllReduce(e->xflag.p, e->xflag.p, 4, ncclInt32, ncclMax, comm, s) == ncclSuccess;
+   if (red) he = hipMemcpyAsync(hst, e->xflag.p, 16, hipMemcpyDeviceToHost, s);
+   if (he == hipSuccess) he = hipStreamSynchronize(s);
+   if (!red || he != hipSuccess) return fail(e, GNOC_EHIP, "sharded step status all-reduce failed");
+   const int32_t st[4] = { hst[0], hst[1], hst[2], hst[3] };
+   if (st[0]) return lrc ? lrc : fail(e, GNOC_EHIP, "gnoc_run_sharded failed on another rank");
+   if (st[1])
+   {
+      // a rank's X phase did not complete (a chain decline, an unsplittable burst, an
+      // injected decline): the step reruns on the synchronous protocol everywhere.
+      // gnoc_run_finish accounts the rerun (one run, its reruns); the stream attempt
+      // adds one fallback.
+      *accounted = true;
+      e->fin_closed = false;
+      const int rc = run_sharded_sync(e, su, ru);
+      e->n_fallback++;
+      e->tot_fallback++;
+      return rc;
+   }
+   if (st[2]) return fail(e, GNOC_EHIP, "internal: route-count invariant violated (sharded step)");
+   int rc = finish_check(e);
+   if (st[3]) rc = shard_agree(e, rc, "gnoc_run_finish");   // some rank reran its Y levels
+   return rc;
+}
+
 int gnoc_run_sharded(gnoc_engine* e)
 {
    if (!e) return GNOC_EINVAL;
    // one rank without a communicator: the plain run; with one, the full protocol
-   // (an empty grouped exchange and the status all-reduces), as every rank of a
-   // larger communicator runs it
+   // (the exchange group, empty unless GNOC_SHARD_SELF_EXCHANGE, and the status
+   // all-reduce), as every rank of a larger communicator runs it
    if (e->nranks <= 1 && !e->nccl && !e->tp.exchange) return gnoc_run(e);
    if (!e->nccl && !e->tp.exchange) return fail(e, GNOC_ESTATE, "gnoc_run_sharded needs gnoc_shard_set_comm or a transport");
    // from here every failure goes through the status agreement, so no peer waits
@@ -2665,19 +2944,27 @@ int gnoc_run_sharded(gnoc_engine* e)
       su[q] = q < e->xs_units.size() ? e->xs_units[q] : 0;
       ru[q] = q < e->xr_units.size() ? e->xr_units[q] : 0;
    }
-   int rc = shard_agree(e, gnoc_run_begin(e, e->xsend.p), "gnoc_run_begin");
-   if (rc) return rc;
-   if (e->nccl) rc = rccl_exchange(e, e->xsend.p, su.data(), e->xrecv.p, ru.data());
-   else if (e->tp.exchange(e->tp.ctx, e->xsend.p, su.data(), e->xrecv.p, ru.data(), e->stream))
-      rc = fail(e, GNOC_EHIP, "transport exchange failed");
-   rc = shard_agree(e, rc, "the turn exchange");
-   if (rc) return rc;
-   return shard_agree(e, gnoc_run_finish(e, e->xrecv.p), "gnoc_run_finish");
+   if (!e->nccl) return run_sharded_sync(e, su.data(), ru.data());
+   e->n_retry = e->n_fallback = 0;
+   bool accounted = false;
+   const int rc = run_sharded_stream(e, su.data(), ru.data(), ns, &accounted);
+   if (!accounted)
+   {
+      e->runs++;
+      e->tot_retry += e->n_retry;
+      e->tot_fallback += e->n_fallback;
+   }
+   return rc;
 }
 
-int gnoc_run_begin(gnoc_engine* e, void* send_buf)
+// The X phase of a sharded run and the pack of the turn records.  sync: the
+// transport is the caller's (or the exchange must not start before the buffer is
+// complete): a declined X chain reruns on levels here, and the send buffer is
+// complete on return.  !sync (gnoc_run_sharded over RCCL): everything stays on the
+// stream; a declined X phase is carried by the pairs' status units instead
+// (shard.hip), and the step's status all-reduce sends every rank to the rerun.
+static int begin_x(gnoc_engine* e, void* send_buf, bool sync)
 {
-   if (!e) return GNOC_EINVAL;
    e->ran = false;
    e->begun = false;
    bool done = false;
@@ -2703,15 +2990,20 @@ int gnoc_run_begin(gnoc_engine* e, void* send_buf)
       e->used_chain = 1;
       e->used_v3 = 4;
       rc = chain_setup(e);
+      e->ch_fused = 0;
       if (!rc) rc = run_levels_v3(e, 0, 1);
       if (!rc) rc = chain_phase(e, 0);
       if (rc) return rc;
+      if (!sync) goto pack;
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
       GNOC_HIP(e, hipStreamSynchronize(s));
       const unsigned f4 = ((const unsigned*) (e->h_pinned + 8))[4];
       if (f4 & ch::F_ROUTE) return fail(e, GNOC_EHIP, "internal: chain route-count invariant violated");
       if (f4 & ch::F_ANY)
       {
+         // an M/G/1 request or exception tails: a property of the batch, so its later
+         // runs take the level engine straight away (a new submit clears this)
+         if ((f4 & ch::F_FALLBACK) && !(f4 & ch::F_TIMEOUT)) e->ch_declined = 1;
          if (f4 & ch::F_RETRY)
          {
             // windows of this rank's X chains overflowed: shorter ones at the next run
@@ -2735,46 +3027,72 @@ int gnoc_run_begin(gnoc_engine* e, void* send_buf)
    else if (!rc)
       rc = run_levels_v3(e, 0, e->lvl_y0);
    if (rc) return rc;
-   // a look-back timeout or a leaf the splitter could not cut leaves garbage in
-   // the turn slots: fail here, before anything is packed for the peers
-   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
-   GNOC_HIP(e, hipStreamSynchronize(s));
-   if (((const unsigned*) (e->h_pinned + 8))[0] & 6u)
-      return fail(e, GNOC_EUNSUPPORTED, "sharded run hit a burst the chunked path cannot split (X phase)");
-   // test knob: this rank reports an X-phase failure (the peers must all abort too)
-   const char* frv = std::getenv("GNOC_FAIL_RANK");
-   if (frv && *frv && std::atoi(frv) == e->rank) return fail(e, GNOC_EHIP, "injected X-phase failure (GNOC_FAIL_RANK)");
+   if (sync)
+   {
+      // a look-back timeout or a leaf the splitter could not cut leaves garbage in
+      // the turn slots: fail here, before anything is packed for the peers
+      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
+      GNOC_HIP(e, hipStreamSynchronize(s));
+      if (((const unsigned*) (e->h_pinned + 8))[0] & 6u)
+         return fail(e, GNOC_EUNSUPPORTED, "sharded run hit a burst the chunked path cannot split (X phase)");
+   }
+pack:
+   {
+      // test knobs: this rank reports an X-phase failure (the peers must all abort too);
+      // this rank's X phase "declines" once on the stream path (its peers' Y phases
+      // skip, and every rank reruns the step)
+      const char* frv = std::getenv("GNOC_FAIL_RANK");
+      if (frv && *frv && std::atoi(frv) == e->rank) return fail(e, GNOC_EHIP, "injected X-phase failure (GNOC_FAIL_RANK)");
+      const char* prv = std::getenv("GNOC_DECLINE_ONCE_RANK");
+      if (!sync && prv && *prv && std::atoi(prv) == e->rank && !e->declined_once)
+      {
+         e->declined_once = 1;
+         GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, ch::F_TIMEOUT, 1, s));
+      }
+   }
    if (e->xs_slots)
    {
       if (!send_buf) return fail(e, GNOC_EINVAL, "null send buffer");
       const uint32_t np = (uint32_t) e->xs_pairs.size();
       hipLaunchKernelGGL(k_x_layout, dim3(np), dim3(1024), 0, s, e->dc.W, e->d_xs_pairs.as<XPair>(),
-                         e->slot_cnt.as<uint32_t>(), e->xs_off.as<uint64_t>(), e->counters.as<unsigned>() + 8);
+                         e->slot_cnt.as<uint32_t>(), e->xs_off.as<uint64_t>(), e->counters.as<unsigned>() + 8,
+                         reinterpret_cast<uint4*>(send_buf), 0);
       GNOC_HIP(e, hipGetLastError());
       hipLaunchKernelGGL(k_x_pack, dim3((e->xs_slots + 3) / 4), dim3(256), 0, s, e->dc.W, e->d_xs_pairs.as<XPair>(), np,
                          e->xs_slots, e->xs_off.as<uint64_t>(), e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(),
                          e->nexc.as<uint32_t>(), e->recs.as<Rec>(), reinterpret_cast<uint4*>(send_buf));
       GNOC_HIP(e, hipGetLastError());
    }
-   GNOC_HIP(e, hipStreamSynchronize(s));   // the send buffer is complete when this returns
+   if (sync) GNOC_HIP(e, hipStreamSynchronize(s));   // the send buffer is complete when this returns
    e->begun = true;
    return GNOC_OK;
 }
 
-static int run_finish_impl(gnoc_engine* e, const void* recv_buf);
+int gnoc_run_begin(gnoc_engine* e, void* send_buf)
+{
+   if (!e) return GNOC_EINVAL;
+   return begin_x(e, send_buf, true);
+}
+
+
 int gnoc_run_finish(gnoc_engine* e, const void* recv_buf)
 {
    if (!e) return GNOC_EINVAL;
-   const int rc = run_finish_impl(e, recv_buf);
+   int rc = finish_enqueue(e, recv_buf);
+   if (!rc) rc = finish_check(e);
    e->runs++;
    e->tot_retry += e->n_retry;
    e->tot_fallback += e->n_fallback;
    return rc;
 }
-static int run_finish_impl(gnoc_engine* e, const void* recv_buf)
+// The Y phase of a sharded run: the received turn records back into their slots,
+// the Y chains (or levels) and the SELF level, the per-packet finish, and the
+// read-back of the flags -- all on the stream, no host sync (finish_check syncs).
+static int finish_enqueue(gnoc_engine* e, const void* recv_buf)
 {
    if (!e->begun) return fail(e, GNOC_ESTATE, "gnoc_run_finish without gnoc_run_begin");
    e->begun = false;
+   e->fin_closed = !e->dc.contention;
    if (!e->dc.contention) return GNOC_OK;   // closed form finished in gnoc_run_begin
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    hipStream_t s = e->stream;
@@ -2783,7 +3101,8 @@ static int run_finish_impl(gnoc_engine* e, const void* recv_buf)
       if (!recv_buf) return fail(e, GNOC_EINVAL, "null receive buffer");
       const uint32_t np = (uint32_t) e->xr_pairs.size();
       hipLaunchKernelGGL(k_x_layout, dim3(np), dim3(1024), 0, s, e->dc.W, e->d_xr_pairs.as<XPair>(),
-                         e->slot_cnt.as<uint32_t>(), e->xr_off.as<uint64_t>(), e->counters.as<unsigned>() + 8);
+                         e->slot_cnt.as<uint32_t>(), e->xr_off.as<uint64_t>(), e->counters.as<unsigned>() + 8,
+                         reinterpret_cast<uint4*>(const_cast<void*>(recv_buf)), 1);
       GNOC_HIP(e, hipGetLastError());
       hipLaunchKernelGGL(k_x_unpack, dim3((e->xr_slots + 3) / 4), dim3(256), 0, s, e->dc.W, e->d_xr_pairs.as<XPair>(), np,
                          e->xr_slots, e->xr_off.as<uint64_t>(), e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(),
@@ -2797,30 +3116,42 @@ static int run_finish_impl(gnoc_engine* e, const void* recv_buf)
    {
       rc = chain_phase(e, 1);
       if (!rc) rc = run_levels_v3(e, L - 1, L);
-      if (!rc) rc = run_post(e, false);
-      if (rc == GNOC_CH_EXC || rc == GNOC_CH_YFALL) rc = GNOC_CH_FALLBACK;   // (the sharded path's own Y fallback below)
-      // the windows of the next run: from this run's measured fill, or shorter
-      // for the chains that overflowed (results never depend on them)
-      if (!rc && !e->ch_resized) adapt_windows(e);
-      if (rc == GNOC_CH_RETRY) (void) halve_overflowed(e, e->chD);
-      e->ch_resized = 0;
-      if (rc != GNOC_CH_RETRY && rc != GNOC_CH_FALLBACK) return rc;
-      // the Y chains declined: Y and SELF levels on k_level (fresh look-back state)
-      e->n_fallback++;
-      e->used_chain = 0;
-      GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, 0, 8, s));
-      const uint32_t np = e->dc.N * PORTS;
-      hipLaunchKernelGGL(ch::k_zero_ports, dim3((np + 255) / 256), dim3(256), 0, s, np,
-                         (1u << P_UP) | (1u << P_DOWN) | (1u << P_SELF), e->port_sum.as<unsigned long long>(),
-                         e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
-                         e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>());
-      GNOC_HIP(e, hipGetLastError());
-      rc = run_plan_v3(e);
-      if (rc) return rc;
    }
-   rc = run_levels_v3(e, e->lvl_y0, L);
-   if (rc) return rc;
-   return run_post(e, false);
+   else
+      rc = run_levels_v3(e, e->lvl_y0, L);
+   if (!rc) rc = run_post_enqueue(e, false);
+   return rc;
+}
+// After finish_enqueue: the one host sync, then the checks; a rank whose Y chains
+// declined reruns its Y and SELF levels here (local: the exchange is done).
+static int finish_check(gnoc_engine* e)
+{
+   if (e->fin_closed) return GNOC_OK;
+   hipStream_t s = e->stream;
+   int rc = run_post_check(e, false);
+   if (rc == GNOC_V3_RETRY) return fail(e, GNOC_EUNSUPPORTED, "sharded run hit a burst the chunked path cannot split");
+   if (!e->used_chain) return rc;
+   if (rc == GNOC_CH_EXC || rc == GNOC_CH_YFALL) rc = GNOC_CH_FALLBACK;   // (the sharded path's own Y fallback below)
+   // the windows of the next run: from this run's measured fill, or shorter
+   // for the chains that overflowed (results never depend on them)
+   if (!rc && !e->ch_resized) adapt_windows(e);
+   if (rc == GNOC_CH_RETRY) (void) halve_overflowed(e, e->chD);
+   e->ch_resized = 0;
+   if (rc != GNOC_CH_RETRY && rc != GNOC_CH_FALLBACK) return rc;
+   // the Y chains declined: Y and SELF levels on k_level (fresh look-back state)
+   e->n_fallback++;
+   e->used_chain = 0;
+   GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, 0, 8, s));
+   const uint32_t np = e->dc.N * PORTS;
+   hipLaunchKernelGGL(ch::k_zero_ports, dim3((np + 255) / 256), dim3(256), 0, s, np,
+                      (1u << P_UP) | (1u << P_DOWN) | (1u << P_SELF), e->port_sum.as<unsigned long long>(),
+                      e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),
+                      e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>());
+   GNOC_HIP(e, hipGetLastError());
+   rc = run_plan_v3(e);
+   if (!rc) rc = run_levels_v3(e, e->lvl_y0, (uint32_t) e->lvl_off.size() - 1);
+   if (!rc) rc = run_post(e, false);
+   return rc;
 }
 
 int gnoc_get_packet_results(gnoc_engine* e, uint64_t* final_ps, uint64_t* zero_load_ps, uint64_t* contention_ps, size_t n)
@@ -2930,7 +3261,7 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
    while (sh < 63 && (2ull << sh) <= dm[0]) sh++;
    out->window_shift = e->used_chain ? sh : 0u;
    out->windows_y = nwm[1];
-   out->abi_pad = 0;
+   out->chain_protocol = e->used_chain ? 0x100u | e->ch_lb_run[0] | (e->ch_lb_run[1] << 1) | (e->ch_fused ? 0x200u : 0u) : 0u;
    out->window_ps_x = dm[0];
    out->window_ps_y = dm[1];
    out->runs = e->runs;
@@ -2984,16 +3315,30 @@ __attribute__((visibility("default"))) int gnoc_debug_chain_stamps(gnoc_engine* 
                                                                    size_t* count, uint32_t* geom)
 {
    if (!e || !count) return GNOC_EINVAL;
-   const DevBuf& sb = phase ? e->ch_stamps1 : e->ch_stamps0;
-   const uint32_t len = phase ? e->dc.H - 1 : e->dc.W - 1;
-   const uint32_t ncp = phase ? e->ncpy : e->ncpx;
-   const uint32_t nch = len ? ncp / len : 0;
-   (void) nch;
-   const size_t nt = e->h_tasks[phase].size();
+   // phase 2: the fused launch (X and Y tasks in one table; geom[3] = its X tasks; the
+   // table itself through gnoc_debug_xy_tasks)
+   const DevBuf& sb = phase == 1 ? e->ch_stamps1 : e->ch_stamps0;
+   const uint32_t len = phase == 2 ? std::max(e->dc.W, e->dc.H) - 1 : phase ? e->dc.H - 1 : e->dc.W - 1;
+   const size_t nt = phase == 2 ? e->h_xy.size() : e->h_tasks[phase].size();
    *count = nt * len * 16;
-   if (geom) { geom[0] = 1; geom[1] = (uint32_t) nt; geom[2] = len; geom[3] = 0; }   // tasks in start-time order
+   if (geom)
+   {
+      geom[0] = 1;
+      geom[1] = (uint32_t) nt;
+      geom[2] = len;
+      geom[3] = phase == 2 ? (uint32_t) e->h_tasks[0].size() : 0u;   // tasks in key order
+   }
    if (!out || !sb.p) return GNOC_OK;
    GNOC_HIP(e, hipMemcpy(out, sb.p, std::min(cap, *count) * 8, hipMemcpyDeviceToHost));
+   return GNOC_OK;
+}
+
+// Debug: the fused launch's task table (bit 31: Y task, bits 16-30 chain, 0-15 window).
+__attribute__((visibility("default"))) int gnoc_debug_xy_tasks(gnoc_engine* e, uint32_t* out, size_t cap, size_t* count)
+{
+   if (!e || !count) return GNOC_EINVAL;
+   *count = e->h_xy.size();
+   if (out) std::copy(e->h_xy.begin(), e->h_xy.begin() + std::min(cap, e->h_xy.size()), out);
    return GNOC_OK;
 }
 

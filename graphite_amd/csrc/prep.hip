@@ -144,7 +144,8 @@ template <bool LH>
 __global__ __launch_bounds__(256) void k_validate(DevCfg c, uint64_t n, const uint64_t* __restrict__ inj,
                                                   const uint32_t* __restrict__ src, const uint32_t* __restrict__ dst,
                                                   const uint32_t* __restrict__ bits, const uint32_t* __restrict__ flags,
-                                                  int tree, uint32_t sweep, uint32_t nr, uint32_t rank, ValOut* __restrict__ vo,
+                                                  int tree, uint32_t sweep, uint32_t nr, uint32_t rank, uint32_t xself,
+                                                  ValOut* __restrict__ vo,
                                                   int* __restrict__ gtab, uint32_t ntab, int* __restrict__ part,
                                                   unsigned long long* __restrict__ xcnt)
 {
@@ -230,7 +231,15 @@ __global__ __launch_bounds__(256) void k_validate(DevCfg c, uint64_t n, const ui
          atomicAdd(&dyd[dx * (H + 1) + sy + 1], -1);
          atomicAdd(&insy[(sy * W + dx) * 2 + 1], 1);
       }
-      if (nr <= 1) rec += 2 + ax + ay;
+      if (nr <= 1)
+      {
+         rec += 2 + ax + ay;
+         if (xself && c.contention)   // the self-exchange test knob: one turn record per routed packet
+         {
+            if (LH) atomicAdd(&lx[0], 1u);
+            else atomicAdd(&xcnt[0], 1ull);
+         }
+      }
       else
       {
          // records this rank materialises: injection + X leg in its row band (all

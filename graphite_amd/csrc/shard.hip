@@ -19,8 +19,14 @@
 // stream.
 //
 // Buffer layout per (r -> d) pair, in 16-byte units:
-//   [ nexc of the pair's turn slots, u32 each, padded to 16 B ][ records, slot order ]
+//   [ status ][ nexc of the pair's turn slots, u32 each, padded to 16 B ][ records, slot order ]
 // Pair slot order: tiles row-major over (rows(r) x cols(d)), 9 slots per tile.
+// The status unit carries the sender's X-phase outcome: nonzero when its X phase
+// did not complete (a chain decline, a level the chunked path could not finish, a
+// route-count error, or a host-side failure that left the buffer unpacked).  The
+// receiver then raises its own X flag word, so its Y chains and levels return at
+// once instead of reading the peer's incomplete turn slots; the step's status
+// all-reduce makes every rank rerun it (engine.hip gnoc_run_sharded).
 #include "common.h"
 
 namespace gnoc {
@@ -45,15 +51,25 @@ __device__ __forceinline__ uint32_t xs_slot(const XPair& p, uint32_t k, uint32_t
    return slot_of((p.y0 + ty) * W + p.x0 + tx, dir, in);
 }
 
+constexpr uint32_t XR_PEER = 1u << 16;   // errflag[4] reason bit: a peer's X phase did not complete
+
 // One block per pair: exclusive scan of the pair's slot counts -> each slot's
 // first record position in the buffer.  Checks the pair total against the
-// host's count (route invariant, errflag bit 0).
+// host's count (route invariant, errflag bit 0).  Send side (buf = the send
+// buffer): the pair's status unit from this rank's X-phase flags.  Receive side
+// (buf = the received buffer): a peer's nonzero status raises the X flag word.
 __global__ __launch_bounds__(1024) void k_x_layout(uint32_t W, const XPair* __restrict__ pairs,
                                                    const uint32_t* __restrict__ slot_cnt,
-                                                   uint64_t* __restrict__ xoff, unsigned* __restrict__ errflag)
+                                                   uint64_t* __restrict__ xoff, unsigned* __restrict__ errflag,
+                                                   uint4* __restrict__ buf, int recv_side)
 {
    __shared__ uint64_t part[1024];
    const XPair p = pairs[blockIdx.x];
+   if (recv_side && threadIdx.x == 0)
+   {
+      const uint4 st = buf[p.hdr_unit];
+      if (st.x | st.y | st.z | st.w) atomicOr(errflag + 4, 2u | XR_PEER);   // ch::F_FALLBACK | XR_PEER
+   }
    uint64_t carry = 0;
    for (uint32_t k0 = 0; k0 < p.nslots; k0 += 1024)
    {
@@ -73,6 +89,14 @@ __global__ __launch_bounds__(1024) void k_x_layout(uint32_t W, const XPair* __re
       __syncthreads();
    }
    if (threadIdx.x == 0 && carry != p.expect) atomicOr(errflag, 1u);
+   if (!recv_side && threadIdx.x == 0)
+   {
+      // this rank's X phase: level errors (route, look-back timeout, unsplittable
+      // leaf) and chain flags; written after this pair's own count check
+      const unsigned e0 = __hip_atomic_load(errflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned e4 = __hip_atomic_load(errflag + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      buf[p.hdr_unit] = make_uint4((e0 & 7u) | (carry != p.expect ? 1u : 0u), e4 & 0xFu, 0u, 0u);
+   }
 }
 
 __device__ __forceinline__ uint32_t xs_pair_of(const XPair* __restrict__ pairs, uint32_t np, uint32_t w)
@@ -100,7 +124,7 @@ __global__ __launch_bounds__(256) void k_x_pack(uint32_t W, const XPair* __restr
    const uint4* src = reinterpret_cast<const uint4*>(recs + slot_base[s]);
    uint4* dst = buf + xoff[w];
    for (uint32_t i = lane; i < n; i += 64) dst[i] = src[i];
-   if (lane == 0) reinterpret_cast<uint32_t*>(buf + p.hdr_unit)[k] = nexc[s];
+   if (lane == 0) reinterpret_cast<uint32_t*>(buf + p.hdr_unit + 1)[k] = nexc[s];
 }
 
 // One wave per turn slot: records back into the slot, key samples of the FIFO
@@ -121,7 +145,7 @@ __global__ __launch_bounds__(256) void k_x_unpack(uint32_t W, const XPair* __res
    const uint32_t k = w - p.slot0;
    const uint32_t s = xs_slot(p, k, W);
    const uint32_t n = slot_cnt[s];
-   const uint32_t ne = reinterpret_cast<const uint32_t*>(buf + p.hdr_unit)[k];
+   const uint32_t ne = reinterpret_cast<const uint32_t*>(buf + p.hdr_unit + 1)[k];
    const uint64_t base = slot_base[s];
    const uint4* src = buf + xoff[w];
    uint4* dst = reinterpret_cast<uint4*>(recs + base);
@@ -142,6 +166,22 @@ __global__ __launch_bounds__(256) void k_x_unpack(uint32_t W, const XPair* __res
       if (ne) atomicOr(errflag + 2, 1u);
       if (ne > n) atomicOr(errflag, 1u);
    }
+}
+
+// The step's status on the stream path (engine.hip gnoc_run_sharded), as four
+// words every rank max-reduces: [0] a host-side failure on this rank, [1] the step
+// must rerun on the synchronous protocol (this rank's X phase or a peer's did not
+// complete, or a chunked level hit a burst it could not split), [2] a route-count
+// invariant broke (internal error), [3] this rank's Y chains declined (it reruns
+// its Y levels locally; every rank then agrees on the outcome).
+__global__ void k_shard_status(const unsigned* __restrict__ errflag, int host_err, int* __restrict__ st)
+{
+   if (threadIdx.x != 0) return;
+   const unsigned e0 = errflag[0], e4 = errflag[4], e5 = errflag[5];
+   st[0] = host_err ? 1 : 0;
+   st[1] = ((e4 & 0xFu) || (e0 & 6u)) ? 1 : 0;       // ch::F_ANY on the X word; level errors
+   st[2] = ((e0 & 1u) || ((e4 | e5) & 4u)) ? 1 : 0;   // ch::F_ROUTE
+   st[3] = (e5 & 0xFu) ? 1 : 0;
 }
 
 }  // namespace gnoc

@@ -117,7 +117,7 @@ class GnocSummary(ctypes.Structure):
         ("windows", ctypes.c_uint32),
         ("window_shift", ctypes.c_uint32),
         ("windows_y", ctypes.c_uint32),
-        ("abi_pad", ctypes.c_uint32),
+        ("chain_protocol", ctypes.c_uint32),
         ("window_ps_x", ctypes.c_uint64),
         ("window_ps_y", ctypes.c_uint64),
         ("runs", ctypes.c_uint32),
@@ -165,9 +165,9 @@ def load() -> ctypes.CDLL:
         ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_uint64, ctypes.c_double, ctypes.c_int32, vp, vp, vp, vp, sz, ctypes.POINTER(sz)]
     lib.gnoc_abi_version.argtypes = []
-    # an older library (A/B timing against an earlier build) fills a prefix of the
-    # summary and has no build id
-    if not 2 <= lib.gnoc_abi_version() <= ABI_VERSION:
+    # the summary layout (runs, retries_total, fallbacks_total, chain_protocol) is ABI 3's:
+    # an older library would leave the rerun totals the bench checks at zero
+    if lib.gnoc_abi_version() != ABI_VERSION:
         raise RuntimeError(f"{LIB_PATH}: ABI {lib.gnoc_abi_version()}, this module speaks {ABI_VERSION}")
     if hasattr(lib, "gnoc_build_id"):
         lib.gnoc_build_id.argtypes = []

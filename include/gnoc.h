@@ -166,7 +166,11 @@ typedef struct gnoc_summary
    uint32_t windows;            /* chain-engine time windows of the last attempt, X phase (0 = not used) */
    uint32_t window_shift;       /* floor(log2) of the X phase's window length in ps     */
    uint32_t windows_y;          /* Y phase's windows                                     */
-   uint32_t abi_pad;
+   uint32_t chain_protocol;     /* hand-off protocol of the last chain run: bit 8 set when the chain
+                                   engine ran; bit 0 / bit 1 set when the X / Y phase used the
+                                   look-back protocol (else serial; look-back is kept only when it
+                                   measured > 5% faster than serial on the batch's windows); bit 9
+                                   set when both phases ran in one fused launch */
    uint64_t window_ps_x;        /* window length (ps) of the X phase                     */
    uint64_t window_ps_y;        /* ... of the Y phase                                    */
    /* since the last gnoc_submit: runs, and the retries / fallbacks of all of them

@@ -35,7 +35,12 @@ CASES = {
     "32x32_uniform_l0.005_ppt10000": (32, 32, 0.005, 10000, 1, 0.0),
     "32x32_hotspot_l0.005_ppt10000": (32, 32, 0.005, 10000, 1, 0.2),
     "64x64_uniform_l0.002_ppt10000": (64, 64, 0.002, 10000, 1, 0.0),
+    # configs[1]'s uniform batch behind a cycle-0 burst of 4 packets per tile (uniform
+    # random destinations, seed 7): the history tree's analytical branch
+    # (queue_model_history_tree.cc:58-64) serves requests in injection AND mesh ports
+    "32x32_burst4_l0.005_ppt10000": (32, 32, 0.005, 10000, 1, 0.0, 4),
 }
+BURST_SEED = 7
 RESULT_FIELDS = ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1",
                  "port_flit", "port_last")
 
@@ -45,8 +50,19 @@ def sha(a) -> str:
 
 
 def trace_of(name):
-    W, H, load, ppt, seed, hot = CASES[name]
-    return gnoc.synthetic_trace(W, H, load, ppt, seed=seed, hotspot_fraction=hot, num_hotspots=16)
+    W, H, load, ppt, seed, hot = CASES[name][:6]
+    tr = gnoc.synthetic_trace(W, H, load, ppt, seed=seed, hotspot_fraction=hot, num_hotspots=16)
+    burst = CASES[name][6] if len(CASES[name]) > 6 else 0
+    if not burst:
+        return tr
+    rng = np.random.default_rng(BURST_SEED)
+    N = W * H
+    bs = np.repeat(np.arange(N, dtype=np.uint32), burst)
+    bd = rng.integers(0, N, bs.size).astype(np.uint32)
+    cat = lambda a, b: np.concatenate([a.astype(b.dtype), b])
+    fl = tr.flags if tr.flags is not None else np.zeros(len(tr), np.uint32)
+    return gnoc.Trace(cat(np.zeros(bs.size, np.uint64), tr.inject_ps), cat(bs, tr.src), cat(bd, tr.dst),
+                      cat(np.full(bs.size, 576, np.uint32), tr.bits), cat(np.zeros(bs.size, np.uint32), fl))
 
 
 def trace_hash(tr) -> str:
@@ -67,7 +83,8 @@ def main(only=None):
     if os.path.exists(OUT):
         with open(OUT) as fh:
             out = json.load(fh)
-    for name, (W, H, load, ppt, seed, hot) in CASES.items():
+    for name, spec in CASES.items():
+        W, H, load, ppt, seed, hot = spec[:6]
         if only and not name.startswith(only):
             continue
         tr = trace_of(name)
@@ -77,7 +94,7 @@ def main(only=None):
         dt = time.time() - t0
         hops = int(r.port_count.reshape(-1, 6)[:, :5].sum())
         out[name] = {"W": W, "H": H, "load": load, "ppt": ppt, "seed": seed, "hotspot_fraction": hot,
-                     "num_hotspots": 16, "packets": len(tr), "mesh_hops": hops, "trace_sha256": trace_hash(tr),
+                     "num_hotspots": 16, "burst_per_tile": spec[6] if len(spec) > 6 else 0, "packets": len(tr), "mesh_hops": hops, "trace_sha256": trace_hash(tr),
                      "mg1_uses": int(r.port_mg1.sum()), "results": digest(r), "oracle_s": round(dt, 1)}
         print(f"{name}: {len(tr)} packets, {hops} mesh hops, oracle {dt:.1f} s", flush=True)
         with open(OUT, "w") as fh:

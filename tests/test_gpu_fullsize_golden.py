@@ -10,6 +10,8 @@ from its seed (its own SHA-256 checked first), run through the engine, and
 every result array must hash identically:
 * configs[1]: 32x32 uniform and hotspot, load 0.005, 10,000 packets per tile
   (10.24 M packets, 228 M mesh hops) -- the bench workload;
+* configs[1]'s uniform batch behind a cycle-0 burst of 4 packets per tile,
+  whose M/G/1 requests (injection and mesh ports) the pin counts;
 * configs[2]: 64x64 uniform, load 0.002, 10,000 packets per tile (40.96 M
   packets, 1.79 G mesh hops), on one engine and sharded over 8 row / column
   band ranks (gnoc.LocalShardSet, all ranks on the one test GPU).
@@ -59,6 +61,32 @@ def test_configs1_full_size_matches_oracle(name, lookback, monkeypatch):
         assert s["mesh_hops"] == GOLD[name]["mesh_hops"]
         _check(name, eng.results())
     eng.close()
+
+
+@pytest.mark.parametrize("lookback", ["0", "1"])
+def test_configs1_full_size_mg1_burst_matches_oracle(lookback, monkeypatch):
+    """configs[1]'s uniform batch behind a cycle-0 burst (4 packets per tile): the
+    analytical M/G/1 branch serves requests in injection and mesh ports, so the
+    pin covers mg1_uses > 0 at full size.  Every result array hashes as the
+    oracle's and the summary's M/G/1 count equals the oracle's; the engine path
+    each run took is printed (the chains run the no-gap M/G/1 prefix serially or
+    the batch takes a slower exact path; the bench reports which)."""
+    monkeypatch.setenv("GNOC_CHAIN_LOOKBACK", lookback)
+    name = "32x32_burst4_l0.005_ppt10000"
+    assert GOLD[name]["mg1_uses"] > 0
+    assert GOLD[name]["results"]["port_mg1"]["sum"] == GOLD[name]["mg1_uses"]
+    tr = _trace(name)
+    eng = gnoc.Engine(gnoc.EngineConfig(num_tiles=1024))
+    eng.submit(tr)
+    paths = []
+    for _ in range(3):
+        eng.run()
+        s = eng.summary()
+        paths.append(int(s["engine_path"]))
+        assert s["mg1_uses"] == GOLD[name]["mg1_uses"], (s["mg1_uses"], GOLD[name]["mg1_uses"])
+        _check(name, eng.results())
+    eng.close()
+    print("engine paths", paths)
 
 
 def test_configs1_full_size_level_engine_matches_oracle(monkeypatch):

@@ -136,33 +136,105 @@ def test_bad_packet_on_one_rank_fails_every_rank(bad):
     assert msgs[0] == msgs[1] and str(k) in msgs[0], msgs
 
 
-@pytest.mark.parametrize("W,load,ppt", [(8, 0.05, 300), (32, 0.005, 1000)])
-def test_rccl_one_rank_run_sharded(W, load, ppt):
-    """gnoc_run_sharded over a real RCCL communicator (libgnoc's own RCCL,
-    gnoc_rccl_comm_init) at one rank: the grouped send / receive of the turn
-    exchange and the status all-reduces run on the engine's stream, and the
-    results equal the unsharded run's and the oracle's."""
+def _rccl_one_rank(cfg, tr, runs=2):
+    """gnoc_run_sharded on a 1-rank RCCL communicator of libgnoc's own RCCL."""
     import numpy as np
     from graphite_amd import gnoc
-    from oracle import oracle
-    cfg = gnoc.EngineConfig(num_tiles=W * W)
-    tr = gnoc.synthetic_trace(W, W, load, ppt, seed=11)
     comm = gnoc.RcclComm(1, 0, 0)
     eng = gnoc.NativeShardedEngine(cfg, 0, 1, comm)
     eng.submit(tr)
-    for _ in range(2):
+    su, ru = np.zeros(1, np.uint64), np.zeros(1, np.uint64)
+    eng._check(eng.lib.gnoc_exchange_counts(eng._h, su.ctypes.data, ru.ctypes.data, 1))
+    for _ in range(runs):
         eng.run()
-    got = eng.results()
+    got, summ = eng.results(), eng.summary()
     eng.close()
     comm.close()
+    return got, summ, int(su[0]), int(ru[0])
+
+
+def _unsharded(cfg, tr):
+    from graphite_amd import gnoc
     ref = gnoc.Engine(cfg)
     ref.submit(tr)
     ref.run()
     want = ref.results()
     ref.close()
-    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1", "port_flit",
-              "port_last"):
+    return want
+
+
+RESULT_KEYS = ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1", "port_flit",
+               "port_last")
+
+
+@pytest.mark.parametrize("W,load,ppt", [(8, 0.05, 300), (32, 0.005, 1000)])
+def test_rccl_one_rank_self_exchange(W, load, ppt, monkeypatch):
+    """gnoc_run_sharded over a real RCCL communicator at one rank, with the
+    self-exchange knob: the rank's own turn records (one per routed packet) are
+    packed, moved by ncclSend / ncclRecv to itself inside the group, and unpacked
+    back into their slots, then the Y phase reads them -- on the stream path (one
+    host sync per step, the status all-reduce on the stream).  The results equal
+    the unsharded run's and the oracle's."""
+    import numpy as np
+    from graphite_amd import gnoc
+    from oracle import oracle
+    monkeypatch.setenv("GNOC_SHARD_SELF_EXCHANGE", "1")
+    cfg = gnoc.EngineConfig(num_tiles=W * W)
+    tr = gnoc.synthetic_trace(W, W, load, ppt, seed=11)
+    got, summ, su, ru = _rccl_one_rank(cfg, tr)
+    routed = int(summ["routed_packets"])
+    # 16-B units: the pair's status unit, its exception-count header, one record per routed packet
+    hdr = 1 + (W * W * 9 + 3) // 4
+    assert su == ru == hdr + routed and routed > 0, (su, ru, routed)
+    assert summ["fallbacks"] == 0 and summ["engine_path"] == 4, summ
+    want = _unsharded(cfg, tr)
+    for k in RESULT_KEYS:
         assert np.array_equal(getattr(got, k), getattr(want, k)), k
     if W <= 8:
         orc = oracle.run(cfg, tr)
         assert np.array_equal(got.final_ps, orc.final_ps)
+
+
+def test_rccl_one_rank_no_self_exchange_is_empty():
+    """Without the knob a 1-rank communicator moves nothing (its turn records
+    stay in place) and still runs the stream protocol exactly."""
+    import numpy as np
+    from graphite_amd import gnoc
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = gnoc.synthetic_trace(8, 8, 0.05, 300, seed=12)
+    got, summ, su, ru = _rccl_one_rank(cfg, tr)
+    assert su == ru == 0
+    want = _unsharded(cfg, tr)
+    for k in RESULT_KEYS:
+        assert np.array_equal(getattr(got, k), getattr(want, k)), k
+
+
+def test_rccl_declined_x_phase_poisons_and_reruns(monkeypatch):
+    """A rank whose X phase does not complete on the stream path (injected once:
+    GNOC_DECLINE_ONCE_RANK) marks its send buffer's pair status units; the
+    receiving Y phase skips, the step's status all-reduce sends the rank to the
+    synchronous protocol, and the rerun is exact.  One fallback is counted."""
+    import numpy as np
+    from graphite_amd import gnoc
+    monkeypatch.setenv("GNOC_SHARD_SELF_EXCHANGE", "1")
+    monkeypatch.setenv("GNOC_DECLINE_ONCE_RANK", "0")
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = gnoc.synthetic_trace(8, 8, 0.05, 300, seed=13)
+    comm = gnoc.RcclComm(1, 0, 0)
+    eng = gnoc.NativeShardedEngine(cfg, 0, 1, comm)
+    eng.submit(tr)
+    eng.run()
+    s1 = eng.summary()
+    first = eng.results()
+    for _ in range(3):   # (the windows adapt to the measured fill: an overflow on the next run reruns too)
+        eng.run()
+    s2 = eng.summary()
+    got = eng.results()
+    eng.close()
+    comm.close()
+    assert s1["fallbacks"] >= 1 and s1["runs"] == 1, s1
+    assert s2["fallbacks"] == 0 and s2["runs"] == 4, s2
+    want = _unsharded(cfg, tr)
+    for k in RESULT_KEYS:
+        assert np.array_equal(getattr(first, k), getattr(want, k)), k
+        assert np.array_equal(getattr(got, k), getattr(want, k)), k

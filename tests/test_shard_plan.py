@@ -51,7 +51,8 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         m = gnoc.turn_counts(random_trace(4000, 8, 8, seed=2), 8, 8, world)
-        hdr = lambda r, d: (len(gnoc.band(r, world, 8)) * len(gnoc.band(d, world, 8)) * 9 + 3) // 4
+        # per pair: a status unit, then the exception counts (u32 per turn slot, 9 per tile)
+        hdr = lambda r, d: 1 + (len(gnoc.band(r, world, 8)) * len(gnoc.band(d, world, 8)) * 9 + 3) // 4
         su = [0 if d == rank else hdr(rank, d) + int(m[rank, d]) for d in range(world)]
         ru = [0 if r == rank else hdr(r, rank) + int(m[r, rank]) for r in range(world)]
         # unit k of the block for peer d carries (rank, d, k) so the receiver can check provenance
