@@ -127,11 +127,12 @@ def main():
     # end to end (SURVEY.md 8(d) "trace resident in host memory -> results in host
     # memory"): submit from pinned host arrays (host-side trace validation + H2D),
     # run, final_ps back into a pinned host array; reported beside the HBM-resident value
-    e2e_ms = e2e_serial_ms = e2e_wide_ms = None
+    e2e_ms = e2e_serial_ms = e2e_wide_ms = e2e_fin_ms = None
     wire = None
     if not sharded:
         ptr = pinned_trace(tr)
         fins = [torch.empty(len(tr), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64) for _ in range(2)]
+        lats = [pinned_array(len(tr), np.uint32) for _ in range(2)]
         K = max(2, a.steps // 2)
         # the narrow wire format (gnoc_packets_narrow: u16 tile ids / lengths, u8 flags,
         # 15 B per packet) where the batch fits it, else the 24-B one
@@ -141,29 +142,37 @@ def main():
         except ValueError:
             ntr, sub, sub_async, wire = ptr, eng.submit, eng.submit_async, 24
 
-        def pipelined(submit, submit_async, x):
-            # batch k+1's upload and batch k's read-back run on copy streams beside run k
+        def pipelined(submit, submit_async, x, latency=False):
+            # batch k+1's upload and batch k's read-back run on copy streams beside run k;
+            # the read-back is final_ps (u64) or, narrow, the per-packet latency (u32)
             barrier_sync()
             t_e = time.perf_counter()
             submit(x)
+            outs = lats if latency else fins
             for k in range(K):
                 if k + 1 < K:
                     submit_async(x)
                 eng.run()
-                eng.fetch_final_ps(fins[k % 2])
+                (eng.fetch_latency if latency else eng.fetch_final_ps)(outs[k % 2])
                 if k + 1 < K:
                     eng.submit_commit()
             eng.fetch_wait()
             ms = (time.perf_counter() - t_e) / K * 1e3
             want = eng.results().final_ps
-            assert all(np.array_equal(f, want) for f in fins), "pipelined read-back differs from the run's final_ps"
+            if latency:
+                want = (want - tr.inject_ps).astype(np.uint32)
+            assert all(np.array_equal(f, want) for f in outs), "pipelined read-back differs from the run's results"
             return ms
-        # untimed: the second trace buffers, copy streams and staging areas get allocated
+        # untimed: the second trace buffers, copy streams, staging areas and latency
+        # arrays get allocated
         for sa, x in ((sub_async, ntr), (eng.submit_async, ptr)):
             sa(x)
             eng.submit_commit()
             eng.run()
             eng.fetch_final_ps(fins[0])
+            eng.fetch_wait()
+            eng.run()
+            eng.fetch_latency(lats[0])
             eng.fetch_wait()
         # one batch at a time: submit (H2D + device checks), run, final_ps read-back
         barrier_sync()
@@ -173,8 +182,9 @@ def main():
             eng.run()
             eng.final_ps_into(fins[0])
         e2e_serial_ms = (time.perf_counter() - t_e) / K * 1e3
-        e2e_ms = pipelined(sub, sub_async, ntr)
-        e2e_wide_ms = pipelined(eng.submit, eng.submit_async, ptr) if wire == 15 else e2e_ms
+        e2e_ms = pipelined(sub, sub_async, ntr, latency=True)
+        e2e_fin_ms = pipelined(sub, sub_async, ntr)
+        e2e_wide_ms = pipelined(eng.submit, eng.submit_async, ptr) if wire == 15 else e2e_fin_ms
 
     # this rank's share: mesh hops through the ports it owns, packets it delivers
     res = eng.results()
@@ -257,12 +267,15 @@ def main():
             "build_id": bid,
             "e2e_ms_per_step": e2e_ms,
             "e2e_serial_ms_per_step": e2e_serial_ms,
+            "e2e_final_ps_ms_per_step": e2e_fin_ms,
             "e2e_24B_ms_per_step": e2e_wide_ms,
             "e2e_wire_bytes_per_packet": wire,
-            "e2e_note": "host trace (pinned) -> host final_ps per batch: submit (H2D + device-side trace checks) + run + "
-                        "final_ps D2H; e2e_ms_per_step pipelined (batch k+1's upload and batch k's read-back on copy "
-                        "streams beside the runs) in the narrow wire format, e2e_serial_ms_per_step one batch at a "
-                        "time (same format), e2e_24B_ms_per_step pipelined with the 24-B format",
+            "e2e_note": "host trace (pinned) -> host results per batch: submit (H2D + device-side trace checks) + run + "
+                        "read-back; e2e_ms_per_step pipelined (batch k+1's upload and batch k's read-back on copy "
+                        "streams beside the runs) in the narrow wire format with the per-packet latency read back "
+                        "as u32 (gnoc_fetch_latency), e2e_final_ps_ms_per_step the same with final_ps (u64), "
+                        "e2e_serial_ms_per_step one batch at a time (narrow upload, final_ps), e2e_24B_ms_per_step "
+                        "pipelined with the 24-B upload and final_ps",
             "roofline": {
                 "bound": "hbm",
                 "achieved": rf["achieved"],
@@ -348,7 +361,7 @@ def chain_protocol(summ):
     if not v & 0x100:
         return None
     return {"x": "lookback" if v & 1 else "serial", "y": "lookback" if v & 2 else "serial",
-            "launch": "fused x+y" if v & 0x200 else "x, y"}
+            "launch": "fused x+y" if v & 0x200 else "x, y", "mg1_serial": bool(v & 0x400)}
 
 
 def roofline(kst, pc, summ, my_pkts):
@@ -530,19 +543,35 @@ def pmc_traffic(workload, kernel, bid):
 
 
 def cpu_baseline(a, W, H, load, hot):
-    """The CPU oracle (event-driven restatement of the reference path) timed on
-    one host core over a bounded sample of the same workload."""
+    """The reference path on one host core over a bounded sample of the same workload:
+    the oracle's event loop (oracle/gnoc_oracle.c, the reference's per-hop walk
+    restated) with every history-tree queue being the reference's OWN IntervalTree +
+    QueueModelMG1 objects, compiled from its sources into oracle/_ref (ref_driver.cc
+    restates only computeQueueDelay's 80 lines over them).  Where oracle/_ref is not
+    built, the all-restated oracle (sorted-array free list) instead, and the record
+    says so.  The restated oracle's rate on the same sample is reported beside it."""
     from graphite_amd import gnoc
     from oracle import oracle
     tr = gnoc.synthetic_trace(W, H, load, a.cpu_sample_ppt, seed=a.seed, hotspot_fraction=hot, num_hotspots=16)
     cfg = gnoc.EngineConfig(num_tiles=W * H)
     t0 = time.perf_counter()
     r = oracle.run(cfg, tr)
-    dt = time.perf_counter() - t0
+    dt_port = time.perf_counter() - t0
     hops = int(r.port_count.reshape(-1, 6)[:, :5].sum())
+    ref_q = oracle.ref_lib() is not None
+    dt = dt_port
+    if ref_q:
+        t0 = time.perf_counter()
+        rq = oracle.run(cfg, tr, ref_queues=True)
+        dt = time.perf_counter() - t0
+        assert np.array_equal(rq.final_ps, r.final_ps), "reference queue objects disagree with the oracle"
     return {"value": hops / dt, "unit": "packet-hops/s", "cores": 1, "kind": "port",
-            "what": "oracle restatement of the reference path (oracle/gnoc_oracle.c), 1 core, sorted-array "
-                    "free list instead of the reference's AVL tree",
+            "what": ("the reference's per-hop event walk restated (oracle/gnoc_oracle.c) with the reference's own "
+                     "IntervalTree + QueueModelMG1 objects compiled from its sources (oracle/_ref) as every "
+                     "history-tree queue, 1 core" if ref_q else
+                     "oracle restatement of the reference path (oracle/gnoc_oracle.c), 1 core, sorted-array free "
+                     "list instead of the reference's AVL tree (oracle/_ref not built)"),
+            "restated_queues_value": hops / dt_port,
             "sample": f"{W}x{H} {a.mix} load={load} pkts/tile={a.cpu_sample_ppt}: {len(tr)} packets, "
                       f"{hops} mesh hops in {dt:.2f} s",
             # the reference itself (compiled from its sources, survey probe, SURVEY.md 6): context only,

@@ -77,8 +77,10 @@ constexpr int NLMAX = 3;                  // local insert lists (Y ports: LOCAL,
 //   KO   the port's consumed spill prefix after this window
 //   POST (after the outputs, its spill stores drained): the chain outputs before this
 //        window (low 32 bits) and its kept count (bits 32..47)
-constexpr int SW = 12;
-enum : int { G_X = 0, G_CNT = 1, G_MODE = 5, G_AB = 6, G_AA = 7, G_AC = 8, G_KO = 9, G_POST = 10 };
+//   MG   (with INC while the queue has had no gap yet): the QueueModelMG1 sums narr, s1,
+//        s2 (exact integers) and newest, lanes G_MG .. G_MG + 3
+constexpr int SW = 16;
+enum : int { G_X = 0, G_CNT = 1, G_MODE = 5, G_AB = 6, G_AA = 7, G_AC = 8, G_KO = 9, G_POST = 10, G_MG = 12 };
 constexpr uint64_t INC_MASK = 0x3Full, AGG_MASK = 0x1C0ull;
 constexpr int SW_SER = 8;                 // the serial protocol's state: X, 4 counts, "no gap yet", KO, spill end
 constexpr int LB_POST = 2 * SW;           // the look-back prefetch's lane for POST of (w-1, i-1)
@@ -179,6 +181,8 @@ struct ChainArgs
    unsigned* xprefix;             // leading X tasks known done (advanced by the Y tasks that wait on it)
    const ChainWin* xcw;           // Y tasks: the X phase's windows ...
    const uint64_t* xst;           // ... and hand-off state (the producer ports' cumulative route counts)
+   uint32_t* nexc;                // exception-tail counts per slot (M/G/1-served turns, mg_emit)
+   unsigned long long* port_mg1;  // per-port M/G/1 requests
 };
 
 
@@ -204,6 +208,18 @@ __device__ __forceinline__ void st1(uint64_t* p, uint64_t v)
 }
 // Compiler-only ordering point between LDS phases of the one wave.
 __device__ __forceinline__ void wsync() { asm volatile("" ::: "memory"); }
+// Every vector memory op of the wave done (s_waitcnt vmcnt(0), nothing else), once per
+// step before the outputs: the state loads before it are issued under exec masks on
+// some paths only, and with one such load possibly pending the compiler's wait pass
+// puts a vmcnt(0) (which also waits for the row's write-through stores) in front of
+// every later reuse of its registers, i.e. into every output row.
+#ifndef CH_VMDRAIN
+#define CH_VMDRAIN 1
+#endif
+__device__ __forceinline__ void vm_drain()
+{
+   if (CH_VMDRAIN) __builtin_amdgcn_s_waitcnt(0x0F70);
+}
 
 template <int CTRL, int RM, int BM>
 __device__ __forceinline__ uint32_t dpp32(uint32_t v)
@@ -522,6 +538,34 @@ __device__ __forceinline__ void load_rows(Smem& sm, uint32_t nK, uint32_t IB, ui
    }
 }
 
+#ifndef CH_BRANK
+#define CH_BRANK 1   // 0: route ranks by a DPP prefix sum and field tables by ds_bpermute
+#endif
+// A row's route fields (2 bits per lane, valid lanes a prefix of the row) by three
+// ballots: per-field counts packed 8 bits per field, and each lane's rank among the
+// lanes of its own field (lanes below it with the same two bits).  Scalar bit counts
+// and two mask selects instead of a dependent cross-lane scan.
+__device__ __forceinline__ uint32_t field_tot(bool valid, uint32_t f, uint64_t& b0, uint64_t& b1)
+{
+   b0 = __ballot(valid && (f & 1u));
+   b1 = __ballot(valid && (f & 2u));
+   const uint64_t vm = __ballot(valid);
+   const uint32_t c0 = (uint32_t) __popcll(vm & ~(b0 | b1)), c1 = (uint32_t) __popcll(b0 & ~b1);
+   const uint32_t c2 = (uint32_t) __popcll(b1 & ~b0), c3 = (uint32_t) __popcll(b0 & b1);
+   return c0 | c1 << 8 | c2 << 16 | c3 << 24;
+}
+__device__ __forceinline__ uint32_t field_rank(uint32_t f, uint64_t b0, uint64_t b1)
+{
+   const uint64_t m = ((f & 1u) ? b0 : ~b0) & ((f & 2u) ? b1 : ~b1);
+   return mbcnt(m);
+}
+// Lane-wise pick of one of four wave-uniform values by a 2-bit field.
+__device__ __forceinline__ uint32_t sel4(uint32_t f, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3)
+{
+   const uint32_t lo = (f & 1u) ? v1 : v0, hi = (f & 1u) ? v3 : v2;
+   return (f & 2u) ? hi : lo;
+}
+
 // Per-field tables: lane 1 + q holds route field q (SELF, cont, UP, DOWN), the
 // lanes of the state words that carry the route counts.
 // Lane 1 + q of a row's packed field counts (8 bits per field).
@@ -589,6 +633,222 @@ __device__ __forceinline__ void out_record(gptr<Rec> recs, gptr<uint64_t> samp_t
 
 
 
+
+
+// ---------------------------------------------------------------------------
+// a port whose history tree has had no gap yet: the analytical branch
+// ---------------------------------------------------------------------------
+// While a queue has never idled its tree holds the one free interval [X, inf): a
+// request with X > t + p is served by the M/G/1 formula and leaves X alone
+// (queue_model_history_tree.cc:58-64, queue_model_m_g_1.cc:17-46), any other one is
+// FIFO, and the first idle cycle makes a gap that ends this for good (:79-86;
+// max_list_size >= 3 never prunes it).  A step of such a port first scans FIFO
+// (mode_scan): if the branch cannot fire before the first gap, the row-parallel
+// emit is exact; otherwise the window's records go through serial_step (kernels.hip,
+// the level engine's restatement) in order (mg_emit).
+
+// FIFO scan of the window from the carried tail Xr: the first record that finds the
+// queue idle (a gap), the first the branch would serve, and sum p^2 (the M/G/1 sums).
+template <typename CycF>
+__device__ __forceinline__ void mode_scan(const uint64_t (&rk)[ROWS], const uint32_t (&ra)[ROWS], uint32_t n, uint32_t Xr,
+                                          CycF cyc, uint32_t& fgap, uint32_t& ffire, uint64_t& sp2)
+{
+   const uint32_t lane = threadIdx.x;
+   uint32_t Xc = Xr;
+   uint64_t s2 = 0;
+   fgap = ffire = NONE;
+#pragma unroll
+   for (int r = 0; r < ROWS; r++)
+   {
+      if ((uint32_t) r * T >= n) break;
+      const uint32_t p0 = (uint32_t) r * T;
+      const bool valid = p0 + lane < n;
+      const uint32_t tc = cyc((uint32_t) (rk[r] >> 32));
+      const uint32_t p = aux_F(ra[r]);
+      uint32_t A = valid ? p : 0u, B = valid ? tc + p : 0u;
+      wave_scan(A, B);
+      const uint32_t exA = dpp32<0x138, 0xF, 0xF>(A), exB = dpp32<0x138, 0xF, 0xF>(B);   // wave_shr 1
+      const uint32_t xa = Xc + exA;
+      const uint32_t Xb = xa > exB ? xa : exB;
+      const uint64_t gm = __ballot(valid && tc > Xb), fm = __ballot(valid && Xb > tc + p);
+      if (fgap == NONE && gm) fgap = p0 + (uint32_t) __builtin_ctzll(gm);
+      if (ffire == NONE && fm) ffire = p0 + (uint32_t) __builtin_ctzll(fm);
+      const uint32_t Xm = Xb > tc ? Xb : tc;
+      Xc = rdl(Xm + p, (int) min(63u, n - 1 - p0));
+      s2 += valid ? (uint64_t) p * p : 0ull;
+   }
+   sp2 = rdl64(wave_sum64(s2), 63);
+}
+
+// The window's records in order through serial_step, uniform across the wave (lane 0
+// stores).  FIFO-served records take the next FIFO position of their field as in the
+// row-parallel emit; an M/G/1-served one may leave FIFO order: kept, it joins the
+// kept list (sorted afterwards), turning, it goes to the exception tail of its output
+// slot (nexc; k_exc_merge puts the tails in order before the next phase, k_level reads
+// them), spilled, the step fails (it would break the spill ranges' order).  A kept
+// record after a spilled one fails too (the kept records must stay a prefix of the
+// window's continuing records).  mst: lanes 0-3 the M/G/1 sums in and out.
+struct MgOut
+{
+   uint64_t ssum, X, maxdep;
+   uint32_t nkeep, mode, mg1;
+   bool rte, spilled, bad;
+};
+// (only in the MG instantiation of k_chain: its serial loop raises the register
+// allocation, and the common kernel should not pay for it)
+template <bool F1>
+__device__ __forceinline__ MgOut mg_emit(Smem& sm, const ChainArgs& a, const uint64_t (&rk)[ROWS], const uint32_t (&ra)[ROWS],
+                                         uint32_t n, uint32_t fpack, uint32_t wr, uint32_t d0, uint64_t wb, uint64_t wbase,
+                                         uint32_t wlen, uint32_t Xr, uint64_t& mst, uint32_t pd0, uint32_t P0n, uint32_t& run_t)
+{
+   const double fq = a.c.f;
+   const gptr<Rec> recs = (gptr<Rec>) a.recs;
+   const gptr<uint64_t> samp_t = (gptr<uint64_t>) a.samp_t;
+   const gptr<uint32_t> samp_id = (gptr<uint32_t>) a.samp_id;
+   auto cyc = [&](uint32_t off) -> uint32_t {
+      if (F1) return rcyc(off, wr, d0);
+      return (uint32_t) (cyc_of<false>(wbase + off, fq) - wb);
+   };
+   auto cps = [&](uint64_t cc) -> uint64_t { return F1 ? cc * 1000ull : ps_of<false>(cc, fq); };
+   const uint32_t lane = threadIdx.x;
+   const uint32_t nx = rdl(pd0, PD_NX), ny = rdl(pd0, PD_NY), rl = rdl(pd0, PD_RL), dir = rdl(pd0, 19);
+   const uint32_t ntile = ny * a.c.W + nx, nside = in_side_after(dir);
+   uint32_t rf[4], ob[4], oc[4], osl[4];
+#pragma unroll
+   for (int f = 0; f < 4; f++)
+   {
+      rf[f] = rdl(run_t, 1 + f);
+      ob[f] = rdl(pd0, PD_OBASE + f);
+      oc[f] = rdl(pd0, PD_OCAP + f);
+      const uint32_t fd = f == 0 ? P_SELF : f == 1 ? dir : f == 2 ? P_UP : P_DOWN;
+      osl[f] = slot_of(ntile, fd, slot_side(fd, nside));
+   }
+   SerialState st;
+   st.X = wb + Xr;
+   st.g = 0;
+   st.mode = 1;
+   st.narr = rdl64(mst, 0);
+   st.s1 = (double) rdl64(mst, 1);
+   st.s2 = (double) rdl64(mst, 2);
+   st.newest = rdl64(mst, 3);
+   st.mg1 = 0;
+   MgOut o{};
+   bool kept_exc = false;
+#pragma unroll
+   for (int r = 0; r < ROWS; r++)
+   {
+      if ((uint32_t) r * T >= n) break;
+      const uint32_t m = min((uint32_t) T, n - (uint32_t) r * T);
+      for (uint32_t L = 0; L < m; L++)
+      {
+         const uint64_t key = rdl64(rk[r], (int) L);
+         const uint32_t ax = rdl(ra[r], (int) L);
+         const uint32_t off = (uint32_t) (key >> 32), id = (uint32_t) key;
+         const uint32_t f = (rdl(fpack, (int) L) >> (2 * r)) & 3u;
+         const uint64_t tca = wb + cyc(off);
+         const uint64_t F = aux_F(ax);
+         const uint64_t mg0 = st.mg1;
+         const uint64_t d = serial_step(st, tca, F, (int) a.c.max_list, a.c.analytical);
+         const bool exc = st.mg1 != mg0;
+         o.ssum += d;
+         const uint64_t dep = tca + d + F;
+         o.maxdep = dep > o.maxdep ? dep : o.maxdep;
+         const uint64_t dn = (uint64_t) off + cps(d) + rl;   // t' - wbase
+         if (f == 1 && dn < wlen)
+         {
+            if (o.spilled) o.bad = true;                      // kept after a spill
+            if (lane == 0)
+            {
+               sm.key[rf[1] - P0n] = (dn << 32) | id;
+               sm.aux[rf[1] - P0n] = ax;
+            }
+            rf[1]++;
+            o.nkeep++;
+            kept_exc |= exc;
+         }
+         else if (f == 1 || !exc)
+         {
+            if (f == 1 && exc) o.bad = true;                  // an M/G/1-served spill
+            if (rf[f] >= oc[f]) o.rte = true;
+            else if (lane == 0) out_record(recs, samp_t, samp_id, (uint64_t) ob[f] + rf[f], wbase + dn, id, ax, f == 1);
+            o.spilled |= f == 1;
+            rf[f]++;
+         }
+         else if (lane == 0)
+         {
+            // M/G/1-served turn: the exception tail of its output slot (level.hip does the same)
+            const uint32_t x = atomicAdd(a.nexc + osl[f], 1u);
+            atomicOr(a.errflag + 2, 1u);
+            if (x >= oc[f]) atomicOr(a.errflag, 1u);
+            else
+            {
+               const gptr<uint64_t> q = (gptr<uint64_t>) (recs + (uint64_t) ob[f] + oc[f] - 1 - x);
+               __hip_atomic_store(q, wbase + dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+               __hip_atomic_store(q + 1, (uint64_t) id | ((uint64_t) ax << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+         }
+      }
+   }
+   wsync();
+   if (kept_exc && lane == 0)
+   {
+      // the kept list into (t, id) order: nearly sorted (insertion sort)
+      for (uint32_t i = 1; i < o.nkeep; i++)
+      {
+         const uint64_t k = sm.key[i];
+         const uint32_t v = sm.aux[i];
+         uint32_t j = i;
+         while (j > 0 && sm.key[j - 1] > k)
+         {
+            sm.key[j] = sm.key[j - 1];
+            sm.aux[j] = sm.aux[j - 1];
+            j--;
+         }
+         sm.key[j] = k;
+         sm.aux[j] = v;
+      }
+   }
+   wsync();
+   run_t = lane == 1 ? rf[0] : lane == 2 ? rf[1] : lane == 3 ? rf[2] : lane == 4 ? rf[3] : 0u;
+   o.X = st.X;
+   o.mode = st.g == 0 ? 1u : 0u;
+   o.mg1 = (uint32_t) st.mg1;
+   const uint64_t s1 = (uint64_t) st.s1, s2 = (uint64_t) st.s2;
+   mst = lane == 0 ? st.narr : lane == 1 ? s1 : lane == 2 ? s2 : lane == 3 ? st.newest : 0ull;
+   o.bad |= st.newest > M48 || s2 > M48 || st.narr > M48;
+   return o;
+}
+
+// The M/G/1 sums after a window served FIFO with no gap (every request updates them,
+// queue_model_history_tree.cc:118): n requests, sum p, sum p^2; newest = the last
+// departure (FIFO: the tail).  mg_emit already did it for its window.
+__device__ __forceinline__ uint64_t mg_after(uint64_t mst, bool mg, uint32_t n, uint32_t totA, uint64_t sp2, uint64_t Xo)
+{
+   if (mg) return mst;
+   const uint32_t lane = threadIdx.x;
+   if (lane == 0) return mst + n;
+   if (lane == 1) return mst + totA;
+   if (lane == 2) return mst + sp2;
+   if (lane == 3) return mst > Xo ? mst : Xo;
+   return mst;
+}
+// Every output slot filled: per route field, the FIFO records written plus the
+// slot's exception tail (M/G/1-served turns) equal its capacity.
+__device__ __forceinline__ bool route_filled(const ChainArgs& a, uint32_t pd0, uint32_t run_t, uint32_t ocf_t)
+{
+   const uint32_t lane = threadIdx.x;
+   bool bad = lane - 1u < 4u && run_t != ocf_t;
+   if (!__any(bad)) return true;
+   const uint32_t nx = rdl(pd0, PD_NX), ny = rdl(pd0, PD_NY), dir = rdl(pd0, 19);
+   if (bad)
+   {
+      const uint32_t f = lane - 1u;
+      const uint32_t fd = f == 0 ? P_SELF : f == 1 ? dir : f == 2 ? P_UP : P_DOWN;
+      const uint32_t sl = slot_of(ny * a.c.W + nx, fd, slot_side(fd, in_side_after(dir)));
+      bad = f == 1 || run_t + __hip_atomic_load(a.nexc + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ocf_t;
+   }
+   return !__any(bad);
+}
 
 // ---------------------------------------------------------------------------
 // the fused launch (k_chain_xy): a Y task's dependence on the launch's X tasks
@@ -760,7 +1020,7 @@ __device__ __forceinline__ uint64_t state_word_ser(uint32_t lane, uint64_t Xo, u
    if (lane == 7) v = Pend;
    return v;
 }
-template <int NL, bool F1, bool FU>
+template <int NL, bool F1, bool FU, bool MG = false>
 __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk, uint32_t aux)
 {
    constexpr bool XC = NL == 1;
@@ -844,6 +1104,7 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
       uint32_t totA = 0, totB = 0;
       bool first = true, published = false;
       uint32_t Xr = 0, mode = mode0, Kpp = 0, Pep = 0, Kout = 0, Pend = 0;
+      uint64_t mst = 0;   // lanes 0-3: the M/G/1 sums while the queue has had no gap (window 0: none yet)
       uint32_t cin_t = 0;
       const uint32_t itot = itot_f;
       for (;;)
@@ -869,8 +1130,13 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
             totA += rA;
             const uint32_t f = route_field<XC>(nx, ny, ra[r]);
             fpack |= (valid ? f : 0u) << (2 * r);
-            const uint32_t inc = wave_sum32(valid ? 1u << (8 * f) : 0u);
-            tc_t += field_cnt(rdl(inc, 63), lane);
+            if (CH_BRANK)
+            {
+               uint64_t b0, b1;
+               tc_t += field_cnt(field_tot(valid, f, b0, b1), lane);
+            }
+            else
+               tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
          }
          if (!first) break;
          CH_STAMP(2);
@@ -903,8 +1169,17 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
             mode = (uint32_t) (rdl64(pv, 5) & 1u);
             Kpp = (uint32_t) (rdl64(pv, 6) & M48);
             Pep = (uint32_t) (rdl64(pv, 7) & M48);
+            // no gap yet: the M/G/1 sums after window w-1 (published with its state; only
+            // the MG instantiation serves the branch, the other one declines where it fires)
+            if (MG && ok && mode)
+            {
+               uint64_t mv = 0;
+               ok = poll_words(a, stp + G_MG, 4, lane, mv);
+               mst = lane < 4u ? mv & M48 : 0ull;
+            }
          }
          CH_STAMP(4);
+         vm_drain();
          if (!ok) return;
          // window-relative tail: an earlier tail behaves like the base cycle (every tc > wb)
          const uint64_t xr = X_in > wb ? X_in - wb : 0;
@@ -997,6 +1272,16 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
       const uint32_t rl = rdl(pd0, PD_RL);
       // field tables (lane 1 + q): output slot base, capacity, records routed so far
       const uint32_t obf_t = bperm(pd0, lane - 1u), ocf_t = bperm(pd0, lane + 3u);
+      // (CH_BRANK) the same per field as wave-uniform values: output slot base, capacity,
+      // records routed so far
+      uint32_t ob_s[4], oc_s[4], rn_s[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+      {
+         ob_s[q] = rdl(pd0, PD_OBASE + q);
+         oc_s[q] = rdl(pd0, PD_OCAP + q);
+         rn_s[q] = rdl(cin_t, 1 + q);
+      }
       uint32_t run_t = cin_t;
       const uint32_t P0n = rdl(cin_t, 2);   // chain-direction records before this window
       const gptr<uint64_t> samp_t = sptr(a.samp_t);
@@ -1004,6 +1289,34 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
       uint64_t ssum = 0;
       uint32_t Xc = Xr, nkeep = 0, fgap = NONE, ffire = NONE;
       uint64_t rte = 0, spm = 0;   // lanes (over all rows) that overflowed an output slot / spilled
+      // a port with no gap yet: does the analytical branch fire before the first gap?
+      uint64_t sp2 = 0;
+      bool mg = false;
+      if (MG && mode)
+      {
+         // (the other instantiations find the first gap and firing in the output rows and
+         // decline after them: the serial path lives in the MG one, which the host
+         // switches a batch to after such a decline)
+         mode_scan(rk, ra, n, Xr, cyc, fgap, ffire, sp2);
+         mg = ffire != NONE && (fgap == NONE || ffire < fgap);
+      }
+      if (mg && FU)
+      {
+         // the fused launch's Y tasks read the X turns in-launch: no exception tails
+         if (lane == 0) flag(a, F_FALLBACK | R_MG1);
+         return;
+      }
+      MgOut mo{};
+      const bool mgr = MG && !FU && mg;   // this window went through mg_emit
+      if constexpr (MG && !FU)
+      {
+         if (mg)
+         {
+            mo = mg_emit<F1>(sm, a, rk, ra, n, fpack, wr, d0, wb, wbase, wlen, Xr, mst, pd0, P0n, run_t);
+            nkeep = mo.nkeep;
+         }
+      }
+      if (!mgr)
 #pragma unroll
       for (int r = 0; r < ROWS; r++)
       {
@@ -1025,7 +1338,7 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
          const uint32_t Xm = Xb > tc ? Xb : tc;
          const uint32_t cc = valid ? Xm - tc : 0u;
          const uint32_t Xa = Xm + p;
-         if (mode)
+         if (!MG && mode)
          {
             // history tree with no gap yet: an idle period makes one (:79-86); the M/G/1
             // branch fires while there is none and the tail lies beyond t + p (:58-64)
@@ -1038,14 +1351,29 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
          const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
          // route ranks: a packed (8 bits per field) prefix count over the row
          const uint32_t f = (fpack >> (2 * r)) & 3u;
-         const uint32_t one = valid ? 1u << (8 * f) : 0u;
-         const uint32_t inc = wave_sum32(one);
-         const uint32_t rank = ((inc - one) >> (8 * f)) & 0xFFu;
-         const uint32_t rtot = rdl(inc, 63);
-         const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
-         const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
-         const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
-         run_t += field_cnt(rtot, lane);
+         uint32_t rank, gb, room, kb;
+         if (CH_BRANK)
+         {
+            uint64_t b0, b1;
+            const uint32_t rtot = field_tot(valid, f, b0, b1);
+            rank = field_rank(f, b0, b1);
+            gb = sel4(f, ob_s[0] + rn_s[0], ob_s[1] + rn_s[1], ob_s[2] + rn_s[2], ob_s[3] + rn_s[3]);
+            room = sel4(f, oc_s[0] - rn_s[0], oc_s[1] - rn_s[1], oc_s[2] - rn_s[2], oc_s[3] - rn_s[3]);
+            kb = rn_s[1] - P0n;
+#pragma unroll
+            for (int q = 0; q < 4; q++) rn_s[q] += (rtot >> (8 * q)) & 0xFFu;
+         }
+         else
+         {
+            const uint32_t one = valid ? 1u << (8 * f) : 0u;
+            const uint32_t inc = wave_sum32(one);
+            rank = ((inc - one) >> (8 * f)) & 0xFFu;
+            const uint32_t rtot = rdl(inc, 63);
+            gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
+            room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
+            kb = rdl(run_t, 2) - P0n;              // kept records so far
+            run_t += field_cnt(rtot, lane);
+         }
          // continuing: kept (a prefix of the window's continuing records) or spilled;
          // everything else leaves through one 16-B write-through store (turns and spills
          // alike: a spill is read in-launch by task (chain, w+1), MI355X_MICROARCH.md
@@ -1064,32 +1392,45 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
          if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
       }
       CH_STAMP(6);
-      const bool spilled = spm != 0;
-      if (rte && lane == 0) flag(a, F_ROUTE);
+      if (CH_BRANK && !mgr) run_t = lane - 1u < 4u ? sel4(lane - 1u, rn_s[0], rn_s[1], rn_s[2], rn_s[3]) : run_t;
+      const bool spilled = mgr ? mo.spilled : spm != 0;
+      if ((mgr ? mo.rte : rte != 0) && lane == 0) flag(a, F_ROUTE);
+      if (mgr && mo.bad && lane == 0) flag(a, F_FALLBACK | R_MG1);
+      // (not the MG instantiation) the M/G/1 branch serves a request before the first gap
+      if (!MG && mode && ffire != NONE && (fgap == NONE || ffire < fgap))
+      {
+         if (lane == 0) flag(a, F_FALLBACK | R_MG1);
+         return;
+      }
       if (spilled && lastw && lane == 0) flag(a, F_FALLBACK | R_LASTSPILL);   // the last window keeps everything
-      const uint64_t ssw = rdl64(wave_sum64(ssum), 63);
+      const uint64_t ssw = mgr ? mo.ssum : rdl64(wave_sum64(ssum), 63);
       if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drained before the next publish
       wsync();
 
       // ---- [F] late publish (no gap yet), port counters, route check
       const uint32_t x0 = Xr + totA;
-      const uint64_t Xo = wb + (x0 > totB ? x0 : totB);
+      const uint64_t Xo = mgr ? mo.X : wb + (x0 > totB ? x0 : totB);
       if (!published && mode)
       {
-         // the M/G/1 branch would serve a request that arrives before the first gap
-         if (lane == 0 && ffire != NONE && (fgap == NONE || ffire < fgap)) flag(a, F_FALLBACK | R_MG1);
-         if (lane < (uint32_t) SW_SER) st1(stw + lane, a.etag | state_word_ser(lane, Xo, run_t, fgap == NONE ? 1u : 0u, Kout, Pend));
+         // the state after the window: still no gap -> the M/G/1 sums go along
+         const uint32_t mout = mgr ? mo.mode : (fgap == NONE ? 1u : 0u);
+         if (MG && mout) mst = mg_after(mst, mgr, n, totA, sp2, Xo);
+         if (lane < (uint32_t) SW_SER) st1(stw + lane, a.etag | state_word_ser(lane, Xo, run_t, mout, Kout, Pend));
+         if (MG && mout && lane < 4u) st1(stw + G_MG + lane, a.etag | mst);
       }
-      // every record of the port has passed at the last window: the route counts fill
-      // every output slot
-      if (lastw && __any(lane - 1u < 4u && run_t != ocf_t) && lane == 0) flag(a, F_ROUTE);
+      // every record of the port has passed at the last window: the route counts (and
+      // the exception tails) fill every output slot
+      // (only mg_emit writes exception tails of chain outputs)
+      if (lastw && (MG ? !route_filled(a, pd0, run_t, ocf_t) : __any(lane - 1u < 4u && run_t != ocf_t)) && lane == 0)
+         flag(a, F_ROUTE);
       if (lane == 0 && n)
       {
          const uint32_t port = rdl(pd0, PD_PORT);
          atomicAdd(&a.port_sum[port], (unsigned long long) ssw);
          atomicAdd(&a.port_cnt[port], (unsigned long long) n);
          atomicAdd(&a.port_flit[port], (unsigned long long) totA);
-         atomicMax(&a.port_last[port], (unsigned long long) Xo);
+         atomicMax(&a.port_last[port], (unsigned long long) (mgr && mo.maxdep > Xo ? mo.maxdep : Xo));
+         if (mgr && mo.mg1) atomicAdd(&a.port_mg1[port], (unsigned long long) mo.mg1);
       }
       nmax = n > nmax ? n : nmax;
       imax = itot > imax ? itot : imax;   // the next port's inserts (checked against ICAP at landing)
@@ -1140,7 +1481,7 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
 // ---------------------------------------------------------------------------
 // one task, look-back protocol (AGG / INC / KO / POST granules)
 // ---------------------------------------------------------------------------
-template <int NL, bool F1, bool FU>
+template <int NL, bool F1, bool FU, bool MG = false>
 __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk, uint32_t aux)
 {
    constexpr bool XC = NL == 1;
@@ -1253,7 +1594,13 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
             totA += rA;
             const uint32_t f = route_field<XC>(nx, ny, ra[r]);
             fpack |= (valid ? f : 0u) << (2 * r);
-            tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
+            if (CH_BRANK)
+            {
+               uint64_t b0, b1;
+               tc_t += field_cnt(field_tot(valid, f, b0, b1), lane);
+            }
+            else
+               tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
          }
          if (!first) break;
          first = false;
@@ -1409,6 +1756,7 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
       // model on) the exact state of window w-1 is needed: wait for its INC.
       uint64_t X_in = 0;
       uint32_t cin_t = 0, mode = mode0;
+      uint64_t mst = 0;   // lanes 0-3: the M/G/1 sums while the queue has had no gap (window 0: none yet)
       if (w)
       {
          // lanes [0, SW) hold window w - d, [SW, 2 SW) window w - d - 1; (cA, cB, ccnt_t) is the
@@ -1499,7 +1847,15 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
             ld_flag(a, lane, ef);
          }
       }
+      if (MG && w && mode)
+      {
+         // no gap yet after window w-1 (its own INC, d == 1): the M/G/1 sums it published
+         uint64_t mv = 0;
+         if (!poll_words(a, stw - SW + G_MG, 4, lane, mv)) return;
+         mst = lane < 4u ? mv & M48 : 0ull;
+      }
       CH_STAMP(4);
+      vm_drain();
       // window-relative tail: an earlier tail behaves like the base cycle (every tc > wb)
       const uint64_t xr = X_in > wb ? X_in - wb : 0;
       if (xr >= (1ull << 31))
@@ -1521,6 +1877,16 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
       const uint32_t rl = rdl(pd0, PD_RL);
       // field tables (lane 1 + q): output slot base, capacity, records routed so far
       const uint32_t obf_t = bperm(pd0, lane - 1u), ocf_t = bperm(pd0, lane + 3u);
+      // (CH_BRANK) the same per field as wave-uniform values: output slot base, capacity,
+      // records routed so far
+      uint32_t ob_s[4], oc_s[4], rn_s[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+      {
+         ob_s[q] = rdl(pd0, PD_OBASE + q);
+         oc_s[q] = rdl(pd0, PD_OCAP + q);
+         rn_s[q] = rdl(cin_t, 1 + q);
+      }
       uint32_t run_t = cin_t;
       const uint32_t P0n = rdl(cin_t, 2);   // chain-direction records before this window
       const gptr<uint64_t> samp_t = sptr(a.samp_t);
@@ -1528,6 +1894,34 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
       uint64_t ssum = 0;
       uint32_t Xc = Xr, nkeep = 0, fgap = NONE, ffire = NONE;
       uint64_t rte = 0, spm = 0;   // lanes (over all rows) that overflowed an output slot / spilled
+      // a port with no gap yet: does the analytical branch fire before the first gap?
+      uint64_t sp2 = 0;
+      bool mg = false;
+      if (MG && mode)
+      {
+         // (the other instantiations find the first gap and firing in the output rows and
+         // decline after them: the serial path lives in the MG one, which the host
+         // switches a batch to after such a decline)
+         mode_scan(rk, ra, n, Xr, cyc, fgap, ffire, sp2);
+         mg = ffire != NONE && (fgap == NONE || ffire < fgap);
+      }
+      if (mg && FU)
+      {
+         // the fused launch's Y tasks read the X turns in-launch: no exception tails
+         if (lane == 0) flag(a, F_FALLBACK | R_MG1);
+         return;
+      }
+      MgOut mo{};
+      const bool mgr = MG && !FU && mg;   // this window went through mg_emit
+      if constexpr (MG && !FU)
+      {
+         if (mg)
+         {
+            mo = mg_emit<F1>(sm, a, rk, ra, n, fpack, wr, d0, wb, wbase, wlen, Xr, mst, pd0, P0n, run_t);
+            nkeep = mo.nkeep;
+         }
+      }
+      if (!mgr)
 #pragma unroll
       for (int r = 0; r < ROWS; r++)
       {
@@ -1549,7 +1943,7 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
          const uint32_t Xm = Xb > tc ? Xb : tc;
          const uint32_t cc = valid ? Xm - tc : 0u;
          const uint32_t Xa = Xm + p;
-         if (mode)
+         if (!MG && mode)
          {
             // history tree with no gap yet: an idle period makes one (:79-86); the M/G/1
             // branch fires while there is none and the tail lies beyond t + p (:58-64)
@@ -1562,14 +1956,29 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
          const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
          // route ranks: a packed (8 bits per field) prefix count over the row
          const uint32_t f = (fpack >> (2 * r)) & 3u;
-         const uint32_t one = valid ? 1u << (8 * f) : 0u;
-         const uint32_t inc = wave_sum32(one);
-         const uint32_t rank = ((inc - one) >> (8 * f)) & 0xFFu;
-         const uint32_t rtot = rdl(inc, 63);
-         const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
-         const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
-         const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
-         run_t += field_cnt(rtot, lane);
+         uint32_t rank, gb, room, kb;
+         if (CH_BRANK)
+         {
+            uint64_t b0, b1;
+            const uint32_t rtot = field_tot(valid, f, b0, b1);
+            rank = field_rank(f, b0, b1);
+            gb = sel4(f, ob_s[0] + rn_s[0], ob_s[1] + rn_s[1], ob_s[2] + rn_s[2], ob_s[3] + rn_s[3]);
+            room = sel4(f, oc_s[0] - rn_s[0], oc_s[1] - rn_s[1], oc_s[2] - rn_s[2], oc_s[3] - rn_s[3]);
+            kb = rn_s[1] - P0n;
+#pragma unroll
+            for (int q = 0; q < 4; q++) rn_s[q] += (rtot >> (8 * q)) & 0xFFu;
+         }
+         else
+         {
+            const uint32_t one = valid ? 1u << (8 * f) : 0u;
+            const uint32_t inc = wave_sum32(one);
+            rank = ((inc - one) >> (8 * f)) & 0xFFu;
+            const uint32_t rtot = rdl(inc, 63);
+            gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
+            room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
+            kb = rdl(run_t, 2) - P0n;              // kept records so far
+            run_t += field_cnt(rtot, lane);
+         }
          // continuing: kept (a prefix of the window's continuing records) or spilled
          const bool keep = valid && f == 1 && dn < wlen;
          const bool out = valid && !keep;
@@ -1585,35 +1994,48 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
          if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
       }
       CH_STAMP(6);
-      const bool spilled = spm != 0;
-      if (rte && lane == 0) flag(a, F_ROUTE);
+      if (CH_BRANK && !mgr) run_t = lane - 1u < 4u ? sel4(lane - 1u, rn_s[0], rn_s[1], rn_s[2], rn_s[3]) : run_t;
+      const bool spilled = mgr ? mo.spilled : spm != 0;
+      if ((mgr ? mo.rte : rte != 0) && lane == 0) flag(a, F_ROUTE);
+      if (mgr && mo.bad && lane == 0) flag(a, F_FALLBACK | R_MG1);
+      // (not the MG instantiation) the M/G/1 branch serves a request before the first gap
+      if (!MG && mode && ffire != NONE && (fgap == NONE || ffire < fgap))
+      {
+         if (lane == 0) flag(a, F_FALLBACK | R_MG1);
+         return;
+      }
       if (spilled && lastw && lane == 0) flag(a, F_FALLBACK | R_LASTSPILL);   // the last window keeps everything
-      const uint64_t ssw = rdl64(wave_sum64(ssum), 63);
+      const uint64_t ssw = mgr ? mo.ssum : rdl64(wave_sum64(ssum), 63);
       if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drained before the next publish
       wsync();
 
       // ---- [F] late INC (no gap yet), POST, port counters, route check
       const uint32_t x0 = Xr + totA;
-      const uint64_t Xo = wb + (x0 > totB ? x0 : totB);
+      const uint64_t Xo = mgr ? mo.X : wb + (x0 > totB ? x0 : totB);
       if (mode)
       {
-         // the M/G/1 branch would serve a request that arrives before the first gap
-         if (lane == 0 && ffire != NONE && (fgap == NONE || ffire < fgap)) flag(a, F_FALLBACK | R_MG1);
-         if (lane < (uint32_t) G_AB) st1(stw + lane, a.etag | inc_word(lane, Xo, run_t, fgap == NONE ? 1u : 0u));
+         // the state after the window: still no gap -> the M/G/1 sums go along
+         const uint32_t mout = mgr ? mo.mode : (fgap == NONE ? 1u : 0u);
+         if (MG && mout) mst = mg_after(mst, mgr, n, totA, sp2, Xo);
+         if (MG && mout && lane < 4u) st1(stw + G_MG + lane, a.etag | mst);
+         if (lane < (uint32_t) G_AB) st1(stw + lane, a.etag | inc_word(lane, Xo, run_t, mout));
       }
       // POST: the chain outputs before this window and whether it kept any (the next
       // window's spill range at the next port, without waiting for its KO)
       if (lane == G_POST) st1(stw + G_POST, a.etag | (uint64_t) P0n | (uint64_t) nkeep << 32);
-      // every record of the port has passed at the last window: the route counts fill
-      // every output slot
-      if (lastw && __any(lane - 1u < 4u && run_t != ocf_t) && lane == 0) flag(a, F_ROUTE);
+      // every record of the port has passed at the last window: the route counts (and
+      // the exception tails) fill every output slot
+      // (only mg_emit writes exception tails of chain outputs)
+      if (lastw && (MG ? !route_filled(a, pd0, run_t, ocf_t) : __any(lane - 1u < 4u && run_t != ocf_t)) && lane == 0)
+         flag(a, F_ROUTE);
       if (lane == 0 && n)
       {
          const uint32_t port = rdl(pd0, PD_PORT);
          atomicAdd(&a.port_sum[port], (unsigned long long) ssw);
          atomicAdd(&a.port_cnt[port], (unsigned long long) n);
          atomicAdd(&a.port_flit[port], (unsigned long long) totA);
-         atomicMax(&a.port_last[port], (unsigned long long) Xo);
+         atomicMax(&a.port_last[port], (unsigned long long) (mgr && mo.maxdep > Xo ? mo.maxdep : Xo));
+         if (mgr && mo.mg1) atomicAdd(&a.port_mg1[port], (unsigned long long) mo.mg1);
       }
       nmax = n > nmax ? n : nmax;
       imax = itot > imax ? itot : imax;   // the next port's inserts (checked against ICAP at landing)
@@ -1659,7 +2081,7 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
    }
 }
 
-template <int NL, bool F1, bool LB>
+template <int NL, bool F1, bool LB, bool MG = false>
 __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
 {
    __shared__ Smem sm;
@@ -1682,8 +2104,8 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
       tk = rdl(tk, 0);
       if (tk >= ntasks || flagged(a)) return;
       const uint32_t cw = a.tasks[tk];
-      if (LB) task_lb<NL, F1, false>(sm, a, cw >> 16, cw & 0xFFFFu, tk, 0u);
-      else task_ser<NL, F1, false>(sm, a, cw >> 16, cw & 0xFFFFu, tk, 0u);
+      if (LB) task_lb<NL, F1, false, MG>(sm, a, cw >> 16, cw & 0xFFFFu, tk, 0u);
+      else task_ser<NL, F1, false, MG>(sm, a, cw >> 16, cw & 0xFFFFu, tk, 0u);
       wsync();
    }
 }

@@ -125,6 +125,10 @@ struct gnoc_engine
    hipStream_t s_h2d = nullptr, s_d2h = nullptr;
    hipEvent_t ev_h2d = nullptr, ev_done = nullptr, ev_fin = nullptr, ev_alt = nullptr;
    DevBuf t2_inj, t2_src, t2_dst, t2_bits, t2_flags, final_alt;
+   // gnoc_fetch_latency: k_finalize also writes final_ps - inject_ps as u32 (double
+   // buffered with final_ps) once a caller has asked for it; lat_ovf: one did not fit
+   DevBuf lat32, lat32_alt;
+   bool want_lat32 = false, lat_ovf = false, lat_written = false;
    DevBuf nw_stage, nw_stage2;               // narrow wire format (gnoc_packets_narrow) before widening
    bool staged_narrow = false;
    bool staged = false, fetched = false;
@@ -219,6 +223,7 @@ struct gnoc_engine
    int ch_ydeclined = 0;                    // only its Y phase did: later runs take X chains + Y levels (path 5)
    unsigned ch_yflags = 0;                  // the Y phase's chain flags of the last run that declined
    int exc_fix = 0;                         // this batch's injection level leaves exception tails: k_exc_merge
+   int ch_mg = 0;                           // this batch's chains meet the no-gap M/G/1 branch: k_chain's MG instantiation
    std::vector<std::pair<void*, uint64_t>> zq;   // buffers to zero before the first level launch (one k_zero_segs)
    int ch_resized = 0;                      // the windows were already changed during this (sharded) run
    int used_chain = 0;
@@ -673,6 +678,7 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
    e->ch_declined = 0;
    e->ch_ydeclined = 0;
    e->exc_fix = 0;
+   e->ch_mg = 0;
    if (same) return;
    const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size (2^shift ps)
    const char* pv = std::getenv("GNOC_WINDOW_PS");      // test knob: force the window size (ps)
@@ -1370,6 +1376,49 @@ int gnoc_fetch_final_ps(gnoc_engine* e, uint64_t* host_out, size_t n)
    return GNOC_OK;
 }
 
+int gnoc_fetch_latency(gnoc_engine* e, uint32_t* host_out, size_t n)
+{
+   if (!e || !host_out) return GNOC_EINVAL;
+   if (!e->ran) return fail(e, GNOC_ESTATE, "no results: call gnoc_run first");
+   if (e->part || e->nranks > 1) return fail(e, GNOC_EUNSUPPORTED, "a sharded rank's results: gnoc_get_packet_results");
+   if (n != e->n) return fail(e, GNOC_EINVAL, "n differs from the submitted batch");
+   if (e->nb) return fail(e, GNOC_EUNSUPPORTED, "broadcast batches: gnoc_get_packet_results");
+   if (e->ma_type && e->dc.contention) return fail(e, GNOC_EUNSUPPORTED, "moving-average queues: gnoc_fetch_final_ps");
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   if (!e->lat_written)
+   {
+      // the first call: the u32 array of the last run now (k_finalize again: the same
+      // zero-load and contention values), and every later run writes it in k_finalize
+      e->want_lat32 = true;
+      hipStream_t s = e->stream;
+      GNOC_HIP(e, e->lat32.ensure(n * 4 + 4));
+      unsigned* lovf = e->counters.as<unsigned>() + 8 + 6;
+      const uint32_t fin_grid = (uint32_t) std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 8192));
+      const int cf = e->dc.contention ? 0 : 1;
+      if (n && e->f1)
+         hipLaunchKernelGGL(k_finalize<true>, dim3(fin_grid), dim3(256), 0, s, e->dc, (uint64_t) n, e->d_inj, e->d_src,
+                            e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
+                            e->cont.as<uint64_t>(), cf, e->cx0, e->cx1, e->lat32.as<uint32_t>(), lovf);
+      else if (n)
+         hipLaunchKernelGGL(k_finalize<false>, dim3(fin_grid), dim3(256), 0, s, e->dc, (uint64_t) n, e->d_inj, e->d_src,
+                            e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
+                            e->cont.as<uint64_t>(), cf, e->cx0, e->cx1, e->lat32.as<uint32_t>(), lovf);
+      GNOC_HIP(e, hipGetLastError());
+      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
+      GNOC_HIP(e, hipStreamSynchronize(s));
+      e->lat_ovf = (((const unsigned*) (e->h_pinned + 8))[6] & 1u) != 0;
+      e->lat_written = true;
+   }
+   if (e->lat_ovf) return fail(e, GNOC_EUNSUPPORTED, "a packet latency of 2^32 ps or more: use gnoc_fetch_final_ps");
+   GNOC_HIP(e, pipe_streams(e));
+   GNOC_HIP(e, hipEventRecord(e->ev_done, e->stream));
+   GNOC_HIP(e, hipStreamWaitEvent(e->s_d2h, e->ev_done, 0));
+   if (n) GNOC_HIP(e, hipMemcpyAsync(host_out, e->lat32.p, n * 4, hipMemcpyDeviceToHost, e->s_d2h));
+   GNOC_HIP(e, hipEventRecord(e->ev_fin, e->s_d2h));
+   e->fetched = true;   // the next run writes the other buffers
+   return GNOC_OK;
+}
+
 int gnoc_fetch_wait(gnoc_engine* e)
 {
    if (!e) return GNOC_EINVAL;
@@ -1604,6 +1653,7 @@ constexpr int GNOC_CH_RETRY = 1001;      // a chain window overflowed LDS: small
 constexpr int GNOC_CH_FALLBACK = 1002;   // the chain engine cannot take this batch: level engine
 constexpr int GNOC_CH_EXC = 1003;        // only the injection level's exception tails: merge them, rerun
 constexpr int GNOC_CH_YFALL = 1004;      // only the Y chains declined: Y and SELF levels on k_level
+constexpr int GNOC_CH_MG = 1005;         // the chains met the M/G/1 branch: rerun on the MG instantiation
 
 // ---------------------------------------------------------------------------
 // v4: chain engine for the X and Y phases (chain.hip); INJ and SELF levels on k_level
@@ -1720,6 +1770,11 @@ static ChainArgs chain_args(gnoc_engine* e, int phase)
    a.stamps = nullptr;
    a.lookback = e->ch_lb_run[phase];
    a.fw = a.fw2 = phase ? 5u : 4u;
+   a.nexc = e->nexc.as<uint32_t>();
+   a.port_mg1 = e->port_mg1.as<unsigned long long>();
+   // the Y phase runs after k_exc_merge put the X phase's exception tails (M/G/1-served
+   // turns, chain.hip mg_emit) in order
+   if (phase && e->dc.analytical) a.excfix = 1;
    return a;
 }
 
@@ -1749,11 +1804,15 @@ static int chain_phase(gnoc_engine* e, int phase)
    const uint32_t grid = (uint32_t) std::min<uint64_t>((uint64_t) e->ch_grid, (uint64_t) a.ntasks);
    GNOC_HIP(e, hipEventRecord(e->ch_ev[phase][0], s));
    // f != 1 GHz: the copy with the reference's double ps <-> cycle conversions
-#define GNOC_CHAIN(NLV, F1V)                                                                                  \
-   do                                                                                                          \
-   {                                                                                                           \
-      if (a.lookback) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<NLV, F1V, true>), dim3(grid), dim3(ch::T), 0, s, a); \
-      else GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<NLV, F1V, false>), dim3(grid), dim3(ch::T), 0, s, a);         \
+   // (ch_mg: the batch's chains met the no-gap M/G/1 branch; the instantiation with
+   // the serial path, whose register allocation the common one does not pay for)
+#define GNOC_CHAIN(NLV, F1V)                                                                                         \
+   do                                                                                                                 \
+   {                                                                                                                  \
+      if (e->ch_mg && a.lookback) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<NLV, F1V, true, true>), dim3(grid), dim3(ch::T), 0, s, a); \
+      else if (e->ch_mg) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<NLV, F1V, false, true>), dim3(grid), dim3(ch::T), 0, s, a); \
+      else if (a.lookback) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<NLV, F1V, true>), dim3(grid), dim3(ch::T), 0, s, a); \
+      else GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain<NLV, F1V, false>), dim3(grid), dim3(ch::T), 0, s, a);                \
    } while (0)
    if (phase && e->f1) GNOC_CHAIN(3, true);
    else if (phase) GNOC_CHAIN(3, false);
@@ -1772,7 +1831,7 @@ static bool chain_fusable(const gnoc_engine* e)
 {
    const char* v = std::getenv("GNOC_XY");
    if (!v || !*v || std::atoi(v) == 0) return false;
-   if (e->nranks > 1 || e->ch_ydeclined || !e->ncpx || !e->ncpy || e->dc.H - 1 > 64) return false;
+   if (e->nranks > 1 || e->ch_ydeclined || e->ch_mg || !e->ncpx || !e->ncpy || e->dc.H - 1 > 64) return false;
    return !e->ch_trial;
 }
 
@@ -2105,17 +2164,25 @@ static int run_post_enqueue(gnoc_engine* e, bool closed_form)
    const size_t n = e->n;
    hipStream_t s = e->stream;
    const uint32_t fin_grid = (uint32_t) std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 8192));
+   uint32_t* lat = nullptr;
+   if (e->want_lat32 && n && !e->nb)
+   {
+      GNOC_HIP(e, e->lat32.ensure(n * 4));
+      lat = e->lat32.as<uint32_t>();
+   }
    if (n)
    {
+      unsigned* lovf = e->counters.as<unsigned>() + 8 + 6;   // errflag[6]
       if (e->f1)
          GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<true>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
                      e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
-                     e->cont.as<uint64_t>(), (int) closed_form, e->cx0, e->cx1);
+                     e->cont.as<uint64_t>(), (int) closed_form, e->cx0, e->cx1, lat, lovf);
       else
          GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<false>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj,
                      e->d_src, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
-                     e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), (int) closed_form, e->cx0, e->cx1);
+                     e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), (int) closed_form, e->cx0, e->cx1, lat, lovf);
    }
+   e->lat_written = lat != nullptr;
    if (e->nb)
    {
 #define GNOC_BFIN(F1V)                                                                                                \
@@ -2129,10 +2196,10 @@ static int run_post_enqueue(gnoc_engine* e, bool closed_form)
    }
    GNOC_HIP(e, hipEventRecord(e->ev1, s));
    GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, e->counters.p, 24, hipMemcpyDeviceToHost, s));
+   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
    if (!closed_form)
    {
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 3, e->gtot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
-      GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
       if (e->used_chain)
          GNOC_HIP(e, hipMemcpyAsync(e->h_nmax, e->ch_nmax.p, 8 * (e->h_cw[0].size() + e->h_cw[1].size()),
                                     hipMemcpyDeviceToHost, s));
@@ -2149,6 +2216,7 @@ static int run_post_check(gnoc_engine* e, bool closed_form)
    GNOC_HIP(e, hipEventElapsedTime(&ms, e->ev0, e->ev1));
    e->last_ms = ms;
    GNOC_HIP(e, prof_collect(e));
+   e->lat_ovf = (((const unsigned*) (e->h_pinned + 8))[6] & 1u) != 0;
    if (closed_form)
    {
       e->ran = true;
@@ -2183,6 +2251,10 @@ static int run_post_check(gnoc_engine* e, bool closed_form)
          std::snprintf(m, sizeof m, "internal: chain route-count invariant violated (flags 0x%x 0x%x)", ef[4], ef[5]);
          return fail(e, GNOC_EHIP, m);
       }
+      // the no-gap M/G/1 branch (and nothing the MG instantiation would decline again):
+      // rerun the chains with the serial path compiled in
+      if (!e->ch_mg && e->nranks <= 1 && (cf & ch::R_MG1) && !(cf & (ch::F_RETRY | ch::F_TIMEOUT)))
+         return GNOC_CH_MG;
       // only the Y chains declined, for a reason the level engine takes (the M/G/1
       // branch, a spill range, a hand-off timeout): the X phase's outputs stand
       e->ch_yflags = ef[5];
@@ -2234,6 +2306,8 @@ static int run_once(gnoc_engine* e)
       else
       {
          if (!rc) rc = chain_phase(e, 0);
+         // turns the X chains served by M/G/1 wait in exception tails: into order first
+         if (!rc && !e->ch_ydeclined && e->dc.analytical) rc = exc_merge(e);
          if (!rc && !e->ch_ydeclined) rc = chain_phase(e, 1);
       }
       const char* xv = std::getenv("GNOC_CHAIN_EXPERIMENT");
@@ -2513,6 +2587,7 @@ static int run_impl(gnoc_engine* e)
       // other buffer, once that buffer's own read-back (two runs ago) has ended
       GNOC_HIP(e, hipSetDevice(e->cfg.device));
       e->final_ps.swap(e->final_alt);
+      e->lat32.swap(e->lat32_alt);
       std::swap(e->ev_fin, e->ev_alt);
       GNOC_HIP(e, hipStreamWaitEvent(e->stream, e->ev_fin, 0));
       e->fetched = false;
@@ -2566,6 +2641,12 @@ static int run_impl(gnoc_engine* e)
             continue;
          }
          if (rc == GNOC_CH_EXC) rc = GNOC_CH_FALLBACK;
+         if (rc == GNOC_CH_MG)
+         {
+            e->ch_mg = 1;
+            e->n_retry++;
+            continue;
+         }
          // halve the windows of the chains that overflowed (all, when none is marked)
          if (rc == GNOC_CH_RETRY && halvings < 3 && halve_overflowed(e, e->chD_run))
          {
@@ -3111,10 +3192,12 @@ static int finish_enqueue(gnoc_engine* e, const void* recv_buf)
       GNOC_HIP(e, hipGetLastError());
    }
    const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
-   int rc;
+   int rc = GNOC_OK;
    if (e->used_chain)
    {
-      rc = chain_phase(e, 1);
+      // exception tails (M/G/1-served turns, here or at a peer) into order for the Y chains
+      if (e->dc.analytical) rc = exc_merge(e);
+      if (!rc) rc = chain_phase(e, 1);
       if (!rc) rc = run_levels_v3(e, L - 1, L);
    }
    else
@@ -3261,7 +3344,7 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
    while (sh < 63 && (2ull << sh) <= dm[0]) sh++;
    out->window_shift = e->used_chain ? sh : 0u;
    out->windows_y = nwm[1];
-   out->chain_protocol = e->used_chain ? 0x100u | e->ch_lb_run[0] | (e->ch_lb_run[1] << 1) | (e->ch_fused ? 0x200u : 0u) : 0u;
+   out->chain_protocol = e->used_chain ? 0x100u | e->ch_lb_run[0] | (e->ch_lb_run[1] << 1) | (e->ch_fused ? 0x200u : 0u) | (e->ch_mg ? 0x400u : 0u) : 0u;
    out->window_ps_x = dm[0];
    out->window_ps_y = dm[1];
    out->runs = e->runs;

@@ -647,8 +647,11 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
                                                   const uint32_t* __restrict__ src, const uint32_t* __restrict__ aux,
                                                   const uint8_t* __restrict__ routed, uint64_t* __restrict__ final_ps,
                                                   uint64_t* __restrict__ zl, uint64_t* __restrict__ cont, int closed_form,
-                                                  uint32_t cx0, uint32_t cx1)
+                                                  uint32_t cx0, uint32_t cx1, uint32_t* __restrict__ lat32,
+                                                  unsigned* __restrict__ lat_ovf)
 {
+   // lat32 (gnoc_fetch_latency): final_ps - inject_ps as u32; one that does not fit
+   // sets *lat_ovf.  Undelivered (other rank) and broadcast packets are not written.
    for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
    {
       const uint32_t dx = aux_dx(aux[i]), dy = aux_dy(aux[i]);
@@ -656,7 +659,18 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
       // others are zeroed when results are read (k_mask_unowned), not here
       if (dx < cx0 || dx >= cx1) continue;
       if (aux[i] & AUX_BC) continue;   // k_bcast_final
-      if (!(routed[i] & 1)) { zl[i] = 0; cont[i] = 0; continue; }
+      if (!(routed[i] & 1))
+      {
+         zl[i] = 0;
+         cont[i] = 0;
+         if (lat32)
+         {
+            const uint64_t l = final_ps[i] - inj[i];
+            lat32[i] = (uint32_t) l;
+            if (l >> 32) atomicOr(lat_ovf, 1u);
+         }
+         continue;
+      }
       uint32_t sx, sy;
       tile_xy(src[i], c.W, c.magicW, sx, sy);
       const uint64_t hops = (uint64_t) ((sx > dx ? sx - dx : dx - sx) + (sy > dy ? sy - dy : dy - sy) + 1);
@@ -666,7 +680,13 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
                                        : ps_of<F1>(0, c.f) + hops * rl_of(c, src[i]) + ps_of<F1>(aux_F(aux[i]), c.f);
       zl[i] = z;
       if (closed_form) final_ps[i] = inj[i] + z;
-      cont[i] = final_ps[i] - inj[i] - z;
+      const uint64_t l = final_ps[i] - inj[i];
+      cont[i] = l - z;
+      if (lat32)
+      {
+         lat32[i] = (uint32_t) l;
+         if (l >> 32) atomicOr(lat_ovf, 1u);
+      }
    }
 }
 
@@ -784,8 +804,10 @@ template __global__ void k_bcast_final<false>(DevCfg, const uint32_t*, const uin
                                               const uint8_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t*,
                                               uint64_t*, int);
 template __global__ void k_finalize<true>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,
-                                          const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int, uint32_t, uint32_t);
+                                          const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int, uint32_t, uint32_t,
+                                          uint32_t*, unsigned*);
 template __global__ void k_finalize<false>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,
-                                           const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int, uint32_t, uint32_t);
+                                           const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int, uint32_t, uint32_t,
+                                           uint32_t*, unsigned*);
 
 }  // namespace gnoc

@@ -45,7 +45,7 @@ EXPORTED = (
     "gnoc_create_sweep", "gnoc_sweep_layout", "gnoc_get_port_utilization", "gnoc_create_hop_counter",
     "gnoc_get_broadcast_results", "gnoc_get_broadcast_info", "gnoc_set_basic_moving_average",
     "gnoc_build_id", "gnoc_rccl_unique_id", "gnoc_rccl_comm_init", "gnoc_rccl_comm_destroy",
-    "gnoc_submit_async", "gnoc_submit_commit", "gnoc_fetch_final_ps", "gnoc_fetch_wait",
+    "gnoc_submit_async", "gnoc_submit_commit", "gnoc_fetch_final_ps", "gnoc_fetch_latency", "gnoc_fetch_wait",
     "gnoc_submit_narrow", "gnoc_submit_async_narrow",
 )
 
@@ -200,6 +200,7 @@ def load() -> ctypes.CDLL:
         lib.gnoc_submit_async.argtypes = [vp, ctypes.POINTER(GnocPackets), sz]
         lib.gnoc_submit_commit.argtypes = [vp]
         lib.gnoc_fetch_final_ps.argtypes = [vp, vp, sz]
+        lib.gnoc_fetch_latency.argtypes = [vp, vp, sz]
         lib.gnoc_fetch_wait.argtypes = [vp]
     lib.gnoc_shard_set_comm.argtypes = [vp, vp]
     lib.gnoc_run_sharded.argtypes = [vp]
@@ -498,6 +499,13 @@ class Engine:
         the batch size); complete after fetch_wait()."""
         assert out.dtype.itemsize == 8 and out.shape[0] == self._n and out.flags["C_CONTIGUOUS"]
         self._check(self.lib.gnoc_fetch_final_ps(self._h, out.ctypes.data, self._n))
+
+    def fetch_latency(self, out: np.ndarray) -> None:
+        """Start copying the last run's per-packet latency (final_ps - inject_ps, u32
+        ps) into `out` (page-locked uint32 of the batch size): half the bytes of
+        final_ps; complete after fetch_wait()."""
+        assert out.dtype.itemsize == 4 and out.shape[0] == self._n and out.flags["C_CONTIGUOUS"]
+        self._check(self.lib.gnoc_fetch_latency(self._h, out.ctypes.data, self._n))
 
     def fetch_wait(self) -> None:
         self._check(self.lib.gnoc_fetch_wait(self._h))

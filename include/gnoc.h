@@ -170,7 +170,9 @@ typedef struct gnoc_summary
                                    engine ran; bit 0 / bit 1 set when the X / Y phase used the
                                    look-back protocol (else serial; look-back is kept only when it
                                    measured > 5% faster than serial on the batch's windows); bit 9
-                                   set when both phases ran in one fused launch */
+                                   set when both phases ran in one fused launch; bit 10 set when
+                                   the chains ran the no-gap M/G/1 prefix serially (the batch
+                                   meets the history tree's analytical branch in mesh ports) */
    uint64_t window_ps_x;        /* window length (ps) of the X phase                     */
    uint64_t window_ps_y;        /* ... of the Y phase                                    */
    /* since the last gnoc_submit: runs, and the retries / fallbacks of all of them
@@ -380,6 +382,13 @@ int gnoc_submit_async(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
 int gnoc_submit_async_narrow(gnoc_engine *eng, const gnoc_packets_narrow *pk, size_t n);
 int gnoc_submit_commit(gnoc_engine *eng);
 int gnoc_fetch_final_ps(gnoc_engine *eng, uint64_t *final_ps_out, size_t n);
+/* The narrow read-back: per packet latency_ps = final_ps - inject_ps (NetPacket::time
+ * minus its send time, network.cc:215-262) as u32, half the bytes of final_ps.
+ * Pipelined like gnoc_fetch_final_ps (same double buffering, gnoc_fetch_wait).
+ * GNOC_EUNSUPPORTED if a latency of the last run is 2^32 ps or more (then read
+ * final_ps).  The run writes the u32 array only once a caller has asked for it
+ * (the first call reads it after the next run). */
+int gnoc_fetch_latency(gnoc_engine *eng, uint32_t *latency_ps_out, size_t n);
 int gnoc_fetch_wait(gnoc_engine *eng);
 
 const char *gnoc_last_error(const gnoc_engine *eng);

@@ -97,7 +97,25 @@ typedef struct
    /* counters */
    uint64_t mg1_uses;     /* _total_requests_using_analytical_model        */
    uint64_t total_requests, util_cycles, last_request_time; /* queue_model.cc:40-53 */
+   void *ext;             /* history_tree through orc_set_queue_hooks: the hook's queue */
 } orc_queue;
+
+/* Optional history-tree queues from outside (bench.py's CPU baseline: the reference's
+ * own IntervalTree + QueueModelMG1, oracle/ref_driver.cc over oracle/_ref); NULL: the
+ * sorted-array restatement below. */
+static void *(*hk_create)(int, int, uint64_t);
+static uint64_t (*hk_compute)(void *, uint64_t, uint64_t);
+static uint64_t (*hk_mg1_uses)(void *);
+static void (*hk_destroy)(void *);
+
+ORC_EXPORT void orc_set_queue_hooks(void *(*create)(int, int, uint64_t), uint64_t (*compute)(void *, uint64_t, uint64_t),
+                                    uint64_t (*mg1_uses)(void *), void (*destroy)(void *))
+{
+   hk_create = create;
+   hk_compute = compute;
+   hk_mg1_uses = mg1_uses;
+   hk_destroy = destroy;
+}
 
 /* QueueModel::create(type, min_processing_time), queue_model.cc:18-38.
  * basic: moving average disabled (queue_model_basic.cc:7-30 with
@@ -120,6 +138,7 @@ ORC_EXPORT orc_queue *orc_queue_create_type(int type, int max_list_size, int ana
    q->iv[0].first = 0;
    q->iv[0].second = UINT64_MAX;
    q->n = 1;
+   if (type == ORC_Q_HISTORY_TREE && hk_create) q->ext = hk_create(max_list_size, analytical, min_proc);
    return q;
 }
 
@@ -196,12 +215,13 @@ ORC_EXPORT orc_queue *orc_queue_create(int max_list_size, int analytical, uint64
 ORC_EXPORT void orc_queue_destroy(orc_queue *q)
 {
    if (!q) return;
+   if (q->ext && hk_destroy) hk_destroy(q->ext);
    free(q->ma_list);
    free(q->iv);
    free(q);
 }
 
-ORC_EXPORT uint64_t orc_queue_mg1_uses(const orc_queue *q) { return q->mg1_uses; }
+ORC_EXPORT uint64_t orc_queue_mg1_uses(const orc_queue *q) { return q->ext ? hk_mg1_uses(q->ext) : q->mg1_uses; }
 ORC_EXPORT int orc_queue_size(const orc_queue *q) { return q->n; }
 
 static void iv_remove(orc_queue *q, int i)
@@ -374,6 +394,12 @@ ORC_EXPORT uint64_t orc_queue_compute(orc_queue *q, uint64_t t, uint64_t p)
 {
    if (q->type == ORC_Q_BASIC) return basic_queue_delay(q, t, p);
    if (q->type == ORC_Q_HISTORY_LIST) return hl_queue_delay(q, t, p);
+   if (q->ext)
+   {
+      const uint64_t dh = hk_compute(q->ext, t, p);
+      util_update(q, t, p, dh);
+      return dh;
+   }
    uint64_t d = UINT64_MAX;
    const uint64_t m = q->min_proc;
 
@@ -742,7 +768,7 @@ ORC_EXPORT int orc_run(int mesh_width, int mesh_height, int flit_width,
    {
       for (size_t p = 0; p < nports; p++)
       {
-         port_mg1[p] = q[p]->mg1_uses;
+         port_mg1[p] = orc_queue_mg1_uses(q[p]);
          /* QueueModel::getQueueUtilization's operands, queue_model.cc:49-62 */
          if (port_flits) port_flits[p] = q[p]->util_cycles;
          if (port_last) port_last[p] = q[p]->last_request_time;

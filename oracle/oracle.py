@@ -165,10 +165,26 @@ class OracleResult:
     bcast_zero_load_ps: np.ndarray = None
 
 
-def run(cfg, tr) -> OracleResult:
+def run(cfg, tr, ref_queues: bool = False) -> OracleResult:
     """Event-driven reference walk of every packet (see gnoc_oracle.c).  cfg is a
-    graphite_amd.gnoc.EngineConfig-like object, tr a Trace-like object."""
+    graphite_amd.gnoc.EngineConfig-like object, tr a Trace-like object.
+    ref_queues: the history-tree queues are the reference's own IntervalTree and
+    QueueModelMG1 objects (oracle/_ref, compiled from its sources; ref_driver.cc
+    restates only computeQueueDelay's 80 lines over them) instead of the sorted-array
+    restatement: bench.py's CPU baseline.  Needs oracle/_ref (ValueError otherwise)."""
     L = lib()
+    if ref_queues:
+        R = ref_lib()
+        if R is None:
+            raise ValueError("oracle/_ref is not built (needs /root/reference at build time)")
+        vp = ctypes.c_void_p
+        L.orc_set_queue_hooks.argtypes = [vp, vp, vp, vp]
+        L.orc_set_queue_hooks(*(ctypes.cast(getattr(R, f), vp) for f in
+                                ("ref_queue_create", "ref_queue_compute", "ref_queue_mg1_uses", "ref_queue_destroy")))
+        try:
+            return run(cfg, tr)
+        finally:
+            L.orc_set_queue_hooks(None, None, None, None)
     n = int(tr.inject_ps.shape[0])
     W, H = cfg.width, cfg.height
     inj = np.ascontiguousarray(tr.inject_ps, np.uint64)

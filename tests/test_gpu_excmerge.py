@@ -122,6 +122,10 @@ def column_burst_trace(W, H, ax, ay, k, seed, tail=3000):
 
 @pytest.mark.parametrize("W,ax,ay,k", [(8, 3, 4, 14), (8, 6, 1, 20), (16, 9, 8, 24)])
 def test_y_only_mg1_keeps_x_on_chain(W, ax, ay, k):
+    """M/G/1 in Y ports only: the first run's Y chains decline for the analytical
+    branch and the batch reruns on k_chain's MG instantiation (engine path 4, one
+    retry, chain_protocol bit 10), or -- when the serial prefix itself declines -- its
+    Y and SELF levels run on k_level (engine path 5, one fallback).  Bit-exact either way."""
     cfg = gnoc.EngineConfig(num_tiles=W * W)
     tr = column_burst_trace(W, W, ax, ay, k, seed=W * 7 + k)
     ref = oracle.run(cfg, tr)
@@ -130,11 +134,18 @@ def test_y_only_mg1_keeps_x_on_chain(W, ax, ay, k):
     assert mg[:, [1, 2]].sum() == 0                      # none in LEFT / RIGHT
     eng = gnoc.Engine(cfg)
     eng.submit(tr)
+    paths = []
     for r in range(3):
         eng.run()
         got = eng.results()
         same(got, ref)
         s = got.summary
-        assert s["engine_path"] == 5, s
-        assert s["fallbacks"] == (1 if r == 0 else 0), s
+        paths.append(int(s["engine_path"]))
+        if s["engine_path"] == 4:
+            assert s["fallbacks"] == 0 and s["chain_protocol"] & 0x400, s
+            assert s["retries"] == (1 if r == 0 else 0), s
+        else:
+            assert s["engine_path"] == 5, s
+            assert s["fallbacks"] == (1 if r == 0 else 0), s
     eng.close()
+    print("engine paths", paths)

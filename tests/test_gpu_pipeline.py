@@ -100,3 +100,59 @@ def test_narrow_wire_format_matches_wide():
     big.bits[0] = 1 << 16
     with pytest.raises(ValueError):
         gnoc.NarrowTrace.of(big)
+
+
+def test_pipelined_latency_readback_matches_final_ps():
+    """gnoc_fetch_latency: the u32 latency (final_ps - inject_ps) read back on the
+    copy stream, pipelined across batches of different sizes; the first call of an
+    engine computes the array of the run before it, later runs write it in k_finalize."""
+    cfg = gnoc.EngineConfig(num_tiles=256)
+    trs = [gnoc.synthetic_trace(16, 16, ld, ppt, seed=s) for ld, ppt, s in
+           ((0.01, 400, 1), (0.03, 250, 2), (0.05, 150, 4))]
+    want = []
+    eng = gnoc.Engine(cfg)
+    for tr in trs:
+        eng.submit(tr)
+        eng.run()
+        want.append((eng.results().final_ps - tr.inject_ps).astype(np.uint32))
+    eng.close()
+    ptrs = [pinned(tr.normalized()) for tr in trs]
+    outs = [torch.empty(len(tr), dtype=torch.int32, pin_memory=True).numpy().view(np.uint32) for tr in trs]
+    eng = gnoc.Engine(cfg)
+    eng.submit(ptrs[0])
+    for k in range(len(trs)):
+        if k + 1 < len(trs):
+            eng.submit_async(ptrs[k + 1])
+        eng.run()
+        eng.fetch_latency(outs[k])
+        if k + 1 < len(trs):
+            eng.submit_commit()
+    eng.fetch_wait()
+    eng.close()
+    for k in range(len(trs)):
+        assert np.array_equal(outs[k], want[k]), f"batch {k}"
+
+
+def test_latency_readback_refuses_overflow():
+    """A latency of 2^32 ps or more cannot be read back as u32: a burst of 130 K
+    36-flit packets into one tile at cycle 0 (FIFO queues) queues the last one ~4.7 M
+    cycles; gnoc_fetch_latency refuses, gnoc_fetch_final_ps still works."""
+    n = 130000
+    cfg = gnoc.EngineConfig(num_tiles=16, flit_width=16, analytical_enabled=False)
+    rng = np.random.default_rng(3)
+    src = rng.integers(1, 16, n).astype(np.uint32)
+    tr = gnoc.Trace(np.zeros(n, np.uint64), src, np.zeros(n, np.uint32), np.full(n, 576, np.uint32),
+                    np.zeros(n, np.uint32))
+    eng = gnoc.Engine(cfg)
+    eng.submit(pinned(tr))
+    eng.run()
+    fin = eng.results().final_ps
+    assert int(fin.max()) >= 1 << 32
+    out = torch.empty(n, dtype=torch.int32, pin_memory=True).numpy().view(np.uint32)
+    with pytest.raises(gnoc.GnocError):
+        eng.fetch_latency(out)
+    f64 = torch.empty(n, dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+    eng.fetch_final_ps(f64)
+    eng.fetch_wait()
+    assert np.array_equal(f64, fin)
+    eng.close()

@@ -181,3 +181,23 @@ def test_history_list_out_of_order_uses_gaps():
     assert q.compute(10, 5) == 0      # busy [10, 15), gap [0, 10)
     assert q.compute(2, 3) == 0       # fits the gap
     assert q.compute(12, 4) == 3      # waits for 15
+
+
+@pytest.mark.parametrize("W,load,ppt,seed", [(8, 0.05, 400, 1), (8, 0.3, 250, 2), (6, 0.1, 300, 3)])
+def test_network_walk_with_reference_queue_objects(W, load, ppt, seed):
+    """The oracle's event loop with every history-tree queue replaced by the
+    reference's own IntervalTree + QueueModelMG1 objects (oracle/_ref, compiled from
+    its sources; bench.py's CPU baseline runs this) gives the restatement's results
+    exactly: per packet and per port, M/G/1 uses included."""
+    if oracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built (no /root/reference)")
+    from graphite_amd import gnoc
+    cfg = gnoc.EngineConfig(num_tiles=W * W)
+    tr = gnoc.synthetic_trace(W, W, load, ppt, seed=seed)
+    a = oracle.run(cfg, tr)
+    b = oracle.run(cfg, tr, ref_queues=True)
+    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_mg1", "port_flit",
+              "port_last"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    if load >= 0.3:
+        assert a.port_mg1.sum() > 0
