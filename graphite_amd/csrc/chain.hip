@@ -92,7 +92,8 @@ constexpr uint32_t F_TIMEOUT = 8u;        // a hand-off wait timed out
 constexpr uint32_t F_ANY = F_RETRY | F_FALLBACK | F_ROUTE | F_TIMEOUT;
 // why a chain run declined (bits above F_ANY; reported with GNOC_CHAIN_DEBUG=1)
 enum : uint32_t { R_OFFSET = 1u << 8, R_TAIL = 1u << 9, R_SPILLIN = 1u << 10, R_LASTSPILL = 1u << 11, R_MG1 = 1u << 12,
-                  R_EXC = 1u << 13, R_OVF_INS = 1u << 14, R_OVF_STREAM = 1u << 15, R_XDONE = 1u << 17 };
+                  R_EXC = 1u << 13, R_OVF_INS = 1u << 14, R_OVF_STREAM = 1u << 15, R_XDONE = 1u << 17,
+                  R_MGBAD = 1u << 18, R_MGB_KEPT = 1u << 19, R_MGB_SPILL = 1u << 20, R_MGB_OVF = 1u << 21 };
 constexpr uint64_t SPIN_CYCLES = 1ull << 31;
 constexpr uint64_t M48 = (1ull << 48) - 1;
 constexpr uint64_t OFF_LIM = (1ull << 32) - 4096;   // time offsets within a window (32-bit cycle math)
@@ -538,34 +539,6 @@ __device__ __forceinline__ void load_rows(Smem& sm, uint32_t nK, uint32_t IB, ui
    }
 }
 
-#ifndef CH_BRANK
-#define CH_BRANK 1   // 0: route ranks by a DPP prefix sum and field tables by ds_bpermute
-#endif
-// A row's route fields (2 bits per lane, valid lanes a prefix of the row) by three
-// ballots: per-field counts packed 8 bits per field, and each lane's rank among the
-// lanes of its own field (lanes below it with the same two bits).  Scalar bit counts
-// and two mask selects instead of a dependent cross-lane scan.
-__device__ __forceinline__ uint32_t field_tot(bool valid, uint32_t f, uint64_t& b0, uint64_t& b1)
-{
-   b0 = __ballot(valid && (f & 1u));
-   b1 = __ballot(valid && (f & 2u));
-   const uint64_t vm = __ballot(valid);
-   const uint32_t c0 = (uint32_t) __popcll(vm & ~(b0 | b1)), c1 = (uint32_t) __popcll(b0 & ~b1);
-   const uint32_t c2 = (uint32_t) __popcll(b1 & ~b0), c3 = (uint32_t) __popcll(b0 & b1);
-   return c0 | c1 << 8 | c2 << 16 | c3 << 24;
-}
-__device__ __forceinline__ uint32_t field_rank(uint32_t f, uint64_t b0, uint64_t b1)
-{
-   const uint64_t m = ((f & 1u) ? b0 : ~b0) & ((f & 2u) ? b1 : ~b1);
-   return mbcnt(m);
-}
-// Lane-wise pick of one of four wave-uniform values by a 2-bit field.
-__device__ __forceinline__ uint32_t sel4(uint32_t f, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3)
-{
-   const uint32_t lo = (f & 1u) ? v1 : v0, hi = (f & 1u) ? v3 : v2;
-   return (f & 2u) ? hi : lo;
-}
-
 // Per-field tables: lane 1 + q holds route field q (SELF, cont, UP, DOWN), the
 // lanes of the state words that carry the route counts.
 // Lane 1 + q of a row's packed field counts (8 bits per field).
@@ -692,7 +665,8 @@ struct MgOut
 {
    uint64_t ssum, X, maxdep;
    uint32_t nkeep, mode, mg1;
-   bool rte, spilled, bad;
+   uint32_t bad;   // R_MGB_* reasons
+   bool rte, spilled;
 };
 // (only in the MG instantiation of k_chain: its serial loop raises the register
 // allocation, and the common kernel should not pay for it)
@@ -756,7 +730,7 @@ __device__ __forceinline__ MgOut mg_emit(Smem& sm, const ChainArgs& a, const uin
          const uint64_t dn = (uint64_t) off + cps(d) + rl;   // t' - wbase
          if (f == 1 && dn < wlen)
          {
-            if (o.spilled) o.bad = true;                      // kept after a spill
+            if (o.spilled) o.bad |= R_MGB_KEPT;                // kept after a spill
             if (lane == 0)
             {
                sm.key[rf[1] - P0n] = (dn << 32) | id;
@@ -768,7 +742,7 @@ __device__ __forceinline__ MgOut mg_emit(Smem& sm, const ChainArgs& a, const uin
          }
          else if (f == 1 || !exc)
          {
-            if (f == 1 && exc) o.bad = true;                  // an M/G/1-served spill
+            if (f == 1 && exc) o.bad |= R_MGB_SPILL;          // an M/G/1-served spill
             if (rf[f] >= oc[f]) o.rte = true;
             else if (lane == 0) out_record(recs, samp_t, samp_id, (uint64_t) ob[f] + rf[f], wbase + dn, id, ax, f == 1);
             o.spilled |= f == 1;
@@ -815,7 +789,7 @@ __device__ __forceinline__ MgOut mg_emit(Smem& sm, const ChainArgs& a, const uin
    o.mg1 = (uint32_t) st.mg1;
    const uint64_t s1 = (uint64_t) st.s1, s2 = (uint64_t) st.s2;
    mst = lane == 0 ? st.narr : lane == 1 ? s1 : lane == 2 ? s2 : lane == 3 ? st.newest : 0ull;
-   o.bad |= st.newest > M48 || s2 > M48 || st.narr > M48;
+   if (st.newest > M48 || s2 > M48 || st.narr > M48) o.bad |= R_MGB_OVF;
    return o;
 }
 
@@ -1130,13 +1104,7 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
             totA += rA;
             const uint32_t f = route_field<XC>(nx, ny, ra[r]);
             fpack |= (valid ? f : 0u) << (2 * r);
-            if (CH_BRANK)
-            {
-               uint64_t b0, b1;
-               tc_t += field_cnt(field_tot(valid, f, b0, b1), lane);
-            }
-            else
-               tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
+            tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
          }
          if (!first) break;
          CH_STAMP(2);
@@ -1272,16 +1240,6 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
       const uint32_t rl = rdl(pd0, PD_RL);
       // field tables (lane 1 + q): output slot base, capacity, records routed so far
       const uint32_t obf_t = bperm(pd0, lane - 1u), ocf_t = bperm(pd0, lane + 3u);
-      // (CH_BRANK) the same per field as wave-uniform values: output slot base, capacity,
-      // records routed so far
-      uint32_t ob_s[4], oc_s[4], rn_s[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-      {
-         ob_s[q] = rdl(pd0, PD_OBASE + q);
-         oc_s[q] = rdl(pd0, PD_OCAP + q);
-         rn_s[q] = rdl(cin_t, 1 + q);
-      }
       uint32_t run_t = cin_t;
       const uint32_t P0n = rdl(cin_t, 2);   // chain-direction records before this window
       const gptr<uint64_t> samp_t = sptr(a.samp_t);
@@ -1351,29 +1309,14 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
          const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
          // route ranks: a packed (8 bits per field) prefix count over the row
          const uint32_t f = (fpack >> (2 * r)) & 3u;
-         uint32_t rank, gb, room, kb;
-         if (CH_BRANK)
-         {
-            uint64_t b0, b1;
-            const uint32_t rtot = field_tot(valid, f, b0, b1);
-            rank = field_rank(f, b0, b1);
-            gb = sel4(f, ob_s[0] + rn_s[0], ob_s[1] + rn_s[1], ob_s[2] + rn_s[2], ob_s[3] + rn_s[3]);
-            room = sel4(f, oc_s[0] - rn_s[0], oc_s[1] - rn_s[1], oc_s[2] - rn_s[2], oc_s[3] - rn_s[3]);
-            kb = rn_s[1] - P0n;
-#pragma unroll
-            for (int q = 0; q < 4; q++) rn_s[q] += (rtot >> (8 * q)) & 0xFFu;
-         }
-         else
-         {
-            const uint32_t one = valid ? 1u << (8 * f) : 0u;
-            const uint32_t inc = wave_sum32(one);
-            rank = ((inc - one) >> (8 * f)) & 0xFFu;
-            const uint32_t rtot = rdl(inc, 63);
-            gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
-            room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
-            kb = rdl(run_t, 2) - P0n;              // kept records so far
-            run_t += field_cnt(rtot, lane);
-         }
+         const uint32_t one = valid ? 1u << (8 * f) : 0u;
+         const uint32_t inc = wave_sum32(one);
+         const uint32_t rank = ((inc - one) >> (8 * f)) & 0xFFu;
+         const uint32_t rtot = rdl(inc, 63);
+         const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
+         const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
+         const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
+         run_t += field_cnt(rtot, lane);
          // continuing: kept (a prefix of the window's continuing records) or spilled;
          // everything else leaves through one 16-B write-through store (turns and spills
          // alike: a spill is read in-launch by task (chain, w+1), MI355X_MICROARCH.md
@@ -1392,16 +1335,15 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
          if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
       }
       CH_STAMP(6);
-      if (CH_BRANK && !mgr) run_t = lane - 1u < 4u ? sel4(lane - 1u, rn_s[0], rn_s[1], rn_s[2], rn_s[3]) : run_t;
       const bool spilled = mgr ? mo.spilled : spm != 0;
       if ((mgr ? mo.rte : rte != 0) && lane == 0) flag(a, F_ROUTE);
-      if (mgr && mo.bad && lane == 0) flag(a, F_FALLBACK | R_MG1);
-      // (not the MG instantiation) the M/G/1 branch serves a request before the first gap
-      if (!MG && mode && ffire != NONE && (fgap == NONE || ffire < fgap))
+      if (mgr && mo.bad)
       {
-         if (lane == 0) flag(a, F_FALLBACK | R_MG1);
+         // an M/G/1-served spill (or a kept record after a spill): the level engine takes it
+         if (lane == 0) flag(a, F_FALLBACK | R_MG1 | R_MGBAD | mo.bad);
          return;
       }
+
       if (spilled && lastw && lane == 0) flag(a, F_FALLBACK | R_LASTSPILL);   // the last window keeps everything
       const uint64_t ssw = mgr ? mo.ssum : rdl64(wave_sum64(ssum), 63);
       if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drained before the next publish
@@ -1413,6 +1355,8 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
       if (!published && mode)
       {
          // the state after the window: still no gap -> the M/G/1 sums go along
+         // (not the MG instantiation) the M/G/1 branch served a request before the first gap
+         if (!MG && lane == 0 && ffire != NONE && (fgap == NONE || ffire < fgap)) flag(a, F_FALLBACK | R_MG1);
          const uint32_t mout = mgr ? mo.mode : (fgap == NONE ? 1u : 0u);
          if (MG && mout) mst = mg_after(mst, mgr, n, totA, sp2, Xo);
          if (lane < (uint32_t) SW_SER) st1(stw + lane, a.etag | state_word_ser(lane, Xo, run_t, mout, Kout, Pend));
@@ -1594,13 +1538,7 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
             totA += rA;
             const uint32_t f = route_field<XC>(nx, ny, ra[r]);
             fpack |= (valid ? f : 0u) << (2 * r);
-            if (CH_BRANK)
-            {
-               uint64_t b0, b1;
-               tc_t += field_cnt(field_tot(valid, f, b0, b1), lane);
-            }
-            else
-               tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
+            tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
          }
          if (!first) break;
          first = false;
@@ -1877,16 +1815,6 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
       const uint32_t rl = rdl(pd0, PD_RL);
       // field tables (lane 1 + q): output slot base, capacity, records routed so far
       const uint32_t obf_t = bperm(pd0, lane - 1u), ocf_t = bperm(pd0, lane + 3u);
-      // (CH_BRANK) the same per field as wave-uniform values: output slot base, capacity,
-      // records routed so far
-      uint32_t ob_s[4], oc_s[4], rn_s[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-      {
-         ob_s[q] = rdl(pd0, PD_OBASE + q);
-         oc_s[q] = rdl(pd0, PD_OCAP + q);
-         rn_s[q] = rdl(cin_t, 1 + q);
-      }
       uint32_t run_t = cin_t;
       const uint32_t P0n = rdl(cin_t, 2);   // chain-direction records before this window
       const gptr<uint64_t> samp_t = sptr(a.samp_t);
@@ -1956,29 +1884,14 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
          const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
          // route ranks: a packed (8 bits per field) prefix count over the row
          const uint32_t f = (fpack >> (2 * r)) & 3u;
-         uint32_t rank, gb, room, kb;
-         if (CH_BRANK)
-         {
-            uint64_t b0, b1;
-            const uint32_t rtot = field_tot(valid, f, b0, b1);
-            rank = field_rank(f, b0, b1);
-            gb = sel4(f, ob_s[0] + rn_s[0], ob_s[1] + rn_s[1], ob_s[2] + rn_s[2], ob_s[3] + rn_s[3]);
-            room = sel4(f, oc_s[0] - rn_s[0], oc_s[1] - rn_s[1], oc_s[2] - rn_s[2], oc_s[3] - rn_s[3]);
-            kb = rn_s[1] - P0n;
-#pragma unroll
-            for (int q = 0; q < 4; q++) rn_s[q] += (rtot >> (8 * q)) & 0xFFu;
-         }
-         else
-         {
-            const uint32_t one = valid ? 1u << (8 * f) : 0u;
-            const uint32_t inc = wave_sum32(one);
-            rank = ((inc - one) >> (8 * f)) & 0xFFu;
-            const uint32_t rtot = rdl(inc, 63);
-            gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
-            room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
-            kb = rdl(run_t, 2) - P0n;              // kept records so far
-            run_t += field_cnt(rtot, lane);
-         }
+         const uint32_t one = valid ? 1u << (8 * f) : 0u;
+         const uint32_t inc = wave_sum32(one);
+         const uint32_t rank = ((inc - one) >> (8 * f)) & 0xFFu;
+         const uint32_t rtot = rdl(inc, 63);
+         const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
+         const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
+         const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
+         run_t += field_cnt(rtot, lane);
          // continuing: kept (a prefix of the window's continuing records) or spilled
          const bool keep = valid && f == 1 && dn < wlen;
          const bool out = valid && !keep;
@@ -1994,16 +1907,15 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
          if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
       }
       CH_STAMP(6);
-      if (CH_BRANK && !mgr) run_t = lane - 1u < 4u ? sel4(lane - 1u, rn_s[0], rn_s[1], rn_s[2], rn_s[3]) : run_t;
       const bool spilled = mgr ? mo.spilled : spm != 0;
       if ((mgr ? mo.rte : rte != 0) && lane == 0) flag(a, F_ROUTE);
-      if (mgr && mo.bad && lane == 0) flag(a, F_FALLBACK | R_MG1);
-      // (not the MG instantiation) the M/G/1 branch serves a request before the first gap
-      if (!MG && mode && ffire != NONE && (fgap == NONE || ffire < fgap))
+      if (mgr && mo.bad)
       {
-         if (lane == 0) flag(a, F_FALLBACK | R_MG1);
+         // an M/G/1-served spill (or a kept record after a spill): the level engine takes it
+         if (lane == 0) flag(a, F_FALLBACK | R_MG1 | R_MGBAD | mo.bad);
          return;
       }
+
       if (spilled && lastw && lane == 0) flag(a, F_FALLBACK | R_LASTSPILL);   // the last window keeps everything
       const uint64_t ssw = mgr ? mo.ssum : rdl64(wave_sum64(ssum), 63);
       if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drained before the next publish
@@ -2015,6 +1927,8 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
       if (mode)
       {
          // the state after the window: still no gap -> the M/G/1 sums go along
+         // (not the MG instantiation) the M/G/1 branch served a request before the first gap
+         if (!MG && lane == 0 && ffire != NONE && (fgap == NONE || ffire < fgap)) flag(a, F_FALLBACK | R_MG1);
          const uint32_t mout = mgr ? mo.mode : (fgap == NONE ? 1u : 0u);
          if (MG && mout) mst = mg_after(mst, mgr, n, totA, sp2, Xo);
          if (MG && mout && lane < 4u) st1(stw + G_MG + lane, a.etag | mst);

@@ -2251,18 +2251,17 @@ static int run_post_check(gnoc_engine* e, bool closed_form)
          std::snprintf(m, sizeof m, "internal: chain route-count invariant violated (flags 0x%x 0x%x)", ef[4], ef[5]);
          return fail(e, GNOC_EHIP, m);
       }
-      // the no-gap M/G/1 branch (and nothing the MG instantiation would decline again):
-      // rerun the chains with the serial path compiled in
-      if (!e->ch_mg && e->nranks <= 1 && (cf & ch::R_MG1) && !(cf & (ch::F_RETRY | ch::F_TIMEOUT)))
-         return GNOC_CH_MG;
+      e->ch_yflags = ef[5];
+      // Reruns that change how the chains run, each at most once per batch (a rerun
+      // meets whatever else declined again, so the other reasons wait for it):
+      // the injection level left exception tails -> merge them first ...
+      if (!e->exc_fix && e->nranks <= 1 && (ef[4] & ch::R_EXC) && !(ef[2] & 2u)) return GNOC_CH_EXC;
+      // ... the no-gap M/G/1 branch -> the instantiation with the serial path
+      if (!e->ch_mg && e->nranks <= 1 && (cf & ch::R_MG1) && !(cf & ch::F_TIMEOUT)) return GNOC_CH_MG;
       // only the Y chains declined, for a reason the level engine takes (the M/G/1
       // branch, a spill range, a hand-off timeout): the X phase's outputs stand
-      e->ch_yflags = ef[5];
       if (!(ef[4] & ch::F_ANY) && (ef[5] & (ch::F_FALLBACK | ch::F_TIMEOUT)) && !(ef[5] & ch::F_RETRY) && e->nranks <= 1)
          return GNOC_CH_YFALL;
-      // declined only because the injection level left exception tails: rerun with them merged
-      if (!e->exc_fix && e->nranks <= 1 && ef[4] == (ch::F_FALLBACK | ch::R_EXC) && !(ef[5] & ch::F_ANY) && !(ef[2] & 2u))
-         return GNOC_CH_EXC;
       return (cf & (ch::F_FALLBACK | ch::F_TIMEOUT)) ? GNOC_CH_FALLBACK : GNOC_CH_RETRY;
    }
    // a leaf the splitter could not cut (or a look-back timeout) leaves garbage
@@ -2346,6 +2345,9 @@ static int y_levels_rerun(gnoc_engine* e)
 {
    hipStream_t s = e->stream;
    GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 5, 0, 4, s));
+   // the MG instantiation's Y chains may have left exception tails in the SELF slots;
+   // every other slot's tails were merged (k_exc_merge) before the Y phase
+   if (e->ch_mg) GNOC_HIP(e, hipMemsetAsync(e->nexc.p, 0, (size_t) e->dc.N * PORTS * INS * 4, s));
    const uint32_t np = e->dc.N * PORTS;
    GNOC_LAUNCH(e, KC_CHAIN, ch::k_zero_ports, dim3((np + 255) / 256), dim3(256), 0, s, np,
                (1u << P_UP) | (1u << P_DOWN) | (1u << P_SELF), e->port_sum.as<unsigned long long>(),
@@ -3084,7 +3086,12 @@ static int begin_x(gnoc_engine* e, void* send_buf, bool sync)
       {
          // an M/G/1 request or exception tails: a property of the batch, so its later
          // runs take the level engine straight away (a new submit clears this)
-         if ((f4 & ch::F_FALLBACK) && !(f4 & ch::F_TIMEOUT)) e->ch_declined = 1;
+         // (the M/G/1 branch alone: later runs take k_chain's MG instantiation)
+         if ((f4 & ch::F_FALLBACK) && !(f4 & ch::F_TIMEOUT))
+         {
+            if ((f4 & ch::R_MG1) && !e->ch_mg && !(f4 & ch::F_RETRY)) e->ch_mg = 1;
+            else e->ch_declined = 1;
+         }
          if (f4 & ch::F_RETRY)
          {
             // windows of this rank's X chains overflowed: shorter ones at the next run
@@ -3193,7 +3200,7 @@ static int finish_enqueue(gnoc_engine* e, const void* recv_buf)
    }
    const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
    int rc = GNOC_OK;
-   if (e->used_chain)
+   if (e->used_chain && !e->ch_ydeclined)
    {
       // exception tails (M/G/1-served turns, here or at a peer) into order for the Y chains
       if (e->dc.analytical) rc = exc_merge(e);
@@ -3201,7 +3208,10 @@ static int finish_enqueue(gnoc_engine* e, const void* recv_buf)
       if (!rc) rc = run_levels_v3(e, L - 1, L);
    }
    else
+   {
+      if (e->used_chain) e->used_v3 = 5;   // X chains, Y levels (this batch's Y chains declined)
       rc = run_levels_v3(e, e->lvl_y0, L);
+   }
    if (!rc) rc = run_post_enqueue(e, false);
    return rc;
 }
@@ -3214,7 +3224,19 @@ static int finish_check(gnoc_engine* e)
    int rc = run_post_check(e, false);
    if (rc == GNOC_V3_RETRY) return fail(e, GNOC_EUNSUPPORTED, "sharded run hit a burst the chunked path cannot split");
    if (!e->used_chain) return rc;
-   if (rc == GNOC_CH_EXC || rc == GNOC_CH_YFALL) rc = GNOC_CH_FALLBACK;   // (the sharded path's own Y fallback below)
+   // (the sharded path's own Y fallback below; its chains run the common instantiation,
+   // which declines where the M/G/1 branch fires and leaves no exception tails)
+   if (rc == GNOC_CH_EXC || rc == GNOC_CH_YFALL || rc == GNOC_CH_MG) rc = GNOC_CH_FALLBACK;
+   // the MG instantiation's Y chains may have left exception tails in the SELF slots
+   const bool mg_ran = e->ch_mg != 0;
+   // a decline for a property of the batch (not a hand-off timeout): the M/G/1 branch
+   // sends later runs to the MG instantiation once, anything else (or the MG
+   // instantiation declining too) to the Y levels straight after the exchange
+   if (rc == GNOC_CH_FALLBACK && (e->ch_yflags & ch::F_FALLBACK) && !(e->ch_yflags & ch::F_TIMEOUT))
+   {
+      if ((e->ch_yflags & ch::R_MG1) && !mg_ran) e->ch_mg = 1;
+      else e->ch_ydeclined = 1;
+   }
    // the windows of the next run: from this run's measured fill, or shorter
    // for the chains that overflowed (results never depend on them)
    if (!rc && !e->ch_resized) adapt_windows(e);
@@ -3225,6 +3247,7 @@ static int finish_check(gnoc_engine* e)
    e->n_fallback++;
    e->used_chain = 0;
    GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, 0, 8, s));
+   if (mg_ran) GNOC_HIP(e, hipMemsetAsync(e->nexc.p, 0, (size_t) e->dc.N * PORTS * INS * 4, s));
    const uint32_t np = e->dc.N * PORTS;
    hipLaunchKernelGGL(ch::k_zero_ports, dim3((np + 255) / 256), dim3(256), 0, s, np,
                       (1u << P_UP) | (1u << P_DOWN) | (1u << P_SELF), e->port_sum.as<unsigned long long>(),

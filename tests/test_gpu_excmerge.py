@@ -143,7 +143,8 @@ def test_y_only_mg1_keeps_x_on_chain(W, ax, ay, k):
         paths.append(int(s["engine_path"]))
         if s["engine_path"] == 4:
             assert s["fallbacks"] == 0 and s["chain_protocol"] & 0x400, s
-            assert s["retries"] == (1 if r == 0 else 0), s
+            # (first run: the MG rerun, and possibly one for the windows the burst overflowed)
+            assert (1 <= s["retries"] <= 2) if r == 0 else s["retries"] == 0, s
         else:
             assert s["engine_path"] == 5, s
             assert s["fallbacks"] == (1 if r == 0 else 0), s
