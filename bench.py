@@ -127,19 +127,23 @@ def main():
     # end to end (SURVEY.md 8(d) "trace resident in host memory -> results in host
     # memory"): submit from pinned host arrays (host-side trace validation + H2D),
     # run, final_ps back into a pinned host array; reported beside the HBM-resident value
-    e2e_ms = e2e_serial_ms = e2e_wide_ms = e2e_fin_ms = None
+    e2e_ms = e2e_serial_ms = e2e_wide_ms = e2e_fin_ms = e2e_narrow_ms = None
     wire = None
     if not sharded:
         ptr = pinned_trace(tr)
         fins = [torch.empty(len(tr), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64) for _ in range(2)]
         lats = [pinned_array(len(tr), np.uint32) for _ in range(2)]
         K = max(2, a.steps // 2)
-        # the narrow wire format (gnoc_packets_narrow: u16 tile ids / lengths, u8 flags,
-        # 15 B per packet) where the batch fits it, else the 24-B one
+        # the delta wire format (gnoc_packets_packed: u16 inject-time differences and
+        # tile ids, lengths / flags only where they vary: 6 B per packet here) and the
+        # narrow one (15 B) where the batch fits them, else the 24-B one
+        pin = lambda shape, dt: pinned_array(shape[0], dt)   # noqa: E731
         try:
-            ntr = gnoc.NarrowTrace.of(tr, alloc=lambda shape, dt: pinned_array(shape[0], dt))
-            sub, sub_async, wire = eng.submit_narrow, eng.submit_async_narrow, 15
+            ntr15 = gnoc.NarrowTrace.of(tr, alloc=pin)
+            ktr = gnoc.PackedTrace.of(tr, alloc=pin)
+            sub, sub_async, ntr, wire = eng.submit_packed, eng.submit_async_packed, ktr, ktr.wire_bytes() / len(tr)
         except ValueError:
+            ntr15 = None
             ntr, sub, sub_async, wire = ptr, eng.submit, eng.submit_async, 24
 
         def pipelined(submit, submit_async, x, latency=False):
@@ -165,7 +169,7 @@ def main():
             return ms
         # untimed: the second trace buffers, copy streams, staging areas and latency
         # arrays get allocated
-        for sa, x in ((sub_async, ntr), (eng.submit_async, ptr)):
+        for sa, x in ((sub_async, ntr), (eng.submit_async, ptr)) + (((eng.submit_async_narrow, ntr15),) if ntr15 else ()):
             sa(x)
             eng.submit_commit()
             eng.run()
@@ -184,7 +188,9 @@ def main():
         e2e_serial_ms = (time.perf_counter() - t_e) / K * 1e3
         e2e_ms = pipelined(sub, sub_async, ntr, latency=True)
         e2e_fin_ms = pipelined(sub, sub_async, ntr)
-        e2e_wide_ms = pipelined(eng.submit, eng.submit_async, ptr) if wire == 15 else e2e_fin_ms
+        if ntr15 is not None:
+            e2e_narrow_ms = pipelined(eng.submit_narrow, eng.submit_async_narrow, ntr15, latency=True)
+        e2e_wide_ms = pipelined(eng.submit, eng.submit_async, ptr) if wire != 24 else e2e_fin_ms
 
     # this rank's share: mesh hops through the ports it owns, packets it delivers
     res = eng.results()
@@ -268,14 +274,17 @@ def main():
             "e2e_ms_per_step": e2e_ms,
             "e2e_serial_ms_per_step": e2e_serial_ms,
             "e2e_final_ps_ms_per_step": e2e_fin_ms,
+            "e2e_15B_ms_per_step": e2e_narrow_ms,
             "e2e_24B_ms_per_step": e2e_wide_ms,
             "e2e_wire_bytes_per_packet": wire,
-            "e2e_note": "host trace (pinned) -> host results per batch: submit (H2D + device-side trace checks) + run + "
-                        "read-back; e2e_ms_per_step pipelined (batch k+1's upload and batch k's read-back on copy "
-                        "streams beside the runs) in the narrow wire format with the per-packet latency read back "
-                        "as u32 (gnoc_fetch_latency), e2e_final_ps_ms_per_step the same with final_ps (u64), "
-                        "e2e_serial_ms_per_step one batch at a time (narrow upload, final_ps), e2e_24B_ms_per_step "
-                        "pipelined with the 24-B upload and final_ps",
+            "e2e_note": "host trace (pinned) -> host results per batch: submit (H2D + device-side decode and trace "
+                        "checks) + run + read-back; e2e_ms_per_step pipelined (batch k+1's upload, decode and checks "
+                        "on the upload stream and batch k's read-back on a copy stream, beside the runs; the first "
+                        "upload and the last read-back inside the clock) in the delta wire format (gnoc_packets_packed)"
+                        " with the per-packet latency read back as u32 (gnoc_fetch_latency); "
+                        "e2e_final_ps_ms_per_step the same with final_ps (u64); e2e_15B_ms_per_step the narrow wire "
+                        "format with the latency; e2e_serial_ms_per_step one batch at a time (delta upload, final_ps);"
+                        " e2e_24B_ms_per_step pipelined with the 24-B upload and final_ps",
             "roofline": {
                 "bound": "hbm",
                 "achieved": rf["achieved"],

@@ -154,6 +154,9 @@ struct gnoc_engine
    uint32_t h_levels = 0;
    double last_ms = 0.0;
    uint64_t* h_pinned = nullptr;
+   uint64_t* h_val = nullptr;               // (pinned, 128 B) a staged batch's ValOut
+   DevBuf vbuf2;                            // a staged batch's validation scratch (upload stream)
+   bool staged_val = false;                 // the staged batch was validated on the upload stream
 
    // a sharded rank's partitioned trace (gnoc_submit): only the packets of its
    // row band (sources) or column band (destinations), in trace order; gid maps
@@ -475,6 +478,7 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    if (he == hipSuccess) he = hipEventCreate(&e->ev0);
    if (he == hipSuccess) he = hipEventCreate(&e->ev1);
    if (he == hipSuccess) he = hipHostMalloc((void**) &e->h_pinned, 256, hipHostMallocDefault);
+   if (he == hipSuccess) he = hipHostMalloc((void**) &e->h_val, 128, hipHostMallocDefault);
    // per chain fill maxima: 2 u32 for each of the <= 2 (W + H) chains
    if (he == hipSuccess)
       he = hipHostMalloc((void**) &e->h_nmax, 16 * ((size_t) e->dc.W + e->dc.H) + 64, hipHostMallocDefault);
@@ -614,6 +618,7 @@ void gnoc_destroy(gnoc_engine* e)
    if (e->ev0) (void) hipEventDestroy(e->ev0);
    if (e->ev1) (void) hipEventDestroy(e->ev1);
    if (e->h_pinned) (void) hipHostFree(e->h_pinned);
+   if (e->h_val) (void) hipHostFree(e->h_val);
    if (e->h_nmax) (void) hipHostFree(e->h_nmax);
    for (hipEvent_t ev : e->evpool) (void) hipEventDestroy(ev);
    for (hipStream_t q : { e->s_h2d, e->s_d2h })
@@ -862,10 +867,20 @@ static int chain_tables(gnoc_engine* e)
 // (prep.hip k_validate over e->d_*): the first offending packet of any check,
 // the hop records this engine materialises, the turn exchange counts of a
 // sharded engine, and the chain engine's window size from the busiest port.
-static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t* nbc)
+// The trace arrays a validation reads (the current batch's, or a staged one's).
+struct ValTrace
+{
+   const uint64_t* inj;
+   const uint32_t *src, *dst, *bits, *flags;
+};
+static int validate_finish(gnoc_engine* e, const void* h_out, uint64_t* records, uint64_t* nbc);
+// The device-side checks and statistics of a batch, enqueued on stream s into the
+// scratch vb; the ValOut summary lands in the pinned h_out (validate_finish reads it
+// once the stream got there).  xcnt (the exchange counts) stays in vb.
+static int validate_launch(gnoc_engine* e, size_t n, ValTrace t, hipStream_t s, DevBuf& vb, void* h_out,
+                           unsigned long long** xcnt_out)
 {
    const uint32_t N = e->dc.N, W = e->dc.W, H = e->dc.H, nr = (uint32_t) e->nranks;
-   hipStream_t s = e->stream;
    const size_t nd = (size_t) 2 * H * (W + 1) + (size_t) 2 * W * (H + 1);   // difference arrays (int)
    const size_t ni = (size_t) 4 * N;                                       // inserts per X / Y port
    const size_t off_x = (sizeof(ValOut) + (nd + ni) * 4 + 7) / 8 * 8;
@@ -878,10 +893,10 @@ static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t
    const size_t off_p = (off_x + (size_t) nr * nr * 8 + 255) / 256 * 256;
    const size_t bytes = off_p + (size_t) nblk * ntab * 4;
    static_assert(sizeof(ValOut) <= 128, "ValOut lands in the 128-B pinned staging");
-   GNOC_HIP(e, e->vbuf.ensure(bytes));
-   GNOC_HIP(e, hipMemsetAsync(e->vbuf.p, 0, off_p, s));
-   GNOC_HIP(e, hipMemsetAsync(e->vbuf.p, 0xFF, sizeof(unsigned long long) * VB_KINDS, s));
-   char* base = static_cast<char*>(e->vbuf.p);
+   GNOC_HIP(e, vb.ensure(bytes));
+   GNOC_HIP(e, hipMemsetAsync(vb.p, 0, off_p, s));
+   GNOC_HIP(e, hipMemsetAsync(vb.p, 0xFF, sizeof(unsigned long long) * VB_KINDS, s));
+   char* base = static_cast<char*>(vb.p);
    ValOut* vo = reinterpret_cast<ValOut*>(base);
    int* dxr = reinterpret_cast<int*>(base + sizeof(ValOut));
    int* dxl = dxr + (size_t) H * (W + 1);
@@ -900,27 +915,43 @@ static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t
          if (lds > 64 * 1024)
             GNOC_HIP(e, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_validate<true>),
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
-         hipLaunchKernelGGL(k_validate<true>, dim3(nblk), dim3(256), lds, s, e->dc, (uint64_t) n, e->d_inj, e->d_src,
-                            e->d_dst, e->d_bits, e->d_flags, tree, sweep, nr, (uint32_t) e->rank, (uint32_t) e->xself, vo, dxr, ntab, part, xcnt);
+         hipLaunchKernelGGL(k_validate<true>, dim3(nblk), dim3(256), lds, s, e->dc, (uint64_t) n, t.inj, t.src,
+                            t.dst, t.bits, t.flags, tree, sweep, nr, (uint32_t) e->rank, (uint32_t) e->xself, vo, dxr, ntab, part, xcnt);
          GNOC_HIP(e, hipGetLastError());
          hipLaunchKernelGGL(k_validate_sum, dim3((ntab + 255) / 256), dim3(256), 0, s, ntab, nblk, part, dxr);
       }
       else
       {
          const uint32_t grid = (uint32_t) std::min<uint64_t>((n + 255) / 256, 4096);
-         hipLaunchKernelGGL(k_validate<false>, dim3(grid), dim3(256), 0, s, e->dc, (uint64_t) n, e->d_inj, e->d_src,
-                            e->d_dst, e->d_bits, e->d_flags, tree, sweep, nr, (uint32_t) e->rank, (uint32_t) e->xself, vo, dxr, ntab, part, xcnt);
+         hipLaunchKernelGGL(k_validate<false>, dim3(grid), dim3(256), 0, s, e->dc, (uint64_t) n, t.inj, t.src,
+                            t.dst, t.bits, t.flags, tree, sweep, nr, (uint32_t) e->rank, (uint32_t) e->xself, vo, dxr, ntab, part, xcnt);
       }
       GNOC_HIP(e, hipGetLastError());
       hipLaunchKernelGGL(k_validate_max, dim3(1), dim3(1024), 0, s, W, H, dxr, dxl, dyu, dyd, insx, insy, vo);
       GNOC_HIP(e, hipGetLastError());
    }
-   GNOC_HIP(e, hipMemcpyAsync(e->h_pinned, vo, sizeof(ValOut), hipMemcpyDeviceToHost, s));
+   GNOC_HIP(e, hipMemcpyAsync(h_out, vo, sizeof(ValOut), hipMemcpyDeviceToHost, s));
+   if (xcnt_out) *xcnt_out = xcnt;
+   return GNOC_OK;
+}
+static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t* nbc)
+{
+   const uint32_t nr = (uint32_t) e->nranks;
+   hipStream_t s = e->stream;
+   unsigned long long* xcnt = nullptr;
+   int rc = validate_launch(e, n, ValTrace{ e->d_inj, e->d_src, e->d_dst, e->d_bits, e->d_flags }, s, e->vbuf, e->h_pinned, &xcnt);
+   if (rc) return rc;
    e->x_cnt.assign((size_t) nr * nr, 0);
    if (nr > 1 || e->xself) GNOC_HIP(e, hipMemcpyAsync(e->x_cnt.data(), xcnt, (size_t) nr * nr * 8, hipMemcpyDeviceToHost, s));
    GNOC_HIP(e, hipStreamSynchronize(s));
+   return validate_finish(e, e->h_pinned, records, nbc);
+}
+// The host side of a validation: the first offending packet, or the batch's window
+// sizing and record bound.
+static int validate_finish(gnoc_engine* e, const void* h_out, uint64_t* records, uint64_t* nbc)
+{
    ValOut v;
-   std::memcpy(&v, e->h_pinned, sizeof v);
+   std::memcpy(&v, h_out, sizeof v);
    // the first offending packet (one check per packet: the first that fails)
    uint32_t k = VB_KINDS;
    for (uint32_t q = 0; q < VB_KINDS; q++)
@@ -944,7 +975,7 @@ static int device_validate(gnoc_engine* e, size_t n, uint64_t* records, uint64_t
          default: return fail(e, GNOC_EUNSUPPORTED, "inject time beyond 2^50 ps at packet " + at);
       }
    }
-   choose_windows(e, v.pmax, v.imax, n ? v.tlast : 0);
+   choose_windows(e, v.pmax, v.imax, v.tlast);   // (an empty batch: all zero)
    *records = v.records;
    *nbc = v.nbc;
    return GNOC_OK;
@@ -1112,7 +1143,7 @@ static int partition_trace(gnoc_engine* e, const gnoc_packets* pk, size_t n, gno
    return GNOC_OK;
 }
 
-static int submit_tail(gnoc_engine* e, const gnoc_packets* pk, size_t n);
+static int submit_tail(gnoc_engine* e, const gnoc_packets* pk, size_t n, bool prevalidated = false);
 
 // Narrow wire format -> the engine's u32 trace arrays (one pass, coalesced).
 __global__ __launch_bounds__(256) void k_widen(uint64_t n, const uint16_t* __restrict__ src, const uint16_t* __restrict__ dst,
@@ -1127,6 +1158,223 @@ __global__ __launch_bounds__(256) void k_widen(uint64_t n, const uint16_t* __res
       obits[i] = bits[i];
       oflags[i] = flags ? flags[i] : 0u;
    }
+}
+
+// Delta wire format (gnoc_packets_packed) -> the engine's trace arrays.  Blocks of
+// PK_B packets, PK_PT consecutive ones per thread.  k_dt_block: each block's escapes
+// (dt == 0xFFFF) and its difference sum after the last one; k_dt_carry (one
+// workgroup): the escapes before each block and the inject time before its first
+// packet, by a segmented scan of the block aggregates (an escape restarts the sum
+// at its absolute time); k_dt_unpack: the same inside each block, writing inject_ps
+// and widening the other fields.
+constexpr uint32_t PK_T = 256, PK_PT = 8, PK_B = PK_T * PK_PT;
+constexpr uint16_t PK_ESC = 0xFFFF;
+struct PkAgg
+{
+   uint64_t tail;    // the differences after the last escape (all of them without one)
+   uint32_t nesc;
+   uint32_t pad;
+};
+// Segmented inclusive scan over a workgroup of (restart, value) pairs in LDS.
+__device__ __forceinline__ void seg_scan(uint32_t* fl, uint64_t* va, uint32_t tid, uint32_t nt)
+{
+   for (uint32_t d = 1; d < nt; d <<= 1)
+   {
+      uint32_t f = 0;
+      uint64_t v = 0;
+      const bool take = tid >= d;
+      if (take)
+      {
+         f = fl[tid - d];
+         v = va[tid - d];
+      }
+      __syncthreads();
+      if (take && !fl[tid])
+      {
+         fl[tid] = f;
+         va[tid] += v;
+      }
+      __syncthreads();
+   }
+}
+__global__ __launch_bounds__(PK_T) void k_dt_block(uint64_t n, const uint16_t* __restrict__ dt, PkAgg* __restrict__ agg)
+{
+   __shared__ uint32_t fl[PK_T], ne[PK_T];
+   __shared__ uint64_t va[PK_T];
+   const uint32_t tid = threadIdx.x;
+   const uint64_t i0 = (uint64_t) blockIdx.x * PK_B + (uint64_t) tid * PK_PT;
+   uint32_t f = 0, c = 0;
+   uint64_t v = 0;
+   for (uint32_t k = 0; k < PK_PT; k++)
+   {
+      if (i0 + k >= n) break;
+      const uint16_t d = dt[i0 + k];
+      if (d == PK_ESC)
+      {
+         f = 1;
+         v = 0;
+         c++;
+      }
+      else v += d;
+   }
+   fl[tid] = f;
+   va[tid] = v;
+   ne[tid] = c;
+   __syncthreads();
+   seg_scan(fl, va, tid, PK_T);
+   if (tid == 0)
+   {
+      uint32_t t = 0;
+      for (uint32_t q = 0; q < PK_T; q++) t += ne[q];
+      agg[blockIdx.x] = PkAgg{ va[PK_T - 1], t, fl[PK_T - 1] };
+   }
+}
+__global__ __launch_bounds__(1024) void k_dt_carry(uint32_t nblk, uint64_t t0, const uint64_t* __restrict__ abs_ps,
+                                                   const PkAgg* __restrict__ agg, uint64_t* __restrict__ carry,
+                                                   uint64_t* __restrict__ escbase)
+{
+   __shared__ uint32_t fl[1024];
+   __shared__ uint64_t va[1024], eb[1024];
+   __shared__ uint64_t s_t, s_e;
+   const uint32_t tid = threadIdx.x;
+   if (tid == 0) { s_t = t0; s_e = 0; }
+   __syncthreads();
+   for (uint32_t b0 = 0; b0 < nblk; b0 += 1024)
+   {
+      const uint32_t b = b0 + tid;
+      const PkAgg g = b < nblk ? agg[b] : PkAgg{ 0, 0, 0 };
+      eb[tid] = g.nesc;
+      __syncthreads();
+      for (uint32_t d = 1; d < 1024; d <<= 1)   // inclusive prefix of the escape counts
+      {
+         const uint64_t x = tid >= d ? eb[tid - d] : 0;
+         __syncthreads();
+         eb[tid] += x;
+         __syncthreads();
+      }
+      const uint64_t ebase = s_e + eb[tid] - g.nesc;   // escapes before block b
+      fl[tid] = g.pad;                                  // the block has an escape
+      va[tid] = g.pad ? abs_ps[ebase + g.nesc - 1] + g.tail : g.tail;
+      __syncthreads();
+      seg_scan(fl, va, tid, 1024);
+      // the time before block b: the previous inclusive value (or the carried one)
+      const uint64_t prev = tid == 0 ? s_t : (fl[tid - 1] ? va[tid - 1] : s_t + va[tid - 1]);
+      if (b < nblk)
+      {
+         carry[b] = prev;
+         escbase[b] = ebase;
+      }
+      __syncthreads();
+      if (tid == 1023)
+      {
+         s_t = fl[1023] ? va[1023] : s_t + va[1023];
+         s_e += eb[1023];
+      }
+      __syncthreads();
+   }
+}
+__global__ __launch_bounds__(PK_T) void k_dt_unpack(uint64_t n, const uint16_t* __restrict__ dt,
+                                                    const uint64_t* __restrict__ abs_ps, const uint64_t* __restrict__ carry,
+                                                    const uint64_t* __restrict__ escbase, const uint16_t* __restrict__ src,
+                                                    const uint16_t* __restrict__ dst, const uint16_t* __restrict__ bits,
+                                                    uint32_t bits_all, const uint8_t* __restrict__ flags,
+                                                    uint64_t* __restrict__ oinj, uint32_t* __restrict__ osrc,
+                                                    uint32_t* __restrict__ odst, uint32_t* __restrict__ obits,
+                                                    uint32_t* __restrict__ oflags)
+{
+   __shared__ uint32_t fl[PK_T], ne[PK_T];
+   __shared__ uint64_t va[PK_T];
+   const uint32_t tid = threadIdx.x;
+   const uint64_t i0 = (uint64_t) blockIdx.x * PK_B + (uint64_t) tid * PK_PT;
+   uint16_t d[PK_PT];
+   uint32_t c = 0, f = 0;
+   uint64_t tail = 0;
+#pragma unroll
+   for (uint32_t k = 0; k < PK_PT; k++)
+   {
+      d[k] = i0 + k < n ? dt[i0 + k] : (uint16_t) 0;
+      if (i0 + k < n && d[k] == PK_ESC)
+      {
+         f = 1;
+         tail = 0;
+         c++;
+      }
+      else tail += d[k];
+   }
+   ne[tid] = c;
+   __syncthreads();
+   for (uint32_t s = 1; s < PK_T; s <<= 1)   // inclusive prefix of the escape counts
+   {
+      const uint32_t x = tid >= s ? ne[tid - s] : 0u;
+      __syncthreads();
+      ne[tid] += x;
+      __syncthreads();
+   }
+   uint64_t eo = escbase[blockIdx.x] + ne[tid] - c;   // this thread's first escape ordinal
+   fl[tid] = f;
+   va[tid] = f ? abs_ps[eo + c - 1] + tail : tail;
+   __syncthreads();
+   seg_scan(fl, va, tid, PK_T);
+   const uint64_t cin = carry[blockIdx.x];
+   uint64_t T = tid == 0 ? cin : (fl[tid - 1] ? va[tid - 1] : cin + va[tid - 1]);
+#pragma unroll
+   for (uint32_t k = 0; k < PK_PT; k++)
+   {
+      const uint64_t i = i0 + k;
+      if (i >= n) break;
+      T = d[k] == PK_ESC ? abs_ps[eo++] : T + d[k];
+      oinj[i] = T;
+      osrc[i] = src[i];
+      odst[i] = dst[i];
+      obits[i] = bits ? (uint32_t) bits[i] : bits_all;
+      oflags[i] = flags ? (uint32_t) flags[i] : 0u;
+   }
+}
+
+// Copy a packed trace (host) into the stage buffer and decode it into (inj, src, dst,
+// bits, flags) on stream q.
+static int stage_packed(gnoc_engine* e, const gnoc_packets_packed* pk, size_t n, DevBuf& stage, DevBuf& inj, DevBuf& src,
+                        DevBuf& dst, DevBuf& bits, DevBuf& flags, hipStream_t q)
+{
+   if (n && (!pk->dt || !pk->src || !pk->dst)) return fail(e, GNOC_EINVAL, "null trace array");
+   if (pk->n_abs && !pk->abs_ps) return fail(e, GNOC_EINVAL, "null abs_ps with n_abs > 0");
+   if (pk->n_abs > n) return fail(e, GNOC_EINVAL, "more absolute inject times than packets");
+   if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
+   if (e->nranks > 1) return fail(e, GNOC_EUNSUPPORTED, "a sharded engine takes gnoc_submit");
+   if (e->dc.N > 65536) return fail(e, GNOC_EUNSUPPORTED, "the packed wire format needs at most 65,536 tiles");
+   GNOC_HIP(e, inj.ensure(n * 8));
+   GNOC_HIP(e, src.ensure(n * 4));
+   GNOC_HIP(e, dst.ensure(n * 4));
+   GNOC_HIP(e, bits.ensure(n * 4));
+   GNOC_HIP(e, flags.ensure(n * 4));
+   const uint32_t nblk = (uint32_t) ((n + PK_B - 1) / PK_B);
+   // dt, src, dst, bits (u16) | flags (u8) | abs_ps | block aggregates, carries, escape bases (8-B aligned)
+   const size_t o_f8 = n * 8, o_abs = (o_f8 + n + 15) / 16 * 16, o_agg = o_abs + (size_t) pk->n_abs * 8;
+   const size_t o_car = o_agg + (size_t) nblk * sizeof(PkAgg), o_eb = o_car + (size_t) nblk * 8;
+   GNOC_HIP(e, stage.ensure(o_eb + (size_t) nblk * 8 + 16));
+   if (!n) return GNOC_OK;
+   char* sb = static_cast<char*>(stage.p);
+   uint16_t* s16 = reinterpret_cast<uint16_t*>(sb);
+   uint8_t* f8 = reinterpret_cast<uint8_t*>(sb + o_f8);
+   uint64_t* ab = reinterpret_cast<uint64_t*>(sb + o_abs);
+   PkAgg* agg = reinterpret_cast<PkAgg*>(sb + o_agg);
+   uint64_t* car = reinterpret_cast<uint64_t*>(sb + o_car);
+   uint64_t* ebs = reinterpret_cast<uint64_t*>(sb + o_eb);
+   GNOC_HIP(e, hipMemcpyAsync(s16, pk->dt, n * 2, hipMemcpyHostToDevice, q));
+   GNOC_HIP(e, hipMemcpyAsync(s16 + n, pk->src, n * 2, hipMemcpyHostToDevice, q));
+   GNOC_HIP(e, hipMemcpyAsync(s16 + 2 * n, pk->dst, n * 2, hipMemcpyHostToDevice, q));
+   if (pk->bits) GNOC_HIP(e, hipMemcpyAsync(s16 + 3 * n, pk->bits, n * 2, hipMemcpyHostToDevice, q));
+   if (pk->flags) GNOC_HIP(e, hipMemcpyAsync(f8, pk->flags, n, hipMemcpyHostToDevice, q));
+   if (pk->n_abs) GNOC_HIP(e, hipMemcpyAsync(ab, pk->abs_ps, (size_t) pk->n_abs * 8, hipMemcpyHostToDevice, q));
+   hipLaunchKernelGGL(k_dt_block, dim3(nblk), dim3(PK_T), 0, q, (uint64_t) n, (const uint16_t*) s16, agg);
+   hipLaunchKernelGGL(k_dt_carry, dim3(1), dim3(1024), 0, q, nblk, pk->t0, (const uint64_t*) ab, (const PkAgg*) agg, car, ebs);
+   hipLaunchKernelGGL(k_dt_unpack, dim3(nblk), dim3(PK_T), 0, q, (uint64_t) n, (const uint16_t*) s16, (const uint64_t*) ab,
+                      (const uint64_t*) car, (const uint64_t*) ebs, (const uint16_t*) (s16 + n), (const uint16_t*) (s16 + 2 * n),
+                      pk->bits ? (const uint16_t*) (s16 + 3 * n) : nullptr, pk->bits_all,
+                      pk->flags ? (const uint8_t*) f8 : nullptr, inj.as<uint64_t>(), src.as<uint32_t>(), dst.as<uint32_t>(),
+                      bits.as<uint32_t>(), flags.as<uint32_t>());
+   GNOC_HIP(e, hipGetLastError());
+   return GNOC_OK;
 }
 
 // Copy a narrow trace (host) into the stage buffer and widen it into (inj, src, dst,
@@ -1166,6 +1414,26 @@ int gnoc_submit_narrow(gnoc_engine* e, const gnoc_packets_narrow* pk, size_t n)
    e->submitted = false;
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    int rc = stage_narrow(e, pk, n, e->nw_stage, e->t_inj, e->t_src, e->t_dst, e->t_bits, e->t_flags, e->stream);
+   if (rc) return rc;
+   e->part = false;
+   e->n_glob = n;
+   e->dc.g2l = nullptr;
+   e->d_inj = e->t_inj.as<uint64_t>();
+   e->d_src = e->t_src.as<uint32_t>();
+   e->d_dst = e->t_dst.as<uint32_t>();
+   e->d_bits = e->t_bits.as<uint32_t>();
+   e->d_flags = e->t_flags.as<uint32_t>();
+   e->n = n;
+   e->dc.npk = n;
+   return submit_tail(e, nullptr, n);
+}
+
+int gnoc_submit_packed(gnoc_engine* e, const gnoc_packets_packed* pk, size_t n)
+{
+   if (!e || !pk) return GNOC_EINVAL;
+   e->submitted = false;
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   int rc = stage_packed(e, pk, n, e->nw_stage, e->t_inj, e->t_src, e->t_dst, e->t_bits, e->t_flags, e->stream);
    if (rc) return rc;
    e->part = false;
    e->n_glob = n;
@@ -1244,10 +1512,12 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk_in, size_t n)
 // The rest of a host-trace submit, once the trace is in the engine's buffers
 // (d_inj .. d_flags, n): the device-side contract checks and statistics, the
 // record bound, broadcast tables (from the host flags), the exchange layout.
-static int submit_tail(gnoc_engine* e, const gnoc_packets* pk, size_t n)
+static int submit_tail(gnoc_engine* e, const gnoc_packets* pk, size_t n, bool prevalidated)
 {
    uint64_t records = 0, nbc = 0;
-   int rc = device_validate(e, n, &records, &nbc);   // (its sync also ends the copies)
+   // (device_validate's sync also ends the copies; a staged batch was checked on the
+   // upload stream beside the previous run, its summary is in h_val)
+   int rc = prevalidated ? validate_finish(e, e->h_val, &records, &nbc) : device_validate(e, n, &records, &nbc);
    if (rc) return rc;
    if (record_bound(e, records) >= (1ull << 31)) return fail(e, GNOC_EUNSUPPORTED, "more than 2^31 hop records");
    e->rec_bound = record_bound(e, records);
@@ -1280,6 +1550,20 @@ static hipError_t pipe_streams(gnoc_engine* e)
    return he;
 }
 
+// A staged batch's device checks on the upload stream, right behind its copies: they
+// run beside the current batch's run instead of after it (gnoc_submit_commit then only
+// reads the summary).  Not for the exchange-count statistics of the self-exchange knob.
+static int stage_validate(gnoc_engine* e, size_t n)
+{
+   e->staged_val = false;
+   if (e->nranks > 1 || e->xself) return GNOC_OK;
+   const int rc = validate_launch(e, n, ValTrace{ e->t2_inj.as<uint64_t>(), e->t2_src.as<uint32_t>(), e->t2_dst.as<uint32_t>(),
+                                                  e->t2_bits.as<uint32_t>(), e->t2_flags.as<uint32_t>() },
+                                  e->s_h2d, e->vbuf2, e->h_val, nullptr);
+   if (!rc) e->staged_val = true;
+   return rc;
+}
+
 int gnoc_submit_async(gnoc_engine* e, const gnoc_packets* pk, size_t n)
 {
    if (!e || !pk) return GNOC_EINVAL;
@@ -1304,6 +1588,8 @@ int gnoc_submit_async(gnoc_engine* e, const gnoc_packets* pk, size_t n)
       if (pk->flags) GNOC_HIP(e, hipMemcpyAsync(e->t2_flags.p, pk->flags, n * 4, hipMemcpyHostToDevice, q));
       else GNOC_HIP(e, hipMemsetAsync(e->t2_flags.p, 0, n * 4, q));
    }
+   int rc = stage_validate(e, n);
+   if (rc) return rc;
    GNOC_HIP(e, hipEventRecord(e->ev_h2d, e->s_h2d));
    e->staged = true;
    e->staged_narrow = false;
@@ -1319,10 +1605,28 @@ int gnoc_submit_async_narrow(gnoc_engine* e, const gnoc_packets_narrow* pk, size
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    GNOC_HIP(e, pipe_streams(e));
    int rc = stage_narrow(e, pk, n, e->nw_stage2, e->t2_inj, e->t2_src, e->t2_dst, e->t2_bits, e->t2_flags, e->s_h2d);
+   if (!rc) rc = stage_validate(e, n);
    if (rc) return rc;
    GNOC_HIP(e, hipEventRecord(e->ev_h2d, e->s_h2d));
    e->staged = true;
    e->staged_narrow = true;
+   e->staged_pk = gnoc_packets{};
+   e->staged_n = n;
+   return GNOC_OK;
+}
+
+int gnoc_submit_async_packed(gnoc_engine* e, const gnoc_packets_packed* pk, size_t n)
+{
+   if (!e || !pk) return GNOC_EINVAL;
+   if (e->staged) return fail(e, GNOC_ESTATE, "a staged batch is waiting for gnoc_submit_commit");
+   GNOC_HIP(e, hipSetDevice(e->cfg.device));
+   GNOC_HIP(e, pipe_streams(e));
+   int rc = stage_packed(e, pk, n, e->nw_stage2, e->t2_inj, e->t2_src, e->t2_dst, e->t2_bits, e->t2_flags, e->s_h2d);
+   if (!rc) rc = stage_validate(e, n);
+   if (rc) return rc;
+   GNOC_HIP(e, hipEventRecord(e->ev_h2d, e->s_h2d));
+   e->staged = true;
+   e->staged_narrow = true;   // (no host arrays kept: unicast batches only, as narrow)
    e->staged_pk = gnoc_packets{};
    e->staged_n = n;
    return GNOC_OK;
@@ -1356,7 +1660,10 @@ int gnoc_submit_commit(gnoc_engine* e)
    gnoc_packets pk = e->staged_pk;
    const bool narrow = e->staged_narrow;
    e->staged_narrow = false;
-   return submit_tail(e, narrow ? nullptr : &pk, n);
+   const bool pre = e->staged_val;
+   e->staged_val = false;
+   if (pre) GNOC_HIP(e, hipEventSynchronize(e->ev_h2d));   // (the checks' summary is in h_val)
+   return submit_tail(e, narrow ? nullptr : &pk, n, pre);
 }
 
 int gnoc_fetch_final_ps(gnoc_engine* e, uint64_t* host_out, size_t n)

@@ -46,7 +46,7 @@ EXPORTED = (
     "gnoc_get_broadcast_results", "gnoc_get_broadcast_info", "gnoc_set_basic_moving_average",
     "gnoc_build_id", "gnoc_rccl_unique_id", "gnoc_rccl_comm_init", "gnoc_rccl_comm_destroy",
     "gnoc_submit_async", "gnoc_submit_commit", "gnoc_fetch_final_ps", "gnoc_fetch_latency", "gnoc_fetch_wait",
-    "gnoc_submit_narrow", "gnoc_submit_async_narrow",
+    "gnoc_submit_narrow", "gnoc_submit_async_narrow", "gnoc_submit_packed", "gnoc_submit_async_packed",
 )
 
 
@@ -84,6 +84,21 @@ class GnocPackets(ctypes.Structure):
         ("src", ctypes.c_void_p),
         ("dst", ctypes.c_void_p),
         ("bits", ctypes.c_void_p),
+        ("flags", ctypes.c_void_p),
+    ]
+
+
+class GnocPacketsPacked(ctypes.Structure):
+    _fields_ = [
+        ("t0", ctypes.c_uint64),
+        ("dt", ctypes.c_void_p),
+        ("abs_ps", ctypes.c_void_p),
+        ("n_abs", ctypes.c_uint64),
+        ("src", ctypes.c_void_p),
+        ("dst", ctypes.c_void_p),
+        ("bits", ctypes.c_void_p),
+        ("bits_all", ctypes.c_uint32),
+        ("pad", ctypes.c_uint32),
         ("flags", ctypes.c_void_p),
     ]
 
@@ -196,6 +211,9 @@ def load() -> ctypes.CDLL:
     if hasattr(lib, "gnoc_submit_narrow"):
         lib.gnoc_submit_narrow.argtypes = [vp, ctypes.POINTER(GnocPacketsNarrow), sz]
         lib.gnoc_submit_async_narrow.argtypes = [vp, ctypes.POINTER(GnocPacketsNarrow), sz]
+    if hasattr(lib, "gnoc_submit_packed"):
+        lib.gnoc_submit_packed.argtypes = [vp, ctypes.POINTER(GnocPacketsPacked), sz]
+        lib.gnoc_submit_async_packed.argtypes = [vp, ctypes.POINTER(GnocPacketsPacked), sz]
     if hasattr(lib, "gnoc_submit_async"):
         lib.gnoc_submit_async.argtypes = [vp, ctypes.POINTER(GnocPackets), sz]
         lib.gnoc_submit_commit.argtypes = [vp]
@@ -314,6 +332,64 @@ class NarrowTrace:
     def packets(self) -> GnocPacketsNarrow:
         return GnocPacketsNarrow(self.inject_ps.ctypes.data, self.src.ctypes.data, self.dst.ctypes.data,
                                  self.bits.ctypes.data, self.flags.ctypes.data)
+
+
+@dataclass
+class PackedTrace:
+    """A trace in the delta wire format (gnoc_packets_packed): u16 inject-time
+    differences (0xFFFF = the next absolute time in abs_ps), u16 tile ids, and the
+    modeled lengths / flags only where they vary -- 6 bytes per packet for a batch of
+    one length without flags."""
+    t0: int
+    dt: np.ndarray
+    abs_ps: np.ndarray
+    src: np.ndarray
+    dst: np.ndarray
+    bits: object          # np.ndarray, or None (every packet has bits_all)
+    bits_all: int
+    flags: object         # np.ndarray, or None (all zero)
+
+    ESC = 0xFFFF
+
+    def __len__(self) -> int:
+        return int(self.dt.shape[0])
+
+    @staticmethod
+    def of(tr: "Trace", alloc=np.empty) -> "PackedTrace":
+        """Pack a trace (ValueError if a tile id, length or flag does not fit the
+        narrow fields); alloc(shape, dtype) places the arrays (e.g. page-locked)."""
+        tr = tr.normalized()
+        n = len(tr)
+        for name, a, lim in (("src", tr.src, 1 << 16), ("dst", tr.dst, 1 << 16), ("bits", tr.bits, 1 << 16),
+                             ("flags", tr.flags, 1 << 8)):
+            if n and int(a.max()) >= lim:
+                raise ValueError(f"{name} does not fit the packed wire format")
+        t = tr.inject_ps.astype(np.uint64)
+        t0 = int(t[0]) if n else 0
+        d = np.diff(t, prepend=np.uint64(t0)) if n else np.zeros(0, np.uint64)
+        esc = d >= PackedTrace.ESC
+
+        def put(a, dt):
+            b = alloc((a.shape[0],), dt)
+            b[:] = a
+            return b
+        dt16 = put(np.where(esc, PackedTrace.ESC, d).astype(np.uint16), np.uint16)
+        absv = put(t[esc], np.uint64)
+        one_len = n == 0 or bool((tr.bits == tr.bits[0]).all())
+        bits = None if one_len else put(tr.bits.astype(np.uint16), np.uint16)
+        flags = None if n == 0 or not tr.flags.any() else put(tr.flags.astype(np.uint8), np.uint8)
+        return PackedTrace(t0, dt16, absv, put(tr.src.astype(np.uint16), np.uint16), put(tr.dst.astype(np.uint16), np.uint16),
+                           bits, int(tr.bits[0]) if n and one_len else 0, flags)
+
+    def wire_bytes(self) -> int:
+        return int(self.dt.nbytes + self.abs_ps.nbytes + self.src.nbytes + self.dst.nbytes +
+                   (self.bits.nbytes if self.bits is not None else 0) + (self.flags.nbytes if self.flags is not None else 0))
+
+    def packets(self) -> GnocPacketsPacked:
+        return GnocPacketsPacked(self.t0, self.dt.ctypes.data, self.abs_ps.ctypes.data if self.abs_ps.size else None,
+                                 int(self.abs_ps.size), self.src.ctypes.data, self.dst.ctypes.data,
+                                 self.bits.ctypes.data if self.bits is not None else None, self.bits_all, 0,
+                                 self.flags.ctypes.data if self.flags is not None else None)
 
 
 # synthetic_network.cc NetworkTrafficType (:16-24), include/gnoc.h GNOC_TRAFFIC_*
@@ -488,6 +564,15 @@ class Engine:
     def submit_async_narrow(self, nt: "NarrowTrace") -> None:
         self._check(self.lib.gnoc_submit_async_narrow(self._h, ctypes.byref(nt.packets()), len(nt)))
         self._staged = (nt, len(nt))
+
+    def submit_packed(self, pt: "PackedTrace") -> None:
+        """gnoc_submit_packed: the delta wire format (decoded on the device)."""
+        self._check(self.lib.gnoc_submit_packed(self._h, ctypes.byref(pt.packets()), len(pt)))
+        self._n = len(pt)
+
+    def submit_async_packed(self, pt: "PackedTrace") -> None:
+        self._check(self.lib.gnoc_submit_async_packed(self._h, ctypes.byref(pt.packets()), len(pt)))
+        self._staged = (pt, len(pt))
 
     def submit_commit(self) -> None:
         self._check(self.lib.gnoc_submit_commit(self._h))

@@ -139,6 +139,27 @@ typedef struct gnoc_packets_narrow
    const uint8_t *flags;        /* may be NULL = all zero */
 } gnoc_packets_narrow;
 
+/* The trace in a delta wire format for streamed batches, 6 bytes per packet when
+ * the packets share one modeled length and carry no flags (8 / 9 bytes with the
+ * optional arrays): the inject times as u16 differences, dt[i] = inject_ps[i] -
+ * inject_ps[i-1] with inject_ps[-1] = t0, or 0xFFFF when the difference does not
+ * fit below it -- that packet's inject_ps is then the next entry of abs_ps (in
+ * packet order, n_abs entries in all).  Tile ids and lengths as in
+ * gnoc_packets_narrow.  Decoded on the device by one scan. */
+typedef struct gnoc_packets_packed
+{
+   uint64_t t0;
+   const uint16_t *dt;
+   const uint64_t *abs_ps;      /* may be NULL when n_abs == 0 */
+   uint64_t n_abs;
+   const uint16_t *src;
+   const uint16_t *dst;
+   const uint16_t *bits;        /* may be NULL: every packet has bits_all */
+   uint32_t bits_all;
+   uint32_t pad;
+   const uint8_t *flags;        /* may be NULL = all zero */
+} gnoc_packets_packed;
+
 typedef struct gnoc_engine gnoc_engine;
 
 typedef struct gnoc_summary
@@ -216,6 +237,7 @@ int gnoc_submit(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
  * they must stay valid until gnoc_run returns. */
 int gnoc_submit_device(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
 int gnoc_submit_narrow(gnoc_engine *eng, const gnoc_packets_narrow *pk, size_t n);
+int gnoc_submit_packed(gnoc_engine *eng, const gnoc_packets_packed *pk, size_t n);
 
 /* Runs the whole batch (all hops of all packets) on the GPU.  Blocking. */
 int gnoc_run(gnoc_engine *eng);
@@ -380,6 +402,7 @@ int gnoc_rccl_comm_destroy(void *comm);
  * submit_commit(k+1).  Unsharded engines, unicast batches. */
 int gnoc_submit_async(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
 int gnoc_submit_async_narrow(gnoc_engine *eng, const gnoc_packets_narrow *pk, size_t n);
+int gnoc_submit_async_packed(gnoc_engine *eng, const gnoc_packets_packed *pk, size_t n);
 int gnoc_submit_commit(gnoc_engine *eng);
 int gnoc_fetch_final_ps(gnoc_engine *eng, uint64_t *final_ps_out, size_t n);
 /* The narrow read-back: per packet latency_ps = final_ps - inject_ps (NetPacket::time

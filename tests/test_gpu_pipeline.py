@@ -102,6 +102,48 @@ def test_narrow_wire_format_matches_wide():
         gnoc.NarrowTrace.of(big)
 
 
+@pytest.mark.parametrize("case", ["one_length", "mixed", "gaps"])
+def test_packed_wire_format_matches_wide(case):
+    """gnoc_submit_packed / gnoc_submit_async_packed (u16 inject-time differences with
+    absolute-time escapes, decoded on the device by a segmented scan) give the same
+    results as the 24-B format: one modeled length and no flags (6 B per packet),
+    mixed lengths with unmodeled packets, and idle gaps longer than the u16
+    difference (escapes in many decode blocks, including two in a row)."""
+    from tests.traces import random_trace
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    if case == "one_length":
+        tr = gnoc.synthetic_trace(8, 8, 0.02, 800, seed=5)
+    else:
+        tr = random_trace(9000, 8, 8, seed=19, max_cycle=6000, burst0=5, self_frac=0.05)
+        if case == "mixed":
+            tr.flags[::41] |= gnoc.PKT_UNMODELED
+        else:
+            t = tr.inject_ps.astype(np.uint64)
+            t[3000:] += np.uint64(70_000_000)      # one long idle gap
+            t[5000:] += np.uint64(123_457)         # another one
+            t[5001:] += np.uint64(65_535)          # and an escape right behind it
+            tr = gnoc.Trace(t, tr.src, tr.dst, tr.bits, tr.flags)
+    pt = gnoc.PackedTrace.of(tr)
+    if case == "one_length":
+        assert pt.bits is None and pt.flags is None and pt.wire_bytes() <= 6 * len(pt) + 8 * pt.abs_ps.size
+    if case == "gaps":
+        assert pt.abs_ps.size >= 3
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    want = eng.results()
+    eng.submit_packed(pt)
+    eng.run()
+    got = eng.results()
+    for k in ("final_ps", "zero_load_ps", "contention_ps", "port_sum_delay", "port_count", "port_flit"):
+        assert np.array_equal(getattr(got, k), getattr(want, k)), k
+    eng.submit_async_packed(pt)
+    eng.submit_commit()
+    eng.run()
+    assert np.array_equal(eng.results().final_ps, want.final_ps)
+    eng.close()
+
+
 def test_pipelined_latency_readback_matches_final_ps():
     """gnoc_fetch_latency: the u32 latency (final_ps - inject_ps) read back on the
     copy stream, pipelined across batches of different sizes; the first call of an

@@ -41,3 +41,27 @@ def test_pattern_refusals():
         assert ex.value.code == -1
     with pytest.raises(ValueError):
         gnoc.synthetic_trace(4, 4, 0.05, 5, pattern="hotspot_storm")
+
+
+def test_packed_wire_format_round_trip_on_host():
+    """gnoc.PackedTrace (gnoc_packets_packed): the u16 differences with 0xFFFF escapes
+    to absolute times restate the inject times exactly (host decode of the format the
+    device scan decodes); one-length batches drop the length array."""
+    import numpy as np
+    from graphite_amd import gnoc
+    tr = gnoc.synthetic_trace(8, 8, 0.02, 500, seed=3).normalized()
+    t = tr.inject_ps.astype(np.uint64)
+    t[100:] += np.uint64(1 << 40)
+    t[101:] += np.uint64(65_535)
+    tr = gnoc.Trace(t, tr.src, tr.dst, tr.bits, tr.flags)
+    pt = gnoc.PackedTrace.of(tr)
+    assert pt.bits is None and pt.flags is None and pt.abs_ps.size >= 2
+    out, T, k = [], pt.t0, 0
+    for d in pt.dt.tolist():
+        if d == gnoc.PackedTrace.ESC:
+            T, k = int(pt.abs_ps[k]), k + 1
+        else:
+            T += d
+        out.append(T)
+    assert k == pt.abs_ps.size
+    assert np.array_equal(np.array(out, np.uint64), t)

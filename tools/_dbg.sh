@@ -1,2 +1,1 @@
-cd /root/repo && mkdir -p gpurun_out && GNOC_CHAIN_DEBUG=1 timeout -k 10 300 python -u bench.py --workload sweep --steps 3 --warmup 1 --cpu-baseline 0 > gpurun_out/sweepdbg.json 2> gpurun_out/sweepdbg.err && timeout -k 10 300 python -u -m pytest tests/test_gpu_sweep.py tests/test_gpu_excmerge.py -q -s --timeout 120 --timeout-method thread > gpurun_out/sweeptest.log 2>&1; grep declined gpurun_out/sweepdbg.err | sort | uniq -c; python -c "
-import json; d=json.loads(open('gpurun_out/sweepdbg.json').read().strip().split(chr(10))[-1]); print(d['ms_per_step'], d.get('reruns'), d['config'].get('engine_path'), d.get('kernel_ms'))"; tail -5 gpurun_out/sweeptest.log
+cd /root/repo && mkdir -p gpurun_out && timeout -k 10 300 python -u tools/e2e_probe.py > gpurun_out/e2e_probe.txt 2>&1; grep -v amdgpu.ids gpurun_out/e2e_probe.txt

@@ -16,7 +16,9 @@ tr = gnoc.synthetic_trace(32, 32, 0.005, 10000, seed=1)
 cfg = gnoc.EngineConfig(num_tiles=1024)
 eng = gnoc.Engine(cfg)
 ntr = gnoc.NarrowTrace.of(tr, alloc=lambda shape, dt: pinned_array(shape[0], dt))
+ktr = gnoc.PackedTrace.of(tr, alloc=lambda shape, dt: pinned_array(shape[0], dt))
 fins = [pinned_array(len(tr), np.uint64) for _ in range(2)]
+lats = [pinned_array(len(tr), np.uint32) for _ in range(2)]
 eng.submit_narrow(ntr)
 for _ in range(5):
     eng.run()
@@ -26,6 +28,10 @@ for _ in range(2):
     eng.run()
     eng.fetch_final_ps(fins[0])
     eng.fetch_wait()
+    eng.run()
+    eng.fetch_latency(lats[0])
+    eng.fetch_wait()
+print("trace bytes per packet (narrow wire):", sum(getattr(ntr, f).itemsize for f in ntr.__dataclass_fields__) if hasattr(ntr, "__dataclass_fields__") else "?")
 
 
 def clock(name, body):
@@ -60,6 +66,42 @@ def full(k):
     eng.submit_commit()
 
 
+def run_lat(k):
+    eng.run()
+    eng.fetch_latency(lats[k % 2])
+
+
+def full_lat(k):
+    eng.submit_async_narrow(ntr)
+    eng.run()
+    eng.fetch_latency(lats[k % 2])
+    eng.submit_commit()
+
+
+def lat_only(k):
+    eng.fetch_latency(lats[k % 2])
+    eng.fetch_wait()
+
+
+def run_upk(k):
+    eng.submit_async_packed(ktr)
+    eng.run()
+    eng.submit_commit()
+
+
+def full_pk(k):
+    eng.submit_async_packed(ktr)
+    eng.run()
+    eng.fetch_latency(lats[k % 2])
+    eng.submit_commit()
+
+
+def upk_only(k):
+    eng.submit_async_packed(ktr)
+    eng.submit_commit()
+    torch.cuda.synchronize()
+
+
 def fetch_only(k):
     eng.fetch_final_ps(fins[k % 2])
     eng.fetch_wait()
@@ -76,8 +118,11 @@ def submit_serial(k):
 
 
 for name, body in (("run", run_only), ("run + fetch (pipelined)", run_fetch), ("fetch alone", fetch_only),
+                   ("run + latency (pipelined)", run_lat), ("latency alone", lat_only),
                    ("run + upload (pipelined)", run_upload), ("run + upload + fetch", full),
-                   ("upload+commit alone", upload_only), ("submit_narrow alone", submit_serial),
-                   ("run", run_only), ("fetch alone", fetch_only)):
+                   ("run + upload + latency", full_lat), ("upload+commit alone", upload_only),
+                   ("run + packed upload", run_upk), ("run + packed upload + latency", full_pk),
+                   ("packed upload+commit alone", upk_only),
+                   ("submit_narrow alone", submit_serial), ("run", run_only), ("fetch alone", fetch_only)):
     clock(name, body)
 eng.close()
