@@ -533,7 +533,7 @@ def pinned_trace(tr):
                       pin(tr.flags if tr.flags is not None else np.zeros(len(tr), np.uint32)))
 
 
-PMC_FILE = "r3_pmc.json"
+PMC_FILE = "r4_pmc.json"
 
 
 def pmc_traffic(workload, kernel, bid):

@@ -209,18 +209,6 @@ __device__ __forceinline__ void st1(uint64_t* p, uint64_t v)
 }
 // Compiler-only ordering point between LDS phases of the one wave.
 __device__ __forceinline__ void wsync() { asm volatile("" ::: "memory"); }
-// Every vector memory op of the wave done (s_waitcnt vmcnt(0), nothing else), once per
-// step before the outputs: the state loads before it are issued under exec masks on
-// some paths only, and with one such load possibly pending the compiler's wait pass
-// puts a vmcnt(0) (which also waits for the row's write-through stores) in front of
-// every later reuse of its registers, i.e. into every output row.
-#ifndef CH_VMDRAIN
-#define CH_VMDRAIN 1
-#endif
-__device__ __forceinline__ void vm_drain()
-{
-   if (CH_VMDRAIN) __builtin_amdgcn_s_waitcnt(0x0F70);
-}
 
 template <int CTRL, int RM, int BM>
 __device__ __forceinline__ uint32_t dpp32(uint32_t v)
@@ -1147,7 +1135,6 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
             }
          }
          CH_STAMP(4);
-         vm_drain();
          if (!ok) return;
          // window-relative tail: an earlier tail behaves like the base cycle (every tc > wb)
          const uint64_t xr = X_in > wb ? X_in - wb : 0;
@@ -1793,7 +1780,6 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
          mst = lane < 4u ? mv & M48 : 0ull;
       }
       CH_STAMP(4);
-      vm_drain();
       // window-relative tail: an earlier tail behaves like the base cycle (every tc > wb)
       const uint64_t xr = X_in > wb ? X_in - wb : 0;
       if (xr >= (1ull << 31))

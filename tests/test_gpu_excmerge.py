@@ -150,3 +150,26 @@ def test_y_only_mg1_keeps_x_on_chain(W, ax, ay, k):
             assert s["fallbacks"] == (1 if r == 0 else 0), s
     eng.close()
     print("engine paths", paths)
+
+
+def test_overflow_then_y_mg1_decline_is_exact(monkeypatch):
+    """a first run whose windows overflow LDS (forced long windows,
+    a dense column burst) reruns with halved windows, and that rerun meets the Y
+    ports' M/G/1 branch: the run must end exact on the chains (MG instantiation) or
+    on the Y levels, never return an internal rerun code."""
+    monkeypatch.setenv("GNOC_WINDOW_PS", "4000000")
+    W = 8
+    cfg = gnoc.EngineConfig(num_tiles=W * W)
+    tr = column_burst_trace(W, W, 3, 4, 16, seed=71, tail=20000)
+    ref = oracle.run(cfg, tr)
+    assert ref.port_mg1.reshape(-1, 6)[:, [3, 4]].sum() > 0
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    s = eng.summary()
+    same(eng.results(), ref)
+    assert s["retries"] >= 1 and s["engine_path"] in (1, 4, 5), s
+    eng.run()
+    same(eng.results(), ref)
+    eng.close()
+    print("summary", s)
