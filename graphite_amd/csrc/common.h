@@ -89,13 +89,13 @@ struct DevCfg
    const uint64_t* bc_prev; // [v * BCS + ...] previous pass
    uint64_t* bc_cur;        // [v * BCS + ...] this pass (zeroed before it)
    uint64_t* bc_fin;        // [b * N + tile] receipt time (ps)
-   uint64_t npk;            // packets of the batch: a SELF port never writes final_ps beyond it
-   // A sharded rank's partitioned trace (gnoc_submit): records carry global packet
-   // ids (their ties order every rank alike); the rank's per-packet arrays are
-   // indexed by its own packet index, g2l[global id].  nullptr: ids are indices.
-   const uint32_t* g2l;
+   // packets of the batch: a SELF port never writes final times beyond it.  A sharded
+   // rank's partitioned trace (gnoc_submit): records carry global packet ids (their
+   // ties order every rank alike), npk is the whole trace's count, and the delivery
+   // level writes by global id into an array of that size (k_finalize reads it back
+   // through the rank's gid map)
+   uint64_t npk;
 };
-__device__ __forceinline__ uint64_t pk_index(const DevCfg& c, uint32_t id) { return c.g2l ? c.g2l[id] : id; }
 
 // A broadcast record's neighbourhood in its port's queue (cycles): the
 // arrivals of the records just before and after it (a_prev, a_next), the

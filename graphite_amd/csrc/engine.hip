@@ -160,15 +160,17 @@ struct gnoc_engine
 
    // a sharded rank's partitioned trace (gnoc_submit): only the packets of its
    // row band (sources) or column band (destinations), in trace order; gid maps
-   // them to their global index, g2l back
+   // them to their global index.  Its delivery level writes final times by global
+   // id into fin_glob (a plain scattered store), and k_finalize reads the rank's
+   // delivered packets' back by gid.
    bool part = false;
-   int xself = 0;
+   int xself = 0;                           // test knob GNOC_SHARD_SELF_EXCHANGE: own turn records through the transport
    int declined_once = 0;                   // test knob GNOC_DECLINE_ONCE_RANK: fired
-   bool fin_closed = false;                 // finish_enqueue: the closed form finished in run_begin                           // test knob GNOC_SHARD_SELF_EXCHANGE: own turn records through the transport
+   bool fin_closed = false;                 // finish_enqueue: the closed form finished in run_begin
    size_t n_glob = 0;
    uint64_t h_glob_hops = 0, h_glob_routed = 0;
    std::vector<uint32_t> h_gid;
-   DevBuf d_gid, d_g2l;
+   DevBuf d_gid, fin_glob;
 
    // one mesh over several GPUs (gnoc_shard): this rank's row band (X phase)
    // and column band (Y phase), the turn-record exchange layout per peer
@@ -470,7 +472,6 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    d.hop_counter = 0;
    d.pt_rl = nullptr;
    d.pt_fw = nullptr;
-   d.g2l = nullptr;
    build_static_levels(e);
 
    hipError_t he = hipSetDevice(c.device);
@@ -1075,11 +1076,7 @@ __global__ __launch_bounds__(256) void k_zero_segs(ZeroSegs z, uint32_t w10)
       p[i] = (blockIdx.y == 0 && i == 10) ? w10 : 0u;
 }
 
-__global__ void k_g2l(uint64_t n, const uint32_t* __restrict__ gid, uint32_t* __restrict__ g2l)
-{
-   for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
-      g2l[gid[i]] = (uint32_t) i;
-}
+
 
 // A sharded rank keeps only the packets it touches: sources in its row band
 // (injection, X phase, turn) or destinations in its column band (Y phase, SELF,
@@ -1417,7 +1414,6 @@ int gnoc_submit_narrow(gnoc_engine* e, const gnoc_packets_narrow* pk, size_t n)
    if (rc) return rc;
    e->part = false;
    e->n_glob = n;
-   e->dc.g2l = nullptr;
    e->d_inj = e->t_inj.as<uint64_t>();
    e->d_src = e->t_src.as<uint32_t>();
    e->d_dst = e->t_dst.as<uint32_t>();
@@ -1437,7 +1433,6 @@ int gnoc_submit_packed(gnoc_engine* e, const gnoc_packets_packed* pk, size_t n)
    if (rc) return rc;
    e->part = false;
    e->n_glob = n;
-   e->dc.g2l = nullptr;
    e->d_inj = e->t_inj.as<uint64_t>();
    e->d_src = e->t_src.as<uint32_t>();
    e->d_dst = e->t_dst.as<uint32_t>();
@@ -1461,7 +1456,6 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk_in, size_t n)
    e->part = e->nranks > 1 && e->dc.W <= 64 && e->dc.H <= 64 && e->npoints == 1 && !e->dc.hop_counter && e->dc.contention &&
              !std::getenv("GNOC_NO_PARTITION");
    e->n_glob = n;
-   e->dc.g2l = nullptr;
    if (e->part)
    {
       const int prc = partition_trace(e, pk_in, n, &sub, l_inj, l_src, l_dst, l_bits, l_flags);
@@ -1496,15 +1490,8 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk_in, size_t n)
    if (e->part)
    {
       GNOC_HIP(e, e->d_gid.ensure(n * 4 + 4));
-      GNOC_HIP(e, e->d_g2l.ensure(e->n_glob * 4 + 4));
-      if (n)
-      {
-         GNOC_HIP(e, hipMemcpyAsync(e->d_gid.p, e->h_gid.data(), n * 4, hipMemcpyHostToDevice, e->stream));
-         hipLaunchKernelGGL(k_g2l, dim3((uint32_t) std::min<size_t>((n + 255) / 256, 8192)), dim3(256), 0, e->stream,
-                            (uint64_t) n, e->d_gid.as<uint32_t>(), e->d_g2l.as<uint32_t>());
-         GNOC_HIP(e, hipGetLastError());
-      }
-      e->dc.g2l = e->d_g2l.as<uint32_t>();
+      GNOC_HIP(e, e->fin_glob.ensure(e->n_glob * 8 + 8));
+      if (n) GNOC_HIP(e, hipMemcpyAsync(e->d_gid.p, e->h_gid.data(), n * 4, hipMemcpyHostToDevice, e->stream));
    }
    return submit_tail(e, pk, n);
 }
@@ -1649,7 +1636,6 @@ int gnoc_submit_commit(gnoc_engine* e)
    const size_t n = e->staged_n;
    e->part = false;
    e->n_glob = n;
-   e->dc.g2l = nullptr;
    e->d_inj = e->t_inj.as<uint64_t>();
    e->d_src = e->t_src.as<uint32_t>();
    e->d_dst = e->t_dst.as<uint32_t>();
@@ -1705,11 +1691,11 @@ int gnoc_fetch_latency(gnoc_engine* e, uint32_t* host_out, size_t n)
       if (n && e->f1)
          hipLaunchKernelGGL(k_finalize<true>, dim3(fin_grid), dim3(256), 0, s, e->dc, (uint64_t) n, e->d_inj, e->d_src,
                             e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
-                            e->cont.as<uint64_t>(), cf, e->cx0, e->cx1, e->lat32.as<uint32_t>(), lovf);
+                            e->cont.as<uint64_t>(), cf, e->cx0, e->cx1, e->lat32.as<uint32_t>(), lovf, nullptr, nullptr);
       else if (n)
          hipLaunchKernelGGL(k_finalize<false>, dim3(fin_grid), dim3(256), 0, s, e->dc, (uint64_t) n, e->d_inj, e->d_src,
                             e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
-                            e->cont.as<uint64_t>(), cf, e->cx0, e->cx1, e->lat32.as<uint32_t>(), lovf);
+                            e->cont.as<uint64_t>(), cf, e->cx0, e->cx1, e->lat32.as<uint32_t>(), lovf, nullptr, nullptr);
       GNOC_HIP(e, hipGetLastError());
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 8, e->counters.as<unsigned int>() + 8, 32, hipMemcpyDeviceToHost, s));
       GNOC_HIP(e, hipStreamSynchronize(s));
@@ -1739,8 +1725,7 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    {
       e->part = false;   // a device trace is used as is (every rank reads all of it)
       e->n_glob = n;
-      e->dc.g2l = nullptr;
-   }
+      }
    if (!e || !pk) return GNOC_EINVAL;
    if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return fail(e, GNOC_EINVAL, "null trace array");
    if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
@@ -1774,6 +1759,13 @@ int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
 // ---------------------------------------------------------------------------
 // v1: whole-port streams, host-built plan (f != 1 GHz, max_list_size <= 2, retries)
 // ---------------------------------------------------------------------------
+// Where the delivery level writes final times: the local array, or (a partitioned
+// rank) the global-id array that k_finalize reads back by gid.
+static uint64_t* fin_out(gnoc_engine* e)
+{
+   return e->part ? e->fin_glob.as<uint64_t>() : e->final_ps.as<uint64_t>();
+}
+
 static int run_levels_v1(gnoc_engine* e)
 {
    const DevCfg& c = e->dc;
@@ -1813,7 +1805,7 @@ static int run_levels_v1(gnoc_engine* e)
       const uint32_t* pp = e->plan_ports.as<uint32_t>() + off[l];
 #define GNOC_PORT(F1V, BCV)                                                                                         \
    GNOC_LAUNCH(e, KC_PORT, (k_port_stream<F1V, BCV>), dim3(cnt), dim3(STHREADS), 0, s, c, pp, e->slot_cnt.as<uint32_t>(), \
-               e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(), e->port_sum.as<uint64_t>(),   \
+               e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), fin_out(e), e->port_sum.as<uint64_t>(),                   \
                e->port_cnt.as<uint64_t>(), e->port_mg1.as<uint64_t>(), e->port_flit.as<uint64_t>(),                     \
                e->port_last.as<uint64_t>(), e->dirty.as<uint32_t>(), e->counters.as<unsigned int>() + 8,                \
                (const uint32_t*) e->d_bcnt.as<uint32_t>(), e->d_btail.as<uint32_t>())
@@ -1922,7 +1914,7 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
 #define GNOC_LEVEL_ARGS(lvl)                                                                                         \
    c, (lvl), e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
       e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(),                 \
-      e->st.as<uint64_t>(), e->final_ps.as<uint64_t>(), e->port_sum.as<unsigned long long>(),                          \
+      e->st.as<uint64_t>(), fin_out(e), e->port_sum.as<unsigned long long>(),                                          \
       e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),                                     \
       e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>(), e->counters.as<unsigned>() + 8,   \
       e->done.as<uint32_t>(), stp
@@ -2480,14 +2472,16 @@ static int run_post_enqueue(gnoc_engine* e, bool closed_form)
    if (n)
    {
       unsigned* lovf = e->counters.as<unsigned>() + 8 + 6;   // errflag[6]
+      const uint32_t* gid_f = e->part ? e->d_gid.as<uint32_t>() : nullptr;   // (final times by global id)
       if (e->f1)
          GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<true>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj, e->d_src,
                      e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(), e->zl.as<uint64_t>(),
-                     e->cont.as<uint64_t>(), (int) closed_form, e->cx0, e->cx1, lat, lovf);
+                     e->cont.as<uint64_t>(), (int) closed_form, e->cx0, e->cx1, lat, lovf, gid_f, e->fin_glob.as<uint64_t>());
       else
          GNOC_LAUNCH(e, KC_FINALIZE, k_finalize<false>, dim3(fin_grid), dim3(256), 0, s, c, (uint64_t) n, e->d_inj,
                      e->d_src, e->aux.as<uint32_t>(), e->routed.as<uint8_t>(), e->final_ps.as<uint64_t>(),
-                     e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), (int) closed_form, e->cx0, e->cx1, lat, lovf);
+                     e->zl.as<uint64_t>(), e->cont.as<uint64_t>(), (int) closed_form, e->cx0, e->cx1, lat, lovf, gid_f,
+                     e->fin_glob.as<uint64_t>());
    }
    e->lat_written = lat != nullptr;
    if (e->nb)

@@ -565,7 +565,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
             {
                const uint64_t fin = tn + ps_of<F1>(aux_F(ax), c.f);
                if (bcr) c.bc_fin[v] = fin;
-               else final_ps[pk_index(c, id)] = fin;
+               else final_ps[id] = fin;
                continue;
             }
             Rec o;
@@ -648,10 +648,13 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
                                                   const uint8_t* __restrict__ routed, uint64_t* __restrict__ final_ps,
                                                   uint64_t* __restrict__ zl, uint64_t* __restrict__ cont, int closed_form,
                                                   uint32_t cx0, uint32_t cx1, uint32_t* __restrict__ lat32,
-                                                  unsigned* __restrict__ lat_ovf)
+                                                  unsigned* __restrict__ lat_ovf, const uint32_t* __restrict__ gid,
+                                                  const uint64_t* __restrict__ fin_glob)
 {
    // lat32 (gnoc_fetch_latency): final_ps - inject_ps as u32; one that does not fit
    // sets *lat_ovf.  Undelivered (other rank) and broadcast packets are not written.
+   // gid (a partitioned sharded rank): its delivery level wrote the final times by
+   // global id into fin_glob; a routed packet's comes from there.
    for (uint64_t i = blockIdx.x * (uint64_t) blockDim.x + threadIdx.x; i < n; i += (uint64_t) gridDim.x * blockDim.x)
    {
       const uint32_t dx = aux_dx(aux[i]), dy = aux_dy(aux[i]);
@@ -679,8 +682,11 @@ __global__ __launch_bounds__(256) void k_finalize(DevCfg c, uint64_t n, const ui
       const uint64_t z = c.hop_counter ? ps_of<F1>((hops - 1) * (c.R + c.Lk), c.f) + ps_of<F1>(aux_F(aux[i]), c.f)
                                        : ps_of<F1>(0, c.f) + hops * rl_of(c, src[i]) + ps_of<F1>(aux_F(aux[i]), c.f);
       zl[i] = z;
-      if (closed_form) final_ps[i] = inj[i] + z;
-      const uint64_t l = final_ps[i] - inj[i];
+      uint64_t fin;
+      if (closed_form) fin = inj[i] + z;
+      else fin = gid ? fin_glob[gid[i]] : final_ps[i];
+      if (closed_form || gid) final_ps[i] = fin;
+      const uint64_t l = fin - inj[i];
       cont[i] = l - z;
       if (lat32)
       {
@@ -805,9 +811,9 @@ template __global__ void k_bcast_final<false>(DevCfg, const uint32_t*, const uin
                                               uint64_t*, int);
 template __global__ void k_finalize<true>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,
                                           const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int, uint32_t, uint32_t,
-                                          uint32_t*, unsigned*);
+                                          uint32_t*, unsigned*, const uint32_t*, const uint64_t*);
 template __global__ void k_finalize<false>(DevCfg, uint64_t, const uint64_t*, const uint32_t*, const uint32_t*,
                                            const uint8_t*, uint64_t*, uint64_t*, uint64_t*, int, uint32_t, uint32_t,
-                                           uint32_t*, unsigned*);
+                                           uint32_t*, unsigned*, const uint32_t*, const uint64_t*);
 
 }  // namespace gnoc

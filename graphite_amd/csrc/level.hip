@@ -764,7 +764,7 @@ __device__ void lv_serial(LvSmem& sm, const DevCfg& c, Rec* __restrict__ recs, u
          const uint64_t tn = t + LV_PS(cc) + rl;
          if (dir == P_SELF)
          {
-            if (id < c.npk) final_ps[pk_index(c, id)] = tn + LV_PS(aux_F(ax));
+            if (id < c.npk) final_ps[id] = tn + LV_PS(aux_F(ax));
             else atomicOr(errflag, 1u);
             continue;
          }
@@ -838,7 +838,7 @@ __device__ void lv_emit(LvSmem& sm, const DevCfg& c, const Seg& sg, const Scan3&
          if (dir == P_SELF)
          {
             // NetworkModel::processReceivedPacket: + serialization (network_model.cc:142-150)
-            if (id < c.npk) final_ps[pk_index(c, id)] = tn + LV_PS(aux_F(ax));
+            if (id < c.npk) final_ps[id] = tn + LV_PS(aux_F(ax));
             else atomicOr(errflag, 1u);
             continue;
          }

@@ -1,9 +1,6 @@
-cd /tmp && export TMPDIR=/tmp && cd /root/repo && mkdir -p gpurun_out/kt_shard && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/kt_shard -o kt -- python3 -u tools/shard_timing.py 64 8 > gpurun_out/kt_shard/out.json 2>&1; python3 - <<'PY'
-import csv, glob
-f = glob.glob('gpurun_out/kt_shard/**/kt_kernel_trace.csv', recursive=True) or glob.glob('gpurun_out/kt_shard/*kernel_trace.csv')
-rows = list(csv.DictReader(open(f[0])))
-lv = [r for r in rows if 'k_level' in r['Kernel_Name']]
-print(len(lv), 'k_level dispatches')
-for r in lv[-40:]:
-    print(r['Grid_Size'], (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1000.0)
-PY
+cd /root/repo && mkdir -p gpurun_out && timeout -k 10 600 python -u -m pytest tests/test_gpu_shard.py tests/test_gpu_fullsize_golden.py -k "shard or rank or configs2" -q --timeout 300 --timeout-method thread > gpurun_out/shard_tests.log 2>&1 && timeout -k 10 300 python -u tools/shard_timing.py 64 8 > gpurun_out/shard_timing_r4b.json 2> gpurun_out/shard_timing_r4b.err; tail -3 gpurun_out/shard_tests.log; python -c "
+import json
+d=json.load(open('gpurun_out/shard_timing_r4b.json'))
+print(d['max_rank_device_ms'], d['one_gpu_k_chain_ms'])
+for r in d['per_rank']: print(r['rank'], r['device_ms'], r['k_level_ms'], r['k_chain_ms'], r['kernels'].get('k_finalize'), r['prep_ms'])
+"
