@@ -198,3 +198,32 @@ def test_latency_readback_refuses_overflow():
     eng.fetch_wait()
     assert np.array_equal(f64, fin)
     eng.close()
+
+
+@pytest.mark.parametrize("n,esc_every", [(0, 0), (1, 0), (2047, 0), (2048, 1), (2049, 2048), (6145, 7), (4097, 2047)])
+def test_packed_decode_block_edges(n, esc_every):
+    """The delta decode's segmented scan at its block edges (2,048 packets per
+    decode block): batch sizes around one and several blocks, escapes on every
+    packet, at block boundaries and scattered; the decoded inject times (read back
+    as final_ps - latency of a contention-free run, i.e. through the whole path)
+    equal the 24-B upload's results."""
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    rng = np.random.default_rng(n + esc_every)
+    gaps = rng.integers(0, 3, n).astype(np.uint64) * np.uint64(1000)
+    if esc_every:
+        gaps[::esc_every] += np.uint64(70_000)          # differences that need an escape
+    t = np.cumsum(gaps, dtype=np.uint64) + np.uint64(5_000)
+    src = rng.integers(0, 64, n).astype(np.uint32)
+    dst = rng.integers(0, 64, n).astype(np.uint32)
+    tr = gnoc.Trace(t, src, dst, np.full(n, 576, np.uint32), np.zeros(n, np.uint32))
+    pt = gnoc.PackedTrace.of(tr)
+    if esc_every == 1:
+        assert pt.abs_ps.size == n - 1   # (the first packet is t0 itself)
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    eng.run()
+    want = eng.results().final_ps.copy()
+    eng.submit_packed(pt)
+    eng.run()
+    assert np.array_equal(eng.results().final_ps, want)
+    eng.close()
