@@ -133,7 +133,7 @@ def main():
         ptr = pinned_trace(tr)
         fins = [torch.empty(len(tr), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64) for _ in range(2)]
         lats = [pinned_array(len(tr), np.uint32) for _ in range(2)]
-        K = max(2, a.steps // 2)
+        K = max(2, a.steps)   # batches per pipelined stream (the fill and the drain inside the clock)
         # the delta wire format (gnoc_packets_packed: u16 inject-time differences and
         # tile ids, lengths / flags only where they vary: 6 B per packet here) and the
         # narrow one (15 B) where the batch fits them, else the 24-B one
@@ -279,8 +279,8 @@ def main():
             "e2e_wire_bytes_per_packet": wire,
             "e2e_note": "host trace (pinned) -> host results per batch: submit (H2D + device-side decode and trace "
                         "checks) + run + read-back; e2e_ms_per_step pipelined (batch k+1's upload, decode and checks "
-                        "on the upload stream and batch k's read-back on a copy stream, beside the runs; the first "
-                        "upload and the last read-back inside the clock) in the delta wire format (gnoc_packets_packed)"
+                        "on the upload stream and batch k's read-back on a copy stream, beside the runs; a stream of "
+                        "--steps batches, its first upload and last read-back inside the clock) in the delta wire format (gnoc_packets_packed)"
                         " with the per-packet latency read back as u32 (gnoc_fetch_latency); "
                         "e2e_final_ps_ms_per_step the same with final_ps (u64); e2e_15B_ms_per_step the narrow wire "
                         "format with the latency; e2e_serial_ms_per_step one batch at a time (delta upload, final_ps);"

@@ -1198,14 +1198,25 @@ __global__ __launch_bounds__(PK_T) void k_dt_block(uint64_t n, const uint16_t* _
 {
    __shared__ uint32_t fl[PK_T], ne[PK_T];
    __shared__ uint64_t va[PK_T];
+   __shared__ uint16_t sd[PK_B];
    const uint32_t tid = threadIdx.x;
-   const uint64_t i0 = (uint64_t) blockIdx.x * PK_B + (uint64_t) tid * PK_PT;
+   const uint64_t b0 = (uint64_t) blockIdx.x * PK_B;
+   // the block's differences through LDS (coalesced), then each thread's PK_PT
+   // consecutive ones
+#pragma unroll
+   for (uint32_t k = 0; k < PK_PT; k++)
+   {
+      const uint64_t i = b0 + k * PK_T + tid;
+      sd[k * PK_T + tid] = i < n ? dt[i] : (uint16_t) 0;
+   }
+   __syncthreads();
+   const uint64_t i0 = b0 + (uint64_t) tid * PK_PT;
    uint32_t f = 0, c = 0;
    uint64_t v = 0;
    for (uint32_t k = 0; k < PK_PT; k++)
    {
       if (i0 + k >= n) break;
-      const uint16_t d = dt[i0 + k];
+      const uint16_t d = sd[tid * PK_PT + k];
       if (d == PK_ESC)
       {
          f = 1;
@@ -1281,15 +1292,34 @@ __global__ __launch_bounds__(PK_T) void k_dt_unpack(uint64_t n, const uint16_t* 
 {
    __shared__ uint32_t fl[PK_T], ne[PK_T];
    __shared__ uint64_t va[PK_T];
+   __shared__ uint16_t sd[PK_B];
+   __shared__ uint64_t st[PK_B];
    const uint32_t tid = threadIdx.x;
-   const uint64_t i0 = (uint64_t) blockIdx.x * PK_B + (uint64_t) tid * PK_PT;
+   const uint64_t b0 = (uint64_t) blockIdx.x * PK_B;
+   // the other fields widen lane-strided (coalesced); the differences go through
+   // LDS to each thread's PK_PT consecutive ones, and the inject times back
+#pragma unroll
+   for (uint32_t k = 0; k < PK_PT; k++)
+   {
+      const uint64_t i = b0 + k * PK_T + tid;
+      sd[k * PK_T + tid] = i < n ? dt[i] : (uint16_t) 0;
+      if (i < n)
+      {
+         osrc[i] = src[i];
+         odst[i] = dst[i];
+         obits[i] = bits ? (uint32_t) bits[i] : bits_all;
+         oflags[i] = flags ? (uint32_t) flags[i] : 0u;
+      }
+   }
+   __syncthreads();
+   const uint64_t i0 = b0 + (uint64_t) tid * PK_PT;
    uint16_t d[PK_PT];
    uint32_t c = 0, f = 0;
    uint64_t tail = 0;
 #pragma unroll
    for (uint32_t k = 0; k < PK_PT; k++)
    {
-      d[k] = i0 + k < n ? dt[i0 + k] : (uint16_t) 0;
+      d[k] = sd[tid * PK_PT + k];
       if (i0 + k < n && d[k] == PK_ESC)
       {
          f = 1;
@@ -1317,14 +1347,16 @@ __global__ __launch_bounds__(PK_T) void k_dt_unpack(uint64_t n, const uint16_t* 
 #pragma unroll
    for (uint32_t k = 0; k < PK_PT; k++)
    {
-      const uint64_t i = i0 + k;
-      if (i >= n) break;
+      if (i0 + k >= n) break;
       T = d[k] == PK_ESC ? abs_ps[eo++] : T + d[k];
-      oinj[i] = T;
-      osrc[i] = src[i];
-      odst[i] = dst[i];
-      obits[i] = bits ? (uint32_t) bits[i] : bits_all;
-      oflags[i] = flags ? (uint32_t) flags[i] : 0u;
+      st[tid * PK_PT + k] = T;
+   }
+   __syncthreads();
+#pragma unroll
+   for (uint32_t k = 0; k < PK_PT; k++)
+   {
+      const uint64_t i = b0 + k * PK_T + tid;
+      if (i < n) oinj[i] = st[k * PK_T + tid];
    }
 }
 
