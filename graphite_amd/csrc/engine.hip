@@ -157,6 +157,10 @@ struct gnoc_engine
    uint64_t* h_val = nullptr;               // (pinned, 128 B) a staged batch's ValOut
    DevBuf vbuf2;                            // a staged batch's validation scratch (upload stream)
    bool staged_val = false;                 // the staged batch was validated on the upload stream
+   // a delta-format batch (stage_packed): its decoded escape count on the device and
+   // the absolute times the caller gave, checked by the validation that follows
+   const uint64_t* val_esc = nullptr;
+   uint64_t val_nabs = 0;
 
    // a sharded rank's partitioned trace (gnoc_submit): only the packets of its
    // row band (sources) or column band (destinations), in trace order; gid maps
@@ -868,6 +872,7 @@ static int chain_tables(gnoc_engine* e)
 // (prep.hip k_validate over e->d_*): the first offending packet of any check,
 // the hop records this engine materialises, the turn exchange counts of a
 // sharded engine, and the chain engine's window size from the busiest port.
+__global__ void k_pk_check(const uint64_t* __restrict__ esc, uint64_t n_abs, unsigned long long* __restrict__ bad);
 // The trace arrays a validation reads (the current batch's, or a staged one's).
 struct ValTrace
 {
@@ -931,6 +936,12 @@ static int validate_launch(gnoc_engine* e, size_t n, ValTrace t, hipStream_t s, 
       hipLaunchKernelGGL(k_validate_max, dim3(1), dim3(1024), 0, s, W, H, dxr, dxl, dyu, dyd, insx, insy, vo);
       GNOC_HIP(e, hipGetLastError());
    }
+   if (e->val_esc)
+   {
+      hipLaunchKernelGGL(k_pk_check, dim3(1), dim3(1), 0, s, e->val_esc, e->val_nabs, &vo->bad[VB_PACKED]);
+      GNOC_HIP(e, hipGetLastError());
+      e->val_esc = nullptr;
+   }
    GNOC_HIP(e, hipMemcpyAsync(h_out, vo, sizeof(ValOut), hipMemcpyDeviceToHost, s));
    if (xcnt_out) *xcnt_out = xcnt;
    return GNOC_OK;
@@ -973,6 +984,7 @@ static int validate_finish(gnoc_engine* e, const void* h_out, uint64_t* records,
          case VB_SWEEP: return fail(e, GNOC_ETRACE, "sweep packet crosses sweep points at packet " + at);
          case VB_ZERO_F: return fail(e, GNOC_ETRACE, "zero-flit packet " + at);
          case VB_F_MAX: return fail(e, GNOC_EUNSUPPORTED, "packet longer than 2047 flits (packet " + at + ")");
+         case VB_PACKED: return fail(e, GNOC_ETRACE, "packed trace: the dt escapes (0xFFFF) do not match n_abs");
          default: return fail(e, GNOC_EUNSUPPORTED, "inject time beyond 2^50 ps at packet " + at);
       }
    }
@@ -1280,6 +1292,13 @@ __global__ __launch_bounds__(1024) void k_dt_carry(uint32_t nblk, uint64_t t0, c
       }
       __syncthreads();
    }
+   if (tid == 0) escbase[nblk] = s_e;   // the batch's escapes (checked against n_abs)
+}
+// The validation's verdict on a delta-format batch: its escapes must be exactly the
+// absolute times the caller gave (else the decode read past them).
+__global__ void k_pk_check(const uint64_t* __restrict__ esc, uint64_t n_abs, unsigned long long* __restrict__ bad)
+{
+   if (*esc != n_abs) *bad = 0ull;
 }
 __global__ __launch_bounds__(PK_T) void k_dt_unpack(uint64_t n, const uint16_t* __restrict__ dt,
                                                     const uint64_t* __restrict__ abs_ps, const uint64_t* __restrict__ carry,
@@ -1380,8 +1399,14 @@ static int stage_packed(gnoc_engine* e, const gnoc_packets_packed* pk, size_t n,
    // dt, src, dst, bits (u16) | flags (u8) | abs_ps | block aggregates, carries, escape bases (8-B aligned)
    const size_t o_f8 = n * 8, o_abs = (o_f8 + n + 15) / 16 * 16, o_agg = o_abs + (size_t) pk->n_abs * 8;
    const size_t o_car = o_agg + (size_t) nblk * sizeof(PkAgg), o_eb = o_car + (size_t) nblk * 8;
-   GNOC_HIP(e, stage.ensure(o_eb + (size_t) nblk * 8 + 16));
-   if (!n) return GNOC_OK;
+   GNOC_HIP(e, stage.ensure(o_eb + ((size_t) nblk + 1) * 8 + 16));   // (+ the escape total)
+   e->val_esc = nullptr;
+   e->val_nabs = pk->n_abs;
+   if (!n)
+   {
+      if (pk->n_abs) return fail(e, GNOC_ETRACE, "packed trace: absolute times given for an empty batch");
+      return GNOC_OK;
+   }
    char* sb = static_cast<char*>(stage.p);
    uint16_t* s16 = reinterpret_cast<uint16_t*>(sb);
    uint8_t* f8 = reinterpret_cast<uint8_t*>(sb + o_f8);
@@ -1397,6 +1422,7 @@ static int stage_packed(gnoc_engine* e, const gnoc_packets_packed* pk, size_t n,
    if (pk->n_abs) GNOC_HIP(e, hipMemcpyAsync(ab, pk->abs_ps, (size_t) pk->n_abs * 8, hipMemcpyHostToDevice, q));
    hipLaunchKernelGGL(k_dt_block, dim3(nblk), dim3(PK_T), 0, q, (uint64_t) n, (const uint16_t*) s16, agg);
    hipLaunchKernelGGL(k_dt_carry, dim3(1), dim3(1024), 0, q, nblk, pk->t0, (const uint64_t*) ab, (const PkAgg*) agg, car, ebs);
+   e->val_esc = ebs + nblk;
    hipLaunchKernelGGL(k_dt_unpack, dim3(nblk), dim3(PK_T), 0, q, (uint64_t) n, (const uint16_t*) s16, (const uint64_t*) ab,
                       (const uint64_t*) car, (const uint64_t*) ebs, (const uint16_t*) (s16 + n), (const uint16_t*) (s16 + 2 * n),
                       pk->bits ? (const uint16_t*) (s16 + 3 * n) : nullptr, pk->bits_all,

@@ -121,6 +121,7 @@ enum : uint32_t
    VB_ZERO_F,        // routed packet of zero flits
    VB_F_MAX,         // more than AUX_F_MAX flits
    VB_T_MAX,         // inject time >= 2^50 ps
+   VB_PACKED,        // delta wire format: the escapes do not match the absolute times given
    VB_KINDS
 };
 struct ValOut

@@ -227,3 +227,30 @@ def test_packed_decode_block_edges(n, esc_every):
     eng.run()
     assert np.array_equal(eng.results().final_ps, want)
     eng.close()
+
+
+def test_packed_escape_count_is_checked():
+    """A delta-format batch whose 0xFFFF escapes do not match the absolute times it
+    gives (n_abs) is refused by the submit's checks (synchronous and staged), instead
+    of decoding past the given times."""
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    t = (np.arange(3000, dtype=np.uint64) * np.uint64(40_000))   # every difference escapes
+    rng = np.random.default_rng(5)
+    tr = gnoc.Trace(t, rng.integers(0, 64, 3000).astype(np.uint32), rng.integers(0, 64, 3000).astype(np.uint32),
+                    np.full(3000, 576, np.uint32), np.zeros(3000, np.uint32))
+    pt = gnoc.PackedTrace.of(tr)
+    assert pt.abs_ps.size == 0   # 40,000 ps differences fit below 0xFFFF
+    bad = gnoc.PackedTrace(pt.t0, pt.dt.copy(), np.array([7], np.uint64), pt.src, pt.dst, pt.bits, pt.bits_all, pt.flags)
+    bad.dt[1000] = gnoc.PackedTrace.ESC
+    bad.dt[1001] = gnoc.PackedTrace.ESC   # two escapes, one absolute time
+    eng = gnoc.Engine(cfg)
+    with pytest.raises(gnoc.GnocError, match="escapes"):
+        eng.submit_packed(bad)
+    eng.submit(tr)
+    eng.run()
+    eng.submit_async_packed(bad)
+    with pytest.raises(gnoc.GnocError, match="escapes"):
+        eng.submit_commit()
+    eng.submit_packed(pt)          # a correct one still goes through
+    eng.run()
+    eng.close()
