@@ -1,9 +1,11 @@
 """Exception tails of the injection level merged into order before the chains
 (chain.hip k_exc_merge): a batch whose injection queues serve cycle-0 bursts by
 M/G/1 (the history tree's analytical branch, queue_model_history_tree.cc:58-64)
-stays on the chain engine, bit-exact against the oracle.  A batch whose M/G/1
-requests reach only Y-direction ports keeps its X phase on the chains and runs
-the Y and SELF levels on k_level (engine path 5)."""
+stays on the chain engine, bit-exact against the oracle.  M/G/1 requests in mesh
+ports send the batch to k_chain's MG instantiation (the no-gap prefix served
+serially); where that declines too (an M/G/1-served spill) the
+Y and SELF levels run on k_level (engine path 5) or the batch on the level
+engine (path 1).  Every path is bit-exact."""
 import numpy as np
 import pytest
 
