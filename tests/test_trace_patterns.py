@@ -65,3 +65,22 @@ def test_packed_wire_format_round_trip_on_host():
         out.append(T)
     assert k == pt.abs_ps.size
     assert np.array_equal(np.array(out, np.uint64), t)
+
+
+def test_packed_wire_format_optional_arrays():
+    """gnoc.PackedTrace keeps the length array only when lengths vary and the flag
+    array only when a flag is set; the fields it keeps equal the trace's."""
+    import numpy as np
+    from graphite_amd import gnoc
+    tr = gnoc.synthetic_trace(8, 8, 0.02, 300, seed=4).normalized()
+    bits = tr.bits.copy()
+    bits[::5] = 72
+    flags = tr.flags.copy()
+    flags[::7] |= gnoc.PKT_UNMODELED
+    pt = gnoc.PackedTrace.of(gnoc.Trace(tr.inject_ps, tr.src, tr.dst, bits, flags))
+    assert pt.bits is not None and pt.flags is not None
+    assert np.array_equal(pt.bits, bits.astype(np.uint16)) and np.array_equal(pt.flags, flags.astype(np.uint8))
+    assert np.array_equal(pt.src, tr.src.astype(np.uint16)) and np.array_equal(pt.dst, tr.dst.astype(np.uint16))
+    assert pt.wire_bytes() == len(pt) * 9 + 8 * pt.abs_ps.size
+    empty = gnoc.PackedTrace.of(gnoc.Trace(tr.inject_ps[:0], tr.src[:0], tr.dst[:0], tr.bits[:0], tr.flags[:0]))
+    assert len(empty) == 0 and empty.abs_ps.size == 0 and empty.wire_bytes() == 0
