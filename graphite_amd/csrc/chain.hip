@@ -252,6 +252,8 @@ __device__ __forceinline__ uint32_t wave_sum32(uint32_t v)
    v += dpp32<0x143, 0xC, 0xF>(v);
    return v;
 }
+// Inclusive wave prefix sum (lane l: lanes 0..l), DPP row_shr / row_bcast.
+__device__ __forceinline__ uint32_t wave_sum32_incl(uint32_t v) { return wave_sum32(v); }
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v)
 {
    v += dpp64<0x111, 0xF, 0xF>(v);

@@ -31,6 +31,7 @@
 #include "shard.hip"
 #include "serial.hip"
 #include "chain.hip"
+#include "pipe.hip"
 
 
 namespace gnoc {
@@ -87,12 +88,12 @@ struct DevBuf
 enum KernelClass
 {
    KC_CLASSIFY, KC_SRC_TOT, KC_INJ_BASE, KC_SRC_OFFS, KC_SCATTER, KC_ROW_HIST, KC_PROW, KC_SLOT_COUNTS, KC_SCAN,
-   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_BCAST, KC_CHAIN, KC_BOUNDS, KC_N
+   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_BCAST, KC_CHAIN, KC_BOUNDS, KC_PIPE, KC_N
 };
 static const char* const kKernelNames[KC_N] = { "k_classify", "k_src_tot", "k_inj_base", "k_src_offs", "k_scatter",
                                                 "k_row_hist", "k_prow", "k_slot_counts", "k_scan_slots", "k_plan",
                                                 "k_level", "k_port_stream", "k_finalize", "k_bcast",
-                                                "k_chain", "k_win_bounds" };
+                                                "k_chain", "k_win_bounds", "k_pipe" };
 
 struct gnoc_engine
 {
@@ -227,6 +228,7 @@ struct gnoc_engine
    double xy_lag = -1.0;                    // Y task key lag, in units of the batch's last injection time
    uint32_t ch_epoch = 0;
    int ch_grid = 0;
+   int ncu = 256;                           // compute units of the device
    int force_levels = 0;
    int ch_declined = 0;                     // this batch fell back from the chain engine: later runs skip it
    int ch_ydeclined = 0;                    // only its Y phase did: later runs take X chains + Y levels (path 5)
@@ -249,6 +251,16 @@ struct gnoc_engine
    int ch_lb_dec[2] = { -1, -1 };           // the decision per phase (-1: none yet: serial)
    int ch_trial = 0;                        // this run times a protocol (phases as separate launches)
    hipEvent_t ch_ev[2][2] = { { nullptr, nullptr }, { nullptr, nullptr } };
+
+   // v6 port pipelines (pipe.hip): one wave per chain port
+   int used_pipe = 0;
+   int pipe_declined = 0;                   // this batch fell back from the pipelines: later runs take the chains
+   uint32_t pipe_tag = 0;                   // epoch of the segment-link records (1 .. 65535)
+   const void* pipe_recs = nullptr;         // the record buffer the tags were cleared in
+   size_t pipe_recs_bytes = 0;
+   uint32_t pipe_S[2] = { 0, 0 };           // ports per segment of the last pipeline run (X, Y)
+   unsigned pipe_flags[2] = { 0, 0 };       // the last pipeline run's flag words
+   DevBuf pipe_ctr, pipe_dbg0, pipe_dbg1;
 
    // kernel profiling (gnoc_set_profiling)
    bool prof = false;
@@ -499,6 +511,7 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
       if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c1, ch::k_chain<1, true, false>, ch::T, 0);
       if (he == hipSuccess) he = hipOccupancyMaxActiveBlocksPerMultiprocessor(&c3, ch::k_chain<3, true, true>, ch::T, 0);
       e->ch_grid = std::max(1, std::min(c1, c3)) * std::max(1, cus);
+      e->ncu = std::max(1, cus);
    }
    if (he != hipSuccess)
    {
@@ -689,6 +702,7 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
    e->ch_ydeclined = 0;
    e->exc_fix = 0;
    e->ch_mg = 0;
+   e->pipe_declined = 0;
    if (same) return;
    const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size (2^shift ps)
    const char* pv = std::getenv("GNOC_WINDOW_PS");      // test knob: force the window size (ps)
@@ -2011,6 +2025,7 @@ constexpr int GNOC_CH_FALLBACK = 1002;   // the chain engine cannot take this ba
 constexpr int GNOC_CH_EXC = 1003;        // only the injection level's exception tails: merge them, rerun
 constexpr int GNOC_CH_YFALL = 1004;      // only the Y chains declined: Y and SELF levels on k_level
 constexpr int GNOC_CH_MG = 1005;         // the chains met the M/G/1 branch: rerun on the MG instantiation
+constexpr int GNOC_PIPE_DECLINE = 1006;  // the port pipelines cannot take this batch: rerun on the chains
 
 // ---------------------------------------------------------------------------
 // v4: chain engine for the X and Y phases (chain.hip); INJ and SELF levels on k_level
@@ -2249,6 +2264,115 @@ static int chain_fused(gnoc_engine* e)
    return GNOC_OK;
 }
 
+// ---------------------------------------------------------------------------
+// v6: the X and Y phases as port pipelines (pipe.hip), one wave per chain port
+// ---------------------------------------------------------------------------
+// A 1 GHz, unsharded batch whose chains the chain engine could take.  The pipelines
+// decline what they do not serve exactly (the no-gap M/G/1 branch in a chain port,
+// times beyond 2^31 cycles): the batch then reruns on the chain engine (path 4), and
+// later runs of it start there.  GNOC_PIPE=0 turns the pipelines off.
+static bool pipe_usable(const gnoc_engine* e)
+{
+   const char* v = std::getenv("GNOC_PIPE");
+   if (!(v && *v && std::atoi(v) != 0)) return false;   // (opt-in while it is measured against the chains)
+   return e->f1 && !e->pipe_declined && !e->ch_mg && e->nranks <= 1;
+}
+
+// Ports per segment workgroup: about one workgroup per CU (the phase's ports over the
+// CUs), at least 2 so that both hand-offs (LDS ring, HBM link) run; GNOC_PIPE_S forces it.
+static uint32_t pipe_seg(const gnoc_engine* e, uint32_t ports, uint32_t len)
+{
+   const char* v = std::getenv("GNOC_PIPE_S");
+   uint32_t S = v && std::atoi(v) > 0 ? (uint32_t) std::atoi(v) : (ports + e->ncu - 1) / std::max(1, e->ncu);
+   S = std::max<uint32_t>(S, 2u);
+   S = std::min<uint32_t>(S, 8u);
+   return std::max<uint32_t>(1u, std::min(S, len));
+}
+
+static int pipe_setup(gnoc_engine* e)
+{
+   const DevCfg& c = e->dc;
+   hipStream_t s = e->stream;
+   e->ncpx = c.W > 1 ? 2 * (e->ry1 - e->ry0) * (c.W - 1) : 0;
+   e->ncpy = c.H > 1 ? 2 * (e->cx1 - e->cx0) * (c.H - 1) : 0;
+   const uint32_t ncp = e->ncpx + e->ncpy;
+   GNOC_HIP(e, e->ch_cp.ensure((size_t) std::max<uint32_t>(ncp, 1) * sizeof(ChainPort)));
+   GNOC_HIP(e, e->pipe_ctr.ensure(256));
+   e->zq.push_back({ e->pipe_ctr.p, 256 });   // (zq_flush: before the first level)
+   for (int p = 0; p < 2; p++)
+      for (int q = 0; q < 2; q++)
+         if (!e->ch_ev[p][q]) GNOC_HIP(e, hipEventCreate(&e->ch_ev[p][q]));
+   e->pipe_tag++;   // (run_prep cleared the record buffer when it was new or the epoch wrapped)
+   if (ncp)
+      GNOC_LAUNCH(e, KC_PLAN, ch::k_chain_plan, dim3((ncp + 255) / 256), dim3(256), 0, s, c, e->ncpx, e->ncpy, e->ry0,
+                  e->cx0, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->ch_cp.as<ChainPort>());
+   return GNOC_OK;
+}
+
+static int pipe_phase(gnoc_engine* e, int phase)
+{
+   {
+      const int zr = zq_flush(e, e->stream);
+      if (zr) return zr;
+   }
+   hipStream_t s = e->stream;
+   const uint32_t ncp = phase ? e->ncpy : e->ncpx;
+   if (!ncp) return GNOC_OK;
+   const uint32_t len = phase ? e->dc.H - 1 : e->dc.W - 1;
+   pp::PipeArgs a{};
+   a.cp = e->ch_cp.as<ChainPort>() + (phase ? e->ncpx : 0);
+   a.recs = e->recs.as<Rec>();
+   a.samp_t = e->samp_t.as<uint64_t>();
+   a.samp_id = e->samp_id.as<uint32_t>();
+   a.port_sum = e->port_sum.as<unsigned long long>();
+   a.port_cnt = e->port_cnt.as<unsigned long long>();
+   a.port_flit = e->port_flit.as<unsigned long long>();
+   a.port_last = e->port_last.as<unsigned long long>();
+   a.errflag = e->counters.as<unsigned>() + 8;
+   a.ctr = e->pipe_ctr.as<unsigned>() + phase;
+   a.nch = ncp / len;
+   a.len = len;
+   a.S = pipe_seg(e, ncp, len);
+   a.fw = phase ? 5u : 4u;
+   a.rcap = 512;
+   a.scap = 128;
+   a.mcap = 128;
+   a.tag = e->pipe_tag;
+   a.excfix = (uint32_t) e->exc_fix;
+   a.analytical = (uint32_t) e->dc.analytical;
+   a.nsamp = (uint32_t) (e->rec_bound / 64 + 1);
+   a.spin_shift = 33;
+   a.dbg = nullptr;
+   const char* dv = std::getenv("GNOC_PIPE_DEBUG");
+   if (dv && *dv)
+   {
+      // every wave's state at its end (or where it gave up), printed after the run
+      const size_t nd = ((size_t) ncp + (size_t) (ncp / len) * ((len + 1) / 2 + 1)) * pp::DBG_W;
+      DevBuf& db = phase ? e->pipe_dbg1 : e->pipe_dbg0;
+      GNOC_HIP(e, db.ensure(nd * 4));
+      GNOC_HIP(e, hipMemsetAsync(db.p, 0, nd * 4, s));
+      a.dbg = db.as<uint32_t>();
+      a.spin_shift = (uint32_t) std::max(20, std::min(36, std::atoi(dv) > 1 ? std::atoi(dv) : 31));
+   }
+   e->pipe_S[phase] = a.S;
+   const uint32_t nseg = (len + a.S - 1) / a.S;
+   const uint32_t grid = a.nch * nseg;
+   const size_t lds = phase ? pp::lds_bytes<3>(a.S, a.rcap, a.scap, a.mcap) : pp::lds_bytes<1>(a.S, a.rcap, a.scap, a.mcap);
+   GNOC_HIP(e, hipEventRecord(e->ch_ev[phase][0], s));
+   if (phase)
+   {
+      GNOC_HIP(e, hipFuncSetAttribute((const void*) pp::k_pipe<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
+      GNOC_LAUNCH(e, KC_PIPE, pp::k_pipe<3>, dim3(grid), dim3(64 * (a.S + 1)), lds, s, a);
+   }
+   else
+   {
+      GNOC_HIP(e, hipFuncSetAttribute((const void*) pp::k_pipe<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
+      GNOC_LAUNCH(e, KC_PIPE, pp::k_pipe<1>, dim3(grid), dim3(64 * (a.S + 1)), lds, s, a);
+   }
+   GNOC_HIP(e, hipEventRecord(e->ch_ev[phase][1], s));
+   return GNOC_OK;
+}
+
 static int run_post(gnoc_engine* e, bool closed_form);
 static int run_post_enqueue(gnoc_engine* e, bool closed_form);
 static int run_post_check(gnoc_engine* e, bool closed_form);
@@ -2328,6 +2452,16 @@ static int run_prep(gnoc_engine* e, bool* done)
    GNOC_HIP(e, e->counters.ensure(64));
    GNOC_HIP(e, e->gtot.ensure(16));
    GNOC_HIP(e, e->recs.ensure(e->rec_bound * sizeof(Rec)));
+   // the port pipelines' segment links carry a 16-bit epoch tag (pipe.hip): the record
+   // buffer is cleared when it is new (stale records of another engine could carry any
+   // tag) and when the epoch wraps, before this run's scatter writes into it
+   if (e->recs.p != e->pipe_recs || e->recs.bytes != e->pipe_recs_bytes || e->pipe_tag >= 0xFFFEu)
+   {
+      GNOC_HIP(e, hipMemsetAsync(e->recs.p, 0, e->recs.bytes, s));
+      e->pipe_recs = e->recs.p;
+      e->pipe_recs_bytes = e->recs.bytes;
+      e->pipe_tag = 0;
+   }
    GNOC_HIP(e, e->samp_t.ensure((e->rec_bound / 64 + 1) * 8));
    GNOC_HIP(e, e->samp_id.ensure((e->rec_bound / 64 + 1) * 4));
    GNOC_HIP(e, e->Hs.ensure((size_t) N * W * 3 * 4));
@@ -2586,6 +2720,49 @@ static int run_post_check(gnoc_engine* e, bool closed_form)
    const unsigned* ef = (const unsigned*) (e->h_pinned + 8);
    const unsigned errf = ef[0];
    const unsigned cf = ef[4] | ef[5];   // the X phase's and the Y phase's chain flags
+   if (e->used_pipe)
+   {
+      e->pipe_flags[0] = ef[4];
+      e->pipe_flags[1] = ef[5];
+      if (std::getenv("GNOC_PIPE_DEBUG") && *std::getenv("GNOC_PIPE_DEBUG"))
+         for (int p = 0; p < 2; p++)
+         {
+            const DevBuf& db = p ? e->pipe_dbg1 : e->pipe_dbg0;
+            if (!db.p) continue;
+            std::vector<uint32_t> h(db.bytes / 4);
+            if (hipMemcpy(h.data(), db.p, db.bytes, hipMemcpyDeviceToHost) != hipSuccess) continue;
+            uint32_t ends = 0, stuck = 0;
+            for (size_t r = 0; r + pp::DBG_W <= h.size(); r += pp::DBG_W)
+            {
+               const uint32_t tagw = h[r] >> 16, why = h[r] & 0xFFFFu;
+               if (tagw != 0xB0DEu && tagw != 0xC0DEu) continue;
+               ends++;
+               if (!why && !std::getenv("GNOC_PIPE_DEBUG_ALL")) continue;
+               stuck += why != 0;
+               std::fprintf(stderr, "gnoc pipe %c %s #%zu why %u:", p ? 'Y' : 'X', tagw == 0xB0DEu ? "port" : "svc",
+                            r / pp::DBG_W, why);
+               for (uint32_t q = 1; q < 16; q++) std::fprintf(stderr, " %u", h[r + q]);
+               std::fprintf(stderr, " |");
+               for (uint32_t q = 16; q < 27; q++) std::fprintf(stderr, " %u", h[r + q]);
+               std::fprintf(stderr, "\n");
+            }
+            std::fprintf(stderr, "gnoc pipe %c: %u waves reported, %u gave up\n", p ? 'Y' : 'X', ends, stuck);
+         }
+   }
+   if (e->used_pipe && (cf & ch::F_ANY))
+   {
+      if (std::getenv("GNOC_CHAIN_DEBUG"))
+         std::fprintf(stderr, "gnoc: port pipelines declined, flags X 0x%x Y 0x%x\n", ef[4], ef[5]);
+      if (cf & ch::F_ROUTE)
+      {
+         char m[96];
+         std::snprintf(m, sizeof m, "internal: pipeline route-count invariant violated (flags 0x%x 0x%x)", ef[4], ef[5]);
+         return fail(e, GNOC_EHIP, m);
+      }
+      // the injection level left exception tails -> merge them first (as the chains do)
+      if (!e->exc_fix && (ef[4] & ch::R_EXC) && !(ef[2] & 2u)) return GNOC_CH_EXC;
+      return GNOC_PIPE_DECLINE;
+   }
    if (e->used_chain && !e->ch_fused && e->ch_trial && !(cf & ch::F_ANY))
    {
       // this run's time of each phase's protocol (chain_setup keeps the faster one)
@@ -2649,7 +2826,22 @@ static int run_once(gnoc_engine* e)
    const bool v3 = e->dc.max_list >= 3 && !e->force_v1;
    e->used_v3 = v3;
    e->used_chain = 0;
-   if (v3 && chain_usable(e))
+   e->used_pipe = 0;
+   if (v3 && chain_usable(e) && pipe_usable(e))
+   {
+      // v6: INJ level, X pipelines, Y pipelines, SELF level
+      const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
+      e->used_pipe = 1;
+      e->used_v3 = 6;
+      rc = run_plan_v3(e);
+      if (!rc) rc = pipe_setup(e);
+      if (!rc) rc = run_levels_v3(e, 0, 1);
+      if (!rc && e->exc_fix) rc = exc_merge(e);
+      if (!rc) rc = pipe_phase(e, 0);
+      if (!rc) rc = pipe_phase(e, 1);
+      if (!rc) rc = run_levels_v3(e, L - 1, L);
+   }
+   else if (v3 && chain_usable(e))
    {
       // v4: INJ level, X chains, Y chains, SELF level
       const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
@@ -3005,6 +3197,13 @@ static int run_impl(gnoc_engine* e)
          if (rc == GNOC_CH_MG)
          {
             e->ch_mg = 1;
+            e->n_retry++;
+            continue;
+         }
+         if (rc == GNOC_PIPE_DECLINE)
+         {
+            // the chain engine reruns the batch (and takes its later runs)
+            e->pipe_declined = 1;
             e->n_retry++;
             continue;
          }
