@@ -2362,5 +2362,13 @@ __global__ __launch_bounds__(256) void k_zero_ports(uint32_t nports, uint32_t dm
    s4[p] = 0;
 }
 
+// The SELF slots' exception counts (the MG instantiation's Y chains may leave tails
+// there); every other slot keeps its count, k_exc_merge's refused slots included.
+__global__ __launch_bounds__(256) void k_zero_self_nexc(uint32_t ntiles, uint32_t* __restrict__ nexc)
+{
+   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+   if (i < ntiles * INS) nexc[slot_of(i / INS, P_SELF, i % INS)] = 0;
+}
+
 }  // namespace ch
 }  // namespace gnoc

@@ -1263,8 +1263,14 @@ __global__ __launch_bounds__(PK_T) void k_dt_block(uint64_t n, const uint16_t* _
       agg[blockIdx.x] = PkAgg{ va[PK_T - 1], t, fl[PK_T - 1] };
    }
 }
+// An escape ordinal past the caller's n_abs absolute times reads 0 (never past the
+// array); k_pk_check reports the mismatch of escape count and n_abs as a bad batch.
+__device__ __forceinline__ uint64_t pk_abs(const uint64_t* __restrict__ abs_ps, uint64_t n_abs, uint64_t i)
+{
+   return i < n_abs ? abs_ps[i] : 0ull;
+}
 __global__ __launch_bounds__(1024) void k_dt_carry(uint32_t nblk, uint64_t t0, const uint64_t* __restrict__ abs_ps,
-                                                   const PkAgg* __restrict__ agg, uint64_t* __restrict__ carry,
+                                                   uint64_t n_abs, const PkAgg* __restrict__ agg, uint64_t* __restrict__ carry,
                                                    uint64_t* __restrict__ escbase)
 {
    __shared__ uint32_t fl[1024];
@@ -1288,7 +1294,7 @@ __global__ __launch_bounds__(1024) void k_dt_carry(uint32_t nblk, uint64_t t0, c
       }
       const uint64_t ebase = s_e + eb[tid] - g.nesc;   // escapes before block b
       fl[tid] = g.pad;                                  // the block has an escape
-      va[tid] = g.pad ? abs_ps[ebase + g.nesc - 1] + g.tail : g.tail;
+      va[tid] = g.pad ? pk_abs(abs_ps, n_abs, ebase + g.nesc - 1) + g.tail : g.tail;
       __syncthreads();
       seg_scan(fl, va, tid, 1024);
       // the time before block b: the previous inclusive value (or the carried one)
@@ -1315,7 +1321,8 @@ __global__ void k_pk_check(const uint64_t* __restrict__ esc, uint64_t n_abs, uns
    if (*esc != n_abs) *bad = 0ull;
 }
 __global__ __launch_bounds__(PK_T) void k_dt_unpack(uint64_t n, const uint16_t* __restrict__ dt,
-                                                    const uint64_t* __restrict__ abs_ps, const uint64_t* __restrict__ carry,
+                                                    const uint64_t* __restrict__ abs_ps, uint64_t n_abs,
+                                                    const uint64_t* __restrict__ carry,
                                                     const uint64_t* __restrict__ escbase, const uint16_t* __restrict__ src,
                                                     const uint16_t* __restrict__ dst, const uint16_t* __restrict__ bits,
                                                     uint32_t bits_all, const uint8_t* __restrict__ flags,
@@ -1372,7 +1379,7 @@ __global__ __launch_bounds__(PK_T) void k_dt_unpack(uint64_t n, const uint16_t* 
    }
    uint64_t eo = escbase[blockIdx.x] + ne[tid] - c;   // this thread's first escape ordinal
    fl[tid] = f;
-   va[tid] = f ? abs_ps[eo + c - 1] + tail : tail;
+   va[tid] = f ? pk_abs(abs_ps, n_abs, eo + c - 1) + tail : tail;
    __syncthreads();
    seg_scan(fl, va, tid, PK_T);
    const uint64_t cin = carry[blockIdx.x];
@@ -1381,7 +1388,7 @@ __global__ __launch_bounds__(PK_T) void k_dt_unpack(uint64_t n, const uint16_t* 
    for (uint32_t k = 0; k < PK_PT; k++)
    {
       if (i0 + k >= n) break;
-      T = d[k] == PK_ESC ? abs_ps[eo++] : T + d[k];
+      T = d[k] == PK_ESC ? pk_abs(abs_ps, n_abs, eo++) : T + d[k];
       st[tid * PK_PT + k] = T;
    }
    __syncthreads();
@@ -1435,10 +1442,11 @@ static int stage_packed(gnoc_engine* e, const gnoc_packets_packed* pk, size_t n,
    if (pk->flags) GNOC_HIP(e, hipMemcpyAsync(f8, pk->flags, n, hipMemcpyHostToDevice, q));
    if (pk->n_abs) GNOC_HIP(e, hipMemcpyAsync(ab, pk->abs_ps, (size_t) pk->n_abs * 8, hipMemcpyHostToDevice, q));
    hipLaunchKernelGGL(k_dt_block, dim3(nblk), dim3(PK_T), 0, q, (uint64_t) n, (const uint16_t*) s16, agg);
-   hipLaunchKernelGGL(k_dt_carry, dim3(1), dim3(1024), 0, q, nblk, pk->t0, (const uint64_t*) ab, (const PkAgg*) agg, car, ebs);
+   hipLaunchKernelGGL(k_dt_carry, dim3(1), dim3(1024), 0, q, nblk, pk->t0, (const uint64_t*) ab, (uint64_t) pk->n_abs,
+                      (const PkAgg*) agg, car, ebs);
    e->val_esc = ebs + nblk;
    hipLaunchKernelGGL(k_dt_unpack, dim3(nblk), dim3(PK_T), 0, q, (uint64_t) n, (const uint16_t*) s16, (const uint64_t*) ab,
-                      (const uint64_t*) car, (const uint64_t*) ebs, (const uint16_t*) (s16 + n), (const uint16_t*) (s16 + 2 * n),
+                      (uint64_t) pk->n_abs, (const uint64_t*) car, (const uint64_t*) ebs, (const uint16_t*) (s16 + n), (const uint16_t*) (s16 + 2 * n),
                       pk->bits ? (const uint16_t*) (s16 + 3 * n) : nullptr, pk->bits_all,
                       pk->flags ? (const uint8_t*) f8 : nullptr, inj.as<uint64_t>(), src.as<uint32_t>(), dst.as<uint32_t>(),
                       bits.as<uint32_t>(), flags.as<uint32_t>());
@@ -1481,6 +1489,7 @@ int gnoc_submit_narrow(gnoc_engine* e, const gnoc_packets_narrow* pk, size_t n)
 {
    if (!e || !pk) return GNOC_EINVAL;
    e->submitted = false;
+   e->val_esc = nullptr;   // no packed decode behind this batch
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    int rc = stage_narrow(e, pk, n, e->nw_stage, e->t_inj, e->t_src, e->t_dst, e->t_bits, e->t_flags, e->stream);
    if (rc) return rc;
@@ -1521,6 +1530,7 @@ int gnoc_submit(gnoc_engine* e, const gnoc_packets* pk_in, size_t n)
    if (n && (!pk_in->inject_ps || !pk_in->src || !pk_in->dst || !pk_in->bits)) return fail(e, GNOC_EINVAL, "null trace array");
    if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
    e->submitted = false;
+   e->val_esc = nullptr;   // no packed decode behind this batch
    const gnoc_packets* pk = pk_in;
    gnoc_packets sub{};
    std::vector<uint64_t> l_inj;
@@ -1630,6 +1640,7 @@ int gnoc_submit_async(gnoc_engine* e, const gnoc_packets* pk, size_t n)
    if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
    if (e->nranks > 1) return fail(e, GNOC_EUNSUPPORTED, "a sharded engine takes gnoc_submit");
    if (e->staged) return fail(e, GNOC_ESTATE, "a staged batch is waiting for gnoc_submit_commit");
+   e->val_esc = nullptr;   // no packed decode behind this batch
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    GNOC_HIP(e, pipe_streams(e));
    GNOC_HIP(e, e->t2_inj.ensure(n * 8));
@@ -1661,6 +1672,7 @@ int gnoc_submit_async_narrow(gnoc_engine* e, const gnoc_packets_narrow* pk, size
 {
    if (!e || !pk) return GNOC_EINVAL;
    if (e->staged) return fail(e, GNOC_ESTATE, "a staged batch is waiting for gnoc_submit_commit");
+   e->val_esc = nullptr;   // no packed decode behind this batch
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    GNOC_HIP(e, pipe_streams(e));
    int rc = stage_narrow(e, pk, n, e->nw_stage2, e->t2_inj, e->t2_src, e->t2_dst, e->t2_bits, e->t2_flags, e->s_h2d);
@@ -1793,12 +1805,10 @@ int gnoc_fetch_wait(gnoc_engine* e)
 
 int gnoc_submit_device(gnoc_engine* e, const gnoc_packets* pk, size_t n)
 {
-   if (e)
-   {
-      e->part = false;   // a device trace is used as is (every rank reads all of it)
-      e->n_glob = n;
-      }
    if (!e || !pk) return GNOC_EINVAL;
+   e->val_esc = nullptr;   // no packed decode behind this batch
+   e->part = false;        // a device trace is used as is (every rank reads all of it)
+   e->n_glob = n;
    if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits)) return fail(e, GNOC_EINVAL, "null trace array");
    if (n >= (1ull << 32) - 1) return fail(e, GNOC_EUNSUPPORTED, "more than 2^32-2 packets");
    if (e->nranks > 1) return fail(e, GNOC_EUNSUPPORTED, "a sharded engine takes host traces (gnoc_submit)");
@@ -2839,6 +2849,10 @@ static int run_once(gnoc_engine* e)
       if (!rc && e->exc_fix) rc = exc_merge(e);
       if (!rc) rc = pipe_phase(e, 0);
       if (!rc) rc = pipe_phase(e, 1);
+      if (!rc)
+         GNOC_LAUNCH(e, KC_PIPE, pp::k_pipe_samples, dim3(e->dc.N * INS), dim3(256), 0, e->stream, e->dc.N,
+                     e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(),
+                     e->samp_id.as<uint32_t>());
       if (!rc) rc = run_levels_v3(e, L - 1, L);
    }
    else if (v3 && chain_usable(e))
@@ -2898,7 +2912,9 @@ static int y_levels_rerun(gnoc_engine* e)
    GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 5, 0, 4, s));
    // the MG instantiation's Y chains may have left exception tails in the SELF slots;
    // every other slot's tails were merged (k_exc_merge) before the Y phase
-   if (e->ch_mg) GNOC_HIP(e, hipMemsetAsync(e->nexc.p, 0, (size_t) e->dc.N * PORTS * INS * 4, s));
+   if (e->ch_mg)
+      GNOC_LAUNCH(e, KC_CHAIN, ch::k_zero_self_nexc, dim3((e->dc.N * INS + 255) / 256), dim3(256), 0, s, e->dc.N,
+                  e->nexc.as<uint32_t>());
    const uint32_t np = e->dc.N * PORTS;
    GNOC_LAUNCH(e, KC_CHAIN, ch::k_zero_ports, dim3((np + 255) / 256), dim3(256), 0, s, np,
                (1u << P_UP) | (1u << P_DOWN) | (1u << P_SELF), e->port_sum.as<unsigned long long>(),
@@ -3805,7 +3821,12 @@ static int finish_check(gnoc_engine* e)
    e->n_fallback++;
    e->used_chain = 0;
    GNOC_HIP(e, hipMemsetAsync(e->counters.as<unsigned int>() + 8 + 4, 0, 8, s));
-   if (mg_ran) GNOC_HIP(e, hipMemsetAsync(e->nexc.p, 0, (size_t) e->dc.N * PORTS * INS * 4, s));
+   if (mg_ran)
+   {
+      hipLaunchKernelGGL(ch::k_zero_self_nexc, dim3((e->dc.N * INS + 255) / 256), dim3(256), 0, s, e->dc.N,
+                         e->nexc.as<uint32_t>());
+      GNOC_HIP(e, hipGetLastError());
+   }
    const uint32_t np = e->dc.N * PORTS;
    hipLaunchKernelGGL(ch::k_zero_ports, dim3((np + 255) / 256), dim3(256), 0, s, np,
                       (1u << P_UP) | (1u << P_DOWN) | (1u << P_SELF), e->port_sum.as<unsigned long long>(),

@@ -59,12 +59,18 @@ constexpr uint32_t C_WC = 0;           // [w] ring w written (by port w-1, or th
 constexpr uint32_t C_RC = 16;          // [w] ring w consumed (by port w)
 constexpr uint32_t C_SW = 32;          // [3 w + j] insert list j of port w staged (service wave)
 constexpr uint32_t C_SR = 80;          // [3 w + j] staged records consumed (port w)
+#ifndef PIPE_K
+#define PIPE_K 4   // records per lane per block (K = 8: 4.37 ms vs 3.86 ms on configs[1] uniform)
+#endif
 constexpr uint32_t C_SCR = 128;        // [SCR_W w ..] port w's scratch (the block's insert bitmap)
-constexpr uint32_t SCR_W = 16;
+constexpr uint32_t SCR_W = 16;         // (>= BLK / 32 bitmap words)
 constexpr uint32_t C_N = C_SCR + SCR_W * 16;
-constexpr uint32_t K = 4;              // records per lane in a block
+constexpr uint32_t K = PIPE_K;         // records per lane in a block
 constexpr uint32_t KB = K;
 constexpr uint32_t BLK = K * 64;       // records per block
+static_assert(BLK / 32 <= SCR_W && (BLK / 32) % 4 == 0, "bitmap words in the scratch");
+constexpr uint32_t RPAD = 16;          // entries after each ring: a trash entry for branch-free writes
+constexpr uint32_t OOB = 0xFFFFFFF0u;  // a buffer offset beyond every descriptor: the store is dropped
 
 struct PipeArgs
 {
@@ -98,7 +104,7 @@ constexpr bool TIMING = true;    // (a -DPIPE_TIMING build) cycles per activity 
 constexpr bool TIMING = false;
 #endif
 
-struct R4
+struct __attribute__((aligned(16))) R4   // (16-B aligned: one ds_read_b128 / ds_write_b128 per record)
 {
    uint32_t klo, khi, id, aux;
 };
@@ -179,7 +185,7 @@ __device__ __forceinline__ Lay lay_of(const PipeArgs& a, uint4* lds)
    Lay L;
    L.cnt = reinterpret_cast<uint32_t*>(lds);
    L.rings = reinterpret_cast<R4*>(lds + C_N / 4);
-   L.stage = L.rings + (size_t) a.S * a.rcap;
+   L.stage = L.rings + (size_t) a.S * (a.rcap + RPAD);
    L.mbuf = L.stage + (size_t) a.S * NL * a.scap;
    L.raw = L.mbuf + (NL > 1 ? (size_t) a.S * a.mcap : 0);
    return L;
@@ -187,7 +193,7 @@ __device__ __forceinline__ Lay lay_of(const PipeArgs& a, uint4* lds)
 template <int NL>
 __host__ __device__ inline size_t lds_bytes(uint32_t S, uint32_t rcap, uint32_t scap, uint32_t mcap)
 {
-   return C_N * 4 + (size_t) S * 16 * (rcap + (size_t) NL * scap + (NL > 1 ? mcap : 0)) + (size_t) (NLK + NLD) * 64 * 16;
+   return C_N * 4 + (size_t) S * 16 * (rcap + RPAD + (size_t) NL * scap + (NL > 1 ? mcap : 0)) + (size_t) (NLK + NLD) * 64 * 16;
 }
 
 // Entries of the window w[0, av) (a ring from base, mask m; av <= 64) below x: binary
@@ -406,8 +412,9 @@ __device__ void run_port(const PipeArgs& a, const Lay& L, uint32_t c, uint32_t i
    const uint32_t S = a.S, len = a.len, rmask = a.rcap - 1u, smask = a.scap - 1u, mmask = a.mcap - 1u;
    const uint32_t k = c * len + i;
    uint32_t* const cnt = L.cnt;
-   R4* const ring_in = L.rings + (size_t) w * a.rcap;
-   R4* const ring_out = ring_in + a.rcap;
+   R4* const ring_in = L.rings + (size_t) w * (a.rcap + RPAD);
+   R4* const ring_out = ring_in + a.rcap + RPAD;
+   R4* const trash = ring_out + a.rcap;                 // (writes of lanes with nothing to write)
    R4* const stg = L.stage + (size_t) w * NL * a.scap;
    R4* const mb = L.mbuf + (size_t) w * a.mcap;
 
@@ -422,6 +429,12 @@ __device__ void run_port(const PipeArgs& a, const Lay& L, uint32_t c, uint32_t i
    const uint32_t nins = ic0 + ic1 + ic2;
    const uint32_t ob0 = P.obase[0], ob1 = P.obase[1], ob2 = XC ? P.obase[2] : 0u, ob3 = XC ? P.obase[3] : 0u;
    const uint32_t oc0 = P.ocap[0], oc1 = P.ocap[1], oc2 = XC ? P.ocap[2] : 0u, oc3 = XC ? P.ocap[3] : 0u;
+   // the turn slots of the next tile (SELF, UP, DOWN) as one record range [tlo, thi)
+   uint32_t tlo = 0xFFFFFFFFu, thi = 0;
+   if (oc0) tlo = ob0, thi = ob0 + oc0;
+   if (oc2) tlo = min(tlo, ob2), thi = max(thi, ob2 + oc2);
+   if (oc3) tlo = min(tlo, ob3), thi = max(thi, ob3 + oc3);
+   if (thi == 0) tlo = 0;
 
    uint32_t rh = 0;                       // chain records consumed
    uint32_t ih = 0;                       // inserts consumed
@@ -546,7 +559,10 @@ __device__ void run_port(const PipeArgs& a, const Lay& L, uint32_t c, uint32_t i
          uint32_t rank = 0;
          if (ni)
          {
-            const R4 I = lane < ni ? ib[(ih + lane) & imask] : r4_inf();
+            // rank = chain candidates below the insert: three levels of a k-ary search
+            // (strides 64, 8, 1; the pivots of a level are read together, so the search
+            // costs three LDS round trips)
+            const R4 I = ib[(ih + lane) & imask];   // (lanes >= ni: not used)
             const uint64_t ik = key64(I);
 #pragma unroll
             for (uint32_t step = BLK; step; step >>= 1)
@@ -600,21 +616,31 @@ __device__ void run_port(const PipeArgs& a, const Lay& L, uint32_t c, uint32_t i
       // the bitmap's word prefix counts, then each record from its ring
       R4 x[KB];
       {
-         const uint32_t* const bm = cnt + C_SCR + SCR_W * w;
+         // the 8 bitmap words in every lane (two broadcast reads), lane L's word (L / 8)
+         // and the inserts in the words before it
+         constexpr uint32_t NW = BLK / 32;                   // bitmap words
+         const uint4* const bm4 = reinterpret_cast<const uint4*>(cnt + C_SCR + SCR_W * w);
+         uint32_t bw[NW];
+#pragma unroll
+         for (uint32_t d = 0; d < NW / 4; d++)
+         {
+            const uint4 v = bm4[d];
+            bw[4 * d] = v.x;
+            bw[4 * d + 1] = v.y;
+            bw[4 * d + 2] = v.z;
+            bw[4 * d + 3] = v.w;
+         }
          const uint32_t pb = K * lane;                       // first position of this lane
          const uint32_t wi = pb >> 5, bo = pb & 31u;
-         const uint32_t mwd = bm[wi];
-         const uint32_t wc = lane < BLK / 32 ? __builtin_popcount(bm[lane]) : 0u;
-         // exclusive prefix of the word counts (lanes 0 .. BLK/32 - 1), then lane L's word's
-         uint32_t pc = wc;
+         uint32_t mwd = 0, pc = 0, run = 0;
 #pragma unroll
-         for (uint32_t d = 1; d < BLK / 32; d <<= 1)
+         for (uint32_t d = 0; d < NW; d++)
          {
-            const uint32_t v = ch::bperm(pc, lane - d);
-            pc += lane >= d ? v : 0u;
+            mwd = wi == d ? bw[d] : mwd;
+            pc = wi == d ? run : pc;
+            run += __builtin_popcount(bw[d]);
          }
-         pc -= wc;
-         uint32_t before = ch::bperm(pc, wi) + __builtin_popcount(mwd & ((1u << bo) - 1u));
+         uint32_t before = pc + __builtin_popcount(mwd & ((1u << bo) - 1u));
 #pragma unroll
          for (uint32_t j = 0; j < KB; j++)
          {
@@ -741,69 +767,48 @@ __device__ void run_port(const PipeArgs& a, const Lay& L, uint32_t c, uint32_t i
          if (why) break;
          if (TIMING) tw_room += __builtin_amdgcn_s_memtime() - tr0;
       }
-      const __amdgpu_buffer_rsrc_t r0 = slot_rsrc(a, ob0, oc0);
       const __amdgpu_buffer_rsrc_t r1 = slot_rsrc(a, ob1, out_hbm ? oc1 : 0u);
-      const __amdgpu_buffer_rsrc_t r2 = slot_rsrc(a, ob2, oc2);
-      const __amdgpu_buffer_rsrc_t r3 = slot_rsrc(a, ob3, oc3);
-      const __amdgpu_buffer_rsrc_t rst = rsrc_of(a.samp_t, a.nsamp * 8u);
-      const __amdgpu_buffer_rsrc_t rsi = rsrc_of(a.samp_id, a.nsamp * 4u);
+      const __amdgpu_buffer_rsrc_t rT = slot_rsrc(a, tlo, thi - tlo);   // the turn slots (one range)
+      // each turn field's next position, relative to tlo
+      const uint32_t rb0 = ob0 - tlo + cnt0, rb2 = ob2 - tlo + cnt2, rb3 = ob3 - tlo + cnt3;
+      // branch-free per record: a lane with nothing to write for a target writes the
+      // trash entry (LDS) or an out-of-range offset (buffer stores drop it)
 #pragma unroll
       for (uint32_t j = 0; j < KB; j++)
       {
-         if (!vd[j]) continue;
          const uint32_t f = fd[j];
-         uint32_t pos;
-         if (f < 2u)
+         const bool lo = f < 2u;
+         const uint32_t sh = (f & 1u) * 16u;
+         const uint32_t pos = ((lo ? p01 : p23) >> sh) & 0xFFFFu;
+         const uint32_t inc = vd[j] ? 1u << sh : 0u;
+         p01 += lo ? inc : 0u;
+         p23 += lo ? 0u : inc;
+         const bool isc = vd[j] && f == 1u, ist = vd[j] && f != 1u;
+         // continuing: the next port's ring (or the next segment's link slot)
+         R4 o;
+         o.klo = (tcn[j] << 10) | (x[j].klo & 1023u);
+         o.khi = tcn[j] >> 22;
+         o.id = x[j].id;
+         o.aux = x[j].aux;
+         if (out_lds) *(isc ? ring_out + ((cnt1 + pos) & rmask) : trash) = o;
+         else if (out_hbm)
          {
-            pos = (p01 >> (16u * f)) & 0xFFFFu;
-            p01 += 1u << (16u * f);
+            v4u l;
+            l.x = o.klo;
+            l.y = o.khi | (a.tag << 16);
+            l.z = o.id;
+            l.w = o.aux;
+            __builtin_amdgcn_raw_buffer_store_b128(l, r1, isc ? (cnt1 + pos) * 16u : OOB, 0, AUX_SC1);
          }
-         else
-         {
-            pos = (p23 >> (16u * (f - 2u))) & 0xFFFFu;
-            p23 += 1u << (16u * (f - 2u));
-         }
-         if (f == 1u)
-         {
-            R4 o;
-            o.klo = (tcn[j] << 10) | (x[j].klo & 1023u);
-            o.khi = tcn[j] >> 22;
-            o.id = x[j].id;
-            o.aux = x[j].aux;
-            if (out_lds) ring_out[(cnt1 + pos) & rmask] = o;
-            else if (out_hbm)
-            {
-               v4u l;
-               l.x = o.klo;
-               l.y = o.khi | (a.tag << 16);
-               l.z = o.id;
-               l.w = o.aux;
-               __builtin_amdgcn_raw_buffer_store_b128(l, r1, (cnt1 + pos) * 16u, 0, AUX_SC1);
-            }
-         }
-         else
-         {
-            // a turn: the next ports' slots, HBM records {t', id, aux} (t' = 1000 tc' - rho)
-            const uint64_t tn = (uint64_t) tcn[j] * 1000ull + (uint64_t) (x[j].klo & 1023u) - 1023ull;
-            v4u hv;
-            hv.x = (uint32_t) tn;
-            hv.y = (uint32_t) (tn >> 32);
-            hv.z = x[j].id;
-            hv.w = x[j].aux;
-            const uint32_t gpos = (f == 0u ? cnt0 : f == 2u ? cnt2 : cnt3) + pos;
-            if (f == 0u) __builtin_amdgcn_raw_buffer_store_b128(hv, r0, gpos * 16u, 0, 0);
-            else if (f == 2u) __builtin_amdgcn_raw_buffer_store_b128(hv, r2, gpos * 16u, 0, 0);
-            else __builtin_amdgcn_raw_buffer_store_b128(hv, r3, gpos * 16u, 0, 0);
-            const uint32_t gp = (f == 0u ? ob0 : f == 2u ? ob2 : ob3) + gpos;
-            if ((gp & 63u) == 0)
-            {
-               v2u tv;
-               tv.x = (uint32_t) tn;
-               tv.y = (uint32_t) (tn >> 32);
-               __builtin_amdgcn_raw_buffer_store_b64(tv, rst, (gp >> 6) * 8u, 0, 0);
-               __builtin_amdgcn_raw_buffer_store_b32(x[j].id, rsi, (gp >> 6) * 4u, 0, 0);
-            }
-         }
+         // turning: the next ports' slots, HBM records {t', id, aux} (t' = 1000 tc' - rho)
+         const uint64_t tn = (uint64_t) tcn[j] * 1000ull + (uint64_t) (x[j].klo & 1023u) - 1023ull;
+         v4u hv;
+         hv.x = (uint32_t) tn;
+         hv.y = (uint32_t) (tn >> 32);
+         hv.z = x[j].id;
+         hv.w = x[j].aux;
+         const uint32_t gp = (f == 0u ? rb0 : f == 2u ? rb2 : rb3) + pos;   // relative to tlo
+         __builtin_amdgcn_raw_buffer_store_b128(hv, rT, ist ? gp * 16u : OOB, 0, 0);
       }
       if (nc && out_lds)
       {
@@ -869,6 +874,26 @@ __device__ void run_port(const PipeArgs& a, const Lay& L, uint32_t c, uint32_t i
       d[24] = (uint32_t) (t_b >> 8);
       d[25] = (uint32_t) (t_c >> 8);
       d[26] = (uint32_t) (t_d >> 8);
+   }
+}
+
+// The key samples (every 64th record's key, level.hip) of the SELF slots, which the
+// SELF level after the pipelines searches; the pipelines' own streams need none.
+// One workgroup per (tile, input side) slot.
+__global__ __launch_bounds__(256) void k_pipe_samples(uint32_t N, const uint32_t* __restrict__ slot_cnt,
+                                                      const uint64_t* __restrict__ slot_base, const Rec* __restrict__ recs,
+                                                      uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id)
+{
+   const uint32_t tile = blockIdx.x / INS, side = blockIdx.x % INS;
+   if (tile >= N) return;
+   const uint32_t sl = slot_of(tile, P_SELF, side);
+   const uint64_t b = slot_base[sl];
+   const uint32_t n = slot_cnt[sl];
+   for (uint32_t q = threadIdx.x; q * 64u < n; q += blockDim.x)
+   {
+      const uint64_t r = b + (uint64_t) q * 64u;   // (slots start 64-record aligned)
+      samp_t[r >> 6] = recs[r].t;
+      samp_id[r >> 6] = recs[r].id;
    }
 }
 

@@ -15,7 +15,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GNOC_LIB", os.path.join(_HERE, "_build", "libgnoc.so"))
-ABI_VERSION = 3   # include/gnoc.h GNOC_ABI_VERSION
+ABI_VERSION = 4   # include/gnoc.h GNOC_ABI_VERSION (4: the packed format, gnoc_fetch_latency)
 
 GNOC_OK = 0
 GNOC_EINVAL = -1
@@ -180,7 +180,7 @@ def load() -> ctypes.CDLL:
         ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_uint64, ctypes.c_uint32,
         ctypes.c_uint64, ctypes.c_double, ctypes.c_int32, vp, vp, vp, vp, sz, ctypes.POINTER(sz)]
     lib.gnoc_abi_version.argtypes = []
-    # the summary layout (runs, retries_total, fallbacks_total, chain_protocol) is ABI 3's:
+    # the summary layout (runs, retries_total, fallbacks_total, chain_protocol) is ABI 3-4's:
     # an older library would leave the rerun totals the bench checks at zero
     if lib.gnoc_abi_version() != ABI_VERSION:
         raise RuntimeError(f"{LIB_PATH}: ABI {lib.gnoc_abi_version()}, this module speaks {ABI_VERSION}")

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GNOC_ABI_VERSION 3
+#define GNOC_ABI_VERSION 4   /* 4: gnoc_submit_packed, gnoc_submit_async_packed, gnoc_fetch_latency */
 
 /* error codes */
 #define GNOC_OK             0
@@ -202,7 +202,7 @@ typedef struct gnoc_summary
    uint32_t retries_total;
    uint32_t fallbacks_total;
    uint32_t abi_pad2;
-} gnoc_summary;   /* ABI 3 layout: a client checks gnoc_abi_version() == GNOC_ABI_VERSION first */
+} gnoc_summary;   /* ABI 3-4 layout: a client checks gnoc_abi_version() == GNOC_ABI_VERSION first */
 
 /* Replaces NetworkModel::createModel(..., NETWORK_EMESH_HOP_BY_HOP)
  * (network_model.cc:50-71) + the RouterModel/QueueModel::create calls of

@@ -28,7 +28,7 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_defaults():
     lib = gnoc.load()
-    assert lib.gnoc_abi_version() == 3 == gnoc.ABI_VERSION
+    assert lib.gnoc_abi_version() == 4 == gnoc.ABI_VERSION
     # the summary layout of ABI 3 (include/gnoc.h): 112 bytes, the cumulative counters last
     assert ctypes.sizeof(gnoc.GnocSummary) == 112
     assert gnoc.GnocSummary.runs.offset == 96 and gnoc.GnocSummary.abi_pad2.offset == 108

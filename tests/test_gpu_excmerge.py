@@ -42,7 +42,9 @@ def burst_trace(W, H, per_tile, tail, seed, max_cycle=4000):
 def test_cycle0_burst_mg1_exact_over_reruns(W, H, per_tile, seed):
     """Cycle-0 bursts from every tile: M/G/1 requests in injection AND mesh ports.
     Bit-exact against the oracle on three runs of the batch, whichever engine path
-    each run takes (printed; the path is asserted by the tests that pin one)."""
+    each run takes (printed).  The 16 x 16 case pins its path: after the first run
+    the batch runs on k_chain's MG instantiation (engine path 4, chain_protocol bit
+    10) with no rerun."""
     cfg = gnoc.EngineConfig(num_tiles=W * H, mesh_width=W, mesh_height=H)
     tr = burst_trace(W, H, per_tile, 4000, seed)
     ref = oracle.run(cfg, tr)
@@ -50,11 +52,15 @@ def test_cycle0_burst_mg1_exact_over_reruns(W, H, per_tile, seed):
     eng = gnoc.Engine(cfg)
     eng.submit(tr)
     paths = []
-    for _ in range(3):
+    for r in range(3):
         eng.run()
         got = eng.results()
         same(got, ref)
-        paths.append(got.summary["engine_path"])
+        s = got.summary
+        paths.append(s["engine_path"])
+        if W == 16 and r:
+            assert s["engine_path"] == 4 and s["chain_protocol"] & 0x400, s
+            assert s["retries"] == 0 and s["fallbacks"] == 0, s
     eng.close()
     print("engine paths", paths, "mg1 uses", int(ref.port_mg1.sum()))
 
@@ -175,3 +181,35 @@ def test_overflow_then_y_mg1_decline_is_exact(monkeypatch):
     same(eng.results(), ref)
     eng.close()
     print("summary", s)
+
+
+def test_refused_exception_slot_with_y_mg1_is_exact():
+    """an injection queue whose M/G/1 exception tail (2,600 records into
+    one RIGHT slot) is longer than k_exc_merge merges (XM = 2,048), together with
+    M/G/1 in Y ports (a column burst).  A decline after the MG instantiation's Y
+    chains clears only the SELF slots' exception counts; the refused slot's tail is
+    still served in order by the level engine.  Bit-exact on every run."""
+    W = 8
+    cfg = gnoc.EngineConfig(num_tiles=W * W)
+    rng = np.random.default_rng(77)
+    big = 4 * W + 1
+    t_big = np.zeros(2600, np.uint64)
+    col = column_burst_trace(W, W, 3, 2, 20, seed=78, tail=4000)
+    t = np.concatenate([t_big, col.inject_ps])
+    src = np.concatenate([np.full(2600, big, np.uint32), col.src])
+    dst = np.concatenate([np.full(2600, 4 * W + 6, np.uint32), col.dst])
+    order = np.argsort(t, kind="stable")
+    tr = gnoc.Trace(t[order], src[order], dst[order], np.full(t.size, 576, np.uint32), np.zeros(t.size, np.uint32))
+    ref = oracle.run(cfg, tr)
+    mg = ref.port_mg1.reshape(-1, 6)
+    assert mg[big, 5] > 2048 and mg[:, [3, 4]].sum() > 0
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    paths = []
+    for _ in range(3):
+        eng.run()
+        got = eng.results()
+        same(got, ref)
+        paths.append(int(got.summary["engine_path"]))
+    eng.close()
+    print("engine paths", paths)

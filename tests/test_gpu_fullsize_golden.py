@@ -79,12 +79,15 @@ def test_configs1_full_size_mg1_burst_matches_oracle(lookback, monkeypatch):
     eng = gnoc.Engine(gnoc.EngineConfig(num_tiles=1024))
     eng.submit(tr)
     paths = []
-    for _ in range(3):
+    for r in range(3):
         eng.run()
         s = eng.summary()
         paths.append(int(s["engine_path"]))
         assert s["mg1_uses"] == GOLD[name]["mg1_uses"], (s["mg1_uses"], GOLD[name]["mg1_uses"])
         _check(name, eng.results())
+        if r:   # later runs go straight to k_chain's MG instantiation (bit 10)
+            assert s["engine_path"] == 4 and s["chain_protocol"] & 0x400, s
+            assert s["retries"] == 0 and s["fallbacks"] == 0, s
     eng.close()
     print("engine paths", paths)
 

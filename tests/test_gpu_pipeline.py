@@ -231,8 +231,9 @@ def test_packed_decode_block_edges(n, esc_every):
 
 def test_packed_escape_count_is_checked():
     """A delta-format batch whose 0xFFFF escapes do not match the absolute times it
-    gives (n_abs) is refused by the submit's checks (synchronous and staged), instead
-    of decoding past the given times."""
+    gives (n_abs) is refused by the submit's checks (synchronous and staged).  The
+    decoder never reads past the n_abs given times (an escape beyond them decodes
+    as 0, engine.hip pk_abs); k_pk_check's count mismatch is what refuses the batch."""
     cfg = gnoc.EngineConfig(num_tiles=64)
     t = (np.arange(3000, dtype=np.uint64) * np.uint64(40_000))   # every difference escapes
     rng = np.random.default_rng(5)
@@ -253,4 +254,32 @@ def test_packed_escape_count_is_checked():
         eng.submit_commit()
     eng.submit_packed(pt)          # a correct one still goes through
     eng.run()
+    eng.close()
+
+
+@pytest.mark.parametrize("nesc", [1, 700, 5000])
+def test_packed_escapes_without_absolute_times_are_refused(nesc):
+    """n_abs = 0 with escapes spread over many decode blocks (2,048
+    packets each).  Every escape ordinal is past the (empty) absolute-time array:
+    the decode stays in bounds and the submit is refused, synchronous and staged,
+    and the engine takes the next good batch."""
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    n = 20000
+    rng = np.random.default_rng(nesc)
+    t = np.sort(rng.integers(0, 40_000_000, n)).astype(np.uint64)
+    tr = gnoc.Trace(t, rng.integers(0, 64, n).astype(np.uint32), rng.integers(0, 64, n).astype(np.uint32),
+                    np.full(n, 576, np.uint32), np.zeros(n, np.uint32))
+    pt = gnoc.PackedTrace.of(tr)
+    dt = pt.dt.copy()
+    dt[rng.choice(n, nesc, replace=False)] = gnoc.PackedTrace.ESC
+    bad = gnoc.PackedTrace(pt.t0, dt, np.zeros(0, np.uint64), pt.src, pt.dst, pt.bits, pt.bits_all, pt.flags)
+    eng = gnoc.Engine(cfg)
+    with pytest.raises(gnoc.GnocError, match="escapes"):
+        eng.submit_packed(bad)
+    eng.submit_async_packed(bad)
+    with pytest.raises(gnoc.GnocError, match="escapes"):
+        eng.submit_commit()
+    eng.submit_packed(pt)
+    eng.run()
+    np.testing.assert_array_equal(eng.results().final_ps, oracle.run(cfg, tr).final_ps)
     eng.close()
