@@ -946,6 +946,20 @@ __device__ bool y_bounds(const ChainArgs& a, uint32_t c, uint32_t w, uint64_t D,
    } while (0)
 #endif
 
+// Wave priority over a step: raised from the step's start until its state is
+// published (the part a successor window waits on), default for the outputs.
+// configs[1]: 3.11 -> 3.01 ms per run at priority 2 (CH_PRIO=0: off).
+#ifndef CH_PRIO
+#define CH_PRIO 2
+#endif
+#if CH_PRIO
+#define CH_PRIO_HI() __builtin_amdgcn_s_setprio(CH_PRIO)
+#define CH_PRIO_LO() __builtin_amdgcn_s_setprio(0)
+#else
+#define CH_PRIO_HI() do {} while (0)
+#define CH_PRIO_LO() do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // one task, serial protocol: every window waits for window w-1's state of the
 // port (published as early as possible); the state block holds SW_SER granules
@@ -1058,6 +1072,7 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
       uint64_t* const stw = a.st + st_off + ((uint64_t) i * nW + w) * SW;          // this window's state
       const uint64_t* const stp = w ? stw - SW : nullptr;                           // predecessor's
       CH_STAMP(0);
+      CH_PRIO_HI();
       uint64_t pv = 0;
       if (w && lane < (uint32_t) SW_SER) pv = ld1(stp + lane);
       const uint32_t nx = rdl(pd0, PD_NX), ny = rdl(pd0, PD_NY);
@@ -1225,6 +1240,7 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
          st1(stw + lane, a.etag | state_word_ser(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u, Kout, Pend));
       }
 
+      CH_PRIO_LO();
       // ---- [E] recurrence and outputs, row by row: kept records in place into the kept list
       const uint32_t rl = rdl(pd0, PD_RL);
       // field tables (lane 1 + q): output slot base, capacity, records routed so far
@@ -1487,6 +1503,7 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
       const bool has_next = i + 1 < len;
       uint64_t* const stw = a.st + st_off + ((uint64_t) i * nW + w) * SW;          // this window's state
       CH_STAMP(0);
+      CH_PRIO_HI();
       // prefetch for the look-back: lanes [0, SW) the state of (w-1, i), [SW, 2 SW) of (w-2, i),
       // lane LB_POST the POST granule of (w-1, i-1) (the kept count that gives this port's spill range)
       uint64_t pv = 0;
@@ -1799,6 +1816,7 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
       }
       CH_STAMP(5);
 
+      CH_PRIO_LO();
       // ---- [E] recurrence and outputs, row by row: kept records in place into the kept list
       const uint32_t rl = rdl(pd0, PD_RL);
       // field tables (lane 1 + q): output slot base, capacity, records routed so far

@@ -160,6 +160,7 @@ struct gnoc_engine
    bool staged_val = false;                 // the staged batch was validated on the upload stream
    // a delta-format batch (stage_packed): its decoded escape count on the device and
    // the absolute times the caller gave, checked by the validation that follows
+   uint64_t layout_bound = 0;   // records the slot layout may span (run_prep)
    const uint64_t* val_esc = nullptr;
    uint64_t val_nabs = 0;
 
@@ -1925,12 +1926,21 @@ static uint64_t chunk_bound_of(const gnoc_engine* e, uint32_t P)
 }
 
 static int zq_flush(gnoc_engine* e, hipStream_t s);
-static int run_plan_v3(gnoc_engine* e)
+// ends_only: chunks for the injection and SELF levels only (the chain engine runs the
+// X and Y levels; a decline that reruns them on k_level plans again in full).
+static int run_plan_v3(gnoc_engine* e, bool ends_only = false)
 {
    const DevCfg& c = e->dc;
    hipStream_t s = e->stream;
    const uint32_t P = (uint32_t) e->lvl_ports.size();
    const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
+   uint32_t klo0 = 0, khi0 = P, klo1 = 0, khi1 = 0;
+   if (ends_only && L >= 2)
+   {
+      khi0 = e->lvl_off[1];
+      klo1 = e->lvl_off[L - 1];
+      khi1 = e->lvl_off[L];
+   }
    const uint64_t chunk_bound = chunk_bound_of(e, P);
    const uint32_t ctgt = chunk_target();
    GNOC_HIP(e, e->pio.ensure((size_t) P * sizeof(PortIO3)));
@@ -1945,7 +1955,7 @@ static int run_plan_v3(gnoc_engine* e)
    const uint32_t pg = (P + 255) / 256;
    GNOC_LAUNCH(e, KC_PLAN, k_plan_ports, dim3(pg), dim3(256), 0, s, c, P, e->d_lvl_ports.as<uint32_t>(),
                e->d_port_k.as<uint32_t>(), e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->pio.as<PortIO3>(), e->pnc.as<uint32_t>(),
-               ctgt);
+               ctgt, klo0, khi0, klo1, khi1);
    GNOC_LAUNCH(e, KC_PLAN, k_plan_guided, dim3(L), dim3(1024), 0, s, e->d_lvl_off.as<uint32_t>(), e->pnc.as<uint32_t>(),
                ctgt, (uint64_t) e->level_grid);
    GNOC_LAUNCH(e, KC_PLAN, k_plan_scan, dim3(1), dim3(1024), 0, s, P, L, e->d_lvl_off.as<uint32_t>(),
@@ -2462,6 +2472,11 @@ static int run_prep(gnoc_engine* e, bool* done)
    GNOC_HIP(e, e->counters.ensure(64));
    GNOC_HIP(e, e->gtot.ensure(16));
    GNOC_HIP(e, e->recs.ensure(e->rec_bound * sizeof(Rec)));
+   // the slot layout's bound (k_scan_slots empties the mesh slots past it);
+   // GNOC_TEST_LAYOUT_BOUND lowers it to exercise that guard
+   e->layout_bound = e->rec_bound;
+   if (const char* lb = std::getenv("GNOC_TEST_LAYOUT_BOUND"))
+      if (*lb) e->layout_bound = std::min<uint64_t>(e->rec_bound, std::strtoull(lb, nullptr, 10));
    // the port pipelines' segment links carry a 16-bit epoch tag (pipe.hip): the record
    // buffer is cleared when it is new (stale records of another engine could carry any
    // tag) and when the epoch wraps, before this run's scatter writes into it
@@ -2642,7 +2657,7 @@ static int run_prep(gnoc_engine* e, bool* done)
    }
    if (N * 25 <= 4 * SCAN_SPAN)
       GNOC_LAUNCH(e, KC_SCAN, k_scan_slots, dim3(1), dim3(1024), 0, s, N, e->slot_cnt.as<uint32_t>(),
-                  e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>(), e->gtot.as<uint64_t>() + 1);
+                  e->slot_base.as<uint64_t>(), e->gtot.as<uint64_t>(), e->gtot.as<uint64_t>() + 1, (uint64_t) e->layout_bound);
    else
    {
       const uint32_t nq = N * 25, nspan = (nq + SCAN_SPAN - 1) / SCAN_SPAN;
@@ -2652,7 +2667,8 @@ static int run_prep(gnoc_engine* e, bool* done)
       GNOC_LAUNCH(e, KC_SCAN, k_scan_span_offsets, dim3(1), dim3(1024), 0, s, nspan, e->span.as<uint64_t>(),
                   e->gtot.as<uint64_t>(), e->gtot.as<uint64_t>() + 1);
       GNOC_LAUNCH(e, KC_SCAN, k_scan_span_bases, dim3(nspan), dim3(256), 0, s, nq, e->slot_cnt.as<uint32_t>(),
-                  e->span.as<uint64_t>(), e->slot_base.as<uint64_t>());
+                  e->span.as<uint64_t>(), e->slot_base.as<uint64_t>(), (const uint64_t*) (e->gtot.as<uint64_t>() + 1),
+                  (uint64_t) e->layout_bound);
    }
    return GNOC_OK;
 }
@@ -2726,7 +2742,7 @@ static int run_post_check(gnoc_engine* e, bool closed_form)
       return GNOC_OK;
    }
    e->h_records = e->h_counters[0] + e->h_counters[1] + e->h_pinned[2];
-   if (e->h_pinned[3] > e->rec_bound) return fail(e, GNOC_EHIP, "internal: slot layout exceeds the record bound");
+   if (e->h_pinned[3] > e->layout_bound) return fail(e, GNOC_EHIP, "internal: slot layout exceeds the record bound");
    const unsigned* ef = (const unsigned*) (e->h_pinned + 8);
    const unsigned errf = ef[0];
    const unsigned cf = ef[4] | ef[5];   // the X phase's and the Y phase's chain flags
@@ -2843,7 +2859,7 @@ static int run_once(gnoc_engine* e)
       const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
       e->used_pipe = 1;
       e->used_v3 = 6;
-      rc = run_plan_v3(e);
+      rc = run_plan_v3(e, true);
       if (!rc) rc = pipe_setup(e);
       if (!rc) rc = run_levels_v3(e, 0, 1);
       if (!rc && e->exc_fix) rc = exc_merge(e);
@@ -2861,7 +2877,7 @@ static int run_once(gnoc_engine* e)
       const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
       e->used_chain = 1;
       e->used_v3 = 4;
-      rc = run_plan_v3(e);
+      rc = run_plan_v3(e, !e->ch_ydeclined);   // (Y on k_level: its levels too)
       if (!rc) rc = chain_setup(e);
       if (!rc) rc = run_levels_v3(e, 0, 1);
       if (!rc && e->exc_fix) rc = exc_merge(e);
@@ -2922,7 +2938,8 @@ static int y_levels_rerun(gnoc_engine* e)
                e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>());
    e->used_chain = 0;
    e->used_v3 = 5;
-   int rc = run_levels_v3(e, e->lvl_y0, (uint32_t) e->lvl_off.size() - 1);
+   int rc = run_plan_v3(e);   // the Y levels' chunks (the chains' plan covered INJ and SELF only)
+   if (!rc) rc = run_levels_v3(e, e->lvl_y0, (uint32_t) e->lvl_off.size() - 1);
    if (!rc) rc = run_post(e, false);
    return rc;
 }

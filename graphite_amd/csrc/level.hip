@@ -1585,10 +1585,14 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
                                                     const uint32_t* __restrict__ port_k,
                                                     const uint32_t* __restrict__ slot_cnt,
                                                     const uint64_t* __restrict__ slot_base, PortIO3* __restrict__ pio,
-                                                    uint32_t* __restrict__ pnc, uint32_t ctgt)
+                                                    uint32_t* __restrict__ pnc, uint32_t ctgt, uint32_t klo0,
+                                                    uint32_t khi0, uint32_t klo1, uint32_t khi1)
 {
    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
    if (k >= P) return;
+   // ports outside [klo0, khi0) and [klo1, khi1) get no chunks (the chain engine runs
+   // only the injection and SELF levels on k_level)
+   const bool planned = (k >= klo0 && k < khi0) || (k >= klo1 && k < khi1);
    const uint32_t port = lvl_ports[k];
    PortIO3 io;
    const uint32_t tile = port / PORTS, dir = port % PORTS;
@@ -1646,7 +1650,7 @@ __global__ __launch_bounds__(256) void k_plan_ports(DevCfg c, uint32_t P, const 
    io.rl = (uint32_t) rl_of(c, tile);
    io.pad1 = io.pad2 = 0;
    pio[k] = io;
-   pnc[k] = tot;  // records of the port (k_plan_scan turns it into a chunk count)
+   pnc[k] = planned ? tot : 0u;  // records of the port (k_plan_scan turns it into a chunk count)
 }
 
 // One block per level.  Records -> chunk counts.  A level runs in rounds of the

@@ -942,9 +942,13 @@ __global__ __launch_bounds__(256) void k_bcast_slots(DevCfg c, uint32_t nb, cons
 // ---------------------------------------------------------------------------
 // 6. bases of the non-injection slots, after the injection region (single block)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_scan_slots(uint32_t N, const uint32_t* __restrict__ cnt,
+// A layout past the record buffer (bound: sized on the host from the trace checks)
+// cannot come from a consistent batch; should it happen, the mesh slots are emptied
+// (count and base 0) so no later kernel writes outside the buffer, and the host
+// refuses the run (gtot[1] > rec_bound).
+__global__ __launch_bounds__(1024) void k_scan_slots(uint32_t N, uint32_t* __restrict__ cnt,
                                                      uint64_t* __restrict__ base, const uint64_t* __restrict__ inj_total,
-                                                     uint64_t* __restrict__ total)
+                                                     uint64_t* __restrict__ total, uint64_t bound)
 {
    __shared__ uint64_t part[1024];
    // enumerate the 5 mesh directions x 5 inputs of every tile: q -> slot (tile*6 + dir)*5 + in, dir < 5
@@ -964,10 +968,13 @@ __global__ __launch_bounds__(1024) void k_scan_slots(uint32_t N, const uint32_t*
       __syncthreads();
    }
    uint64_t run = *inj_total + part[threadIdx.x] - s;
+   const bool over = *inj_total + part[1023] > bound;
    for (uint32_t q = lo; q < hi; q++)
    {
-      base[slot(q)] = run;
-      run += (cnt[slot(q)] + 63) & ~63u;
+      const uint32_t c = cnt[slot(q)];
+      base[slot(q)] = over ? 0ull : run;
+      if (over) cnt[slot(q)] = 0;
+      run += (c + 63) & ~63u;
    }
    if (threadIdx.x == 1023) *total = *inj_total + part[1023];
 }
@@ -1040,8 +1047,9 @@ __global__ __launch_bounds__(1024) void k_scan_span_offsets(uint32_t nspan, uint
    if (threadIdx.x == 1023) *total = *inj_total + part[1023];
 }
 
-__global__ __launch_bounds__(256) void k_scan_span_bases(uint32_t nq, const uint32_t* __restrict__ cnt,
-                                                         const uint64_t* __restrict__ span_off, uint64_t* __restrict__ base)
+__global__ __launch_bounds__(256) void k_scan_span_bases(uint32_t nq, uint32_t* __restrict__ cnt,
+                                                         const uint64_t* __restrict__ span_off, uint64_t* __restrict__ base,
+                                                         const uint64_t* __restrict__ total, uint64_t bound)
 {
    __shared__ uint64_t part[256];
    const uint32_t q0 = blockIdx.x * SCAN_SPAN, q1 = min(q0 + SCAN_SPAN, nq);
@@ -1059,10 +1067,13 @@ __global__ __launch_bounds__(256) void k_scan_span_bases(uint32_t nq, const uint
       __syncthreads();
    }
    uint64_t run = span_off[blockIdx.x] + part[threadIdx.x] - s;
+   const bool over = *total > bound;   // (k_scan_slots: the same guard)
    for (uint32_t q = lo; q < hi; q++)
    {
-      base[scan_slot_of(q)] = run;
-      run += (cnt[scan_slot_of(q)] + 63) & ~63u;
+      const uint32_t c = cnt[scan_slot_of(q)];
+      base[scan_slot_of(q)] = over ? 0ull : run;
+      if (over) cnt[scan_slot_of(q)] = 0;
+      run += (c + 63) & ~63u;
    }
 }
 

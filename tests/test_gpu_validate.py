@@ -85,3 +85,24 @@ def test_device_resident_trace_matches_host_submit():
     assert sa["windows"] == sb["windows"]
     for f in ("final_ps", "contention_ps", "port_sum_delay", "port_count", "port_flit", "port_last"):
         assert np.array_equal(getattr(ra, f), getattr(rb, f)), f
+
+
+@pytest.mark.parametrize("bound", ["1", "3000"])
+def test_slot_layout_past_the_record_bound_is_refused(bound, monkeypatch):
+    """The slot-layout guard (prep.hip k_scan_slots): a layout that would reach past
+    the record buffer (here: the bound lowered by GNOC_TEST_LAYOUT_BOUND, below the
+    mesh slots or below even the injection slots) empties the mesh slots, so no
+    later kernel writes outside the buffer, and the run is refused.  The engine
+    then runs the batch exactly with the bound restored."""
+    from oracle import oracle
+    cfg = gnoc.EngineConfig(num_tiles=64)
+    tr = gnoc.synthetic_trace(8, 8, 0.02, 300, seed=5)
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    monkeypatch.setenv("GNOC_TEST_LAYOUT_BOUND", bound)
+    with pytest.raises(gnoc.GnocError, match="record bound"):
+        eng.run()
+    monkeypatch.delenv("GNOC_TEST_LAYOUT_BOUND")
+    eng.run()
+    np.testing.assert_array_equal(eng.results().final_ps, oracle.run(cfg, tr).final_ps)
+    eng.close()
