@@ -643,27 +643,35 @@ __device__ __forceinline__ void mode_scan(const uint64_t (&rk)[ROWS], const uint
    sp2 = rdl64(wave_sum64(s2), 63);
 }
 
-// The window's records in order through serial_step, uniform across the wave (lane 0
-// stores).  FIFO-served records take the next FIFO position of their field as in the
-// row-parallel emit; an M/G/1-served one may leave FIFO order: kept, it joins the
-// kept list (sorted afterwards), turning, it goes to the exception tail of its output
-// slot (nexc; k_exc_merge puts the tails in order before the next phase, k_level reads
-// them), spilled, the step fails (it would break the spill ranges' order).  A kept
-// record after a spilled one fails too (the kept records must stay a prefix of the
-// window's continuing records).  mst: lanes 0-3 the M/G/1 sums in and out.
+// A window of a port whose history tree has had no gap yet, when the M/G/1 branch
+// fires in it (queue_model_history_tree.cc:58-64; serial_step is the one-request
+// restatement).  Row by row, the requests up to the next event are served FIFO in
+// parallel exactly as the common emit serves them: the tail before each lane is
+// the row's max-plus prefix from the carried tail X, and two ballots find the first
+// lane whose request fires the branch (X > t + p) or finds the queue idle (t > X).
+// An M/G/1-served request is served alone (every lane computes the same FP64
+// delay from the M/G/1 sums, queue_model_m_g_1.cc:17-46); it leaves X as it is and
+// may leave FIFO order: kept, it joins the kept list (sorted afterwards), turning,
+// it goes to the exception tail of its output slot (nexc; k_exc_merge puts the tails
+// in order before the next phase, k_level reads them), spilled, the step fails (it
+// would break the spill ranges' order).  The first idle request ends the no-gap
+// prefix for good (:79-86): the rest of the window is plain FIFO.  The M/G/1 sums
+// (every request updates them, :48-56) are exact integers: n, sum p, sum p^2, and
+// the newest departure.  mst: lanes 0-3 the M/G/1 sums in and out.
 struct MgOut
 {
    uint64_t ssum, X, maxdep;
    uint32_t nkeep, mode, mg1;
-   uint32_t bad;   // R_MGB_* reasons
-   bool rte, spilled;
+   uint32_t bad;    // R_MGB_* reasons
+   uint32_t kend;   // records served here (all of the window)
+   bool rte, spilled, kept_exc;
 };
-// (only in the MG instantiation of k_chain: its serial loop raises the register
-// allocation, and the common kernel should not pay for it)
+// (only in the MG instantiation of k_chain: the common kernel should not pay for it)
 template <bool F1>
 __device__ __forceinline__ MgOut mg_emit(Smem& sm, const ChainArgs& a, const uint64_t (&rk)[ROWS], const uint32_t (&ra)[ROWS],
                                          uint32_t n, uint32_t fpack, uint32_t wr, uint32_t d0, uint64_t wb, uint64_t wbase,
-                                         uint32_t wlen, uint32_t Xr, uint64_t& mst, uint32_t pd0, uint32_t P0n, uint32_t& run_t)
+                                         uint32_t wlen, uint32_t Xr, uint64_t& mst, uint32_t pd0, uint32_t P0n, uint32_t& run_t,
+                                         uint32_t obf_t, uint32_t ocf_t)
 {
    const double fq = a.c.f;
    const gptr<Rec> recs = (gptr<Rec>) a.recs;
@@ -677,87 +685,159 @@ __device__ __forceinline__ MgOut mg_emit(Smem& sm, const ChainArgs& a, const uin
    const uint32_t lane = threadIdx.x;
    const uint32_t nx = rdl(pd0, PD_NX), ny = rdl(pd0, PD_NY), rl = rdl(pd0, PD_RL), dir = rdl(pd0, 19);
    const uint32_t ntile = ny * a.c.W + nx, nside = in_side_after(dir);
-   uint32_t rf[4], ob[4], oc[4], osl[4];
-#pragma unroll
-   for (int f = 0; f < 4; f++)
-   {
-      rf[f] = rdl(run_t, 1 + f);
-      ob[f] = rdl(pd0, PD_OBASE + f);
-      oc[f] = rdl(pd0, PD_OCAP + f);
-      const uint32_t fd = f == 0 ? P_SELF : f == 1 ? dir : f == 2 ? P_UP : P_DOWN;
-      osl[f] = slot_of(ntile, fd, slot_side(fd, nside));
-   }
-   SerialState st;
-   st.X = wb + Xr;
-   st.g = 0;
-   st.mode = 1;
-   st.narr = rdl64(mst, 0);
-   st.s1 = (double) rdl64(mst, 1);
-   st.s2 = (double) rdl64(mst, 2);
-   st.newest = rdl64(mst, 3);
-   st.mg1 = 0;
+   uint64_t narr = rdl64(mst, 0), s1 = rdl64(mst, 1), s2 = rdl64(mst, 2), newest = rdl64(mst, 3);
+   uint32_t Xc = Xr;    // the tail, relative to wb
+   bool nogap = true;
    MgOut o{};
+   o.kend = n;
+   uint64_t ssum = 0, rte = 0, spm = 0, ssum_mg = 0;
+   uint32_t nkeep = 0, s = 0;   // s: the first request not served yet
    bool kept_exc = false;
 #pragma unroll
    for (int r = 0; r < ROWS; r++)
    {
       if ((uint32_t) r * T >= n) break;
-      const uint32_t m = min((uint32_t) T, n - (uint32_t) r * T);
-      for (uint32_t L = 0; L < m; L++)
+      const uint32_t p0 = (uint32_t) r * T, rowlen = min((uint32_t) T, n - p0);
+      const uint32_t off = (uint32_t) (rk[r] >> 32), id = (uint32_t) rk[r], ax = ra[r];
+      const uint32_t tc = cyc(off), p = aux_F(ax), f = (fpack >> (2 * r)) & 3u;
+      while (s < p0 + rowlen)
       {
-         const uint64_t key = rdl64(rk[r], (int) L);
-         const uint32_t ax = rdl(ra[r], (int) L);
-         const uint32_t off = (uint32_t) (key >> 32), id = (uint32_t) key;
-         const uint32_t f = (rdl(fpack, (int) L) >> (2 * r)) & 3u;
-         const uint64_t tca = wb + cyc(off);
-         const uint64_t F = aux_F(ax);
-         const uint64_t mg0 = st.mg1;
-         const uint64_t d = serial_step(st, tca, F, (int) a.c.max_list, a.c.analytical);
-         const bool exc = st.mg1 != mg0;
-         o.ssum += d;
-         const uint64_t dep = tca + d + F;
-         o.maxdep = dep > o.maxdep ? dep : o.maxdep;
-         const uint64_t dn = (uint64_t) off + cps(d) + rl;   // t' - wbase
-         if (f == 1 && dn < wlen)
+         const uint32_t lo = s - p0;
+         const bool inseg = lane >= lo && lane < rowlen;
+         uint32_t A = inseg ? p : 0u, B = inseg ? tc + p : 0u;
+         wave_scan(A, B);
+         const uint32_t exA = dpp32<0x138, 0xF, 0xF>(A), exB = dpp32<0x138, 0xF, 0xF>(B);   // wave_shr 1
+         const uint32_t xa = Xc + exA;
+         const uint32_t Xb = xa > exB ? xa : exB;   // the tail ahead of this lane, lanes [lo, lane) served FIFO
+         uint32_t q = rowlen;
+         bool isgap = false;
+         if (nogap)
          {
-            if (o.spilled) o.bad |= R_MGB_KEPT;                // kept after a spill
+            const uint64_t gm = __ballot(inseg && tc > Xb), fm = __ballot(inseg && Xb > tc + p);
+            if (gm | fm)
+            {
+               q = (uint32_t) __builtin_ctzll(gm | fm);
+               isgap = (gm >> q) & 1ull;
+            }
+         }
+         // lanes [lo, q): FIFO-served, as the common emit serves them
+         const bool valid = lane >= lo && lane < q;
+         const uint32_t Xm = Xb > tc ? Xb : tc;
+         const uint32_t cc = valid ? Xm - tc : 0u;
+         if (q > lo) Xc = rdl(Xm + p, (int) (q - 1));
+         ssum += cc;
+         const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
+         const uint32_t one = valid ? 1u << (8 * f) : 0u;
+         const uint32_t inc = wave_sum32(one);
+         const uint32_t rank = ((inc - one) >> (8 * f)) & 0xFFu;
+         const uint32_t rtot = rdl(inc, 63);
+         const uint32_t gb = bperm(obf_t + run_t, 1u + f);
+         const uint32_t room = bperm(ocf_t - run_t, 1u + f);
+         const uint32_t kb = rdl(run_t, 2) - P0n;
+         run_t += field_cnt(rtot, lane);
+         const bool keep = valid && f == 1 && dn < wlen;
+         const bool out = valid && !keep;
+         const bool st = out && rank < room;
+         nkeep += (uint32_t) __popcll(__ballot(keep));
+         rte |= __ballot(out && rank >= room);
+         spm |= __ballot(st && f == 1);
+         if (keep)
+         {
+            sm.key[kb + rank] = (dn << 32) | id;
+            sm.aux[kb + rank] = ax;
+         }
+         if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
+         if (nogap && q > lo)
+         {
+            // the M/G/1 sums of the FIFO-served requests; FIFO departures rise, the last is X
+            narr += q - lo;
+            s1 += rdl(A, (int) (q - 1));
+            s2 += rdl(wave_sum32(valid ? p * p : 0u), 63);
+            newest = newest > wb + Xc ? newest : wb + Xc;
+         }
+         s = p0 + q;
+         if (q == rowlen) break;
+         if (isgap)
+         {
+            // request q finds the queue idle: the no-gap prefix ends here, q on are FIFO
+            nogap = false;
+            continue;
+         }
+         // request q: M/G/1-served, the tail untouched
+         const uint32_t tq = rdl(tc, (int) q), pq = rdl(p, (int) q), oq = rdl(off, (int) q), iq = rdl(id, (int) q);
+         const uint32_t aq = rdl(ax, (int) q), fq1 = rdl(f, (int) q);
+         SerialState ms;
+         ms.X = wb + Xc;
+         ms.g = 0;
+         ms.mode = 1;
+         ms.s1 = (double) s1;
+         ms.s2 = (double) s2;
+         ms.narr = narr;
+         ms.newest = newest;
+         ms.mg1 = 0;
+         const uint64_t d = mg1_delay(ms);
+         o.mg1++;
+         narr += 1;
+         s1 += pq;
+         s2 += (uint64_t) pq * pq;
+         const uint64_t dep = wb + tq + d + pq;
+         newest = newest > dep ? newest : dep;
+         o.maxdep = dep > o.maxdep ? dep : o.maxdep;
+         ssum_mg += d;
+         const uint64_t dq = (uint64_t) oq + cps(d) + rl;
+         if (fq1 == 1 && dq < wlen)
+         {
+            if (spm) o.bad |= R_MGB_KEPT;   // kept after a spill
+            const uint32_t kq = rdl(run_t, 2) - P0n;
             if (lane == 0)
             {
-               sm.key[rf[1] - P0n] = (dn << 32) | id;
-               sm.aux[rf[1] - P0n] = ax;
+               sm.key[kq] = (dq << 32) | iq;
+               sm.aux[kq] = aq;
             }
-            rf[1]++;
-            o.nkeep++;
-            kept_exc |= exc;
+            run_t += lane == 2 ? 1u : 0u;
+            nkeep++;
+            kept_exc = true;
          }
-         else if (f == 1 || !exc)
-         {
-            if (f == 1 && exc) o.bad |= R_MGB_SPILL;          // an M/G/1-served spill
-            if (rf[f] >= oc[f]) o.rte = true;
-            else if (lane == 0) out_record(recs, samp_t, samp_id, (uint64_t) ob[f] + rf[f], wbase + dn, id, ax, f == 1);
-            o.spilled |= f == 1;
-            rf[f]++;
-         }
+         else if (fq1 == 1)
+            o.bad |= R_MGB_SPILL;   // an M/G/1-served spill
          else if (lane == 0)
          {
             // M/G/1-served turn: the exception tail of its output slot (level.hip does the same)
-            const uint32_t x = atomicAdd(a.nexc + osl[f], 1u);
+            const uint32_t fd = fq1 == 0 ? P_SELF : fq1 == 2 ? P_UP : P_DOWN;
+            const uint32_t osl = slot_of(ntile, fd, slot_side(fd, nside));
+            const uint32_t ob = rdl(pd0, PD_OBASE + fq1), oc = rdl(pd0, PD_OCAP + fq1);
+            const uint32_t x = atomicAdd(a.nexc + osl, 1u);
             atomicOr(a.errflag + 2, 1u);
-            if (x >= oc[f]) atomicOr(a.errflag, 1u);
+            if (x >= oc) atomicOr(a.errflag, 1u);
             else
             {
-               const gptr<uint64_t> q = (gptr<uint64_t>) (recs + (uint64_t) ob[f] + oc[f] - 1 - x);
-               __hip_atomic_store(q, wbase + dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-               __hip_atomic_store(q + 1, (uint64_t) id | ((uint64_t) ax << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+               const gptr<uint64_t> qq = (gptr<uint64_t>) (recs + (uint64_t) ob + oc - 1 - x);
+               __hip_atomic_store(qq, wbase + dq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+               __hip_atomic_store(qq + 1, (uint64_t) iq | ((uint64_t) aq << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
          }
+         s = p0 + q + 1;
       }
    }
    wsync();
-   if (kept_exc && lane == 0)
-   {
-      // the kept list into (t, id) order: nearly sorted (insertion sort)
-      for (uint32_t i = 1; i < o.nkeep; i++)
+   o.ssum = rdl64(wave_sum64(ssum), 63) + ssum_mg;
+   o.X = wb + Xc;
+   o.mode = nogap ? 1u : 0u;
+   o.nkeep = nkeep;
+   o.rte = rte != 0;
+   o.spilled = spm != 0;
+   o.kept_exc = kept_exc;
+   mst = lane == 0 ? narr : lane == 1 ? s1 : lane == 2 ? s2 : lane == 3 ? newest : 0ull;
+   if (newest > M48 || s2 > M48 || narr > M48) o.bad |= R_MGB_OVF;
+   return o;
+}
+
+// The kept list into (t, id) order after M/G/1-served records joined it: nearly
+// sorted (insertion sort, lane 0).
+__device__ __forceinline__ void kept_sort(Smem& sm, uint32_t nkeep)
+{
+   if (threadIdx.x == 0)
+      for (uint32_t i = 1; i < nkeep; i++)
       {
          const uint64_t k = sm.key[i];
          const uint32_t v = sm.aux[i];
@@ -771,16 +851,7 @@ __device__ __forceinline__ MgOut mg_emit(Smem& sm, const ChainArgs& a, const uin
          sm.key[j] = k;
          sm.aux[j] = v;
       }
-   }
    wsync();
-   run_t = lane == 1 ? rf[0] : lane == 2 ? rf[1] : lane == 3 ? rf[2] : lane == 4 ? rf[3] : 0u;
-   o.X = st.X;
-   o.mode = st.g == 0 ? 1u : 0u;
-   o.mg1 = (uint32_t) st.mg1;
-   const uint64_t s1 = (uint64_t) st.s1, s2 = (uint64_t) st.s2;
-   mst = lane == 0 ? st.narr : lane == 1 ? s1 : lane == 2 ? s2 : lane == 3 ? st.newest : 0ull;
-   if (st.newest > M48 || s2 > M48 || st.narr > M48) o.bad |= R_MGB_OVF;
-   return o;
 }
 
 // The M/G/1 sums after a window served FIFO with no gap (every request updates them,
@@ -1275,17 +1346,21 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
       {
          if (mg)
          {
-            mo = mg_emit<F1>(sm, a, rk, ra, n, fpack, wr, d0, wb, wbase, wlen, Xr, mst, pd0, P0n, run_t);
+            mo = mg_emit<F1>(sm, a, rk, ra, n, fpack, wr, d0, wb, wbase, wlen, Xr, mst, pd0, P0n, run_t, obf_t, ocf_t);
             nkeep = mo.nkeep;
+            Xc = (uint32_t) (mo.X - wb);   // (the rest of the window, if any, from here)
          }
       }
-      if (!mgr)
+      // records [k0, n): FIFO, row-parallel (all of them, or those after an M/G/1 prefix)
+      const uint32_t k0 = mgr ? mo.kend : 0u;
+      if (k0 < n)
 #pragma unroll
       for (int r = 0; r < ROWS; r++)
       {
          if ((uint32_t) r * T >= n) break;
          const uint32_t p0 = (uint32_t) r * T;
-         const bool valid = p0 + lane < n;
+         if (p0 + T <= k0) continue;
+         const bool valid = p0 + lane < n && p0 + lane >= k0;
          const uint32_t off = (uint32_t) (rk[r] >> 32);
          const uint32_t id = (uint32_t) rk[r];
          const uint32_t ax = ra[r];
@@ -1340,8 +1415,10 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
          if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
       }
       CH_STAMP(6);
-      const bool spilled = mgr ? mo.spilled : spm != 0;
-      if ((mgr ? mo.rte : rte != 0) && lane == 0) flag(a, F_ROUTE);
+      const bool spilled = (mgr && mo.spilled) || spm != 0;
+      if (((mgr && mo.rte) || rte != 0) && lane == 0) flag(a, F_ROUTE);
+      if (mgr && mo.kept_exc) kept_sort(sm, nkeep);
+      if (mgr && mo.spilled && nkeep > mo.nkeep) mo.bad |= R_MGB_KEPT;   // (FIFO after a spill cannot keep)
       if (mgr && mo.bad)
       {
          // an M/G/1-served spill (or a kept record after a spill): the level engine takes it
@@ -1350,13 +1427,13 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
       }
 
       if (spilled && lastw && lane == 0) flag(a, F_FALLBACK | R_LASTSPILL);   // the last window keeps everything
-      const uint64_t ssw = mgr ? mo.ssum : rdl64(wave_sum64(ssum), 63);
+      const uint64_t ssw = (mgr ? mo.ssum : 0ull) + rdl64(wave_sum64(ssum), 63);
       if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drained before the next publish
       wsync();
 
       // ---- [F] late publish (no gap yet), port counters, route check
       const uint32_t x0 = Xr + totA;
-      const uint64_t Xo = mgr ? mo.X : wb + (x0 > totB ? x0 : totB);
+      const uint64_t Xo = mgr ? (k0 < n ? wb + Xc : mo.X) : wb + (x0 > totB ? x0 : totB);
       if (!published && mode)
       {
          // the state after the window: still no gap -> the M/G/1 sums go along
@@ -1851,17 +1928,21 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
       {
          if (mg)
          {
-            mo = mg_emit<F1>(sm, a, rk, ra, n, fpack, wr, d0, wb, wbase, wlen, Xr, mst, pd0, P0n, run_t);
+            mo = mg_emit<F1>(sm, a, rk, ra, n, fpack, wr, d0, wb, wbase, wlen, Xr, mst, pd0, P0n, run_t, obf_t, ocf_t);
             nkeep = mo.nkeep;
+            Xc = (uint32_t) (mo.X - wb);   // (the rest of the window, if any, from here)
          }
       }
-      if (!mgr)
+      // records [k0, n): FIFO, row-parallel (all of them, or those after an M/G/1 prefix)
+      const uint32_t k0 = mgr ? mo.kend : 0u;
+      if (k0 < n)
 #pragma unroll
       for (int r = 0; r < ROWS; r++)
       {
          if ((uint32_t) r * T >= n) break;
          const uint32_t p0 = (uint32_t) r * T;
-         const bool valid = p0 + lane < n;
+         if (p0 + T <= k0) continue;
+         const bool valid = p0 + lane < n && p0 + lane >= k0;
          const uint32_t off = (uint32_t) (rk[r] >> 32);
          const uint32_t id = (uint32_t) rk[r];
          const uint32_t ax = ra[r];
@@ -1913,8 +1994,10 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
          if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
       }
       CH_STAMP(6);
-      const bool spilled = mgr ? mo.spilled : spm != 0;
-      if ((mgr ? mo.rte : rte != 0) && lane == 0) flag(a, F_ROUTE);
+      const bool spilled = (mgr && mo.spilled) || spm != 0;
+      if (((mgr && mo.rte) || rte != 0) && lane == 0) flag(a, F_ROUTE);
+      if (mgr && mo.kept_exc) kept_sort(sm, nkeep);
+      if (mgr && mo.spilled && nkeep > mo.nkeep) mo.bad |= R_MGB_KEPT;   // (FIFO after a spill cannot keep)
       if (mgr && mo.bad)
       {
          // an M/G/1-served spill (or a kept record after a spill): the level engine takes it
@@ -1923,13 +2006,13 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
       }
 
       if (spilled && lastw && lane == 0) flag(a, F_FALLBACK | R_LASTSPILL);   // the last window keeps everything
-      const uint64_t ssw = mgr ? mo.ssum : rdl64(wave_sum64(ssum), 63);
+      const uint64_t ssw = (mgr ? mo.ssum : 0ull) + rdl64(wave_sum64(ssum), 63);
       if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // drained before the next publish
       wsync();
 
       // ---- [F] late INC (no gap yet), POST, port counters, route check
       const uint32_t x0 = Xr + totA;
-      const uint64_t Xo = mgr ? mo.X : wb + (x0 > totB ? x0 : totB);
+      const uint64_t Xo = mgr ? (k0 < n ? wb + Xc : mo.X) : wb + (x0 > totB ? x0 : totB);
       if (mode)
       {
          // the state after the window: still no gap -> the M/G/1 sums go along

@@ -26,7 +26,11 @@ def one(label):
     ms = (time.perf_counter() - t) / K * 1e3
     s = eng.summary()
     print(label, f"{ms:.3f} ms/run", {k: s[k] for k in ("engine_path", "chain_protocol", "mg1_uses", "retries",
-                                                         "fallbacks", "mesh_hops")}, flush=True)
+                                                         "fallbacks", "mesh_hops", "windows", "windows_y",
+                                                         "window_ps_x", "window_ps_y")}, flush=True)
+    eng.set_profiling(True)
+    eng.run()
+    print(label, "kernel_ms", {k: round(v[0], 4) for k, v in eng.kernel_stats().items()}, flush=True)
     eng.close()
 
 
