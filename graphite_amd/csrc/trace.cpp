@@ -270,3 +270,85 @@ extern "C" int gnoc_trace_file_read_q(const char* path, gnoc_config* cfg_out, gn
    std::fclose(f);
    return ok ? GNOC_OK : GNOC_ETRACE;
 }
+
+// The delta wire format's encoder (include/gnoc.h gnoc_pack_trace): blocks of the
+// trace on the host's threads; pass 1 validates and counts each block's escapes,
+// pass 2 writes, each block's escapes at its offset in abs_ps.
+extern "C" int gnoc_pack_trace(const gnoc_packets* pk, size_t n, uint16_t* dt, uint16_t* src, uint16_t* dst,
+                               uint16_t* bits, uint8_t* flags, uint64_t* abs_ps, size_t abs_cap, gnoc_pack_info* info)
+{
+   if (!pk || !info) return GNOC_EINVAL;
+   if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits || !dt || !src || !dst)) return GNOC_EINVAL;
+   const uint64_t* t = pk->inject_ps;
+   const uint64_t t0 = n ? t[0] : 0;
+   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+   const size_t nt = std::max<size_t>(1, std::min<size_t>({ (size_t) hw, (size_t) 16, n / 65536 + 1 }));
+   const size_t blk = (n + nt - 1) / std::max<size_t>(nt, 1);
+   struct Part
+   {
+      uint64_t esc = 0;
+      uint32_t fl = 0;
+      bool bad = false, one = true;
+   };
+   std::vector<Part> part(nt);
+   const uint32_t b0 = n ? pk->bits[0] : 0u;
+   auto count = [&](size_t k) {
+      Part& q = part[k];
+      const size_t lo = k * blk, hi = std::min(n, lo + blk);
+      for (size_t i = lo; i < hi; i++)
+      {
+         const uint64_t d = t[i] - (i ? t[i - 1] : t0);
+         q.esc += d >= 0xFFFFull;
+         const uint32_t f = pk->flags ? pk->flags[i] : 0u;
+         q.fl |= f;
+         q.one &= pk->bits[i] == b0;
+         q.bad |= pk->src[i] > 0xFFFFu || pk->dst[i] > 0xFFFFu || pk->bits[i] > 0xFFFFu || f > 0xFFu;
+      }
+   };
+   {
+      std::vector<std::thread> th;
+      for (size_t k = 1; k < nt; k++) th.emplace_back(count, k);
+      count(0);
+      for (auto& x : th) x.join();
+   }
+   uint64_t nesc = 0;
+   uint32_t fl = 0;
+   bool bad = false, one = true;
+   std::vector<uint64_t> eoff(nt);
+   for (size_t k = 0; k < nt; k++)
+   {
+      eoff[k] = nesc;
+      nesc += part[k].esc;
+      fl |= part[k].fl;
+      bad |= part[k].bad;
+      one &= part[k].one;
+   }
+   info->t0 = t0;
+   info->n_abs = nesc;
+   info->bits_all = one ? b0 : 0xFFFFFFFFu;
+   info->flags_any = fl;
+   if (bad || nesc > abs_cap || (nesc && !abs_ps) || (!one && !bits) || (fl && !flags)) return GNOC_EINVAL;
+   auto write = [&](size_t k) {
+      const size_t lo = k * blk, hi = std::min(n, lo + blk);
+      uint64_t e = eoff[k];
+      for (size_t i = lo; i < hi; i++)
+      {
+         const uint64_t d = t[i] - (i ? t[i - 1] : t0);
+         if (d >= 0xFFFFull)
+         {
+            dt[i] = 0xFFFFu;
+            abs_ps[e++] = t[i];
+         }
+         else dt[i] = (uint16_t) d;
+         src[i] = (uint16_t) pk->src[i];
+         dst[i] = (uint16_t) pk->dst[i];
+         if (bits) bits[i] = (uint16_t) pk->bits[i];
+         if (flags) flags[i] = (uint8_t) (pk->flags ? pk->flags[i] : 0u);
+      }
+   };
+   std::vector<std::thread> th;
+   for (size_t k = 1; k < nt; k++) th.emplace_back(write, k);
+   write(0);
+   for (auto& x : th) x.join();
+   return GNOC_OK;
+}

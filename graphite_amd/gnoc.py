@@ -47,6 +47,7 @@ EXPORTED = (
     "gnoc_build_id", "gnoc_rccl_unique_id", "gnoc_rccl_comm_init", "gnoc_rccl_comm_destroy",
     "gnoc_submit_async", "gnoc_submit_commit", "gnoc_fetch_final_ps", "gnoc_fetch_latency", "gnoc_fetch_wait",
     "gnoc_submit_narrow", "gnoc_submit_async_narrow", "gnoc_submit_packed", "gnoc_submit_async_packed",
+    "gnoc_pack_trace",
 )
 
 
@@ -101,6 +102,11 @@ class GnocPacketsPacked(ctypes.Structure):
         ("pad", ctypes.c_uint32),
         ("flags", ctypes.c_void_p),
     ]
+
+
+class GnocPackInfo(ctypes.Structure):
+    _fields_ = [("t0", ctypes.c_uint64), ("n_abs", ctypes.c_uint64), ("bits_all", ctypes.c_uint32),
+                ("flags_any", ctypes.c_uint32)]
 
 
 class GnocPacketsNarrow(ctypes.Structure):
@@ -214,6 +220,8 @@ def load() -> ctypes.CDLL:
     if hasattr(lib, "gnoc_submit_packed"):
         lib.gnoc_submit_packed.argtypes = [vp, ctypes.POINTER(GnocPacketsPacked), sz]
         lib.gnoc_submit_async_packed.argtypes = [vp, ctypes.POINTER(GnocPacketsPacked), sz]
+    lib.gnoc_pack_trace.argtypes = [ctypes.POINTER(GnocPackets), sz, vp, vp, vp, vp, vp, vp, sz,
+                                    ctypes.POINTER(GnocPackInfo)]
     if hasattr(lib, "gnoc_submit_async"):
         lib.gnoc_submit_async.argtypes = [vp, ctypes.POINTER(GnocPackets), sz]
         lib.gnoc_submit_commit.argtypes = [vp]
@@ -357,7 +365,49 @@ class PackedTrace:
     @staticmethod
     def of(tr: "Trace", alloc=np.empty) -> "PackedTrace":
         """Pack a trace (ValueError if a tile id, length or flag does not fit the
-        narrow fields); alloc(shape, dtype) places the arrays (e.g. page-locked)."""
+        narrow fields) with the library's encoder (gnoc_pack_trace, the host's
+        cores); alloc(shape, dtype) places the arrays (e.g. page-locked)."""
+        tr = tr.normalized()
+        lib = load()
+        n = len(tr)
+        dt, src, dst = alloc((n,), np.uint16), alloc((n,), np.uint16), alloc((n,), np.uint16)
+        bits, flags = np.empty(n, np.uint16), np.empty(n, np.uint8)
+        cap = n // 64 + 64
+        for _ in range(2):
+            absv = alloc((cap,), np.uint64)
+            info = GnocPackInfo()
+            pk = GnocPackets(tr.inject_ps.ctypes.data, tr.src.ctypes.data, tr.dst.ctypes.data, tr.bits.ctypes.data,
+                             tr.flags.ctypes.data)
+            rc = lib.gnoc_pack_trace(ctypes.byref(pk), n, dt.ctypes.data, src.ctypes.data, dst.ctypes.data,
+                                     bits.ctypes.data, flags.ctypes.data, absv.ctypes.data, cap, ctypes.byref(info))
+            if rc == 0 or info.n_abs <= cap:
+                break
+            cap = int(info.n_abs)
+        if rc:
+            raise ValueError("the trace does not fit the packed wire format")
+        one_len = info.bits_all != 0xFFFFFFFF
+        if one_len:
+            bits = None
+        else:
+            b = alloc((n,), np.uint16)
+            b[:] = bits
+            bits = b
+        if info.flags_any:
+            f = alloc((n,), np.uint8)
+            f[:] = flags
+            flags = f
+        else:
+            flags = None
+        na = int(info.n_abs)
+        if na < cap:
+            a2 = alloc((na,), np.uint64)
+            a2[:] = absv[:na]
+            absv = a2
+        return PackedTrace(int(info.t0), dt, absv, src, dst, bits, int(info.bits_all) if one_len and n else 0, flags)
+
+    @staticmethod
+    def of_numpy(tr: "Trace", alloc=np.empty) -> "PackedTrace":
+        """The same encoding in numpy (the reference the library's encoder is tested against)."""
         tr = tr.normalized()
         n = len(tr)
         for name, a, lim in (("src", tr.src, 1 << 16), ("dst", tr.dst, 1 << 16), ("bits", tr.bits, 1 << 16),

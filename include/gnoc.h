@@ -192,8 +192,10 @@ typedef struct gnoc_summary
                                    look-back protocol (else serial; look-back is kept only when it
                                    measured > 5% faster than serial on the batch's windows); bit 9
                                    set when both phases ran in one fused launch; bit 10 set when
-                                   the chains ran the no-gap M/G/1 prefix serially (the batch
-                                   meets the history tree's analytical branch in mesh ports) */
+                                   the chains served the no-gap M/G/1 prefix (the batch meets the
+                                   history tree's analytical branch in mesh ports); bit 11 set
+                                   when only the windows that can serve M/G/1 requests ran on
+                                   that instantiation (the rest on the common one) */
    uint64_t window_ps_x;        /* window length (ps) of the X phase                     */
    uint64_t window_ps_y;        /* ... of the Y phase                                    */
    /* since the last gnoc_submit: runs, and the retries / fallbacks of all of them
@@ -238,6 +240,25 @@ int gnoc_submit(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
 int gnoc_submit_device(gnoc_engine *eng, const gnoc_packets *pk, size_t n);
 int gnoc_submit_narrow(gnoc_engine *eng, const gnoc_packets_narrow *pk, size_t n);
 int gnoc_submit_packed(gnoc_engine *eng, const gnoc_packets_packed *pk, size_t n);
+
+/* The host side of the delta wire format: encode a trace as gnoc_submit would take it
+ * (the capture hook's layout) into the caller's arrays, one pass over the trace on
+ * the host's cores.  dt, src, dst: n entries; bits, flags: n entries each, or NULL
+ * (then every packet must have one length / no flags); abs_ps: room for abs_cap
+ * escapes.  info: t0, the escapes the trace needs (n_abs; GNOC_EINVAL, arrays
+ * unspecified, when above abs_cap: call again with room for n_abs), the length
+ * every packet has (bits_all; 0xFFFFFFFF when they differ: pass bits) and the OR
+ * of all flags.  GNOC_EINVAL when a tile id, length or flag does not fit the
+ * narrow fields.  No engine, no device. */
+typedef struct gnoc_pack_info
+{
+   uint64_t t0;
+   uint64_t n_abs;
+   uint32_t bits_all;
+   uint32_t flags_any;
+} gnoc_pack_info;
+int gnoc_pack_trace(const gnoc_packets *pk, size_t n, uint16_t *dt, uint16_t *src, uint16_t *dst, uint16_t *bits,
+                    uint8_t *flags, uint64_t *abs_ps, size_t abs_cap, gnoc_pack_info *info);
 
 /* Runs the whole batch (all hops of all packets) on the GPU.  Blocking. */
 int gnoc_run(gnoc_engine *eng);
