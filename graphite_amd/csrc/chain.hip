@@ -134,7 +134,8 @@ struct __attribute__((aligned(16))) ChainPort
    uint32_t nx, ny;      // [15-16] next tile
    uint32_t rl;          // [17]    R + Lk (ps)
    uint32_t tile, dir, cont, nl;   // [18-21] (k_win_bounds, debugging)
-   uint32_t pad0[10];
+   uint32_t oslot[4];    // [22-25] output slot index per field (their exception-tail counts, nexc)
+   uint32_t pad0[6];
 };
 static_assert(sizeof(ChainPort) == 128, "ChainPort is one 128-B line");
 
@@ -184,6 +185,8 @@ struct ChainArgs
    const uint64_t* xst;           // ... and hand-off state (the producer ports' cumulative route counts)
    uint32_t* nexc;                // exception-tail counts per slot (M/G/1-served turns, mg_emit)
    unsigned long long* port_mg1;  // per-port M/G/1 requests
+   unsigned* mgk;                 // [nch] 2 + the last window after which a port of the chain still had no gap
+   const uint32_t* mgk_lim;       // k_chain_mix: [nch] windows below it take the M/G/1 path
 };
 
 
@@ -325,7 +328,7 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t l)
 // it ran at its start (y_bounds: list 2 i + j - 1 packed lo | (hi - lo) << 24 in
 // lane L % 64 of bnd[L / 64]), the IN_LOCAL bounds from k_win_bounds.
 enum : int { PD_OBASE = 0, PD_OCAP = 4, PD_IBASE = 8, PD_ICNT = 11, PD_PORT = 14, PD_NX = 15, PD_NY = 16, PD_RL = 17,
-             PD_LO = 32 };
+             PD_OSLOT = 22, PD_LO = 32 };
 template <int NL, bool FU>
 __device__ __forceinline__ uint32_t load_pd(const ChainArgs& a, uint32_t cpi, uint64_t bt_off, uint32_t nW, uint32_t i,
                                             uint32_t w, uint32_t bnd0 = 0u, uint32_t bnd1 = 0u)
@@ -874,14 +877,9 @@ __device__ __forceinline__ bool route_filled(const ChainArgs& a, uint32_t pd0, u
    const uint32_t lane = threadIdx.x;
    bool bad = lane - 1u < 4u && run_t != ocf_t;
    if (!__any(bad)) return true;
-   const uint32_t nx = rdl(pd0, PD_NX), ny = rdl(pd0, PD_NY), dir = rdl(pd0, 19);
-   if (bad)
-   {
-      const uint32_t f = lane - 1u;
-      const uint32_t fd = f == 0 ? P_SELF : f == 1 ? dir : f == 2 ? P_UP : P_DOWN;
-      const uint32_t sl = slot_of(ny * a.c.W + nx, fd, slot_side(fd, in_side_after(dir)));
-      bad = f == 1 || run_t + __hip_atomic_load(a.nexc + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ocf_t;
-   }
+   // (a turn slot may end in an exception tail; the continuing slot never does)
+   const uint32_t sl = bperm(pd0, (uint32_t) PD_OSLOT - 1u + lane);
+   if (bad) bad = lane == 2 || run_t + __hip_atomic_load(a.nexc + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ocf_t;
    return !__any(bad);
 }
 
@@ -1069,8 +1067,8 @@ __device__ __forceinline__ uint64_t state_word_ser(uint32_t lane, uint64_t Xo, u
    if (lane == 7) v = Pend;
    return v;
 }
-template <int NL, bool F1, bool FU, bool MG = false>
-__device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk, uint32_t aux)
+template <int NL, bool F1, bool FU, bool MG = false, bool RF = false>
+__device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk, uint32_t aux)
 {
    constexpr bool XC = NL == 1;
    const uint32_t lane = threadIdx.x;
@@ -1442,12 +1440,14 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
          const uint32_t mout = mgr ? mo.mode : (fgap == NONE ? 1u : 0u);
          if (MG && mout) mst = mg_after(mst, mgr, n, totA, sp2, Xo);
          if (lane < (uint32_t) SW_SER) st1(stw + lane, a.etag | state_word_ser(lane, Xo, run_t, mout, Kout, Pend));
+         if (MG && mout && lane == 0) atomicMax(a.mgk + c, w + 2u);   // window w + 1 may still serve M/G/1
          if (MG && mout && lane < 4u) st1(stw + G_MG + lane, a.etag | mst);
       }
       // every record of the port has passed at the last window: the route counts (and
       // the exception tails) fill every output slot
-      // (only mg_emit writes exception tails of chain outputs)
-      if (lastw && (MG ? !route_filled(a, pd0, run_t, ocf_t) : __any(lane - 1u < 4u && run_t != ocf_t)) && lane == 0)
+      // (only mg_emit writes exception tails of chain outputs: RF, the common windows of
+      // a launch whose first windows take the M/G/1 path, count them too)
+      if (lastw && (MG || RF ? !route_filled(a, pd0, run_t, ocf_t) : __any(lane - 1u < 4u && run_t != ocf_t)) && lane == 0)
          flag(a, F_ROUTE);
       if (lane == 0 && n)
       {
@@ -1507,8 +1507,8 @@ __device__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, u
 // ---------------------------------------------------------------------------
 // one task, look-back protocol (AGG / INC / KO / POST granules)
 // ---------------------------------------------------------------------------
-template <int NL, bool F1, bool FU, bool MG = false>
-__device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk, uint32_t aux)
+template <int NL, bool F1, bool FU, bool MG = false, bool RF = false>
+__device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk, uint32_t aux)
 {
    constexpr bool XC = NL == 1;
    const uint32_t lane = threadIdx.x;
@@ -2022,14 +2022,16 @@ __device__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, ui
          if (MG && mout) mst = mg_after(mst, mgr, n, totA, sp2, Xo);
          if (MG && mout && lane < 4u) st1(stw + G_MG + lane, a.etag | mst);
          if (lane < (uint32_t) G_AB) st1(stw + lane, a.etag | inc_word(lane, Xo, run_t, mout));
+         if (MG && mout && lane == 0) atomicMax(a.mgk + c, w + 2u);   // window w + 1 may still serve M/G/1
       }
       // POST: the chain outputs before this window and whether it kept any (the next
       // window's spill range at the next port, without waiting for its KO)
       if (lane == G_POST) st1(stw + G_POST, a.etag | (uint64_t) P0n | (uint64_t) nkeep << 32);
       // every record of the port has passed at the last window: the route counts (and
       // the exception tails) fill every output slot
-      // (only mg_emit writes exception tails of chain outputs)
-      if (lastw && (MG ? !route_filled(a, pd0, run_t, ocf_t) : __any(lane - 1u < 4u && run_t != ocf_t)) && lane == 0)
+      // (only mg_emit writes exception tails of chain outputs: RF, the common windows of
+      // a launch whose first windows take the M/G/1 path, count them too)
+      if (lastw && (MG || RF ? !route_filled(a, pd0, run_t, ocf_t) : __any(lane - 1u < 4u && run_t != ocf_t)) && lane == 0)
          flag(a, F_ROUTE);
       if (lane == 0 && n)
       {
@@ -2113,6 +2115,42 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
    }
 }
 
+// An MG batch whose M/G/1 windows are known (mgk_lim[c]: chain c's windows below it
+// may serve M/G/1 requests): those tasks take the MG path, the others the common one
+// (with the route check that counts exception tails) -- in one launch, so the rest of
+// the phase does not wait for the M/G/1 windows' tasks to drain first.
+template <int NL, bool F1, bool LB>
+__global__ __launch_bounds__(T, CH_MINW) void k_chain_mix(ChainArgs a)
+{
+   __shared__ Smem sm;
+   const uint32_t ntasks = a.ntasks;
+   if (a.fw != 4 && (a.errflag[4] & F_ANY)) return;
+   if (a.errflag[2] != 0 && (!a.excfix || (a.errflag[2] & 2u)))
+   {
+      if (threadIdx.x == 0 && blockIdx.x == 0) flag(a, F_FALLBACK | R_EXC);
+      return;
+   }
+   for (;;)
+   {
+      uint32_t tk = 0;
+      if (threadIdx.x == 0) tk = atomicAdd(a.ctr, 1u);
+      tk = rdl(tk, 0);
+      if (tk >= ntasks || flagged(a)) return;
+      const uint32_t cw = a.tasks[tk], c = cw >> 16, w = cw & 0xFFFFu;
+      if (w < a.mgk_lim[c])
+      {
+         if (LB) task_lb<NL, F1, false, true>(sm, a, c, w, tk, 0u);
+         else task_ser<NL, F1, false, true>(sm, a, c, w, tk, 0u);
+      }
+      else
+      {
+         if (LB) task_lb<NL, F1, false, false, true>(sm, a, c, w, tk, 0u);
+         else task_ser<NL, F1, false, false, true>(sm, a, c, w, tk, 0u);
+      }
+      wsync();
+   }
+}
+
 // The X and Y phases in ONE persistent launch: the Y tasks fill the slots the X
 // phase's drain leaves empty.  One table in key order: X task (c, w) at its window's
 // start w D_c, Y task (c, w) at its window's end (w+1) D_c plus a lag (GNOC_XY_LAG),
@@ -2176,6 +2214,8 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain_xy(XYArgs xa)
 // raises errflag[2] bit 1 and the chains decline the batch as before.
 constexpr int XM = 2048;
 constexpr int XT = 256;
+constexpr uint32_t XS = 32;   // slots a workgroup scans per round (the tails are spread over the grid)
+constexpr uint32_t XU = 8;    // records per thread per moved chunk
 __device__ __forceinline__ bool key_lt(uint64_t ta, uint32_t ia, uint64_t tb, uint32_t ib)
 {
    return ta < tb || (ta == tb && ia < ib);
@@ -2190,12 +2230,12 @@ __global__ __launch_bounds__(XT) void k_exc_merge(uint32_t nslots, const uint32_
    __shared__ uint32_t s_list[XT], s_n;
    if (errflag[2] == 0) return;   // no exception anywhere
    const uint32_t tid = threadIdx.x;
-   for (uint32_t s0 = blockIdx.x * XT; s0 < nslots; s0 += gridDim.x * XT)
+   for (uint32_t s0 = blockIdx.x * XS; s0 < nslots; s0 += gridDim.x * XS)
    {
       if (tid == 0) s_n = 0;
       __syncthreads();
       const uint32_t sl = s0 + tid;
-      if (sl < nslots && nexc[sl]) s_list[atomicAdd(&s_n, 1u)] = sl;
+      if (tid < XS && sl < nslots && nexc[sl]) s_list[atomicAdd(&s_n, 1u)] = sl;
       __syncthreads();
       const uint32_t nl = s_n;
       for (uint32_t q = 0; q < nl; q++)
@@ -2269,35 +2309,49 @@ __global__ __launch_bounds__(XT) void k_exc_merge(uint32_t nslots, const uint32_
          }
          __syncthreads();
          // FIFO records from the first exception's position up move by the exceptions
-         // before them: top chunk first, each chunk read completely before it is written
+         // before them: top chunk first (XU records per thread, their loads in flight
+         // together), each chunk read completely before it is written
          const uint32_t i0 = x ? edst[0] : m;
+         constexpr uint32_t CH = XU * XT;
          for (uint32_t top = m; top > i0;)
          {
-            const uint32_t a0 = top > i0 + XT ? top - XT : i0;
-            const uint32_t i = a0 + tid;
-            Rec r;
-            uint32_t d = 0;
-            if (i < top)
+            const uint32_t a0 = top > i0 + CH ? top - CH : i0;
+            Rec r[XU];
+            uint32_t d[XU];
+#pragma unroll
+            for (uint32_t u = 0; u < XU; u++)
             {
-               r = recs[b + i];
+               const uint32_t i = a0 + u * XT + tid;
+               if (i < top) r[u] = recs[b + i];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < XU; u++)
+            {
+               const uint32_t i = a0 + u * XT + tid;
                uint32_t lo = 0, hi = x;
-               while (lo < hi)
-               {
-                  const uint32_t mid = (lo + hi) >> 1;
-                  if (key_lt(et[mid], eid[mid], r.t, r.id)) lo = mid + 1;
-                  else hi = mid;
-               }
-               d = i + lo;
+               if (i < top)
+                  while (lo < hi)
+                  {
+                     const uint32_t mid = (lo + hi) >> 1;
+                     if (key_lt(et[mid], eid[mid], r[u].t, r[u].id)) lo = mid + 1;
+                     else hi = mid;
+                  }
+               d[u] = i + lo;
             }
             __syncthreads();
-            if (i < top)
+#pragma unroll
+            for (uint32_t u = 0; u < XU; u++)
             {
-               const uint64_t g = b + d;
-               recs[g] = r;
-               if ((g & 63) == 0)
+               const uint32_t i = a0 + u * XT + tid;
+               if (i < top)
                {
-                  samp_t[g >> 6] = r.t;
-                  samp_id[g >> 6] = r.id;
+                  const uint64_t g = b + d[u];
+                  recs[g] = r[u];
+                  if ((g & 63) == 0)
+                  {
+                     samp_t[g >> 6] = r[u].t;
+                     samp_id[g >> 6] = r[u].id;
+                  }
                }
             }
             __syncthreads();
@@ -2369,6 +2423,7 @@ __global__ __launch_bounds__(256) void k_chain_plan(DevCfg c, uint32_t ncpx, uin
       const uint32_t os = slot_of(ntile, fdir[f], slot_side(fdir[f], nside));
       p.obase[f] = used ? (uint32_t) slot_base[os] : 0u;
       p.ocap[f] = used ? slot_cnt[os] : 0u;
+      p.oslot[f] = os;
    }
    const uint32_t sides[3] = { IN_LOCAL, IN_W, IN_E };
    for (uint32_t j = 0; j < 3; j++)
@@ -2385,7 +2440,7 @@ __global__ __launch_bounds__(256) void k_chain_plan(DevCfg c, uint32_t ncpx, uin
    p.ny = ntile / W;
    p.rl = (uint32_t) rl_of(c, tile);
    p.nl = nl;
-   for (int q = 0; q < 10; q++) p.pad0[q] = 0;
+   for (int q = 0; q < 6; q++) p.pad0[q] = 0;
    out[k] = p;
 }
 

@@ -236,6 +236,14 @@ struct gnoc_engine
    unsigned ch_yflags = 0;                  // the Y phase's chain flags of the last run that declined
    int exc_fix = 0;                         // this batch's injection level leaves exception tails: k_exc_merge
    int ch_mg = 0;                           // this batch's chains meet the no-gap M/G/1 branch: k_chain's MG instantiation
+   // MG batches: per phase and chain, the windows that may serve M/G/1 requests (from
+   // the last MG run on these windows); those run on the MG instantiation, the rest of
+   // the phase on the common one (chain_phase)
+   std::vector<uint32_t> h_mgk[2], up_mgk[2], h_tasks2[2];
+   std::vector<uint64_t> mgk_D[2];          // the windows h_mgk was measured on
+   void* up_p[2] = { nullptr, nullptr };
+   int mgk_ok = 0, ch_split = 0;
+   DevBuf ch_tasks2;
    std::vector<std::pair<void*, uint64_t>> zq;   // buffers to zero before the first level launch (one k_zero_segs)
    int ch_resized = 0;                      // the windows were already changed during this (sharded) run
    int used_chain = 0;
@@ -499,7 +507,7 @@ int gnoc_create(const gnoc_config* cfg, gnoc_engine** out)
    if (he == hipSuccess) he = hipHostMalloc((void**) &e->h_val, 128, hipHostMallocDefault);
    // per chain fill maxima: 2 u32 for each of the <= 2 (W + H) chains
    if (he == hipSuccess)
-      he = hipHostMalloc((void**) &e->h_nmax, 16 * ((size_t) e->dc.W + e->dc.H) + 64, hipHostMallocDefault);
+      he = hipHostMalloc((void**) &e->h_nmax, 32 * ((size_t) e->dc.W + e->dc.H) + 64, hipHostMallocDefault);
    if (he == hipSuccess) he = upload_levels(e);
    if (he == hipSuccess)
    {
@@ -703,6 +711,7 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
    e->ch_ydeclined = 0;
    e->exc_fix = 0;
    e->ch_mg = 0;
+   e->mgk_ok = 0;
    e->pipe_declined = 0;
    if (same) return;
    const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size (2^shift ps)
@@ -2075,7 +2084,8 @@ static int chain_setup(gnoc_engine* e)
    GNOC_HIP(e, e->ch_ctr.ensure(256));   // [0, 1] dequeue heads
    // per chain fill maxima, away from the flag word every hand-off poll reads (task-end
    // atomics next to it slowed the polls by half)
-   const size_t nmx = 2 * (e->h_cw[0].size() + e->h_cw[1].size());
+   // (then per chain the M/G/1 window bound, k_chain mgk)
+   const size_t nmx = 3 * (e->h_cw[0].size() + e->h_cw[1].size());
    GNOC_HIP(e, e->ch_nmax.ensure(std::max<size_t>(nmx, 1) * 4));
    e->zq.push_back({ e->ch_nmax.p, (uint64_t) std::max<size_t>(nmx, 1) * 4 });   // (zq_flush: before the INJ level)
    const size_t stb = (e->ch_st_words[0] + e->ch_st_words[1] + ch::SW) * 8;
@@ -2157,6 +2167,7 @@ static ChainArgs chain_args(gnoc_engine* e, int phase)
    a.tasks = e->ch_tasks.as<uint32_t>() + (phase ? e->h_tasks[0].size() : 0);
    a.cp0 = 0;
    a.nmax = e->ch_nmax.as<unsigned>() + (phase ? 2 * e->h_cw[0].size() : 0);
+   a.mgk = e->ch_nmax.as<unsigned>() + 2 * (e->h_cw[0].size() + e->h_cw[1].size()) + (phase ? e->h_cw[0].size() : 0);
    a.excfix = (uint32_t) e->exc_fix;
    a.etag = (uint64_t) e->ch_epoch << 48;
    a.stamps = nullptr;
@@ -2195,6 +2206,41 @@ static int chain_phase(gnoc_engine* e, int phase)
    }
    const uint32_t grid = (uint32_t) std::min<uint64_t>((uint64_t) e->ch_grid, (uint64_t) a.ntasks);
    GNOC_HIP(e, hipEventRecord(e->ch_ev[phase][0], s));
+   // an MG batch whose M/G/1 windows are known for these windows: only those tasks take
+   // the MG path (each chain's first windows), the rest of the phase the common one, in
+   // one launch (k_chain_mix)
+   const std::vector<uint32_t>& mk = e->h_mgk[phase];
+   const bool split = e->ch_mg && e->mgk_ok && e->mgk_D[phase] == e->chD_run[phase] && !a.stamps && e->nranks <= 1 &&
+                      mk.size() == (size_t) a.nch && !std::getenv("GNOC_MG_SPLIT_OFF");
+   if (split)
+   {
+      std::vector<uint32_t>& lim = e->h_tasks2[phase];   // (kept: the source of an async copy)
+      lim.assign(mk.begin(), mk.end());
+      for (uint32_t& v : lim) v = std::max(1u, v);
+      const size_t off = phase ? e->h_cw[0].size() : 0;
+      GNOC_HIP(e, e->ch_tasks2.ensure((e->h_cw[0].size() + e->h_cw[1].size()) * 4 + 4));
+      if (e->up_mgk[phase] != lim || e->up_p[phase] != e->ch_tasks2.p)
+      {
+         GNOC_HIP(e, hipMemcpyAsync(e->ch_tasks2.as<uint32_t>() + off, lim.data(), lim.size() * 4, hipMemcpyHostToDevice, s));
+         e->up_mgk[phase] = lim;
+         e->up_p[phase] = e->ch_tasks2.p;
+      }
+      a.mgk_lim = e->ch_tasks2.as<uint32_t>() + off;
+#define GNOC_CHAIN_MIX(NLV, F1V)                                                                                  \
+   do                                                                                                             \
+   {                                                                                                              \
+      if (a.lookback) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain_mix<NLV, F1V, true>), dim3(grid), dim3(ch::T), 0, s, a); \
+      else GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain_mix<NLV, F1V, false>), dim3(grid), dim3(ch::T), 0, s, a);        \
+   } while (0)
+      if (phase && e->f1) GNOC_CHAIN_MIX(3, true);
+      else if (phase) GNOC_CHAIN_MIX(3, false);
+      else if (e->f1) GNOC_CHAIN_MIX(1, true);
+      else GNOC_CHAIN_MIX(1, false);
+#undef GNOC_CHAIN_MIX
+      e->ch_split |= 1 << phase;
+      GNOC_HIP(e, hipEventRecord(e->ch_ev[phase][1], s));
+      return GNOC_OK;
+   }
    // f != 1 GHz: the copy with the reference's double ps <-> cycle conversions
    // (ch_mg: the batch's chains met the no-gap M/G/1 branch; the instantiation with
    // the serial path, whose register allocation the common one does not pay for)
@@ -2423,7 +2469,7 @@ static int zq_flush(gnoc_engine* e, hipStream_t s)
 static int exc_merge(gnoc_engine* e)
 {
    const uint32_t nslots = e->dc.N * PORTS * INS;
-   const uint32_t wins = (nslots + ch::XT - 1) / ch::XT;
+   const uint32_t wins = (nslots + ch::XS - 1) / ch::XS;
    GNOC_LAUNCH(e, KC_BOUNDS, ch::k_exc_merge, dim3(std::max(1u, std::min(wins, 2048u))), dim3(ch::XT), 0, e->stream, nslots,
                e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->nexc.as<uint32_t>(), e->recs.as<Rec>(),
                e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->counters.as<unsigned>() + 8);
@@ -2720,7 +2766,7 @@ static int run_post_enqueue(gnoc_engine* e, bool closed_form)
    {
       GNOC_HIP(e, hipMemcpyAsync(e->h_pinned + 3, e->gtot.as<uint64_t>() + 1, 8, hipMemcpyDeviceToHost, s));
       if (e->used_chain)
-         GNOC_HIP(e, hipMemcpyAsync(e->h_nmax, e->ch_nmax.p, 8 * (e->h_cw[0].size() + e->h_cw[1].size()),
+         GNOC_HIP(e, hipMemcpyAsync(e->h_nmax, e->ch_nmax.p, 12 * (e->h_cw[0].size() + e->h_cw[1].size()),
                                     hipMemcpyDeviceToHost, s));
    }
    return GNOC_OK;
@@ -2818,7 +2864,13 @@ static int run_post_check(gnoc_engine* e, bool closed_form)
       // meets whatever else declined again, so the other reasons wait for it):
       // the injection level left exception tails -> merge them first ...
       if (!e->exc_fix && e->nranks <= 1 && (ef[4] & ch::R_EXC) && !(ef[2] & 2u)) return GNOC_CH_EXC;
-      // ... the no-gap M/G/1 branch -> the instantiation with the serial path
+      // ... the no-gap M/G/1 branch -> the instantiation with the serial path (a split
+      // run whose common launch met it: the MG instantiation for every window again)
+      if (e->ch_split && (cf & ch::R_MG1) && !(cf & ch::F_TIMEOUT) && !(cf & ch::R_MGBAD))
+      {
+         e->mgk_ok = 0;
+         return GNOC_CH_MG;
+      }
       if (!e->ch_mg && e->nranks <= 1 && (cf & ch::R_MG1) && !(cf & ch::F_TIMEOUT)) return GNOC_CH_MG;
       // only the Y chains declined, for a reason the level engine takes (the M/G/1
       // branch, a spill range, a hand-off timeout): the X phase's outputs stand
@@ -2834,6 +2886,18 @@ static int run_post_check(gnoc_engine* e, bool closed_form)
       return GNOC_V3_RETRY;
    }
    if (errf & 1u) return fail(e, GNOC_EHIP, "internal: route-count invariant violated");
+   if (e->used_chain && e->ch_mg)
+   {
+      // the windows of each chain that may serve M/G/1 requests (k_chain mgk): the next
+      // run of the batch on these windows gives the MG instantiation only those
+      const size_t n0 = e->h_cw[0].size(), n1 = e->h_cw[1].size();
+      const unsigned* mk = e->h_nmax + 2 * (n0 + n1);
+      e->h_mgk[0].assign(mk, mk + n0);
+      e->h_mgk[1].assign(mk + n0, mk + n0 + n1);
+      e->mgk_D[0] = e->chD_run[0];
+      e->mgk_D[1] = e->chD_run[1];
+      e->mgk_ok = 1;
+   }
    e->ran = true;
    return GNOC_OK;
 }
@@ -2877,6 +2941,7 @@ static int run_once(gnoc_engine* e)
       const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
       e->used_chain = 1;
       e->used_v3 = 4;
+      e->ch_split = 0;
       rc = run_plan_v3(e, !e->ch_ydeclined);   // (Y on k_level: its levels too)
       if (!rc) rc = chain_setup(e);
       if (!rc) rc = run_levels_v3(e, 0, 1);
@@ -3963,7 +4028,8 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
    while (sh < 63 && (2ull << sh) <= dm[0]) sh++;
    out->window_shift = e->used_chain ? sh : 0u;
    out->windows_y = nwm[1];
-   out->chain_protocol = e->used_chain ? 0x100u | e->ch_lb_run[0] | (e->ch_lb_run[1] << 1) | (e->ch_fused ? 0x200u : 0u) | (e->ch_mg ? 0x400u : 0u) : 0u;
+   out->chain_protocol = e->used_chain ? 0x100u | e->ch_lb_run[0] | (e->ch_lb_run[1] << 1) | (e->ch_fused ? 0x200u : 0u) | (e->ch_mg ? 0x400u : 0u) |
+                                         (e->ch_split ? 0x800u : 0u) : 0u;
    out->window_ps_x = dm[0];
    out->window_ps_y = dm[1];
    out->runs = e->runs;

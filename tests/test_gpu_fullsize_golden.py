@@ -102,15 +102,18 @@ def test_configs1_full_size_mg1_burst_matches_oracle(lookback, monkeypatch):
     eng = gnoc.Engine(gnoc.EngineConfig(num_tiles=1024))
     eng.submit(tr)
     paths = []
-    for r in range(3):
+    for r in range(5):
         eng.run()
         s = eng.summary()
         paths.append(int(s["engine_path"]))
         assert s["mg1_uses"] == GOLD[name]["mg1_uses"], (s["mg1_uses"], GOLD[name]["mg1_uses"])
         _check(name, eng.results())
-        if r:   # later runs go straight to k_chain's MG instantiation (bit 10)
+        if r:   # later runs go straight to k_chain's MG instantiation (bit 10) ...
             assert s["engine_path"] == 4 and s["chain_protocol"] & 0x400, s
             assert s["retries"] == 0 and s["fallbacks"] == 0, s
+    # ... and once the windows have settled and its M/G/1 windows are known, only those
+    # take the M/G/1 path (bit 11, k_chain_mix)
+    assert s["chain_protocol"] & 0x800, s
     eng.close()
     print("engine paths", paths)
 
