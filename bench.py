@@ -534,7 +534,7 @@ def pinned_trace(tr):
                       pin(tr.flags if tr.flags is not None else np.zeros(len(tr), np.uint32)))
 
 
-PMC_FILE = "r4_pmc.json"
+PMC_FILE = "r5_pmc.json"
 
 
 def pmc_traffic(workload, kernel, bid):
