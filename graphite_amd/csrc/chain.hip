@@ -2451,9 +2451,9 @@ __global__ __launch_bounds__(256) void k_chain_plan(DevCfg c, uint32_t ncpx, uin
 // that launch (y_bounds).
 __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict__ cp, uint32_t nl, uint32_t len,
                                                     const ChainWin* __restrict__ cw, const Rec* __restrict__ recs,
-                                                    uint32_t* __restrict__ bt, uint32_t nlrun)
+                                                    uint32_t* __restrict__ bt, uint32_t nlrun, uint32_t j0)
 {
-   const uint32_t k = blockIdx.x / nlrun, j = blockIdx.x % nlrun, c = k / len, i = k % len;
+   const uint32_t k = blockIdx.x / nlrun, j = j0 + blockIdx.x % nlrun, c = k / len, i = k % len;
    const uint64_t D = cw[c].D;
    const uint32_t nW = cw[c].nW;
    const uint64_t base = cp[k].ibase[j];

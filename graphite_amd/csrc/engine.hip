@@ -243,6 +243,7 @@ struct gnoc_engine
    std::vector<uint64_t> mgk_D[2];          // the windows h_mgk was measured on
    void* up_p[2] = { nullptr, nullptr };
    int mgk_ok = 0, ch_split = 0;
+   int ch_ylocal = 0;   // this run's Y IN_LOCAL window bounds were made beside the X phase's
    DevBuf ch_tasks2;
    std::vector<std::pair<void*, uint64_t>> zq;   // buffers to zero before the first level launch (one k_zero_segs)
    int ch_resized = 0;                      // the windows were already changed during this (sharded) run
@@ -2193,8 +2194,26 @@ static int chain_phase(gnoc_engine* e, int phase)
    if (!ncp) return GNOC_OK;
    ChainArgs a = chain_args(e, phase);
    const uint32_t nl = phase ? 3u : 1u;
-   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, a.cp, nl, a.len, a.cw, e->recs.as<Rec>(),
-               const_cast<uint32_t*>(a.bt), nl);
+   // The Y ports' IN_LOCAL lists are injection outputs, complete with the X phase's
+   // inserts: one-engine runs bound them beside the X lists, the Y launch then only
+   // its IN_W / IN_E lists (the X phase's turns)
+   const bool ylocal = e->nranks <= 1 && e->ncpy;
+   if (phase == 0 || !e->ch_ylocal)
+      GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, a.cp, nl, a.len, a.cw, e->recs.as<Rec>(),
+                  const_cast<uint32_t*>(a.bt), nl, 0u);
+   else
+      GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * 2), dim3(256), 0, s, a.cp, nl, a.len, a.cw, e->recs.as<Rec>(),
+                  const_cast<uint32_t*>(a.bt), 2u, 1u);
+   if (phase == 0)
+   {
+      if (ylocal)
+      {
+         const ChainArgs ay = chain_args(e, 1);
+         GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpy), dim3(256), 0, s, ay.cp, 3u, ay.len, ay.cw,
+                     e->recs.as<Rec>(), const_cast<uint32_t*>(ay.bt), 1u, 0u);
+         e->ch_ylocal = 1;
+      }
+   }
    const char* stv = std::getenv("GNOC_STAMPS");
    if (stv && *stv == '1')
    {
@@ -2285,9 +2304,9 @@ static int chain_fused(gnoc_engine* e)
    xa.y = chain_args(e, 1);
    // X inserts (injection outputs) and the Y ports' IN_LOCAL lists: complete before the launch
    GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpx), dim3(256), 0, s, xa.x.cp, 1u, xa.x.len, xa.x.cw,
-               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.x.bt), 1u);
+               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.x.bt), 1u, 0u);
    GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpy), dim3(256), 0, s, xa.y.cp, 3u, xa.y.len, xa.y.cw,
-               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.y.bt), 1u);
+               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.y.bt), 1u, 0u);
    const uint32_t nx = (uint32_t) e->h_tasks[0].size();
    xa.x.fw2 = 5u;                                  // an X decline stops the Y tasks too
    xa.y.ctr = xa.x.ctr;                            // one dequeue head
@@ -2942,6 +2961,7 @@ static int run_once(gnoc_engine* e)
       e->used_chain = 1;
       e->used_v3 = 4;
       e->ch_split = 0;
+      e->ch_ylocal = 0;
       rc = run_plan_v3(e, !e->ch_ydeclined);   // (Y on k_level: its levels too)
       if (!rc) rc = chain_setup(e);
       if (!rc) rc = run_levels_v3(e, 0, 1);
