@@ -2503,6 +2503,237 @@ __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict_
    }
 }
 
+// ---------------------------------------------------------------------------
+// The injection level streamed: one workgroup per source tile walks its injection
+// slot in blocks of 1,024 records (4 consecutive per thread), the queue's tail X
+// carried from block to block -- no chunk plan, no look-back.  A block: each
+// thread composes its records' max-plus aggregate, a wave scan and the four waves'
+// aggregates (in order, from X) give every record the tail ahead of it; route
+// counts per output field (LEFT, RIGHT, DOWN, UP of the same tile) give FIFO
+// positions.  Relative cycles (to the block's first cycle) keep the scan in 32
+// bits.  The no-gap M/G/1 prefix (queue_model_history_tree.cc:58-64) is not served
+// here: a port whose first arrival is at cycle 0 is checked until its first idle
+// cycle, and where the branch would fire the kernel declines (errflag[7]); the host
+// has queued k_inj_undo and k_level's injection level behind it, which then run the
+// level (they return at once otherwise).  Unicast batches of the chain path only.
+// ---------------------------------------------------------------------------
+constexpr uint32_t IJ_T = 256, IJ_PER = 4, IJ_BLK = IJ_T * IJ_PER;
+template <bool F1>
+__global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* __restrict__ slot_cnt,
+                                                     const uint64_t* __restrict__ slot_base, Rec* __restrict__ recs,
+                                                     uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id,
+                                                     unsigned long long* __restrict__ port_sum,
+                                                     unsigned long long* __restrict__ port_cnt,
+                                                     unsigned long long* __restrict__ port_flit,
+                                                     unsigned long long* __restrict__ port_last, unsigned* __restrict__ errflag)
+{
+   __shared__ uint32_t wA[4], wB[4], wc01[4], wc23[4];
+   __shared__ uint32_t s_xin[4], s_fb[4][4], s_run[4], s_ev[2], s_decl;
+   __shared__ uint64_t s_X;
+   __shared__ unsigned long long s_sum[4], s_flit[4];
+   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+   const uint32_t tile = blockIdx.x;
+   const uint32_t sl = slot_of(tile, P_INJ, IN_LOCAL);
+   const uint32_t n = slot_cnt[sl];
+   if (n == 0) return;
+   const uint64_t base = slot_base[sl];
+   uint32_t x, y;
+   tile_xy(tile, c.W, c.magicW, x, y);
+   uint32_t ob[4], oc[4];
+#pragma unroll
+   for (uint32_t q = 0; q < 4; q++)
+   {
+      const uint32_t d = P_LEFT + q;   // LEFT, RIGHT, DOWN, UP
+      const uint32_t os = slot_of(tile, d, slot_side(d, IN_LOCAL));
+      ob[q] = (uint32_t) slot_base[os];
+      oc[q] = slot_cnt[os];
+   }
+   const double f = c.f;
+   if (tid < 4) s_run[tid] = 0;
+   if (tid == 0)
+   {
+      s_X = 0;
+      s_decl = 0;
+   }
+   // the port starts with no gap in its history tree only if its first request is at cycle 0
+   bool nogap = c.analytical && cyc_of<F1>(recs[base].t, f) == 0;
+   uint64_t ssum = 0, flits = 0;
+   __syncthreads();
+   for (uint32_t b0 = 0; b0 < n; b0 += IJ_BLK)
+   {
+      const uint64_t bc = cyc_of<F1>(recs[base + b0].t, f);   // the block's first cycle (the slot is sorted)
+      Rec r[IJ_PER];
+      uint32_t tr[IJ_PER], pr[IJ_PER], fr[IJ_PER];
+      bool vr[IJ_PER];
+#pragma unroll
+      for (uint32_t k = 0; k < IJ_PER; k++)
+      {
+         const uint32_t j = b0 + tid * IJ_PER + k;
+         vr[k] = j < n;
+         if (vr[k]) r[k] = recs[base + j];
+      }
+      uint32_t A = 0, B = 0, c01 = 0, c23 = 0;
+      bool wide = false;
+#pragma unroll
+      for (uint32_t k = 0; k < IJ_PER; k++)
+      {
+         tr[k] = pr[k] = fr[k] = 0;
+         if (!vr[k]) continue;
+         const uint64_t tc = cyc_of<F1>(r[k].t, f) - bc;
+         wide |= tc >= (1ull << 30);
+         tr[k] = (uint32_t) tc;
+         pr[k] = aux_F(r[k].aux);
+         const uint32_t d = xy_dir(x, y, aux_dx(r[k].aux), aux_dy(r[k].aux)) - P_LEFT;   // 0..3 (never SELF)
+         fr[k] = d;
+         const uint32_t nb = B + pr[k], nt = tr[k] + pr[k];
+         B = nb > nt ? nb : nt;
+         A += pr[k];
+         if (d < 2) c01 += 1u << (16 * d);
+         else c23 += 1u << (16 * (d - 2));
+      }
+      // the waves' inclusive prefixes; lane 63 holds each wave's aggregate
+      uint32_t iA = A, iB = B;
+      wave_scan(iA, iB);
+      const uint32_t i01 = wave_sum32(c01), i23 = wave_sum32(c23);
+      if (lane == 63)
+      {
+         wA[wv] = iA;
+         wB[wv] = iB;
+         wc01[wv] = i01;
+         wc23[wv] = i23;
+      }
+      if (wide) s_decl = 1;
+      __syncthreads();
+      if (tid == 0)
+      {
+         uint64_t Xr = s_X > bc ? s_X - bc : 0;   // an earlier tail behaves like the block's first cycle
+         if (Xr >= (1ull << 30)) s_decl = 1;
+         for (uint32_t q = 0; q < 4; q++)
+         {
+            s_xin[q] = (uint32_t) Xr;
+            const uint64_t xa = Xr + wA[q];
+            Xr = xa > wB[q] ? xa : wB[q];
+            for (uint32_t d = 0; d < 4; d++)
+            {
+               s_fb[q][d] = s_run[d];
+               s_run[d] += d < 2 ? (wc01[q] >> (16 * d)) & 0xFFFFu : (wc23[q] >> (16 * (d - 2))) & 0xFFFFu;
+            }
+         }
+         s_X = bc + Xr;
+         s_ev[0] = s_ev[1] = 0xFFFFFFFFu;
+      }
+      __syncthreads();
+      if (s_decl)
+      {
+         if (tid == 0) atomicOr(errflag + 7, 1u);
+         return;
+      }
+      // the tail ahead of this thread: its wave's entry composed with the lanes before it
+      const uint32_t exA = dpp32<0x138, 0xF, 0xF>(iA), exB = dpp32<0x138, 0xF, 0xF>(iB);   // wave_shr 1
+      const uint32_t xa = s_xin[wv] + exA;
+      uint32_t Xt = xa > exB ? xa : exB;
+      const uint32_t x01 = i01 - c01, x23 = i23 - c23;   // the wave's field counts ahead of this thread
+      uint32_t kr[4] = { 0, 0, 0, 0 };
+#pragma unroll
+      for (uint32_t k = 0; k < IJ_PER; k++)
+      {
+         if (!vr[k]) continue;
+         const uint32_t tc = tr[k], p = pr[k], d = fr[k];
+         if (nogap)
+         {
+            const uint32_t at = tid * IJ_PER + k;
+            if (tc > Xt) atomicMin(&s_ev[0], at);            // the first idle cycle
+            else if (Xt > tc + p) atomicMin(&s_ev[1], at);   // the M/G/1 branch would serve it
+         }
+         const uint32_t cc = Xt > tc ? Xt - tc : 0u;
+         Xt = (Xt > tc ? Xt : tc) + p;
+         ssum += cc;
+         flits += p;
+         uint32_t kk = 0, ahead = 0;
+#pragma unroll
+         for (uint32_t q = 0; q < 4; q++)
+            if (q == d)
+            {
+               kk = kr[q]++;
+               ahead = q < 2 ? (x01 >> (16 * q)) & 0xFFFFu : (x23 >> (16 * (q - 2))) & 0xFFFFu;
+            }
+         uint32_t obd = 0, ocd = 0;
+#pragma unroll
+         for (uint32_t q = 0; q < 4; q++)
+            if (q == d)
+            {
+               obd = ob[q];
+               ocd = oc[q];
+            }
+         const uint32_t pos = s_fb[wv][d] + ahead + kk;
+         if (pos >= ocd)
+         {
+            atomicOr(errflag, 1u);   // route-count invariant broken: never write outside the slot
+            continue;
+         }
+         const uint64_t gp = (uint64_t) obd + pos;
+         Rec o;
+         o.t = r[k].t + ps_of<F1>(cc, f);
+         o.id = r[k].id;
+         o.aux = r[k].aux;
+         recs[gp] = o;
+         if ((gp & 63) == 0)
+         {
+            samp_t[gp >> 6] = o.t;
+            samp_id[gp >> 6] = o.id;
+         }
+      }
+      __syncthreads();
+      if (nogap)
+      {
+         // the no-gap prefix: an M/G/1 request before the first idle cycle -> decline;
+         // an idle cycle ends the prefix for good (queue_model_history_tree.cc:79-86)
+         if (s_ev[1] != 0xFFFFFFFFu && s_ev[1] < s_ev[0])
+         {
+            if (tid == 0) atomicOr(errflag + 7, 2u);
+            return;
+         }
+         nogap = s_ev[0] == 0xFFFFFFFFu;
+      }
+   }
+   // the port's counters (router_model.cc:136-144): contention cycles, requests, flits, last departure
+   uint64_t a0 = ssum, a1 = flits;
+   for (int off = 32; off > 0; off >>= 1)
+   {
+      a0 += __shfl_down(a0, off);
+      a1 += __shfl_down(a1, off);
+   }
+   if (lane == 0)
+   {
+      s_sum[wv] = a0;
+      s_flit[wv] = a1;
+   }
+   __syncthreads();
+   if (tid == 0)
+   {
+      const uint32_t port = tile * PORTS + P_INJ;
+      atomicAdd(&port_sum[port], s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3]);
+      atomicAdd(&port_cnt[port], (unsigned long long) n);
+      atomicAdd(&port_flit[port], s_flit[0] + s_flit[1] + s_flit[2] + s_flit[3]);
+      atomicMax(&port_last[port], (unsigned long long) s_X);
+   }
+}
+// After k_inj_stream declined (errflag[7]): the injection ports' counters back to zero
+// for k_level's rerun of the level.
+__global__ __launch_bounds__(256) void k_inj_undo(uint32_t N, const unsigned* __restrict__ errflag,
+                                                  unsigned long long* __restrict__ s0, unsigned long long* __restrict__ s1,
+                                                  unsigned long long* __restrict__ s2, unsigned long long* __restrict__ s3)
+{
+   if (!errflag[7]) return;
+   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+   if (t >= N) return;
+   const uint32_t p = t * PORTS + P_INJ;
+   s0[p] = 0;
+   s1[p] = 0;
+   s2[p] = 0;
+   s3[p] = 0;
+}
+
 // Zero the per-port counters of ports whose direction is in dmask (a phase
 // that reruns on the level engine after the chain engine declined it).
 __global__ __launch_bounds__(256) void k_zero_ports(uint32_t nports, uint32_t dmask, unsigned long long* __restrict__ s0,

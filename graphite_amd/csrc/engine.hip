@@ -88,12 +88,12 @@ struct DevBuf
 enum KernelClass
 {
    KC_CLASSIFY, KC_SRC_TOT, KC_INJ_BASE, KC_SRC_OFFS, KC_SCATTER, KC_ROW_HIST, KC_PROW, KC_SLOT_COUNTS, KC_SCAN,
-   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_BCAST, KC_CHAIN, KC_BOUNDS, KC_PIPE, KC_N
+   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_BCAST, KC_CHAIN, KC_BOUNDS, KC_PIPE, KC_INJ, KC_N
 };
 static const char* const kKernelNames[KC_N] = { "k_classify", "k_src_tot", "k_inj_base", "k_src_offs", "k_scatter",
                                                 "k_row_hist", "k_prow", "k_slot_counts", "k_scan_slots", "k_plan",
                                                 "k_level", "k_port_stream", "k_finalize", "k_bcast",
-                                                "k_chain", "k_win_bounds", "k_pipe" };
+                                                "k_chain", "k_win_bounds", "k_pipe", "k_inj_stream" };
 
 struct gnoc_engine
 {
@@ -1981,8 +1981,9 @@ static int run_plan_v3(gnoc_engine* e, bool ends_only = false)
    return GNOC_OK;
 }
 
-// Levels [l0, l1) of the plan built by run_plan_v3.
-static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
+// Levels [l0, l1) of the plan built by run_plan_v3 (cond: each launch runs only if the
+// streamed injection level declined, errflag[7]).
+static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1, bool cond = false)
 {
    const DevCfg& c = e->dc;
    hipStream_t s = e->stream;
@@ -2014,7 +2015,7 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
    const bool xl = xlv && *xlv == '1' && e->nranks == 1 && !e->nb && e->f1;
    uint64_t* stp = stamps ? e->stamps.as<uint64_t>() : nullptr;
 #define GNOC_LEVEL_ARGS(lvl)                                                                                         \
-   c, (lvl), e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
+   c, (lvl) | (cond ? 0x80000000u : 0u), e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
       e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(),                 \
       e->st.as<uint64_t>(), fin_out(e), e->port_sum.as<unsigned long long>(),                                          \
       e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),                                     \
@@ -2047,6 +2048,33 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1)
    }
 #undef GNOC_LEVEL_ARGS
    return GNOC_OK;
+}
+
+// The injection level of a one-engine unicast chain / pipeline run: k_inj_stream,
+// then k_inj_undo and the k_level launch that run only if it declined.
+static int inj_level(gnoc_engine* e)
+{
+   const char* v = std::getenv("GNOC_INJ_STREAM");
+   if ((v && *v && std::atoi(v) == 0) || e->nb || e->nranks > 1) return run_levels_v3(e, 0, 1);
+   {
+      const int zr = zq_flush(e, e->stream);
+      if (zr) return zr;
+   }
+   hipStream_t s = e->stream;
+   const uint32_t N = e->dc.N;
+#define GNOC_INJS(F1V)                                                                                               \
+   GNOC_LAUNCH(e, KC_INJ, ch::k_inj_stream<F1V>, dim3(N), dim3(ch::IJ_T), 0, s, e->dc, e->slot_cnt.as<uint32_t>(),  \
+               e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(),  \
+               e->port_sum.as<unsigned long long>(), e->port_cnt.as<unsigned long long>(),                          \
+               e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>(), e->counters.as<unsigned>() + 8)
+   if (e->f1) GNOC_INJS(true);
+   else GNOC_INJS(false);
+#undef GNOC_INJS
+   GNOC_LAUNCH(e, KC_INJ, ch::k_inj_undo, dim3((N + 255) / 256), dim3(256), 0, s, N,
+               (const unsigned*) (e->counters.as<unsigned>() + 8), e->port_sum.as<unsigned long long>(),
+               e->port_cnt.as<unsigned long long>(), e->port_flit.as<unsigned long long>(),
+               e->port_last.as<unsigned long long>());
+   return run_levels_v3(e, 0, 1, true);
 }
 
 constexpr int GNOC_V3_RETRY = 1000;
@@ -2944,7 +2972,7 @@ static int run_once(gnoc_engine* e)
       e->used_v3 = 6;
       rc = run_plan_v3(e, true);
       if (!rc) rc = pipe_setup(e);
-      if (!rc) rc = run_levels_v3(e, 0, 1);
+      if (!rc) rc = inj_level(e);
       if (!rc && e->exc_fix) rc = exc_merge(e);
       if (!rc) rc = pipe_phase(e, 0);
       if (!rc) rc = pipe_phase(e, 1);
@@ -2964,7 +2992,7 @@ static int run_once(gnoc_engine* e)
       e->ch_ylocal = 0;
       rc = run_plan_v3(e, !e->ch_ydeclined);   // (Y on k_level: its levels too)
       if (!rc) rc = chain_setup(e);
-      if (!rc) rc = run_levels_v3(e, 0, 1);
+      if (!rc) rc = inj_level(e);
       if (!rc && e->exc_fix) rc = exc_merge(e);
       e->ch_fused = 0;
       if (!rc && chain_fusable(e)) rc = chain_fused(e);

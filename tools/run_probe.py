@@ -3,6 +3,8 @@ library GNOC_LIB names and print the per-run ms (for rocprofv3 kernel traces of
 timing variants).
 
     python tools/run_probe.py [runs] [hotspot_fraction]
+
+GNOC_PROBE_PROF=1 adds one profiled run's per-kernel-class device ms.
 """
 import os
 import sys
@@ -23,6 +25,10 @@ def main():
         ms.append(round(eng.summary()["last_run_ms"], 3))
     s = eng.summary()
     print("lib", os.environ.get("GNOC_LIB", "default"), "path", s["engine_path"], "ms", ms, flush=True)
+    if os.environ.get("GNOC_PROBE_PROF"):
+        eng.set_profiling(True)
+        eng.run()
+        print("kernel_ms", {k: round(v[0], 4) for k, v in eng.kernel_stats().items() if v[1]}, flush=True)
     eng.close()
 
 
