@@ -2451,8 +2451,10 @@ __global__ __launch_bounds__(256) void k_chain_plan(DevCfg c, uint32_t ncpx, uin
 // that launch (y_bounds).
 __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict__ cp, uint32_t nl, uint32_t len,
                                                     const ChainWin* __restrict__ cw, const Rec* __restrict__ recs,
-                                                    uint32_t* __restrict__ bt, uint32_t nlrun, uint32_t j0)
+                                                    uint32_t* __restrict__ bt, uint32_t nlrun, uint32_t j0,
+                                                    const unsigned* __restrict__ cond)
 {
+   if (cond && *cond == 0) return;   // k_inj_stream wrote these bounds (it did not decline)
    const uint32_t k = blockIdx.x / nlrun, j = j0 + blockIdx.x % nlrun, c = k / len, i = k % len;
    const uint64_t D = cw[c].D;
    const uint32_t nW = cw[c].nW;
@@ -2517,7 +2519,21 @@ __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict_
 // has queued k_inj_undo and k_level's injection level behind it, which then run the
 // level (they return at once otherwise).  Unicast batches of the chain path only.
 // ---------------------------------------------------------------------------
-constexpr uint32_t IJ_T = 256, IJ_PER = 4, IJ_BLK = IJ_T * IJ_PER;
+#ifndef IJ_PER_V
+#define IJ_PER_V 4
+#endif
+#ifndef IJ_PF
+#define IJ_PF 1
+#endif
+constexpr uint32_t IJ_T = 256, IJ_PER = IJ_PER_V, IJ_BLK = IJ_T * IJ_PER;
+constexpr uint32_t IJ_NWB = 1025;   // window bounds kept in LDS: chains of at most 1,024 windows
+//
+// With cwx (single-mesh chain runs) it also writes k_win_bounds' bounds of the four
+// chain ports' IN_LOCAL lists it fills (X ports: list 0 of bt; Y ports: list 0 of
+// 3): bt[w] = first record of the slot with t >= w D, bt[nW] = count.  The output
+// slots are FIFO-served in order, so their times do not decrease: every record
+// lowers its window's entry (LDS atomicMin), then a suffix min fills the empty
+// windows.  Those k_win_bounds launches run only when this kernel declined.
 template <bool F1>
 __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* __restrict__ slot_cnt,
                                                      const uint64_t* __restrict__ slot_base, Rec* __restrict__ recs,
@@ -2525,17 +2541,24 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
                                                      unsigned long long* __restrict__ port_sum,
                                                      unsigned long long* __restrict__ port_cnt,
                                                      unsigned long long* __restrict__ port_flit,
-                                                     unsigned long long* __restrict__ port_last, unsigned* __restrict__ errflag)
+                                                     unsigned long long* __restrict__ port_last, unsigned* __restrict__ errflag,
+                                                     const ChainWin* __restrict__ cwx, uint32_t* __restrict__ btx,
+                                                     const ChainWin* __restrict__ cwy, uint32_t* __restrict__ bty)
 {
    __shared__ uint32_t wA[4], wB[4], wc01[4], wc23[4];
    __shared__ uint32_t s_xin[4], s_fb[4][4], s_run[4], s_ev[2], s_decl;
    __shared__ uint64_t s_X;
    __shared__ unsigned long long s_sum[4], s_flit[4];
+   __shared__ uint32_t s_bt[4][IJ_NWB], s_nW[4];
+   __shared__ uint64_t s_D[4];
+   __shared__ double s_inv[4];
+   __shared__ uint32_t* s_bp[4];
    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
    const uint32_t tile = blockIdx.x;
    const uint32_t sl = slot_of(tile, P_INJ, IN_LOCAL);
    const uint32_t n = slot_cnt[sl];
-   if (n == 0) return;
+   const bool bnd = cwx != nullptr;
+   if (n == 0 && !bnd) return;
    const uint64_t base = slot_base[sl];
    uint32_t x, y;
    tile_xy(tile, c.W, c.magicW, x, y);
@@ -2555,10 +2578,46 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
       s_X = 0;
       s_decl = 0;
    }
+   if (bnd)
+   {
+      if (tid < 4)
+      {
+         // the chain port (k_chain_plan's numbering, rows / columns from 0) of field tid
+         const uint32_t d = P_LEFT + tid;
+         const bool xd = d == P_LEFT || d == P_RIGHT;
+         const bool ex = d == P_RIGHT ? x + 1 < c.W : d == P_LEFT ? x >= 1 : d == P_UP ? y + 1 < c.H : y >= 1;
+         const uint32_t ch = xd ? 2 * y + (d == P_LEFT) : 2 * x + (d == P_DOWN);
+         const uint32_t i = d == P_RIGHT ? x : d == P_LEFT ? c.W - 1 - x : d == P_UP ? y : c.H - 1 - y;
+         const ChainWin* cw = xd ? cwx : cwy;
+         uint32_t nW = 0;
+         if (ex && cw)
+         {
+            nW = cw[ch].nW;
+            s_D[tid] = cw[ch].D;
+            s_inv[tid] = 1.0 / (double) cw[ch].D;
+            s_bp[tid] = (xd ? btx : bty) + cw[ch].bt_off + (uint64_t) i * (xd ? 1u : 3u) * (nW + 1);
+         }
+         s_nW[tid] = nW;
+      }
+      __syncthreads();
+      for (uint32_t q = 0; q < 4; q++)
+         for (uint32_t v = tid; v < s_nW[q]; v += IJ_T) s_bt[q][v] = 0xFFFFFFFFu;
+   }
    // the port starts with no gap in its history tree only if its first request is at cycle 0
-   bool nogap = c.analytical && cyc_of<F1>(recs[base].t, f) == 0;
+   bool nogap = n && c.analytical && cyc_of<F1>(recs[base].t, f) == 0;
    uint64_t ssum = 0, flits = 0;
    __syncthreads();
+   // the next block's records are loaded while this one is placed (IJ_PF)
+   Rec rn[IJ_PER];
+   if (IJ_PF)
+   {
+#pragma unroll
+      for (uint32_t k = 0; k < IJ_PER; k++)
+      {
+         const uint32_t j = tid * IJ_PER + k;
+         if (j < n) rn[k] = recs[base + j];
+      }
+   }
    for (uint32_t b0 = 0; b0 < n; b0 += IJ_BLK)
    {
       const uint64_t bc = cyc_of<F1>(recs[base + b0].t, f);   // the block's first cycle (the slot is sorted)
@@ -2570,7 +2629,17 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
       {
          const uint32_t j = b0 + tid * IJ_PER + k;
          vr[k] = j < n;
-         if (vr[k]) r[k] = recs[base + j];
+         if (IJ_PF) r[k] = rn[k];
+         else if (vr[k]) r[k] = recs[base + j];
+      }
+      if (IJ_PF)
+      {
+#pragma unroll
+         for (uint32_t k = 0; k < IJ_PER; k++)
+         {
+            const uint32_t j = b0 + IJ_BLK + tid * IJ_PER + k;
+            if (j < n) rn[k] = recs[base + j];
+         }
       }
       uint32_t A = 0, B = 0, c01 = 0, c23 = 0;
       bool wide = false;
@@ -2682,6 +2751,16 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
             samp_t[gp >> 6] = o.t;
             samp_id[gp >> 6] = o.id;
          }
+         if (bnd && s_nW[d])
+         {
+            // window of the record: t / D by a double reciprocal and one correction (as k_win_bounds)
+            const uint64_t D = s_D[d];
+            uint64_t w = (uint64_t) ((double) o.t * s_inv[d]);
+            if (w * D > o.t) w--;
+            else if ((w + 1) * D <= o.t) w++;
+            const uint32_t wl = s_nW[d] - 1;
+            atomicMin(&s_bt[d][w < wl ? w : wl], pos);
+         }
       }
       __syncthreads();
       if (nogap)
@@ -2695,6 +2774,32 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
          }
          nogap = s_ev[0] == 0xFFFFFFFFu;
       }
+   }
+   if (bnd)
+   {
+      // wave q: field q's bounds, a suffix min from the last window down (64 windows a step)
+      __syncthreads();
+      const uint32_t nW = s_nW[wv];
+      if (nW)
+      {
+         uint32_t* bp = s_bp[wv];
+         uint32_t carry = oc[wv];
+         if (lane == 0) bp[nW] = carry;
+         for (int top = (int) nW - 1; top >= 0; top -= 64)
+         {
+            const int idx = top - (int) lane;
+            uint32_t v = idx >= 0 ? s_bt[wv][idx] : 0xFFFFFFFFu;
+            for (int off = 1; off < 64; off <<= 1)
+            {
+               const uint32_t u = (uint32_t) __shfl_up((int) v, off);
+               if ((int) lane >= off) v = v < u ? v : u;
+            }
+            v = v < carry ? v : carry;
+            if (idx >= 0) bp[idx] = v;
+            carry = (uint32_t) __shfl((int) v, 63);
+         }
+      }
+      if (n == 0) return;
    }
    // the port's counters (router_model.cc:136-144): contention cycles, requests, flits, last departure
    uint64_t a0 = ssum, a1 = flits;

@@ -114,6 +114,7 @@ struct gnoc_engine
    uint64_t rec_bound = 0;    // records incl. slot padding (from the trace at submit)
    uint32_t runs = 0, tot_retry = 0, tot_fallback = 0;   // since the last submit (gnoc_summary)
    bool submitted = false, ran = false;
+   int inj_bnd = 0;   // this run's k_inj_stream wrote the IN_LOCAL window bounds (unless it declined)
    const uint64_t* d_inj = nullptr;
    const uint32_t *d_src = nullptr, *d_dst = nullptr, *d_bits = nullptr, *d_flags = nullptr;
    DevBuf t_inj, t_src, t_dst, t_bits, t_flags;
@@ -2052,7 +2053,8 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1, bool cond = f
 
 // The injection level of a one-engine unicast chain / pipeline run: k_inj_stream,
 // then k_inj_undo and the k_level launch that run only if it declined.
-static int inj_level(gnoc_engine* e)
+static ChainArgs chain_args(gnoc_engine* e, int phase);
+static int inj_level(gnoc_engine* e, bool chain_bounds)
 {
    const char* v = std::getenv("GNOC_INJ_STREAM");
    if ((v && *v && std::atoi(v) == 0) || e->nb || e->nranks > 1) return run_levels_v3(e, 0, 1);
@@ -2062,11 +2064,37 @@ static int inj_level(gnoc_engine* e)
    }
    hipStream_t s = e->stream;
    const uint32_t N = e->dc.N;
+   // the chain ports' IN_LOCAL window bounds in the same pass (chain_phase's X launch
+   // then bounds only what a decline left), when every chain fits its LDS table
+   const ChainWin *cwx = nullptr, *cwy = nullptr;
+   uint32_t *btx = nullptr, *bty = nullptr;
+   e->inj_bnd = 0;
+   const char* bv = std::getenv("GNOC_INJ_BOUNDS");
+   if (chain_bounds && !(bv && *bv && std::atoi(bv) == 0) && e->ncpx && e->ry0 == 0 && e->cx0 == 0)
+   {
+      bool fit = true;
+      for (int p = 0; p < 2; p++)
+         for (const ChainWin& w : e->h_cw[p]) fit = fit && w.nW + 1 <= ch::IJ_NWB;
+      if (fit)
+      {
+         const ChainArgs ax = chain_args(e, 0);
+         cwx = ax.cw;
+         btx = const_cast<uint32_t*>(ax.bt);
+         if (e->ncpy)
+         {
+            const ChainArgs ay = chain_args(e, 1);
+            cwy = ay.cw;
+            bty = const_cast<uint32_t*>(ay.bt);
+         }
+         e->inj_bnd = 1;
+      }
+   }
 #define GNOC_INJS(F1V)                                                                                               \
    GNOC_LAUNCH(e, KC_INJ, ch::k_inj_stream<F1V>, dim3(N), dim3(ch::IJ_T), 0, s, e->dc, e->slot_cnt.as<uint32_t>(),  \
                e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(),  \
                e->port_sum.as<unsigned long long>(), e->port_cnt.as<unsigned long long>(),                          \
-               e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>(), e->counters.as<unsigned>() + 8)
+               e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>(),                        \
+               e->counters.as<unsigned>() + 8, cwx, btx, cwy, bty)
    if (e->f1) GNOC_INJS(true);
    else GNOC_INJS(false);
 #undef GNOC_INJS
@@ -2226,19 +2254,21 @@ static int chain_phase(gnoc_engine* e, int phase)
    // inserts: one-engine runs bound them beside the X lists, the Y launch then only
    // its IN_W / IN_E lists (the X phase's turns)
    const bool ylocal = e->nranks <= 1 && e->ncpy;
+   // (the IN_LOCAL lists' bounds: already written by k_inj_stream unless it declined)
+   const unsigned* icond = e->inj_bnd ? e->counters.as<unsigned>() + 8 + 7 : nullptr;
    if (phase == 0 || !e->ch_ylocal)
       GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, a.cp, nl, a.len, a.cw, e->recs.as<Rec>(),
-                  const_cast<uint32_t*>(a.bt), nl, 0u);
+                  const_cast<uint32_t*>(a.bt), nl, 0u, phase == 0 ? icond : nullptr);
    else
       GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * 2), dim3(256), 0, s, a.cp, nl, a.len, a.cw, e->recs.as<Rec>(),
-                  const_cast<uint32_t*>(a.bt), 2u, 1u);
+                  const_cast<uint32_t*>(a.bt), 2u, 1u, (const unsigned*) nullptr);
    if (phase == 0)
    {
       if (ylocal)
       {
          const ChainArgs ay = chain_args(e, 1);
          GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpy), dim3(256), 0, s, ay.cp, 3u, ay.len, ay.cw,
-                     e->recs.as<Rec>(), const_cast<uint32_t*>(ay.bt), 1u, 0u);
+                     e->recs.as<Rec>(), const_cast<uint32_t*>(ay.bt), 1u, 0u, icond);
          e->ch_ylocal = 1;
       }
    }
@@ -2331,10 +2361,11 @@ static int chain_fused(gnoc_engine* e)
    xa.x = chain_args(e, 0);
    xa.y = chain_args(e, 1);
    // X inserts (injection outputs) and the Y ports' IN_LOCAL lists: complete before the launch
+   const unsigned* icond = e->inj_bnd ? e->counters.as<unsigned>() + 8 + 7 : nullptr;
    GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpx), dim3(256), 0, s, xa.x.cp, 1u, xa.x.len, xa.x.cw,
-               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.x.bt), 1u, 0u);
+               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.x.bt), 1u, 0u, icond);
    GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpy), dim3(256), 0, s, xa.y.cp, 3u, xa.y.len, xa.y.cw,
-               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.y.bt), 1u, 0u);
+               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.y.bt), 1u, 0u, icond);
    const uint32_t nx = (uint32_t) e->h_tasks[0].size();
    xa.x.fw2 = 5u;                                  // an X decline stops the Y tasks too
    xa.y.ctr = xa.x.ctr;                            // one dequeue head
@@ -2529,6 +2560,7 @@ static int exc_merge(gnoc_engine* e)
 static int run_prep(gnoc_engine* e, bool* done)
 {
    *done = false;
+   e->inj_bnd = 0;
    if (!e->submitted) return fail(e, GNOC_ESTATE, "gnoc_run before gnoc_submit");
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    const DevCfg& c = e->dc;
@@ -2972,7 +3004,7 @@ static int run_once(gnoc_engine* e)
       e->used_v3 = 6;
       rc = run_plan_v3(e, true);
       if (!rc) rc = pipe_setup(e);
-      if (!rc) rc = inj_level(e);
+      if (!rc) rc = inj_level(e, false);
       if (!rc && e->exc_fix) rc = exc_merge(e);
       if (!rc) rc = pipe_phase(e, 0);
       if (!rc) rc = pipe_phase(e, 1);
@@ -2992,7 +3024,7 @@ static int run_once(gnoc_engine* e)
       e->ch_ylocal = 0;
       rc = run_plan_v3(e, !e->ch_ydeclined);   // (Y on k_level: its levels too)
       if (!rc) rc = chain_setup(e);
-      if (!rc) rc = inj_level(e);
+      if (!rc) rc = inj_level(e, true);
       if (!rc && e->exc_fix) rc = exc_merge(e);
       e->ch_fused = 0;
       if (!rc && chain_fusable(e)) rc = chain_fused(e);
