@@ -2823,20 +2823,296 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
       atomicMax(&port_last[port], (unsigned long long) s_X);
    }
 }
-// After k_inj_stream declined (errflag[7]): the injection ports' counters back to zero
-// for k_level's rerun of the level.
-__global__ __launch_bounds__(256) void k_inj_undo(uint32_t N, const unsigned* __restrict__ errflag,
+// After a streamed level declined (*flag: errflag[7] injection, errflag[8] SELF): its
+// ports' counters back to zero for k_level's rerun of the level.
+__global__ __launch_bounds__(256) void k_inj_undo(uint32_t N, const unsigned* __restrict__ flag, uint32_t dir,
                                                   unsigned long long* __restrict__ s0, unsigned long long* __restrict__ s1,
                                                   unsigned long long* __restrict__ s2, unsigned long long* __restrict__ s3)
 {
-   if (!errflag[7]) return;
+   if (!*flag) return;
    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
    if (t >= N) return;
-   const uint32_t p = t * PORTS + P_INJ;
+   const uint32_t p = t * PORTS + dir;
    s0[p] = 0;
    s1[p] = 0;
    s2[p] = 0;
    s3[p] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// The SELF (delivery) level streamed: one workgroup per tile merges its SELF port's
+// four input slots (from W, E, S, N; each FIFO output of one port, so strictly
+// time-ordered) block by block and serves them in (t, id) order with the tail X
+// carried -- no chunk plan, no look-back.  A block: every list's next SS_B records
+// in LDS; the threshold T = the least (SS_B+1)-th key over the lists that have one
+// takes each list's records below T (SS_B .. 4 SS_B in all, every list's share
+// inside its window); two merge-path merges (W with E, S with N) and a third merge
+// the block's order; then the max-plus scan of k_inj_stream and the receipts
+// final_ps[id] = t + wait + R + Lk + F (network_model.cc:142-150).  Declines
+// (errflag[8]) on exception tails (nexc), wide blocks or the no-gap M/G/1 branch;
+// k_inj_undo and k_level's SELF level then run.  Unicast batches only.
+// ---------------------------------------------------------------------------
+#ifndef SS_B_V
+#define SS_B_V 512
+#endif
+#ifndef SS_T_V
+#define SS_T_V 256
+#endif
+constexpr uint32_t SS_T = SS_T_V, SS_B = SS_B_V, SS_PER = 4 * SS_B / SS_T;
+static_assert(SS_B <= 512 && SS_PER <= 16, "SELF stream block");
+
+struct SsSmem
+{
+   uint64_t kt[4][SS_B];
+   uint32_t ki[4][SS_B], ka[4][SS_B];
+   uint16_t mA[2 * SS_B], mB[2 * SS_B], perm[4 * SS_B];
+};
+
+// key(a) < key(b); a code is list << 9 | index
+__device__ __forceinline__ bool ss_less(const SsSmem& m, uint32_t a, uint32_t b)
+{
+   const uint64_t ta = m.kt[a >> 9][a & 511u], tb = m.kt[b >> 9][b & 511u];
+   return ta < tb || (ta == tb && m.ki[a >> 9][a & 511u] < m.ki[b >> 9][b & 511u]);
+}
+
+// Merge path: out[0 .. na + nb) = merge of A and B (codes; keys unique), each
+// thread one contiguous run of the output from a binary search on its diagonal.
+template <class GA, class GB>
+__device__ __forceinline__ void ss_merge(const SsSmem& m, GA ga, uint32_t na, GB gb, uint32_t nb, uint16_t* __restrict__ out)
+{
+   const uint32_t n = na + nb, per = (n + SS_T - 1) / SS_T;
+   const uint32_t d0 = min(threadIdx.x * per, n), d1 = min(d0 + per, n);
+   if (d0 >= d1) return;
+   uint32_t lo = d0 > nb ? d0 - nb : 0u, hi = d0 < na ? d0 : na;
+   while (lo < hi)
+   {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (ss_less(m, ga(mid), gb(d0 - 1 - mid))) lo = mid + 1;
+      else hi = mid;
+   }
+   uint32_t i = lo, j = d0 - lo;
+   for (uint32_t k = d0; k < d1; k++)
+   {
+      const bool ta = i < na && (j >= nb || ss_less(m, ga(i), gb(j)));
+      out[k] = (uint16_t) (ta ? ga(i++) : gb(j++));
+   }
+}
+
+template <bool F1>
+__global__ __launch_bounds__(SS_T) void k_self_stream(DevCfg c, const uint32_t* __restrict__ slot_cnt,
+                                                      const uint64_t* __restrict__ slot_base, const uint32_t* __restrict__ nexc,
+                                                      const Rec* __restrict__ recs, uint64_t* __restrict__ final_ps,
+                                                      unsigned long long* __restrict__ port_sum,
+                                                      unsigned long long* __restrict__ port_cnt,
+                                                      unsigned long long* __restrict__ port_flit,
+                                                      unsigned long long* __restrict__ port_last, unsigned* __restrict__ errflag)
+{
+   __shared__ SsSmem m;
+   __shared__ uint32_t wA[SS_T / 64], wB[SS_T / 64], s_xin[SS_T / 64], s_ev[2], s_decl, s_c[4], s_p[4], s_n[4];
+   __shared__ uint64_t s_tt[4], s_X, s_base[4];
+   __shared__ uint32_t s_ti[4];
+   __shared__ unsigned long long s_sum[SS_T / 64], s_flit[SS_T / 64];
+   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+   const uint32_t tile = blockIdx.x;
+   if (tid < 4)
+   {
+      const uint32_t sl = slot_of(tile, P_SELF, IN_W + tid);   // W, E, S, N
+      s_n[tid] = slot_cnt[sl];
+      s_base[tid] = slot_base[sl];
+      s_p[tid] = 0;
+      // exception tails are out of order: the level engine merges them
+      if (nexc[sl]) atomicOr(errflag + 8, 1u);
+   }
+   if (tid == 0)
+   {
+      s_X = 0;
+      s_decl = 0;
+      if (slot_cnt[slot_of(tile, P_SELF, IN_LOCAL)]) atomicOr(errflag + 8, 1u);
+   }
+   __syncthreads();
+   const uint32_t ntot = s_n[0] + s_n[1] + s_n[2] + s_n[3];
+   // (errflag[4] / [5]: the chains or pipelines declined -- the host reruns the batch)
+   if (ntot == 0 || errflag[8] || errflag[4] || errflag[5]) return;
+   const double f = c.f;
+   const uint64_t rl = rl_of(c, tile);
+   bool nogap = c.analytical != 0, first = true;
+   uint64_t ssum = 0, flits = 0;
+   for (uint32_t done = 0; done < ntot;)
+   {
+      // 1. windows and threshold candidates
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++)
+      {
+         const uint32_t rem = s_n[q] - s_p[q], w = rem < SS_B ? rem : SS_B;
+         const Rec* src = recs + s_base[q] + s_p[q];
+         for (uint32_t j = tid; j < w; j += SS_T)
+         {
+            const Rec r = src[j];
+            m.kt[q][j] = r.t;
+            m.ki[q][j] = r.id;
+            m.ka[q][j] = r.aux;
+         }
+         if (tid == q)
+         {
+            s_tt[q] = ~0ull;
+            s_ti[q] = 0xFFFFFFFFu;
+            if (rem > SS_B)
+            {
+               const Rec r = src[SS_B];
+               s_tt[q] = r.t;
+               s_ti[q] = r.id;
+            }
+         }
+      }
+      __syncthreads();
+      // 2. each list's records below T
+      if (tid < 4)
+      {
+         uint64_t Tt = ~0ull;
+         uint32_t Ti = 0xFFFFFFFFu;
+         for (uint32_t q = 0; q < 4; q++)
+            if (s_tt[q] < Tt || (s_tt[q] == Tt && s_ti[q] < Ti))
+            {
+               Tt = s_tt[q];
+               Ti = s_ti[q];
+            }
+         const uint32_t rem = s_n[tid] - s_p[tid], w = rem < SS_B ? rem : SS_B;
+         uint32_t lo = 0, hi = w;
+         if (Tt == ~0ull && Ti == 0xFFFFFFFFu) lo = w;   // no list beyond its window: take all
+         while (lo < hi)
+         {
+            const uint32_t mid = (lo + hi) >> 1;
+            const uint64_t t = m.kt[tid][mid];
+            if (t < Tt || (t == Tt && m.ki[tid][mid] < Ti)) lo = mid + 1;
+            else hi = mid;
+         }
+         s_c[tid] = lo;
+      }
+      __syncthreads();
+      const uint32_t c0 = s_c[0], c1 = s_c[1], c2 = s_c[2], c3 = s_c[3];
+      const uint32_t M = c0 + c1 + c2 + c3;
+      if (M == 0 || M > ntot - done)
+      {
+         if (tid == 0) atomicOr(errflag + 8, 8u);   // (cannot happen: the least T list gives SS_B)
+         return;
+      }
+      // 3. merge: W with E, S with N, then the two
+      ss_merge(m, [](uint32_t i) { return i; }, c0, [](uint32_t i) { return (1u << 9) | i; }, c1, m.mA);
+      ss_merge(m, [](uint32_t i) { return (2u << 9) | i; }, c2, [](uint32_t i) { return (3u << 9) | i; }, c3, m.mB);
+      __syncthreads();
+      ss_merge(m, [&](uint32_t i) { return (uint32_t) m.mA[i]; }, c0 + c1, [&](uint32_t i) { return (uint32_t) m.mB[i]; },
+               c2 + c3, m.perm);
+      __syncthreads();
+      // 4. the block's max-plus scan (relative cycles, as k_inj_stream)
+      const uint32_t p0 = m.perm[0];
+      const uint64_t bc = cyc_of<F1>(m.kt[p0 >> 9][p0 & 511u], f);
+      if (first)
+      {
+         nogap = nogap && bc == 0;   // the port's first request at cycle 0: no gap in its history tree yet
+         first = false;
+      }
+      const uint32_t per = (M + SS_T - 1) / SS_T;
+      const uint32_t a0 = min(tid * per, M), a1 = min(a0 + per, M);
+      uint32_t A = 0, B = 0;
+      bool wide = false;
+      for (uint32_t k = a0; k < a1; k++)
+      {
+         const uint32_t cd = m.perm[k];
+         const uint64_t tc = cyc_of<F1>(m.kt[cd >> 9][cd & 511u], f) - bc;
+         wide |= tc >= (1ull << 30);
+         const uint32_t p = aux_F(m.ka[cd >> 9][cd & 511u]);
+         const uint32_t nb = B + p, nt = (uint32_t) tc + p;
+         B = nb > nt ? nb : nt;
+         A += p;
+      }
+      uint32_t iA = A, iB = B;
+      wave_scan(iA, iB);
+      if (lane == 63)
+      {
+         wA[wv] = iA;
+         wB[wv] = iB;
+      }
+      if (wide) s_decl = 1;
+      __syncthreads();
+      if (tid == 0)
+      {
+         uint64_t Xr = s_X > bc ? s_X - bc : 0;
+         if (Xr >= (1ull << 30)) s_decl = 1;
+         for (uint32_t q = 0; q < SS_T / 64; q++)
+         {
+            s_xin[q] = (uint32_t) Xr;
+            const uint64_t xa = Xr + wA[q];
+            Xr = xa > wB[q] ? xa : wB[q];
+         }
+         s_X = bc + Xr;
+         s_ev[0] = s_ev[1] = 0xFFFFFFFFu;
+         for (uint32_t q = 0; q < 4; q++) s_p[q] += s_c[q];
+      }
+      __syncthreads();
+      if (s_decl)
+      {
+         if (tid == 0) atomicOr(errflag + 8, 2u);
+         return;
+      }
+      const uint32_t exA = dpp32<0x138, 0xF, 0xF>(iA), exB = dpp32<0x138, 0xF, 0xF>(iB);   // wave_shr 1
+      const uint32_t xa = s_xin[wv] + exA;
+      uint32_t Xt = xa > exB ? xa : exB;
+      for (uint32_t k = a0; k < a1; k++)
+      {
+         const uint32_t cd = m.perm[k];
+         const uint64_t t = m.kt[cd >> 9][cd & 511u];
+         const uint32_t id = m.ki[cd >> 9][cd & 511u], p = aux_F(m.ka[cd >> 9][cd & 511u]);
+         const uint32_t tc = (uint32_t) (cyc_of<F1>(t, f) - bc);
+         if (nogap)
+         {
+            if (tc > Xt) atomicMin(&s_ev[0], k);            // the first idle cycle
+            else if (Xt > tc + p) atomicMin(&s_ev[1], k);   // the M/G/1 branch would serve it
+         }
+         const uint32_t cc = Xt > tc ? Xt - tc : 0u;
+         Xt = (Xt > tc ? Xt : tc) + p;
+         ssum += cc;
+         flits += p;
+         if (id < c.npk) final_ps[id] = t + ps_of<F1>(cc, f) + rl + ps_of<F1>(p, f);
+         else atomicOr(errflag, 1u);
+      }
+      __syncthreads();
+      if (nogap)
+      {
+         if (s_ev[1] != 0xFFFFFFFFu && s_ev[1] < s_ev[0])
+         {
+            if (tid == 0) atomicOr(errflag + 8, 4u);
+            return;
+         }
+         nogap = s_ev[0] == 0xFFFFFFFFu;
+      }
+      done += M;
+   }
+   uint64_t a0 = ssum, a1 = flits;
+   for (int off = 32; off > 0; off >>= 1)
+   {
+      a0 += __shfl_down(a0, off);
+      a1 += __shfl_down(a1, off);
+   }
+   if (lane == 0)
+   {
+      s_sum[wv] = a0;
+      s_flit[wv] = a1;
+   }
+   __syncthreads();
+   if (tid == 0)
+   {
+      const uint32_t port = tile * PORTS + P_SELF;
+      unsigned long long ts = 0, tf = 0;
+      for (uint32_t q = 0; q < SS_T / 64; q++)
+      {
+         ts += s_sum[q];
+         tf += s_flit[q];
+      }
+      atomicAdd(&port_sum[port], ts);
+      atomicAdd(&port_cnt[port], (unsigned long long) ntot);
+      atomicAdd(&port_flit[port], tf);
+      atomicMax(&port_last[port], (unsigned long long) s_X);
+   }
 }
 
 // Zero the per-port counters of ports whose direction is in dmask (a phase

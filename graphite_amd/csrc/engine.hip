@@ -88,12 +88,13 @@ struct DevBuf
 enum KernelClass
 {
    KC_CLASSIFY, KC_SRC_TOT, KC_INJ_BASE, KC_SRC_OFFS, KC_SCATTER, KC_ROW_HIST, KC_PROW, KC_SLOT_COUNTS, KC_SCAN,
-   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_BCAST, KC_CHAIN, KC_BOUNDS, KC_PIPE, KC_INJ, KC_N
+   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_BCAST, KC_CHAIN, KC_BOUNDS, KC_PIPE, KC_INJ, KC_SELF, KC_N
 };
 static const char* const kKernelNames[KC_N] = { "k_classify", "k_src_tot", "k_inj_base", "k_src_offs", "k_scatter",
                                                 "k_row_hist", "k_prow", "k_slot_counts", "k_scan_slots", "k_plan",
                                                 "k_level", "k_port_stream", "k_finalize", "k_bcast",
-                                                "k_chain", "k_win_bounds", "k_pipe", "k_inj_stream" };
+                                                "k_chain", "k_win_bounds", "k_pipe", "k_inj_stream",
+                                                "k_self_stream" };
 
 struct gnoc_engine
 {
@@ -1983,8 +1984,8 @@ static int run_plan_v3(gnoc_engine* e, bool ends_only = false)
 }
 
 // Levels [l0, l1) of the plan built by run_plan_v3 (cond: each launch runs only if the
-// streamed injection level declined, errflag[7]).
-static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1, bool cond = false)
+// streamed level declined, 1: injection, errflag[7]; 2: SELF, errflag[8]).
+static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1, int cond = 0)
 {
    const DevCfg& c = e->dc;
    hipStream_t s = e->stream;
@@ -2016,7 +2017,7 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1, bool cond = f
    const bool xl = xlv && *xlv == '1' && e->nranks == 1 && !e->nb && e->f1;
    uint64_t* stp = stamps ? e->stamps.as<uint64_t>() : nullptr;
 #define GNOC_LEVEL_ARGS(lvl)                                                                                         \
-   c, (lvl) | (cond ? 0x80000000u : 0u), e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
+   c, (lvl) | (cond == 1 ? 0x80000000u : cond == 2 ? 0x40000000u : 0u), e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
       e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(), e->nexc.as<uint32_t>(),                 \
       e->st.as<uint64_t>(), fin_out(e), e->port_sum.as<unsigned long long>(),                                          \
       e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),                                     \
@@ -2099,10 +2100,40 @@ static int inj_level(gnoc_engine* e, bool chain_bounds)
    else GNOC_INJS(false);
 #undef GNOC_INJS
    GNOC_LAUNCH(e, KC_INJ, ch::k_inj_undo, dim3((N + 255) / 256), dim3(256), 0, s, N,
-               (const unsigned*) (e->counters.as<unsigned>() + 8), e->port_sum.as<unsigned long long>(),
+               (const unsigned*) (e->counters.as<unsigned>() + 8 + 7), (uint32_t) P_INJ, e->port_sum.as<unsigned long long>(),
                e->port_cnt.as<unsigned long long>(), e->port_flit.as<unsigned long long>(),
                e->port_last.as<unsigned long long>());
-   return run_levels_v3(e, 0, 1, true);
+   return run_levels_v3(e, 0, 1, 1);
+}
+
+// The SELF level.  Default: k_level's chunks.  GNOC_SELF_STREAM=1: streamed per tile
+// (k_self_stream), k_level's SELF level behind it running only if it declined
+// (errflag[8]) -- exact, but measured slower on configs[1] (0.32 ms against 0.24:
+// ten serial merge blocks per tile), so opt-in.
+static int self_level(gnoc_engine* e)
+{
+   const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
+   const char* v = std::getenv("GNOC_SELF_STREAM");
+   if (!(v && *v && std::atoi(v) == 1) || e->nb || e->nranks > 1) return run_levels_v3(e, L - 1, L);
+   {
+      const int zr = zq_flush(e, e->stream);
+      if (zr) return zr;
+   }
+   hipStream_t s = e->stream;
+   const uint32_t N = e->dc.N;
+#define GNOC_SELFS(F1V)                                                                                              \
+   GNOC_LAUNCH(e, KC_SELF, ch::k_self_stream<F1V>, dim3(N), dim3(ch::SS_T), 0, s, e->dc, e->slot_cnt.as<uint32_t>(), \
+               e->slot_base.as<uint64_t>(), e->nexc.as<uint32_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),     \
+               e->port_sum.as<unsigned long long>(), e->port_cnt.as<unsigned long long>(),                          \
+               e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>(), e->counters.as<unsigned>() + 8)
+   if (e->f1) GNOC_SELFS(true);
+   else GNOC_SELFS(false);
+#undef GNOC_SELFS
+   GNOC_LAUNCH(e, KC_SELF, ch::k_inj_undo, dim3((N + 255) / 256), dim3(256), 0, s, N,
+               (const unsigned*) (e->counters.as<unsigned>() + 8 + 8), (uint32_t) P_SELF, e->port_sum.as<unsigned long long>(),
+               e->port_cnt.as<unsigned long long>(), e->port_flit.as<unsigned long long>(),
+               e->port_last.as<unsigned long long>());
+   return run_levels_v3(e, L - 1, L, 2);
 }
 
 constexpr int GNOC_V3_RETRY = 1000;
@@ -2594,7 +2625,7 @@ static int run_prep(gnoc_engine* e, bool* done)
    GNOC_HIP(e, e->tot.ensure((size_t) N * 4));
    GNOC_HIP(e, e->slot_cnt.ensure((size_t) nslots * 4));
    GNOC_HIP(e, e->slot_base.ensure(((size_t) nslots + 1) * 8));
-   GNOC_HIP(e, e->counters.ensure(64));
+   GNOC_HIP(e, e->counters.ensure(128));
    GNOC_HIP(e, e->gtot.ensure(16));
    GNOC_HIP(e, e->recs.ensure(e->rec_bound * sizeof(Rec)));
    // the slot layout's bound (k_scan_slots empties the mesh slots past it);
@@ -2649,7 +2680,7 @@ static int run_prep(gnoc_engine* e, bool* done)
          mx = std::max(mx, bytes / 4);
          ns++;
       };
-      seg(e->counters.p, 64);
+      seg(e->counters.p, 128);
       seg(e->slot_cnt.p, (uint64_t) nslots * 4);
       seg(e->nexc.p, (uint64_t) nslots * 4);
       seg(e->port_sum.p, nports * 8);
@@ -2999,7 +3030,6 @@ static int run_once(gnoc_engine* e)
    if (v3 && chain_usable(e) && pipe_usable(e))
    {
       // v6: INJ level, X pipelines, Y pipelines, SELF level
-      const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
       e->used_pipe = 1;
       e->used_v3 = 6;
       rc = run_plan_v3(e, true);
@@ -3012,7 +3042,7 @@ static int run_once(gnoc_engine* e)
          GNOC_LAUNCH(e, KC_PIPE, pp::k_pipe_samples, dim3(e->dc.N * INS), dim3(256), 0, e->stream, e->dc.N,
                      e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(),
                      e->samp_id.as<uint32_t>());
-      if (!rc) rc = run_levels_v3(e, L - 1, L);
+      if (!rc) rc = self_level(e);
    }
    else if (v3 && chain_usable(e))
    {
@@ -3049,7 +3079,7 @@ static int run_once(gnoc_engine* e)
          return GNOC_OK;
       }
       // Y phase on the chains, or (this batch's Y chains declined before) on levels
-      if (!rc) rc = run_levels_v3(e, e->ch_ydeclined ? e->lvl_y0 : L - 1, L);
+      if (!rc) rc = e->ch_ydeclined ? run_levels_v3(e, e->lvl_y0, L) : self_level(e);
       if (e->ch_ydeclined) e->used_v3 = 5;
    }
    else if (v3)
@@ -3120,13 +3150,13 @@ static int run_ma_tb(gnoc_engine* e, uint32_t tb, bool* wider)
    GNOC_HIP(e, e->ma_m.ensure(64));
    GNOC_HIP(e, e->ma_bcnt.ensure(((size_t) nbk + 1) * 4));
    GNOC_HIP(e, e->ma_hist.ensure(((size_t) RS_BINS * nbk + RS_BINS) * 4));
-   GNOC_HIP(e, e->counters.ensure(64));
+   GNOC_HIP(e, e->counters.ensure(128));
    for (DevBuf* b : { &e->port_sum, &e->port_cnt, &e->port_mg1, &e->port_flit, &e->port_last })
    {
       GNOC_HIP(e, b->ensure(nports * 8));
       GNOC_HIP(e, hipMemsetAsync(b->p, 0, nports * 8, s));
    }
-   GNOC_HIP(e, hipMemsetAsync(e->counters.p, 0, 64, s));
+   GNOC_HIP(e, hipMemsetAsync(e->counters.p, 0, 128, s));
    GNOC_HIP(e, hipEventRecord(e->ev0, s));
    const uint32_t grid = (uint32_t) std::max<size_t>(1, std::min<size_t>((n + 255) / 256, 8192));
    unsigned* err = e->counters.as<unsigned>() + 8;

@@ -1272,10 +1272,11 @@ __global__ __launch_bounds__(LV_T, LV_MIN_WAVES) void k_level(DevCfg c, uint32_t
 {
    __shared__ LvSmem sm;
    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-   // bit 31: the level runs only if the streamed injection level declined (chain.hip
-   // k_inj_stream, errflag[7])
+   // bit 31 / 30: the level runs only if the streamed injection / SELF level declined
+   // (chain.hip k_inj_stream, errflag[7]; k_self_stream, errflag[8])
    if ((level >> 31) && errflag[7] == 0) return;
-   level &= 0x7FFFFFFFu;
+   if (((level >> 30) & 1u) && errflag[8] == 0) return;
+   level &= 0x3FFFFFFFu;
    // per-level launch: chunks of `level`; cross-level launch (XL, level = number of levels): all chunks
    const uint32_t cb0 = XL ? 0u : lvl_cbase[level];
    const uint32_t nch = XL ? lvl_cbase[level] : lvl_cbase[level + 1] - cb0;
