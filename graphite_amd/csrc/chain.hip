@@ -2543,8 +2543,12 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
                                                      unsigned long long* __restrict__ port_flit,
                                                      unsigned long long* __restrict__ port_last, unsigned* __restrict__ errflag,
                                                      const ChainWin* __restrict__ cwx, uint32_t* __restrict__ btx,
-                                                     const ChainWin* __restrict__ cwy, uint32_t* __restrict__ bty)
+                                                     const ChainWin* __restrict__ cwy, uint32_t* __restrict__ bty,
+                                                     uint32_t stop)
 {
+   // stop (the chain path, nothing queued behind): a decline also flags the X chains
+   // (errflag[4]) so that every later kernel of the run returns at once
+   const unsigned dfl = stop ? F_FALLBACK : 0u;
    __shared__ uint32_t wA[4], wB[4], wc01[4], wc23[4];
    __shared__ uint32_t s_xin[4], s_fb[4][4], s_run[4], s_ev[2], s_decl;
    __shared__ uint64_t s_X;
@@ -2694,7 +2698,11 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
       __syncthreads();
       if (s_decl)
       {
-         if (tid == 0) atomicOr(errflag + 7, 1u);
+         if (tid == 0)
+         {
+            atomicOr(errflag + 7, 1u);
+            if (dfl) atomicOr(errflag + 4, dfl);
+         }
          return;
       }
       // the tail ahead of this thread: its wave's entry composed with the lanes before it
@@ -2769,7 +2777,11 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
          // an idle cycle ends the prefix for good (queue_model_history_tree.cc:79-86)
          if (s_ev[1] != 0xFFFFFFFFu && s_ev[1] < s_ev[0])
          {
-            if (tid == 0) atomicOr(errflag + 7, 2u);
+            if (tid == 0)
+            {
+               atomicOr(errflag + 7, 2u);
+               if (dfl) atomicOr(errflag + 4, dfl);
+            }
             return;
          }
          nogap = s_ev[0] == 0xFFFFFFFFu;

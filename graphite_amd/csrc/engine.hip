@@ -116,6 +116,8 @@ struct gnoc_engine
    uint32_t runs = 0, tot_retry = 0, tot_fallback = 0;   // since the last submit (gnoc_summary)
    bool submitted = false, ran = false;
    int inj_bnd = 0;   // this run's k_inj_stream wrote the IN_LOCAL window bounds (unless it declined)
+   int inj_host = 0;       // this run's k_inj_stream has no k_level behind it: a decline reruns the batch
+   int inj_declined = 0;   // this batch's injection queues fire M/G/1 (or span wide blocks): k_level's level
    const uint64_t* d_inj = nullptr;
    const uint32_t *d_src = nullptr, *d_dst = nullptr, *d_bits = nullptr, *d_flags = nullptr;
    DevBuf t_inj, t_src, t_dst, t_bits, t_flags;
@@ -716,6 +718,7 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
    e->ch_mg = 0;
    e->mgk_ok = 0;
    e->pipe_declined = 0;
+   e->inj_declined = 0;
    if (same) return;
    const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size (2^shift ps)
    const char* pv = std::getenv("GNOC_WINDOW_PS");      // test knob: force the window size (ps)
@@ -2055,10 +2058,17 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1, int cond = 0)
 // The injection level of a one-engine unicast chain / pipeline run: k_inj_stream,
 // then k_inj_undo and the k_level launch that run only if it declined.
 static ChainArgs chain_args(gnoc_engine* e, int phase);
+// chain_bounds (the chain path): the stream also writes the chain ports' IN_LOCAL
+// window bounds, and nothing is queued behind it -- a decline flags the X chains
+// (errflag[4], so every later kernel of the run returns at once) and the host
+// reruns the batch with the injection level on k_level (inj_declined).  Otherwise
+// (pipe path) k_inj_undo and k_level's injection level are queued behind it and run
+// only if it declined.
 static int inj_level(gnoc_engine* e, bool chain_bounds)
 {
    const char* v = std::getenv("GNOC_INJ_STREAM");
-   if ((v && *v && std::atoi(v) == 0) || e->nb || e->nranks > 1) return run_levels_v3(e, 0, 1);
+   if ((v && *v && std::atoi(v) == 0) || e->nb || e->nranks > 1 || (chain_bounds && e->inj_declined))
+      return run_levels_v3(e, 0, 1);
    {
       const int zr = zq_flush(e, e->stream);
       if (zr) return zr;
@@ -2095,10 +2105,15 @@ static int inj_level(gnoc_engine* e, bool chain_bounds)
                e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(),  \
                e->port_sum.as<unsigned long long>(), e->port_cnt.as<unsigned long long>(),                          \
                e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>(),                        \
-               e->counters.as<unsigned>() + 8, cwx, btx, cwy, bty)
+               e->counters.as<unsigned>() + 8, cwx, btx, cwy, bty, (uint32_t) chain_bounds)
    if (e->f1) GNOC_INJS(true);
    else GNOC_INJS(false);
 #undef GNOC_INJS
+   if (chain_bounds)
+   {
+      e->inj_host = 1;
+      return GNOC_OK;
+   }
    GNOC_LAUNCH(e, KC_INJ, ch::k_inj_undo, dim3((N + 255) / 256), dim3(256), 0, s, N,
                (const unsigned*) (e->counters.as<unsigned>() + 8 + 7), (uint32_t) P_INJ, e->port_sum.as<unsigned long long>(),
                e->port_cnt.as<unsigned long long>(), e->port_flit.as<unsigned long long>(),
@@ -2141,6 +2156,7 @@ constexpr int GNOC_CH_RETRY = 1001;      // a chain window overflowed LDS: small
 constexpr int GNOC_CH_FALLBACK = 1002;   // the chain engine cannot take this batch: level engine
 constexpr int GNOC_CH_EXC = 1003;        // only the injection level's exception tails: merge them, rerun
 constexpr int GNOC_CH_YFALL = 1004;      // only the Y chains declined: Y and SELF levels on k_level
+constexpr int GNOC_INJ_DECLINE = 1007;   // the streamed injection level declined: rerun with it on k_level
 constexpr int GNOC_CH_MG = 1005;         // the chains met the M/G/1 branch: rerun on the MG instantiation
 constexpr int GNOC_PIPE_DECLINE = 1006;  // the port pipelines cannot take this batch: rerun on the chains
 
@@ -2285,12 +2301,14 @@ static int chain_phase(gnoc_engine* e, int phase)
    // inserts: one-engine runs bound them beside the X lists, the Y launch then only
    // its IN_W / IN_E lists (the X phase's turns)
    const bool ylocal = e->nranks <= 1 && e->ncpy;
-   // (the IN_LOCAL lists' bounds: already written by k_inj_stream unless it declined)
-   const unsigned* icond = e->inj_bnd ? e->counters.as<unsigned>() + 8 + 7 : nullptr;
-   if (phase == 0 || !e->ch_ylocal)
+   // (the IN_LOCAL lists' bounds: already written by k_inj_stream, whose decline
+   // stops the run; on the pipe path's conditional stream only if it declined)
+   const bool ibnd = e->inj_bnd && e->inj_host;
+   const unsigned* icond = e->inj_bnd && !e->inj_host ? e->counters.as<unsigned>() + 8 + 7 : nullptr;
+   if ((phase == 0 && !ibnd) || (phase == 1 && !e->ch_ylocal))
       GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, a.cp, nl, a.len, a.cw, e->recs.as<Rec>(),
                   const_cast<uint32_t*>(a.bt), nl, 0u, phase == 0 ? icond : nullptr);
-   else
+   else if (phase == 1)
       GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * 2), dim3(256), 0, s, a.cp, nl, a.len, a.cw, e->recs.as<Rec>(),
                   const_cast<uint32_t*>(a.bt), 2u, 1u, (const unsigned*) nullptr);
    if (phase == 0)
@@ -2298,8 +2316,9 @@ static int chain_phase(gnoc_engine* e, int phase)
       if (ylocal)
       {
          const ChainArgs ay = chain_args(e, 1);
-         GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpy), dim3(256), 0, s, ay.cp, 3u, ay.len, ay.cw,
-                     e->recs.as<Rec>(), const_cast<uint32_t*>(ay.bt), 1u, 0u, icond);
+         if (!ibnd)
+            GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpy), dim3(256), 0, s, ay.cp, 3u, ay.len, ay.cw,
+                        e->recs.as<Rec>(), const_cast<uint32_t*>(ay.bt), 1u, 0u, icond);
          e->ch_ylocal = 1;
       }
    }
@@ -2392,11 +2411,13 @@ static int chain_fused(gnoc_engine* e)
    xa.x = chain_args(e, 0);
    xa.y = chain_args(e, 1);
    // X inserts (injection outputs) and the Y ports' IN_LOCAL lists: complete before the launch
-   const unsigned* icond = e->inj_bnd ? e->counters.as<unsigned>() + 8 + 7 : nullptr;
-   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpx), dim3(256), 0, s, xa.x.cp, 1u, xa.x.len, xa.x.cw,
-               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.x.bt), 1u, 0u, icond);
-   GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpy), dim3(256), 0, s, xa.y.cp, 3u, xa.y.len, xa.y.cw,
-               e->recs.as<Rec>(), const_cast<uint32_t*>(xa.y.bt), 1u, 0u, icond);
+   if (!(e->inj_bnd && e->inj_host))
+   {
+      GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpx), dim3(256), 0, s, xa.x.cp, 1u, xa.x.len, xa.x.cw,
+                  e->recs.as<Rec>(), const_cast<uint32_t*>(xa.x.bt), 1u, 0u, (const unsigned*) nullptr);
+      GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpy), dim3(256), 0, s, xa.y.cp, 3u, xa.y.len, xa.y.cw,
+                  e->recs.as<Rec>(), const_cast<uint32_t*>(xa.y.bt), 1u, 0u, (const unsigned*) nullptr);
+   }
    const uint32_t nx = (uint32_t) e->h_tasks[0].size();
    xa.x.fw2 = 5u;                                  // an X decline stops the Y tasks too
    xa.y.ctr = xa.x.ctr;                            // one dequeue head
@@ -2592,6 +2613,7 @@ static int run_prep(gnoc_engine* e, bool* done)
 {
    *done = false;
    e->inj_bnd = 0;
+   e->inj_host = 0;
    if (!e->submitted) return fail(e, GNOC_ESTATE, "gnoc_run before gnoc_submit");
    GNOC_HIP(e, hipSetDevice(e->cfg.device));
    const DevCfg& c = e->dc;
@@ -2900,6 +2922,8 @@ static int run_post_check(gnoc_engine* e, bool closed_form)
    e->h_records = e->h_counters[0] + e->h_counters[1] + e->h_pinned[2];
    if (e->h_pinned[3] > e->layout_bound) return fail(e, GNOC_EHIP, "internal: slot layout exceeds the record bound");
    const unsigned* ef = (const unsigned*) (e->h_pinned + 8);
+   // the streamed injection level declined and stopped the run (inj_level)
+   if (e->inj_host && ef[7]) return GNOC_INJ_DECLINE;
    const unsigned errf = ef[0];
    const unsigned cf = ef[4] | ef[5];   // the X phase's and the Y phase's chain flags
    if (e->used_pipe)
@@ -3062,7 +3086,8 @@ static int run_once(gnoc_engine* e)
       {
          if (!rc) rc = chain_phase(e, 0);
          // turns the X chains served by M/G/1 wait in exception tails: into order first
-         if (!rc && !e->ch_ydeclined && e->dc.analytical) rc = exc_merge(e);
+         // (only the MG instantiation, mg_emit, writes exception tails)
+         if (!rc && !e->ch_ydeclined && e->dc.analytical && e->ch_mg) rc = exc_merge(e);
          if (!rc && !e->ch_ydeclined) rc = chain_phase(e, 1);
       }
       const char* xv = std::getenv("GNOC_CHAIN_EXPERIMENT");
@@ -3405,6 +3430,12 @@ static int run_impl(gnoc_engine* e)
          if (rc == GNOC_CH_MG)
          {
             e->ch_mg = 1;
+            e->n_retry++;
+            continue;
+         }
+         if (rc == GNOC_INJ_DECLINE)
+         {
+            e->inj_declined = 1;
             e->n_retry++;
             continue;
          }

@@ -82,8 +82,10 @@ def star_trace(W, H, ax, ay, seed, tail=3000):
 
 @pytest.mark.parametrize("W,ax,ay", [(8, 4, 4), (16, 7, 9), (8, 2, 5)])
 def test_injection_only_mg1_runs_on_chain(W, ax, ay):
-    """M/G/1 only in one injection queue: the first run merges its exception tails and
-    reruns on the chains (one retry), later runs merge up front; bit-exact throughout."""
+    """M/G/1 only in one injection queue: the first run's streamed injection level
+    declines (the run stops, one retry with the level on k_level), that level's
+    exception tails are merged and the run reruns on the chains (a second retry);
+    later runs do both up front; bit-exact throughout."""
     cfg = gnoc.EngineConfig(num_tiles=W * W)
     tr = star_trace(W, W, ax, ay, seed=W + ax)
     ref = oracle.run(cfg, tr)
@@ -97,7 +99,7 @@ def test_injection_only_mg1_runs_on_chain(W, ax, ay):
         s = got.summary
         assert s["engine_path"] == 4, s
         assert s["fallbacks"] == 0
-        assert s["retries"] == (1 if k == 0 else 0), s
+        assert s["retries"] == (2 if k == 0 else 0), s
     eng.close()
 
 
@@ -151,8 +153,10 @@ def test_y_only_mg1_keeps_x_on_chain(W, ax, ay, k):
         paths.append(int(s["engine_path"]))
         if s["engine_path"] == 4:
             assert s["fallbacks"] == 0 and s["chain_protocol"] & 0x400, s
-            # (first run: the MG rerun, and possibly one for the windows the burst overflowed)
-            assert (1 <= s["retries"] <= 2) if r == 0 else s["retries"] == 0, s
+            # (first run: the MG rerun, and possibly one for the windows the burst overflowed
+            # and one for the streamed injection level, which declines on the burst's
+            # source queue)
+            assert (1 <= s["retries"] <= 3) if r == 0 else s["retries"] == 0, s
         else:
             assert s["engine_path"] == 5, s
             assert s["fallbacks"] == (1 if r == 0 else 0), s
