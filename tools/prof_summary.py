@@ -37,27 +37,26 @@ print("kernel                calls   avg_us   total_ms")
 for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
     print(f"{k:20s} {len(v):6d} {sum(v) / len(v) / 1e3:8.2f} {sum(v) / 1e6:10.3f}")
 
-# one step = the run of k_level launches between two k_classify launches; use the last step
+# one step = the kernels from a k_classify launch to the next k_finalize; use the
+# last complete step: its kernels, busy time, span and the gaps between launches
 steps, cur = [], None
 for r in kt:
     n = short(r["Kernel_Name"])
     if n == "k_classify":
         cur = []
-        steps.append(cur)
     if cur is not None:
         cur.append(r)
+        if n == "k_finalize":
+            steps.append(cur)
+            cur = None
 if steps:
     last = steps[-1]
-    lv = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in last if short(r["Kernel_Name"]) == "k_level"]
-    if lv:
-        dur = [e - s for s, e in lv]
-        gaps = [lv[i + 1][0] - lv[i][1] for i in range(len(lv) - 1)]
-        gaps.sort()
-        print(f"\nlast step: {len(lv)} k_level launches, busy {sum(dur) / 1e6:.3f} ms, span {(lv[-1][1] - lv[0][0]) / 1e6:.3f} ms, "
-              f"launch gaps total {sum(gaps) / 1e6:.3f} ms (median {gaps[len(gaps) // 2] / 1e3:.2f} us)")
-        print("level durations (us):", " ".join(f"{x / 1e3:.0f}" for x in dur))
-        s0, e1 = int(last[0]["Start_Timestamp"]), int(last[-1]["End_Timestamp"])
-        print(f"step span (first to last kernel) {(e1 - s0) / 1e6:.3f} ms")
+    se = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in last)
+    busy = sum(e - s for s, e, _ in se)
+    gaps = [max(0, se[i + 1][0] - se[i][1]) for i in range(len(se) - 1)]
+    print(f"\nlast step: {len(se)} kernels, busy {busy / 1e6:.3f} ms, span {(se[-1][1] - se[0][0]) / 1e6:.3f} ms, "
+          f"gaps between launches {sum(gaps) / 1e6:.3f} ms")
+    print("  " + ", ".join(f"{n} {(e - s) / 1e3:.1f}" for s, e, n in se))
 
 
 def pmc(pattern, counter, kernel):
