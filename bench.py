@@ -370,7 +370,7 @@ def chain_protocol(summ):
     if not v & 0x100:
         return None
     return {"x": "lookback" if v & 1 else "serial", "y": "lookback" if v & 2 else "serial",
-            "launch": "fused x+y" if v & 0x200 else "x, y", "mg1_serial": bool(v & 0x400),
+            "mg1_serial": bool(v & 0x400),
             "mg1_split": bool(v & 0x800)}
 
 

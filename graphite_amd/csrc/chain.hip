@@ -176,13 +176,6 @@ struct ChainArgs
    uint64_t* stamps;              // debug (GNOC_STAMPS=1): [(task * len + i) * 16 + k] phase stamps, else null
    uint32_t lookback;             // 1: look-back over earlier windows' AGG / INC; 0: wait for window w-1's INC
    uint32_t fw;                   // this phase's flag word: errflag[4] (X) or errflag[5] (Y)
-   // the fused launch (k_chain_xy: X and Y tasks in one persistent grid)
-   uint32_t fw2;                  // flags are mirrored here too (X: Y's word, so Y tasks see an X decline)
-   uint32_t nx_tasks;             // X tasks of the launch
-   uint64_t* xdone;               // [nx_tasks] epoch tag once X task (in key order) has drained its outputs
-   unsigned* xprefix;             // leading X tasks known done (advanced by the Y tasks that wait on it)
-   const ChainWin* xcw;           // Y tasks: the X phase's windows ...
-   const uint64_t* xst;           // ... and hand-off state (the producer ports' cumulative route counts)
    uint32_t* nexc;                // exception-tail counts per slot (M/G/1-served turns, mg_emit)
    unsigned long long* port_mg1;  // per-port M/G/1 requests
    unsigned* mgk;                 // [nch] 2 + the last window after which a port of the chain still had no gap
@@ -296,7 +289,6 @@ __device__ __forceinline__ uint32_t lb(const uint64_t* a, uint32_t n, uint64_t k
 __device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f)
 {
    atomicOr(a.errflag + a.fw, f);
-   if (a.fw2 != a.fw) atomicOr(a.errflag + a.fw2, f);
 }
 // A window of chain c overflowed LDS: the run retries, halving that chain's windows.
 __device__ __forceinline__ void flag_overflow(const ChainArgs& a, uint32_t c)
@@ -324,31 +316,17 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t l)
 
 // Port descriptor fields (lanes 0-31 of a "pd" register) and the port's insert
 // bounds of window w (lanes 32 + j: first record of list j, 32 + nl + j: end).
-// A Y task of the fused launch (FU) takes its IN_W / IN_E bounds from the search
-// it ran at its start (y_bounds: list 2 i + j - 1 packed lo | (hi - lo) << 24 in
-// lane L % 64 of bnd[L / 64]), the IN_LOCAL bounds from k_win_bounds.
 enum : int { PD_OBASE = 0, PD_OCAP = 4, PD_IBASE = 8, PD_ICNT = 11, PD_PORT = 14, PD_NX = 15, PD_NY = 16, PD_RL = 17,
              PD_OSLOT = 22, PD_LO = 32 };
-template <int NL, bool FU>
+template <int NL>
 __device__ __forceinline__ uint32_t load_pd(const ChainArgs& a, uint32_t cpi, uint64_t bt_off, uint32_t nW, uint32_t i,
-                                            uint32_t w, uint32_t bnd0 = 0u, uint32_t bnd1 = 0u)
+                                            uint32_t w)
 {
    const uint32_t lane = threadIdx.x;
-   uint32_t fb = 0;
-   if (FU && NL == 3)
-   {
-      // (every lane takes part in the permutes)
-      const uint32_t l = lane - 32u, j = l < 3u ? l : l - 3u;
-      const uint32_t L = 2u * i + (j ? j - 1u : 0u);
-      const uint32_t v0 = bperm(bnd0, L & 63u), v1 = bperm(bnd1, L & 63u);
-      const uint32_t v = L < 64u ? v0 : v1;
-      fb = (v & 0xFFFFFFu) + (l < 3u ? 0u : v >> 24);
-   }
    if (lane < 32) return reinterpret_cast<const uint32_t*>(a.cp + cpi)[lane];
    const uint32_t l = lane - 32;
    if (l >= 2u * NL) return 0u;
    const uint32_t j = l < (uint32_t) NL ? l : l - NL;
-   if (FU && NL == 3 && j) return fb;
    return a.bt[bt_off + ((uint64_t) i * NL + j) * (nW + 1) + w + (l < (uint32_t) NL ? 0u : 1u)];
 }
 
@@ -377,9 +355,7 @@ __device__ __forceinline__ Ins<NL> ins_lists(uint32_t pd)
    return L;
 }
 // Issue the loads of a port's inserts of this window (registers); returns their count.
-// A fused launch's Y task reads the IN_W / IN_E lists, written in this launch by X
-// tasks with write-through stores, with sc1 loads (MI355X_MICROARCH.md "Valid forms").
-template <int NL, bool FU>
+template <int NL>
 __device__ __forceinline__ uint32_t fetch_inserts(const ChainArgs& a, uint32_t pd, Rec (&iv)[IROWS])
 {
    const uint32_t lane = threadIdx.x;
@@ -398,17 +374,7 @@ __device__ __forceinline__ uint32_t fetch_inserts(const ChainArgs& a, uint32_t p
 #pragma unroll
          for (int l = 1; l < NL; l++)
             if (g >= L.off[l]) j = (uint32_t) l;
-         const uint64_t ri = (uint64_t) L.base[j] + (g - L.off[j]);
-         if (FU && NL == 3 && j)
-         {
-            const uint64_t* r = reinterpret_cast<const uint64_t*>(a.recs + ri);
-            const uint64_t t = ld1(r), ia = ld1(r + 1);
-            iv[q].t = t;
-            iv[q].id = (uint32_t) ia;
-            iv[q].aux = (uint32_t) (ia >> 32);
-         }
-         else
-            iv[q] = a.recs[ri];
+         iv[q] = a.recs[(uint64_t) L.base[j] + (g - L.off[j])];
       }
    }
    return itot;
@@ -567,6 +533,12 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 #ifndef CH_TURN16
 #define CH_TURN16 0   // 1: turns as one plain 16-B store (measured: see DESIGN.md 7)
 #endif
+#ifndef CH_TURN_PLAIN
+#define CH_TURN_PLAIN 0   // 1: turns as plain 8-B stores (written back at the launch's end), spills sc1
+#endif
+#ifndef CH_EARLY_PF
+#define CH_EARLY_PF 0     // 1: the next ports' inserts / descriptor loaded right after a step's landing
+#endif
 // A record that leaves the chain at slot position gp.  A turn is read by the next
 // launch: one plain 16-B store.  A spill is read in this launch by a later window's
 // task once the producer published a state after draining its stores: write-through
@@ -575,7 +547,13 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void out_record(gptr<Rec> recs, gptr<uint64_t> samp_t, gptr<uint32_t> samp_id, uint64_t gp,
                                            uint64_t tn, uint32_t id, uint32_t ax, bool spill)
 {
-   if (!CH_TURN16 || spill)
+   if (CH_TURN_PLAIN && !spill)
+   {
+      const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
+      q[0] = tn;
+      q[1] = (uint64_t) id | ((uint64_t) ax << 32);
+   }
+   else if (!CH_TURN16 || spill)
    {
       const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
       __hip_atomic_store(q, tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -884,119 +862,6 @@ __device__ __forceinline__ bool route_filled(const ChainArgs& a, uint32_t pd0, u
 }
 
 // ---------------------------------------------------------------------------
-// the fused launch (k_chain_xy): a Y task's dependence on the launch's X tasks
-// ---------------------------------------------------------------------------
-// Wait until the first `need` X tasks in key order (every X task whose window starts
-// before this Y window ends: only those can emit a turn record with t below its
-// end) have drained their outputs.  The waiting tasks advance the shared prefix over
-// the per-task done granules, 64 at a time.  False on abort.
-__device__ bool wait_x_prefix(const ChainArgs& a, uint32_t need, uint32_t lane)
-{
-   const uint64_t t0 = __builtin_amdgcn_s_memtime();
-   uint32_t ef = 0;
-   for (;;)
-   {
-      uint32_t P = 0;
-      if (lane == 0) P = __hip_atomic_load(a.xprefix, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      P = rdl(P, 0);
-      if (P >= need) return true;
-      uint64_t d = 0;
-      if (P + lane < a.nx_tasks) d = ld1(a.xdone + P + lane);
-      ld_flag(a, lane, ef);
-      const uint64_t m = __ballot(P + lane < a.nx_tasks && d == a.etag);
-      const uint32_t run = m == ~0ull ? 64u : (uint32_t) __builtin_ctzll(~m);
-      if (run)
-      {
-         if (lane == 0) atomicMax(a.xprefix, P + run);
-         continue;
-      }
-      if (aborted(ef)) return false;
-      if (__builtin_amdgcn_s_memtime() - t0 > SPIN_CYCLES)
-      {
-         if (lane == 0) flag(a, F_TIMEOUT);
-         return false;
-      }
-      __builtin_amdgcn_s_sleep(2);
-   }
-}
-
-// The IN_W / IN_E insert bounds of every port of Y chain c in window w ([w D, (w+1) D),
-// the last one unbounded), once wait_x_prefix has returned: list L = 2 p + j - 1 (port
-// p, side IN_W / IN_E) in lane L % 64 of bnd[L / 64], packed lo | (hi - lo) << 24.  The
-// slot's producer is an X port (RIGHT of (x-1, y) / LEFT of (x+1, y)); its cumulative
-// count K of this field after its window that holds (w+1) D - 1 is an INC granule, and
-// the slot's first K records (FIFO departures: sorted by t) are every record with
-// t < (w+1) D plus a few later ones.  lo / hi = K minus the records at the end of
-// [0, K) with t >= w D / t >= (w+1) D, counted backwards 8 loads at a time.  False
-// when a granule is missing or a bound leaves the packed range.
-__device__ bool y_bounds(const ChainArgs& a, uint32_t c, uint32_t w, uint64_t D, uint32_t nW, uint32_t& bnd0,
-                         uint32_t& bnd1)
-{
-   const uint32_t lane = threadIdx.x, len = a.len, W = a.c.W, H = a.c.H;
-   const uint32_t x = c / 2u;                  // (fused launches are unsharded: column band = all)
-   const bool up = (c & 1u) == 0u;
-   const bool lastw = w + 1 >= nW;
-   const uint64_t Tlo = (uint64_t) w * D, Thi = lastw ? ~0ull : (uint64_t) (w + 1) * D;
-   const uint64_t Tstop = w ? Tlo : Thi;       // window 0: lo = 0, the scan looks for hi only
-   const uint32_t field = up ? 2u : 3u;
-   bool bad = false;
-   uint32_t out[2] = { 0u, 0u };
-#pragma unroll
-   for (int r = 0; r < 2; r++)
-   {
-      if (64u * (uint32_t) r >= 2u * len) break;
-      const uint32_t L = lane + 64u * (uint32_t) r;
-      const uint32_t p = L >> 1, j = 1u + (L & 1u);
-      const bool act = p < len && (j == 1u ? x > 0u : x + 1u < W);
-      uint32_t K = 0, base = 0;
-      if (act)
-      {
-         const uint32_t y = up ? p : H - 1u - p;
-         const uint32_t xc = 2u * y + (j == 2u ? 1u : 0u);
-         const uint32_t xp = j == 1u ? x - 1u : W - 2u - x;
-         const ChainWin cw = a.xcw[xc];
-         uint32_t wr = cw.nW - 1u;
-         if (!lastw)
-         {
-            const uint64_t q = (Thi - 1) / cw.D;
-            if (q < wr) wr = (uint32_t) q;
-         }
-         const uint64_t g = ld1(a.xst + cw.st_off + ((uint64_t) xp * cw.nW + wr) * SW + G_CNT + field);
-         bad |= (g & ~M48) != a.etag || (g & M48) >= (1ull << 24);
-         K = (uint32_t) (g & M48);
-         base = a.cp[c * len + p].ibase[j];
-      }
-      uint32_t clo = 0, chi = 0, pos = K;
-      bool scan = act && !(w == 0 && lastw);
-      while (__any(scan))
-      {
-         uint64_t tq[8];
-#pragma unroll
-         for (int q = 0; q < 8; q++)
-            tq[q] = scan && pos > (uint32_t) q ? ld1(reinterpret_cast<const uint64_t*>(a.recs + base + pos - 1 - q)) : 0ull;
-#pragma unroll
-         for (int q = 0; q < 8; q++)
-         {
-            if (scan && pos > (uint32_t) q && tq[q] >= Tstop)
-            {
-               clo += tq[q] >= Tlo ? 1u : 0u;
-               chi += tq[q] >= Thi ? 1u : 0u;
-            }
-            else
-               scan = false;
-         }
-         pos = pos >= 8u ? pos - 8u : 0u;
-      }
-      const uint32_t lo = w ? K - clo : 0u, hi = K - chi;
-      bad |= act && lo >= (1u << 24);
-      out[r] = lo | (min(hi - lo, 255u) << 24);
-   }
-   bnd0 = out[0];
-   bnd1 = out[1];
-   return !__any(bad);
-}
-
-// ---------------------------------------------------------------------------
 // one task: chain c, window w (one wave)
 // ---------------------------------------------------------------------------
 // Phase stamps (tools/chain_stamps.py): a -DCH_STAMPS build with GNOC_STAMPS=1.
@@ -1067,8 +932,8 @@ __device__ __forceinline__ uint64_t state_word_ser(uint32_t lane, uint64_t Xo, u
    if (lane == 7) v = Pend;
    return v;
 }
-template <int NL, bool F1, bool FU, bool MG = false, bool RF = false>
-__device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk, uint32_t aux)
+template <int NL, bool F1, bool MG = false, bool RF = false>
+__device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
 {
    constexpr bool XC = NL == 1;
    const uint32_t lane = threadIdx.x;
@@ -1095,38 +960,25 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
    const uint32_t cpb = c * len;
    const uint32_t mode0 = a.c.analytical ? 1u : 0u;
    const gptr<Rec> recs = sptr(a.recs);
-   // fused launch, Y task: the X tasks it depends on are done; its IN_W / IN_E bounds
-   uint32_t bnd0 = 0, bnd1 = 0;
 #ifdef CH_STAMPS
    if (a.stamps && lane == 0) a.stamps[(uint64_t) tk * len * 16 + 10] = __builtin_amdgcn_s_memrealtime();
 #endif
-   if (FU && NL == 3)
-   {
-      if (!wait_x_prefix(a, aux, lane)) return;
-#ifdef CH_STAMPS
-      if (a.stamps && lane == 0) a.stamps[(uint64_t) tk * len * 16 + 11] = __builtin_amdgcn_s_memrealtime();
-#endif
-      if (!y_bounds(a, c, w, D, nW, bnd0, bnd1))
-      {
-         if (lane == 0) flag(a, F_FALLBACK | R_XDONE);
-         return;
-      }
-   }
 
    // ---- prologue: descriptors of ports 0..2 (with their insert bounds), port 0's
    // inserts landed, port 1's in flight
-   uint32_t pd0 = load_pd<NL, FU>(a, cpb, bt_off, nW, 0, w, bnd0, bnd1);
-   uint32_t pd1 = len > 1 ? load_pd<NL, FU>(a, cpb + 1, bt_off, nW, 1, w, bnd0, bnd1) : 0u;
-   uint32_t pd2 = len > 2 ? load_pd<NL, FU>(a, cpb + 2, bt_off, nW, 2, w, bnd0, bnd1) : 0u;
+   uint32_t pd0 = load_pd<NL>(a, cpb, bt_off, nW, 0, w);
+   uint32_t pd1 = len > 1 ? load_pd<NL>(a, cpb + 1, bt_off, nW, 1, w) : 0u;
+   uint32_t pd2 = len > 2 ? load_pd<NL>(a, cpb + 2, bt_off, nW, 2, w) : 0u;
    Rec iv[IROWS];
-   uint32_t nI = fetch_inserts<NL, FU>(a, pd0, iv);
+   uint32_t nI = fetch_inserts<NL>(a, pd0, iv);
    if (nI > (uint32_t) ICAP)
    {
       if (lane == 0) flag_overflow(a, c);
       return;
    }
    if (land_inserts<NL>(sm, iv, nI, wbase, pd0) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
-   uint32_t itot_f = len > 1 ? fetch_inserts<NL, FU>(a, pd1, iv) : 0u;   // port 1's inserts, landed in step 0
+   uint32_t itot_f = len > 1 ? fetch_inserts<NL>(a, pd1, iv) : 0u;   // port 1's inserts, landed in step 0
+   uint32_t pdn_e = 0;           // (CH_EARLY_PF) port i+3's descriptor, loaded after this step's landing
 
    uint64_t rk[ROWS];
    uint32_t ra[ROWS];
@@ -1197,6 +1049,13 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
 #pragma unroll
             for (int q = 0; q < IROWS; q++) asm volatile("" : "+v"(iv[q].t), "+v"(iv[q].id), "+v"(iv[q].aux) : "s"(totB));
             if (land_inserts<NL>(sm, iv, itot, wbase, pd1) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
+            if (CH_EARLY_PF)
+            {
+               // the insert registers are free again: port i+2's inserts and port i+3's
+               // descriptor load while this step scans and emits (the ring moves at the end)
+               if (i + 2 < len) itot_f = fetch_inserts<NL>(a, pd2, iv);
+               pdn_e = i + 3 < len ? load_pd<NL>(a, cpb + i + 3, bt_off, nW, i + 3, w) : 0u;
+            }
          }
          CH_STAMP(3);
 
@@ -1332,15 +1191,9 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
          mode_scan(rk, ra, n, Xr, cyc, fgap, ffire, sp2);
          mg = ffire != NONE && (fgap == NONE || ffire < fgap);
       }
-      if (mg && FU)
-      {
-         // the fused launch's Y tasks read the X turns in-launch: no exception tails
-         if (lane == 0) flag(a, F_FALLBACK | R_MG1);
-         return;
-      }
       MgOut mo{};
-      const bool mgr = MG && !FU && mg;   // this window went through mg_emit
-      if constexpr (MG && !FU)
+      const bool mgr = MG && mg;   // this window went through mg_emit
+      if constexpr (MG)
       {
          if (mg)
          {
@@ -1483,8 +1336,8 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
       nI = itot;
       // ---- next prefetches: port i+2's inserts (its descriptor landed a step ago), port
       // i+3's descriptor and bounds; the ring moves on
-      if (i + 2 < len) itot_f = fetch_inserts<NL, FU>(a, pd2, iv);
-      const uint32_t pdn = i + 3 < len ? load_pd<NL, FU>(a, cpb + i + 3, bt_off, nW, i + 3, w, bnd0, bnd1) : 0u;
+      if (!CH_EARLY_PF && i + 2 < len) itot_f = fetch_inserts<NL>(a, pd2, iv);
+      const uint32_t pdn = CH_EARLY_PF ? pdn_e : i + 3 < len ? load_pd<NL>(a, cpb + i + 3, bt_off, nW, i + 3, w) : 0u;
       pd0 = pd1;
       pd1 = pd2;
       pd2 = pdn;
@@ -1494,21 +1347,14 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
       atomicMax(a.nmax + 2 * c, nmax);
       atomicMax(a.nmax + 2 * c + 1, imax);
    }
-   if (FU && NL == 1)
-   {
-      // fused launch: every output of this X task has landed (write-through stores);
-      // its done granule lets the Y tasks that wait on it read them (sc1 loads)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) st1(a.xdone + aux, a.etag);
-   }
 }
 
 
 // ---------------------------------------------------------------------------
 // one task, look-back protocol (AGG / INC / KO / POST granules)
 // ---------------------------------------------------------------------------
-template <int NL, bool F1, bool FU, bool MG = false, bool RF = false>
-__device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk, uint32_t aux)
+template <int NL, bool F1, bool MG = false, bool RF = false>
+__device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c, uint32_t w, uint32_t tk)
 {
    constexpr bool XC = NL == 1;
    const uint32_t lane = threadIdx.x;
@@ -1535,38 +1381,25 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
    const uint32_t cpb = c * len;
    const uint32_t mode0 = a.c.analytical ? 1u : 0u;
    const gptr<Rec> recs = sptr(a.recs);
-   // fused launch, Y task: the X tasks it depends on are done; its IN_W / IN_E bounds
-   uint32_t bnd0 = 0, bnd1 = 0;
 #ifdef CH_STAMPS
    if (a.stamps && lane == 0) a.stamps[(uint64_t) tk * len * 16 + 10] = __builtin_amdgcn_s_memrealtime();
 #endif
-   if (FU && NL == 3)
-   {
-      if (!wait_x_prefix(a, aux, lane)) return;
-#ifdef CH_STAMPS
-      if (a.stamps && lane == 0) a.stamps[(uint64_t) tk * len * 16 + 11] = __builtin_amdgcn_s_memrealtime();
-#endif
-      if (!y_bounds(a, c, w, D, nW, bnd0, bnd1))
-      {
-         if (lane == 0) flag(a, F_FALLBACK | R_XDONE);
-         return;
-      }
-   }
 
    // ---- prologue: descriptors of ports 0..2 (with their insert bounds), port 0's
    // inserts landed, port 1's in flight
-   uint32_t pd0 = load_pd<NL, FU>(a, cpb, bt_off, nW, 0, w, bnd0, bnd1);
-   uint32_t pd1 = len > 1 ? load_pd<NL, FU>(a, cpb + 1, bt_off, nW, 1, w, bnd0, bnd1) : 0u;
-   uint32_t pd2 = len > 2 ? load_pd<NL, FU>(a, cpb + 2, bt_off, nW, 2, w, bnd0, bnd1) : 0u;
+   uint32_t pd0 = load_pd<NL>(a, cpb, bt_off, nW, 0, w);
+   uint32_t pd1 = len > 1 ? load_pd<NL>(a, cpb + 1, bt_off, nW, 1, w) : 0u;
+   uint32_t pd2 = len > 2 ? load_pd<NL>(a, cpb + 2, bt_off, nW, 2, w) : 0u;
    Rec iv[IROWS];
-   uint32_t nI = fetch_inserts<NL, FU>(a, pd0, iv);
+   uint32_t nI = fetch_inserts<NL>(a, pd0, iv);
    if (nI > (uint32_t) ICAP)
    {
       if (lane == 0) flag_overflow(a, c);
       return;
    }
    if (land_inserts<NL>(sm, iv, nI, wbase, pd0) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
-   uint32_t itot_f = len > 1 ? fetch_inserts<NL, FU>(a, pd1, iv) : 0u;   // port 1's inserts, landed in step 0
+   uint32_t itot_f = len > 1 ? fetch_inserts<NL>(a, pd1, iv) : 0u;   // port 1's inserts, landed in step 0
+   uint32_t pdn_e = 0;           // (CH_EARLY_PF) port i+3's descriptor, loaded after this step's landing
 
    uint64_t rk[ROWS];
    uint32_t ra[ROWS];
@@ -1640,6 +1473,13 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
 #pragma unroll
             for (int q = 0; q < IROWS; q++) asm volatile("" : "+v"(iv[q].t), "+v"(iv[q].id), "+v"(iv[q].aux) : "s"(totB));
             if (land_inserts<NL>(sm, iv, itot, wbase, pd1) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
+            if (CH_EARLY_PF)
+            {
+               // the insert registers are free again: port i+2's inserts and port i+3's
+               // descriptor load while this step scans and emits (the ring moves at the end)
+               if (i + 2 < len) itot_f = fetch_inserts<NL>(a, pd2, iv);
+               pdn_e = i + 3 < len ? load_pd<NL>(a, cpb + i + 3, bt_off, nW, i + 3, w) : 0u;
+            }
          }
          // ---- [D1] the predecessor window's state: its KO (or POST) for the spill range,
          // and, with the serial protocol, its INC; one poll reloads every prefetched lane
@@ -1916,15 +1756,9 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
          mode_scan(rk, ra, n, Xr, cyc, fgap, ffire, sp2);
          mg = ffire != NONE && (fgap == NONE || ffire < fgap);
       }
-      if (mg && FU)
-      {
-         // the fused launch's Y tasks read the X turns in-launch: no exception tails
-         if (lane == 0) flag(a, F_FALLBACK | R_MG1);
-         return;
-      }
       MgOut mo{};
-      const bool mgr = MG && !FU && mg;   // this window went through mg_emit
-      if constexpr (MG && !FU)
+      const bool mgr = MG && mg;   // this window went through mg_emit
+      if constexpr (MG)
       {
          if (mg)
          {
@@ -2066,8 +1900,8 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
       nI = itot;
       // ---- next prefetches: port i+2's inserts (its descriptor landed a step ago), port
       // i+3's descriptor and bounds; the ring moves on
-      if (i + 2 < len) itot_f = fetch_inserts<NL, FU>(a, pd2, iv);
-      const uint32_t pdn = i + 3 < len ? load_pd<NL, FU>(a, cpb + i + 3, bt_off, nW, i + 3, w, bnd0, bnd1) : 0u;
+      if (!CH_EARLY_PF && i + 2 < len) itot_f = fetch_inserts<NL>(a, pd2, iv);
+      const uint32_t pdn = CH_EARLY_PF ? pdn_e : i + 3 < len ? load_pd<NL>(a, cpb + i + 3, bt_off, nW, i + 3, w) : 0u;
       pd0 = pd1;
       pd1 = pd2;
       pd2 = pdn;
@@ -2076,13 +1910,6 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
    {
       atomicMax(a.nmax + 2 * c, nmax);
       atomicMax(a.nmax + 2 * c + 1, imax);
-   }
-   if (FU && NL == 1)
-   {
-      // fused launch: every output of this X task has landed (write-through stores);
-      // its done granule lets the Y tasks that wait on it read them (sc1 loads)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) st1(a.xdone + aux, a.etag);
    }
 }
 
@@ -2109,8 +1936,8 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
       tk = rdl(tk, 0);
       if (tk >= ntasks || flagged(a)) return;
       const uint32_t cw = a.tasks[tk];
-      if (LB) task_lb<NL, F1, false, MG>(sm, a, cw >> 16, cw & 0xFFFFu, tk, 0u);
-      else task_ser<NL, F1, false, MG>(sm, a, cw >> 16, cw & 0xFFFFu, tk, 0u);
+      if (LB) task_lb<NL, F1, MG>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
+      else task_ser<NL, F1, MG>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
       wsync();
    }
 }
@@ -2139,63 +1966,13 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain_mix(ChainArgs a)
       const uint32_t cw = a.tasks[tk], c = cw >> 16, w = cw & 0xFFFFu;
       if (w < a.mgk_lim[c])
       {
-         if (LB) task_lb<NL, F1, false, true>(sm, a, c, w, tk, 0u);
-         else task_ser<NL, F1, false, true>(sm, a, c, w, tk, 0u);
+         if (LB) task_lb<NL, F1, true>(sm, a, c, w, tk);
+         else task_ser<NL, F1, true>(sm, a, c, w, tk);
       }
       else
       {
-         if (LB) task_lb<NL, F1, false, false, true>(sm, a, c, w, tk, 0u);
-         else task_ser<NL, F1, false, false, true>(sm, a, c, w, tk, 0u);
-      }
-      wsync();
-   }
-}
-
-// The X and Y phases in ONE persistent launch: the Y tasks fill the slots the X
-// phase's drain leaves empty.  One table in key order: X task (c, w) at its window's
-// start w D_c, Y task (c, w) at its window's end (w+1) D_c plus a lag (GNOC_XY_LAG),
-// so every X task a Y task waits for (wait_x_prefix) and its predecessor window are
-// handed out before it (no deadlock).  taux: an X task's rank in the X tasks' key
-// order (its done granule), a Y task's count of X tasks that must be done first.  An
-// X decline (mirrored into the Y flag word) stops every task; a Y decline only the
-// Y tasks (the X outputs stand: the host reruns the Y and SELF levels, path 5).
-struct XYArgs
-{
-   ChainArgs x, y;
-   const uint32_t* tasks;         // bit 31: Y task; bits 16-30 chain; bits 0-15 window
-   const uint32_t* taux;
-   uint32_t ntasks;
-};
-template <bool F1, bool XLB, bool YLB>
-__global__ __launch_bounds__(T, CH_MINW) void k_chain_xy(XYArgs xa)
-{
-   __shared__ Smem sm;
-   const ChainArgs& ax = xa.x;
-   const ChainArgs& ay = xa.y;
-   if (ax.errflag[2] != 0 && (!ax.excfix || (ax.errflag[2] & 2u)))
-   {
-      if (threadIdx.x == 0 && blockIdx.x == 0) flag(ax, F_FALLBACK | R_EXC);
-      return;
-   }
-   for (;;)
-   {
-      uint32_t tk = 0;
-      if (threadIdx.x == 0) tk = atomicAdd(ax.ctr, 1u);
-      tk = rdl(tk, 0);
-      if (tk >= xa.ntasks) return;
-      const uint32_t e = xa.tasks[tk], aux = xa.taux[tk];
-      const uint32_t c = (e >> 16) & 0x7FFFu, w = e & 0xFFFFu;
-      if (e >> 31)
-      {
-         if (flagged(ay)) continue;   // (X flags are mirrored into Y's word)
-         if (YLB) task_lb<3, F1, true>(sm, ay, c, w, tk, aux);
-         else task_ser<3, F1, true>(sm, ay, c, w, tk, aux);
-      }
-      else
-      {
-         if (flagged(ax)) return;
-         if (XLB) task_lb<1, F1, true>(sm, ax, c, w, tk, aux);
-         else task_ser<1, F1, true>(sm, ax, c, w, tk, aux);
+         if (LB) task_lb<NL, F1, false, true>(sm, a, c, w, tk);
+         else task_ser<NL, F1, false, true>(sm, a, c, w, tk);
       }
       wsync();
    }
@@ -2515,9 +2292,9 @@ __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict_
 // positions.  Relative cycles (to the block's first cycle) keep the scan in 32
 // bits.  The no-gap M/G/1 prefix (queue_model_history_tree.cc:58-64) is not served
 // here: a port whose first arrival is at cycle 0 is checked until its first idle
-// cycle, and where the branch would fire the kernel declines (errflag[7]); the host
-// has queued k_inj_undo and k_level's injection level behind it, which then run the
-// level (they return at once otherwise).  Unicast batches of the chain path only.
+// cycle, and where the branch would fire the kernel declines (errflag[7]; it also
+// flags the X chains, so the rest of the run returns at once): the host reruns the
+// batch with k_level's injection level.  Unicast batches of the chain path only.
 // ---------------------------------------------------------------------------
 #ifndef IJ_PER_V
 #define IJ_PER_V 4
@@ -2679,6 +2456,10 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
       __syncthreads();
       if (tid == 0)
       {
+         // the block's first request finds the queue idle when the tail lies before its
+         // cycle (a gap, queue_model_history_tree.cc:79-86): the relative tail below is
+         // clamped to 0 there, so the per-record check (tc > Xt) cannot see it
+         const bool gap0 = s_X < bc;
          uint64_t Xr = s_X > bc ? s_X - bc : 0;   // an earlier tail behaves like the block's first cycle
          if (Xr >= (1ull << 30)) s_decl = 1;
          for (uint32_t q = 0; q < 4; q++)
@@ -2693,7 +2474,8 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
             }
          }
          s_X = bc + Xr;
-         s_ev[0] = s_ev[1] = 0xFFFFFFFFu;
+         s_ev[0] = gap0 ? 0u : 0xFFFFFFFFu;
+         s_ev[1] = 0xFFFFFFFFu;
       }
       __syncthreads();
       if (s_decl)
@@ -2835,298 +2617,6 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
       atomicMax(&port_last[port], (unsigned long long) s_X);
    }
 }
-// After a streamed level declined (*flag: errflag[7] injection, errflag[8] SELF): its
-// ports' counters back to zero for k_level's rerun of the level.
-__global__ __launch_bounds__(256) void k_inj_undo(uint32_t N, const unsigned* __restrict__ flag, uint32_t dir,
-                                                  unsigned long long* __restrict__ s0, unsigned long long* __restrict__ s1,
-                                                  unsigned long long* __restrict__ s2, unsigned long long* __restrict__ s3)
-{
-   if (!*flag) return;
-   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-   if (t >= N) return;
-   const uint32_t p = t * PORTS + dir;
-   s0[p] = 0;
-   s1[p] = 0;
-   s2[p] = 0;
-   s3[p] = 0;
-}
-
-// ---------------------------------------------------------------------------
-// The SELF (delivery) level streamed: one workgroup per tile merges its SELF port's
-// four input slots (from W, E, S, N; each FIFO output of one port, so strictly
-// time-ordered) block by block and serves them in (t, id) order with the tail X
-// carried -- no chunk plan, no look-back.  A block: every list's next SS_B records
-// in LDS; the threshold T = the least (SS_B+1)-th key over the lists that have one
-// takes each list's records below T (SS_B .. 4 SS_B in all, every list's share
-// inside its window); two merge-path merges (W with E, S with N) and a third merge
-// the block's order; then the max-plus scan of k_inj_stream and the receipts
-// final_ps[id] = t + wait + R + Lk + F (network_model.cc:142-150).  Declines
-// (errflag[8]) on exception tails (nexc), wide blocks or the no-gap M/G/1 branch;
-// k_inj_undo and k_level's SELF level then run.  Unicast batches only.
-// ---------------------------------------------------------------------------
-#ifndef SS_B_V
-#define SS_B_V 512
-#endif
-#ifndef SS_T_V
-#define SS_T_V 256
-#endif
-constexpr uint32_t SS_T = SS_T_V, SS_B = SS_B_V, SS_PER = 4 * SS_B / SS_T;
-static_assert(SS_B <= 512 && SS_PER <= 16, "SELF stream block");
-
-struct SsSmem
-{
-   uint64_t kt[4][SS_B];
-   uint32_t ki[4][SS_B], ka[4][SS_B];
-   uint16_t mA[2 * SS_B], mB[2 * SS_B], perm[4 * SS_B];
-};
-
-// key(a) < key(b); a code is list << 9 | index
-__device__ __forceinline__ bool ss_less(const SsSmem& m, uint32_t a, uint32_t b)
-{
-   const uint64_t ta = m.kt[a >> 9][a & 511u], tb = m.kt[b >> 9][b & 511u];
-   return ta < tb || (ta == tb && m.ki[a >> 9][a & 511u] < m.ki[b >> 9][b & 511u]);
-}
-
-// Merge path: out[0 .. na + nb) = merge of A and B (codes; keys unique), each
-// thread one contiguous run of the output from a binary search on its diagonal.
-template <class GA, class GB>
-__device__ __forceinline__ void ss_merge(const SsSmem& m, GA ga, uint32_t na, GB gb, uint32_t nb, uint16_t* __restrict__ out)
-{
-   const uint32_t n = na + nb, per = (n + SS_T - 1) / SS_T;
-   const uint32_t d0 = min(threadIdx.x * per, n), d1 = min(d0 + per, n);
-   if (d0 >= d1) return;
-   uint32_t lo = d0 > nb ? d0 - nb : 0u, hi = d0 < na ? d0 : na;
-   while (lo < hi)
-   {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (ss_less(m, ga(mid), gb(d0 - 1 - mid))) lo = mid + 1;
-      else hi = mid;
-   }
-   uint32_t i = lo, j = d0 - lo;
-   for (uint32_t k = d0; k < d1; k++)
-   {
-      const bool ta = i < na && (j >= nb || ss_less(m, ga(i), gb(j)));
-      out[k] = (uint16_t) (ta ? ga(i++) : gb(j++));
-   }
-}
-
-template <bool F1>
-__global__ __launch_bounds__(SS_T) void k_self_stream(DevCfg c, const uint32_t* __restrict__ slot_cnt,
-                                                      const uint64_t* __restrict__ slot_base, const uint32_t* __restrict__ nexc,
-                                                      const Rec* __restrict__ recs, uint64_t* __restrict__ final_ps,
-                                                      unsigned long long* __restrict__ port_sum,
-                                                      unsigned long long* __restrict__ port_cnt,
-                                                      unsigned long long* __restrict__ port_flit,
-                                                      unsigned long long* __restrict__ port_last, unsigned* __restrict__ errflag)
-{
-   __shared__ SsSmem m;
-   __shared__ uint32_t wA[SS_T / 64], wB[SS_T / 64], s_xin[SS_T / 64], s_ev[2], s_decl, s_c[4], s_p[4], s_n[4];
-   __shared__ uint64_t s_tt[4], s_X, s_base[4];
-   __shared__ uint32_t s_ti[4];
-   __shared__ unsigned long long s_sum[SS_T / 64], s_flit[SS_T / 64];
-   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
-   const uint32_t tile = blockIdx.x;
-   if (tid < 4)
-   {
-      const uint32_t sl = slot_of(tile, P_SELF, IN_W + tid);   // W, E, S, N
-      s_n[tid] = slot_cnt[sl];
-      s_base[tid] = slot_base[sl];
-      s_p[tid] = 0;
-      // exception tails are out of order: the level engine merges them
-      if (nexc[sl]) atomicOr(errflag + 8, 1u);
-   }
-   if (tid == 0)
-   {
-      s_X = 0;
-      s_decl = 0;
-      if (slot_cnt[slot_of(tile, P_SELF, IN_LOCAL)]) atomicOr(errflag + 8, 1u);
-   }
-   __syncthreads();
-   const uint32_t ntot = s_n[0] + s_n[1] + s_n[2] + s_n[3];
-   // (errflag[4] / [5]: the chains or pipelines declined -- the host reruns the batch)
-   if (ntot == 0 || errflag[8] || errflag[4] || errflag[5]) return;
-   const double f = c.f;
-   const uint64_t rl = rl_of(c, tile);
-   bool nogap = c.analytical != 0, first = true;
-   uint64_t ssum = 0, flits = 0;
-   for (uint32_t done = 0; done < ntot;)
-   {
-      // 1. windows and threshold candidates
-#pragma unroll
-      for (uint32_t q = 0; q < 4; q++)
-      {
-         const uint32_t rem = s_n[q] - s_p[q], w = rem < SS_B ? rem : SS_B;
-         const Rec* src = recs + s_base[q] + s_p[q];
-         for (uint32_t j = tid; j < w; j += SS_T)
-         {
-            const Rec r = src[j];
-            m.kt[q][j] = r.t;
-            m.ki[q][j] = r.id;
-            m.ka[q][j] = r.aux;
-         }
-         if (tid == q)
-         {
-            s_tt[q] = ~0ull;
-            s_ti[q] = 0xFFFFFFFFu;
-            if (rem > SS_B)
-            {
-               const Rec r = src[SS_B];
-               s_tt[q] = r.t;
-               s_ti[q] = r.id;
-            }
-         }
-      }
-      __syncthreads();
-      // 2. each list's records below T
-      if (tid < 4)
-      {
-         uint64_t Tt = ~0ull;
-         uint32_t Ti = 0xFFFFFFFFu;
-         for (uint32_t q = 0; q < 4; q++)
-            if (s_tt[q] < Tt || (s_tt[q] == Tt && s_ti[q] < Ti))
-            {
-               Tt = s_tt[q];
-               Ti = s_ti[q];
-            }
-         const uint32_t rem = s_n[tid] - s_p[tid], w = rem < SS_B ? rem : SS_B;
-         uint32_t lo = 0, hi = w;
-         if (Tt == ~0ull && Ti == 0xFFFFFFFFu) lo = w;   // no list beyond its window: take all
-         while (lo < hi)
-         {
-            const uint32_t mid = (lo + hi) >> 1;
-            const uint64_t t = m.kt[tid][mid];
-            if (t < Tt || (t == Tt && m.ki[tid][mid] < Ti)) lo = mid + 1;
-            else hi = mid;
-         }
-         s_c[tid] = lo;
-      }
-      __syncthreads();
-      const uint32_t c0 = s_c[0], c1 = s_c[1], c2 = s_c[2], c3 = s_c[3];
-      const uint32_t M = c0 + c1 + c2 + c3;
-      if (M == 0 || M > ntot - done)
-      {
-         if (tid == 0) atomicOr(errflag + 8, 8u);   // (cannot happen: the least T list gives SS_B)
-         return;
-      }
-      // 3. merge: W with E, S with N, then the two
-      ss_merge(m, [](uint32_t i) { return i; }, c0, [](uint32_t i) { return (1u << 9) | i; }, c1, m.mA);
-      ss_merge(m, [](uint32_t i) { return (2u << 9) | i; }, c2, [](uint32_t i) { return (3u << 9) | i; }, c3, m.mB);
-      __syncthreads();
-      ss_merge(m, [&](uint32_t i) { return (uint32_t) m.mA[i]; }, c0 + c1, [&](uint32_t i) { return (uint32_t) m.mB[i]; },
-               c2 + c3, m.perm);
-      __syncthreads();
-      // 4. the block's max-plus scan (relative cycles, as k_inj_stream)
-      const uint32_t p0 = m.perm[0];
-      const uint64_t bc = cyc_of<F1>(m.kt[p0 >> 9][p0 & 511u], f);
-      if (first)
-      {
-         nogap = nogap && bc == 0;   // the port's first request at cycle 0: no gap in its history tree yet
-         first = false;
-      }
-      const uint32_t per = (M + SS_T - 1) / SS_T;
-      const uint32_t a0 = min(tid * per, M), a1 = min(a0 + per, M);
-      uint32_t A = 0, B = 0;
-      bool wide = false;
-      for (uint32_t k = a0; k < a1; k++)
-      {
-         const uint32_t cd = m.perm[k];
-         const uint64_t tc = cyc_of<F1>(m.kt[cd >> 9][cd & 511u], f) - bc;
-         wide |= tc >= (1ull << 30);
-         const uint32_t p = aux_F(m.ka[cd >> 9][cd & 511u]);
-         const uint32_t nb = B + p, nt = (uint32_t) tc + p;
-         B = nb > nt ? nb : nt;
-         A += p;
-      }
-      uint32_t iA = A, iB = B;
-      wave_scan(iA, iB);
-      if (lane == 63)
-      {
-         wA[wv] = iA;
-         wB[wv] = iB;
-      }
-      if (wide) s_decl = 1;
-      __syncthreads();
-      if (tid == 0)
-      {
-         uint64_t Xr = s_X > bc ? s_X - bc : 0;
-         if (Xr >= (1ull << 30)) s_decl = 1;
-         for (uint32_t q = 0; q < SS_T / 64; q++)
-         {
-            s_xin[q] = (uint32_t) Xr;
-            const uint64_t xa = Xr + wA[q];
-            Xr = xa > wB[q] ? xa : wB[q];
-         }
-         s_X = bc + Xr;
-         s_ev[0] = s_ev[1] = 0xFFFFFFFFu;
-         for (uint32_t q = 0; q < 4; q++) s_p[q] += s_c[q];
-      }
-      __syncthreads();
-      if (s_decl)
-      {
-         if (tid == 0) atomicOr(errflag + 8, 2u);
-         return;
-      }
-      const uint32_t exA = dpp32<0x138, 0xF, 0xF>(iA), exB = dpp32<0x138, 0xF, 0xF>(iB);   // wave_shr 1
-      const uint32_t xa = s_xin[wv] + exA;
-      uint32_t Xt = xa > exB ? xa : exB;
-      for (uint32_t k = a0; k < a1; k++)
-      {
-         const uint32_t cd = m.perm[k];
-         const uint64_t t = m.kt[cd >> 9][cd & 511u];
-         const uint32_t id = m.ki[cd >> 9][cd & 511u], p = aux_F(m.ka[cd >> 9][cd & 511u]);
-         const uint32_t tc = (uint32_t) (cyc_of<F1>(t, f) - bc);
-         if (nogap)
-         {
-            if (tc > Xt) atomicMin(&s_ev[0], k);            // the first idle cycle
-            else if (Xt > tc + p) atomicMin(&s_ev[1], k);   // the M/G/1 branch would serve it
-         }
-         const uint32_t cc = Xt > tc ? Xt - tc : 0u;
-         Xt = (Xt > tc ? Xt : tc) + p;
-         ssum += cc;
-         flits += p;
-         if (id < c.npk) final_ps[id] = t + ps_of<F1>(cc, f) + rl + ps_of<F1>(p, f);
-         else atomicOr(errflag, 1u);
-      }
-      __syncthreads();
-      if (nogap)
-      {
-         if (s_ev[1] != 0xFFFFFFFFu && s_ev[1] < s_ev[0])
-         {
-            if (tid == 0) atomicOr(errflag + 8, 4u);
-            return;
-         }
-         nogap = s_ev[0] == 0xFFFFFFFFu;
-      }
-      done += M;
-   }
-   uint64_t a0 = ssum, a1 = flits;
-   for (int off = 32; off > 0; off >>= 1)
-   {
-      a0 += __shfl_down(a0, off);
-      a1 += __shfl_down(a1, off);
-   }
-   if (lane == 0)
-   {
-      s_sum[wv] = a0;
-      s_flit[wv] = a1;
-   }
-   __syncthreads();
-   if (tid == 0)
-   {
-      const uint32_t port = tile * PORTS + P_SELF;
-      unsigned long long ts = 0, tf = 0;
-      for (uint32_t q = 0; q < SS_T / 64; q++)
-      {
-         ts += s_sum[q];
-         tf += s_flit[q];
-      }
-      atomicAdd(&port_sum[port], ts);
-      atomicAdd(&port_cnt[port], (unsigned long long) ntot);
-      atomicAdd(&port_flit[port], tf);
-      atomicMax(&port_last[port], (unsigned long long) s_X);
-   }
-}
-
 // Zero the per-port counters of ports whose direction is in dmask (a phase
 // that reruns on the level engine after the chain engine declined it).
 __global__ __launch_bounds__(256) void k_zero_ports(uint32_t nports, uint32_t dmask, unsigned long long* __restrict__ s0,

@@ -31,7 +31,6 @@
 #include "shard.hip"
 #include "serial.hip"
 #include "chain.hip"
-#include "pipe.hip"
 
 
 namespace gnoc {
@@ -88,13 +87,12 @@ struct DevBuf
 enum KernelClass
 {
    KC_CLASSIFY, KC_SRC_TOT, KC_INJ_BASE, KC_SRC_OFFS, KC_SCATTER, KC_ROW_HIST, KC_PROW, KC_SLOT_COUNTS, KC_SCAN,
-   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_BCAST, KC_CHAIN, KC_BOUNDS, KC_PIPE, KC_INJ, KC_SELF, KC_N
+   KC_PLAN, KC_LEVEL, KC_PORT, KC_FINALIZE, KC_BCAST, KC_CHAIN, KC_BOUNDS, KC_INJ, KC_N
 };
 static const char* const kKernelNames[KC_N] = { "k_classify", "k_src_tot", "k_inj_base", "k_src_offs", "k_scatter",
                                                 "k_row_hist", "k_prow", "k_slot_counts", "k_scan_slots", "k_plan",
                                                 "k_level", "k_port_stream", "k_finalize", "k_bcast",
-                                                "k_chain", "k_win_bounds", "k_pipe", "k_inj_stream",
-                                                "k_self_stream" };
+                                                "k_chain", "k_win_bounds", "k_inj_stream" };
 
 struct gnoc_engine
 {
@@ -226,11 +224,6 @@ struct gnoc_engine
    uint64_t ch_st_words[2] = { 0, 0 }, ch_bt_words[2] = { 0, 0 };
    unsigned* h_nmax = nullptr;               // pinned: per chain fill maxima of the last run
    DevBuf ch_cw, ch_tasks, ch_nmax;
-   // the fused launch (k_chain_xy): one task table in key order (tasks, then their aux words)
-   std::vector<uint32_t> h_xy, h_xy_aux;
-   DevBuf ch_xy, ch_xdone;
-   int ch_fused = 0;                        // the last chain run was one fused launch
-   double xy_lag = -1.0;                    // Y task key lag, in units of the batch's last injection time
    uint32_t ch_epoch = 0;
    int ch_grid = 0;
    int ncu = 256;                           // compute units of the device
@@ -265,16 +258,6 @@ struct gnoc_engine
    int ch_lb_dec[2] = { -1, -1 };           // the decision per phase (-1: none yet: serial)
    int ch_trial = 0;                        // this run times a protocol (phases as separate launches)
    hipEvent_t ch_ev[2][2] = { { nullptr, nullptr }, { nullptr, nullptr } };
-
-   // v6 port pipelines (pipe.hip): one wave per chain port
-   int used_pipe = 0;
-   int pipe_declined = 0;                   // this batch fell back from the pipelines: later runs take the chains
-   uint32_t pipe_tag = 0;                   // epoch of the segment-link records (1 .. 65535)
-   const void* pipe_recs = nullptr;         // the record buffer the tags were cleared in
-   size_t pipe_recs_bytes = 0;
-   uint32_t pipe_S[2] = { 0, 0 };           // ports per segment of the last pipeline run (X, Y)
-   unsigned pipe_flags[2] = { 0, 0 };       // the last pipeline run's flag words
-   DevBuf pipe_ctr, pipe_dbg0, pipe_dbg1;
 
    // kernel profiling (gnoc_set_profiling)
    bool prof = false;
@@ -717,7 +700,6 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
    e->exc_fix = 0;
    e->ch_mg = 0;
    e->mgk_ok = 0;
-   e->pipe_declined = 0;
    e->inj_declined = 0;
    if (same) return;
    const char* fv = std::getenv("GNOC_WINDOW_SHIFT");   // test knob: force the window size (2^shift ps)
@@ -833,53 +815,6 @@ static int chain_tables(gnoc_engine* e)
       e->ch_st_words[p] = st;
       e->ch_bt_words[p] = bt;
    }
-   {
-      // the fused table: X task (c, w) keyed by its window's start w D_c, Y task (c, w) by
-      // its window's end (w+1) D_c + lag; ties: X first.  aux: an X task's rank among the
-      // X tasks (its done granule), a Y task's count of X tasks keyed before its window's
-      // end (all must be done before it reads their turn records).
-      if (e->xy_lag < 0)
-      {
-         const char* lv = std::getenv("GNOC_XY_LAG");
-         e->xy_lag = lv && *lv ? std::atof(lv) : 0.1;
-      }
-      const uint64_t lag = (uint64_t) (e->xy_lag * (double) (e->h_tlast + 1));
-      std::vector<uint64_t> xkey;
-      xkey.reserve(e->h_tasks[0].size());
-      for (uint32_t t : e->h_tasks[0]) xkey.push_back((uint64_t) (t & 0xFFFFu) * e->h_cw[0][t >> 16].D);
-      std::vector<std::pair<uint64_t, uint32_t>> yk;
-      yk.reserve(e->h_tasks[1].size());
-      for (uint32_t t : e->h_tasks[1])
-      {
-         const ChainWin& w = e->h_cw[1][t >> 16];
-         const uint32_t wi = t & 0xFFFFu;
-         yk.push_back({ (uint64_t) (wi + 1) * w.D + lag, t });
-      }
-      std::stable_sort(yk.begin(), yk.end(), [](const std::pair<uint64_t, uint32_t>& x, const std::pair<uint64_t, uint32_t>& y) {
-         return x.first < y.first;
-      });
-      e->h_xy.clear();
-      e->h_xy_aux.clear();
-      size_t ix = 0;
-      for (size_t iy = 0; iy <= yk.size(); iy++)
-      {
-         const uint64_t ky = iy < yk.size() ? yk[iy].first : ~0ull;
-         for (; ix < xkey.size() && xkey[ix] <= ky; ix++)
-         {
-            e->h_xy.push_back(e->h_tasks[0][ix]);
-            e->h_xy_aux.push_back((uint32_t) ix);
-         }
-         if (iy == yk.size()) break;
-         const uint32_t t = yk[iy].second;
-         const ChainWin& w = e->h_cw[1][t >> 16];
-         const uint32_t wi = t & 0xFFFFu;
-         uint32_t need = (uint32_t) xkey.size();
-         if (wi + 1 < w.nW)
-            need = (uint32_t) (std::lower_bound(xkey.begin(), xkey.end(), (uint64_t) (wi + 1) * w.D) - xkey.begin());
-         e->h_xy.push_back(t | 0x80000000u);
-         e->h_xy_aux.push_back(need);
-      }
-   }
    const size_t ncw = e->h_cw[0].size() + e->h_cw[1].size(), nt = e->h_tasks[0].size() + e->h_tasks[1].size();
    GNOC_HIP(e, e->ch_cw.ensure(std::max<size_t>(ncw, 1) * sizeof(ChainWin)));
    GNOC_HIP(e, e->ch_tasks.ensure(std::max<size_t>(nt, 1) * 4));
@@ -888,10 +823,6 @@ static int chain_tables(gnoc_engine* e)
                          hipMemcpyHostToDevice));
    GNOC_HIP(e, hipMemcpy(e->ch_tasks.p, e->h_tasks[0].data(), e->h_tasks[0].size() * 4, hipMemcpyHostToDevice));
    GNOC_HIP(e, hipMemcpy(e->ch_tasks.as<uint32_t>() + e->h_tasks[0].size(), e->h_tasks[1].data(), e->h_tasks[1].size() * 4,
-                         hipMemcpyHostToDevice));
-   GNOC_HIP(e, e->ch_xy.ensure(std::max<size_t>(e->h_xy.size(), 1) * 8));
-   GNOC_HIP(e, hipMemcpy(e->ch_xy.p, e->h_xy.data(), e->h_xy.size() * 4, hipMemcpyHostToDevice));
-   GNOC_HIP(e, hipMemcpy(e->ch_xy.as<uint32_t>() + e->h_xy.size(), e->h_xy_aux.data(), e->h_xy_aux.size() * 4,
                          hipMemcpyHostToDevice));
    e->chD_up[0] = e->chD_run[0];
    e->chD_up[1] = e->chD_run[1];
@@ -2012,12 +1943,8 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1, int cond = 0)
       const int zr = zq_flush(e, s);
       if (zr) return zr;
    }
-   // default: one launch per level (the launch boundary is the level barrier).
-   // GNOC_XLEVEL=1: one persistent launch over every level with port-level
-   // release/acquire hand-offs -- exact, but a consumer still waits for whole
-   // producer ports and every chunk pays an L2 write-back: 2.8x slower on 32x32.
-   const char* xlv = std::getenv("GNOC_XLEVEL");
-   const bool xl = xlv && *xlv == '1' && e->nranks == 1 && !e->nb && e->f1;
+   // one launch per level (the launch boundary is the level barrier; a persistent
+   // cross-level launch with port-level hand-offs was exact but 2.8x slower on 32x32)
    uint64_t* stp = stamps ? e->stamps.as<uint64_t>() : nullptr;
 #define GNOC_LEVEL_ARGS(lvl)                                                                                         \
    c, (lvl) | (cond == 1 ? 0x80000000u : cond == 2 ? 0x40000000u : 0u), e->lvl_cbase.as<uint32_t>(), e->lvl_qb.as<uint32_t>(), e->lvl_ctr.as<unsigned>(), e->cdesc.as<PortIO3>(), \
@@ -2026,12 +1953,6 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1, int cond = 0)
       e->port_cnt.as<unsigned long long>(), e->port_mg1.as<unsigned long long>(),                                     \
       e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>(), e->counters.as<unsigned>() + 8,   \
       e->done.as<uint32_t>(), stp
-   if (xl && l0 == 0)
-   {
-      if (stamps) GNOC_LAUNCH(e, KC_LEVEL, (k_level<true, true, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(L));
-      else GNOC_LAUNCH(e, KC_LEVEL, (k_level<false, true, false>), dim3(e->level_grid), dim3(LV_T), 0, s, GNOC_LEVEL_ARGS(L));
-   }
-   else
    {
       for (uint32_t l = l0; l < l1 && l < L; l++)
       {
@@ -2055,19 +1976,17 @@ static int run_levels_v3(gnoc_engine* e, uint32_t l0, uint32_t l1, int cond = 0)
    return GNOC_OK;
 }
 
-// The injection level of a one-engine unicast chain / pipeline run: k_inj_stream,
-// then k_inj_undo and the k_level launch that run only if it declined.
+// The injection level of a one-engine unicast chain run: k_inj_stream.  The stream
+// also writes the chain ports' IN_LOCAL window bounds, and nothing is queued behind
+// it -- a decline flags the X chains (errflag[4], so every later kernel of the run
+// returns at once) and the host reruns the batch with the injection level on k_level
+// (inj_declined).
 static ChainArgs chain_args(gnoc_engine* e, int phase);
-// chain_bounds (the chain path): the stream also writes the chain ports' IN_LOCAL
-// window bounds, and nothing is queued behind it -- a decline flags the X chains
-// (errflag[4], so every later kernel of the run returns at once) and the host
-// reruns the batch with the injection level on k_level (inj_declined).  Otherwise
-// (pipe path) k_inj_undo and k_level's injection level are queued behind it and run
-// only if it declined.
-static int inj_level(gnoc_engine* e, bool chain_bounds)
+static int inj_level(gnoc_engine* e)
 {
+   const bool chain_bounds = true;
    const char* v = std::getenv("GNOC_INJ_STREAM");
-   if ((v && *v && std::atoi(v) == 0) || e->nb || e->nranks > 1 || (chain_bounds && e->inj_declined))
+   if ((v && *v && std::atoi(v) == 0) || e->nb || e->nranks > 1 || e->inj_declined)
       return run_levels_v3(e, 0, 1);
    {
       const int zr = zq_flush(e, e->stream);
@@ -2109,46 +2028,15 @@ static int inj_level(gnoc_engine* e, bool chain_bounds)
    if (e->f1) GNOC_INJS(true);
    else GNOC_INJS(false);
 #undef GNOC_INJS
-   if (chain_bounds)
-   {
-      e->inj_host = 1;
-      return GNOC_OK;
-   }
-   GNOC_LAUNCH(e, KC_INJ, ch::k_inj_undo, dim3((N + 255) / 256), dim3(256), 0, s, N,
-               (const unsigned*) (e->counters.as<unsigned>() + 8 + 7), (uint32_t) P_INJ, e->port_sum.as<unsigned long long>(),
-               e->port_cnt.as<unsigned long long>(), e->port_flit.as<unsigned long long>(),
-               e->port_last.as<unsigned long long>());
-   return run_levels_v3(e, 0, 1, 1);
+   e->inj_host = 1;
+   return GNOC_OK;
 }
 
-// The SELF level.  Default: k_level's chunks.  GNOC_SELF_STREAM=1: streamed per tile
-// (k_self_stream), k_level's SELF level behind it running only if it declined
-// (errflag[8]) -- exact, but measured slower on configs[1] (0.32 ms against 0.24:
-// ten serial merge blocks per tile), so opt-in.
+// The SELF level, on k_level's chunks.
 static int self_level(gnoc_engine* e)
 {
    const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
-   const char* v = std::getenv("GNOC_SELF_STREAM");
-   if (!(v && *v && std::atoi(v) == 1) || e->nb || e->nranks > 1) return run_levels_v3(e, L - 1, L);
-   {
-      const int zr = zq_flush(e, e->stream);
-      if (zr) return zr;
-   }
-   hipStream_t s = e->stream;
-   const uint32_t N = e->dc.N;
-#define GNOC_SELFS(F1V)                                                                                              \
-   GNOC_LAUNCH(e, KC_SELF, ch::k_self_stream<F1V>, dim3(N), dim3(ch::SS_T), 0, s, e->dc, e->slot_cnt.as<uint32_t>(), \
-               e->slot_base.as<uint64_t>(), e->nexc.as<uint32_t>(), e->recs.as<Rec>(), e->final_ps.as<uint64_t>(),     \
-               e->port_sum.as<unsigned long long>(), e->port_cnt.as<unsigned long long>(),                          \
-               e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>(), e->counters.as<unsigned>() + 8)
-   if (e->f1) GNOC_SELFS(true);
-   else GNOC_SELFS(false);
-#undef GNOC_SELFS
-   GNOC_LAUNCH(e, KC_SELF, ch::k_inj_undo, dim3((N + 255) / 256), dim3(256), 0, s, N,
-               (const unsigned*) (e->counters.as<unsigned>() + 8 + 8), (uint32_t) P_SELF, e->port_sum.as<unsigned long long>(),
-               e->port_cnt.as<unsigned long long>(), e->port_flit.as<unsigned long long>(),
-               e->port_last.as<unsigned long long>());
-   return run_levels_v3(e, L - 1, L, 2);
+   return run_levels_v3(e, L - 1, L);
 }
 
 constexpr int GNOC_V3_RETRY = 1000;
@@ -2158,7 +2046,6 @@ constexpr int GNOC_CH_EXC = 1003;        // only the injection level's exception
 constexpr int GNOC_CH_YFALL = 1004;      // only the Y chains declined: Y and SELF levels on k_level
 constexpr int GNOC_INJ_DECLINE = 1007;   // the streamed injection level declined: rerun with it on k_level
 constexpr int GNOC_CH_MG = 1005;         // the chains met the M/G/1 branch: rerun on the MG instantiation
-constexpr int GNOC_PIPE_DECLINE = 1006;  // the port pipelines cannot take this batch: rerun on the chains
 
 // ---------------------------------------------------------------------------
 // v4: chain engine for the X and Y phases (chain.hip); INJ and SELF levels on k_level
@@ -2193,17 +2080,14 @@ static int chain_setup(gnoc_engine* e)
    GNOC_HIP(e, e->ch_nmax.ensure(std::max<size_t>(nmx, 1) * 4));
    e->zq.push_back({ e->ch_nmax.p, (uint64_t) std::max<size_t>(nmx, 1) * 4 });   // (zq_flush: before the INJ level)
    const size_t stb = (e->ch_st_words[0] + e->ch_st_words[1] + ch::SW) * 8;
-   const size_t xdb = std::max<size_t>(e->h_tasks[0].size(), 1) * 8;
-   const bool fresh = e->ch_st.bytes < stb || e->ch_xdone.bytes < xdb;
+   const bool fresh = e->ch_st.bytes < stb;
    GNOC_HIP(e, e->ch_st.ensure(stb));
-   GNOC_HIP(e, e->ch_xdone.ensure(xdb));
    // hand-off granules carry a 16-bit epoch: a new epoch per attempt, the buffer
    // zeroed when it is new or the epoch wraps
    e->ch_epoch = (e->ch_epoch + 1) & 0xFFFFu;
    if (fresh || e->ch_epoch == 0)
    {
       GNOC_HIP(e, hipMemsetAsync(e->ch_st.p, 0, e->ch_st.bytes, s));
-      GNOC_HIP(e, hipMemsetAsync(e->ch_xdone.p, 0, e->ch_xdone.bytes, s));
       if (e->ch_epoch == 0) e->ch_epoch = 1;
    }
    e->zq.push_back({ e->ch_ctr.p, 256 });
@@ -2276,7 +2160,7 @@ static ChainArgs chain_args(gnoc_engine* e, int phase)
    a.etag = (uint64_t) e->ch_epoch << 48;
    a.stamps = nullptr;
    a.lookback = e->ch_lb_run[phase];
-   a.fw = a.fw2 = phase ? 5u : 4u;
+   a.fw = phase ? 5u : 4u;
    a.nexc = e->nexc.as<uint32_t>();
    a.port_mg1 = e->port_mg1.as<unsigned long long>();
    // the Y phase runs after k_exc_merge put the X phase's exception tails (M/G/1-served
@@ -2302,9 +2186,9 @@ static int chain_phase(gnoc_engine* e, int phase)
    // its IN_W / IN_E lists (the X phase's turns)
    const bool ylocal = e->nranks <= 1 && e->ncpy;
    // (the IN_LOCAL lists' bounds: already written by k_inj_stream, whose decline
-   // stops the run; on the pipe path's conditional stream only if it declined)
+   // stops the run)
    const bool ibnd = e->inj_bnd && e->inj_host;
-   const unsigned* icond = e->inj_bnd && !e->inj_host ? e->counters.as<unsigned>() + 8 + 7 : nullptr;
+   const unsigned* icond = nullptr;
    if ((phase == 0 && !ibnd) || (phase == 1 && !e->ch_ylocal))
       GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, a.cp, nl, a.len, a.cw, e->recs.as<Rec>(),
                   const_cast<uint32_t*>(a.bt), nl, 0u, phase == 0 ? icond : nullptr);
@@ -2384,187 +2268,6 @@ static int chain_phase(gnoc_engine* e, int phase)
    else if (e->f1) GNOC_CHAIN(1, true);
    else GNOC_CHAIN(1, false);
 #undef GNOC_CHAIN
-   GNOC_HIP(e, hipEventRecord(e->ch_ev[phase][1], s));
-   return GNOC_OK;
-}
-
-// Both phases in one launch (chain.hip k_chain_xy, GNOC_XY=1): a single unsharded
-// mesh whose Y chains have at most 64 ports, outside the protocol trial runs (which
-// launch the phases separately).  Measured on configs[1] it is exact but not faster
-// than the two launches, so the two launches are the default.
-static bool chain_fusable(const gnoc_engine* e)
-{
-   const char* v = std::getenv("GNOC_XY");
-   if (!v || !*v || std::atoi(v) == 0) return false;
-   if (e->nranks > 1 || e->ch_ydeclined || e->ch_mg || !e->ncpx || !e->ncpy || e->dc.H - 1 > 64) return false;
-   return !e->ch_trial;
-}
-
-static int chain_fused(gnoc_engine* e)
-{
-   {
-      const int zr = zq_flush(e, e->stream);
-      if (zr) return zr;
-   }
-   hipStream_t s = e->stream;
-   ch::XYArgs xa;
-   xa.x = chain_args(e, 0);
-   xa.y = chain_args(e, 1);
-   // X inserts (injection outputs) and the Y ports' IN_LOCAL lists: complete before the launch
-   if (!(e->inj_bnd && e->inj_host))
-   {
-      GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpx), dim3(256), 0, s, xa.x.cp, 1u, xa.x.len, xa.x.cw,
-                  e->recs.as<Rec>(), const_cast<uint32_t*>(xa.x.bt), 1u, 0u, (const unsigned*) nullptr);
-      GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpy), dim3(256), 0, s, xa.y.cp, 3u, xa.y.len, xa.y.cw,
-                  e->recs.as<Rec>(), const_cast<uint32_t*>(xa.y.bt), 1u, 0u, (const unsigned*) nullptr);
-   }
-   const uint32_t nx = (uint32_t) e->h_tasks[0].size();
-   xa.x.fw2 = 5u;                                  // an X decline stops the Y tasks too
-   xa.y.ctr = xa.x.ctr;                            // one dequeue head
-   for (ChainArgs* q : { &xa.x, &xa.y })
-   {
-      q->nx_tasks = nx;
-      q->xdone = e->ch_xdone.as<uint64_t>();
-      q->xprefix = e->ch_ctr.as<unsigned>() + 2;   // (zeroed with the dequeue heads)
-      q->xcw = xa.x.cw;
-      q->xst = xa.x.st;
-   }
-   xa.tasks = e->ch_xy.as<uint32_t>();
-   xa.taux = e->ch_xy.as<uint32_t>() + e->h_xy.size();
-   xa.ntasks = (uint32_t) e->h_xy.size();
-   const char* stv = std::getenv("GNOC_STAMPS");
-   if (stv && *stv == '1')
-   {
-      const size_t nst = (size_t) xa.ntasks * std::max(xa.x.len, xa.y.len) * 16;
-      GNOC_HIP(e, e->ch_stamps0.ensure(nst * 8));
-      GNOC_HIP(e, hipMemsetAsync(e->ch_stamps0.p, 0, nst * 8, s));
-      xa.x.stamps = xa.y.stamps = e->ch_stamps0.as<uint64_t>();
-   }
-   const uint32_t grid = (uint32_t) std::min<uint64_t>((uint64_t) e->ch_grid, (uint64_t) xa.ntasks);
-   GNOC_HIP(e, hipEventRecord(e->ch_ev[0][0], s));
-#define GNOC_XYL(F1V, XL, YL) GNOC_LAUNCH(e, KC_CHAIN, (ch::k_chain_xy<F1V, XL, YL>), dim3(grid), dim3(ch::T), 0, s, xa)
-#define GNOC_XYF(F1V)                                  \
-   do                                                  \
-   {                                                   \
-      if (xa.x.lookback && xa.y.lookback) GNOC_XYL(F1V, true, true);        \
-      else if (xa.x.lookback) GNOC_XYL(F1V, true, false);                   \
-      else if (xa.y.lookback) GNOC_XYL(F1V, false, true);                   \
-      else GNOC_XYL(F1V, false, false);                                     \
-   } while (0)
-   if (e->f1) GNOC_XYF(true);
-   else GNOC_XYF(false);
-#undef GNOC_XYF
-#undef GNOC_XYL
-   GNOC_HIP(e, hipEventRecord(e->ch_ev[0][1], s));
-   e->ch_fused = 1;
-   return GNOC_OK;
-}
-
-// ---------------------------------------------------------------------------
-// v6: the X and Y phases as port pipelines (pipe.hip), one wave per chain port
-// ---------------------------------------------------------------------------
-// A 1 GHz, unsharded batch whose chains the chain engine could take.  The pipelines
-// decline what they do not serve exactly (the no-gap M/G/1 branch in a chain port,
-// times beyond 2^31 cycles): the batch then reruns on the chain engine (path 4), and
-// later runs of it start there.  GNOC_PIPE=0 turns the pipelines off.
-static bool pipe_usable(const gnoc_engine* e)
-{
-   const char* v = std::getenv("GNOC_PIPE");
-   if (!(v && *v && std::atoi(v) != 0)) return false;   // (opt-in while it is measured against the chains)
-   return e->f1 && !e->pipe_declined && !e->ch_mg && e->nranks <= 1;
-}
-
-// Ports per segment workgroup: about one workgroup per CU (the phase's ports over the
-// CUs), at least 2 so that both hand-offs (LDS ring, HBM link) run; GNOC_PIPE_S forces it.
-static uint32_t pipe_seg(const gnoc_engine* e, uint32_t ports, uint32_t len)
-{
-   const char* v = std::getenv("GNOC_PIPE_S");
-   uint32_t S = v && std::atoi(v) > 0 ? (uint32_t) std::atoi(v) : (ports + e->ncu - 1) / std::max(1, e->ncu);
-   S = std::max<uint32_t>(S, 2u);
-   S = std::min<uint32_t>(S, 8u);
-   return std::max<uint32_t>(1u, std::min(S, len));
-}
-
-static int pipe_setup(gnoc_engine* e)
-{
-   const DevCfg& c = e->dc;
-   hipStream_t s = e->stream;
-   e->ncpx = c.W > 1 ? 2 * (e->ry1 - e->ry0) * (c.W - 1) : 0;
-   e->ncpy = c.H > 1 ? 2 * (e->cx1 - e->cx0) * (c.H - 1) : 0;
-   const uint32_t ncp = e->ncpx + e->ncpy;
-   GNOC_HIP(e, e->ch_cp.ensure((size_t) std::max<uint32_t>(ncp, 1) * sizeof(ChainPort)));
-   GNOC_HIP(e, e->pipe_ctr.ensure(256));
-   e->zq.push_back({ e->pipe_ctr.p, 256 });   // (zq_flush: before the first level)
-   for (int p = 0; p < 2; p++)
-      for (int q = 0; q < 2; q++)
-         if (!e->ch_ev[p][q]) GNOC_HIP(e, hipEventCreate(&e->ch_ev[p][q]));
-   e->pipe_tag++;   // (run_prep cleared the record buffer when it was new or the epoch wrapped)
-   if (ncp)
-      GNOC_LAUNCH(e, KC_PLAN, ch::k_chain_plan, dim3((ncp + 255) / 256), dim3(256), 0, s, c, e->ncpx, e->ncpy, e->ry0,
-                  e->cx0, e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->ch_cp.as<ChainPort>());
-   return GNOC_OK;
-}
-
-static int pipe_phase(gnoc_engine* e, int phase)
-{
-   {
-      const int zr = zq_flush(e, e->stream);
-      if (zr) return zr;
-   }
-   hipStream_t s = e->stream;
-   const uint32_t ncp = phase ? e->ncpy : e->ncpx;
-   if (!ncp) return GNOC_OK;
-   const uint32_t len = phase ? e->dc.H - 1 : e->dc.W - 1;
-   pp::PipeArgs a{};
-   a.cp = e->ch_cp.as<ChainPort>() + (phase ? e->ncpx : 0);
-   a.recs = e->recs.as<Rec>();
-   a.samp_t = e->samp_t.as<uint64_t>();
-   a.samp_id = e->samp_id.as<uint32_t>();
-   a.port_sum = e->port_sum.as<unsigned long long>();
-   a.port_cnt = e->port_cnt.as<unsigned long long>();
-   a.port_flit = e->port_flit.as<unsigned long long>();
-   a.port_last = e->port_last.as<unsigned long long>();
-   a.errflag = e->counters.as<unsigned>() + 8;
-   a.ctr = e->pipe_ctr.as<unsigned>() + phase;
-   a.nch = ncp / len;
-   a.len = len;
-   a.S = pipe_seg(e, ncp, len);
-   a.fw = phase ? 5u : 4u;
-   a.rcap = 512;
-   a.scap = 128;
-   a.mcap = 128;
-   a.tag = e->pipe_tag;
-   a.excfix = (uint32_t) e->exc_fix;
-   a.analytical = (uint32_t) e->dc.analytical;
-   a.nsamp = (uint32_t) (e->rec_bound / 64 + 1);
-   a.spin_shift = 33;
-   a.dbg = nullptr;
-   const char* dv = std::getenv("GNOC_PIPE_DEBUG");
-   if (dv && *dv)
-   {
-      // every wave's state at its end (or where it gave up), printed after the run
-      const size_t nd = ((size_t) ncp + (size_t) (ncp / len) * ((len + 1) / 2 + 1)) * pp::DBG_W;
-      DevBuf& db = phase ? e->pipe_dbg1 : e->pipe_dbg0;
-      GNOC_HIP(e, db.ensure(nd * 4));
-      GNOC_HIP(e, hipMemsetAsync(db.p, 0, nd * 4, s));
-      a.dbg = db.as<uint32_t>();
-      a.spin_shift = (uint32_t) std::max(20, std::min(36, std::atoi(dv) > 1 ? std::atoi(dv) : 31));
-   }
-   e->pipe_S[phase] = a.S;
-   const uint32_t nseg = (len + a.S - 1) / a.S;
-   const uint32_t grid = a.nch * nseg;
-   const size_t lds = phase ? pp::lds_bytes<3>(a.S, a.rcap, a.scap, a.mcap) : pp::lds_bytes<1>(a.S, a.rcap, a.scap, a.mcap);
-   GNOC_HIP(e, hipEventRecord(e->ch_ev[phase][0], s));
-   if (phase)
-   {
-      GNOC_HIP(e, hipFuncSetAttribute((const void*) pp::k_pipe<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
-      GNOC_LAUNCH(e, KC_PIPE, pp::k_pipe<3>, dim3(grid), dim3(64 * (a.S + 1)), lds, s, a);
-   }
-   else
-   {
-      GNOC_HIP(e, hipFuncSetAttribute((const void*) pp::k_pipe<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int) lds));
-      GNOC_LAUNCH(e, KC_PIPE, pp::k_pipe<1>, dim3(grid), dim3(64 * (a.S + 1)), lds, s, a);
-   }
    GNOC_HIP(e, hipEventRecord(e->ch_ev[phase][1], s));
    return GNOC_OK;
 }
@@ -2655,16 +2358,6 @@ static int run_prep(gnoc_engine* e, bool* done)
    e->layout_bound = e->rec_bound;
    if (const char* lb = std::getenv("GNOC_TEST_LAYOUT_BOUND"))
       if (*lb) e->layout_bound = std::min<uint64_t>(e->rec_bound, std::strtoull(lb, nullptr, 10));
-   // the port pipelines' segment links carry a 16-bit epoch tag (pipe.hip): the record
-   // buffer is cleared when it is new (stale records of another engine could carry any
-   // tag) and when the epoch wraps, before this run's scatter writes into it
-   if (e->recs.p != e->pipe_recs || e->recs.bytes != e->pipe_recs_bytes || e->pipe_tag >= 0xFFFEu)
-   {
-      GNOC_HIP(e, hipMemsetAsync(e->recs.p, 0, e->recs.bytes, s));
-      e->pipe_recs = e->recs.p;
-      e->pipe_recs_bytes = e->recs.bytes;
-      e->pipe_tag = 0;
-   }
    GNOC_HIP(e, e->samp_t.ensure((e->rec_bound / 64 + 1) * 8));
    GNOC_HIP(e, e->samp_id.ensure((e->rec_bound / 64 + 1) * 4));
    GNOC_HIP(e, e->Hs.ensure((size_t) N * W * 3 * 4));
@@ -2926,50 +2619,7 @@ static int run_post_check(gnoc_engine* e, bool closed_form)
    if (e->inj_host && ef[7]) return GNOC_INJ_DECLINE;
    const unsigned errf = ef[0];
    const unsigned cf = ef[4] | ef[5];   // the X phase's and the Y phase's chain flags
-   if (e->used_pipe)
-   {
-      e->pipe_flags[0] = ef[4];
-      e->pipe_flags[1] = ef[5];
-      if (std::getenv("GNOC_PIPE_DEBUG") && *std::getenv("GNOC_PIPE_DEBUG"))
-         for (int p = 0; p < 2; p++)
-         {
-            const DevBuf& db = p ? e->pipe_dbg1 : e->pipe_dbg0;
-            if (!db.p) continue;
-            std::vector<uint32_t> h(db.bytes / 4);
-            if (hipMemcpy(h.data(), db.p, db.bytes, hipMemcpyDeviceToHost) != hipSuccess) continue;
-            uint32_t ends = 0, stuck = 0;
-            for (size_t r = 0; r + pp::DBG_W <= h.size(); r += pp::DBG_W)
-            {
-               const uint32_t tagw = h[r] >> 16, why = h[r] & 0xFFFFu;
-               if (tagw != 0xB0DEu && tagw != 0xC0DEu) continue;
-               ends++;
-               if (!why && !std::getenv("GNOC_PIPE_DEBUG_ALL")) continue;
-               stuck += why != 0;
-               std::fprintf(stderr, "gnoc pipe %c %s #%zu why %u:", p ? 'Y' : 'X', tagw == 0xB0DEu ? "port" : "svc",
-                            r / pp::DBG_W, why);
-               for (uint32_t q = 1; q < 16; q++) std::fprintf(stderr, " %u", h[r + q]);
-               std::fprintf(stderr, " |");
-               for (uint32_t q = 16; q < 27; q++) std::fprintf(stderr, " %u", h[r + q]);
-               std::fprintf(stderr, "\n");
-            }
-            std::fprintf(stderr, "gnoc pipe %c: %u waves reported, %u gave up\n", p ? 'Y' : 'X', ends, stuck);
-         }
-   }
-   if (e->used_pipe && (cf & ch::F_ANY))
-   {
-      if (std::getenv("GNOC_CHAIN_DEBUG"))
-         std::fprintf(stderr, "gnoc: port pipelines declined, flags X 0x%x Y 0x%x\n", ef[4], ef[5]);
-      if (cf & ch::F_ROUTE)
-      {
-         char m[96];
-         std::snprintf(m, sizeof m, "internal: pipeline route-count invariant violated (flags 0x%x 0x%x)", ef[4], ef[5]);
-         return fail(e, GNOC_EHIP, m);
-      }
-      // the injection level left exception tails -> merge them first (as the chains do)
-      if (!e->exc_fix && (ef[4] & ch::R_EXC) && !(ef[2] & 2u)) return GNOC_CH_EXC;
-      return GNOC_PIPE_DECLINE;
-   }
-   if (e->used_chain && !e->ch_fused && e->ch_trial && !(cf & ch::F_ANY))
+   if (e->used_chain && e->ch_trial && !(cf & ch::F_ANY))
    {
       // this run's time of each phase's protocol (chain_setup keeps the faster one)
       for (int p = 0; p < 2; p++)
@@ -3050,25 +2700,7 @@ static int run_once(gnoc_engine* e)
    const bool v3 = e->dc.max_list >= 3 && !e->force_v1;
    e->used_v3 = v3;
    e->used_chain = 0;
-   e->used_pipe = 0;
-   if (v3 && chain_usable(e) && pipe_usable(e))
-   {
-      // v6: INJ level, X pipelines, Y pipelines, SELF level
-      e->used_pipe = 1;
-      e->used_v3 = 6;
-      rc = run_plan_v3(e, true);
-      if (!rc) rc = pipe_setup(e);
-      if (!rc) rc = inj_level(e, false);
-      if (!rc && e->exc_fix) rc = exc_merge(e);
-      if (!rc) rc = pipe_phase(e, 0);
-      if (!rc) rc = pipe_phase(e, 1);
-      if (!rc)
-         GNOC_LAUNCH(e, KC_PIPE, pp::k_pipe_samples, dim3(e->dc.N * INS), dim3(256), 0, e->stream, e->dc.N,
-                     e->slot_cnt.as<uint32_t>(), e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(),
-                     e->samp_id.as<uint32_t>());
-      if (!rc) rc = self_level(e);
-   }
-   else if (v3 && chain_usable(e))
+   if (v3 && chain_usable(e))
    {
       // v4: INJ level, X chains, Y chains, SELF level
       const uint32_t L = (uint32_t) e->lvl_off.size() - 1;
@@ -3078,18 +2710,13 @@ static int run_once(gnoc_engine* e)
       e->ch_ylocal = 0;
       rc = run_plan_v3(e, !e->ch_ydeclined);   // (Y on k_level: its levels too)
       if (!rc) rc = chain_setup(e);
-      if (!rc) rc = inj_level(e, true);
+      if (!rc) rc = inj_level(e);
       if (!rc && e->exc_fix) rc = exc_merge(e);
-      e->ch_fused = 0;
-      if (!rc && chain_fusable(e)) rc = chain_fused(e);
-      else
-      {
-         if (!rc) rc = chain_phase(e, 0);
-         // turns the X chains served by M/G/1 wait in exception tails: into order first
-         // (only the MG instantiation, mg_emit, writes exception tails)
-         if (!rc && !e->ch_ydeclined && e->dc.analytical && e->ch_mg) rc = exc_merge(e);
-         if (!rc && !e->ch_ydeclined) rc = chain_phase(e, 1);
-      }
+      if (!rc) rc = chain_phase(e, 0);
+      // turns the X chains served by M/G/1 wait in exception tails: into order first
+      // (only the MG instantiation, mg_emit, writes exception tails)
+      if (!rc && !e->ch_ydeclined && e->dc.analytical && e->ch_mg) rc = exc_merge(e);
+      if (!rc && !e->ch_ydeclined) rc = chain_phase(e, 1);
       const char* xv = std::getenv("GNOC_CHAIN_EXPERIMENT");
       if (!rc && xv && std::atoi(xv))
       {
@@ -3436,13 +3063,6 @@ static int run_impl(gnoc_engine* e)
          if (rc == GNOC_INJ_DECLINE)
          {
             e->inj_declined = 1;
-            e->n_retry++;
-            continue;
-         }
-         if (rc == GNOC_PIPE_DECLINE)
-         {
-            // the chain engine reruns the batch (and takes its later runs)
-            e->pipe_declined = 1;
             e->n_retry++;
             continue;
          }
@@ -3870,7 +3490,6 @@ static int begin_x(gnoc_engine* e, void* send_buf, bool sync)
       e->used_chain = 1;
       e->used_v3 = 4;
       rc = chain_setup(e);
-      e->ch_fused = 0;
       if (!rc) rc = run_levels_v3(e, 0, 1);
       if (!rc) rc = chain_phase(e, 0);
       if (rc) return rc;
@@ -4169,7 +3788,7 @@ int gnoc_get_summary(gnoc_engine* e, gnoc_summary* out)
    while (sh < 63 && (2ull << sh) <= dm[0]) sh++;
    out->window_shift = e->used_chain ? sh : 0u;
    out->windows_y = nwm[1];
-   out->chain_protocol = e->used_chain ? 0x100u | e->ch_lb_run[0] | (e->ch_lb_run[1] << 1) | (e->ch_fused ? 0x200u : 0u) | (e->ch_mg ? 0x400u : 0u) |
+   out->chain_protocol = e->used_chain ? 0x100u | e->ch_lb_run[0] | (e->ch_lb_run[1] << 1) | (e->ch_mg ? 0x400u : 0u) |
                                          (e->ch_split ? 0x800u : 0u) : 0u;
    out->window_ps_x = dm[0];
    out->window_ps_y = dm[1];
@@ -4224,30 +3843,20 @@ __attribute__((visibility("default"))) int gnoc_debug_chain_stamps(gnoc_engine* 
                                                                    size_t* count, uint32_t* geom)
 {
    if (!e || !count) return GNOC_EINVAL;
-   // phase 2: the fused launch (X and Y tasks in one table; geom[3] = its X tasks; the
-   // table itself through gnoc_debug_xy_tasks)
+   if (phase < 0 || phase > 1) return GNOC_EINVAL;
    const DevBuf& sb = phase == 1 ? e->ch_stamps1 : e->ch_stamps0;
-   const uint32_t len = phase == 2 ? std::max(e->dc.W, e->dc.H) - 1 : phase ? e->dc.H - 1 : e->dc.W - 1;
-   const size_t nt = phase == 2 ? e->h_xy.size() : e->h_tasks[phase].size();
+   const uint32_t len = phase ? e->dc.H - 1 : e->dc.W - 1;
+   const size_t nt = e->h_tasks[phase].size();
    *count = nt * len * 16;
    if (geom)
    {
       geom[0] = 1;
       geom[1] = (uint32_t) nt;
       geom[2] = len;
-      geom[3] = phase == 2 ? (uint32_t) e->h_tasks[0].size() : 0u;   // tasks in key order
+      geom[3] = 0u;
    }
    if (!out || !sb.p) return GNOC_OK;
    GNOC_HIP(e, hipMemcpy(out, sb.p, std::min(cap, *count) * 8, hipMemcpyDeviceToHost));
-   return GNOC_OK;
-}
-
-// Debug: the fused launch's task table (bit 31: Y task, bits 16-30 chain, 0-15 window).
-__attribute__((visibility("default"))) int gnoc_debug_xy_tasks(gnoc_engine* e, uint32_t* out, size_t cap, size_t* count)
-{
-   if (!e || !count) return GNOC_EINVAL;
-   *count = e->h_xy.size();
-   if (out) std::copy(e->h_xy.begin(), e->h_xy.begin() + std::min(cap, e->h_xy.size()), out);
    return GNOC_OK;
 }
 

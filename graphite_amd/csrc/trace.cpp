@@ -271,11 +271,49 @@ extern "C" int gnoc_trace_file_read_q(const char* path, gnoc_config* cfg_out, gn
    return ok ? GNOC_OK : GNOC_ETRACE;
 }
 
+// Run fn(k) for k in [0, nt): blocks 1.. on new threads where the host gives them,
+// the rest (and block 0) on the calling thread -- a thread the system refuses
+// (std::system_error) costs parallelism, not the call.
+template <class F>
+static void run_blocks(size_t nt, F&& fn)
+{
+   std::vector<std::thread> th;
+   size_t k = 1;
+   try
+   {
+      th.reserve(nt);
+      for (; k < nt; k++) th.emplace_back(fn, k);
+   }
+   catch (...)
+   {
+   }
+   for (size_t r = k; r < nt; r++) fn(r);
+   fn(0);
+   for (auto& x : th) x.join();
+}
+
+static int pack_trace(const gnoc_packets* pk, size_t n, uint16_t* dt, uint16_t* src, uint16_t* dst, uint16_t* bits,
+                      uint8_t* flags, uint64_t* abs_ps, size_t abs_cap, gnoc_pack_info* info);
+
 // The delta wire format's encoder (include/gnoc.h gnoc_pack_trace): blocks of the
 // trace on the host's threads; pass 1 validates and counts each block's escapes,
-// pass 2 writes, each block's escapes at its offset in abs_ps.
+// pass 2 writes, each block's escapes at its offset in abs_ps.  Never throws
+// across the C boundary: an allocation failure is GNOC_ENOMEM.
 extern "C" int gnoc_pack_trace(const gnoc_packets* pk, size_t n, uint16_t* dt, uint16_t* src, uint16_t* dst,
                                uint16_t* bits, uint8_t* flags, uint64_t* abs_ps, size_t abs_cap, gnoc_pack_info* info)
+{
+   try
+   {
+      return pack_trace(pk, n, dt, src, dst, bits, flags, abs_ps, abs_cap, info);
+   }
+   catch (...)
+   {
+      return GNOC_ENOMEM;
+   }
+}
+
+static int pack_trace(const gnoc_packets* pk, size_t n, uint16_t* dt, uint16_t* src, uint16_t* dst, uint16_t* bits,
+                      uint8_t* flags, uint64_t* abs_ps, size_t abs_cap, gnoc_pack_info* info)
 {
    if (!pk || !info) return GNOC_EINVAL;
    if (n && (!pk->inject_ps || !pk->src || !pk->dst || !pk->bits || !dt || !src || !dst)) return GNOC_EINVAL;
@@ -305,12 +343,7 @@ extern "C" int gnoc_pack_trace(const gnoc_packets* pk, size_t n, uint16_t* dt, u
          q.bad |= pk->src[i] > 0xFFFFu || pk->dst[i] > 0xFFFFu || pk->bits[i] > 0xFFFFu || f > 0xFFu;
       }
    };
-   {
-      std::vector<std::thread> th;
-      for (size_t k = 1; k < nt; k++) th.emplace_back(count, k);
-      count(0);
-      for (auto& x : th) x.join();
-   }
+   run_blocks(nt, count);
    uint64_t nesc = 0;
    uint32_t fl = 0;
    bool bad = false, one = true;
@@ -346,9 +379,6 @@ extern "C" int gnoc_pack_trace(const gnoc_packets* pk, size_t n, uint16_t* dt, u
          if (flags) flags[i] = (uint8_t) (pk->flags ? pk->flags[i] : 0u);
       }
    };
-   std::vector<std::thread> th;
-   for (size_t k = 1; k < nt; k++) th.emplace_back(write, k);
-   write(0);
-   for (auto& x : th) x.join();
+   run_blocks(nt, write);
    return GNOC_OK;
 }

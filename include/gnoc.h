@@ -190,8 +190,7 @@ typedef struct gnoc_summary
    uint32_t chain_protocol;     /* hand-off protocol of the last chain run: bit 8 set when the chain
                                    engine ran; bit 0 / bit 1 set when the X / Y phase used the
                                    look-back protocol (else serial; look-back is kept only when it
-                                   measured > 5% faster than serial on the batch's windows); bit 9
-                                   set when both phases ran in one fused launch; bit 10 set when
+                                   measured > 5% faster than serial on the batch's windows); bit 10 set when
                                    the chains served the no-gap M/G/1 prefix (the batch meets the
                                    history tree's analytical branch in mesh ports); bit 11 set
                                    when only the windows that can serve M/G/1 requests ran on
@@ -249,7 +248,8 @@ int gnoc_submit_packed(gnoc_engine *eng, const gnoc_packets_packed *pk, size_t n
  * unspecified, when above abs_cap: call again with room for n_abs), the length
  * every packet has (bits_all; 0xFFFFFFFF when they differ: pass bits) and the OR
  * of all flags.  GNOC_EINVAL when a tile id, length or flag does not fit the
- * narrow fields.  No engine, no device. */
+ * narrow fields; GNOC_ENOMEM when the host is out of memory (the call never
+ * throws; threads the host refuses only cost parallelism).  No engine, no device. */
 typedef struct gnoc_pack_info
 {
    uint64_t t0;

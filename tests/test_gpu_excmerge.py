@@ -217,3 +217,32 @@ def test_refused_exception_slot_with_y_mg1_is_exact():
         paths.append(int(got.summary["engine_path"]))
     eng.close()
     print("engine paths", paths)
+
+
+def test_inj_stream_gap_on_block_boundary():
+    """The streamed injection level (chain.hip k_inj_stream) walks a slot in blocks
+    of 1,024 records.  Here tile 0's injection queue is busy without a gap for
+    exactly one block (one 1-flit packet per cycle from cycle 0), idles for a cycle,
+    and the next block opens with a 3-packet burst whose third packet would be
+    served by M/G/1 (X > t + p) had the queue never idled.  The idle cycle falls on
+    the block boundary, where the block-relative tail is clamped to the block's
+    first cycle: the stream must still see the gap (queue_model_history_tree.cc:79-86)
+    and not decline (a false decline reruns the batch and keeps it off the stream)."""
+    W = H = 4
+    cfg = gnoc.EngineConfig(num_tiles=W * H, mesh_width=W, mesh_height=H, flit_width=64)
+    n0 = 1024
+    t = np.concatenate([np.arange(n0, dtype=np.uint64), np.full(3, n0 + 1, np.uint64)]) * np.uint64(1000)
+    dst = (np.arange(t.size, dtype=np.uint32) % (W * H - 1)) + 1
+    src = np.zeros(t.size, np.uint32)
+    tr = gnoc.Trace(t, src, dst, np.full(t.size, 64, np.uint32), np.zeros(t.size, np.uint32))
+    ref = oracle.run(cfg, tr)
+    assert ref.port_mg1.sum() == 0
+    eng = gnoc.Engine(cfg)
+    eng.submit(tr)
+    for _ in range(2):
+        eng.run()
+        got = eng.results()
+        same(got, ref)
+        s = got.summary
+        assert s["engine_path"] == 4 and s["retries"] == 0 and s["fallbacks"] == 0, s
+    eng.close()

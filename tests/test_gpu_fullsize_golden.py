@@ -63,50 +63,6 @@ def test_configs1_full_size_matches_oracle(name, lookback, monkeypatch):
     eng.close()
 
 
-@pytest.mark.parametrize("path", ["fused", "pipe"])
-def test_configs1_full_size_opt_in_paths_match_oracle(path, monkeypatch):
-    """The opt-in engine paths on configs[1]'s uniform batch, every array SHA-pinned:
-    the fused X+Y chain launch (GNOC_XY=1, chain_protocol bit 9) and the port
-    pipelines (GNOC_PIPE=1, engine path 6).  The fused launch starts after the
-    protocol trial runs (which time each phase's launch on its own); every run is
-    pinned, the last one must have taken the path."""
-    monkeypatch.setenv("GNOC_XY" if path == "fused" else "GNOC_PIPE", "1")
-    name = "32x32_uniform_l0.005_ppt10000"
-    tr = _trace(name)
-    eng = gnoc.Engine(gnoc.EngineConfig(num_tiles=1024))
-    eng.submit(tr)
-    for _ in range(6 if path == "fused" else 2):
-        eng.run()
-        s = eng.summary()
-        assert s["fallbacks"] == 0 and (s["engine_path"] == 6) == (path == "pipe"), s
-        _check(name, eng.results())
-    assert s["retries"] == 0, s
-    if path == "fused":
-        assert s["engine_path"] == 4 and s["chain_protocol"] & 0x200, s
-    eng.close()
-
-
-@pytest.mark.parametrize("name", ["32x32_uniform_l0.005_ppt10000", "32x32_burst4_l0.005_ppt10000"])
-def test_configs1_full_size_self_stream_matches_oracle(name, monkeypatch):
-    """The opt-in streamed SELF level (GNOC_SELF_STREAM=1, chain.hip k_self_stream:
-    one workgroup per tile merging its four SELF input slots block by block) on the
-    uniform batch, and on the burst batch, whose exception tails / no-gap M/G/1
-    requests make it decline to k_level's SELF level; every array SHA-pinned."""
-    monkeypatch.setenv("GNOC_SELF_STREAM", "1")
-    tr = _trace(name)
-    eng = gnoc.Engine(gnoc.EngineConfig(num_tiles=1024))
-    eng.submit(tr)
-    for r in range(3):
-        eng.set_profiling(r == 2)
-        eng.run()
-        s = eng.summary()
-        if r:   # (the burst batch's first run may settle on another path)
-            assert s["engine_path"] == 4 and s["fallbacks"] == 0, s
-        _check(name, eng.results())
-    assert eng.kernel_stats()["k_self_stream"][1] >= 1
-    eng.close()
-
-
 @pytest.mark.parametrize("lookback", ["0", "1"])
 def test_configs1_full_size_mg1_burst_matches_oracle(lookback, monkeypatch):
     """configs[1]'s uniform batch behind a cycle-0 burst (4 packets per tile): the
