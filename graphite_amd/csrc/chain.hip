@@ -93,7 +93,8 @@ constexpr uint32_t F_ANY = F_RETRY | F_FALLBACK | F_ROUTE | F_TIMEOUT;
 // why a chain run declined (bits above F_ANY; reported with GNOC_CHAIN_DEBUG=1)
 enum : uint32_t { R_OFFSET = 1u << 8, R_TAIL = 1u << 9, R_SPILLIN = 1u << 10, R_LASTSPILL = 1u << 11, R_MG1 = 1u << 12,
                   R_EXC = 1u << 13, R_OVF_INS = 1u << 14, R_OVF_STREAM = 1u << 15, R_XDONE = 1u << 17,
-                  R_MGBAD = 1u << 18, R_MGB_KEPT = 1u << 19, R_MGB_SPILL = 1u << 20, R_MGB_OVF = 1u << 21 };
+                  R_MGBAD = 1u << 18, R_MGB_KEPT = 1u << 19, R_MGB_SPILL = 1u << 20, R_MGB_OVF = 1u << 21,
+                  R_XCD = 1u << 22 };
 constexpr uint64_t SPIN_CYCLES = 1ull << 31;
 constexpr uint64_t M48 = (1ull << 48) - 1;
 constexpr uint64_t OFF_LIM = (1ull << 32) - 4096;   // time offsets within a window (32-bit cycle math)
@@ -180,6 +181,13 @@ struct ChainArgs
    unsigned long long* port_mg1;  // per-port M/G/1 requests
    unsigned* mgk;                 // [nch] 2 + the last window after which a port of the chain still had no gap
    const uint32_t* mgk_lim;       // k_chain_mix: [nch] windows below it take the M/G/1 path
+   // XCD-local task queues (xcd = 1): chains are assigned to the 8 XCDs; a workgroup takes
+   // tasks only from the queue of the XCD it runs on (HW_REG_XCC_ID), so a chain's windows
+   // hand off through that XCD's L2: granules and spills are stored plain (sc0, kept in the
+   // L2) instead of written through, and read with sc1 loads (L1 bypass, L2-served)
+   const uint32_t* qoff;          // [NQ + 1] first task of each queue in `tasks`
+   unsigned* qctr;                // queue q's dequeue head at qctr[QSTRIDE q]; the exit count at qctr[QSTRIDE NQ]
+   uint32_t xcd, pad3;
 };
 
 
@@ -202,6 +210,19 @@ __device__ __forceinline__ uint64_t ld1(const uint64_t* p)
 __device__ __forceinline__ void st1(uint64_t* p, uint64_t v)
 {
    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// A hand-off store: written through (sc1) for a reader on any XCD, or, with XCD-local
+// queues (producer and consumer share the XCD's L2), kept in the L2 (sc0).
+__device__ __forceinline__ void sth(uint32_t xcd, uint64_t* p, uint64_t v)
+{
+   if (xcd) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+   else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr uint32_t NQ = 8;        // XCD-local queues (MI355X: 8 XCDs)
+constexpr uint32_t QSTRIDE = 32;  // queue heads 128 B apart
+__device__ __forceinline__ uint32_t xcc_id()
+{
+   return (uint32_t) __builtin_amdgcn_s_getreg(20 | (0 << 6) | ((4 - 1) << 11)) & (NQ - 1);   // hwreg(HW_REG_XCC_ID, 0, 4)
 }
 // Compiler-only ordering point between LDS phases of the one wave.
 __device__ __forceinline__ void wsync() { asm volatile("" ::: "memory"); }
@@ -536,6 +557,9 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 #ifndef CH_TURN_PLAIN
 #define CH_TURN_PLAIN 0   // 1: turns as plain 8-B stores (written back at the launch's end), spills sc1
 #endif
+#ifndef CH_RANKS
+#define CH_RANKS 0        // 1: the emit's route ranks kept from the row scans (no second wave sum per row)
+#endif
 #ifndef CH_EARLY_PF
 #define CH_EARLY_PF 0     // 1: the next ports' inserts / descriptor loaded right after a step's landing
 #endif
@@ -545,13 +569,20 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 // 8-B stores (MI355X_MICROARCH.md "Valid forms").  Every 64th position also writes
 // the slot's key sample.
 __device__ __forceinline__ void out_record(gptr<Rec> recs, gptr<uint64_t> samp_t, gptr<uint32_t> samp_id, uint64_t gp,
-                                           uint64_t tn, uint32_t id, uint32_t ax, bool spill)
+                                           uint64_t tn, uint32_t id, uint32_t ax, bool spill, uint32_t xcd)
 {
-   if (CH_TURN_PLAIN && !spill)
+   if ((CH_TURN_PLAIN || xcd) && !spill)
    {
       const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
       q[0] = tn;
       q[1] = (uint64_t) id | ((uint64_t) ax << 32);
+   }
+   else if (xcd)
+   {
+      // a spill read in this launch by the next window of the chain, on this XCD
+      const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
+      __hip_atomic_store(q, tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(q + 1, (uint64_t) id | ((uint64_t) ax << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
    }
    else if (!CH_TURN16 || spill)
    {
@@ -727,7 +758,7 @@ __device__ __forceinline__ MgOut mg_emit(Smem& sm, const ChainArgs& a, const uin
             sm.key[kb + rank] = (dn << 32) | id;
             sm.aux[kb + rank] = ax;
          }
-         if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
+         if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1, a.xcd);
          if (nogap && q > lo)
          {
             // the M/G/1 sums of the FIFO-served requests; FIFO departures rise, the last is X
@@ -1001,6 +1032,7 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
       // ---- [B] the merged stream in rows; per-row max-plus scans, route-field totals
       uint32_t n = nK + nI, IB = CAP;
       uint32_t fpack = 0, tc_t = 0;
+      uint32_t rkp[3] = { 0u, 0u, 0u }, rtv = 0;   // (CH_RANKS) route ranks / field totals per row
       uint32_t totA = 0, totB = 0;
       bool first = true, published = false;
       uint32_t Xr = 0, mode = mode0, Kpp = 0, Pep = 0, Kout = 0, Pend = 0;
@@ -1014,6 +1046,7 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
          totA = totB = 0;
          fpack = 0;
          tc_t = 0;
+         rkp[0] = rkp[1] = rkp[2] = rtv = 0;
 #pragma unroll
          for (int r = 0; r < ROWS; r++)
          {
@@ -1030,7 +1063,16 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
             totA += rA;
             const uint32_t f = route_field<XC>(nx, ny, ra[r]);
             fpack |= (valid ? f : 0u) << (2 * r);
-            tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
+            const uint32_t one = valid ? 1u << (8 * f) : 0u;
+            const uint32_t inc = wave_sum32(one);
+            tc_t += field_cnt(rdl(inc, 63), lane);
+            if (CH_RANKS && !MG)
+            {
+               // the emit's route ranks (< 64: 6 bits, rows 5 to a register) and the row's
+               // packed field totals (lane r)
+               rkp[r / 5] |= (((inc - one) >> (8 * f)) & 0x3Fu) << (6 * (r % 5));
+               rtv = lane == (uint32_t) r ? rdl(inc, 63) : rtv;
+            }
          }
          if (!first) break;
          CH_STAMP(2);
@@ -1097,7 +1139,7 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
          if (published && lane < (uint32_t) SW_SER)
          {
             const uint32_t x0 = Xr + totA;
-            st1(stw + lane, a.etag | state_word_ser(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u, Kout, Pend));
+            sth(a.xcd, stw + lane, a.etag | state_word_ser(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u, Kout, Pend));
          }
          if (Pep == Kpp) break;
          // ---- slow path: spill-ins (records the previous port spilled in earlier windows,
@@ -1165,7 +1207,7 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
       if (!published && !mode && lane < (uint32_t) SW_SER)
       {
          const uint32_t x0 = Xr + totA;
-         st1(stw + lane, a.etag | state_word_ser(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u, Kout, Pend));
+         sth(a.xcd, stw + lane, a.etag | state_word_ser(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u, Kout, Pend));
       }
 
       CH_PRIO_LO();
@@ -1240,10 +1282,19 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
          const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
          // route ranks: a packed (8 bits per field) prefix count over the row
          const uint32_t f = (fpack >> (2 * r)) & 3u;
-         const uint32_t one = valid ? 1u << (8 * f) : 0u;
-         const uint32_t inc = wave_sum32(one);
-         const uint32_t rank = ((inc - one) >> (8 * f)) & 0xFFu;
-         const uint32_t rtot = rdl(inc, 63);
+         uint32_t rank, rtot;
+         if (CH_RANKS && !MG)
+         {
+            rank = (rkp[r / 5] >> (6 * (r % 5))) & 0x3Fu;
+            rtot = rdl(rtv, r);
+         }
+         else
+         {
+            const uint32_t one = valid ? 1u << (8 * f) : 0u;
+            const uint32_t inc = wave_sum32(one);
+            rank = ((inc - one) >> (8 * f)) & 0xFFu;
+            rtot = rdl(inc, 63);
+         }
          const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
          const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
          const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
@@ -1263,7 +1314,7 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
             sm.key[kb + rank] = (dn << 32) | id;
             sm.aux[kb + rank] = ax;
          }
-         if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
+         if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1, a.xcd);
       }
       CH_STAMP(6);
       const bool spilled = (mgr && mo.spilled) || spm != 0;
@@ -1292,9 +1343,9 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
          if (!MG && lane == 0 && ffire != NONE && (fgap == NONE || ffire < fgap)) flag(a, F_FALLBACK | R_MG1);
          const uint32_t mout = mgr ? mo.mode : (fgap == NONE ? 1u : 0u);
          if (MG && mout) mst = mg_after(mst, mgr, n, totA, sp2, Xo);
-         if (lane < (uint32_t) SW_SER) st1(stw + lane, a.etag | state_word_ser(lane, Xo, run_t, mout, Kout, Pend));
+         if (lane < (uint32_t) SW_SER) sth(a.xcd, stw + lane, a.etag | state_word_ser(lane, Xo, run_t, mout, Kout, Pend));
          if (MG && mout && lane == 0) atomicMax(a.mgk + c, w + 2u);   // window w + 1 may still serve M/G/1
-         if (MG && mout && lane < 4u) st1(stw + G_MG + lane, a.etag | mst);
+         if (MG && mout && lane < 4u) sth(a.xcd, stw + G_MG + lane, a.etag | mst);
       }
       // every record of the port has passed at the last window: the route counts (and
       // the exception tails) fill every output slot
@@ -1425,6 +1476,7 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
       uint32_t n = nK + nI, IB = CAP;
       const uint32_t itot = itot_f;
       uint32_t fpack = 0, tc_t = 0, totA = 0, totB = 0;
+      uint32_t rkp[3] = { 0u, 0u, 0u }, rtv = 0;   // (CH_RANKS) route ranks / field totals per row
       bool first = true;
       // spill-ins: records port i-1 spilled in earlier windows (departures after their
       // window's end) that arrive here in this window.  Pending range [Kpp, Pep): Pep = port
@@ -1438,6 +1490,7 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
          load_rows<ROWS>(sm, nK, IB, nI, rk, ra);
          if (first) CH_STAMP(1);
          fpack = tc_t = totA = totB = 0;
+         rkp[0] = rkp[1] = rkp[2] = rtv = 0;
 #pragma unroll
          for (int r = 0; r < ROWS; r++)
          {
@@ -1454,7 +1507,16 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
             totA += rA;
             const uint32_t f = route_field<XC>(nx, ny, ra[r]);
             fpack |= (valid ? f : 0u) << (2 * r);
-            tc_t += field_cnt(rdl(wave_sum32(valid ? 1u << (8 * f) : 0u), 63), lane);
+            const uint32_t one = valid ? 1u << (8 * f) : 0u;
+            const uint32_t inc = wave_sum32(one);
+            tc_t += field_cnt(rdl(inc, 63), lane);
+            if (CH_RANKS && !MG)
+            {
+               // the emit's route ranks (< 64: 6 bits, rows 5 to a register) and the row's
+               // packed field totals (lane r)
+               rkp[r / 5] |= (((inc - one) >> (8 * f)) & 0x3Fu) << (6 * (r % 5));
+               rtv = lane == (uint32_t) r ? rdl(inc, 63) : rtv;
+            }
          }
          if (!first) break;
          first = false;
@@ -1607,7 +1669,7 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
             v = (uint64_t) rdl(tc_t, 1) | (uint64_t) rdl(tc_t, 2) << 12 | (uint64_t) rdl(tc_t, 3) << 24 |
                 (uint64_t) rdl(tc_t, 4) << 36;
          if (lane == G_KO) v = Kout;
-         st1(stw + lane, a.etag | v);
+         sth(a.xcd, stw + lane, a.etag | v);
       }
       CH_STAMP(3);
 
@@ -1729,7 +1791,7 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
       if (!mode && lane < (uint32_t) G_AB)
       {
          const uint32_t x0 = Xr + totA;
-         st1(stw + lane, a.etag | inc_word(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u));
+         sth(a.xcd, stw + lane, a.etag | inc_word(lane, wb + (x0 > totB ? x0 : totB), cin_t + tc_t, 0u));
       }
       CH_STAMP(5);
 
@@ -1805,10 +1867,19 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
          const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
          // route ranks: a packed (8 bits per field) prefix count over the row
          const uint32_t f = (fpack >> (2 * r)) & 3u;
-         const uint32_t one = valid ? 1u << (8 * f) : 0u;
-         const uint32_t inc = wave_sum32(one);
-         const uint32_t rank = ((inc - one) >> (8 * f)) & 0xFFu;
-         const uint32_t rtot = rdl(inc, 63);
+         uint32_t rank, rtot;
+         if (CH_RANKS && !MG)
+         {
+            rank = (rkp[r / 5] >> (6 * (r % 5))) & 0x3Fu;
+            rtot = rdl(rtv, r);
+         }
+         else
+         {
+            const uint32_t one = valid ? 1u << (8 * f) : 0u;
+            const uint32_t inc = wave_sum32(one);
+            rank = ((inc - one) >> (8 * f)) & 0xFFu;
+            rtot = rdl(inc, 63);
+         }
          const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
          const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
          const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
@@ -1825,7 +1896,7 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
             sm.key[kb + rank] = (dn << 32) | id;
             sm.aux[kb + rank] = ax;
          }
-         if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1);
+         if (st) out_record(recs, samp_t, samp_id, (uint64_t) gb + rank, wbase + dn, id, ax, f == 1, a.xcd);
       }
       CH_STAMP(6);
       const bool spilled = (mgr && mo.spilled) || spm != 0;
@@ -1854,13 +1925,13 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
          if (!MG && lane == 0 && ffire != NONE && (fgap == NONE || ffire < fgap)) flag(a, F_FALLBACK | R_MG1);
          const uint32_t mout = mgr ? mo.mode : (fgap == NONE ? 1u : 0u);
          if (MG && mout) mst = mg_after(mst, mgr, n, totA, sp2, Xo);
-         if (MG && mout && lane < 4u) st1(stw + G_MG + lane, a.etag | mst);
-         if (lane < (uint32_t) G_AB) st1(stw + lane, a.etag | inc_word(lane, Xo, run_t, mout));
+         if (MG && mout && lane < 4u) sth(a.xcd, stw + G_MG + lane, a.etag | mst);
+         if (lane < (uint32_t) G_AB) sth(a.xcd, stw + lane, a.etag | inc_word(lane, Xo, run_t, mout));
          if (MG && mout && lane == 0) atomicMax(a.mgk + c, w + 2u);   // window w + 1 may still serve M/G/1
       }
       // POST: the chain outputs before this window and whether it kept any (the next
       // window's spill range at the next port, without waiting for its KO)
-      if (lane == G_POST) st1(stw + G_POST, a.etag | (uint64_t) P0n | (uint64_t) nkeep << 32);
+      if (lane == G_POST) sth(a.xcd, stw + G_POST, a.etag | (uint64_t) P0n | (uint64_t) nkeep << 32);
       // every record of the port has passed at the last window: the route counts (and
       // the exception tails) fill every output slot
       // (only mg_emit writes exception tails of chain outputs: RF, the common windows of
@@ -1913,11 +1984,62 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
    }
 }
 
+// Task dequeue: one head per phase, or (xcd) the queue of the XCD this workgroup runs on.
+// Within a queue tasks are in window start-time order, strictly in order to running
+// workgroups of that XCD: a task's predecessor (same chain, window - 1, same queue) is
+// always held by a running workgroup or done.
+struct Deq
+{
+   const uint32_t* tasks;
+   uint32_t qb, qn;
+   unsigned* head;
+};
+__device__ __forceinline__ Deq deq_init(const ChainArgs& a)
+{
+   Deq d;
+   d.tasks = a.tasks;
+   if (a.xcd)
+   {
+      const uint32_t q = xcc_id();
+      d.qb = a.qoff[q];
+      d.qn = a.qoff[q + 1] - d.qb;
+      d.head = a.qctr + QSTRIDE * q;
+   }
+   else
+   {
+      d.qb = 0;
+      d.qn = a.ntasks;
+      d.head = a.ctr;
+   }
+   return d;
+}
+__device__ __forceinline__ bool deq_next(const ChainArgs& a, const Deq& d, uint32_t& tk)
+{
+   uint32_t k = 0;
+   if (threadIdx.x == 0) k = atomicAdd(d.head, 1u);
+   k = rdl(k, 0);
+   tk = d.qb + k;
+   return k < d.qn && !flagged(a);
+}
+// XCD-local queues: the last workgroup to leave checks that every queue was served (an
+// XCD that got none of the launch's workgroups leaves its chains undone: the run then
+// declines, and the host reruns the batch with the one shared queue).
+__device__ __forceinline__ void deq_exit(const ChainArgs& a)
+{
+   if (!a.xcd || threadIdx.x != 0) return;
+   const unsigned x = atomicAdd(a.qctr + QSTRIDE * NQ, 1u);
+   if (x + 1 != gridDim.x) return;
+   for (uint32_t q = 0; q < NQ; q++)
+   {
+      const unsigned h = __hip_atomic_load(a.qctr + QSTRIDE * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (h < a.qoff[q + 1] - a.qoff[q]) flag(a, F_FALLBACK | R_XCD);
+   }
+}
+
 template <int NL, bool F1, bool LB, bool MG = false>
 __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
 {
    __shared__ Smem sm;
-   const uint32_t ntasks = a.ntasks;
    // an earlier level served a request by M/G/1 (exception tails): the chain's
    // inputs are not in FIFO order -> the level engine reruns the batch
    // the X phase declined: its outputs are incomplete and the batch reruns on levels
@@ -1927,19 +2049,16 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain(ChainArgs a)
       if (threadIdx.x == 0 && blockIdx.x == 0) flag(a, F_FALLBACK | R_EXC);
       return;
    }
-   for (;;)
+   const Deq dq = deq_init(a);
+   uint32_t tk;
+   while (deq_next(a, dq, tk))
    {
-      // in window start-time order, strictly in order to running workgroups: a task's
-      // predecessor (same chain, window - 1) is always held by a running workgroup or done
-      uint32_t tk = 0;
-      if (threadIdx.x == 0) tk = atomicAdd(a.ctr, 1u);
-      tk = rdl(tk, 0);
-      if (tk >= ntasks || flagged(a)) return;
       const uint32_t cw = a.tasks[tk];
       if (LB) task_lb<NL, F1, MG>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
       else task_ser<NL, F1, MG>(sm, a, cw >> 16, cw & 0xFFFFu, tk);
       wsync();
    }
+   deq_exit(a);
 }
 
 // An MG batch whose M/G/1 windows are known (mgk_lim[c]: chain c's windows below it
@@ -1950,19 +2069,16 @@ template <int NL, bool F1, bool LB>
 __global__ __launch_bounds__(T, CH_MINW) void k_chain_mix(ChainArgs a)
 {
    __shared__ Smem sm;
-   const uint32_t ntasks = a.ntasks;
    if (a.fw != 4 && (a.errflag[4] & F_ANY)) return;
    if (a.errflag[2] != 0 && (!a.excfix || (a.errflag[2] & 2u)))
    {
       if (threadIdx.x == 0 && blockIdx.x == 0) flag(a, F_FALLBACK | R_EXC);
       return;
    }
-   for (;;)
+   const Deq dq = deq_init(a);
+   uint32_t tk;
+   while (deq_next(a, dq, tk))
    {
-      uint32_t tk = 0;
-      if (threadIdx.x == 0) tk = atomicAdd(a.ctr, 1u);
-      tk = rdl(tk, 0);
-      if (tk >= ntasks || flagged(a)) return;
       const uint32_t cw = a.tasks[tk], c = cw >> 16, w = cw & 0xFFFFu;
       if (w < a.mgk_lim[c])
       {
@@ -1976,6 +2092,7 @@ __global__ __launch_bounds__(T, CH_MINW) void k_chain_mix(ChainArgs a)
       }
       wsync();
    }
+   deq_exit(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -2249,6 +2366,9 @@ __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict_
    // the neighbouring lane
    const double inv = 1.0 / (double) D;
    auto win = [&](uint64_t t) -> uint64_t {
+      // (a time past 2^52 ps -- never one the submit's checks admit -- is the last
+      // window: the double estimate below stays exact and in range only below it)
+      if (t >= (1ull << 52)) return wl;
       uint64_t q = (uint64_t) ((double) t * inv);
       if (q * D > t) q--;
       else if ((q + 1) * D <= t) q++;
@@ -2545,10 +2665,14 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
          {
             // window of the record: t / D by a double reciprocal and one correction (as k_win_bounds)
             const uint64_t D = s_D[d];
-            uint64_t w = (uint64_t) ((double) o.t * s_inv[d]);
-            if (w * D > o.t) w--;
-            else if ((w + 1) * D <= o.t) w++;
             const uint32_t wl = s_nW[d] - 1;
+            uint64_t w = wl;   // (a time past 2^52 ps: the last window, as k_win_bounds)
+            if (o.t < (1ull << 52))
+            {
+               w = (uint64_t) ((double) o.t * s_inv[d]);
+               if (w * D > o.t) w--;
+               else if ((w + 1) * D <= o.t) w++;
+            }
             atomicMin(&s_bt[d][w < wl ? w : wl], pos);
          }
       }

@@ -221,6 +221,11 @@ struct gnoc_engine
    std::vector<uint64_t> chD_up[2];          // the lengths the device tables hold
    std::vector<ChainWin> h_cw[2];
    std::vector<uint32_t> h_tasks[2];
+   // XCD-local task queues (chain.hip deq_init): per phase the first task of each of the
+   // ch::NQ queues in h_tasks (chains assigned by their windows), the mode the tables
+   // were built for, and whether a run found an XCD without workgroups (then off)
+   std::vector<uint32_t> h_qoff[2];
+   int ch_xcd_tab = -1, ch_xcd_off = 0;
    uint64_t ch_st_words[2] = { 0, 0 }, ch_bt_words[2] = { 0, 0 };
    unsigned* h_nmax = nullptr;               // pinned: per chain fill maxima of the last run
    DevBuf ch_cw, ch_tasks, ch_nmax;
@@ -784,9 +789,19 @@ static bool halve_overflowed(gnoc_engine* e, std::vector<uint64_t>* D)
 // state and bounds blocks; the tasks of each phase in window start-time order
 // (so a task's predecessor, same chain and window - 1, is always handed out
 // first).  Rebuilt only when the lengths change.
+// XCD-local queues (chain.hip deq_init): on by default for a grid that covers every XCD
+// many times over; GNOC_CH_XCD=0 keeps the one shared queue per phase.
+static bool chain_xcd(const gnoc_engine* e)
+{
+   const char* v = std::getenv("GNOC_CH_XCD");
+   if (v && *v && std::atoi(v) == 0) return false;
+   return !e->ch_xcd_off && e->ch_grid >= 64 * (int) ch::NQ;
+}
 static int chain_tables(gnoc_engine* e)
 {
-   if (e->chD_up[0] == e->chD_run[0] && e->chD_up[1] == e->chD_run[1] && e->ch_cw.p) return GNOC_OK;
+   const int xcd = chain_xcd(e) ? 1 : 0;
+   if (e->chD_up[0] == e->chD_run[0] && e->chD_up[1] == e->chD_run[1] && e->ch_cw.p && e->ch_xcd_tab == xcd) return GNOC_OK;
+   e->ch_xcd_tab = xcd;
    const uint32_t lens[2] = { e->dc.W - 1, e->dc.H - 1 }, nls[2] = { 1u, 3u };
    std::vector<std::pair<uint64_t, uint32_t>> order;
    for (int p = 0; p < 2; p++)
@@ -810,20 +825,47 @@ static int chain_tables(gnoc_engine* e)
       }
       std::stable_sort(order.begin(), order.end(),
                        [](const std::pair<uint64_t, uint32_t>& x, const std::pair<uint64_t, uint32_t>& y) { return x.first < y.first; });
-      e->h_tasks[p].resize(order.size());
-      for (size_t k = 0; k < order.size(); k++) e->h_tasks[p][k] = order[k].second;
+      // the chains over the queues: longest processing time first by window count (a
+      // window costs about the same on every chain: each is sized to the same fill)
+      std::vector<uint32_t> qof(cw.size(), 0);
+      const uint32_t nq = xcd ? ch::NQ : 1u;
+      {
+         std::vector<uint32_t> byw(cw.size());
+         for (size_t c = 0; c < cw.size(); c++) byw[c] = (uint32_t) c;
+         std::stable_sort(byw.begin(), byw.end(), [&](uint32_t x, uint32_t y) { return cw[x].nW > cw[y].nW; });
+         std::vector<uint64_t> load(nq, 0);
+         for (uint32_t c : byw)
+         {
+            const uint32_t q = (uint32_t) (std::min_element(load.begin(), load.end()) - load.begin());
+            qof[c] = q;
+            load[q] += cw[c].nW;
+         }
+      }
+      e->h_tasks[p].clear();
+      e->h_tasks[p].reserve(order.size());
+      e->h_qoff[p].assign(ch::NQ + 1, 0);
+      for (uint32_t q = 0; q < nq; q++)
+      {
+         e->h_qoff[p][q] = (uint32_t) e->h_tasks[p].size();
+         for (const auto& o : order)
+            if (qof[o.second >> 16] == q) e->h_tasks[p].push_back(o.second);
+      }
+      for (uint32_t q = nq; q <= ch::NQ; q++) e->h_qoff[p][q] = (uint32_t) e->h_tasks[p].size();
       e->ch_st_words[p] = st;
       e->ch_bt_words[p] = bt;
    }
    const size_t ncw = e->h_cw[0].size() + e->h_cw[1].size(), nt = e->h_tasks[0].size() + e->h_tasks[1].size();
    GNOC_HIP(e, e->ch_cw.ensure(std::max<size_t>(ncw, 1) * sizeof(ChainWin)));
-   GNOC_HIP(e, e->ch_tasks.ensure(std::max<size_t>(nt, 1) * 4));
+   GNOC_HIP(e, e->ch_tasks.ensure((std::max<size_t>(nt, 1) + 2 * (ch::NQ + 1)) * 4));
    GNOC_HIP(e, hipMemcpy(e->ch_cw.p, e->h_cw[0].data(), e->h_cw[0].size() * sizeof(ChainWin), hipMemcpyHostToDevice));
    GNOC_HIP(e, hipMemcpy(e->ch_cw.as<ChainWin>() + e->h_cw[0].size(), e->h_cw[1].data(), e->h_cw[1].size() * sizeof(ChainWin),
                          hipMemcpyHostToDevice));
    GNOC_HIP(e, hipMemcpy(e->ch_tasks.p, e->h_tasks[0].data(), e->h_tasks[0].size() * 4, hipMemcpyHostToDevice));
    GNOC_HIP(e, hipMemcpy(e->ch_tasks.as<uint32_t>() + e->h_tasks[0].size(), e->h_tasks[1].data(), e->h_tasks[1].size() * 4,
                          hipMemcpyHostToDevice));
+   for (int p = 0; p < 2; p++)
+      GNOC_HIP(e, hipMemcpy(e->ch_tasks.as<uint32_t>() + nt + p * (ch::NQ + 1), e->h_qoff[p].data(), (ch::NQ + 1) * 4,
+                            hipMemcpyHostToDevice));
    e->chD_up[0] = e->chD_run[0];
    e->chD_up[1] = e->chD_run[1];
    return GNOC_OK;
@@ -2046,6 +2088,8 @@ constexpr int GNOC_CH_EXC = 1003;        // only the injection level's exception
 constexpr int GNOC_CH_YFALL = 1004;      // only the Y chains declined: Y and SELF levels on k_level
 constexpr int GNOC_INJ_DECLINE = 1007;   // the streamed injection level declined: rerun with it on k_level
 constexpr int GNOC_CH_MG = 1005;         // the chains met the M/G/1 branch: rerun on the MG instantiation
+constexpr int GNOC_CH_XCDOFF = 1008;     // an XCD got none of a chain launch's workgroups: rerun on one shared queue
+constexpr size_t CH_CTR_BYTES = 4096;
 
 // ---------------------------------------------------------------------------
 // v4: chain engine for the X and Y phases (chain.hip); INJ and SELF levels on k_level
@@ -2072,7 +2116,8 @@ static int chain_setup(gnoc_engine* e)
    if (rc) return rc;
    // window bounds and hand-off state: the X phase's, then the Y phase's
    GNOC_HIP(e, e->ch_bt.ensure((e->ch_bt_words[0] + e->ch_bt_words[1] + 1) * 4));
-   GNOC_HIP(e, e->ch_ctr.ensure(256));   // [0, 1] dequeue heads
+   // [0, 1] dequeue heads; XCD-local queues' heads and exit counts from word 64 (X) / 512 (Y)
+   GNOC_HIP(e, e->ch_ctr.ensure(CH_CTR_BYTES));
    // per chain fill maxima, away from the flag word every hand-off poll reads (task-end
    // atomics next to it slowed the polls by half)
    // (then per chain the M/G/1 window bound, k_chain mgk)
@@ -2090,7 +2135,7 @@ static int chain_setup(gnoc_engine* e)
       GNOC_HIP(e, hipMemsetAsync(e->ch_st.p, 0, e->ch_st.bytes, s));
       if (e->ch_epoch == 0) e->ch_epoch = 1;
    }
-   e->zq.push_back({ e->ch_ctr.p, 256 });
+   e->zq.push_back({ e->ch_ctr.p, CH_CTR_BYTES });
    // The hand-off protocol per phase.  GNOC_CHAIN_LOOKBACK=0/1 forces one.  Otherwise,
    // once the windows have settled (this attempt's windows are the previous attempt's),
    // each protocol is timed once on them, the phases as separate launches (the trial
@@ -2163,6 +2208,9 @@ static ChainArgs chain_args(gnoc_engine* e, int phase)
    a.fw = phase ? 5u : 4u;
    a.nexc = e->nexc.as<uint32_t>();
    a.port_mg1 = e->port_mg1.as<unsigned long long>();
+   a.xcd = (uint32_t) e->ch_xcd_tab;
+   a.qoff = e->ch_tasks.as<uint32_t>() + e->h_tasks[0].size() + e->h_tasks[1].size() + phase * (ch::NQ + 1);
+   a.qctr = e->ch_ctr.as<unsigned>() + (phase ? 512 : 64);
    // the Y phase runs after k_exc_merge put the X phase's exception tails (M/G/1-served
    // turns, chain.hip mg_emit) in order
    if (phase && e->dc.analytical) a.excfix = 1;
@@ -2644,6 +2692,13 @@ static int run_post_check(gnoc_engine* e, bool closed_form)
          return fail(e, GNOC_EHIP, m);
       }
       e->ch_yflags = ef[5];
+      // an XCD-local queue was not served (an XCD without workgroups of the launch): the
+      // one shared queue from now on
+      if (cf & ch::R_XCD)
+      {
+         e->ch_xcd_off = 1;
+         return GNOC_CH_XCDOFF;
+      }
       // Reruns that change how the chains run, each at most once per batch (a rerun
       // meets whatever else declined again, so the other reasons wait for it):
       // the injection level left exception tails -> merge them first ...
@@ -3063,6 +3118,11 @@ static int run_impl(gnoc_engine* e)
          if (rc == GNOC_INJ_DECLINE)
          {
             e->inj_declined = 1;
+            e->n_retry++;
+            continue;
+         }
+         if (rc == GNOC_CH_XCDOFF)
+         {
             e->n_retry++;
             continue;
          }
@@ -3642,13 +3702,13 @@ static int finish_check(gnoc_engine* e)
    if (!e->used_chain) return rc;
    // (the sharded path's own Y fallback below; its chains run the common instantiation,
    // which declines where the M/G/1 branch fires and leaves no exception tails)
-   if (rc == GNOC_CH_EXC || rc == GNOC_CH_YFALL || rc == GNOC_CH_MG) rc = GNOC_CH_FALLBACK;
+   if (rc == GNOC_CH_EXC || rc == GNOC_CH_YFALL || rc == GNOC_CH_MG || rc == GNOC_CH_XCDOFF) rc = GNOC_CH_FALLBACK;
    // the MG instantiation's Y chains may have left exception tails in the SELF slots
    const bool mg_ran = e->ch_mg != 0;
    // a decline for a property of the batch (not a hand-off timeout): the M/G/1 branch
    // sends later runs to the MG instantiation once, anything else (or the MG
    // instantiation declining too) to the Y levels straight after the exchange
-   if (rc == GNOC_CH_FALLBACK && (e->ch_yflags & ch::F_FALLBACK) && !(e->ch_yflags & ch::F_TIMEOUT))
+   if (rc == GNOC_CH_FALLBACK && (e->ch_yflags & ch::F_FALLBACK) && !(e->ch_yflags & (ch::F_TIMEOUT | ch::R_XCD)))
    {
       if ((e->ch_yflags & ch::R_MG1) && !mg_ran) e->ch_mg = 1;
       else e->ch_ydeclined = 1;
@@ -3857,6 +3917,21 @@ __attribute__((visibility("default"))) int gnoc_debug_chain_stamps(gnoc_engine* 
    }
    if (!out || !sb.p) return GNOC_OK;
    GNOC_HIP(e, hipMemcpy(out, sb.p, std::min(cap, *count) * 8, hipMemcpyDeviceToHost));
+   return GNOC_OK;
+}
+
+// Debug (tools/chain_stamps.py): the task table of the last chain run, phase 0 (X) or 1
+// (Y): chain << 16 | window per task in dequeue order; out2 (optional) the windows'
+// length D per chain.
+__attribute__((visibility("default"))) int gnoc_debug_chain_tasks(gnoc_engine* e, int phase, uint32_t* out, size_t cap,
+                                                                  size_t* count, uint64_t* dlen, size_t dcap)
+{
+   if (!e || !count || phase < 0 || phase > 1) return GNOC_EINVAL;
+   const std::vector<uint32_t>& t = e->h_tasks[phase];
+   *count = t.size();
+   if (out) std::copy(t.begin(), t.begin() + std::min(cap, t.size()), out);
+   if (dlen)
+      for (size_t c = 0; c < std::min(dcap, e->h_cw[phase].size()); c++) dlen[c] = e->h_cw[phase][c].D;
    return GNOC_OK;
 }
 

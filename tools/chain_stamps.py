@@ -98,6 +98,20 @@ def main():
         busy = task_t[good].sum() / (run.max() * (t1 - t0))
         print(f"  running tasks per 1/{nb} of the phase: " + " ".join(str(x) for x in run))
         print(f"  task-slot utilisation (task time / (peak running x span)): {busy:.3f}")
+        if os.environ.get("CH_STAMPS_DUMP"):
+            # raw per-step stamps for offline analysis: s_memtime stamps 0-7 (low 32 bits),
+            # the step's s_memrealtime end mark, the record counts, and the task table
+            tn = ctypes.c_size_t(0)
+            tf = eng.lib.gnoc_debug_chain_tasks
+            tf.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t,
+                           ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]
+            tf(eng._h, phase, None, 0, ctypes.byref(tn), None, 0)
+            tab = np.zeros(tn.value, np.uint32)
+            dl = np.zeros(4096, np.uint64)
+            tf(eng._h, phase, tab.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), tn.value, ctypes.byref(tn),
+               dl.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), dl.size)
+            np.savez_compressed(f"{os.environ['CH_STAMPS_DUMP']}_{'xy'[phase]}.npz", t=st[:, :, :8].astype(np.uint32),
+                                rt=st[:, :, 9], info=st[:, :, 8], tasks=tab, D=dl)
 
 
 if __name__ == "__main__":
