@@ -66,10 +66,14 @@ constexpr int IROWS = 2;
 constexpr int ICAP = IROWS * T;           // inserts per (port, window); spill-ins of the slow path
 constexpr int SBN = CAP + ICAP;           // stream buffer: kept [0, CAP), inserts [CAP, CAP + ICAP)
 constexpr int BMW = CAP / 32;             // insert bitmap words over merged positions
+#ifndef CH_XCD_ONLY
+#define CH_XCD_ONLY 0     // 1: hand-off stores always kept in the L2 (XCD-local queues only)
+#endif
 #ifndef CH_MINW
 #define CH_MINW 4                         // waves per SIMD the registers must leave room for
 #endif
 constexpr int NLMAX = 3;                  // local insert lists (Y ports: LOCAL, W, E)
+constexpr uint32_t IJ_NWB = 1025;         // window bounds / boundaries kept in LDS: chains of at most 1,024 windows
 // State granules per (chain port, window), each an epoch-tagged u64 written by one
 // sc1 store:
 //   INC  (inclusive, after the look-back): tail X, the 4 cumulative route counts, "no gap yet"
@@ -140,17 +144,36 @@ struct __attribute__((aligned(16))) ChainPort
 };
 static_assert(sizeof(ChainPort) == 128, "ChainPort is one 128-B line");
 
-// One chain's windows: length D (ps), nW of them; its hand-off state block and
-// window-bounds block (offsets into ChainArgs::st / bt).  Chains of a phase may
-// have different windows (each is sized from its own measured fill).
+// One chain's windows: nW of them, window w = [B[w] << qs, B[w+1] << qs) ps with
+// B = wt + wt_off (B[0] = 0, B[nW] = ~0: the last one unbounded; boundaries in units
+// of 2^qs ps so that they fit u32), D the longest (reported); its hand-off state
+// block and window-bounds block (offsets into ChainArgs::st / bt).  Chains of a phase
+// have their own windows, and a chain's windows their own lengths: each window is
+// sized from the fill the previous run measured over its time span (engine.hip
+// adapt_windows).
 struct ChainWin
 {
    uint64_t D;
    uint64_t st_off;               // u64 words: state of (port i, window w) at st_off + (i nW + w) SW
    uint64_t bt_off;               // u32 words: bounds of (port i, list j) at bt_off + (i nl + j)(nW + 1)
+   uint64_t wt_off;               // u32 words: window boundaries B[0 .. nW] at wt_off (and the fills, ChainArgs::wfill)
    uint32_t nW;
    uint32_t pad;
 };
+// The window of time t among B[0 .. nW] (B[0] = 0 <= t): the last w with B[w] <= t >> qs.
+__device__ __forceinline__ uint32_t win_of(const uint32_t* B, uint32_t nW, uint64_t t, uint32_t qs)
+{
+   const uint64_t tq64 = t >> qs;
+   const uint32_t tq = tq64 < 0xFFFFFFFEull ? (uint32_t) tq64 : 0xFFFFFFFEu;
+   uint32_t lo = 0, n = nW;   // B[lo] <= tq; search [lo, lo + n)
+   while (n > 1)
+   {
+      const uint32_t h = n >> 1;
+      if (B[lo + h] <= tq) lo += h, n -= h;
+      else n = h;
+   }
+   return lo;
+}
 
 struct ChainArgs
 {
@@ -168,8 +191,8 @@ struct ChainArgs
    unsigned* errflag;             // [0] route invariant, [2] exception tails exist, [4] chain flags
    unsigned* ctr;                 // dequeue head
    uint32_t nch, len, ntasks, pad2;
-   const ChainWin* cw;            // [nch] windows per chain: window w = [w D, (w + 1) D), the last one unbounded
-   const uint32_t* tasks;         // [ntasks] c << 16 | w, ordered by the window's start time w D
+   const ChainWin* cw;            // [nch] windows per chain
+   const uint32_t* tasks;         // [ntasks] c << 16 | w, ordered by the window's start time
    uint32_t cp0;                  // unused (0)
    uint32_t excfix;               // 1: k_exc_merge put the injection level's exception tails in order
    uint64_t etag;                 // epoch << 48
@@ -187,7 +210,9 @@ struct ChainArgs
    // L2) instead of written through, and read with sc1 loads (L1 bypass, L2-served)
    const uint32_t* qoff;          // [NQ + 1] first task of each queue in `tasks`
    unsigned* qctr;                // queue q's dequeue head at qctr[QSTRIDE q]; the exit count at qctr[QSTRIDE NQ]
-   uint32_t xcd, pad3;
+   uint32_t xcd, qs;              // qs: window boundaries in units of 2^qs ps
+   const uint32_t* wt;            // window boundaries (ChainWin::wt_off)
+   uint32_t* wfill;               // [wt_off + w] the fullest step of window w: stream records | inserts << 16
 };
 
 
@@ -215,7 +240,7 @@ __device__ __forceinline__ void st1(uint64_t* p, uint64_t v)
 // queues (producer and consumer share the XCD's L2), kept in the L2 (sc0).
 __device__ __forceinline__ void sth(uint32_t xcd, uint64_t* p, uint64_t v)
 {
-   if (xcd) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+   if (CH_XCD_ONLY || xcd) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 constexpr uint32_t NQ = 8;        // XCD-local queues (MI355X: 8 XCDs)
@@ -312,9 +337,9 @@ __device__ __forceinline__ void flag(const ChainArgs& a, uint32_t f)
    atomicOr(a.errflag + a.fw, f);
 }
 // A window of chain c overflowed LDS: the run retries, halving that chain's windows.
-__device__ __forceinline__ void flag_overflow(const ChainArgs& a, uint32_t c)
+__device__ __forceinline__ void flag_overflow(const ChainArgs& a, uint32_t c, uint32_t why = 0u)
 {
-   flag(a, F_RETRY);
+   flag(a, F_RETRY | why);
    atomicMax(a.nmax + 2 * c, 0xFFFFFFFFu);
 }
 __device__ __forceinline__ bool flagged(const ChainArgs& a)
@@ -571,13 +596,13 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void out_record(gptr<Rec> recs, gptr<uint64_t> samp_t, gptr<uint32_t> samp_id, uint64_t gp,
                                            uint64_t tn, uint32_t id, uint32_t ax, bool spill, uint32_t xcd)
 {
-   if ((CH_TURN_PLAIN || xcd) && !spill)
+   if ((CH_TURN_PLAIN || CH_XCD_ONLY || xcd) && !spill)
    {
       const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
       q[0] = tn;
       q[1] = (uint64_t) id | ((uint64_t) ax << 32);
    }
-   else if (xcd)
+   else if (CH_XCD_ONLY || xcd)
    {
       // a spill read in this launch by the next window of the chain, on this XCD
       const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
@@ -968,10 +993,14 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
 {
    constexpr bool XC = NL == 1;
    const uint32_t lane = threadIdx.x;
-   const uint64_t D = a.cw[c].D, st_off = a.cw[c].st_off, bt_off = a.cw[c].bt_off;
+   const uint64_t st_off = a.cw[c].st_off, bt_off = a.cw[c].bt_off;
    const uint32_t nW = a.cw[c].nW;
-   const uint64_t wbase = (uint64_t) w * D;
-   const uint32_t wlen = (w + 1 < nW) ? (uint32_t) D : (uint32_t) OFF_LIM;   // kept offsets: t' - wbase < wlen
+   // (wave-uniform: kept in scalar registers)
+   const uint32_t wb0 = (uint32_t) __builtin_amdgcn_readfirstlane((int) a.wt[a.cw[c].wt_off + w]);
+   const uint32_t wb1 = (uint32_t) __builtin_amdgcn_readfirstlane((int) a.wt[a.cw[c].wt_off + w + 1]);
+   const uint64_t wbase = (uint64_t) wb0 << a.qs;
+   const uint32_t wlen = (w + 1 < nW) ? (uint32_t) (((uint64_t) wb1 << a.qs) - wbase)
+                                      : (uint32_t) OFF_LIM;   // kept offsets: t' - wbase < wlen
    const bool lastw = w + 1 >= nW;
    const double fq = a.c.f;
    // base cycle wb: every request of the window has tc >= wb (1 GHz: ceil(t / 1000) > wq - 1;
@@ -1004,7 +1033,7 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
    uint32_t nI = fetch_inserts<NL>(a, pd0, iv);
    if (nI > (uint32_t) ICAP)
    {
-      if (lane == 0) flag_overflow(a, c);
+      if (lane == 0) flag_overflow(a, c, R_OVF_INS);
       return;
    }
    if (land_inserts<NL>(sm, iv, nI, wbase, pd0) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
@@ -1016,7 +1045,7 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
    uint32_t nK = 0;              // this port's kept records
    uint32_t P0cur = 0, nin_prev = 0, ncont_prev = 0;   // this port's chain input: records before / kept / all of this window
    uint32_t ob1p = 0, oc1p = 0;  // the previous port's chain output slot (spill-ins)
-   uint32_t nmax = 0, imax = 0;  // the fullest stream / insert list of this task (window sizing)
+   uint32_t nmax = 0, imax = nI; // the fullest stream / insert list of this task (window sizing)
 
    for (uint32_t i = 0; i < len; i++)
    {
@@ -1082,7 +1111,7 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
          {
             if (itot > (uint32_t) ICAP)
             {
-               if (lane == 0) flag_overflow(a, c);
+               if (lane == 0) flag_overflow(a, c, R_OVF_INS);
                return;
             }
             // the prefetched inserts are consumed only here: tie them to the scan's result so
@@ -1194,7 +1223,7 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
          if (!take) break;                          // nothing merged: the scan stands
          if (n + take > (uint32_t) CAP)
          {
-            if (lane == 0) flag_overflow(a, c);
+            if (lane == 0) flag_overflow(a, c, R_OVF_STREAM);
             return;
          }
          nK = n;
@@ -1380,7 +1409,7 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
       if (!has_next) break;
       if (nkeep + itot > (uint32_t) CAP)
       {
-         if (lane == 0) flag_overflow(a, c);
+         if (lane == 0) flag_overflow(a, c, R_OVF_STREAM);
          return;
       }
       nK = nkeep;
@@ -1397,6 +1426,7 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
    {
       atomicMax(a.nmax + 2 * c, nmax);
       atomicMax(a.nmax + 2 * c + 1, imax);
+      a.wfill[a.cw[c].wt_off + w] = min(nmax, 0xFFFFu) | min(imax, 0xFFFFu) << 16;
    }
 }
 
@@ -1409,10 +1439,14 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
 {
    constexpr bool XC = NL == 1;
    const uint32_t lane = threadIdx.x;
-   const uint64_t D = a.cw[c].D, st_off = a.cw[c].st_off, bt_off = a.cw[c].bt_off;
+   const uint64_t st_off = a.cw[c].st_off, bt_off = a.cw[c].bt_off;
    const uint32_t nW = a.cw[c].nW;
-   const uint64_t wbase = (uint64_t) w * D;
-   const uint32_t wlen = (w + 1 < nW) ? (uint32_t) D : (uint32_t) OFF_LIM;   // kept offsets: t' - wbase < wlen
+   // (wave-uniform: kept in scalar registers)
+   const uint32_t wb0 = (uint32_t) __builtin_amdgcn_readfirstlane((int) a.wt[a.cw[c].wt_off + w]);
+   const uint32_t wb1 = (uint32_t) __builtin_amdgcn_readfirstlane((int) a.wt[a.cw[c].wt_off + w + 1]);
+   const uint64_t wbase = (uint64_t) wb0 << a.qs;
+   const uint32_t wlen = (w + 1 < nW) ? (uint32_t) (((uint64_t) wb1 << a.qs) - wbase)
+                                      : (uint32_t) OFF_LIM;   // kept offsets: t' - wbase < wlen
    const bool lastw = w + 1 >= nW;
    const double fq = a.c.f;
    // base cycle wb: every request of the window has tc >= wb (1 GHz: ceil(t / 1000) > wq - 1;
@@ -1445,7 +1479,7 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
    uint32_t nI = fetch_inserts<NL>(a, pd0, iv);
    if (nI > (uint32_t) ICAP)
    {
-      if (lane == 0) flag_overflow(a, c);
+      if (lane == 0) flag_overflow(a, c, R_OVF_INS);
       return;
    }
    if (land_inserts<NL>(sm, iv, nI, wbase, pd0) && lane == 0) flag(a, F_FALLBACK | R_OFFSET);
@@ -1457,7 +1491,7 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
    uint32_t nK = 0;              // this port's kept records
    uint32_t P0cur = 0, nin_prev = 0;   // the previous port's chain outputs before this window / kept of this window
    uint32_t ob1p = 0, oc1p = 0;  // the previous port's chain output slot (spill-ins)
-   uint32_t nmax = 0, imax = 0;  // the fullest stream / insert list of this task (window sizing)
+   uint32_t nmax = 0, imax = nI; // the fullest stream / insert list of this task (window sizing)
 
    for (uint32_t i = 0; i < len; i++)
    {
@@ -1526,7 +1560,7 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
          {
             if (itot > (uint32_t) ICAP)
             {
-               if (lane == 0) flag_overflow(a, c);
+               if (lane == 0) flag_overflow(a, c, R_OVF_INS);
                return;
             }
             // the prefetched inserts are consumed only here: tie them to the scan's result so
@@ -1649,7 +1683,7 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
          if (!take) break;                          // nothing merged: the scan stands
          if (n + take > (uint32_t) CAP)
          {
-            if (lane == 0) flag_overflow(a, c);
+            if (lane == 0) flag_overflow(a, c, R_OVF_STREAM);
             return;
          }
          nK = n;
@@ -1964,7 +1998,7 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
       if (!has_next) break;
       if (nkeep + itot > (uint32_t) CAP)
       {
-         if (lane == 0) flag_overflow(a, c);
+         if (lane == 0) flag_overflow(a, c, R_OVF_STREAM);
          return;
       }
       nK = nkeep;
@@ -1981,6 +2015,7 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
    {
       atomicMax(a.nmax + 2 * c, nmax);
       atomicMax(a.nmax + 2 * c + 1, imax);
+      a.wfill[a.cw[c].wt_off + w] = min(nmax, 0xFFFFu) | min(imax, 0xFFFFu) << 16;
    }
 }
 
@@ -2028,7 +2063,7 @@ __device__ __forceinline__ void deq_exit(const ChainArgs& a)
 {
    if (!a.xcd || threadIdx.x != 0) return;
    const unsigned x = atomicAdd(a.qctr + QSTRIDE * NQ, 1u);
-   if (x + 1 != gridDim.x) return;
+   if (x + 1 != gridDim.x || flagged(a)) return;   // (an aborted run leaves its queues unfinished)
    for (uint32_t q = 0; q < NQ; q++)
    {
       const unsigned h = __hip_atomic_load(a.qctr + QSTRIDE * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2338,19 +2373,18 @@ __global__ __launch_bounds__(256) void k_chain_plan(DevCfg c, uint32_t ncpx, uin
    out[k] = p;
 }
 
-// One workgroup per (chain port, insert list j < nlrun): bt[w] = first record of
-// the slot with t >= w D (w < nW), bt[nW] = record count.  Window of t:
-// min(t / D, nW - 1) (the last window is unbounded).  The fused launch needs the
-// Y ports' IN_LOCAL lists only (nlrun = 1): their IN_W / IN_E slots are written in
-// that launch (y_bounds).
+// One workgroup per (chain port, insert list j0 + j, j < nlrun): bt[w] = first record
+// of the slot with t at or after window w's start (w < nW), bt[nW] = record count.  The
+// window of t: win_of over the chain's boundaries (the last one is unbounded).
 __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict__ cp, uint32_t nl, uint32_t len,
                                                     const ChainWin* __restrict__ cw, const Rec* __restrict__ recs,
                                                     uint32_t* __restrict__ bt, uint32_t nlrun, uint32_t j0,
-                                                    const unsigned* __restrict__ cond)
+                                                    const unsigned* __restrict__ cond, const uint32_t* __restrict__ wt,
+                                                    uint32_t qs)
 {
    if (cond && *cond == 0) return;   // k_inj_stream wrote these bounds (it did not decline)
+   __shared__ uint32_t sB[IJ_NWB];
    const uint32_t k = blockIdx.x / nlrun, j = j0 + blockIdx.x % nlrun, c = k / len, i = k % len;
-   const uint64_t D = cw[c].D;
    const uint32_t nW = cw[c].nW;
    const uint64_t base = cp[k].ibase[j];
    const uint32_t n = cp[k].icnt[j];
@@ -2361,19 +2395,16 @@ __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict_
       for (uint32_t v = threadIdx.x; v <= nW; v += blockDim.x) b[v] = 0;
       return;
    }
-   // t / D by a double reciprocal and one correction step (t < 2^50, D >= 1024:
-   // the estimate is off by at most one); the previous record's window comes from
-   // the neighbouring lane
-   const double inv = 1.0 / (double) D;
-   auto win = [&](uint64_t t) -> uint64_t {
-      // (a time past 2^52 ps -- never one the submit's checks admit -- is the last
-      // window: the double estimate below stays exact and in range only below it)
-      if (t >= (1ull << 52)) return wl;
-      uint64_t q = (uint64_t) ((double) t * inv);
-      if (q * D > t) q--;
-      else if ((q + 1) * D <= t) q++;
-      return q < wl ? q : wl;
-   };
+   // the chain's window boundaries in LDS (at most IJ_NWB - 1 windows: engine.hip keeps
+   // chains within it), the window of a record by a binary search; the previous record's
+   // window comes from the neighbouring lane
+   const uint32_t* B = wt + cw[c].wt_off;
+   const bool inl = nW + 1 <= IJ_NWB;
+   if (inl)
+      for (uint32_t v = threadIdx.x; v <= nW; v += blockDim.x) sB[v] = B[v];
+   __syncthreads();
+   const uint32_t* Bs = inl ? sB : B;
+   auto win = [&](uint64_t t) -> uint64_t { return win_of(Bs, nW, t, qs); };
    // BW_U rounds of the workgroup per step: their loads are in flight together
    constexpr uint32_t BW_U = 4;
    for (uint32_t i0 = 0; i0 < n; i0 += BW_U * blockDim.x)
@@ -2423,7 +2454,6 @@ __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict_
 #define IJ_PF 1
 #endif
 constexpr uint32_t IJ_T = 256, IJ_PER = IJ_PER_V, IJ_BLK = IJ_T * IJ_PER;
-constexpr uint32_t IJ_NWB = 1025;   // window bounds kept in LDS: chains of at most 1,024 windows
 //
 // With cwx (single-mesh chain runs) it also writes k_win_bounds' bounds of the four
 // chain ports' IN_LOCAL lists it fills (X ports: list 0 of bt; Y ports: list 0 of
@@ -2441,7 +2471,8 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
                                                      unsigned long long* __restrict__ port_last, unsigned* __restrict__ errflag,
                                                      const ChainWin* __restrict__ cwx, uint32_t* __restrict__ btx,
                                                      const ChainWin* __restrict__ cwy, uint32_t* __restrict__ bty,
-                                                     uint32_t stop)
+                                                     uint32_t stop, const uint32_t* __restrict__ wtx,
+                                                     const uint32_t* __restrict__ wty, uint32_t qs)
 {
    // stop (the chain path, nothing queued behind): a decline also flags the X chains
    // (errflag[4]) so that every later kernel of the run returns at once
@@ -2451,9 +2482,9 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
    __shared__ uint64_t s_X;
    __shared__ unsigned long long s_sum[4], s_flit[4];
    __shared__ uint32_t s_bt[4][IJ_NWB], s_nW[4];
-   __shared__ uint64_t s_D[4];
-   __shared__ double s_inv[4];
+   __shared__ uint32_t s_B[4][IJ_NWB];   // the field's chain window boundaries
    __shared__ uint32_t* s_bp[4];
+   __shared__ const uint32_t* s_bx[4];
    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
    const uint32_t tile = blockIdx.x;
    const uint32_t sl = slot_of(tile, P_INJ, IN_LOCAL);
@@ -2494,15 +2525,18 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
          if (ex && cw)
          {
             nW = cw[ch].nW;
-            s_D[tid] = cw[ch].D;
-            s_inv[tid] = 1.0 / (double) cw[ch].D;
             s_bp[tid] = (xd ? btx : bty) + cw[ch].bt_off + (uint64_t) i * (xd ? 1u : 3u) * (nW + 1);
          }
          s_nW[tid] = nW;
+         s_bx[tid] = ex && cw ? (xd ? wtx : wty) + cw[ch].wt_off : nullptr;
       }
       __syncthreads();
       for (uint32_t q = 0; q < 4; q++)
+      {
          for (uint32_t v = tid; v < s_nW[q]; v += IJ_T) s_bt[q][v] = 0xFFFFFFFFu;
+         if (s_nW[q])   // (a field without a chain port -- the mesh edge -- has no boundaries)
+            for (uint32_t v = tid; v <= s_nW[q]; v += IJ_T) s_B[q][v] = s_bx[q][v];
+      }
    }
    // the port starts with no gap in its history tree only if its first request is at cycle 0
    bool nogap = n && c.analytical && cyc_of<F1>(recs[base].t, f) == 0;
@@ -2663,16 +2697,9 @@ __global__ __launch_bounds__(IJ_T) void k_inj_stream(DevCfg c, const uint32_t* _
          }
          if (bnd && s_nW[d])
          {
-            // window of the record: t / D by a double reciprocal and one correction (as k_win_bounds)
-            const uint64_t D = s_D[d];
+            // window of the record among the chain's boundaries (as k_win_bounds)
             const uint32_t wl = s_nW[d] - 1;
-            uint64_t w = wl;   // (a time past 2^52 ps: the last window, as k_win_bounds)
-            if (o.t < (1ull << 52))
-            {
-               w = (uint64_t) ((double) o.t * s_inv[d]);
-               if (w * D > o.t) w--;
-               else if ((w + 1) * D <= o.t) w++;
-            }
+            const uint64_t w = win_of(s_B[d], s_nW[d], o.t, qs);
             atomicMin(&s_bt[d][w < wl ? w : wl], pos);
          }
       }

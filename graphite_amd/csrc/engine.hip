@@ -218,7 +218,19 @@ struct gnoc_engine
    uint64_t h_tlast = 0;                     // last injection time of the batch (k_validate)
    std::vector<uint64_t> chD[2], chCap[2];   // window length; a length that overflowed LDS (0: none)
    std::vector<uint64_t> chD_run[2];         // the attempt in flight
-   std::vector<uint64_t> chD_up[2];          // the lengths the device tables hold
+   std::vector<uint64_t> chD_up[2];          // the window keys the device tables hold (win_key)
+   // variable windows (adapt_windows): per chain its boundaries in ps (nW + 1 of them,
+   // the last ~0), empty while the chain has uniform windows of chD; chB_D the chD
+   // they belong to (a halving changes chD_run and the chain runs uniform windows again)
+   std::vector<std::vector<uint64_t>> chB[2];
+   std::vector<uint64_t> chB_D[2];
+   uint32_t ch_qs = 0;                      // device boundaries in units of 2^qs ps (u32)
+   int ch_adapt_left = 0;                   // variable-window adaptations left for this batch shape
+   std::vector<uint32_t> h_wt;              // both phases' boundaries as the device holds them
+   uint32_t* h_wfill = nullptr;             // (pinned) the last chain run's per-window fills
+   size_t h_wfill_cap = 0;
+   DevBuf ch_wt, ch_wfill;
+   int ch_wfill_read = 0;                   // this run's fills were read back (run_post_enqueue)
    std::vector<ChainWin> h_cw[2];
    std::vector<uint32_t> h_tasks[2];
    // XCD-local task queues (chain.hip deq_init): per phase the first task of each of the
@@ -638,6 +650,7 @@ void gnoc_destroy(gnoc_engine* e)
    if (e->ev0) (void) hipEventDestroy(e->ev0);
    if (e->ev1) (void) hipEventDestroy(e->ev1);
    if (e->h_pinned) (void) hipHostFree(e->h_pinned);
+   if (e->h_wfill) (void) hipHostFree(e->h_wfill);
    if (e->h_val) (void) hipHostFree(e->h_val);
    if (e->h_nmax) (void) hipHostFree(e->h_nmax);
    for (hipEvent_t ev : e->evpool) (void) hipEventDestroy(ev);
@@ -675,6 +688,8 @@ static constexpr double CH_GROW = 1.6;       // most a chain's window grows per 
 static constexpr uint32_t CH_NW_MAX = 4096;
 static constexpr float CH_LB_MARGIN = 0.05f;  // look-back replaces the serial hand-off only when > 5% faster
 static constexpr uint64_t CH_D_MIN = 1024, CH_D_MAX = 1ull << 31;   // 32-bit time offsets in a window
+static constexpr double CH_TARGET_V = 0.85;  // variable windows: each window's predicted fullest step
+static constexpr int CH_ADAPT_RUNS = 3;        // variable-window adaptations per batch shape
 static uint32_t windows_of(uint64_t D, uint64_t t_last) { return (uint32_t) (t_last / D + 1); }
 static uint32_t chain_count(const gnoc_engine* e, int p)
 {
@@ -688,7 +703,36 @@ static uint64_t clamp_window(const gnoc_engine* e, double d)
    uint64_t D = d >= (double) CH_D_MAX ? CH_D_MAX : (uint64_t) d;
    if (D < CH_D_MIN) D = CH_D_MIN;
    if (windows_of(D, t_last) > CH_NW_MAX) D = t_last / (CH_NW_MAX - 1) + 1;
+   // a multiple of the boundaries' unit (2^qs ps)
+   const uint64_t u = 1ull << e->ch_qs;
+   D = std::max(u, (D + u - 1) / u * u);
    return D > CH_D_MAX ? 0 : D;
+}
+// The windows a chain runs in this attempt: its variable boundaries when they belong to
+// the attempt's length, else uniform windows of that length (ps, nW + 1, the last ~0).
+static std::vector<uint64_t> chain_bounds(const gnoc_engine* e, int p, size_t c)
+{
+   if (c < e->chB[p].size() && !e->chB[p][c].empty() && e->chB_D[p][c] == e->chD_run[p][c]) return e->chB[p][c];
+   const uint64_t D = e->chD_run[p][c];
+   const uint32_t nW = windows_of(D, e->h_tlast);
+   std::vector<uint64_t> b(nW + 1);
+   for (uint32_t w = 0; w < nW; w++) b[w] = (uint64_t) w * D;
+   b[nW] = ~0ull;
+   return b;
+}
+// The identity of the attempt's windows per chain (the device tables, the protocol
+// trials and the M/G/1 window limits belong to one): D, or a hash of the boundaries.
+static std::vector<uint64_t> win_key(const gnoc_engine* e, int p)
+{
+   std::vector<uint64_t> k(e->chD_run[p]);
+   for (size_t c = 0; c < k.size(); c++)
+      if (c < e->chB[p].size() && !e->chB[p][c].empty() && e->chB_D[p][c] == e->chD_run[p][c])
+      {
+         uint64_t h = 1469598103934665603ull;
+         for (uint64_t v : e->chB[p][c]) h = (h ^ v) * 1099511628211ull;
+         k[c] = h | (1ull << 63);
+      }
+   return k;
 }
 static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, uint64_t t_last)
 {
@@ -716,6 +760,9 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
    if (fv && std::atoi(fv) > 0) d = (double) (1ull << std::atoi(fv));
    if (pv && std::atoll(pv) > 0) d = (double) std::atoll(pv);
    e->h_tlast = t_last;
+   e->ch_qs = 0;
+   while ((t_last >> e->ch_qs) >= (1ull << 31)) e->ch_qs++;
+   e->ch_adapt_left = CH_ADAPT_RUNS;
    const char* px = std::getenv("GNOC_WINDOW_PS_X");    // experiment knobs: one phase's window size
    const char* py = std::getenv("GNOC_WINDOW_PS_Y");
    e->ch_on = true;
@@ -726,6 +773,8 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
       if (!D) e->ch_on = false;
       e->chD[p].assign(chain_count(e, p), D);
       e->chCap[p].assign(chain_count(e, p), 0);
+      e->chB[p].assign(chain_count(e, p), std::vector<uint64_t>());
+      e->chB_D[p].assign(chain_count(e, p), 0);
    }
    e->ch_declined = 0;
 }
@@ -733,16 +782,106 @@ static void choose_windows(gnoc_engine* e, uint64_t port_max, uint64_t ins_max, 
 // (stream records, inserts) lands near CH_TARGET of the LDS capacity.  Results do
 // not depend on D; a window that overflows later retries with that chain's
 // windows halved, and the overflowing length caps the chain.
+// Variable windows from the run just measured (its per-window fills, k_chain wfill):
+// each window's fullest step (stream records, inserts) over its time span gives a
+// density; new boundaries are placed so that every window's predicted fullest step
+// is CH_TARGET_V of the LDS capacity.  Adopted when a window of the run came close to
+// the capacity, or when the new windows are fewer by more than 5%.  True when the
+// chain was handled here (its windows were measured).
+static bool adapt_chain_variable(gnoc_engine* e, int p, size_t c)
+{
+   if (!e->h_wfill || c >= e->h_cw[p].size()) return false;
+   const ChainWin& cw = e->h_cw[p][c];
+   const uint32_t nW = cw.nW;
+   if (!nW || cw.wt_off + nW >= e->h_wt.size()) return false;
+   const uint32_t qs = e->ch_qs;
+   const uint64_t tl = e->h_tlast + 1;
+   std::vector<uint64_t> b(nW + 1);
+   for (uint32_t w = 0; w < nW; w++) b[w] = (uint64_t) e->h_wt[cw.wt_off + w] << qs;
+   b[nW] = std::max(tl, b[nW - 1] + 1);   // (the last window's span: up to the last injection)
+   std::vector<double> rn(nW), ri(nW);
+   uint32_t mx = 0;
+   for (uint32_t w = 0; w < nW; w++)
+   {
+      const uint32_t f = e->h_wfill[cw.wt_off + w];
+      const uint32_t n = f & 0xFFFFu, ni = f >> 16;
+      mx = std::max(mx, n);
+      const double len = (double) std::max<uint64_t>(b[w + 1] - b[w], 1);
+      rn[w] = (double) std::max(n, 1u) / len;
+      ri[w] = (double) ni / len;
+   }
+   const double tn = CH_TARGET_V * ch::CAP, ti = 0.85 * ch::ICAP;
+   const uint64_t u = 1ull << qs;
+   const uint64_t dmin = std::max(u, (CH_D_MIN + u - 1) / u * u), dmax = CH_D_MAX / u * u;
+   std::vector<uint64_t> nb{ 0 };
+   uint64_t s0 = 0, dlong = 0;
+   uint32_t w = 0;
+   for (;;)
+   {
+      // extend the window from s0 through the old windows' densities
+      double an = 0, ai = 0;
+      uint64_t t = s0, e1 = ~0ull;
+      while (w < nW && b[w + 1] <= t) w++;
+      for (uint32_t k = w; k < nW; k++)
+      {
+         const uint64_t lo = std::max(t, b[k]), hi = b[k + 1];
+         double room = rn[k] > 0 ? (tn - an) / rn[k] : 1e300;
+         if (ri[k] > 0) room = std::min(room, (ti - ai) / ri[k]);
+         if ((double) lo + room < (double) hi)
+         {
+            e1 = lo + (uint64_t) std::max(room, 0.0);
+            break;
+         }
+         an += rn[k] * (double) (hi - lo);
+         ai += ri[k] * (double) (hi - lo);
+      }
+      // (at most CH_GROW times the run's window there: bursts it did not see)
+      const uint64_t grow = (uint64_t) (CH_GROW * (double) (b[std::min(w, nW - 1) + 1] - b[std::min(w, nW - 1)]));
+      if (e1 > s0 + grow) e1 = s0 + grow;   // (also where the target is not reached before the end)
+      if (e1 == ~0ull || e1 >= tl) break;   // the rest is the last window
+      uint64_t len = e1 > s0 ? (e1 - s0) / u * u : 0;
+      len = std::min(std::max(len, dmin), dmax);
+      s0 += len;
+      if (s0 >= tl) break;
+      nb.push_back(s0);
+      dlong = std::max(dlong, len);
+      if (nb.size() > std::min<size_t>(CH_NW_MAX, ch::IJ_NWB - 1)) return true;   // too many: keep the run's windows
+   }
+   nb.push_back(~0ull);
+   const uint32_t nWn = (uint32_t) nb.size() - 1;
+   const bool hot = mx > 0.97 * ch::CAP;
+   if (std::getenv("GNOC_CHAIN_DEBUG") && nW <= 40)
+   {
+      std::fprintf(stderr, "gnoc: adapt phase %d chain %zu: %u windows ->", p, c, nW);
+      for (uint32_t k = 0; k < nW; k++)
+         std::fprintf(stderr, " [%llu %u/%u]", (unsigned long long) b[k], e->h_wfill[cw.wt_off + k] & 0xFFFFu,
+                      e->h_wfill[cw.wt_off + k] >> 16);
+      std::fprintf(stderr, "\n   new %u:", nWn);
+      for (uint32_t k = 0; k < nWn; k++) std::fprintf(stderr, " %llu", (unsigned long long) nb[k]);
+      std::fprintf(stderr, "\n");
+   }
+   if (!hot && nWn * 100 > nW * 95) return true;   // close enough: no churn
+   e->chB[p][c] = nb;
+   e->chD[p][c] = std::max(dlong, dmin);
+   e->chB_D[p][c] = e->chD[p][c];
+   return true;
+}
 static void adapt_windows(gnoc_engine* e)
 {
    if (std::getenv("GNOC_WINDOW_SHIFT") || std::getenv("GNOC_WINDOW_PS") || std::getenv("GNOC_WINDOW_PS_X") ||
        std::getenv("GNOC_WINDOW_PS_Y"))
       return;
+   const char* vv = std::getenv("GNOC_CH_VARWIN");   // 0: uniform windows per chain only
+   const bool var = e->ch_adapt_left > 0 && e->ch_wfill_read && !(vv && *vv && std::atoi(vv) == 0);
+   if (e->ch_adapt_left > 0) e->ch_adapt_left--;
    const unsigned* nm = e->h_nmax;
    for (int p = 0; p < 2; p++)
    {
       for (size_t c = 0; c < e->chD[p].size(); c++)
       {
+         if (var && adapt_chain_variable(e, p, c)) continue;
+         // (a chain on variable windows keeps them once they settled)
+         if (c < e->chB[p].size() && !e->chB[p][c].empty() && e->chB_D[p][c] == e->chD[p][c]) continue;
          const unsigned n = nm[2 * c], ni = nm[2 * c + 1];
          if (!n || n == 0xFFFFFFFFu) continue;
          double r = CH_TARGET * ch::CAP / (double) n;
@@ -776,6 +915,29 @@ static bool halve_overflowed(gnoc_engine* e, std::vector<uint64_t>* D)
       {
          if (any && nm[2 * c] != 0xFFFFFFFFu) continue;
          uint64_t& d = D[p][c];
+         if (c < e->chB[p].size() && !e->chB[p][c].empty() && e->chB_D[p][c] == d)
+         {
+            // variable windows: each one split in two (the chain keeps its shape)
+            const std::vector<uint64_t>& b = e->chB[p][c];
+            const uint64_t u = 1ull << e->ch_qs;
+            std::vector<uint64_t> nb;
+            for (size_t w = 0; w + 1 < b.size(); w++)
+            {
+               nb.push_back(b[w]);
+               const uint64_t hi = w + 2 < b.size() ? b[w + 1] : std::max<uint64_t>(b[w] + 2 * u, e->h_tlast + 1);
+               const uint64_t mid = b[w] + (hi - b[w]) / 2 / u * u;
+               if (mid > b[w] && mid < hi && (w + 2 < b.size() || mid <= e->h_tlast)) nb.push_back(mid);
+            }
+            nb.push_back(~0ull);
+            if (nb.size() - 1 > std::min<size_t>(CH_NW_MAX, ch::IJ_NWB - 1) || d < 2 * CH_D_MIN) ok = false;
+            else
+            {
+               e->chB[p][c] = nb;
+               d /= 2;
+               e->chB_D[p][c] = d;
+            }
+            continue;
+         }
          if (!e->chCap[p][c] || d < e->chCap[p][c]) e->chCap[p][c] = d;
          if (d < 2 * CH_D_MIN || 2ull * windows_of(d, e->h_tlast) > CH_NW_MAX) ok = false;
          else d /= 2;
@@ -800,10 +962,12 @@ static bool chain_xcd(const gnoc_engine* e)
 static int chain_tables(gnoc_engine* e)
 {
    const int xcd = chain_xcd(e) ? 1 : 0;
-   if (e->chD_up[0] == e->chD_run[0] && e->chD_up[1] == e->chD_run[1] && e->ch_cw.p && e->ch_xcd_tab == xcd) return GNOC_OK;
+   const std::vector<uint64_t> key[2] = { win_key(e, 0), win_key(e, 1) };
+   if (e->chD_up[0] == key[0] && e->chD_up[1] == key[1] && e->ch_cw.p && e->ch_xcd_tab == xcd) return GNOC_OK;
    e->ch_xcd_tab = xcd;
    const uint32_t lens[2] = { e->dc.W - 1, e->dc.H - 1 }, nls[2] = { 1u, 3u };
    std::vector<std::pair<uint64_t, uint32_t>> order;
+   e->h_wt.clear();
    for (int p = 0; p < 2; p++)
    {
       auto& cw = e->h_cw[p];
@@ -812,16 +976,22 @@ static int chain_tables(gnoc_engine* e)
       order.clear();
       for (size_t c = 0; c < cw.size(); c++)
       {
-         const uint64_t D = e->chD_run[p][c];
-         const uint32_t nW = windows_of(D, e->h_tlast);
-         cw[c].D = D;
+         // the chain's windows, [b[w], b[w + 1]), the last one unbounded
+         const std::vector<uint64_t> b = chain_bounds(e, p, c);
+         const uint32_t nW = (uint32_t) b.size() - 1;
+         uint64_t dlong = e->chD_run[p][c];
+         for (uint32_t w = 0; w + 1 < nW; w++) dlong = std::max(dlong, b[w + 1] - b[w]);
+         cw[c].D = dlong;
          cw[c].nW = nW;
          cw[c].st_off = st;
          cw[c].bt_off = bt;
+         cw[c].wt_off = e->h_wt.size();
          cw[c].pad = 0;
+         for (uint32_t w = 0; w < nW; w++) e->h_wt.push_back((uint32_t) (b[w] >> e->ch_qs));
+         e->h_wt.push_back(0xFFFFFFFFu);
          st += (uint64_t) lens[p] * nW * ch::SW;
          bt += (uint64_t) lens[p] * nls[p] * (nW + 1);
-         for (uint32_t w = 0; w < nW; w++) order.push_back({ (uint64_t) w * D, (uint32_t) (c << 16) | w });
+         for (uint32_t w = 0; w < nW; w++) order.push_back({ b[w], (uint32_t) (c << 16) | w });
       }
       std::stable_sort(order.begin(), order.end(),
                        [](const std::pair<uint64_t, uint32_t>& x, const std::pair<uint64_t, uint32_t>& y) { return x.first < y.first; });
@@ -866,8 +1036,21 @@ static int chain_tables(gnoc_engine* e)
    for (int p = 0; p < 2; p++)
       GNOC_HIP(e, hipMemcpy(e->ch_tasks.as<uint32_t>() + nt + p * (ch::NQ + 1), e->h_qoff[p].data(), (ch::NQ + 1) * 4,
                             hipMemcpyHostToDevice));
-   e->chD_up[0] = e->chD_run[0];
-   e->chD_up[1] = e->chD_run[1];
+   // window boundaries, and the per-window fills the runs report (read back while the
+   // windows still adapt)
+   GNOC_HIP(e, e->ch_wt.ensure(std::max<size_t>(e->h_wt.size(), 1) * 4));
+   GNOC_HIP(e, e->ch_wfill.ensure(std::max<size_t>(e->h_wt.size(), 1) * 4));
+   GNOC_HIP(e, hipMemcpy(e->ch_wt.p, e->h_wt.data(), e->h_wt.size() * 4, hipMemcpyHostToDevice));
+   if (e->h_wfill_cap < e->h_wt.size())
+   {
+      if (e->h_wfill) (void) hipHostFree(e->h_wfill);
+      e->h_wfill = nullptr;
+      e->h_wfill_cap = 0;
+      GNOC_HIP(e, hipHostMalloc((void**) &e->h_wfill, e->h_wt.size() * 4, hipHostMallocDefault));
+      e->h_wfill_cap = e->h_wt.size();
+   }
+   e->chD_up[0] = key[0];
+   e->chD_up[1] = key[1];
    return GNOC_OK;
 }
 
@@ -2066,7 +2249,8 @@ static int inj_level(gnoc_engine* e)
                e->slot_base.as<uint64_t>(), e->recs.as<Rec>(), e->samp_t.as<uint64_t>(), e->samp_id.as<uint32_t>(),  \
                e->port_sum.as<unsigned long long>(), e->port_cnt.as<unsigned long long>(),                          \
                e->port_flit.as<unsigned long long>(), e->port_last.as<unsigned long long>(),                        \
-               e->counters.as<unsigned>() + 8, cwx, btx, cwy, bty, (uint32_t) chain_bounds)
+               e->counters.as<unsigned>() + 8, cwx, btx, cwy, bty, (uint32_t) chain_bounds,                         \
+               (const uint32_t*) e->ch_wt.as<uint32_t>(), (const uint32_t*) e->ch_wt.as<uint32_t>(), e->ch_qs)
    if (e->f1) GNOC_INJS(true);
    else GNOC_INJS(false);
 #undef GNOC_INJS
@@ -2144,17 +2328,18 @@ static int chain_setup(gnoc_engine* e)
    // (configs[1]'s uniform X phase) keep the serial protocol in every process.  Until a
    // decision exists, serial.
    const char* lbv = std::getenv("GNOC_CHAIN_LOOKBACK");
-   const bool settled = e->chD_run[0] == e->ch_prevD[0] && e->chD_run[1] == e->ch_prevD[1];
-   e->ch_prevD[0] = e->chD_run[0];
-   e->ch_prevD[1] = e->chD_run[1];
+   const std::vector<uint64_t> wkey[2] = { win_key(e, 0), win_key(e, 1) };
+   const bool settled = wkey[0] == e->ch_prevD[0] && wkey[1] == e->ch_prevD[1];
+   e->ch_prevD[0] = wkey[0];
+   e->ch_prevD[1] = wkey[1];
    e->ch_trial = 0;
    for (int p = 0; p < 2; p++)
    {
       if (!e->ch_ev[p][0]) GNOC_HIP(e, hipEventCreate(&e->ch_ev[p][0]));
       if (!e->ch_ev[p][1]) GNOC_HIP(e, hipEventCreate(&e->ch_ev[p][1]));
-      if (e->ch_lb_D[p] != e->chD_run[p])
+      if (e->ch_lb_D[p] != wkey[p])
       {
-         e->ch_lb_D[p] = e->chD_run[p];
+         e->ch_lb_D[p] = wkey[p];
          e->ch_lb_ms[p][0] = e->ch_lb_ms[p][1] = -1.f;
       }
       const float* m = e->ch_lb_ms[p];
@@ -2211,6 +2396,9 @@ static ChainArgs chain_args(gnoc_engine* e, int phase)
    a.xcd = (uint32_t) e->ch_xcd_tab;
    a.qoff = e->ch_tasks.as<uint32_t>() + e->h_tasks[0].size() + e->h_tasks[1].size() + phase * (ch::NQ + 1);
    a.qctr = e->ch_ctr.as<unsigned>() + (phase ? 512 : 64);
+   a.qs = e->ch_qs;
+   a.wt = e->ch_wt.as<uint32_t>();
+   a.wfill = e->ch_wfill.as<uint32_t>();
    // the Y phase runs after k_exc_merge put the X phase's exception tails (M/G/1-served
    // turns, chain.hip mg_emit) in order
    if (phase && e->dc.analytical) a.excfix = 1;
@@ -2239,10 +2427,10 @@ static int chain_phase(gnoc_engine* e, int phase)
    const unsigned* icond = nullptr;
    if ((phase == 0 && !ibnd) || (phase == 1 && !e->ch_ylocal))
       GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * nl), dim3(256), 0, s, a.cp, nl, a.len, a.cw, e->recs.as<Rec>(),
-                  const_cast<uint32_t*>(a.bt), nl, 0u, phase == 0 ? icond : nullptr);
+                  const_cast<uint32_t*>(a.bt), nl, 0u, phase == 0 ? icond : nullptr, a.wt, a.qs);
    else if (phase == 1)
       GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(ncp * 2), dim3(256), 0, s, a.cp, nl, a.len, a.cw, e->recs.as<Rec>(),
-                  const_cast<uint32_t*>(a.bt), 2u, 1u, (const unsigned*) nullptr);
+                  const_cast<uint32_t*>(a.bt), 2u, 1u, (const unsigned*) nullptr, a.wt, a.qs);
    if (phase == 0)
    {
       if (ylocal)
@@ -2250,7 +2438,7 @@ static int chain_phase(gnoc_engine* e, int phase)
          const ChainArgs ay = chain_args(e, 1);
          if (!ibnd)
             GNOC_LAUNCH(e, KC_BOUNDS, ch::k_win_bounds, dim3(e->ncpy), dim3(256), 0, s, ay.cp, 3u, ay.len, ay.cw,
-                        e->recs.as<Rec>(), const_cast<uint32_t*>(ay.bt), 1u, 0u, icond);
+                        e->recs.as<Rec>(), const_cast<uint32_t*>(ay.bt), 1u, 0u, icond, ay.wt, ay.qs);
          e->ch_ylocal = 1;
       }
    }
@@ -2269,7 +2457,7 @@ static int chain_phase(gnoc_engine* e, int phase)
    // the MG path (each chain's first windows), the rest of the phase the common one, in
    // one launch (k_chain_mix)
    const std::vector<uint32_t>& mk = e->h_mgk[phase];
-   const bool split = e->ch_mg && e->mgk_ok && e->mgk_D[phase] == e->chD_run[phase] && !a.stamps && e->nranks <= 1 &&
+   const bool split = e->ch_mg && e->mgk_ok && e->mgk_D[phase] == win_key(e, phase) && !a.stamps && e->nranks <= 1 &&
                       mk.size() == (size_t) a.nch && !std::getenv("GNOC_MG_SPLIT_OFF");
    if (split)
    {
@@ -2641,6 +2829,13 @@ static int run_post_enqueue(gnoc_engine* e, bool closed_form)
       if (e->used_chain)
          GNOC_HIP(e, hipMemcpyAsync(e->h_nmax, e->ch_nmax.p, 12 * (e->h_cw[0].size() + e->h_cw[1].size()),
                                     hipMemcpyDeviceToHost, s));
+      // the per-window fills, while the windows adapt (adapt_windows)
+      e->ch_wfill_read = 0;
+      if (e->used_chain && e->ch_adapt_left > 0 && e->h_wfill && e->h_wt.size() <= e->h_wfill_cap)
+      {
+         GNOC_HIP(e, hipMemcpyAsync(e->h_wfill, e->ch_wfill.p, e->h_wt.size() * 4, hipMemcpyDeviceToHost, s));
+         e->ch_wfill_read = 1;
+      }
    }
    return GNOC_OK;
 }
@@ -2733,8 +2928,8 @@ static int run_post_check(gnoc_engine* e, bool closed_form)
       const unsigned* mk = e->h_nmax + 2 * (n0 + n1);
       e->h_mgk[0].assign(mk, mk + n0);
       e->h_mgk[1].assign(mk + n0, mk + n0 + n1);
-      e->mgk_D[0] = e->chD_run[0];
-      e->mgk_D[1] = e->chD_run[1];
+      e->mgk_D[0] = win_key(e, 0);
+      e->mgk_D[1] = win_key(e, 1);
       e->mgk_ok = 1;
    }
    e->ran = true;

@@ -66,3 +66,28 @@ def test_sweep_256_points_full_grid():
         pts.append(gnoc.SweepPoint(fw, r, int(np.ceil(0.01 * tw)), tw))
         trs.append(gnoc.synthetic_trace(8, 8, load, 12, seed=1000 + k))
     check_points(base, pts, trs)
+
+
+def test_sweep_256_points_benched_length_pinned():
+    """BASELINE.json configs[4] at the length bench.py times it: all 256 points at
+    2,000 packets per tile (bench.py's seeds), one batch, every point's eight result
+    arrays against the oracle's SHA-256 (tests/golden/make_sweep.py).  The saturated
+    points' long queues and M/G/1 requests are exercised here at full length."""
+    import json
+    import os
+    from tests.golden import make_sweep as ms
+    with open(os.path.join(os.path.dirname(__file__), "golden", "sweep_hashes.json")) as fh:
+        gold = json.load(fh)
+    pts = ms.points()
+    trs = [ms.trace(i, load) for i, (_, load) in enumerate(pts)]
+    for i in (0, 127, 255):
+        assert ms.trace_hash(trs[i]) == gold["points"][i]["trace_sha256"], "sweep trace generator changed"
+    eng = gnoc.SweepEngine(gnoc.EngineConfig(num_tiles=64), [q for q, _ in pts])
+    eng.submit(trs)
+    for _ in range(2):
+        eng.run()
+        got = eng.results()
+        bad = [i for i in range(len(pts)) if ms.point_hash(got[i]) != gold["points"][i]["hash"]]
+        assert not bad, f"{len(bad)} points differ from the oracle, first {bad[0]}: {pts[bad[0]]}"
+    print("sweep engine path", eng.summary()["engine_path"], "mg1 uses", sum(p["mg1_uses"] for p in gold["points"]))
+    eng.close()

@@ -24,7 +24,9 @@ def main():
         eng.run()
         ms.append(round(eng.summary()["last_run_ms"], 3))
     s = eng.summary()
-    print("lib", os.environ.get("GNOC_LIB", "default"), "path", s["engine_path"], "ms", ms, flush=True)
+    print("lib", os.environ.get("GNOC_LIB", "default"), "path", s["engine_path"], "ms", ms,
+          "windows", s.get("windows"), s.get("windows_y"), "reruns", s.get("retries_total"), s.get("fallbacks_total"),
+          flush=True)
     if os.environ.get("GNOC_PROBE_PROF"):
         eng.set_profiling(True)
         eng.run()
