@@ -2375,15 +2375,26 @@ __global__ __launch_bounds__(256) void k_chain_plan(DevCfg c, uint32_t ncpx, uin
 
 // One workgroup per (chain port, insert list j0 + j, j < nlrun): bt[w] = first record
 // of the slot with t at or after window w's start (w < nW), bt[nW] = record count.  The
-// window of t: win_of over the chain's boundaries (the last one is unbounded).
+// window of t: win_of over the chain's boundaries (the last one is unbounded), so
+// bt[w] (0 < w < nW) is the first record whose key t >> qs reaches B[w].  Slots of up
+// to WB_SMAX samples search: the slot's 1-in-64 key samples (written by its producer)
+// in LDS, one thread per boundary, then the 63 records after the sample in HBM; the
+// slot's records themselves are not streamed.  Larger slots scan every record.
+constexpr uint32_t WB_SMAX = 4096;
+__device__ __forceinline__ uint32_t key_of(uint64_t t, uint32_t qs)
+{
+   const uint64_t tq64 = t >> qs;
+   return tq64 < 0xFFFFFFFEull ? (uint32_t) tq64 : 0xFFFFFFFEu;   // (as win_of)
+}
 __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict__ cp, uint32_t nl, uint32_t len,
                                                     const ChainWin* __restrict__ cw, const Rec* __restrict__ recs,
-                                                    uint32_t* __restrict__ bt, uint32_t nlrun, uint32_t j0,
-                                                    const unsigned* __restrict__ cond, const uint32_t* __restrict__ wt,
-                                                    uint32_t qs)
+                                                    const uint64_t* __restrict__ samp_t, uint32_t* __restrict__ bt,
+                                                    uint32_t nlrun, uint32_t j0, const unsigned* __restrict__ cond,
+                                                    const uint32_t* __restrict__ wt, uint32_t qs)
 {
    if (cond && *cond == 0) return;   // k_inj_stream wrote these bounds (it did not decline)
    __shared__ uint32_t sB[IJ_NWB];
+   __shared__ uint32_t sS[WB_SMAX];
    const uint32_t k = blockIdx.x / nlrun, j = j0 + blockIdx.x % nlrun, c = k / len, i = k % len;
    const uint32_t nW = cw[c].nW;
    const uint64_t base = cp[k].ibase[j];
@@ -2395,10 +2406,49 @@ __global__ __launch_bounds__(256) void k_win_bounds(const ChainPort* __restrict_
       for (uint32_t v = threadIdx.x; v <= nW; v += blockDim.x) b[v] = 0;
       return;
    }
+   const uint32_t* B = wt + cw[c].wt_off;
+   const uint32_t ns = (n + 63) / 64;
+   if (ns <= WB_SMAX)
+   {
+      // (slot bases are 64-record aligned: sample s is record 64 s of the slot)
+      const uint64_t* sp = samp_t + (base >> 6);
+      for (uint32_t s = threadIdx.x; s < ns; s += blockDim.x) sS[s] = key_of(sp[s], qs);
+      __syncthreads();
+      const Rec* r = recs + base;
+      for (uint32_t v = threadIdx.x; v <= nW; v += blockDim.x)
+      {
+         uint32_t res = n;
+         if (v == 0) res = 0;
+         else if (v < nW)
+         {
+            const uint32_t key = B[v];
+            uint32_t lo = 0, hi = ns;   // first sample at or past key
+            while (lo < hi)
+            {
+               const uint32_t m = (lo + hi) >> 1;
+               if (sS[m] < key) lo = m + 1;
+               else hi = m;
+            }
+            if (lo == 0) res = 0;
+            else
+            {
+               uint32_t a = 64 * (lo - 1) + 1, e = min(64 * lo, n);   // record 64 (lo - 1) is below key
+               while (a < e)
+               {
+                  const uint32_t m = (a + e) >> 1;
+                  if (key_of(r[m].t, qs) < key) a = m + 1;
+                  else e = m;
+               }
+               res = a;
+            }
+         }
+         b[v] = res;
+      }
+      return;
+   }
    // the chain's window boundaries in LDS (at most IJ_NWB - 1 windows: engine.hip keeps
    // chains within it), the window of a record by a binary search; the previous record's
    // window comes from the neighbouring lane
-   const uint32_t* B = wt + cw[c].wt_off;
    const bool inl = nW + 1 <= IJ_NWB;
    if (inl)
       for (uint32_t v = threadIdx.x; v <= nW; v += blockDim.x) sB[v] = B[v];
