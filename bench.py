@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--cpu-sample-ppt", type=int, default=1000)
     ap.add_argument("--verify", type=int, default=0, help="also check the GPU result vs the oracle (slow)")
     ap.add_argument("--hotspot", type=int, default=1, help="also time the hotspot half of configs[1] (N=1 mesh)")
+    ap.add_argument("--e2e", type=int, default=1, help="also time end to end (host trace -> host results)")
     ap.add_argument("--workload", choices=("auto", "mesh", "sharded", "replicas", "sweep"), default="auto",
                     help="auto: one 32x32 mesh at N=1, one 64x64 mesh sharded over N ranks at N>1")
     return ap.parse_args()
@@ -129,7 +130,7 @@ def main():
     # run, final_ps back into a pinned host array; reported beside the HBM-resident value
     e2e_ms = e2e_serial_ms = e2e_wide_ms = e2e_fin_ms = e2e_narrow_ms = None
     wire = None
-    if not sharded:
+    if not sharded and a.e2e:
         ptr = pinned_trace(tr)
         fins = [torch.empty(len(tr), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64) for _ in range(2)]
         lats = [pinned_array(len(tr), np.uint32) for _ in range(2)]
@@ -534,7 +535,7 @@ def pinned_trace(tr):
                       pin(tr.flags if tr.flags is not None else np.zeros(len(tr), np.uint32)))
 
 
-PMC_FILE = "r5_pmc.json"
+PMC_FILE = "r6_pmc.json"
 
 
 def pmc_traffic(workload, kernel, bid):

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 TAG=${1:-r1}
 P=gpurun_out/prof_$TAG
 mkdir -p $P ${P}_hot
-BENCH="bench.py --steps 10 --warmup 2 --cpu-baseline 0 --hotspot 0"   # the first run sizes the chain windows: a small share of the average
+BENCH="bench.py --steps 10 --warmup 2 --cpu-baseline 0 --hotspot 0 --e2e 0"   # the first run sizes the chain windows: a small share of the average
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1 &&
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err &&
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $P -o run -- python3 -u $BENCH > $P/bench_kt.json 2>&1 &&

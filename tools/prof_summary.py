@@ -36,6 +36,15 @@ for r in kt:
 print("kernel                calls   avg_us   total_ms")
 for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
     print(f"{k:20s} {len(v):6d} {sum(v) / len(v) / 1e3:8.2f} {sum(v) / 1e6:10.3f}")
+# the profiled command's first runs size the chain windows (different windows, and a
+# first run that adapts them): the steady state is the launches after those runs
+STEADY = 20
+for k in ("k_chain", "k_level"):
+    v = per.get(k, [])
+    if len(v) > STEADY:
+        t = v[-STEADY:]
+        print(f"{k} steady state (its last {STEADY} launches, after the window settle runs): avg_us "
+              f"{sum(t) / len(t) / 1e3:.2f}, min {min(t) / 1e3:.2f}, max {max(t) / 1e3:.2f}")
 
 # one step = the kernels from a k_classify launch to the next k_finalize; use the
 # last complete step: its kernels, busy time, span and the gaps between launches
@@ -87,9 +96,11 @@ for k in [dom] + [x for x in ("k_chain", "k_level") if x != dom]:
     fb = 2 * 1024 * sum(fe) / len(fe)
     wb = 1024 * sum(wr) / len(wr)
     avg_us = sum(per[k]) / len(per[k]) / 1e3 if per.get(k) else None
+    st = per.get(k, [])[-STEADY:]
     out["per_kernel"][k] = {"launches_fetch": len(fe), "launches_write": len(wr),
                             "fetch_bytes_per_launch_corrected": fb, "write_bytes_per_launch": wb,
-                            "traffic_bytes_per_launch": fb + wb, "kernel_trace_avg_us": avg_us}
+                            "traffic_bytes_per_launch": fb + wb, "kernel_trace_avg_us": avg_us,
+                            "kernel_trace_steady_avg_us": sum(st) / len(st) / 1e3 if st else None}
     print("\nPMC per %s launch: fetch %.1f MB (corrected), write %.1f MB, total %.1f MB" % (k, fb / 1e6, wb / 1e6, (fb + wb) / 1e6))
 if dom in out["per_kernel"]:
     out.update(out["per_kernel"][dom])
