@@ -565,7 +565,7 @@ __global__ __launch_bounds__(STHREADS) void k_port_stream(DevCfg c, const uint32
             {
                const uint64_t fin = tn + ps_of<F1>(aux_F(ax), c.f);
                if (bcr) c.bc_fin[v] = fin;
-               else final_ps[id] = fin;
+               else if (id < c.npk) final_ps[id] = fin;   // (a record's id indexes the batch: bounded as k_level's)
                continue;
             }
             Rec o;
