@@ -2089,17 +2089,19 @@ static int run_levels_v1(gnoc_engine* e)
 // ---------------------------------------------------------------------------
 // v3: device-planned chunked levels
 // ---------------------------------------------------------------------------
-// Records per chunk: LV_CTGT, or GNOC_CHUNK (test knob: small chunks put serial
+// Records per chunk: LV_CTGT for the chain path's injection and SELF levels,
+// LV_CTGT_FULL when every level runs on k_level (levels of X / Y ports, with more
+// chunks per level in flight), or GNOC_CHUNK (test knob: small chunks put serial
 // M/G/1 prefixes and exception tails across many chunk boundaries).
-static uint32_t chunk_target()
+static uint32_t chunk_target(bool full = true)
 {
    const char* v = std::getenv("GNOC_CHUNK");
    const long t = v ? std::atol(v) : 0;
-   return t > 0 ? (uint32_t) std::min<long>(std::max<long>(t, 64), LV_CMAX) : LV_CTGT;
+   return t > 0 ? (uint32_t) std::min<long>(std::max<long>(t, 64), LV_CMAX) : full ? LV_CTGT_FULL : LV_CTGT;
 }
 static uint64_t chunk_bound_of(const gnoc_engine* e, uint32_t P)
 {
-   const uint32_t tgt = chunk_target();
+   const uint32_t tgt = std::min(chunk_target(true), chunk_target(false));   // (the more chunks)
    const uint32_t cmin = LV_ROUNDS_FIT ? std::min<uint32_t>(LV_CMIN, tgt) : tgt;   // smallest chunk a level can get
    return e->rec_bound / cmin + P + 1;
 }
@@ -2121,7 +2123,7 @@ static int run_plan_v3(gnoc_engine* e, bool ends_only = false)
       khi1 = e->lvl_off[L];
    }
    const uint64_t chunk_bound = chunk_bound_of(e, P);
-   const uint32_t ctgt = chunk_target();
+   const uint32_t ctgt = chunk_target(!ends_only);
    GNOC_HIP(e, e->pio.ensure((size_t) P * sizeof(PortIO3)));
    GNOC_HIP(e, e->pnc.ensure((size_t) P * 4));
    GNOC_HIP(e, e->pgb.ensure((size_t) P * 4));
