@@ -582,9 +582,18 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 #ifndef CH_TURN_PLAIN
 #define CH_TURN_PLAIN 0   // 1: turns as plain 8-B stores (written back at the launch's end), spills sc1
 #endif
-#ifndef CH_RANKS
-#define CH_RANKS 0        // 1: the emit's route ranks kept from the row scans (no second wave sum per row)
+#ifndef CH_PFX
+#define CH_PFX 1          // 1: the row scans stage the emit's prefixes and route ranks in LDS (no rescan)
 #endif
+// A row's emit inputs as the row scan stages them in the kept region of LDS, one u64
+// per lane: the exclusive max-plus prefix (exA: flits, < 64 * 2^11; exB: cycles), the
+// lane's route rank (< 64) and, for lanes 1 + q, the row's count of field q (<= 64).
+constexpr uint32_t PFX_A = (1u << 17) - 1;
+static_assert(64u * AUX_F_MAX <= PFX_A, "a row's flit prefix must fit its 17 bits");
+__device__ __forceinline__ uint64_t pfx_pack(uint32_t exA, uint32_t rank, uint32_t fc, uint32_t exB)
+{
+   return (uint64_t) (exA | rank << 17 | fc << 23) | (uint64_t) exB << 32;
+}
 #ifndef CH_EARLY_PF
 #define CH_EARLY_PF 0     // 1: the next ports' inserts / descriptor loaded right after a step's landing
 #endif
@@ -1061,7 +1070,6 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
       // ---- [B] the merged stream in rows; per-row max-plus scans, route-field totals
       uint32_t n = nK + nI, IB = CAP;
       uint32_t fpack = 0, tc_t = 0;
-      uint32_t rkp[3] = { 0u, 0u, 0u }, rtv = 0;   // (CH_RANKS) route ranks / field totals per row
       uint32_t totA = 0, totB = 0;
       bool first = true, published = false;
       uint32_t Xr = 0, mode = mode0, Kpp = 0, Pep = 0, Kout = 0, Pend = 0;
@@ -1075,7 +1083,6 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
          totA = totB = 0;
          fpack = 0;
          tc_t = 0;
-         rkp[0] = rkp[1] = rkp[2] = rtv = 0;
 #pragma unroll
          for (int r = 0; r < ROWS; r++)
          {
@@ -1094,13 +1101,15 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
             fpack |= (valid ? f : 0u) << (2 * r);
             const uint32_t one = valid ? 1u << (8 * f) : 0u;
             const uint32_t inc = wave_sum32(one);
-            tc_t += field_cnt(rdl(inc, 63), lane);
-            if (CH_RANKS && !MG)
+            const uint32_t fc = field_cnt(rdl(inc, 63), lane);
+            tc_t += fc;
+            if (CH_PFX && !MG)
             {
-               // the emit's route ranks (< 64: 6 bits, rows 5 to a register) and the row's
-               // packed field totals (lane r)
-               rkp[r / 5] |= (((inc - one) >> (8 * f)) & 0x3Fu) << (6 * (r % 5));
-               rtv = lane == (uint32_t) r ? rdl(inc, 63) : rtv;
+               // the emit's inputs of this row into the kept region (the stream is in
+               // registers now; the emit's kept records of rows <= r' land below row
+               // r' + 1's entries, and a rescan after spill-ins stages them again)
+               const uint32_t exA = dpp32<0x138, 0xF, 0xF>(A), exB = dpp32<0x138, 0xF, 0xF>(B);   // wave_shr 1
+               sm.key[(uint32_t) r * T + lane] = pfx_pack(exA, ((inc - one) >> (8 * f)) & 0x3Fu, fc, exB);
             }
          }
          if (!first) break;
@@ -1180,17 +1189,6 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
             if (lane == 0) flag(a, F_FALLBACK | R_SPILLIN);
             return;
          }
-#pragma unroll
-         for (int r = 0; r < ROWS; r++)
-         {
-            const uint32_t p = (uint32_t) r * T + lane;
-            if ((uint32_t) r * T >= n) break;
-            if (p < n)
-            {
-               sm.key[p] = rk[r];
-               sm.aux[p] = ra[r];
-            }
-         }
          uint32_t skip = 0, take = 0;
          for (uint32_t g0 = 0; g0 < spn; g0 += T)
          {
@@ -1225,6 +1223,19 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
          {
             if (lane == 0) flag_overflow(a, c, R_OVF_STREAM);
             return;
+         }
+         // the stream back into the kept region (only now: with nothing merged, the row
+         // scans' staged prefixes there stand), the spill-ins behind it
+#pragma unroll
+         for (int r = 0; r < ROWS; r++)
+         {
+            const uint32_t p = (uint32_t) r * T + lane;
+            if ((uint32_t) r * T >= n) break;
+            if (p < n)
+            {
+               sm.key[p] = rk[r];
+               sm.aux[p] = ra[r];
+            }
          }
          nK = n;
          IB = n;
@@ -1288,11 +1299,24 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
          const uint32_t ax = ra[r];
          const uint32_t tc = cyc(off);
          const uint32_t p = aux_F(ax);
-         // the row's exclusive prefix (rescanned: registers for 11 rows of prefixes cost
-         // more than the scan)
-         uint32_t A = valid ? p : 0u, B = valid ? tc + p : 0u;
-         wave_scan(A, B);
-         const uint32_t exA = dpp32<0x138, 0xF, 0xF>(A), exB = dpp32<0x138, 0xF, 0xF>(B);   // wave_shr 1
+         // the row's exclusive prefix: staged by the row scan, or (MG: the rows after an
+         // M/G/1 prefix start at k0) rescanned
+         uint32_t exA, exB, prk = 0, pfc = 0;
+         if (CH_PFX && !MG)
+         {
+            const uint64_t pf = sm.key[p0 + lane];
+            exA = (uint32_t) pf & PFX_A;
+            prk = ((uint32_t) pf >> 17) & 0x3Fu;
+            pfc = ((uint32_t) pf >> 23) & 0x7Fu;
+            exB = (uint32_t) (pf >> 32);
+         }
+         else
+         {
+            uint32_t A = valid ? p : 0u, B = valid ? tc + p : 0u;
+            wave_scan(A, B);
+            exA = dpp32<0x138, 0xF, 0xF>(A);   // wave_shr 1
+            exB = dpp32<0x138, 0xF, 0xF>(B);
+         }
          const uint32_t xa = Xc + exA;
          const uint32_t Xb = xa > exB ? xa : exB;
          const uint32_t Xm = Xb > tc ? Xb : tc;
@@ -1311,23 +1335,23 @@ __device__ __forceinline__ void task_ser(Smem& sm, const ChainArgs& a, uint32_t 
          const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
          // route ranks: a packed (8 bits per field) prefix count over the row
          const uint32_t f = (fpack >> (2 * r)) & 3u;
-         uint32_t rank, rtot;
-         if (CH_RANKS && !MG)
+         uint32_t rank, fcnt;
+         if (CH_PFX && !MG)
          {
-            rank = (rkp[r / 5] >> (6 * (r % 5))) & 0x3Fu;
-            rtot = rdl(rtv, r);
+            rank = prk;
+            fcnt = pfc;
          }
          else
          {
             const uint32_t one = valid ? 1u << (8 * f) : 0u;
             const uint32_t inc = wave_sum32(one);
             rank = ((inc - one) >> (8 * f)) & 0xFFu;
-            rtot = rdl(inc, 63);
+            fcnt = field_cnt(rdl(inc, 63), lane);
          }
          const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
          const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
          const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
-         run_t += field_cnt(rtot, lane);
+         run_t += fcnt;
          // continuing: kept (a prefix of the window's continuing records) or spilled;
          // everything else leaves through one 16-B write-through store (turns and spills
          // alike: a spill is read in-launch by task (chain, w+1), MI355X_MICROARCH.md
@@ -1510,7 +1534,6 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
       uint32_t n = nK + nI, IB = CAP;
       const uint32_t itot = itot_f;
       uint32_t fpack = 0, tc_t = 0, totA = 0, totB = 0;
-      uint32_t rkp[3] = { 0u, 0u, 0u }, rtv = 0;   // (CH_RANKS) route ranks / field totals per row
       bool first = true;
       // spill-ins: records port i-1 spilled in earlier windows (departures after their
       // window's end) that arrive here in this window.  Pending range [Kpp, Pep): Pep = port
@@ -1524,7 +1547,6 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
          load_rows<ROWS>(sm, nK, IB, nI, rk, ra);
          if (first) CH_STAMP(1);
          fpack = tc_t = totA = totB = 0;
-         rkp[0] = rkp[1] = rkp[2] = rtv = 0;
 #pragma unroll
          for (int r = 0; r < ROWS; r++)
          {
@@ -1543,13 +1565,15 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
             fpack |= (valid ? f : 0u) << (2 * r);
             const uint32_t one = valid ? 1u << (8 * f) : 0u;
             const uint32_t inc = wave_sum32(one);
-            tc_t += field_cnt(rdl(inc, 63), lane);
-            if (CH_RANKS && !MG)
+            const uint32_t fc = field_cnt(rdl(inc, 63), lane);
+            tc_t += fc;
+            if (CH_PFX && !MG)
             {
-               // the emit's route ranks (< 64: 6 bits, rows 5 to a register) and the row's
-               // packed field totals (lane r)
-               rkp[r / 5] |= (((inc - one) >> (8 * f)) & 0x3Fu) << (6 * (r % 5));
-               rtv = lane == (uint32_t) r ? rdl(inc, 63) : rtv;
+               // the emit's inputs of this row into the kept region (the stream is in
+               // registers now; the emit's kept records of rows <= r' land below row
+               // r' + 1's entries, and a rescan after spill-ins stages them again)
+               const uint32_t exA = dpp32<0x138, 0xF, 0xF>(A), exB = dpp32<0x138, 0xF, 0xF>(B);   // wave_shr 1
+               sm.key[(uint32_t) r * T + lane] = pfx_pack(exA, ((inc - one) >> (8 * f)) & 0x3Fu, fc, exB);
             }
          }
          if (!first) break;
@@ -1642,17 +1666,6 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
                if ((uint32_t) po <= Kpp) break;
             }
          }
-#pragma unroll
-         for (int r = 0; r < ROWS; r++)
-         {
-            const uint32_t p = (uint32_t) r * T + lane;
-            if ((uint32_t) r * T >= n) break;
-            if (p < n)
-            {
-               sm.key[p] = rk[r];
-               sm.aux[p] = ra[r];
-            }
-         }
          for (uint32_t g0 = 0; g0 < spn; g0 += T)
          {
             const uint32_t g = g0 + lane;
@@ -1685,6 +1698,19 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
          {
             if (lane == 0) flag_overflow(a, c, R_OVF_STREAM);
             return;
+         }
+         // the stream back into the kept region (only now: with nothing merged, the row
+         // scans' staged prefixes there stand), the spill-ins behind it
+#pragma unroll
+         for (int r = 0; r < ROWS; r++)
+         {
+            const uint32_t p = (uint32_t) r * T + lane;
+            if ((uint32_t) r * T >= n) break;
+            if (p < n)
+            {
+               sm.key[p] = rk[r];
+               sm.aux[p] = ra[r];
+            }
          }
          nK = n;
          IB = n;
@@ -1878,11 +1904,24 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
          const uint32_t ax = ra[r];
          const uint32_t tc = cyc(off);
          const uint32_t p = aux_F(ax);
-         // the row's exclusive prefix (rescanned: registers for 11 rows of prefixes cost
-         // more than the scan)
-         uint32_t A = valid ? p : 0u, B = valid ? tc + p : 0u;
-         wave_scan(A, B);
-         const uint32_t exA = dpp32<0x138, 0xF, 0xF>(A), exB = dpp32<0x138, 0xF, 0xF>(B);   // wave_shr 1
+         // the row's exclusive prefix: staged by the row scan, or (MG: the rows after an
+         // M/G/1 prefix start at k0) rescanned
+         uint32_t exA, exB, prk = 0, pfc = 0;
+         if (CH_PFX && !MG)
+         {
+            const uint64_t pf = sm.key[p0 + lane];
+            exA = (uint32_t) pf & PFX_A;
+            prk = ((uint32_t) pf >> 17) & 0x3Fu;
+            pfc = ((uint32_t) pf >> 23) & 0x7Fu;
+            exB = (uint32_t) (pf >> 32);
+         }
+         else
+         {
+            uint32_t A = valid ? p : 0u, B = valid ? tc + p : 0u;
+            wave_scan(A, B);
+            exA = dpp32<0x138, 0xF, 0xF>(A);   // wave_shr 1
+            exB = dpp32<0x138, 0xF, 0xF>(B);
+         }
          const uint32_t xa = Xc + exA;
          const uint32_t Xb = xa > exB ? xa : exB;
          const uint32_t Xm = Xb > tc ? Xb : tc;
@@ -1901,23 +1940,23 @@ __device__ __forceinline__ void task_lb(Smem& sm, const ChainArgs& a, uint32_t c
          const uint64_t dn = (uint64_t) off + cps(cc) + rl;   // t' - wbase
          // route ranks: a packed (8 bits per field) prefix count over the row
          const uint32_t f = (fpack >> (2 * r)) & 3u;
-         uint32_t rank, rtot;
-         if (CH_RANKS && !MG)
+         uint32_t rank, fcnt;
+         if (CH_PFX && !MG)
          {
-            rank = (rkp[r / 5] >> (6 * (r % 5))) & 0x3Fu;
-            rtot = rdl(rtv, r);
+            rank = prk;
+            fcnt = pfc;
          }
          else
          {
             const uint32_t one = valid ? 1u << (8 * f) : 0u;
             const uint32_t inc = wave_sum32(one);
             rank = ((inc - one) >> (8 * f)) & 0xFFu;
-            rtot = rdl(inc, 63);
+            fcnt = field_cnt(rdl(inc, 63), lane);
          }
          const uint32_t gb = bperm(obf_t + run_t, 1u + f);     // obase[f] + records of f so far
          const uint32_t room = bperm(ocf_t - run_t, 1u + f);   // ocap[f] - records of f so far
          const uint32_t kb = rdl(run_t, 2) - P0n;              // kept records so far
-         run_t += field_cnt(rtot, lane);
+         run_t += fcnt;
          // continuing: kept (a prefix of the window's continuing records) or spilled
          const bool keep = valid && f == 1 && dn < wlen;
          const bool out = valid && !keep;
