@@ -575,13 +575,6 @@ __device__ __forceinline__ gptr<P> sptr(P* p)
    asm volatile("" : "+s"(p));
    return (gptr<P>) p;
 }
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-#ifndef CH_TURN16
-#define CH_TURN16 0   // 1: turns as one plain 16-B store (measured: see DESIGN.md 7)
-#endif
-#ifndef CH_TURN_PLAIN
-#define CH_TURN_PLAIN 0   // 1: turns as plain 8-B stores (written back at the launch's end), spills sc1
-#endif
 #ifndef CH_PFX
 #define CH_PFX 1          // 1: the row scans stage the emit's prefixes and route ranks in LDS (no rescan)
 #endif
@@ -598,40 +591,29 @@ __device__ __forceinline__ uint64_t pfx_pack(uint32_t exA, uint32_t rank, uint32
 #define CH_EARLY_PF 0     // 1: the next ports' inserts / descriptor loaded right after a step's landing
 #endif
 // A record that leaves the chain at slot position gp.  A turn is read by the next
-// launch: one plain 16-B store.  A spill is read in this launch by a later window's
-// task once the producer published a state after draining its stores: write-through
-// 8-B stores (MI355X_MICROARCH.md "Valid forms").  Every 64th position also writes
-// the slot's key sample.
+// launch (the launch's end writes the L2s back): one plain 16-B store.  A spill is
+// read in this launch by a later window's task once the producer published a state
+// after draining its stores: 8-B stores kept in the XCD's L2 when that task runs on
+// the same XCD (XCD-local queues), written through otherwise (MI355X_MICROARCH.md
+// "Valid forms").  Every 64th position also writes the slot's key sample.
 __device__ __forceinline__ void out_record(gptr<Rec> recs, gptr<uint64_t> samp_t, gptr<uint32_t> samp_id, uint64_t gp,
                                            uint64_t tn, uint32_t id, uint32_t ax, bool spill, uint32_t xcd)
 {
-   if ((CH_TURN_PLAIN || CH_XCD_ONLY || xcd) && !spill)
+   const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
+   if (!spill)
    {
-      const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
       q[0] = tn;
       q[1] = (uint64_t) id | ((uint64_t) ax << 32);
    }
    else if (CH_XCD_ONLY || xcd)
    {
-      // a spill read in this launch by the next window of the chain, on this XCD
-      const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
       __hip_atomic_store(q, tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       __hip_atomic_store(q + 1, (uint64_t) id | ((uint64_t) ax << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
    }
-   else if (!CH_TURN16 || spill)
-   {
-      const gptr<uint64_t> q = (gptr<uint64_t>) (recs + gp);
-      __hip_atomic_store(q, tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(q + 1, (uint64_t) id | ((uint64_t) ax << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-   }
    else
    {
-      v4u o;
-      o.x = (uint32_t) tn;
-      o.y = (uint32_t) (tn >> 32);
-      o.z = id;
-      o.w = ax;
-      *(gptr<v4u>) (recs + gp) = o;
+      __hip_atomic_store(q, tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(q + 1, (uint64_t) id | ((uint64_t) ax << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
    }
    if ((gp & 63) == 0)
    {
