@@ -9,8 +9,8 @@
 //                  (t, id)-ordered; grouping it stably by source tile gives every
 //                  injection queue (emesh_hop_by_hop.cc:109-112, 151-159) its
 //                  arrivals in service order.
-// 3. k_scatter:    the stable group-by-source into the injection slots, one wave
-//                  per chunk, ranks from ballot match masks.
+// 3. k_scatter4:   the stable group-by-source into the injection slots, ranks from
+//                  ballot match masks.
 // 4. k_row_hist:   per (source row, group of sources) LDS histograms of the
 //                  grouped records: per source (dx, y-class) and per destination.
 // 5. k_prow / k_slot_counts: every output-port input slot's record count, in
@@ -421,72 +421,7 @@ __device__ __forceinline__ uint64_t match_mask(uint32_t key, bool valid, int nbi
    return m;
 }
 
-__global__ __launch_bounds__(64) void k_scatter(uint64_t n, uint32_t pch, uint32_t N, int nbits,
-                                                const uint32_t* __restrict__ src, const uint8_t* __restrict__ routed,
-                                                const uint64_t* __restrict__ inj, const uint32_t* __restrict__ aux,
-                                                const uint32_t* __restrict__ offs, Rec* __restrict__ recs,
-                                                uint64_t* __restrict__ samp_t, uint32_t* __restrict__ samp_id)
-{
-   extern __shared__ uint32_t h[];   // N rank counters
-   const uint32_t lane = threadIdx.x;
-   for (uint32_t s = lane; s < N; s += 64) h[s] = 0;
-   __syncthreads();
-   const uint64_t lo = (uint64_t) blockIdx.x * pch;
-   const uint64_t hi = min(lo + pch, n);
-   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-   const uint32_t* orow = offs + (uint64_t) blockIdx.x * N;
-   // 8 groups of 64 packets per batch: their loads (then the source-dependent
-   // offsets) in flight together, so a batch costs two round trips, not sixteen
-   for (uint64_t k0 = lo; k0 < hi; k0 += 512)
-   {
-      bool vv[8];
-      uint32_t sv[8], av[8], ov[8];
-      uint64_t tv[8];
-#pragma unroll
-      for (int q = 0; q < 8; q++)
-      {
-         const uint64_t i = k0 + (uint64_t) (q * 64) + lane;
-         vv[q] = i < hi && (routed[i] & 2);
-         sv[q] = vv[q] ? src[i] : 0u;
-      }
-#pragma unroll
-      for (int q = 0; q < 8; q++)
-      {
-         const uint64_t i = k0 + (uint64_t) (q * 64) + lane;
-         tv[q] = 0; av[q] = 0; ov[q] = 0;
-         if (vv[q]) { tv[q] = inj[i]; av[q] = aux[i]; ov[q] = orow[sv[q]]; }
-      }
-#pragma unroll
-      for (int q = 0; q < 8; q++)
-      {
-         const bool valid = vv[q];
-         const uint32_t sq = sv[q];
-         const uint64_t m = match_mask(sq, valid, nbits);
-         const uint32_t old = valid ? h[sq] : 0u;
-         __builtin_amdgcn_wave_barrier();
-         if (valid)
-         {
-            const uint32_t rank = old + (uint32_t) __popcll(m & lt);
-            if ((63 - __clzll(m)) == (int) lane) h[sq] = old + (uint32_t) __popcll(m);
-            const uint64_t pos = (uint64_t) ov[q] + rank;
-            Rec r;
-            r.t = tv[q];
-            r.id = (uint32_t) (k0 + (uint64_t) (q * 64) + lane);
-            r.aux = av[q];
-            recs[pos] = r;
-            if ((pos & 63) == 0)
-            {
-               samp_t[pos >> 6] = r.t;
-               samp_id[pos >> 6] = r.id;
-            }
-         }
-         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-         __builtin_amdgcn_wave_barrier();
-      }
-   }
-}
-
-// Same contract with NW waves per chunk: each wave owns a contiguous 1/NW of
+// The stable scatter with NW waves per chunk: each wave owns a contiguous 1/NW of
 // the chunk; per-wave source counts in LDS (NW * N words) give each wave its
 // starting rank, then every wave ranks its part in order, with the next 64
 // packets' loads in flight while the current ones are placed.  NW = 8 for
