@@ -324,24 +324,29 @@ def main():
         dist.destroy_process_group()
 
 
+SETTLE_MIN = 12   # > the variable windows' 8 adaptations + the protocol trial runs
+
+
 def measure(eng, a, barrier_sync, settle_fixed=False):
     """Settle the chain windows, W warmup runs, then EXACTLY K timed runs between
     barrier + synchronize; then one profiled run for per-kernel device times (HIP
     events on the engine's stream).  Reruns are counted over the timed runs from
     gnoc_summary's totals since submit."""
     settle = 0
-    # window adaptation (engine.hip adapt_windows): the first runs of a batch size the
-    # chain windows from the fill they measure; runs until one needed no rerun and used
+    # window adaptation (engine.hip adapt_windows): the first runs of a batch shape size
+    # the chain windows from the fill they measure (variable boundaries: up to
+    # CH_ADAPT_RUNS = 8 adaptations), then time each hand-off protocol once on the
+    # settled windows; at least SETTLE_MIN runs, then until one needed no rerun and used
     # the windows of the run before (a sharded engine runs a fixed count: every rank
     # must call the same collectives)
     prev = None
-    for settle in range(1, 9):
+    for settle in range(1, 2 * SETTLE_MIN + 1):
         eng.run()
         sm = eng.summary()
         cur = (sm["windows"], sm["windows_y"], sm["window_ps_x"], sm["window_ps_y"])
-        if settle_fixed and settle >= 3:
+        if settle_fixed and settle >= SETTLE_MIN:
             break
-        if not settle_fixed and sm["retries"] == 0 and sm["fallbacks"] == 0 and cur == prev:
+        if not settle_fixed and settle >= SETTLE_MIN and sm["retries"] == 0 and sm["fallbacks"] == 0 and cur == prev:
             break
         prev = cur
     for _ in range(a.warmup):
